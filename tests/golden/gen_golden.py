@@ -1,0 +1,337 @@
+"""Generate golden vectors by running the REAL reference (/root/reference) on CPU in the survey container.
+
+Run:  python tests/golden/gen_golden.py     (writes tests/golden/<case>.npz; needs /root/reference)
+
+For each case the reference `Dreamer` (world_model/dreamer.py:22) is built from our config surface
+(which mirrors configs/base.yaml key for key), given deterministic weights (oracle/init.py), fed a seeded
+synthetic batch through a stub replay buffer, and its own `update()` (dreamer.py:402-451) is run with:
+  * autocast replaced by a null context (dreamer.py:420 would enter CPU fp16 autocast — SURVEY §6/§8(c));
+  * sampling noise injected: F.gumbel_softmax (distributions.py:33) and Normal.rsample (bounded_normal)
+    draw from oracle/noise.py in the exact call order of _cal_grad (observe ×T, prior ×1 (discarded),
+    then per imagination step: actor, img_step).
+Hooks record encoder/observe/prior/_imagine/_lambda_return outputs. Gradients are recorded as per-tensor
+L2 norms + 32 sampled elements; parameters after the LaProp step the same way. Two updates are run per case
+so LaProp's lr-EMA state and ReturnEMA carry over.
+"""
+import contextlib
+import os
+import sys
+import zlib
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "safe-dreamer_amd"))
+
+from refimport import import_reference  # noqa: E402
+
+from oracle import noise as nz  # noqa: E402
+from oracle.init import params_for  # noqa: E402
+from oracle.ref_cpu import Spec  # noqa: E402
+from sdreamer.config import load_config  # noqa: E402
+
+CASES = {
+    # name: (config, overrides, obs shapes, act_dim, discrete, B, T, H)
+    "proprio_dreamer": ("dmc/proprio", [], {"position": (3,), "velocity": (2,)}, 1, False, 4, 16, 8),
+    "walker_r2": ("dmc/cnn", [], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
+    "walker_dreamer": ("dmc/walker_dreamer", [], {"image": (64, 64, 3)}, 6, False, 2, 4, 3),
+    "atari_r2": ("dmc/atari_breakout", [], {"image": (64, 64, 3)}, 4, True, 2, 4, 3),
+    "maze_r2": ("dmc/memory_maze", [], {"image": (64, 64, 3)}, 6, True, 2, 4, 3),
+}
+PARAM_SEED = 0
+N_SAMPLE = 32
+
+
+def sample_idx(name, numel):
+    rng = np.random.default_rng([7, zlib.crc32(name.encode())])
+    return np.sort(rng.choice(numel, size=min(N_SAMPLE, numel), replace=False))
+
+
+def make_batch(rng, obs, A, discrete, B, T):
+    data = {}
+    for k, shp in obs.items():
+        if len(shp) == 3:
+            data[k] = rng.integers(0, 256, size=(B, T) + shp, dtype=np.uint8)
+        else:
+            data[k] = rng.standard_normal((B, T) + shp).astype(np.float32)
+    if discrete:
+        a = rng.integers(0, A, size=(B, T))
+        data["action"] = np.eye(A, dtype=np.float32)[a]
+    else:
+        data["action"] = rng.uniform(-1.5, 1.5, size=(B, T, A)).astype(np.float32)  # >1 exercises the clip
+    data["reward"] = rng.uniform(-2, 3, size=(B, T, 1)).astype(np.float32)
+    first = rng.random((B, T, 1)) < 0.1
+    first[:, 0] = True
+    data["is_first"] = first
+    term = rng.random((B, T, 1)) < 0.1
+    data["is_terminal"] = term
+    data["is_last"] = term | (rng.random((B, T, 1)) < 0.05)
+    return data
+
+
+def make_initial(rng, S, K, D, B):
+    idx = rng.integers(0, K, size=(B, S))
+    stoch = np.eye(K, dtype=np.float32)[idx]
+    deter = (0.5 * rng.standard_normal((B, D))).astype(np.float32)
+    return stoch, deter
+
+
+class NoiseSeq:
+    """Injects oracle noise in _cal_grad call order (see module doc)."""
+
+    def __init__(self, T, H1, seed):
+        self.T, self.H1, self.seed = T, H1, seed
+        self.g = 0
+        self.n = 0
+
+    def gumbel(self, shape):
+        i = self.g
+        self.g += 1
+        T = self.T
+        if i < T:  # observe step i, (B, S, K)
+            B = shape[0]
+            return nz.gumbel_block(self.seed, nz.STREAM_OBS, i, B, 0, int(np.prod(shape[1:]))).reshape(shape)
+        if i == T:  # prior over (B, T, S, K): sample discarded
+            return np.zeros(shape, np.float32)
+        j = i - T - 1
+        N = shape[0]
+        if self.discrete_act:
+            t, which = divmod(j, 2)
+            stream = nz.STREAM_ACT if which == 0 else nz.STREAM_IMG
+        else:
+            t, stream = j, nz.STREAM_IMG
+        return nz.gumbel_block(self.seed, stream, t, N, 0, int(np.prod(shape[1:]))).reshape(shape)
+
+    def normal(self, shape):
+        t = self.n
+        self.n += 1
+        N = shape[0]
+        return nz.normal_block(self.seed, nz.STREAM_ACT, t, N, 0, int(np.prod(shape[1:]))).reshape(shape)
+
+
+def run_case(name, mods, TD):
+    cfg_name, ovr, obs, A, discrete, B, T, H = CASES[name]
+    cfg = load_config(cfg_name, ["device=cpu", "model.compile=False", f"model.imag_horizon={H}"] + ovr)
+    D = mods["world_model.dreamer"]
+
+    class Sp:
+        def __init__(s, shape):
+            s.shape = shape
+
+    class Spaces:
+        def __init__(s, d):
+            s.spaces = d
+
+    act_space = Sp((A,))
+    if discrete:
+        act_space.discrete = True
+    torch.manual_seed(0)
+    import copy
+    ag = D.Dreamer(copy.deepcopy(cfg.model), Spaces({k: Sp(v) for k, v in obs.items()}), act_space)
+    spec = Spec(cfg.model, obs, A, discrete)
+    sd = ag.state_dict()
+    ref_train = [k for k in sd if not k.startswith("_frozen") and not k.startswith("_slow_value")
+                 and k != "return_ema.ema_vals"]
+    assert sorted(ref_train) == sorted(spec.shapes), (set(ref_train) ^ set(spec.shapes))
+    for k, v in spec.shapes.items():
+        assert tuple(sd[k].shape) == tuple(v), (k, sd[k].shape, v)
+    vals = params_for(spec.shapes, PARAM_SEED)
+    with torch.no_grad():
+        named = dict(ag.named_parameters())
+        for k, v in vals.items():
+            named[k].data.copy_(torch.from_numpy(v))
+        for k, v in named.items():
+            if k.startswith("_slow_value."):
+                v.data.copy_(torch.from_numpy(vals["value." + k[len("_slow_value."):]]))
+    out = {"meta_B": B, "meta_T": T, "meta_H": H, "meta_A": A, "meta_discrete": int(discrete),
+           "meta_param_seed": PARAM_SEED}
+
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    D.autocast = lambda **k: contextlib.nullcontext()
+    orig_gs = torch.nn.functional.gumbel_softmax
+    orig_rs = torch.distributions.Normal.rsample
+    rec = {}
+
+    def hook(obj, attr, key, many=False):
+        orig = getattr(obj, attr)
+
+        def w(*a, **k):
+            r = orig(*a, **k)
+            if many:
+                rec.setdefault(key, []).append(r)
+            else:
+                rec[key] = r
+            return r
+
+        setattr(obj, attr, w)
+
+    hook(ag.rssm, "observe", "observe")
+    hook(ag.rssm, "prior", "prior")
+    hook(ag, "_imagine", "imagine")
+    hook(ag, "_lambda_return", "lret", many=True)
+    ag.encoder.register_forward_hook(lambda m, i, o: rec.__setitem__("embed", o))
+
+    for u in range(2):
+        seed = 1000 + u
+        data_np = make_batch(rng, obs, A, discrete, B, T)
+        init_np = make_initial(rng, spec.S, spec.K, spec.D, B)
+        for k, v in data_np.items():
+            out[f"u{u}_in_{k}"] = v
+        out[f"u{u}_in_init_stoch"] = init_np[0].argmax(-1).astype(np.int16)
+        out[f"u{u}_in_init_deter"] = init_np[1]
+        out[f"u{u}_seed"] = seed
+        seq = NoiseSeq(T, H + 1, seed)
+        seq.discrete_act = discrete
+
+        def gs(logits, tau=1, hard=False, eps=1e-10, dim=-1):
+            g = torch.from_numpy(seq.gumbel(tuple(logits.shape)))
+            y_soft = ((logits + g) / tau).softmax(dim)
+            index = y_soft.max(dim, keepdim=True)[1]
+            y_hard = torch.zeros_like(logits).scatter_(dim, index, 1.0)
+            return y_hard - y_soft.detach() + y_soft
+
+        def rs(self, sample_shape=torch.Size()):
+            shape = self._extended_shape(sample_shape)
+            eps = torch.from_numpy(seq.normal(tuple(shape)))
+            return self.loc + eps * self.scale
+
+        torch.nn.functional.gumbel_softmax = gs
+        torch.distributions.Normal.rsample = rs
+
+        class Buf:
+            def sample(self_):
+                d = TD({k: torch.from_numpy(v) for k, v in data_np.items()}, batch_size=(B, T))
+                return d, None, (torch.from_numpy(init_np[0]), torch.from_numpy(init_np[1]))
+
+            def update(self_, index, stoch, deter):
+                rec["wb"] = (stoch, deter)
+
+        rec.clear()
+        try:
+            mets = ag.update(Buf())
+        finally:
+            torch.nn.functional.gumbel_softmax = orig_gs
+            torch.distributions.Normal.rsample = orig_rs
+        assert seq.g == T + 1 + (H + 1) * (2 if discrete else 1), seq.g
+        assert seq.n == (0 if discrete else H + 1), seq.n
+        ps, pdet, plog = rec["observe"]
+        out[f"u{u}_post_idx"] = ps.argmax(-1).numpy().astype(np.int16)
+        out[f"u{u}_post_deter"] = pdet.detach().numpy()[..., ::4].copy()
+        out[f"u{u}_post_logit"] = plog.detach().numpy()
+        out[f"u{u}_prior_logit"] = rec["prior"][1].detach().numpy()
+        out[f"u{u}_embed"] = rec["embed"].detach().numpy()[..., ::8].copy()
+        ifeat, iact = rec["imagine"]
+        SK = spec.SK
+        out[f"u{u}_imag_idx"] = ifeat[..., :SK].reshape(*ifeat.shape[:2], spec.S, spec.K).argmax(-1).numpy().astype(np.int16)
+        out[f"u{u}_imag_deter"] = ifeat[..., SK::16].numpy().copy()
+        out[f"u{u}_imag_action"] = iact.numpy()
+        out[f"u{u}_imag_ret"] = rec["lret"][0].numpy()
+        out[f"u{u}_replay_ret"] = rec["lret"][1].numpy()
+        for k, v in mets.items():
+            out[f"u{u}_m_{k}"] = np.asarray(float(v), np.float64)
+        out[f"u{u}_ema_vals"] = ag.return_ema.ema_vals.numpy().copy()
+        named = dict(ag.named_parameters())
+        for k in spec.shapes:
+            p = named[k]
+            flat = p.detach().reshape(-1).numpy()
+            idx = sample_idx(k, flat.size)
+            out[f"u{u}_p_{k}__n"] = np.asarray(np.linalg.norm(flat.astype(np.float64)))
+            out[f"u{u}_p_{k}__s"] = flat[idx]
+        st = ag._optimizer.state[named["rssm._img_net.img_net_logit.bias"]]
+        out[f"u{u}_laprop_lr1"] = np.asarray(st["exp_avg_lr_1"])
+        out[f"u{u}_laprop_lr2"] = np.asarray(st["exp_avg_lr_2"])
+        for k in spec.slow_names.values():
+            flat = named[k].detach().reshape(-1).numpy()
+            idx = sample_idx(k, flat.size)
+            out[f"u{u}_p_{k}__s"] = flat[idx]
+    # grads of the FIRST update are not observable after update(); re-run _cal_grad on update-0 inputs with
+    # the initial weights for a gradient fixture.
+    return out
+
+
+def grad_case(name, mods, TD):
+    """Gradients (post-backward, pre-AGC) of _cal_grad on update-0 inputs at the initial weights."""
+    cfg_name, ovr, obs, A, discrete, B, T, H = CASES[name]
+    cfg = load_config(cfg_name, ["device=cpu", "model.compile=False", f"model.imag_horizon={H}"] + ovr)
+    D = mods["world_model.dreamer"]
+    import copy
+
+    class Sp:
+        def __init__(s, shape):
+            s.shape = shape
+
+    class Spaces:
+        def __init__(s, d):
+            s.spaces = d
+
+    act_space = Sp((A,))
+    if discrete:
+        act_space.discrete = True
+    ag = D.Dreamer(copy.deepcopy(cfg.model), Spaces({k: Sp(v) for k, v in obs.items()}), act_space)
+    spec = Spec(cfg.model, obs, A, discrete)
+    vals = params_for(spec.shapes, PARAM_SEED)
+    with torch.no_grad():
+        named = dict(ag.named_parameters())
+        for k, v in vals.items():
+            named[k].data.copy_(torch.from_numpy(v))
+        for k, v in named.items():
+            if k.startswith("_slow_value."):
+                v.data.copy_(torch.from_numpy(vals["value." + k[len("_slow_value."):]]))
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    data_np = make_batch(rng, obs, A, discrete, B, T)
+    init_np = make_initial(rng, spec.S, spec.K, spec.D, B)
+    seq = NoiseSeq(T, H + 1, 1000)
+    seq.discrete_act = discrete
+    orig_gs = torch.nn.functional.gumbel_softmax
+    orig_rs = torch.distributions.Normal.rsample
+
+    def gs(logits, tau=1, hard=False, eps=1e-10, dim=-1):
+        g = torch.from_numpy(seq.gumbel(tuple(logits.shape)))
+        y_soft = ((logits + g) / tau).softmax(dim)
+        index = y_soft.max(dim, keepdim=True)[1]
+        y_hard = torch.zeros_like(logits).scatter_(dim, index, 1.0)
+        return y_hard - y_soft.detach() + y_soft
+
+    def rs(self, sample_shape=torch.Size()):
+        shape = self._extended_shape(sample_shape)
+        return self.loc + torch.from_numpy(seq.normal(tuple(shape))) * self.scale
+
+    torch.nn.functional.gumbel_softmax = gs
+    torch.distributions.Normal.rsample = rs
+    try:
+        d = TD({k: torch.from_numpy(v) for k, v in data_np.items()}, batch_size=(B, T))
+        d = ag.preprocess(d)
+        ag._update_slow_target()
+        ag._cal_grad(d, (torch.from_numpy(init_np[0]), torch.from_numpy(init_np[1])))
+    finally:
+        torch.nn.functional.gumbel_softmax = orig_gs
+        torch.distributions.Normal.rsample = orig_rs
+    out = {}
+    named = dict(ag.named_parameters())
+    for k in spec.shapes:
+        g = named[k].grad
+        flat = (torch.zeros_like(named[k]) if g is None else g).reshape(-1).numpy()
+        idx = sample_idx(k, flat.size)
+        out[f"g_{k}__n"] = np.asarray(np.linalg.norm(flat.astype(np.float64)))
+        out[f"g_{k}__s"] = flat[idx]
+    return out
+
+
+def main():
+    mods, TD = import_reference()
+    torch.set_num_threads(8)
+    only = sys.argv[1:] or list(CASES)
+    for name in only:
+        out = run_case(name, mods, TD)
+        out.update(grad_case(name, mods, TD))
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **out)
+        print(name, "->", path, os.path.getsize(path) // 1024, "KB")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,72 @@
+"""Pin the CPU oracle (oracle/ref_cpu.py) against golden vectors produced by the real reference.
+
+The fixtures (tests/golden/*.npz) come from tests/golden/gen_golden.py, which imports /root/reference and
+runs its own Dreamer.update() (dreamer.py:402-451) with fp32 and injected Philox noise. On the same CPU
+and torch build the restatement is expected to agree to float rounding of reordered-but-equivalent ops.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import CASES, batch, initial, load_case, sample_idx
+from oracle.ref_cpu import OracleAgent
+
+RTOL = 2e-5  # fp32; tightened observation: most values match bit-for-bit
+
+
+def _close(a, b, rtol=RTOL, atol=1e-6, what=""):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    err = np.abs(a - b) - (atol + rtol * np.abs(b))
+    assert err.max(initial=-1) <= 0, f"{what}: max abs diff {np.abs(a - b).max()}"
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_oracle_update_matches_reference(name):
+    z, cfg, spec, params, obs = load_case(name)
+    torch.set_num_threads(8)
+    ag = OracleAgent(spec, params)
+    for u in range(2):
+        keep = {}
+        (ps, pd), losses, mets = ag.update(batch(z, u, obs), initial(z, u, spec), int(z[f"u{u}_seed"]), keep=keep)
+        assert np.array_equal(ps.argmax(-1).numpy(), z[f"u{u}_post_idx"]), "posterior latent indices"
+        _close(pd.detach().numpy()[..., ::4], z[f"u{u}_post_deter"], what="post_deter")
+        _close(keep["post_logit"].detach().numpy(), z[f"u{u}_post_logit"], atol=1e-5, what="post_logit")
+        _close(keep["prior_logit"].detach().numpy(), z[f"u{u}_prior_logit"], atol=1e-5, what="prior_logit")
+        SK = spec.SK
+        ifeat = keep["imag_feat"]
+        iidx = ifeat[..., :SK].reshape(*ifeat.shape[:2], spec.S, spec.K).argmax(-1).numpy()
+        assert np.array_equal(iidx, z[f"u{u}_imag_idx"]), "imagined latent indices"
+        _close(ifeat[..., SK::16].numpy(), z[f"u{u}_imag_deter"], atol=1e-5, what="imag_deter")
+        _close(keep["imag_action"].numpy(), z[f"u{u}_imag_action"], atol=1e-5, what="imag_action")
+        _close(keep["ret"].numpy(), z[f"u{u}_imag_ret"], atol=1e-5, what="imag_ret")
+        _close(keep["rret"].numpy(), z[f"u{u}_replay_ret"], atol=1e-5, what="replay_ret")
+        for k in mets:
+            key = f"u{u}_m_{k}"
+            if key in z:
+                _close(float(mets[k]), z[key], rtol=1e-4, atol=1e-6, what=k)
+        missing = [k[len(f"u{u}_m_"):] for k in z if k.startswith(f"u{u}_m_") and k[len(f"u{u}_m_"):] not in mets]
+        assert not [m for m in missing if m not in ("opt/grad_scale",)], missing
+        _close(ag.ema_vals.numpy(), z[f"u{u}_ema_vals"], atol=1e-6, what="ema_vals")
+        for k in spec.shapes:
+            flat = ag.P[k].detach().reshape(-1).numpy()
+            _close(flat[sample_idx(k, flat.size)], z[f"u{u}_p_{k}__s"], rtol=1e-4, atol=1e-7, what=f"param {k}")
+            _close(np.linalg.norm(flat.astype(np.float64)), z[f"u{u}_p_{k}__n"], rtol=1e-5, what=f"pnorm {k}")
+        for k in spec.slow_names.values():
+            flat = ag.P[k].detach().reshape(-1).numpy()
+            _close(flat[sample_idx(k, flat.size)], z[f"u{u}_p_{k}__s"], rtol=1e-5, atol=1e-7, what=k)
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_oracle_grads_match_reference(name):
+    z, cfg, spec, params, obs = load_case(name)
+    torch.set_num_threads(8)
+    ag = OracleAgent(spec, params)
+    ag.update_slow_target()
+    ag.cal_grad(batch(z, 0, obs), initial(z, 0, spec), int(z["u0_seed"]))
+    for k in spec.shapes:
+        g = ag.P[k].grad
+        flat = (torch.zeros_like(ag.P[k]) if g is None else g).reshape(-1).numpy()
+        _close(np.linalg.norm(flat.astype(np.float64)), z[f"g_{k}__n"], rtol=1e-4, atol=1e-9, what=f"gnorm {k}")
+        ref = z[f"g_{k}__s"]
+        _close(flat[sample_idx(k, flat.size)], ref, rtol=1e-3, atol=1e-6 * max(1e-3, np.abs(ref).max()), what=f"grad {k}")
