@@ -1,0 +1,183 @@
+/* sdhip.h — C ABI of the MI355X-native Dreamer world-model / imagination hot path (libsdhip.so, gfx950).
+ *
+ * The reference (sharmaabhijith/safe-dreamer) has no FFI: its hot path is the Python call chain
+ * Dreamer.update -> _cal_grad -> {encoder, RSSM.observe, RSSM.prior, kl_loss, heads, _imagine,
+ * _lambda_return, ReturnEMA, losses} -> backward -> clip_grad_agc_ -> LaProp.step
+ * (world_model/dreamer.py:402-707, world_model/rssm.py:36-230, world_model/networks.py:24-422,
+ *  world_model/distributions.py:16-271, utils/optim/agc.py:15-53, utils/optim/laprop.py:46-118).
+ * Each entry point below replaces one step of that chain; the comment names the reference code it stands in for.
+ *
+ * Conventions:
+ *  - plain device pointers + sizes; fp32 data, int32 indices; row-major unless stated;
+ *  - every call enqueues on `stream` and never synchronises, allocates or frees (graph-capturable);
+ *  - the caller owns all memory, including workspaces;
+ *  - return 0 on success, a positive hipError_t on launch failure, negative SD_E* on bad arguments.
+ */
+#ifndef SDHIP_H
+#define SDHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* a hipStream_t passed as an opaque handle (0 = the null stream) */
+typedef void* sd_stream;
+
+#define SDHIP_ABI_VERSION 1
+int sd_abi_version(void);
+
+/* ---------------------------------------------------------------- dense contractions (MFMA fp32)
+ * C[b] = alpha * A[b].B[b] (+ bias[b][n]) (+ beta * C[b]);  A: M x K, B: K x N, C: M x N (ldc).
+ * a_kcontig: A(m,k) at A + m*lda + k   (else A + k*lda + m);
+ * b_kcontig: B(k,n) at B + n*ldb + k   (else B + k*ldb + n).
+ * Replaces nn.Linear fwd/bwd (networks.py:325,348-362; rssm.py:16-32,106-130), BlockLinear.forward's
+ * einsum (networks.py:52) as a batch over blocks, Projector (networks.py:380-387) and torch.mm in the
+ * Barlow loss (dreamer.py:528). ksplit > 1 needs workspace >= ksplit*batch*M*N floats (deterministic reduce).
+ * tile: -1 auto, 0: 128x128, 1: 64x64, 2: 32x128, 3: 128x64. */
+typedef struct sd_gemm_desc {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias;
+  long lda, ldb, ldc;
+  long strideA, strideB, strideC, strideBias;
+  int M, N, K, batch;
+  int a_kcontig, b_kcontig;
+  int ksplit, tile;
+  float alpha, beta;
+} sd_gemm_desc;
+int sd_gemm_f32(const sd_gemm_desc* d, float* workspace, long workspace_floats, sd_stream stream);
+
+/* ---------------------------------------------------------------- row norms
+ * y = act(x * rsqrt(mean(x^2) + eps) * w) per row; act 0 = none, 1 = SiLU. rstd (M) saved for backward.
+ * Replaces nn.RMSNorm(eps=1e-4) + nn.SiLU in every MLP/RSSM layer (rssm.py:16-31,106-130; networks.py:326-327)
+ * and RMSNorm2D on channels-last conv activations (networks.py:88-96). N <= 4096. */
+int sd_rmsnorm_fwd(const float* x, const float* w, float* y, float* rstd, int M, int N, float eps, int act,
+                   sd_stream stream);
+/* number of dw partial rows sd_rmsnorm_bwd writes (size dw_partial >= blocks * N) */
+int sd_rmsnorm_bwd_blocks(int M, int N);
+int sd_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* dy, float* dx, float* dw,
+                   float* dw_partial, int M, int N, int act, int accumulate_dx, int accumulate_dw, sd_stream stream);
+/* out[n] (+)= sum_r in[r*ld + n] (fixed-order column sums; bias gradients) */
+int sd_colsum(const float* in, float* out, int R, int N, long ld, int accumulate, sd_stream stream);
+
+/* ---------------------------------------------------------------- categorical latents
+ * Straight-through one-hot sample of unimix categoricals (OneHotDist.__init__/rsample, distributions.py:16-33;
+ * RSSM.get_dist(...).rsample(), rssm.py:177,194,219-220). groups = rows*S categoricals of K logits each.
+ * Gumbel noise = Philox(seed, stream_id, step, (group + group_offset)*K + k) (see oracle/noise.py).
+ * out = onehot(argmax) - y_soft + y_soft; index (groups) optional; entropy (groups) optional (metrics). */
+int sd_onehot_sample_fwd(const float* logits, float* out, int* index, float* entropy, long groups, int K,
+                         float unimix, uint64_t seed, int stream_id, int step, long group_offset, sd_stream stream);
+/* straight-through gradient: d logits (+)= d/dlogits <dout, y_soft> (recomputes y_soft from logits+noise) */
+int sd_onehot_sample_bwd(const float* logits, const float* dout, float* dlogits, long groups, int K, float unimix,
+                         uint64_t seed, int stream_id, int step, long group_offset, int accumulate, sd_stream stream);
+/* discrete actor: log_prob(action one-hot) and entropy of the unimix categorical (OneHotDist, distributions.py:16-36) */
+int sd_onehot_logp_ent_fwd(const float* logits, const float* action, float* logp, float* ent, long rows, int K,
+                           float unimix, sd_stream stream);
+int sd_onehot_logp_ent_bwd(const float* logits, const float* action, const float* glogp, const float* gent,
+                           float* dlogits, long rows, int K, float unimix, sd_stream stream);
+/* KL(post || prior) on raw logits summed over S per row (dists.kl + RSSM.kl_loss sum, rssm.py:222-230) */
+int sd_kl_fwd(const float* post, const float* prior, float* kl_row, int rows, int S, int K, sd_stream stream);
+/* gradients of clip(kl_row, min=free): d_post <- g_rep * pa (lpa - lpb - kl_s), d_prior <- g_dyn * (pb - pa) */
+int sd_kl_bwd(const float* post, const float* prior, const float* kl_row, const float* g_rep, const float* g_dyn,
+              float free_nats, float* d_post, float* d_prior, int rows, int S, int K, int acc_post, int acc_prior,
+              sd_stream stream);
+
+/* ---------------------------------------------------------------- heads
+ * symexp two-hot (TwoHot, distributions.py:67-129; symexp_twohot bins 242-251): mode, log_prob fwd/bwd. NB odd <= 255 */
+int sd_twohot_mode(const float* logits, const float* bins, float* out, long rows, int NB, sd_stream stream);
+int sd_twohot_logp_fwd(const float* logits, const float* bins, const float* target, float* logp, long rows, int NB,
+                       sd_stream stream);
+int sd_twohot_logp_bwd(const float* logits, const float* bins, const float* target, const float* glogp,
+                       float* dlogits, long rows, int NB, int accumulate, sd_stream stream);
+/* bounded normal actor (bounded_normal, distributions.py:217-222): x (rows, 2A) = [mean | std-logit] */
+int sd_bnormal_sample(const float* x, float* action, long rows, int A, float min_std, float max_std, uint64_t seed,
+                      int stream_id, int step, long row_offset, sd_stream stream);
+int sd_bnormal_logp_ent_fwd(const float* x, const float* action, float* logp, float* ent, long rows, int A,
+                            float min_std, float max_std, sd_stream stream);
+int sd_bnormal_logp_ent_bwd(const float* x, const float* action, const float* glogp, const float* gent, float* dx,
+                            long rows, int A, float min_std, float max_std, sd_stream stream);
+/* Bernoulli(logits) continue head (binary, distributions.py:238): logp, mean = sigmoid */
+int sd_bernoulli_fwd(const float* logit, const float* value, float* logp, float* mean, long rows, sd_stream stream);
+int sd_bernoulli_bwd(const float* logit, const float* value, const float* glogp, float* dlogit, long rows,
+                     sd_stream stream);
+
+/* ---------------------------------------------------------------- RSSM deterministic transition
+ * GRU-style gates of Deter.forward (rssm.py:65-75) on the dyn_gru BlockLinear output gates (M, G, 3, Dg). */
+int sd_gru_fwd(const float* gates, const float* h, float* out, long M, int G, int Dg, sd_stream stream);
+int sd_gru_bwd(const float* gates, const float* h, const float* dout, float* dgates, float* dh, long M, int G, int Dg,
+               int accumulate_dh, sd_stream stream);
+/* a / max(|a|, 1) (rssm.py:44) */
+int sd_action_norm(const float* a, float* y, long n, sd_stream stream);
+/* y[r,:] = mask[r*mask_stride] ? 0 : x[r,:]   (reset of the posterior state, rssm.py:161-165) */
+int sd_mask_rows(const float* x, const uint8_t* mask, long mask_stride, float* y, long rows, int width,
+                 sd_stream stream);
+
+/* ---------------------------------------------------------------- returns
+ * Dreamer._lambda_return (dreamer.py:694-707): ret (N, T-1). term/last may be NULL (term = 1 - sigmoid(cont_logit),
+ * last = 0: the imagination case, dreamer.py:597-602). With cont_logit also emits cont = sigmoid and
+ * weight = cumprod(cont * disc). boot(r, t) = boot[r*boot_row_stride + t*boot_t_stride]. */
+int sd_lambda_return(const float* reward, const float* term, const float* cont_logit, const float* last,
+                     const float* boot, long boot_row_stride, long boot_t_stride, float* ret, float* cont,
+                     float* weight, int N, int T, float disc, float lamb, sd_stream stream);
+/* ReturnEMA (networks.py:406-422): torch.quantile(x, [q0, q1]) (exact radix select + lerp), ema <- alpha q +
+ * (1-alpha) ema, offset_scale = (ema[0], max(ema[1]-ema[0], 1)). quantiles (2) optional. */
+int sd_return_ema(const float* x, int n, float* ema, float* offset_scale, float* quantiles, float alpha, float q0,
+                  float q1, sd_stream stream);
+
+/* ---------------------------------------------------------------- convolution (NHWC, implicit GEMM on MFMA)
+ * Conv2dSamePad, stride 1 (networks.py:59-85): out (Nb, Hs<<ups, Ws<<ups, Co); w (Co, kh, kw, Ci); ups = 1 reads
+ * the input through nn.Upsample(2, nearest) (ConvDecoder, networks.py:259-265). */
+int sd_conv2d_fwd(const float* in, const float* w, const float* bias, float* out, int Nb, int Hs, int Ws, int Ci,
+                  int Co, int kh, int kw, int pad, int ups, sd_stream stream);
+/* dw_db (Co, kh*kw*Ci + 1) = [dW | d bias]; ksplit > 1 needs workspace >= ksplit*Co*(kh*kw*Ci+1) floats */
+int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db, float* workspace, long ws_floats, int ksplit,
+                    int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad, int ups, sd_stream stream);
+/* Wf[ci][ky][kx][co] = W[co][kh-1-ky][kw-1-kx][ci]  (input-gradient conv weights) */
+int sd_conv_flip_weight(const float* w, float* wf, int Co, int kh, int kw, int Ci, sd_stream stream);
+/* backward of nearest 2x upsample: din (Nb,H,W,C) = 2x2 sums of du (Nb,2H,2W,C) */
+int sd_sumpool2(const float* du, float* din, int Nb, int H, int W, int C, sd_stream stream);
+/* ConvEncoder layer tail: y = SiLU(RMSNorm2D(MaxPool2d(2)(x))) (networks.py:211-214); pooled/amax/rstd saved.
+ * nchw_flat: write y in the reference's NCHW flatten order (networks.py:232). C <= 128. */
+int sd_pool_rms_fwd(const float* x, const float* w, float* pooled, uint8_t* amax, float* y, float* rstd, int Nb,
+                    int H, int W, int C, float eps, int nchw_flat, sd_stream stream);
+int sd_pool_rms_bwd_blocks(int Nb, int H, int W);
+int sd_pool_rms_bwd(const float* pooled, const uint8_t* amax, const float* w, const float* rstd, const float* dy,
+                    float* dx, float* dw, float* dw_partial, int Nb, int H, int W, int C, int nchw_flat,
+                    int accumulate_dw, sd_stream stream);
+
+/* ---------------------------------------------------------------- optimiser (flat parameter arena)
+ * clip_grad_agc_ (agc.py:15-53) + LaProp.step (laprop.py:46-118) + LambdaLR warm-up (dreamer.py:214-225), fused.
+ * chunk tables are device arrays built once by the caller; scalars = sd_opt_scalars_bytes() zeroed bytes of device
+ * memory (float64 step / lr EMAs); workspace >= 3*nchunks floats; grad_norms (ntensors) optional. */
+int sd_opt_scalars_bytes(void);
+int sd_agc_laprop_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, const long* chunk_beg,
+                       const long* chunk_end, const int* chunk_tensor, const int* tensor_chunk0, int nchunks,
+                       int ntensors, float* workspace, void* scalars, float* grad_norms, float clip, float pmin,
+                       double lr0, double warmup, double beta1, double beta2, double eps, sd_stream stream);
+/* slow critic: dst = mix*src + (1-mix)*dst (Dreamer._update_slow_target, dreamer.py:242-249) */
+int sd_polyak(const float* src, float* dst, long n, float mix, sd_stream stream);
+
+/* ---------------------------------------------------------------- misc
+ * Dreamer.preprocess + ConvEncoder's "-0.5": out = in/255 - shift (dreamer.py:710-713, networks.py:224) */
+int sd_u8_to_f32(const uint8_t* in, float* out, long n, float shift, sd_stream stream);
+/* symlog (distributions.py:8-9) for MLP-encoder inputs (networks.py:333-334) */
+int sd_symlog(const float* x, float* y, long n, sd_stream stream);
+int sd_fill_gumbel(float* out, long n, uint64_t seed, int stream_id, int step, long offset, sd_stream stream);
+int sd_fill_normal(float* out, long n, uint64_t seed, int stream_id, int step, long offset, sd_stream stream);
+/* Barlow-twins loss pieces (dreamer.py:525-532): column mean / unbiased std, standardise fwd/bwd,
+ * loss = sum (c_ii-1)^2 + lambd sum_{i!=j} c_ij^2 (partial >= 2*nblocks floats), dc = g * dloss/dc */
+int sd_colstats(const float* x, int R, int C, float* mean, float* stdv, sd_stream stream);
+int sd_standardize(const float* x, const float* mean, const float* stdv, float* y, long R, int C, float eps,
+                   sd_stream stream);
+int sd_standardize_bwd(const float* x, const float* mean, const float* stdv, const float* dn, float* dx, int R,
+                       int C, float eps, sd_stream stream);
+int sd_barlow_loss(const float* c, int E, float lambd, float* partial, int nblocks, float* loss, sd_stream stream);
+int sd_barlow_dc(const float* c, const float* g, float* dc, int E, float lambd, sd_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

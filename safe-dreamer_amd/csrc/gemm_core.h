@@ -1,0 +1,233 @@
+// Shared fp32-MFMA GEMM block core (see gemm.hip for the design notes). Operand "loaders" supply BK-deep
+// register tiles, so dense matrices (gemm.hip) and implicit-im2col convolution operands (conv.hip) share one
+// MFMA/LDS pipeline and one epilogue.
+#pragma once
+#include "common.h"
+
+namespace sdg {
+namespace {  // internal linkage: the core is instantiated per translation unit
+
+constexpr int BK = 16;
+constexpr int LDS_ROW = BK + 4;  // floats
+
+struct GemmArgs {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias;
+  float* ws;
+  long lda, ldb, ldc;
+  long sA, sB, sC, sBias;
+  int M, N, K, batch, ksplit, kchunk;
+  float alpha, beta;
+};
+
+// Load a ROWS x BK tile of an operand into registers (rows = m for A / n for B).
+// KC: k contiguous (row-major in k, `ld` between rows) ; else rows contiguous (`ld` between k's).
+template <int ROWS, bool KC, bool VEC>
+struct TileLoader {
+  static constexpr int NV = ROWS * BK / 4 / 256 > 0 ? ROWS * BK / 4 / 256 : 1;  // float4 per thread
+  f32x4 r[NV];
+
+  SD_DEV void load(const float* __restrict__ p, long ld, int row0, int nrows, int k0, int kend) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = tid + v * 256;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (i < ROWS * BK / 4) {
+        if (KC) {
+          const int row = i / (BK / 4), kq = i % (BK / 4);
+          const int gr = row0 + row, gk = k0 + 4 * kq;
+          if (gr < nrows) {
+            const float* q = p + (long)gr * ld + gk;
+            if (VEC && gk + 3 < kend) {
+              x = *reinterpret_cast<const f32x4*>(q);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (gk + j < kend) x[j] = q[j];
+            }
+          }
+        } else {
+          const int k = i % BK, rq = i / BK;
+          const int gk = k0 + k, gr = row0 + 4 * rq;
+          if (gk < kend) {
+            const float* q = p + (long)gk * ld + gr;
+            if (VEC && gr + 3 < nrows) {
+              x = *reinterpret_cast<const f32x4*>(q);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (gr + j < nrows) x[j] = q[j];
+            }
+          }
+        }
+      }
+      r[v] = x;
+    }
+  }
+
+  SD_DEV void store(float* lds) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = tid + v * 256;
+      if (i < ROWS * BK / 4) {
+        if (KC) {
+          const int row = i / (BK / 4), kq = i % (BK / 4);
+          *reinterpret_cast<f32x4*>(lds + row * LDS_ROW + 4 * kq) = r[v];
+        } else {
+          const int k = i % BK, rq = i / BK;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) lds[(4 * rq + j) * LDS_ROW + k] = r[v][j];
+        }
+      }
+    }
+  }
+};
+
+// Dense operand: ROWS x BK tiles of a strided matrix (rows = m for A / n for B).
+template <int ROWS, bool KC, bool VEC>
+struct DenseOperand {
+  TileLoader<ROWS, KC, VEC> t;
+  const float* p;
+  long ld;
+  int nrows, row0;
+  SD_DEV DenseOperand(const float* base, long ld_, int nrows_, int row0_) : p(base), ld(ld_), nrows(nrows_), row0(row0_) {}
+  SD_DEV void load(int k0, int kend) { t.load(p, ld, row0, nrows, k0, kend); }
+  SD_DEV void store(float* lds) const { t.store(lds); }
+};
+
+template <int BM, int BN, int WM, int WN, class OpA, class OpB>
+SD_DEV void gemm_block(const GemmArgs& g, OpA& la, OpB& lb, int bm0, int bn0, int b, int split, int kbeg, int kend) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDS_ROW];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  constexpr int STAGE = (BM + BN) * LDS_ROW;  // floats per pipeline stage: [A rows | B rows]
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    la.load(kbeg, kend);
+    lb.load(kbeg, kend);
+    la.store(smem);
+    lb.store(smem + BM * LDS_ROW);
+    __syncthreads();
+  }
+  const int h = lane >> 5, l32 = lane & 31;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      la.load(kbeg + (kt + 1) * BK, kend);
+      lb.load(kbeg + (kt + 1) * BK, kend);
+    }
+    float af[TM][8], bf[TN][8];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* q = smem + cur * STAGE + (wr * WM + 32 * i + l32) * LDS_ROW + 8 * h;
+      f32x4 x0 = *reinterpret_cast<const f32x4*>(q);
+      f32x4 x1 = *reinterpret_cast<const f32x4*>(q + 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) { af[i][s] = x0[s]; af[i][s + 4] = x1[s]; }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* q = smem + cur * STAGE + BM * LDS_ROW + (wc * WN + 32 * j + l32) * LDS_ROW + 8 * h;
+      f32x4 x0 = *reinterpret_cast<const f32x4*>(q);
+      f32x4 x1 = *reinterpret_cast<const f32x4*>(q + 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) { bf[j][s] = x0[s]; bf[j][s + 4] = x1[s]; }
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    if (kt + 1 < nk) {
+      la.store(smem + (cur ^ 1) * STAGE);
+      lb.store(smem + (cur ^ 1) * STAGE + BM * LDS_ROW);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: reg r of a 32x32 tile -> row (r&3) + 8*(r>>2) + 4*h, col l32
+  if (g.ksplit > 1) {
+    float* W = g.ws + ((long)split * g.batch + b) * (long)g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = bn0 + wc * WN + 32 * j + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = bm0 + wr * WM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (m < g.M && n < g.N) W[(long)m * g.N + n] = g.alpha * acc[i][j][r];
+        }
+      }
+    return;
+  }
+  float* C = g.C + (long)b * g.sC;
+  const float* bias = g.bias ? g.bias + (long)b * g.sBias : nullptr;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = bn0 + wc * WN + 32 * j + l32;
+      const float bv = (bias && n < g.N) ? bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = bm0 + wr * WM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < g.M && n < g.N) {
+          float v = g.alpha * acc[i][j][r] + bv;
+          float* c = C + (long)m * g.ldc + n;
+          if (g.beta != 0.f) v += g.beta * *c;
+          *c = v;
+        }
+      }
+    }
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool VA, bool VB>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+  const int bn0 = blockIdx.x * BN, bm0 = blockIdx.y * BM;
+  const int b = blockIdx.z / g.ksplit, split = blockIdx.z % g.ksplit;
+  const int kbeg = split * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  DenseOperand<BM, AK, VA> la(g.A + (long)b * g.sA, g.lda, g.M, bm0);
+  DenseOperand<BN, BKC, VB> lb(g.B + (long)b * g.sB, g.ldb, g.N, bn0);
+  gemm_block<BM, BN, WM, WN>(g, la, lb, bm0, bn0, b, split, kbeg, kend);
+}
+
+__global__ void gemm_reduce_kernel(GemmArgs g) {
+  const long MN = (long)g.M * g.N;
+  const long total = MN * g.batch;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(t / MN);
+    const long mn = t % MN;
+    const int m = (int)(mn / g.N), n = (int)(mn % g.N);
+    float v = 0.f;
+    for (int s = 0; s < g.ksplit; ++s) v += g.ws[((long)s * g.batch + b) * MN + mn];
+    if (g.bias) v += g.bias[(long)b * g.sBias + n];
+    float* c = g.C + (long)b * g.sC + (long)m * g.ldc + n;
+    if (g.beta != 0.f) v += g.beta * *c;
+    *c = v;
+  }
+}
+
+
+}  // namespace
+}  // namespace sdg

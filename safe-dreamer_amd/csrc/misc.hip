@@ -1,0 +1,235 @@
+// Small elementwise / reduction kernels of the update path and the Barlow (r2dreamer) loss.
+//
+//  * image uint8 -> f32 (Dreamer.preprocess, dreamer.py:710-713) with the encoder's "-0.5" (networks.py:224);
+//  * symlog inputs (MLP encoder, networks.py:333-334); action normalisation a / max(|a|, 1) (rssm.py:44);
+//    reset masking of the recurrent state (rssm.py:161-165);
+//  * Barlow twins loss (dreamer.py:525-532): column mean / unbiased std, standardisation fwd/bwd, the
+//    invariance + redundancy reduction over the E x E cross-correlation and its gradient;
+//  * noise buffers (philox.h) for tests and diagnostics.
+#include "common.h"
+#include "philox.h"
+#include "sdhip.h"
+
+namespace {
+
+__global__ void u8_to_f32(const uint8_t* __restrict__ in, float* __restrict__ out, long n, float shift) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (float)in[i] / 255.0f - shift;
+}
+
+__global__ void symlog_kernel(const float* __restrict__ x, float* __restrict__ y, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const float v = x[i];
+    const float s = v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f);
+    y[i] = s * log1pf(fabsf(v));
+  }
+}
+
+__global__ void action_norm_kernel(const float* __restrict__ a, float* __restrict__ y, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = a[i] / fmaxf(fabsf(a[i]), 1.f);
+}
+
+// y[r, :] = mask[r] ? 0 : x[r, :]   (mask is bool/uint8)
+__global__ void mask_rows_kernel(const float* __restrict__ x, const uint8_t* __restrict__ mask, long mask_stride,
+                                 float* __restrict__ y, long rows, int width) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * width) return;
+  const long r = i / width;
+  y[i] = mask[r * mask_stride] ? 0.f : x[i];
+}
+
+__global__ void fill_gumbel(float* out, long n, uint64_t seed, uint32_t stream, uint32_t step, long offset) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = sd_gumbel(seed, stream, step, (uint64_t)(i + offset));
+}
+__global__ void fill_normal(float* out, long n, uint64_t seed, uint32_t stream, uint32_t step, long offset) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = sd_normal(seed, stream, step, (uint64_t)(i + offset));
+}
+
+// column mean and unbiased std of x (R x C): two passes over rows, 4 row-partials per column, fixed order
+__global__ void colstats_kernel(const float* __restrict__ x, int R, int C, float* __restrict__ mean,
+                                float* __restrict__ stdv) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;
+  __shared__ float red[4][64];
+  __shared__ float mu_s[64];
+  float s = 0.f;
+  if (c < C)
+    for (int r = part; r < R; r += 4) s += x[(long)r * C + c];
+  red[part][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (part == 0) {
+    const float mu = (red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]) / (float)R;
+    mu_s[threadIdx.x] = mu;
+    if (c < C) mean[c] = mu;
+  }
+  __syncthreads();
+  const float mu = mu_s[threadIdx.x & 63];
+  float q = 0.f;
+  if (c < C)
+    for (int r = part; r < R; r += 4) {
+      const float d = x[(long)r * C + c] - mu;
+      q += d * d;
+    }
+  red[part][threadIdx.x & 63] = q;
+  __syncthreads();
+  if (part == 0 && c < C)
+    stdv[c] = sqrtf((red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]) / (float)(R - 1));
+}
+
+__global__ void standardize_kernel(const float* __restrict__ x, const float* __restrict__ mean,
+                                   const float* __restrict__ stdv, float* __restrict__ y, long R, int C, float eps) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * C) return;
+  const int c = (int)(i % C);
+  y[i] = (x[i] - mean[c]) / (stdv[c] + eps);
+}
+
+// dx = (dn - mean_r dn)/s - (x - mu) * A / (s^2 (R-1) sigma),  A = sum_r dn (x - mu),  s = sigma + eps
+__global__ void standardize_bwd_kernel(const float* __restrict__ x, const float* __restrict__ mean,
+                                       const float* __restrict__ stdv, const float* __restrict__ dn,
+                                       float* __restrict__ dx, int R, int C, float eps) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;
+  __shared__ float red0[4][64], red1[4][64];
+  __shared__ float mdn[64], aa[64];
+  const float mu = c < C ? mean[c] : 0.f;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < C)
+    for (int r = part; r < R; r += 4) {
+      const float d = dn[(long)r * C + c];
+      s0 += d;
+      s1 += d * (x[(long)r * C + c] - mu);
+    }
+  red0[part][threadIdx.x & 63] = s0;
+  red1[part][threadIdx.x & 63] = s1;
+  __syncthreads();
+  if (part == 0) {
+    const int l = threadIdx.x;
+    mdn[l] = (red0[0][l] + red0[1][l] + red0[2][l] + red0[3][l]) / (float)R;
+    aa[l] = red1[0][l] + red1[1][l] + red1[2][l] + red1[3][l];
+  }
+  __syncthreads();
+  if (c >= C) return;
+  const float sg = stdv[c];
+  const float sc = sg + eps;
+  const float m = mdn[threadIdx.x & 63], A = aa[threadIdx.x & 63];
+  const float k2 = A / (sc * sc * (float)(R - 1) * sg);
+  for (int r = part; r < R; r += 4) {
+    const long o = (long)r * C + c;
+    dx[o] = (dn[o] - m) / sc - (x[o] - mu) * k2;
+  }
+}
+
+// loss = sum_i (c_ii - 1)^2 + lambd * sum_{i!=j} c_ij^2 ; partial per block, then 1 block finishes
+__global__ void barlow_partial(const float* __restrict__ c, int E, float lambd, float* __restrict__ part) {
+  __shared__ float red[4];
+  float inv = 0.f, rd = 0.f;
+  const long n = (long)E * E;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / E), col = (int)(i % E);
+    const float v = c[i];
+    if (r == col) inv += (v - 1.f) * (v - 1.f);
+    else rd += v * v;
+  }
+  inv = block_sum<256>(inv, red);
+  rd = block_sum<256>(rd, red);
+  if (threadIdx.x == 0) { part[2 * blockIdx.x] = inv; part[2 * blockIdx.x + 1] = rd; }
+}
+
+__global__ void barlow_final(const float* __restrict__ part, int nb, float lambd, float* __restrict__ loss) {
+  __shared__ float red[4];
+  float inv = 0.f, rd = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) { inv += part[2 * i]; rd += part[2 * i + 1]; }
+  inv = block_sum<256>(inv, red);
+  rd = block_sum<256>(rd, red);
+  if (threadIdx.x == 0) loss[0] = inv + lambd * rd;
+}
+
+// dc_ij = g * (i == j ? 2 (c_ii - 1) : 2 lambd c_ij)
+__global__ void barlow_dc(const float* __restrict__ c, const float* __restrict__ g, float* __restrict__ dc, int E,
+                          float lambd) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)E * E) return;
+  const int r = (int)(i / E), col = (int)(i % E);
+  const float v = c[i];
+  dc[i] = g[0] * (r == col ? 2.f * (v - 1.f) : 2.f * lambd * v);
+}
+
+int nb(long n) { return (int)((n + 255) / 256); }
+
+}  // namespace
+
+extern "C" int sd_u8_to_f32(const uint8_t* in, float* out, long n, float shift, sd_stream s) {
+  if (n <= 0) return SD_OK;
+  u8_to_f32<<<nb(n), 256, 0, (hipStream_t)s>>>(in, out, n, shift);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_symlog(const float* x, float* y, long n, sd_stream s) {
+  if (n <= 0) return SD_OK;
+  symlog_kernel<<<nb(n), 256, 0, (hipStream_t)s>>>(x, y, n);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_action_norm(const float* a, float* y, long n, sd_stream s) {
+  if (n <= 0) return SD_OK;
+  action_norm_kernel<<<nb(n), 256, 0, (hipStream_t)s>>>(a, y, n);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_mask_rows(const float* x, const uint8_t* mask, long mask_stride, float* y, long rows, int width,
+                            sd_stream s) {
+  if (rows <= 0) return SD_OK;
+  mask_rows_kernel<<<nb(rows * width), 256, 0, (hipStream_t)s>>>(x, mask, mask_stride, y, rows, width);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_fill_gumbel(float* out, long n, uint64_t seed, int stream_id, int step, long offset, sd_stream s) {
+  if (n <= 0) return SD_OK;
+  fill_gumbel<<<nb(n), 256, 0, (hipStream_t)s>>>(out, n, seed, stream_id, step, offset);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_fill_normal(float* out, long n, uint64_t seed, int stream_id, int step, long offset, sd_stream s) {
+  if (n <= 0) return SD_OK;
+  fill_normal<<<nb(n), 256, 0, (hipStream_t)s>>>(out, n, seed, stream_id, step, offset);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_colstats(const float* x, int R, int C, float* mean, float* stdv, sd_stream s) {
+  if (R <= 1 || C <= 0) return SD_EARG;
+  colstats_kernel<<<(C + 63) / 64, 256, 0, (hipStream_t)s>>>(x, R, C, mean, stdv);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_standardize(const float* x, const float* mean, const float* stdv, float* y, long R, int C, float eps,
+                              sd_stream s) {
+  if (R <= 0) return SD_OK;
+  standardize_kernel<<<nb(R * C), 256, 0, (hipStream_t)s>>>(x, mean, stdv, y, R, C, eps);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_standardize_bwd(const float* x, const float* mean, const float* stdv, const float* dn, float* dx,
+                                  int R, int C, float eps, sd_stream s) {
+  if (R <= 1) return SD_EARG;
+  standardize_bwd_kernel<<<(C + 63) / 64, 256, 0, (hipStream_t)s>>>(x, mean, stdv, dn, dx, R, C, eps);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_barlow_loss(const float* c, int E, float lambd, float* partial, int nblocks, float* loss,
+                              sd_stream s) {
+  barlow_partial<<<nblocks, 256, 0, (hipStream_t)s>>>(c, E, lambd, partial);
+  SD_LAUNCH_CHECK();
+  barlow_final<<<1, 256, 0, (hipStream_t)s>>>(partial, nblocks, lambd, loss);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_barlow_dc(const float* c, const float* g, float* dc, int E, float lambd, sd_stream s) {
+  barlow_dc<<<nb((long)E * E), 256, 0, (hipStream_t)s>>>(c, g, dc, E, lambd);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}

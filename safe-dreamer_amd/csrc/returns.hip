@@ -1,0 +1,139 @@
+// λ-returns, imagination weights and the ReturnEMA quantile tracker.
+//
+//  * sd_lambda_return: Dreamer._lambda_return (dreamer.py:694-707), one lane per row, reverse recurrence in
+//    registers; also emits the imagination continue probabilities and cumprod weights (dreamer.py:590-598)
+//    when given continue logits (term = 1 - sigmoid(logit), last = 0).
+//  * sd_return_ema: ReturnEMA.__call__ (networks.py:416-422): torch.quantile(x, [0.05, 0.95]) (linear
+//    interpolation, torch's lerp) via an exact 4-pass 8-bit radix select for the 4 order statistics, then the
+//    EMA update and (offset, scale). One 1024-thread workgroup; no host synchronisation (scalars stay on device).
+#include "common.h"
+#include "sdhip.h"
+
+namespace {
+
+__global__ void lambda_return_kernel(const float* __restrict__ reward, const float* __restrict__ term_in,
+                                     const float* __restrict__ cont_logit, const float* __restrict__ last_in,
+                                     const float* __restrict__ boot, long boot_row_stride, long boot_t_stride,
+                                     float* __restrict__ ret, float* __restrict__ cont_out, float* __restrict__ weight,
+                                     int N, int T, float disc, float lamb) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= N) return;
+  const long base = (long)r * T;
+  if (cont_logit && (cont_out || weight)) {
+    float w = 1.f;
+    for (int t = 0; t < T; ++t) {
+      const float c = sigmoidf_(cont_logit[base + t]);
+      if (cont_out) cont_out[base + t] = c;
+      w = w * (c * disc);  // torch.cumprod(imag_cont * disc)
+      if (weight) weight[base + t] = w;
+    }
+  }
+  float out = boot[(long)r * boot_row_stride + (long)(T - 1) * boot_t_stride];
+  for (int t = T - 2; t >= 0; --t) {
+    const int i = t + 1;
+    float term;
+    if (term_in) term = term_in[base + i];
+    else term = 1.f - sigmoidf_(cont_logit[base + i]);  // term = 1 - imag_cont (dreamer.py:599)
+    const float last = last_in ? last_in[base + i] : 0.f;
+    const float live = (1.f - term) * disc;
+    const float cnt = (1.f - last) * lamb;
+    const float interm = reward[base + i] + (1.f - cnt) * live * boot[(long)r * boot_row_stride + (long)i * boot_t_stride];
+    out = interm + live * cnt * out;
+    ret[(long)r * (T - 1) + t] = out;
+  }
+}
+
+SD_DEV uint32_t fkey(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+SD_DEV float funkey(uint32_t k) {
+  const uint32_t b = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(b);
+}
+
+// x: n floats. ema[2] updated in place; os[0] = offset, os[1] = scale, qout[2] = raw quantiles (optional)
+__global__ __launch_bounds__(1024) void return_ema_kernel(const float* __restrict__ x, int n, float* ema, float* os,
+                                                          float* qout, float alpha, float q0, float q1) {
+  __shared__ unsigned hist[4][256];
+  __shared__ uint32_t prefix[4];
+  __shared__ int rank[4];
+  __shared__ float val[4];
+  const int tid = threadIdx.x;
+  // ranks = q * (n - 1) in float32 (torch.quantile), below = floor, above = ceil
+  const float nm1 = (float)(n - 1);
+  const float r0 = q0 * nm1, r1 = q1 * nm1;
+  if (tid < 4) {
+    const float rr = tid < 2 ? r0 : r1;
+    const int lo = (int)floorf(rr);
+    const int hi = (int)ceilf(rr);
+    rank[tid] = (tid & 1) ? hi : lo;
+    prefix[tid] = 0;
+  }
+  __syncthreads();
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    for (int i = tid; i < 4 * 256; i += 1024) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (32 - 8 * pass));
+    for (int i = tid; i < n; i += 1024) {
+      const uint32_t k = fkey(x[i]);
+      const uint32_t d = (k >> shift) & 0xFFu;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if ((k & hmask) == prefix[q]) atomicAdd(&hist[q][d], 1u);
+    }
+    __syncthreads();
+    if (tid < 4) {
+      int rem = rank[tid];
+      int b = 0;
+      for (; b < 255; ++b) {
+        const int c = (int)hist[tid][b];
+        if (rem < c) break;
+        rem -= c;
+      }
+      prefix[tid] |= ((uint32_t)b << shift);
+      rank[tid] = rem;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    for (int q = 0; q < 4; ++q) val[q] = funkey(prefix[q]);
+    float qv[2];
+    for (int j = 0; j < 2; ++j) {
+      const float rr = j == 0 ? r0 : r1;
+      const float w = rr - floorf(rr);
+      const float a = val[2 * j], b = val[2 * j + 1];
+      qv[j] = w < 0.5f ? a + w * (b - a) : b - (b - a) * (1.f - w);  // torch.lerp
+    }
+    if (qout) { qout[0] = qv[0]; qout[1] = qv[1]; }
+    const float e0 = alpha * qv[0] + (1.f - alpha) * ema[0];
+    const float e1 = alpha * qv[1] + (1.f - alpha) * ema[1];
+    ema[0] = e0;
+    ema[1] = e1;
+    os[0] = e0;
+    os[1] = fmaxf(e1 - e0, 1.f);
+  }
+}
+
+}  // namespace
+
+extern "C" int sd_lambda_return(const float* reward, const float* term, const float* cont_logit, const float* last,
+                                const float* boot, long boot_row_stride, long boot_t_stride, float* ret, float* cont,
+                                float* weight, int N, int T, float disc, float lamb, sd_stream s) {
+  if (N <= 0 || T <= 0) return SD_OK;
+  if (!term && !cont_logit) return SD_EARG;
+  lambda_return_kernel<<<(N + 255) / 256, 256, 0, (hipStream_t)s>>>(reward, term, cont_logit, last, boot,
+                                                                   boot_row_stride, boot_t_stride, ret, cont, weight, N,
+                                                                   T, disc, lamb);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_return_ema(const float* x, int n, float* ema, float* offset_scale, float* quantiles, float alpha,
+                             float q0, float q1, sd_stream s) {
+  if (n <= 0) return SD_EARG;
+  return_ema_kernel<<<1, 1024, 0, (hipStream_t)s>>>(x, n, ema, offset_scale, quantiles, alpha, q0, q1);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}

@@ -1,0 +1,219 @@
+// Row-wise RMSNorm (+ SiLU) forward/backward: the `Linear -> RMSNorm(eps) -> SiLU` body of every MLP in the
+// model (rssm.py:16-31,106-130; networks.py:88-96,252-255,313-336) and RMSNorm2D on channels-last conv
+// activations (a channels-last row is exactly the reference's permuted RMSNorm row).
+//
+// One "team" of TEAM lanes owns a row (TEAM = 16/32/64 inside one wave, or 256 = the whole block for wide
+// rows); each lane keeps VPT columns in registers, so x is read once and y written once (HBM-bound: 8 B/elt).
+// Backward recomputes xhat and the SiLU derivative from (x, rstd) and emits the RMSNorm-weight gradient as
+// per-block partial sums (reduced by sd_colsum in a fixed order: deterministic).
+#include "common.h"
+#include "sdhip.h"
+
+namespace {
+
+template <int TEAM>
+SD_DEV float team_sum(float v, float* red) {
+  if (TEAM <= 64) return group_sum<TEAM>(v);
+  return block_sum<256>(v, red);
+}
+
+template <int TEAM, int VPT>
+__global__ __launch_bounds__(256) void rms_fwd(const float* __restrict__ x, const float* __restrict__ w,
+                                               float* __restrict__ y, float* __restrict__ rstd, int M, int N,
+                                               float eps, int act) {
+  constexpr int TPB = 256 / TEAM;  // teams per block
+  __shared__ float red[4];
+  const int team = threadIdx.x / TEAM, t = threadIdx.x % TEAM;
+  for (long row = (long)blockIdx.x * TPB + team; row < M; row += (long)gridDim.x * TPB) {
+    const float* xr = x + row * N;
+    float v[VPT];
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int c = t + j * TEAM;
+      v[j] = c < N ? xr[c] : 0.f;
+      ss += v[j] * v[j];
+    }
+    ss = team_sum<TEAM>(ss, red);
+    const float r = rsqrtf(ss / (float)N + eps);
+    if (t == 0 && rstd) rstd[row] = r;
+    float* yr = y + row * N;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int c = t + j * TEAM;
+      if (c < N) {
+        float z = v[j] * r * w[c];
+        yr[c] = act ? siluf_(z) : z;
+      }
+    }
+    if (TEAM == 256) __syncthreads();
+  }
+}
+
+// dx = r * (g - xhat * mean(g * xhat)),  g = dz * w,  dz = dy * silu'(z);  dw_part[block] = sum_rows dz * xhat
+template <int TEAM, int VPT>
+__global__ __launch_bounds__(256) void rms_bwd(const float* __restrict__ x, const float* __restrict__ w,
+                                               const float* __restrict__ rstd, const float* __restrict__ dy,
+                                               float* __restrict__ dx, float* __restrict__ dw_part, int M, int N,
+                                               int act, int accumulate_dx) {
+  constexpr int TPB = 256 / TEAM;
+  __shared__ float red[4];
+  __shared__ float wpart[TEAM == 256 ? 1 : TPB * TEAM * VPT];
+  const int team = threadIdx.x / TEAM, t = threadIdx.x % TEAM;
+  float dwacc[VPT];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) dwacc[j] = 0.f;
+  for (long row = (long)blockIdx.x * TPB + team; row < M; row += (long)gridDim.x * TPB) {
+    const float* xr = x + row * N;
+    const float* dyr = dy + row * N;
+    const float r = rstd[row];
+    float xh[VPT], g[VPT];
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int c = t + j * TEAM;
+      xh[j] = 0.f;
+      g[j] = 0.f;
+      if (c < N) {
+        const float xv = xr[c] * r;
+        const float wv = w[c];
+        float dz = dyr[c];
+        if (act) {
+          const float z = xv * wv;
+          const float s = sigmoidf_(z);
+          dz *= s * (1.f + z * (1.f - s));
+        }
+        xh[j] = xv;
+        g[j] = dz * wv;
+        dwacc[j] += dz * xv;
+        dot += g[j] * xv;
+      }
+    }
+    dot = team_sum<TEAM>(dot, red) / (float)N;
+    float* dxr = dx + row * N;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int c = t + j * TEAM;
+      if (c < N) {
+        const float v = r * (g[j] - xh[j] * dot);
+        dxr[c] = accumulate_dx ? dxr[c] + v : v;
+      }
+    }
+    if (TEAM == 256) __syncthreads();
+  }
+  if (!dw_part) return;
+  if (TEAM == 256) {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int c = t + j * TEAM;
+      if (c < N) dw_part[(long)blockIdx.x * N + c] = dwacc[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) wpart[(team * VPT + j) * TEAM + t] = dwacc[j];
+    __syncthreads();
+    for (int c = threadIdx.x; c < N; c += 256) {
+      const int j = c / TEAM, tt = c % TEAM;
+      float s = 0.f;
+      for (int tm = 0; tm < TPB; ++tm) s += wpart[(tm * VPT + j) * TEAM + tt];
+      dw_part[(long)blockIdx.x * N + c] = s;
+    }
+  }
+}
+
+// out[n] (+)= sum_r in[r * ld + n]   (column sums in a fixed order)
+__global__ void colsum_kernel(const float* __restrict__ in, float* __restrict__ out, int R, int N, long ld,
+                              int accumulate) {
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;  // 4 partial sums per column
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (n < N)
+    for (int r = part; r < R; r += 4) s += in[(long)r * ld + n];
+  red[part][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (part == 0 && n < N) {
+    float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    out[n] = accumulate ? out[n] + v : v;
+  }
+}
+
+int pick_vpt(int n) {
+  if (n <= 1) return 1;
+  if (n <= 2) return 2;
+  if (n <= 3) return 3;
+  if (n <= 4) return 4;
+  if (n <= 8) return 8;
+  return 16;
+}
+
+template <int TEAM>
+int grid_for(int M) {
+  long teams = (M + 0L);
+  long blocks = (teams + 256 / TEAM - 1) / (256 / TEAM);
+  return (int)(blocks < 8192 ? blocks : 8192);
+}
+
+#define SD_RMS_DISPATCH(KERNEL, TEAMV, ...)                                             \
+  switch (pick_vpt((N + TEAMV - 1) / TEAMV)) {                                          \
+    case 1: KERNEL<TEAMV, 1><<<grid, 256, 0, stream>>>(__VA_ARGS__); break;              \
+    case 2: KERNEL<TEAMV, 2><<<grid, 256, 0, stream>>>(__VA_ARGS__); break;              \
+    case 3: KERNEL<TEAMV, 3><<<grid, 256, 0, stream>>>(__VA_ARGS__); break;              \
+    case 4: KERNEL<TEAMV, 4><<<grid, 256, 0, stream>>>(__VA_ARGS__); break;              \
+    case 8: KERNEL<TEAMV, 8><<<grid, 256, 0, stream>>>(__VA_ARGS__); break;              \
+    default: KERNEL<TEAMV, 16><<<grid, 256, 0, stream>>>(__VA_ARGS__); break;            \
+  }
+
+int team_for(int N) {
+  if (N <= 64) return 16;
+  if (N <= 1024) return 64;
+  return 256;
+}
+
+}  // namespace
+
+extern "C" int sd_rmsnorm_fwd(const float* x, const float* w, float* y, float* rstd, int M, int N, float eps,
+                              int act, sd_stream stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  if (M <= 0) return SD_OK;
+  if (N <= 0 || N > 4096) return SD_ESHAPE;
+  const int team = team_for(N);
+  if (team == 16) { int grid = grid_for<16>(M); SD_RMS_DISPATCH(rms_fwd, 16, x, w, y, rstd, M, N, eps, act) }
+  else if (team == 64) { int grid = grid_for<64>(M); SD_RMS_DISPATCH(rms_fwd, 64, x, w, y, rstd, M, N, eps, act) }
+  else { int grid = grid_for<256>(M); SD_RMS_DISPATCH(rms_fwd, 256, x, w, y, rstd, M, N, eps, act) }
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_rmsnorm_bwd_blocks(int M, int N) {
+  const int team = team_for(N);
+  return team == 16 ? grid_for<16>(M) : team == 64 ? grid_for<64>(M) : grid_for<256>(M);
+}
+
+extern "C" int sd_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* dy, float* dx,
+                              float* dw, float* dw_partial, int M, int N, int act, int accumulate_dx,
+                              int accumulate_dw, sd_stream stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  if (M <= 0) return SD_OK;
+  if (N <= 0 || N > 4096) return SD_ESHAPE;
+  const int team = team_for(N);
+  float* part = dw ? dw_partial : nullptr;
+  int grid;
+  if (team == 16) { grid = grid_for<16>(M); SD_RMS_DISPATCH(rms_bwd, 16, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
+  else if (team == 64) { grid = grid_for<64>(M); SD_RMS_DISPATCH(rms_bwd, 64, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
+  else { grid = grid_for<256>(M); SD_RMS_DISPATCH(rms_bwd, 256, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
+  SD_LAUNCH_CHECK();
+  if (dw) {
+    colsum_kernel<<<(N + 63) / 64, 256, 0, stream>>>(dw_partial, dw, grid, N, N, accumulate_dw);
+    SD_LAUNCH_CHECK();
+  }
+  return SD_OK;
+}
+
+extern "C" int sd_colsum(const float* in, float* out, int R, int N, long ld, int accumulate, sd_stream stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  if (N <= 0) return SD_OK;
+  colsum_kernel<<<(N + 63) / 64, 256, 0, stream>>>(in, out, R, N, ld, accumulate);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}

@@ -1,0 +1,107 @@
+"""ctypes binding of libsdhip.so (include/sdhip.h) — the only way the product reaches the GPU kernels.
+
+There is no CPU fallback: if the library is missing or fails to load, importing this module raises.
+Device pointers come from torch tensors (PyTorch is the allocator/stream provider only); every call is
+enqueued on torch's current HIP stream, so the whole update can be captured into a HIP graph.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SDHIP_LIB", os.path.join(_HERE, "_lib", "libsdhip.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"libsdhip.so not found at {LIB_PATH}: build it with `make -C safe-dreamer_amd/csrc` "
+        "(or __graft_entry__.build()). The HIP path has no fallback.")
+lib = ctypes.CDLL(LIB_PATH)
+
+c_float_p = ctypes.c_void_p
+c_long = ctypes.c_long
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_ptr = ctypes.c_void_p
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("A", c_ptr), ("B", c_ptr), ("C", c_ptr), ("bias", c_ptr),
+        ("lda", c_long), ("ldb", c_long), ("ldc", c_long),
+        ("strideA", c_long), ("strideB", c_long), ("strideC", c_long), ("strideBias", c_long),
+        ("M", c_int), ("N", c_int), ("K", c_int), ("batch", c_int),
+        ("a_kcontig", c_int), ("b_kcontig", c_int),
+        ("ksplit", c_int), ("tile", c_int),
+        ("alpha", c_float), ("beta", c_float),
+    ]
+
+
+HEADER = os.environ.get("SDHIP_HEADER", os.path.join(_HERE, "..", "..", "include", "sdhip.h"))
+
+_CTYPES = {
+    "int": c_int, "long": c_long, "float": c_float, "double": ctypes.c_double, "uint64_t": ctypes.c_uint64,
+    "sd_stream": c_ptr, "void": None,
+}
+
+
+def _parse_header(path):
+    """name -> argtypes for every `int sd_*(...);` declaration in include/sdhip.h (the ABI's single source)."""
+    import re
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    sigs = {}
+    for m in re.finditer(r"\bint\s+(sd_\w+)\s*\(([^)]*)\)\s*;", text):
+        name, args = m.group(1), m.group(2).strip()
+        types = []
+        if args and args != "void":
+            for a in args.split(","):
+                a = a.strip()
+                if "*" in a:
+                    types.append(ctypes.POINTER(GemmDesc) if "sd_gemm_desc" in a else c_ptr)
+                else:
+                    t = a.replace("const ", "").split()[0]
+                    types.append(_CTYPES[t])
+        sigs[name] = types
+    return sigs
+
+
+_SIGS = _parse_header(HEADER)
+
+
+def _bind(name, argtypes):
+    fn = getattr(lib, name)
+    fn.argtypes = argtypes
+    fn.restype = c_int
+    return fn
+
+
+fns = {}
+
+
+def register(name, argtypes):
+    fns[name] = _bind(name, argtypes)
+    return fns[name]
+
+
+for _n, _a in _SIGS.items():
+    register(_n, _a)
+
+ABI_VERSION = lib.sd_abi_version()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def check(rc, name=""):
+    if rc != 0:
+        raise NativeError(f"{name} failed with status {rc}")
+
+
+def call(name, *args):
+    check(fns[name](*args), name)
+
+
+def exported_symbols():
+    return sorted(_SIGS)

@@ -1,0 +1,400 @@
+"""Dreamer agent (reference: world_model/dreamer.py), MI355X-native.
+
+Public surface kept from the reference: `Dreamer(config.model, obs_space, act_space)`,
+`.update(replay_buffer) -> metrics`, `._cal_grad`, `._imagine`, `._lambda_return`, `.act(obs, state, eval)`,
+`.get_initial_state(B)`, `.preprocess`, `._named_params`, `state_dict()` with the reference's keys (including the
+`_frozen_*` aliases), optimizer found at `._optimizer` / `._scheduler.optimizer`.
+
+Differences by design (documented in DESIGN.md):
+  * fp32 end to end (the reference's fp16 autocast + GradScaler are replaced by exact-f32 MFMA); `opt/grad_scale`=1;
+  * sampling noise is counter-based (seed, stream, step, global row) instead of torch's global RNG, so results are
+    reproducible across devices and identical under data-parallel sharding; `update()` draws seed = base + count;
+  * imagination / heads are time-major internally; returned tensors use the reference layouts;
+  * data parallel: `rank`/`world` row offsets for the noise, RCCL all-reduce of the flat gradient arena, global
+    ReturnEMA quantiles (all-gather) and Barlow statistics (sdreamer/parallel.py).
+"""
+from __future__ import annotations
+
+import copy
+import math
+from collections import OrderedDict
+
+import torch
+from torch import nn
+
+from . import kernels as K
+from . import ops
+from . import parallel
+from .networks import MLPHead, MultiDecoder, MultiEncoder, Projector, ReturnEMA
+from .optim import LaProp, WarmupSchedule
+from .rssm import RSSM, STREAM_ACT, STREAM_IMG, STREAM_POLICY
+
+
+def _symexp_bins(n, device):  # symexp_twohot bins, distributions.py:242-251
+    if n % 2 == 1:
+        half = torch.linspace(-20, 0, (n - 1) // 2 + 1, dtype=torch.float32)
+        half = torch.sign(half) * torch.expm1(torch.abs(half))
+        bins = torch.cat([half, -half[:-1].flip(0)], 0)
+    else:
+        half = torch.linspace(-20, 0, n // 2, dtype=torch.float32)
+        half = torch.sign(half) * torch.expm1(torch.abs(half))
+        bins = torch.cat([half, -half.flip(0)], 0)
+    return bins.to(device)
+
+
+def _tstats(t, prefix):  # tools.tensorstats (tools.py:275-281)
+    return {f"{prefix}_mean": t.mean(), f"{prefix}_std": t.std(), f"{prefix}_min": t.min(), f"{prefix}_max": t.max()}
+
+
+class Dreamer(nn.Module):
+    def __init__(self, config, obs_space, act_space, rank=0, world=1):
+        super().__init__()
+        self.device = torch.device(config.device)
+        if self.device.type != "cuda":
+            raise RuntimeError("sdreamer.Dreamer runs on a HIP device only (config.device must be cuda:N)")
+        self.config = config
+        self.act_entropy = float(config.act_entropy)
+        self.kl_free = float(config.kl_free)
+        self.imag_horizon = int(config.imag_horizon)
+        self.horizon = int(config.horizon)
+        self.lamb = float(config.lamb)
+        self.return_ema = ReturnEMA(device=self.device)
+        self.act_dim = act_space.n if hasattr(act_space, "n") else sum(act_space.shape)
+        self.rep_loss = str(config.rep_loss)
+        self.rank, self.world = int(rank), int(world)
+        shapes = {k: tuple(v.shape) for k, v in obs_space.spaces.items()}
+        if bool(config.use_multimodal_encoder):
+            raise NotImplementedError("multimodal CLIP encoder is out of scope (SURVEY.md §2: OUT OF SCOPE)")
+        self.encoder = MultiEncoder(config.encoder, shapes)
+        self.embed_size = self.encoder.out_dim
+        self.rssm = RSSM(config.rssm, self.embed_size, self.act_dim)
+        self.reward = MLPHead(config.reward, self.rssm.feat_size)
+        self.cont = MLPHead(config.cont, self.rssm.feat_size)
+        config.actor.shape = (act_space.n,) if hasattr(act_space, "n") else tuple(map(int, act_space.shape))
+        self.act_discrete = False
+        if hasattr(act_space, "multi_discrete"):
+            raise NotImplementedError("multi_discrete actions")
+        elif hasattr(act_space, "discrete"):
+            if "name" not in config.actor.dist:
+                config.actor.dist = config.actor.dist.disc
+            self.act_discrete = True
+        elif "name" not in config.actor.dist:
+            config.actor.dist = config.actor.dist.cont
+        self.actor = MLPHead(config.actor, self.rssm.feat_size)
+        self.value = MLPHead(config.critic, self.rssm.feat_size)
+        self.slow_target_update = int(config.slow_target_update)
+        self.slow_target_fraction = float(config.slow_target_fraction)
+        self._slow_value = copy.deepcopy(self.value)
+        for p in self._slow_value.parameters():
+            p.requires_grad = False
+        self._slow_value_updates = 0
+        self._loss_scales = dict(config.loss_scales)
+        self._log_grads = bool(config.log_grads)
+        modules = {"rssm": self.rssm, "actor": self.actor, "value": self.value, "reward": self.reward,
+                   "cont": self.cont, "encoder": self.encoder}
+        if self.rep_loss == "dreamer":
+            self.decoder = MultiDecoder(config.decoder, self.rssm._deter, self.rssm.flat_stoch, shapes)
+            recon = self._loss_scales.pop("recon")
+            self._loss_scales.update({k: recon for k in self.decoder.all_keys})
+            modules["decoder"] = self.decoder
+        elif self.rep_loss == "r2dreamer":
+            self.prj = Projector(self.rssm.feat_size, self.embed_size)
+            modules["projector"] = self.prj
+            self.barlow_lambd = float(config.r2dreamer.lambd)
+            if bool(config.r2dreamer.aug.enabled):
+                raise NotImplementedError("r2dreamer augmentation is an off-path variant (SURVEY.md §8(f) f4)")
+        else:
+            raise NotImplementedError(f"rep_loss={self.rep_loss} (off-path variant, SURVEY.md §8(f) f4)")
+        self._named_params = OrderedDict()
+        for name, module in modules.items():
+            for pn, prm in module.named_parameters():
+                if prm.requires_grad:
+                    self._named_params[f"{name}.{pn}"] = prm
+        super().to(self.device)
+        self._optimizer = LaProp(self._named_params.values(), lr=float(config.lr),
+                                 betas=(float(config.beta1), float(config.beta2)), eps=float(config.eps),
+                                 agc=float(config.agc), pmin=float(config.pmin), warmup=int(config.warmup or 0))
+        self._scheduler = WarmupSchedule(self._optimizer)
+        # slow critic arena mirrors the value head's slice of the parameter arena (one Polyak kernel)
+        a = self._optimizer.arena
+        vparams = [p for n, p in self._named_params.items() if n.startswith("value.")]
+        pos = {id(p): i for i, p in enumerate(a.params)}
+        idx = [pos[id(p)] for p in vparams]
+        self._v_lo, self._v_hi = a.offsets[idx[0]], a.offsets[idx[-1]] + a.sizes[idx[-1]]
+        self._slow_arena = a.data[self._v_lo:self._v_hi].clone()
+        for p, sp in zip(vparams, self._slow_value.parameters()):
+            j = pos[id(p)]
+            o = a.offsets[j] - self._v_lo
+            sp.data = self._slow_arena[o:o + a.sizes[j]].view(sp.shape)
+        self.rbins = _symexp_bins(int(config.reward.dist.bin_num), self.device)
+        self.vbins = _symexp_bins(int(config.critic.dist.bin_num), self.device)
+        self._updates = 0
+        self._seed_base = int(getattr(config, "seed", 0) or 0) * 1_000_003 + 12345
+        self.train()
+
+    # ------------------------------------------------------------------ reference API
+    def to(self, *args, **kwargs):  # dreamer.py:324-328 (frozen copies alias the live tensors by construction)
+        dev = torch.device(args[0]) if args and isinstance(args[0], (str, torch.device)) else None
+        if dev is not None and dev.type == "cuda" and (dev.index or 0) == (self.device.index or 0):
+            return self
+        return super().to(*args, **kwargs)
+
+    def set_task_name(self, task_name):  # dreamer.py:235-240 (no-op without the multimodal encoder)
+        pass
+
+    def train(self, mode=True):
+        super().train(mode)
+        self._slow_value.train(False)
+        return self
+
+    def _update_slow_target(self):  # dreamer.py:242-249
+        if self._slow_value_updates % self.slow_target_update == 0:
+            K.polyak(self._optimizer.arena.data[self._v_lo:self._v_hi], self._slow_arena, self.slow_target_fraction)
+        self._slow_value_updates += 1
+
+    @torch.no_grad()
+    def preprocess(self, data):  # dreamer.py:709-713
+        if "image" in data and data["image"].dtype == torch.uint8:
+            data["image"] = K.u8_to_f32(data["image"].contiguous())
+        return data
+
+    @torch.no_grad()
+    def get_initial_state(self, B):  # dreamer.py:359-363
+        stoch, deter = self.rssm.initial(B)
+        action = torch.zeros(B, self.act_dim, dtype=torch.float32, device=self.device)
+        return {"stoch": stoch, "deter": deter, "prev_action": action}
+
+    @torch.no_grad()
+    def act(self, obs, state, eval=False, seed=None, step=0):
+        """dreamer.py:330-357. obs: dict of (B, *) (image uint8), state: {stoch, deter, prev_action}."""
+        p_obs = self.preprocess(dict(obs))
+        embed = self.encoder({k: v.unsqueeze(1) for k, v in p_obs.items() if k in self.encoder.cnn_shapes
+                              or k in self.encoder.mlp_shapes})[:, 0]
+        B = embed.shape[0]
+        seed = self._seed_base + 7 if seed is None else seed
+        stoch, deter, _ = self.rssm.obs_step(state["stoch"], state["deter"], state["prev_action"], embed,
+                                             obs["is_first"], seed=seed, step=step, stream_id=STREAM_POLICY)
+        feat = self.rssm.get_feat(stoch, deter)
+        logits = self.actor.logits_nograd(feat)
+        if eval:
+            if self.act_discrete:
+                idx = logits.argmax(-1)  # argmax of unimix logits == argmax of raw logits
+                action = torch.nn.functional.one_hot(idx, self.act_dim).float()
+            else:
+                action = torch.tanh(logits[:, : self.act_dim])  # Normal mean = tanh(mean) (dreamer act uses .mode)
+        else:
+            action = self._sample_action(logits, seed, step, 0, STREAM_POLICY)
+        return action, {"stoch": stoch, "deter": deter, "prev_action": action}
+
+    def _sample_action(self, logits, seed, step, row_offset, stream_id):
+        d = self.config.actor.dist
+        if self.act_discrete:
+            return K.onehot_sample(logits.contiguous(), self.act_dim, float(d.unimix_ratio), seed, stream_id, step,
+                                   row_offset)
+        out = torch.empty(logits.shape[0], self.act_dim, dtype=torch.float32, device=logits.device)
+        K.nat.call("sd_bnormal_sample", K.p(logits.contiguous()), K.p(out), logits.shape[0], self.act_dim,
+                   float(d.min_std), float(d.max_std), int(seed), stream_id, int(step), int(row_offset), K.stream())
+        return out
+
+    # ------------------------------------------------------------------ update
+    def update(self, replay_buffer):
+        """dreamer.py:402-451."""
+        data, index, initial = replay_buffer.sample()
+        seed = self._seed_base + self._updates
+        (stoch, deter), mets = self.update_batch(data, initial, seed)
+        replay_buffer.update(index, stoch.detach(), deter.detach())
+        return mets
+
+    def update_batch(self, data, initial, seed, row_offset=None):
+        p_data = self.preprocess(dict(data))
+        self._update_slow_target()
+        self._optimizer.zero_grad()
+        ro = self.rank * p_data["action"].shape[0] if row_offset is None else row_offset
+        post, mets = self._cal_grad(p_data, initial, seed, ro)
+        if self.world > 1:
+            parallel.allreduce_mean_(self._optimizer.arena.grad)
+        self._optimizer.step()
+        self._scheduler.step()
+        mets["opt/lr"] = self._scheduler.get_lr()[0]
+        mets["opt/grad_scale"] = 1.0
+        self._updates += 1
+        return post, mets
+
+    def _cal_grad(self, data, initial, seed=0, row_offset=0):
+        """dreamer.py:453-671 (fp32). data: dict of (B, T, *) device tensors, image float in [0, 1]."""
+        losses, metrics = {}, {}
+        B, T = data["action"].shape[:2]
+        S, Kd, SK, D = self.rssm._stoch, self.rssm._discrete, self.rssm.flat_stoch, self.rssm._deter
+        embed = self.encoder(data)
+        post_stoch, post_deter, post_logit = self.rssm.observe(embed, data["action"], initial, data["is_first"],
+                                                               seed=seed, row_offset=row_offset)
+        prior_logit = self.rssm.prior(post_deter)
+        dyn_loss, rep_loss = self.rssm.kl_loss(post_logit, prior_logit, self.kl_free)
+        losses["dyn"] = dyn_loss.mean()
+        losses["rep"] = rep_loss.mean()
+        feat = self.rssm.get_feat(post_stoch, post_deter)
+        if self.rep_loss == "dreamer":
+            recon = self.decoder(post_stoch, post_deter)
+            for key, mode in recon.items():
+                if key in self.decoder.cnn_shapes:
+                    dist = (mode - data[key]) ** 2  # MSEDist(agg="sum"), distributions.py:146-155
+                    losses[key] = dist.sum(list(range(2, dist.dim()))).mean()
+                else:
+                    d = (mode - K.symlog(data[key].contiguous())) ** 2.0  # SymlogDist mse, distributions.py:174-190
+                    d = torch.where(d < 1e-8, torch.zeros_like(d), d)
+                    losses[key] = d.sum(list(range(2, d.dim()))).mean()
+        else:
+            x1 = self.prj(feat.reshape(B * T, -1))
+            x2 = embed.reshape(B * T, -1).detach()
+            losses["barlow"] = parallel.barlow(x1, x2, self.barlow_lambd, self.world)
+        rew_logits = self.reward(feat)
+        losses["rew"] = -ops.TwoHotLogProbFn.apply(rew_logits, self.rbins, data["reward"].float()).mean()
+        cont = 1.0 - data["is_terminal"].float()
+        losses["con"] = -ops.BernoulliLogProbFn.apply(self.cont(feat), cont).mean()
+        metrics["dyn_entropy"] = self.rssm.entropy(prior_logit).mean()
+        metrics["rep_entropy"] = self.rssm.entropy(post_logit).mean()
+
+        # ---- imagination (dreamer.py:578-636); time-major (H1, N, .)
+        N = B * T
+        H1 = self.imag_horizon + 1
+        H = H1 - 1
+        start = (post_stoch.detach().reshape(N, S, Kd), post_deter.detach().reshape(N, D))
+        ifeat, iact = self._imagine_tm(start, H1, seed, row_offset * T)
+        flat = ifeat.reshape(H1 * N, -1)
+        with torch.no_grad():
+            i_rew = K.twohot_mode(self.reward.logits_nograd(flat), self.rbins).view(H1, N)
+            i_contl = self.cont.logits_nograd(flat).view(H1, N)
+            i_val = K.twohot_mode(self.value.logits_nograd(flat), self.vbins).view(H1, N)
+            i_slow = K.twohot_mode(self._slow_value.logits_nograd(flat), self.vbins).view(H1, N)
+            disc = 1 - 1 / self.horizon
+            rew_n, contl_n, val_n = i_rew.t().contiguous(), i_contl.t().contiguous(), i_val.t().contiguous()
+            i_cont = torch.empty(N, H1, device=self.device)
+            weight = torch.empty(N, H1, device=self.device)
+            ret = K.lambda_return(rew_n, val_n, disc, self.lamb, cont_logit=contl_n, cont_out=i_cont,
+                                  weight_out=weight)  # (N, H)
+            ret_all = parallel.gather_returns(ret, self.world)
+            ret_offset, ret_scale = self.return_ema(ret_all)
+            adv = (ret - val_n[:, :-1]) / ret_scale
+        pl = self.actor(ifeat[:H].reshape(H * N, -1))
+        if self.act_discrete:
+            logpi, ent = ops.OneHotLogProbEntFn.apply(pl, iact[:H].reshape(H * N, -1),
+                                                       float(self.config.actor.dist.unimix_ratio))
+        else:
+            d = self.config.actor.dist
+            logpi, ent = ops.BNormalLogProbEntFn.apply(pl, iact[:H].reshape(H * N, -1), float(d.min_std),
+                                                        float(d.max_std))
+        logpi, ent = logpi.view(H, N).t(), ent.view(H, N).t()
+        w = weight[:, :H]
+        losses["policy"] = torch.mean(w * -(logpi * adv + self.act_entropy * ent))
+        vl = self.value(ifeat[:H].reshape(H * N, -1))
+        lp_tar = ops.TwoHotLogProbFn.apply(vl, self.vbins, ret.t().contiguous().reshape(-1))
+        lp_slow = ops.TwoHotLogProbFn.apply(vl, self.vbins, i_slow[:H].reshape(-1))
+        losses["value"] = torch.mean(w * (-lp_tar - lp_slow).view(H, N).t())
+        with torch.no_grad():
+            ret_normed = (ret - ret_offset) / ret_scale
+            metrics["ret"] = ret_normed.mean()
+            metrics["ret_005"] = self.return_ema.ema_vals[0].clone()
+            metrics["ret_095"] = self.return_ema.ema_vals[1].clone()
+            metrics["adv"] = adv.mean()
+            metrics["adv_std"] = adv.std()
+            metrics["con"] = i_cont.mean()
+            metrics["rew"] = i_rew.mean()
+            metrics["val"] = i_val.mean()
+            metrics["tar"] = ret.mean()
+            metrics["slowval"] = i_slow.mean()
+            metrics["weight"] = weight.mean()
+            metrics["action_entropy"] = ent.detach().mean()
+            metrics.update(_tstats(iact, "action"))
+
+        # ---- replay value (dreamer.py:638-664)
+        with torch.no_grad():
+            last = data["is_last"].float().reshape(B, T)
+            term = data["is_terminal"].float().reshape(B, T)
+            reward = data["reward"].float().reshape(B, T)
+            fd = feat.detach().reshape(N, -1)
+            value = K.twohot_mode(self.value.logits_nograd(fd), self.vbins).view(B, T)
+            slow_value = K.twohot_mode(self._slow_value.logits_nograd(fd), self.vbins).view(B, T)
+            # boot = imag ret[:, 0] (dreamer.py:645): ret is (N, H) with N = (b, t)
+            rret = K.lambda_return(reward.contiguous(), ret, disc, self.lamb, term=term.contiguous(),
+                                   last=last.contiguous(), boot_row_stride=T * H, boot_t_stride=H)  # (B, T-1)
+        vd = self.value(feat[:, :-1])
+        lp_r = ops.TwoHotLogProbFn.apply(vd, self.vbins, rret.reshape(-1))
+        lp_s = ops.TwoHotLogProbFn.apply(vd, self.vbins, slow_value[:, :-1].contiguous().reshape(-1))
+        losses["repval"] = torch.mean((1.0 - last[:, :-1]) * (-lp_r - lp_s))
+        with torch.no_grad():
+            metrics.update(_tstats(rret, "ret_replay"))
+            metrics.update(_tstats(value, "value_replay"))
+            metrics.update(_tstats(slow_value, "slow_value_replay"))
+        total = sum(v * self._loss_scales[k] for k, v in losses.items())
+        total.backward()
+        metrics.update({f"loss/{k}": v.detach() for k, v in losses.items()})
+        metrics["opt/loss"] = total.detach()
+        self._last = dict(embed=embed, post_logit=post_logit, prior_logit=prior_logit, imag_feat_tm=ifeat,
+                          imag_action_tm=iact, ret=ret, rret=rret)
+        return (post_stoch, post_deter), metrics
+
+    @torch.no_grad()
+    def _imagine_tm(self, start, H1, seed, row_offset=0):
+        """Dreamer._imagine (dreamer.py:673-692), time-major: feats (H1, N, F), actions (H1, N, A).
+        The reference's last img_step (whose output is discarded) is skipped."""
+        stoch, deter = start
+        N = deter.shape[0]
+        SK = self.rssm.flat_stoch
+        feats = torch.empty(H1, N, self.rssm.feat_size, dtype=torch.float32, device=deter.device)
+        actions = torch.empty(H1, N, self.act_dim, dtype=torch.float32, device=deter.device)
+        s = stoch.reshape(N, SK).contiguous()
+        h = deter.contiguous()
+        for t in range(H1):
+            feats[t, :, :SK] = s
+            feats[t, :, SK:] = h
+            logits = self.actor.logits_nograd(feats[t])
+            actions[t] = self._sample_action(logits, seed, t, row_offset, STREAM_ACT)
+            if t == H1 - 1:
+                break
+            h = self.rssm._deter_fwd(s, h, K.action_norm(actions[t]))
+            s, _ = self.rssm._prior_nograd(h, seed, t, row_offset, STREAM_IMG)
+        return feats, actions
+
+    @torch.no_grad()
+    def _imagine(self, start, imag_horizon, seed=0, row_offset=0):
+        """Reference-layout wrapper: (N, H1, F), (N, H1, A)."""
+        f, a = self._imagine_tm(start, imag_horizon, seed, row_offset)
+        return f.transpose(0, 1), a.transpose(0, 1)
+
+    @torch.no_grad()
+    def _lambda_return(self, last, term, reward, value, boot, disc, lamb):  # dreamer.py:694-707
+        N, T = reward.shape[:2]
+        r = K.lambda_return(reward.reshape(N, T).float().contiguous(), boot.reshape(N, T).float().contiguous(),
+                            disc, lamb, term=term.reshape(N, T).float().contiguous(),
+                            last=last.reshape(N, T).float().contiguous())
+        return r.unsqueeze(-1)
+
+    # ------------------------------------------------------------------ checkpoint layout (train.py:126-130)
+    _FROZEN = (("encoder", "_frozen_encoder"), ("rssm", "_frozen_rssm"), ("reward", "_frozen_reward"),
+               ("cont", "_frozen_cont"), ("actor", "_frozen_actor"), ("value", "_frozen_value"),
+               ("_slow_value", "_frozen_slow_value"))
+
+    def state_dict(self, *args, **kwargs):
+        sd = super().state_dict(*args, **kwargs)
+        extra = OrderedDict()
+        for src, dst in self._FROZEN:
+            for k, v in sd.items():
+                if k.startswith(src + "."):
+                    extra[dst + k[len(src):]] = v
+        sd.update(extra)
+        return sd
+
+    def load_state_dict(self, state_dict, strict=True):
+        sd = OrderedDict((k, v) for k, v in state_dict.items() if not k.startswith("_frozen_"))
+        out = super().load_state_dict(sd, strict=strict)
+        self._optimizer.arena.rebind()
+        a = self._optimizer.arena
+        pos = {id(p): i for i, p in enumerate(a.params)}
+        for p, sp in zip([p for n, p in self._named_params.items() if n.startswith("value.")],
+                         self._slow_value.parameters()):
+            j = pos[id(p)]
+            o = a.offsets[j] - self._v_lo
+            if sp.data.data_ptr() != self._slow_arena[o:o + a.sizes[j]].data_ptr():
+                self._slow_arena[o:o + a.sizes[j]].copy_(sp.data.reshape(-1))
+                sp.data = self._slow_arena[o:o + a.sizes[j]].view(sp.shape)
+        return out

@@ -1,0 +1,332 @@
+"""Typed wrappers over the C ABI (include/sdhip.h): shape checks in Python, launches on torch's current stream.
+
+Raw kernel calls only (no autograd; that lives in sdreamer/ops.py). Every wrapper requires HIP device tensors:
+there is no CPU fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native as nat
+
+EPS = 1e-4  # nn.RMSNorm(eps=1e-04) everywhere in the reference
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _chk(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise TypeError("sdreamer kernels need HIP device tensors (no CPU fallback)")
+
+
+def _c(t):
+    if not t.is_contiguous():
+        raise ValueError("expected a contiguous tensor")
+    return t
+
+
+def empty(*shape, like=None, device=None, dtype=torch.float32):
+    return torch.empty(*shape, dtype=dtype, device=device if device is not None else like.device)
+
+
+# ------------------------------------------------------------------------------------------------- GEMM
+def _layout(t, rows_dim, k_dim):
+    sr, sk = t.stride(rows_dim), t.stride(k_dim)
+    if sk == 1 and (t.shape[rows_dim] == 1 or sr >= t.shape[k_dim]):
+        return True, max(sr, 1)
+    if sr == 1:
+        return False, max(sk, 1)
+    if sk == 1:
+        return True, max(sr, 1)
+    raise ValueError(f"GEMM operand needs a unit stride, got strides {t.stride()} shape {tuple(t.shape)}")
+
+
+def _auto_split(M, N, K, batch):
+    tiles = -(-M // 64) * -(-N // 64) * batch
+    if tiles >= 256 or K < 512:
+        return 1
+    ks = min(K // 256, max(1, 512 // tiles))
+    return max(1, min(ks, 32))
+
+
+def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1):
+    """out[M,N] = alpha * a[M,K] @ b[K,N] (+ bias[N]) (+ beta*out). Strided views allowed (one unit stride each);
+    3-D operands are a strided batch over dim 0."""
+    _chk(a, b, out, bias)
+    if a.dtype != torch.float32 or b.dtype != torch.float32 or out.dtype != torch.float32:
+        raise TypeError("fp32 GEMM")
+    if a.dim() == 3:
+        Bt, M, K = a.shape
+        Nn = b.shape[2]
+        if b.shape[0] != Bt or b.shape[1] != K or tuple(out.shape) != (Bt, M, Nn):
+            raise ValueError(f"gemm shapes {tuple(a.shape)} {tuple(b.shape)} {tuple(out.shape)}")
+        ak, lda = _layout(a, 1, 2)
+        bk, ldb = _layout(b, 2, 1)
+        sA, sB, sC = a.stride(0), b.stride(0), out.stride(0)
+        if out.stride(2) != 1:
+            raise ValueError("gemm output needs unit column stride")
+        ldc = out.stride(1)
+        sBias = bias.stride(0) if (bias is not None and bias.dim() == 2) else 0
+    else:
+        Bt = 1
+        M, K = a.shape
+        Nn = b.shape[1]
+        if b.shape[0] != K or tuple(out.shape) != (M, Nn):
+            raise ValueError(f"gemm shapes {tuple(a.shape)} {tuple(b.shape)} {tuple(out.shape)}")
+        ak, lda = _layout(a, 0, 1)
+        bk, ldb = _layout(b, 1, 0)
+        sA = sB = sC = sBias = 0
+        if out.stride(1) != 1 and Nn > 1:
+            raise ValueError("gemm output needs unit column stride")
+        ldc = out.stride(0) if M > 1 else max(Nn, 1)
+    if M == 0 or Nn == 0:
+        return out
+    if ksplit is None:
+        ksplit = _auto_split(M, Nn, K, Bt)
+    d = nat.GemmDesc()
+    d.A, d.B, d.C, d.bias = p(a), p(b), p(out), (p(bias) if bias is not None else None)
+    d.lda, d.ldb, d.ldc = lda, ldb, ldc
+    d.strideA, d.strideB, d.strideC, d.strideBias = sA, sB, sC, sBias
+    d.M, d.N, d.K, d.batch = M, Nn, K, Bt
+    d.a_kcontig, d.b_kcontig = int(ak), int(bk)
+    d.ksplit, d.tile = int(ksplit), int(tile)
+    d.alpha, d.beta = float(alpha), float(beta)
+    ws = None
+    if ksplit > 1:
+        ws = torch.empty(ksplit * Bt * M * Nn, dtype=torch.float32, device=out.device)
+    nat.call("sd_gemm_f32", ctypes.byref(d), p(ws), ws.numel() if ws is not None else 0, stream())
+    return out
+
+
+def mm(a, b, bias=None, out=None, **kw):
+    M, Nn = a.shape[-2], b.shape[-1]
+    if out is None:
+        shape = (a.shape[0], M, Nn) if a.dim() == 3 else (M, Nn)
+        out = torch.empty(shape, dtype=torch.float32, device=a.device)
+    return gemm(a, b, out, bias=bias, **kw)
+
+
+def linear(x, w, b=None, out=None, beta=0.0):
+    """x (M, I) @ w(O, I)^T + b  — nn.Linear forward."""
+    return mm(x, w.t(), bias=b, out=out, beta=beta)
+
+
+# ------------------------------------------------------------------------------------------------- row norms
+def rmsnorm_fwd(x, w, act=1, y=None, rstd=None):
+    x = _c(x)
+    N = x.shape[-1]
+    M = x.numel() // N
+    y = torch.empty_like(x) if y is None else y
+    rstd = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device) if rstd is None else rstd
+    nat.call("sd_rmsnorm_fwd", p(x), p(w), p(y), p(rstd), M, N, EPS, int(act), stream())
+    return y, rstd
+
+
+def rmsnorm_bwd(x, w, rstd, dy, act=1, dx=None, dw=None, accumulate_dx=False, accumulate_dw=True):
+    N = x.shape[-1]
+    M = x.numel() // N
+    dy = _c(dy)
+    dx = torch.empty_like(x) if dx is None else dx
+    part = None
+    if dw is not None:
+        nb = nat.fns["sd_rmsnorm_bwd_blocks"](M, N)
+        part = torch.empty(nb * N, dtype=torch.float32, device=x.device)
+    nat.call("sd_rmsnorm_bwd", p(x), p(w), p(rstd), p(dy), p(dx), p(dw), p(part), M, N, int(act),
+             int(accumulate_dx), int(accumulate_dw), stream())
+    return dx
+
+
+def colsum(x2d, out, accumulate=True):
+    R, Nn = x2d.shape
+    if x2d.stride(1) != 1:
+        raise ValueError("colsum needs unit column stride")
+    nat.call("sd_colsum", p(x2d), p(out), R, Nn, x2d.stride(0) if R > 1 else Nn, int(accumulate), stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------------- latents
+def onehot_sample(logits, K, unimix, seed, stream_id, step, group_offset, out=None, index=None, entropy=None):
+    logits = _c(logits)
+    groups = logits.numel() // K
+    out = torch.empty_like(logits) if out is None else out
+    nat.call("sd_onehot_sample_fwd", p(logits), p(out), p(index), p(entropy), groups, K, float(unimix),
+             int(seed), int(stream_id), int(step), int(group_offset), stream())
+    return out
+
+
+def onehot_entropy(logits, K, unimix):
+    groups = logits.numel() // K
+    ent = torch.empty(groups, dtype=torch.float32, device=logits.device)
+    nat.call("sd_onehot_sample_fwd", p(_c(logits)), 0, 0, p(ent), groups, K, float(unimix), 0, 0, 0, 0, stream())
+    return ent
+
+
+def onehot_sample_bwd(logits, dout, K, unimix, seed, stream_id, step, group_offset, dlogits=None, accumulate=False):
+    groups = logits.numel() // K
+    dlogits = torch.empty_like(logits) if dlogits is None else dlogits
+    nat.call("sd_onehot_sample_bwd", p(_c(logits)), p(_c(dout)), p(dlogits), groups, K, float(unimix), int(seed),
+             int(stream_id), int(step), int(group_offset), int(accumulate), stream())
+    return dlogits
+
+
+def gru_fwd(gates, h, G, out=None):
+    M, D = h.shape
+    out = torch.empty_like(h) if out is None else out
+    nat.call("sd_gru_fwd", p(_c(gates)), p(_c(h)), p(out), M, G, D // G, stream())
+    return out
+
+
+def gru_bwd(gates, h, dout, G, dgates=None, dh=None, accumulate_dh=False):
+    M, D = h.shape
+    dgates = torch.empty_like(gates) if dgates is None else dgates
+    dh = torch.empty_like(h) if dh is None else dh
+    nat.call("sd_gru_bwd", p(gates), p(h), p(_c(dout)), p(dgates), p(dh), M, G, D // G, int(accumulate_dh), stream())
+    return dgates, dh
+
+
+def action_norm(a, out=None):
+    out = torch.empty_like(a) if out is None else out
+    nat.call("sd_action_norm", p(_c(a)), p(out), a.numel(), stream())
+    return out
+
+
+def mask_rows(x, mask_u8, mask_stride=1, out=None):
+    rows = mask_u8.numel() if mask_stride == 1 else x.shape[0]
+    width = x.numel() // x.shape[0]
+    out = torch.empty_like(x) if out is None else out
+    nat.call("sd_mask_rows", p(_c(x)), p(mask_u8), int(mask_stride), p(out), x.shape[0], width, stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------------- heads
+def twohot_mode(logits, bins, out=None):
+    NB = logits.shape[-1]
+    rows = logits.numel() // NB
+    out = torch.empty(logits.shape[:-1] + (1,), dtype=torch.float32, device=logits.device) if out is None else out
+    nat.call("sd_twohot_mode", p(_c(logits)), p(bins), p(out), rows, NB, stream())
+    return out
+
+
+def kl_rows(post, prior, S, K):
+    rows = post.numel() // (S * K)
+    out = torch.empty(rows, dtype=torch.float32, device=post.device)
+    nat.call("sd_kl_fwd", p(_c(post)), p(_c(prior)), p(out), rows, S, K, stream())
+    return out
+
+
+def lambda_return(reward, boot, disc, lamb, term=None, cont_logit=None, last=None, boot_row_stride=None,
+                  boot_t_stride=1, cont_out=None, weight_out=None):
+    N, T = reward.shape
+    ret = torch.empty(N, T - 1, dtype=torch.float32, device=reward.device)
+    brs = T if boot_row_stride is None else boot_row_stride
+    nat.call("sd_lambda_return", p(_c(reward)), p(term), p(cont_logit), p(last), p(boot), int(brs), int(boot_t_stride),
+             p(ret), p(cont_out), p(weight_out), N, T, float(disc), float(lamb), stream())
+    return ret
+
+
+def return_ema(x, ema, offset_scale, quantiles=None, alpha=1e-2, q0=0.05, q1=0.95):
+    x = _c(x)
+    nat.call("sd_return_ema", p(x), x.numel(), p(ema), p(offset_scale), p(quantiles), float(alpha), float(q0),
+             float(q1), stream())
+
+
+def polyak(src, dst, mix):
+    nat.call("sd_polyak", p(_c(src)), p(_c(dst)), src.numel(), float(mix), stream())
+
+
+def u8_to_f32(img, shift=0.0, out=None):
+    out = torch.empty(img.shape, dtype=torch.float32, device=img.device) if out is None else out
+    nat.call("sd_u8_to_f32", p(_c(img)), p(out), img.numel(), float(shift), stream())
+    return out
+
+
+def symlog(x):
+    y = torch.empty_like(x)
+    nat.call("sd_symlog", p(_c(x)), p(y), x.numel(), stream())
+    return y
+
+
+def fill_gumbel(n, seed, stream_id, step, offset=0, device="cuda"):
+    out = torch.empty(n, dtype=torch.float32, device=device)
+    nat.call("sd_fill_gumbel", p(out), n, int(seed), int(stream_id), int(step), int(offset), stream())
+    return out
+
+
+def fill_normal(n, seed, stream_id, step, offset=0, device="cuda"):
+    out = torch.empty(n, dtype=torch.float32, device=device)
+    nat.call("sd_fill_normal", p(out), n, int(seed), int(stream_id), int(step), int(offset), stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------------- conv
+def conv2d_fwd(x, w, b, ups=0, pad=None, out=None):
+    """x (Nb, H, W, Ci) NHWC, w (Co, kh, kw, Ci) -> (Nb, H<<ups, W<<ups, Co)"""
+    Nb, H, W, Ci = x.shape
+    Co, kh, kw, _ = w.shape
+    pad = (kh - 1) // 2 if pad is None else pad
+    out = torch.empty(Nb, H << ups, W << ups, Co, dtype=torch.float32, device=x.device) if out is None else out
+    nat.call("sd_conv2d_fwd", p(_c(x)), p(_c(w)), p(b), p(out), Nb, H, W, Ci, Co, kh, kw, pad, ups, stream())
+    return out
+
+
+def conv2d_wgrad(x, dout, kh, kw, ups=0, pad=None):
+    """returns (Co, kh*kw*Ci + 1) = [dW | db]"""
+    Nb, H, W, Ci = x.shape
+    Co = dout.shape[-1]
+    pad = (kh - 1) // 2 if pad is None else pad
+    J = kh * kw * Ci
+    pixels = dout.numel() // Co
+    ks = max(1, min(256, pixels // 4096))
+    tiles = -(-Co // 64) * -(-(J + 1) // 64)
+    ks = max(1, min(ks, max(1, 1024 // tiles)))
+    out = torch.empty(Co, J + 1, dtype=torch.float32, device=x.device)
+    ws = torch.empty(ks * Co * (J + 1), dtype=torch.float32, device=x.device) if ks > 1 else None
+    nat.call("sd_conv2d_wgrad", p(_c(x)), p(_c(dout)), p(out), p(ws), ws.numel() if ws is not None else 0, ks,
+             Nb, H, W, Ci, Co, kh, kw, pad, ups, stream())
+    return out
+
+
+def conv_flip_weight(w):
+    Co, kh, kw, Ci = w.shape
+    wf = torch.empty(Ci, kh, kw, Co, dtype=torch.float32, device=w.device)
+    nat.call("sd_conv_flip_weight", p(_c(w)), p(wf), Co, kh, kw, Ci, stream())
+    return wf
+
+
+def sumpool2(du):
+    Nb, H2, W2, C = du.shape
+    din = torch.empty(Nb, H2 // 2, W2 // 2, C, dtype=torch.float32, device=du.device)
+    nat.call("sd_sumpool2", p(_c(du)), p(din), Nb, H2 // 2, W2 // 2, C, stream())
+    return din
+
+
+def pool_rms_fwd(x, w, nchw_flat=False):
+    Nb, H, W, C = x.shape
+    pooled = torch.empty(Nb, H // 2, W // 2, C, dtype=torch.float32, device=x.device)
+    amax = torch.empty(Nb, H // 2, W // 2, C, dtype=torch.uint8, device=x.device)
+    y = torch.empty_like(pooled)
+    rstd = torch.empty(Nb, H // 2, W // 2, dtype=torch.float32, device=x.device)
+    nat.call("sd_pool_rms_fwd", p(_c(x)), p(w), p(pooled), p(amax), p(y), p(rstd), Nb, H, W, C, EPS, int(nchw_flat),
+             stream())
+    return y, pooled, amax, rstd
+
+
+def pool_rms_bwd(pooled, amax, w, rstd, dy, H, W, dw, nchw_flat=False):
+    Nb, Ho, Wo, C = pooled.shape
+    dx = torch.empty(Nb, H, W, C, dtype=torch.float32, device=pooled.device)
+    nb = nat.fns["sd_pool_rms_bwd_blocks"](Nb, H, W)
+    part = torch.empty(nb * C, dtype=torch.float32, device=pooled.device)
+    nat.call("sd_pool_rms_bwd", p(pooled), p(amax), p(w), p(rstd), p(_c(dy)), p(dx), p(dw), p(part), Nb, H, W, C,
+             int(nchw_flat), 1, stream())
+    return dx

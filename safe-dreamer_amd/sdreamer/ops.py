@@ -1,0 +1,329 @@
+"""Autograd wrappers: each differentiable piece of the update owns a HIP forward AND a HIP backward.
+
+Parameter gradients are accumulated straight into `param.grad` (normally a view into the flat gradient arena,
+see sdreamer/optim.py) by the backward kernels (GEMM beta=1 / accumulate flags) instead of being returned to
+autograd, so weight gradients never take an extra allocation + add pass. Input gradients are returned normally.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as k
+
+
+def grad_buf(param):
+    if param.grad is None:
+        param.grad = torch.zeros_like(param)
+    return param.grad
+
+
+def _flat(x):
+    return x.reshape(-1, x.shape[-1])
+
+
+# ------------------------------------------------------------------------------------------------- dense layers
+class LinearFn(torch.autograd.Function):
+    """nn.Linear (y = x W^T + b)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = _flat(x).contiguous()
+        y = k.mm(x2, w.t(), bias=b)
+        ctx.save_for_backward(x2, w, b)
+        ctx.in_shape = x.shape
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, b = ctx.saved_tensors
+        dy2 = _flat(dy).contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = k.mm(dy2, w).view(ctx.in_shape)
+        if w.requires_grad:
+            k.gemm(dy2.t(), x2, grad_buf(w), beta=1.0)
+        if b is not None and b.requires_grad:
+            k.colsum(dy2, grad_buf(b), accumulate=True)
+        return dx, None, None
+
+
+class RmsSiluFn(torch.autograd.Function):
+    """nn.RMSNorm(eps=1e-4) followed by SiLU (act=1) or nothing (act=0)."""
+
+    @staticmethod
+    def forward(ctx, x, w, act):
+        x = x.contiguous()
+        y, rstd = k.rmsnorm_fwd(x, w, act=act)
+        ctx.save_for_backward(x, w, rstd)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        dw = grad_buf(w) if w.requires_grad else None
+        dx = k.rmsnorm_bwd(x, w, rstd, dy.contiguous(), act=ctx.act, dw=dw)
+        return dx, None, None
+
+
+class BlockLinearFn(torch.autograd.Function):
+    """BlockLinear (networks.py:24-56) with the weight kept packed as (G, O/G, I/G)."""
+
+    @staticmethod
+    def forward(ctx, x, wp, b):
+        G, Og, Ig = wp.shape
+        x2 = _flat(x).contiguous()
+        M = x2.shape[0]
+        y = torch.empty(M, G * Og, dtype=torch.float32, device=x.device)
+        k.gemm(x2.view(M, G, Ig).permute(1, 0, 2), wp.transpose(1, 2), y.view(M, G, Og).permute(1, 0, 2),
+               bias=b.view(G, Og))
+        ctx.save_for_backward(x2, wp, b)
+        ctx.in_shape = x.shape
+        return y.view(*x.shape[:-1], G * Og)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wp, b = ctx.saved_tensors
+        G, Og, Ig = wp.shape
+        M = x2.shape[0]
+        dy2 = _flat(dy).contiguous()
+        dyv = dy2.view(M, G, Og).permute(1, 0, 2)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, G * Ig, dtype=torch.float32, device=dy.device)
+            k.gemm(dyv, wp, dx.view(M, G, Ig).permute(1, 0, 2))
+            dx = dx.view(ctx.in_shape)
+        if wp.requires_grad:
+            k.gemm(dyv.transpose(1, 2), x2.view(M, G, Ig).permute(1, 0, 2), grad_buf(wp), beta=1.0)
+        if b.requires_grad:
+            k.colsum(dy2, grad_buf(b), accumulate=True)
+        return dx, None, None
+
+
+def linear(x, w, b=None):
+    return LinearFn.apply(x, w, b)
+
+
+def rms_silu(x, w, act=1):
+    return RmsSiluFn.apply(x, w, act)
+
+
+def block_linear(x, wp, b):
+    return BlockLinearFn.apply(x, wp, b)
+
+
+# ------------------------------------------------------------------------------------------------- conv
+class ConvPoolNormFn(torch.autograd.Function):
+    """One ConvEncoder stage: Conv2dSamePad -> MaxPool2d(2) -> RMSNorm2D -> SiLU (networks.py:201-216), NHWC."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, nw, nchw_flat):
+        conv = k.conv2d_fwd(x.contiguous(), w, b)
+        y, pooled, amax, rstd = k.pool_rms_fwd(conv, nw, nchw_flat=nchw_flat)
+        del conv
+        ctx.save_for_backward(x, w, b, nw, pooled, amax, rstd)
+        ctx.nchw_flat = nchw_flat
+        if nchw_flat:
+            return y.view(y.shape[0], -1)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, nw, pooled, amax, rstd = ctx.saved_tensors
+        Nb, H, W, _ = x.shape
+        Co, kh, kw, Ci = w.shape
+        dconv = k.pool_rms_bwd(pooled, amax, nw, rstd, dy.contiguous(), H, W, grad_buf(nw), nchw_flat=ctx.nchw_flat)
+        dwdb = k.conv2d_wgrad(x, dconv, kh, kw)
+        grad_buf(w).add_(dwdb[:, :-1].reshape(w.shape))
+        grad_buf(b).add_(dwdb[:, -1])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = k.conv2d_fwd(dconv, k.conv_flip_weight(w), None, pad=kh - 1 - (kh - 1) // 2)
+        return dx, None, None, None, None
+
+
+class UpConvFn(torch.autograd.Function):
+    """nn.Upsample(2, nearest) -> Conv2dSamePad (ConvDecoder, networks.py:259-265), NHWC, no materialised upsample."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        y = k.conv2d_fwd(x.contiguous(), w, b, ups=1)
+        ctx.save_for_backward(x, w, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b = ctx.saved_tensors
+        Co, kh, kw, Ci = w.shape
+        dy = dy.contiguous()
+        dwdb = k.conv2d_wgrad(x, dy, kh, kw, ups=1)
+        grad_buf(w).add_(dwdb[:, :-1].reshape(w.shape))
+        grad_buf(b).add_(dwdb[:, -1])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            du = k.conv2d_fwd(dy, k.conv_flip_weight(w), None, pad=kh - 1 - (kh - 1) // 2)
+            dx = k.sumpool2(du)
+        return dx, None, None
+
+
+# ------------------------------------------------------------------------------------------------- distributions
+class KLFn(torch.autograd.Function):
+    """RSSM.kl_loss (rssm.py:222-230): returns (dyn_row, rep_row) = clip(sum_S KL, min=free) for every row."""
+
+    @staticmethod
+    def forward(ctx, post, prior, free, S, K):
+        post, prior = post.contiguous(), prior.contiguous()
+        kl = k.kl_rows(post, prior, S, K)
+        ctx.save_for_backward(post, prior, kl)
+        ctx.free, ctx.S, ctx.K = free, S, K
+        cl = torch.clamp(kl, min=free)
+        return cl, cl.clone()
+
+    @staticmethod
+    def backward(ctx, g_dyn, g_rep):
+        post, prior, kl = ctx.saved_tensors
+        rows = kl.numel()
+        d_post = torch.empty_like(post) if ctx.needs_input_grad[0] else None
+        d_prior = torch.empty_like(prior) if ctx.needs_input_grad[1] else None
+        gd = g_dyn.contiguous() if g_dyn is not None else None
+        gr = g_rep.contiguous() if g_rep is not None else None
+        k.nat.call("sd_kl_bwd", k.p(post), k.p(prior), k.p(kl), k.p(gr), k.p(gd), float(ctx.free), k.p(d_post),
+                   k.p(d_prior), rows, ctx.S, ctx.K, 0, 0, k.stream())
+        return d_post, d_prior, None, None, None
+
+
+class TwoHotLogProbFn(torch.autograd.Function):
+    """TwoHot.log_prob (distributions.py:100-129) for symexp bins; target detached."""
+
+    @staticmethod
+    def forward(ctx, logits, bins, target):
+        NB = logits.shape[-1]
+        l2 = _flat(logits).contiguous()
+        t = target.reshape(-1).contiguous()
+        out = torch.empty(l2.shape[0], dtype=torch.float32, device=logits.device)
+        k.nat.call("sd_twohot_logp_fwd", k.p(l2), k.p(bins), k.p(t), k.p(out), l2.shape[0], NB, k.stream())
+        ctx.save_for_backward(l2, bins, t)
+        ctx.shape = logits.shape
+        return out.view(logits.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, g):
+        l2, bins, t = ctx.saved_tensors
+        dl = torch.empty_like(l2)
+        k.nat.call("sd_twohot_logp_bwd", k.p(l2), k.p(bins), k.p(t), k.p(g.contiguous()), k.p(dl), l2.shape[0],
+                   l2.shape[1], 0, k.stream())
+        return dl.view(ctx.shape), None, None
+
+
+class BernoulliLogProbFn(torch.autograd.Function):
+    """Independent(Bernoulli(logits), 1).log_prob with a single logit (binary head, distributions.py:238)."""
+
+    @staticmethod
+    def forward(ctx, logit, value):
+        l = logit.reshape(-1).contiguous()
+        v = value.reshape(-1).contiguous().float()
+        out = torch.empty_like(l)
+        k.nat.call("sd_bernoulli_fwd", k.p(l), k.p(v), k.p(out), 0, l.numel(), k.stream())
+        ctx.save_for_backward(l, v)
+        ctx.shape = logit.shape
+        return out.view(logit.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, g):
+        l, v = ctx.saved_tensors
+        dl = torch.empty_like(l)
+        k.nat.call("sd_bernoulli_bwd", k.p(l), k.p(v), k.p(g.contiguous()), k.p(dl), l.numel(), k.stream())
+        return dl.view(ctx.shape), None
+
+
+class BNormalLogProbEntFn(torch.autograd.Function):
+    """bounded_normal (distributions.py:217-222): Independent(Normal(tanh(mean), std)).log_prob(a), .entropy()."""
+
+    @staticmethod
+    def forward(ctx, x, action, min_std, max_std):
+        A = action.shape[-1]
+        x2 = _flat(x).contiguous()
+        a2 = _flat(action).contiguous()
+        rows = x2.shape[0]
+        lp = torch.empty(rows, dtype=torch.float32, device=x.device)
+        ent = torch.empty_like(lp)
+        k.nat.call("sd_bnormal_logp_ent_fwd", k.p(x2), k.p(a2), k.p(lp), k.p(ent), rows, A, float(min_std),
+                   float(max_std), k.stream())
+        ctx.save_for_backward(x2, a2)
+        ctx.args = (A, min_std, max_std, x.shape)
+        return lp.view(x.shape[:-1]), ent.view(x.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, glp, gent):
+        x2, a2 = ctx.saved_tensors
+        A, mn, mx, shape = ctx.args
+        dx = torch.empty_like(x2)
+        k.nat.call("sd_bnormal_logp_ent_bwd", k.p(x2), k.p(a2), k.p(None if glp is None else glp.contiguous()),
+                   k.p(None if gent is None else gent.contiguous()), k.p(dx), x2.shape[0], A, float(mn), float(mx),
+                   k.stream())
+        return dx.view(shape), None, None, None
+
+
+class OneHotLogProbEntFn(torch.autograd.Function):
+    """discrete actor OneHotDist (distributions.py:16-36): log_prob(one-hot action), entropy."""
+
+    @staticmethod
+    def forward(ctx, logits, action, unimix):
+        K = logits.shape[-1]
+        l2 = _flat(logits).contiguous()
+        a2 = _flat(action).contiguous()
+        rows = l2.shape[0]
+        lp = torch.empty(rows, dtype=torch.float32, device=logits.device)
+        ent = torch.empty_like(lp)
+        k.nat.call("sd_onehot_logp_ent_fwd", k.p(l2), k.p(a2), k.p(lp), k.p(ent), rows, K, float(unimix), k.stream())
+        ctx.save_for_backward(l2, a2)
+        ctx.args = (K, unimix, logits.shape)
+        return lp.view(logits.shape[:-1]), ent.view(logits.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, glp, gent):
+        l2, a2 = ctx.saved_tensors
+        K, unimix, shape = ctx.args
+        dl = torch.empty_like(l2)
+        k.nat.call("sd_onehot_logp_ent_bwd", k.p(l2), k.p(a2), k.p(None if glp is None else glp.contiguous()),
+                   k.p(None if gent is None else gent.contiguous()), k.p(dl), l2.shape[0], K, float(unimix),
+                   k.stream())
+        return dl.view(shape), None, None
+
+
+class BarlowFn(torch.autograd.Function):
+    """R2-Dreamer Barlow loss (dreamer.py:525-532) on x1 (N, E) (with grad) and x2 (N, E) (detached)."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, lambd):
+        x1, x2 = x1.contiguous(), x2.contiguous()
+        Nr, E = x1.shape
+        dev = x1.device
+        m1, s1 = torch.empty(E, device=dev), torch.empty(E, device=dev)
+        m2, s2 = torch.empty(E, device=dev), torch.empty(E, device=dev)
+        k.nat.call("sd_colstats", k.p(x1), Nr, E, k.p(m1), k.p(s1), k.stream())
+        k.nat.call("sd_colstats", k.p(x2), Nr, E, k.p(m2), k.p(s2), k.stream())
+        n1 = torch.empty_like(x1)
+        n2 = torch.empty_like(x2)
+        k.nat.call("sd_standardize", k.p(x1), k.p(m1), k.p(s1), k.p(n1), Nr, E, 1e-8, k.stream())
+        k.nat.call("sd_standardize", k.p(x2), k.p(m2), k.p(s2), k.p(n2), Nr, E, 1e-8, k.stream())
+        c = k.mm(n1.t(), n2, alpha=1.0 / Nr)
+        nb = 256
+        part = torch.empty(2 * nb, device=dev)
+        loss = torch.empty(1, device=dev)
+        k.nat.call("sd_barlow_loss", k.p(c), E, float(lambd), k.p(part), nb, k.p(loss), k.stream())
+        ctx.save_for_backward(x1, m1, s1, n2, c)
+        ctx.lambd = lambd
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        x1, m1, s1, n2, c = ctx.saved_tensors
+        Nr, E = x1.shape
+        dc = torch.empty_like(c)
+        gg = g.reshape(1).contiguous()
+        k.nat.call("sd_barlow_dc", k.p(c), k.p(gg), k.p(dc), E, float(ctx.lambd), k.stream())
+        dn1 = k.mm(n2, dc.t(), alpha=1.0 / Nr)  # c = n1^T n2 / N  ->  dn1 = n2 dc^T / N
+        dx1 = torch.empty_like(x1)
+        k.nat.call("sd_standardize_bwd", k.p(x1), k.p(m1), k.p(s1), k.p(dn1), k.p(dx1), Nr, E, 1e-8, k.stream())
+        return dx1, None, None

@@ -1,0 +1,151 @@
+"""LaProp + AGC over a flat parameter arena (reference: utils/optim/laprop.py, utils/optim/agc.py).
+
+All trainable parameters of the Dreamer are re-homed into ONE contiguous fp32 arena (param.data becomes a view),
+and their gradients into a second arena (param.grad views). That gives:
+  * one fused HIP step (sd_agc_laprop_step): per-tensor AGC norms, clip, LaProp moments and the parameter update;
+  * one buffer to all-reduce under data parallelism (RCCL over xGMI) — no per-tensor collectives;
+  * one memset to zero the gradients.
+`LaProp` subclasses torch.optim.Optimizer only so checkpoint tooling that walks attributes for optimizers
+(tools.recursively_collect_optim_state_dict, tools.py:298-318) finds it; its state_dict uses the reference's
+per-parameter state keys {step, exp_avg, exp_avg_lr_1, exp_avg_lr_2, exp_avg_sq} (laprop.py:62-70).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as nat
+from . import kernels as K
+
+CHUNK = 16384  # elements per optimiser block (one 256-thread workgroup streams one chunk of one tensor)
+
+
+class FlatArena:
+    def __init__(self, params, device):
+        self.params = list(params)
+        self.sizes = [p.numel() for p in self.params]
+        self.offsets = []
+        off = 0
+        for n in self.sizes:
+            self.offsets.append(off)
+            off += (n + 63) // 64 * 64  # 256-B aligned starts: float4-friendly views
+        self.total = off
+        self.data = torch.zeros(self.total, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=device)
+        for p, o, n in zip(self.params, self.offsets, self.sizes):
+            self.data[o:o + n].copy_(p.data.reshape(-1))
+            p.data = self.data[o:o + n].view(p.shape)
+            p.grad = self.grad[o:o + n].view(p.shape)
+        # chunk tables
+        beg, end, tens, t0 = [], [], [], [0]
+        for ti, (o, n) in enumerate(zip(self.offsets, self.sizes)):
+            for c in range(0, max(n, 1), CHUNK):
+                beg.append(o + c)
+                end.append(o + min(n, c + CHUNK))
+                tens.append(ti)
+            t0.append(len(beg))
+        self.nchunks, self.ntensors = len(beg), len(self.params)
+        self.chunk_beg = torch.tensor(beg, dtype=torch.int64, device=device)
+        self.chunk_end = torch.tensor(end, dtype=torch.int64, device=device)
+        self.chunk_tensor = torch.tensor(tens, dtype=torch.int32, device=device)
+        self.tensor_chunk0 = torch.tensor(t0, dtype=torch.int32, device=device)
+
+    def rebind(self):
+        """Re-point param.data / param.grad at the arenas (after e.g. load_state_dict replaced them)."""
+        for p, o, n in zip(self.params, self.offsets, self.sizes):
+            if p.data.data_ptr() != self.data[o:o + n].data_ptr():
+                self.data[o:o + n].copy_(p.data.reshape(-1))
+                p.data = self.data[o:o + n].view(p.shape)
+            if p.grad is None or p.grad.data_ptr() != self.grad[o:o + n].data_ptr():
+                p.grad = self.grad[o:o + n].view(p.shape)
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+
+class LaProp(torch.optim.Optimizer):
+    """Drop-in for utils/optim/laprop.py's LaProp (amsgrad/centered/weight_decay unsupported, as unused there),
+    fused with clip_grad_agc_ and the LambdaLR warm-up of Dreamer (dreamer.py:209-225)."""
+
+    def __init__(self, params, lr=4e-4, betas=(0.9, 0.999), eps=1e-15, agc=0.3, pmin=1e-3, warmup=0, arena=None):
+        params = list(params)
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False, centered=False))
+        self.arena = arena if arena is not None else FlatArena(params, params[0].device)
+        dev = self.arena.data.device
+        self.exp_avg = torch.zeros_like(self.arena.data)
+        self.exp_avg_sq = torch.zeros_like(self.arena.data)
+        nb = nat.fns["sd_opt_scalars_bytes"]()
+        self.scalars = torch.zeros((nb + 7) // 8, dtype=torch.float64, device=dev)  # step, lr_ema1, lr_ema2, lr
+        self.workspace = torch.empty(3 * self.arena.nchunks, dtype=torch.float32, device=dev)
+        self.grad_norms = torch.empty(self.arena.ntensors, dtype=torch.float32, device=dev)
+        self.base_lr = float(lr)
+        self.betas = (float(betas[0]), float(betas[1]))
+        self.eps = float(eps)
+        self.agc, self.pmin = float(agc), float(pmin)
+        self.warmup = float(warmup or 0)
+        self.host_steps = 0
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        a = self.arena
+        nat.call("sd_agc_laprop_step", K.p(a.data), K.p(a.grad), K.p(self.exp_avg), K.p(self.exp_avg_sq),
+                 K.p(a.chunk_beg), K.p(a.chunk_end), K.p(a.chunk_tensor), K.p(a.tensor_chunk0), a.nchunks,
+                 a.ntensors, K.p(self.workspace), K.p(self.scalars), K.p(self.grad_norms), self.agc, self.pmin,
+                 self.base_lr, self.warmup, self.betas[0], self.betas[1], self.eps, K.stream())
+        self.host_steps += 1
+
+    def current_lr(self):
+        """lr the NEXT step will use (LambdaLR semantics; host-side bookkeeping, no device sync)."""
+        if self.warmup:
+            return self.base_lr * min(1.0, (self.host_steps + 1) / self.warmup)
+        return self.base_lr
+
+    def zero_grad(self, set_to_none=False):
+        self.arena.zero_grad()
+
+    # ------------------------------------------------------------------ checkpoint compatibility
+    def state_dict(self):
+        sc = self.scalars.detach().cpu().tolist()
+        steps = int(sc[0])
+        st = {}
+        a = self.arena
+        for i, (o, n, p) in enumerate(zip(a.offsets, a.sizes, a.params)):
+            if steps == 0:
+                continue
+            st[i] = {"step": steps, "exp_avg": self.exp_avg[o:o + n].view(p.shape).clone(),
+                     "exp_avg_lr_1": float(sc[1]), "exp_avg_lr_2": float(sc[2]),
+                     "exp_avg_sq": self.exp_avg_sq[o:o + n].view(p.shape).clone()}
+        lr = self.current_lr()
+        groups = [{"lr": lr, "betas": self.betas, "eps": self.eps, "weight_decay": 0, "amsgrad": False,
+                   "centered": False, "initial_lr": self.base_lr, "params": list(range(len(a.params)))}]
+        return {"state": st, "param_groups": groups}
+
+    def load_state_dict(self, sd):
+        a = self.arena
+        st = sd.get("state", {})
+        steps, e1, e2 = 0, 0.0, 0.0
+        for i, (o, n) in enumerate(zip(a.offsets, a.sizes)):
+            s = st.get(i, st.get(str(i)))
+            if not s:
+                continue
+            self.exp_avg[o:o + n].copy_(s["exp_avg"].reshape(-1))
+            self.exp_avg_sq[o:o + n].copy_(s["exp_avg_sq"].reshape(-1))
+            steps, e1, e2 = int(s["step"]), float(s["exp_avg_lr_1"]), float(s["exp_avg_lr_2"])
+        self.scalars.copy_(torch.tensor([steps, e1, e2, 0.0][: self.scalars.numel()], dtype=torch.float64))
+        self.host_steps = steps
+
+
+class WarmupSchedule:
+    """Stands in for LambdaLR(optimizer, min(1, (step+1)/warmup)) (dreamer.py:214-225); the warm-up itself is
+    evaluated inside the fused optimiser kernel from the device step counter."""
+
+    def __init__(self, optimizer):
+        self.optimizer = optimizer
+
+    def step(self):
+        pass
+
+    def get_lr(self):
+        return [self.optimizer.current_lr()]
+
+    def get_last_lr(self):
+        return self.get_lr()

@@ -1,0 +1,373 @@
+"""RSSM (reference: world_model/rssm.py), MI355X-native.
+
+Same module tree / parameter names as the reference (`_deter_net._dyn_in{0,1,2}`, `_dyn_hid`, `_dyn_gru`, `_obs_net`,
+`_img_net`), same public methods (`initial`, `observe`, `obs_step`, `img_step`, `prior`, `imagine_with_action`,
+`get_feat`, `get_dist`-equivalents, `kl_loss`). Compute:
+
+* `observe` is ONE autograd function (ObserveScan). Forward runs the L-step posterior scan; everything that does not
+  depend on the recurrence is hoisted out of the loop and done as one (L*B)-row GEMM: the action branch
+  (_dyn_in2 and its RMSNorm), the embed half of obs_net_0, and — in the backward — every weight gradient
+  (sum over steps of dy_t^T x_t == one GEMM over the time-major (L*B) activations). The serial part of the
+  backward only propagates data gradients (weights streamed once per step).
+* `dyn_hid` is split into its block-diagonal deter part (a G-batched GEMM) and the part shared by all blocks
+  ([x0, x1, x2] @ W_shared, rssm.py:52-58), so the (M, G*(D/G+3U)) concatenation is never materialised.
+* imagination (Dreamer._imagine) is forward-only and runs on the kernels directly (no autograd graph).
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import kernels as K
+from . import ops
+from .networks import Act, BlockLinear, Lambda, Linear, RMSNorm
+
+STREAM_OBS, STREAM_IMG, STREAM_ACT, STREAM_POLICY = 1, 2, 3, 4
+
+
+class Deter(nn.Module):
+    """rssm.py:10-75 (parameters only; the step is computed by RSSM._deter_fwd / ObserveScan)."""
+
+    def __init__(self, deter, stoch, act_dim, hidden, blocks, dynlayers, act="SiLU"):
+        super().__init__()
+        self.blocks = int(blocks)
+        self.dynlayers = int(dynlayers)
+        if self.dynlayers != 1:
+            raise NotImplementedError("dyn_layers != 1 (base.yaml:266 uses 1)")
+        self._dyn_in0 = nn.Sequential(Linear(deter, hidden), RMSNorm(hidden), Act())
+        self._dyn_in1 = nn.Sequential(Linear(stoch, hidden), RMSNorm(hidden), Act())
+        self._dyn_in2 = nn.Sequential(Linear(act_dim, hidden), RMSNorm(hidden), Act())
+        self._dyn_hid = nn.Sequential()
+        in_ch = (3 * hidden + deter // self.blocks) * self.blocks
+        self._dyn_hid.add_module("dyn_hid_0", BlockLinear(in_ch, deter, self.blocks))
+        self._dyn_hid.add_module("norm_0", RMSNorm(deter))
+        self._dyn_hid.add_module("act_0", Act())
+        self._dyn_gru = BlockLinear(deter, 3 * deter, self.blocks)
+
+
+class RSSM(nn.Module):
+    """rssm.py:78-230."""
+
+    def __init__(self, config, embed_size, act_dim):
+        super().__init__()
+        self._stoch = int(config.stoch)
+        self._deter = int(config.deter)
+        self._hidden = int(config.hidden)
+        self._discrete = int(config.discrete)
+        self._unimix_ratio = float(config.unimix_ratio)
+        self._initial = str(config.initial)
+        self._device = torch.device(config.device)
+        self._act_dim = int(act_dim)
+        self._obs_layers = int(config.obs_layers)
+        self._img_layers = int(config.img_layers)
+        self._blocks = int(config.blocks)
+        if self._obs_layers != 1:
+            raise NotImplementedError("obs_layers != 1 (base.yaml:264 uses 1)")
+        self.flat_stoch = self._stoch * self._discrete
+        self.feat_size = self.flat_stoch + self._deter
+        self.embed_size = int(embed_size)
+        self._deter_net = Deter(self._deter, self.flat_stoch, act_dim, self._hidden, self._blocks, config.dyn_layers)
+        self._obs_net = nn.Sequential()
+        self._obs_net.add_module("obs_net_0", Linear(self._deter + embed_size, self._hidden))
+        self._obs_net.add_module("obs_net_n_0", RMSNorm(self._hidden))
+        self._obs_net.add_module("obs_net_a_0", Act())
+        self._obs_net.add_module("obs_net_logit", Linear(self._hidden, self.flat_stoch))
+        self._obs_net.add_module("obs_net_lambda", Lambda())
+        self._img_net = nn.Sequential()
+        inp = self._deter
+        for i in range(self._img_layers):
+            self._img_net.add_module(f"img_net_{i}", Linear(inp, self._hidden))
+            self._img_net.add_module(f"img_net_n_{i}", RMSNorm(self._hidden))
+            self._img_net.add_module(f"img_net_a_{i}", Act())
+            inp = self._hidden
+        self._img_net.add_module("img_net_logit", Linear(inp, self.flat_stoch))
+        self._img_net.add_module("img_net_lambda", Lambda())
+
+    # ------------------------------------------------------------------ parameter views
+    def _p(self):
+        dn = self._deter_net
+        D, G = self._deter, self._blocks
+        Dg = D // G
+        wh = dn._dyn_hid.dyn_hid_0.weight  # (G, Dg, Dg + 3U)
+        Ig = wh.shape[2]
+        return dict(
+            W0=dn._dyn_in0[0].weight, b0=dn._dyn_in0[0].bias, n0=dn._dyn_in0[1].weight,
+            W1=dn._dyn_in1[0].weight, b1=dn._dyn_in1[0].bias, n1=dn._dyn_in1[1].weight,
+            W2=dn._dyn_in2[0].weight, b2=dn._dyn_in2[0].bias, n2=dn._dyn_in2[1].weight,
+            Wh=wh, bh=dn._dyn_hid.dyn_hid_0.bias, nh=dn._dyn_hid.norm_0.weight,
+            Wsh=wh.view(D, Ig)[:, Dg:], Wbd=wh[:, :, :Dg],
+            Wg=dn._dyn_gru.weight, bg=dn._dyn_gru.bias,
+            Wo=self._obs_net.obs_net_0.weight, bo=self._obs_net.obs_net_0.bias, no=self._obs_net.obs_net_n_0.weight,
+            Wl=self._obs_net.obs_net_logit.weight, bl=self._obs_net.obs_net_logit.bias,
+        )
+
+    def _img_mods(self):
+        return [(self._img_net[3 * i], self._img_net[3 * i + 1]) for i in range(self._img_layers)], self._img_net.img_net_logit
+
+    # ------------------------------------------------------------------ reference API
+    def initial(self, batch_size):  # rssm.py:133-138 (always zeros; config.initial is unused there too)
+        deter = torch.zeros(batch_size, self._deter, dtype=torch.float32, device=self._device)
+        stoch = torch.zeros(batch_size, self._stoch, self._discrete, dtype=torch.float32, device=self._device)
+        return stoch, deter
+
+    def get_feat(self, stoch, deter):  # rssm.py:211-217
+        return torch.cat([stoch.reshape(*stoch.shape[:-2], self.flat_stoch), deter], -1)
+
+    def observe(self, embed, action, initial, reset, seed=0, row_offset=0):
+        """rssm.py:140-156. embed (B,T,E), action (B,T,A), initial ((B,S,K),(B,D)), reset (B,T[,1]) bool.
+        `seed`/`row_offset` select the counter-based posterior noise (oracle/noise.py STREAM_OBS)."""
+        B, T = action.shape[:2]
+        r = reset.reshape(B, T).to(torch.uint8)
+        stoch0, deter0 = initial
+        return ObserveScan.apply(embed, action, r, stoch0.reshape(B, -1).contiguous(), deter0.contiguous(), self,
+                                 int(seed), int(row_offset))
+
+    @torch.no_grad()
+    def obs_step(self, stoch, deter, prev_action, embed, reset, seed=0, step=0, row_offset=0,
+                 stream_id=STREAM_POLICY):
+        """rssm.py:158-178 (no-grad form used by Dreamer.act)."""
+        B = prev_action.shape[0]
+        m = reset.reshape(B).to(torch.uint8).contiguous()
+        s_in = K.mask_rows(stoch.reshape(B, -1).contiguous(), m)
+        h_in = K.mask_rows(deter.contiguous(), m)
+        a_in = K.action_norm(K.mask_rows(prev_action.contiguous(), m))
+        deter = self._deter_fwd(s_in, h_in, a_in)
+        P = self._p()
+        D = self._deter
+        op = K.linear(embed.contiguous(), P["Wo"][:, D:], P["bo"])
+        K.gemm(deter, P["Wo"][:, :D].t(), op, beta=1.0)
+        o, _ = K.rmsnorm_fwd(op, P["no"])
+        logit = K.linear(o, P["Wl"], P["bl"])
+        st = K.onehot_sample(logit, self._discrete, self._unimix_ratio, seed, stream_id, step, row_offset * self._stoch)
+        S, Kd = self._stoch, self._discrete
+        return st.view(B, S, Kd), deter, logit.view(B, S, Kd)
+
+    @torch.no_grad()
+    def img_step(self, stoch, deter, prev_action, seed=0, step=0, row_offset=0, stream_id=STREAM_IMG):
+        """rssm.py:180-187."""
+        M = prev_action.shape[0]
+        a_in = K.action_norm(prev_action.contiguous())
+        deter = self._deter_fwd(stoch.reshape(M, -1).contiguous(), deter.contiguous(), a_in)
+        stoch, _ = self._prior_nograd(deter, seed, step, row_offset, stream_id)
+        return stoch, deter
+
+    def prior(self, deter):
+        """rssm.py:189-195: logits of the prior with autograd (the reference's discarded sample is skipped)."""
+        mods, last = self._img_mods()
+        x = deter
+        for lin, norm in mods:
+            x = ops.rms_silu(ops.linear(x, lin.weight, lin.bias), norm.weight)
+        x = ops.linear(x, last.weight, last.bias)
+        return x.reshape(*x.shape[:-1], self._stoch, self._discrete)
+
+    @torch.no_grad()
+    def imagine_with_action(self, stoch, deter, actions, seed=0, row_offset=0):  # rssm.py:197-209
+        T = actions.shape[1]
+        stochs, deters = [], []
+        for i in range(T):
+            stoch, deter = self.img_step(stoch, deter, actions[:, i], seed=seed, step=i, row_offset=row_offset)
+            stochs.append(stoch)
+            deters.append(deter)
+        return torch.stack(stochs, 1), torch.stack(deters, 1)
+
+    def kl_loss(self, post_logit, prior_logit, free):  # rssm.py:222-230 (returns dyn, rep)
+        S, Kd = self._stoch, self._discrete
+        shp = post_logit.shape[:-2]
+        dyn, rep = ops.KLFn.apply(post_logit.reshape(-1, S * Kd), prior_logit.reshape(-1, S * Kd), float(free), S, Kd)
+        return dyn.view(shp), rep.view(shp)
+
+    @torch.no_grad()
+    def entropy(self, logit):
+        """sum_S entropy of the unimix categorical (metrics dyn_entropy/rep_entropy, dreamer.py:575-576)."""
+        S, Kd = self._stoch, self._discrete
+        e = K.onehot_entropy(logit.detach().reshape(-1, Kd).contiguous(), Kd, self._unimix_ratio)
+        return e.view(-1, S).sum(-1)
+
+    # ------------------------------------------------------------------ fused no-grad pieces
+    @torch.no_grad()
+    def _deter_fwd(self, s_in, h_in, a_n, x2=None):
+        """Deter.forward (rssm.py:36-75) on masked/normalised inputs (M rows)."""
+        P = self._p()
+        M = h_in.shape[0]
+        D, G, U = self._deter, self._blocks, self._hidden
+        Dg = D // G
+        xcat = torch.empty(M, 3 * U, dtype=torch.float32, device=h_in.device)
+        xcat[:, :U] = K.rmsnorm_fwd(K.linear(h_in, P["W0"], P["b0"]), P["n0"])[0]
+        xcat[:, U:2 * U] = K.rmsnorm_fwd(K.linear(s_in, P["W1"], P["b1"]), P["n1"])[0]
+        if x2 is None:
+            x2 = K.rmsnorm_fwd(K.linear(a_n, P["W2"], P["b2"]), P["n2"])[0]
+        xcat[:, 2 * U:] = x2
+        hp = K.mm(xcat, P["Wsh"].t(), bias=P["bh"])
+        K.gemm(h_in.view(M, G, Dg).permute(1, 0, 2), P["Wbd"].transpose(1, 2), hp.view(M, G, Dg).permute(1, 0, 2),
+               beta=1.0)
+        h, _ = K.rmsnorm_fwd(hp, P["nh"])
+        gates = torch.empty(M, 3 * D, dtype=torch.float32, device=h_in.device)
+        K.gemm(h.view(M, G, Dg).permute(1, 0, 2), P["Wg"].transpose(1, 2), gates.view(M, G, 3 * Dg).permute(1, 0, 2),
+               bias=P["bg"].view(G, 3 * Dg))
+        return K.gru_fwd(gates, h_in, G)
+
+    @torch.no_grad()
+    def _prior_logits_nograd(self, deter):
+        mods, last = self._img_mods()
+        x = deter
+        for lin, norm in mods:
+            x = K.rmsnorm_fwd(K.linear(x, lin.weight, lin.bias), norm.weight)[0]
+        return K.linear(x, last.weight, last.bias)
+
+    @torch.no_grad()
+    def _prior_nograd(self, deter, seed, step, row_offset, stream_id=STREAM_IMG):
+        logit = self._prior_logits_nograd(deter)
+        st = K.onehot_sample(logit, self._discrete, self._unimix_ratio, seed, stream_id, step, row_offset * self._stoch)
+        return st, logit
+
+
+class ObserveScan(torch.autograd.Function):
+    """RSSM.observe (rssm.py:140-156) forward + BPTT backward on HIP kernels. Saved activations are time-major."""
+
+    @staticmethod
+    def forward(ctx, embed, action, reset, stoch0, deter0, rssm, seed, row_offset):
+        P = rssm._p()
+        B, T, A = action.shape
+        E = embed.shape[-1]
+        S, Kd, D, U, G = rssm._stoch, rssm._discrete, rssm._deter, rssm._hidden, rssm._blocks
+        SK, Dg = S * Kd, D // G
+        dev = embed.device
+        f32 = torch.float32
+        M = T * B
+        rt = reset.t().contiguous()  # (T, B) uint8
+        # ---- hoisted, recurrence-free work over all T*B rows
+        act_t = action.transpose(0, 1).reshape(M, A).contiguous()
+        a_n = K.action_norm(K.mask_rows(act_t, rt.reshape(M)))
+        x2p = K.linear(a_n, P["W2"], P["b2"])
+        x2, r2 = K.rmsnorm_fwd(x2p, P["n2"])
+        emb_t = embed.detach().transpose(0, 1).reshape(M, E).contiguous()
+        eproj = K.linear(emb_t, P["Wo"][:, D:], P["bo"])  # (M, U): embed half of obs_net_0 + bias
+        # ---- per-step buffers (time-major)
+        s_in = torch.empty(T, B, SK, dtype=f32, device=dev)
+        h_in = torch.empty(T, B, D, dtype=f32, device=dev)
+        x0p = torch.empty(T, B, U, dtype=f32, device=dev)
+        x1p = torch.empty(T, B, U, dtype=f32, device=dev)
+        r0 = torch.empty(T, B, dtype=f32, device=dev)
+        r1 = torch.empty(T, B, dtype=f32, device=dev)
+        xcat = torch.empty(T, B, 3 * U, dtype=f32, device=dev)
+        hp = torch.empty(T, B, D, dtype=f32, device=dev)
+        hh = torch.empty(T, B, D, dtype=f32, device=dev)
+        rh = torch.empty(T, B, dtype=f32, device=dev)
+        gates = torch.empty(T, B, 3 * D, dtype=f32, device=dev)
+        deter = torch.empty(T, B, D, dtype=f32, device=dev)
+        op = eproj.view(T, B, U)  # obs_net_0 pre-norm accumulates the deter half in place
+        oo = torch.empty(T, B, U, dtype=f32, device=dev)
+        ro = torch.empty(T, B, dtype=f32, device=dev)
+        logit = torch.empty(T, B, SK, dtype=f32, device=dev)
+        stoch = torch.empty(T, B, SK, dtype=f32, device=dev)
+        xcat[:, :, 2 * U:] = x2.view(T, B, U)
+        prev_s, prev_h = stoch0, deter0
+        for t in range(T):
+            m = rt[t]
+            K.mask_rows(prev_s, m, out=s_in[t])
+            K.mask_rows(prev_h, m, out=h_in[t])
+            K.linear(h_in[t], P["W0"], P["b0"], out=x0p[t])
+            xcat[t, :, :U] = K.rmsnorm_fwd(x0p[t], P["n0"], rstd=r0[t])[0]
+            K.linear(s_in[t], P["W1"], P["b1"], out=x1p[t])
+            xcat[t, :, U:2 * U] = K.rmsnorm_fwd(x1p[t], P["n1"], rstd=r1[t])[0]
+            K.gemm(xcat[t], P["Wsh"].t(), hp[t], bias=P["bh"])
+            K.gemm(h_in[t].view(B, G, Dg).permute(1, 0, 2), P["Wbd"].transpose(1, 2),
+                   hp[t].view(B, G, Dg).permute(1, 0, 2), beta=1.0)
+            K.rmsnorm_fwd(hp[t], P["nh"], y=hh[t], rstd=rh[t])
+            K.gemm(hh[t].view(B, G, Dg).permute(1, 0, 2), P["Wg"].transpose(1, 2),
+                   gates[t].view(B, G, 3 * Dg).permute(1, 0, 2), bias=P["bg"].view(G, 3 * Dg))
+            K.gru_fwd(gates[t], h_in[t], G, out=deter[t])
+            K.gemm(deter[t], P["Wo"][:, :D].t(), op[t], beta=1.0)
+            K.rmsnorm_fwd(op[t], P["no"], y=oo[t], rstd=ro[t])
+            K.linear(oo[t], P["Wl"], P["bl"], out=logit[t])
+            K.onehot_sample(logit[t], Kd, rssm._unimix_ratio, seed, STREAM_OBS, t, row_offset * S, out=stoch[t])
+            prev_s, prev_h = stoch[t], deter[t]
+        ctx.save_for_backward(rt, a_n, x2p, r2, emb_t, s_in, h_in, x0p, x1p, r0, r1, xcat, hp, hh, rh, gates, deter,
+                              op, oo, ro, logit)
+        ctx.rssm, ctx.seed, ctx.row_offset = rssm, seed, row_offset
+        ctx.dims = (B, T, A, E)
+        post_stoch = stoch.transpose(0, 1).reshape(B, T, S, Kd).contiguous()
+        post_deter = deter.transpose(0, 1).contiguous()
+        post_logit = logit.transpose(0, 1).reshape(B, T, S, Kd).contiguous()
+        return post_stoch, post_deter, post_logit
+
+    @staticmethod
+    def backward(ctx, d_stoch, d_deter, d_logit):
+        (rt, a_n, x2p, r2, emb_t, s_in, h_in, x0p, x1p, r0, r1, xcat, hp, hh, rh, gates, deter, op, oo, ro,
+         logit) = ctx.saved_tensors
+        rssm = ctx.rssm
+        P = rssm._p()
+        B, T, A, E = ctx.dims
+        S, Kd, D, U, G = rssm._stoch, rssm._discrete, rssm._deter, rssm._hidden, rssm._blocks
+        SK, Dg = S * Kd, D // G
+        M = T * B
+        dev = logit.device
+        f32 = torch.float32
+
+        def tm(x, width):
+            if x is None:
+                return torch.zeros(T, B, width, dtype=f32, device=dev)
+            return x.reshape(B, T, width).transpose(0, 1).contiguous()
+
+        ds_out = tm(d_stoch, SK)
+        dd_out = tm(d_deter, D)
+        dl_all = tm(d_logit, SK)  # becomes d logit (incl. the straight-through sample gradient) in place
+        d_op = torch.empty(T, B, U, dtype=f32, device=dev)
+        d_gates = torch.empty(T, B, 3 * D, dtype=f32, device=dev)
+        d_hp = torch.empty(T, B, D, dtype=f32, device=dev)
+        d_x0p = torch.empty(T, B, U, dtype=f32, device=dev)
+        d_x1p = torch.empty(T, B, U, dtype=f32, device=dev)
+        d_x2 = torch.empty(T, B, U, dtype=f32, device=dev)
+        carry_s = torch.zeros(B, SK, dtype=f32, device=dev)
+        carry_h = torch.zeros(B, D, dtype=f32, device=dev)
+        gb = ops.grad_buf
+        for t in reversed(range(T)):
+            ds = ds_out[t] + carry_s
+            K.onehot_sample_bwd(logit[t], ds, Kd, rssm._unimix_ratio, ctx.seed, STREAM_OBS, t, ctx.row_offset * S,
+                                dlogits=dl_all[t], accumulate=True)
+            d_o = K.mm(dl_all[t], P["Wl"])
+            K.rmsnorm_bwd(op[t], P["no"], ro[t], d_o, dx=d_op[t], dw=gb(P["no"]))
+            dh = dd_out[t] + carry_h
+            K.gemm(d_op[t], P["Wo"][:, :D], dh, beta=1.0)
+            d_hin = torch.empty(B, D, dtype=f32, device=dev)
+            K.gru_bwd(gates[t], h_in[t], dh, G, dgates=d_gates[t], dh=d_hin)
+            d_h = torch.empty(B, D, dtype=f32, device=dev)
+            K.gemm(d_gates[t].view(B, G, 3 * Dg).permute(1, 0, 2), P["Wg"], d_h.view(B, G, Dg).permute(1, 0, 2))
+            K.rmsnorm_bwd(hp[t], P["nh"], rh[t], d_h, dx=d_hp[t], dw=gb(P["nh"]))
+            d_xcat = K.mm(d_hp[t], P["Wsh"])
+            K.gemm(d_hp[t].view(B, G, Dg).permute(1, 0, 2), P["Wbd"], d_hin.view(B, G, Dg).permute(1, 0, 2), beta=1.0)
+            d_x2[t] = d_xcat[:, 2 * U:]
+            K.rmsnorm_bwd(x0p[t], P["n0"], r0[t], d_xcat[:, :U].contiguous(), dx=d_x0p[t], dw=gb(P["n0"]))
+            K.gemm(d_x0p[t], P["W0"], d_hin, beta=1.0)
+            K.rmsnorm_bwd(x1p[t], P["n1"], r1[t], d_xcat[:, U:2 * U].contiguous(), dx=d_x1p[t], dw=gb(P["n1"]))
+            d_sin = K.mm(d_x1p[t], P["W1"])
+            m = rt[t]
+            carry_h = K.mask_rows(d_hin, m)
+            carry_s = K.mask_rows(d_sin, m)
+        # ---- deferred weight gradients: one GEMM over all T*B rows each
+        f = lambda x: x.reshape(M, -1)  # noqa: E731
+        K.gemm(f(dl_all).t(), f(oo), gb(P["Wl"]), beta=1.0)
+        K.colsum(f(dl_all), gb(P["bl"]))
+        gWo = gb(P["Wo"])
+        K.gemm(f(d_op).t(), f(deter), gWo[:, :D], beta=1.0)
+        K.gemm(f(d_op).t(), emb_t, gWo[:, D:], beta=1.0)
+        K.colsum(f(d_op), gb(P["bo"]))
+        d_emb = K.mm(f(d_op), P["Wo"][:, D:])  # (M, E) time-major
+        K.gemm(f(d_gates).view(M, G, 3 * Dg).permute(1, 2, 0), f(hh).view(M, G, Dg).permute(1, 0, 2), gb(P["Wg"]),
+               beta=1.0)
+        K.colsum(f(d_gates), gb(P["bg"]))
+        gWh = gb(P["Wh"])
+        Ig = gWh.shape[2]
+        K.gemm(f(d_hp).t(), f(xcat), gWh.view(D, Ig)[:, Dg:], beta=1.0)
+        K.gemm(f(d_hp).view(M, G, Dg).permute(1, 2, 0), f(h_in).view(M, G, Dg).permute(1, 0, 2), gWh[:, :, :Dg],
+               beta=1.0)
+        K.colsum(f(d_hp), gb(P["bh"]))
+        K.gemm(f(d_x0p).t(), f(h_in), gb(P["W0"]), beta=1.0)
+        K.colsum(f(d_x0p), gb(P["b0"]))
+        K.gemm(f(d_x1p).t(), f(s_in), gb(P["W1"]), beta=1.0)
+        K.colsum(f(d_x1p), gb(P["b1"]))
+        d_x2p = K.rmsnorm_bwd(x2p, P["n2"], r2, f(d_x2), dw=gb(P["n2"]))
+        K.gemm(d_x2p.t(), a_n, gb(P["W2"]), beta=1.0)
+        K.colsum(d_x2p, gb(P["b2"]))
+        d_embed = d_emb.view(T, B, E).transpose(0, 1).contiguous()
+        return d_embed, None, None, None, None, None, None, None
