@@ -99,7 +99,18 @@ def check(rc, name=""):
         raise NativeError(f"{name} failed with status {rc}")
 
 
+PROBES = []  # active LaunchProbe objects (sdreamer.kernels); empty in normal runs
+
+
 def call(name, *args):
+    if PROBES:
+        hit = [pr for pr in PROBES if pr.match(name, args)]
+        for pr in hit:
+            pr.begin()
+        check(fns[name](*args), name)
+        for pr in hit:
+            pr.end(args)
+        return
     check(fns[name](*args), name)
 
 

@@ -330,3 +330,45 @@ def pool_rms_bwd(pooled, amax, w, rstd, dy, H, W, dw, nchw_flat=False):
     nat.call("sd_pool_rms_bwd", p(pooled), p(amax), p(w), p(rstd), p(_c(dy)), p(dx), p(dw), p(part), Nb, H, W, C,
              int(nchw_flat), 1, stream())
     return dx
+
+
+# ------------------------------------------------------------------------------------------------- launch probe
+class LaunchProbe:
+    """Times every launch of one C-ABI entry point (filtered by its arguments) with HIP events recorded on the
+    stream the kernel is launched on (torch's current stream). Used by bench.py for the roofline fraction."""
+
+    def __init__(self, name, pred, work_fn, bound="mfma", unit="TFLOP/s", peak=157.3, label=""):
+        self.name, self.pred, self.work_fn = name, pred, work_fn
+        self.bound, self.unit, self.peak, self.label = bound, unit, peak, label
+        self.records = []
+        self._start = None
+        nat.PROBES.append(self)
+
+    def match(self, name, args):
+        return name == self.name and self.pred(args)
+
+    def begin(self):
+        self._start = torch.cuda.Event(enable_timing=True)
+        self._start.record()
+
+    def end(self, args):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.records.append((self._start, e, self.work_fn(args)))
+
+    def stop(self):
+        if self in nat.PROBES:
+            nat.PROBES.remove(self)
+        torch.cuda.synchronize()
+
+    def report(self):
+        if not self.records:
+            return None
+        ms = [s.elapsed_time(e) for s, e, _ in self.records]
+        work = [w for _, _, w in self.records]
+        avg_ms = sum(ms) / len(ms)
+        per_launch = sum(work) / len(work)
+        achieved = per_launch / (avg_ms * 1e-3) / (1e12 if self.unit == "TFLOP/s" else 1e9)
+        return {"bound": self.bound, "achieved": achieved, "peak": self.peak, "unit": self.unit,
+                "frac": achieved / self.peak, "traffic": None, "kernel": self.label, "launches": len(ms),
+                "avg_us": avg_ms * 1e3, "work_per_launch": per_launch}
