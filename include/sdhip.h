@@ -62,6 +62,10 @@ int sd_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const floa
                    float* dw_partial, int M, int N, int act, int accumulate_dx, int accumulate_dw, sd_stream stream);
 /* out[n] (+)= sum_r in[r*ld + n] (fixed-order column sums; bias gradients) */
 int sd_colsum(const float* in, float* out, int R, int N, long ld, int accumulate, sd_stream stream);
+/* two-pass variant for long columns: workspace >= sd_colsum_chunks(R) * N floats */
+int sd_colsum_chunks(int R);
+int sd_colsum_ws(const float* in, float* out, int R, int N, long ld, int accumulate, float* workspace,
+                 sd_stream stream);
 
 /* ---------------------------------------------------------------- categorical latents
  * Straight-through one-hot sample of unimix categoricals (OneHotDist.__init__/rsample, distributions.py:16-33;

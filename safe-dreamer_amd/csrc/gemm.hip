@@ -43,6 +43,98 @@ void launch_layout(const GemmArgs& g, int tile, bool va, bool vb, hipStream_t st
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// ---------------------------------------------------------------- skinny GEMM (M <= 32), e.g. the per-step
+// contractions of the RSSM observe scan (B = 16 rows). Weight-streaming bound: no LDS staging, each lane loads
+// its A row and B column as float4 straight to registers, 4 independent 8-deep k chunks in flight per lane,
+// the 4 waves of a workgroup take interleaved k chunks and are summed through LDS at the end; K is further split
+// across workgroups (slabs + the deterministic reduce) so a 16 x 256 x 2048 GEMV still spans ~128 CUs.
+template <bool BKC, bool VA, bool VB>
+__global__ __launch_bounds__(256) void gemm_skinny(GemmArgs g) {
+  constexpr int U = 4;
+  __shared__ float red[4][16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.x * 32;
+  const int split = blockIdx.y, b = blockIdx.z;
+  const int kbeg = split * g.kchunk, kend = min(g.K, kbeg + g.kchunk);
+  const float* A = g.A + (long)b * g.sA;
+  const float* Bp = g.B + (long)b * g.sB;
+  const int m = l32, n = n0 + l32;
+  const bool mv = m < g.M, nv = n < g.N;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int k = kbeg + 8 * wave; k < kend; k += 32 * U) {
+    f32x4 a[U], bb[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      const int kk = k + 32 * i + 4 * h;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f}, y = {0.f, 0.f, 0.f, 0.f};
+      if (kk < kend) {
+        if (mv) {
+          const float* q = A + (long)m * g.lda + kk;
+          if (VA && kk + 3 < kend) x = *reinterpret_cast<const f32x4*>(q);
+          else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) if (kk + j < kend) x[j] = q[j];
+          }
+        }
+        if (nv) {
+          if (BKC) {
+            const float* q = Bp + (long)n * g.ldb + kk;
+            if (VB && kk + 3 < kend) y = *reinterpret_cast<const f32x4*>(q);
+            else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) if (kk + j < kend) y[j] = q[j];
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) if (kk + j < kend) y[j] = Bp[(long)(kk + j) * g.ldb + n];
+          }
+        }
+      }
+      a[i] = x;
+      bb[i] = y;
+    }
+#pragma unroll
+    for (int i = 0; i < U; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][j], bb[i][j], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[r];
+  __syncthreads();
+  // wave w finalises registers r = 4w .. 4w+3
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * wave + q;
+    const float v = (red[0][r][lane] + red[1][r][lane]) + (red[2][r][lane] + red[3][r][lane]);
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (row < g.M && nv) {
+      if (g.ksplit > 1) {
+        g.ws[((long)split * g.batch + b) * (long)g.M * g.N + (long)row * g.N + n] = g.alpha * v;
+      } else {
+        float o = g.alpha * v + (g.bias ? g.bias[(long)b * g.sBias + n] : 0.f);
+        float* c = g.C + (long)b * g.sC + (long)row * g.ldc + n;
+        if (g.beta != 0.f) o += g.beta * *c;
+        *c = o;
+      }
+    }
+  }
+}
+
+void launch_skinny(const GemmArgs& g, bool bk, bool va, bool vb, hipStream_t st) {
+  dim3 grid(sd_cdiv(g.N, 32), g.ksplit, g.batch);
+#define SK_L(B_, A_, V_) gemm_skinny<B_, A_, V_><<<grid, 256, 0, st>>>(g)
+  if (bk) {
+    if (va && vb) SK_L(true, true, true); else if (va) SK_L(true, true, false);
+    else if (vb) SK_L(true, false, true); else SK_L(true, false, false);
+  } else {
+    if (va) SK_L(false, true, false); else SK_L(false, false, false);
+  }
+#undef SK_L
+}
+
 }  // namespace
 
 extern "C" int sd_gemm_f32(const sd_gemm_desc* d, float* workspace, long workspace_floats, sd_stream stream_) {
@@ -59,13 +151,26 @@ extern "C" int sd_gemm_f32(const sd_gemm_desc* d, float* workspace, long workspa
   if (d->K <= 0) ks = 1;
   if (ks > 1 && (!workspace || workspace_floats < (long)ks * d->batch * d->M * d->N)) return SD_EARG;
   g.ksplit = ks;
+  const bool skinny = d->M <= 32 && d->a_kcontig && d->tile < 0;
+  const int kgran = skinny ? 32 : BK;
   long kc = ((long)(d->K > 0 ? d->K : 1) + ks - 1) / ks;
-  kc = (kc + BK - 1) / BK * BK;
+  kc = (kc + kgran - 1) / kgran * kgran;
   g.kchunk = (int)kc;
   const bool ak = d->a_kcontig != 0, bk = d->b_kcontig != 0;
   // float4 staging needs 16-B aligned bases, ld % 4 == 0 and batch strides % 4 == 0
   const bool va = aligned16(d->A) && d->lda % 4 == 0 && (d->batch == 1 || d->strideA % 4 == 0);
   const bool vb = aligned16(d->B) && d->ldb % 4 == 0 && (d->batch == 1 || d->strideB % 4 == 0);
+  if (skinny) {
+    launch_skinny(g, bk, va, vb, stream);
+    SD_LAUNCH_CHECK();
+    if (ks > 1) {
+      long total = (long)d->batch * d->M * d->N;
+      int blocks = (int)((total + 255) / 256);
+      gemm_reduce_kernel<<<blocks, 256, 0, stream>>>(g);
+      SD_LAUNCH_CHECK();
+    }
+    return SD_OK;
+  }
   int tile = d->tile;
   if (tile < 0) {
     long tiles128 = (long)sd_cdiv(d->M, 128) * sd_cdiv(d->N, 128) * d->batch * ks;

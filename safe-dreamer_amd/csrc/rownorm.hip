@@ -9,6 +9,9 @@
 #include "common.h"
 #include "sdhip.h"
 
+extern "C" int sd_colsum_ws(const float* in, float* out, int R, int N, long ld, int accumulate, float* workspace,
+                            sd_stream stream);
+
 namespace {
 
 template <int TEAM>
@@ -121,19 +124,62 @@ __global__ __launch_bounds__(256) void rms_bwd(const float* __restrict__ x, cons
   }
 }
 
-// out[n] (+)= sum_r in[r * ld + n]   (column sums in a fixed order)
+// Column sums in a fixed order (deterministic). Pass 1: block (64 columns x RCH rows), 4 row-phases x 8 independent
+// accumulators per thread (memory-level parallelism); writes part[chunk][n]. Pass 2 sums the chunks.
+constexpr int COLSUM_RCH = 512;
+
+__global__ void colsum_pass1(const float* __restrict__ in, float* __restrict__ part, int R, int N, long ld) {
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int ph = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * COLSUM_RCH;
+  const int r1 = min(R, r0 + COLSUM_RCH);
+  __shared__ float red[4][64];
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    int r = r0 + ph;
+    for (; r + 28 < r1; r += 32) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += in[(long)(r + 4 * j) * ld + n];
+    }
+    for (; r < r1; r += 4) a[0] += in[(long)r * ld + n];
+  }
+  red[ph][threadIdx.x & 63] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (ph == 0 && n < N) {
+    const int l = threadIdx.x;
+    part[(long)blockIdx.y * N + n] = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+  }
+}
+
+__global__ void colsum_pass2(const float* __restrict__ part, float* __restrict__ out, int chunks, int N,
+                             int accumulate) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int c = 0; c < chunks; ++c) s += part[(long)c * N + n];
+  out[n] = accumulate ? out[n] + s : s;
+}
+
+// single-chunk fast path: sum all rows straight into out
 __global__ void colsum_kernel(const float* __restrict__ in, float* __restrict__ out, int R, int N, long ld,
                               int accumulate) {
   const int n = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int part = threadIdx.x >> 6;  // 4 partial sums per column
+  const int ph = threadIdx.x >> 6;
   __shared__ float red[4][64];
-  float s = 0.f;
-  if (n < N)
-    for (int r = part; r < R; r += 4) s += in[(long)r * ld + n];
-  red[part][threadIdx.x & 63] = s;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    int r = ph;
+    for (; r + 28 < R; r += 32) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += in[(long)(r + 4 * j) * ld + n];
+    }
+    for (; r < R; r += 4) a[0] += in[(long)r * ld + n];
+  }
+  red[ph][threadIdx.x & 63] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __syncthreads();
-  if (part == 0 && n < N) {
-    float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+  if (ph == 0 && n < N) {
+    const int l = threadIdx.x;
+    const float v = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
     out[n] = accumulate ? out[n] + v : v;
   }
 }
@@ -152,6 +198,12 @@ int grid_for(int M) {
   long teams = (M + 0L);
   long blocks = (teams + 256 / TEAM - 1) / (256 / TEAM);
   return (int)(blocks < 8192 ? blocks : 8192);
+}
+// backward: fewer, longer-lived blocks so the weight-gradient partials stay few
+template <int TEAM>
+int grid_bwd(int M) {
+  const int g = grid_for<TEAM>(M);
+  return g < 512 ? g : 512;
 }
 
 #define SD_RMS_DISPATCH(KERNEL, TEAMV, ...)                                             \
@@ -187,7 +239,7 @@ extern "C" int sd_rmsnorm_fwd(const float* x, const float* w, float* y, float* r
 
 extern "C" int sd_rmsnorm_bwd_blocks(int M, int N) {
   const int team = team_for(N);
-  return team == 16 ? grid_for<16>(M) : team == 64 ? grid_for<64>(M) : grid_for<256>(M);
+  return team == 16 ? grid_bwd<16>(M) : team == 64 ? grid_bwd<64>(M) : grid_bwd<256>(M);
 }
 
 extern "C" int sd_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* dy, float* dx,
@@ -199,21 +251,34 @@ extern "C" int sd_rmsnorm_bwd(const float* x, const float* w, const float* rstd,
   const int team = team_for(N);
   float* part = dw ? dw_partial : nullptr;
   int grid;
-  if (team == 16) { grid = grid_for<16>(M); SD_RMS_DISPATCH(rms_bwd, 16, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
-  else if (team == 64) { grid = grid_for<64>(M); SD_RMS_DISPATCH(rms_bwd, 64, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
-  else { grid = grid_for<256>(M); SD_RMS_DISPATCH(rms_bwd, 256, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
+  if (team == 16) { grid = grid_bwd<16>(M); SD_RMS_DISPATCH(rms_bwd, 16, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
+  else if (team == 64) { grid = grid_bwd<64>(M); SD_RMS_DISPATCH(rms_bwd, 64, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
+  else { grid = grid_bwd<256>(M); SD_RMS_DISPATCH(rms_bwd, 256, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
   SD_LAUNCH_CHECK();
-  if (dw) {
-    colsum_kernel<<<(N + 63) / 64, 256, 0, stream>>>(dw_partial, dw, grid, N, N, accumulate_dw);
+  if (dw) return sd_colsum_ws(dw_partial, dw, grid, N, N, accumulate_dw, nullptr, stream_);
+  return SD_OK;
+}
+
+extern "C" int sd_colsum_chunks(int R) { return (R + COLSUM_RCH - 1) / COLSUM_RCH; }
+
+// workspace (>= sd_colsum_chunks(R) * N floats) is only needed when R > COLSUM_RCH
+extern "C" int sd_colsum_ws(const float* in, float* out, int R, int N, long ld, int accumulate, float* workspace,
+                            sd_stream stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  if (N <= 0) return SD_OK;
+  const int chunks = (R + COLSUM_RCH - 1) / COLSUM_RCH;
+  if (chunks <= 1 || !workspace) {
+    colsum_kernel<<<(N + 63) / 64, 256, 0, stream>>>(in, out, R, N, ld, accumulate);
     SD_LAUNCH_CHECK();
+    return SD_OK;
   }
+  colsum_pass1<<<dim3((N + 63) / 64, chunks), 256, 0, stream>>>(in, workspace, R, N, ld);
+  SD_LAUNCH_CHECK();
+  colsum_pass2<<<(N + 255) / 256, 256, 0, stream>>>(workspace, out, chunks, N, accumulate);
+  SD_LAUNCH_CHECK();
   return SD_OK;
 }
 
 extern "C" int sd_colsum(const float* in, float* out, int R, int N, long ld, int accumulate, sd_stream stream_) {
-  hipStream_t stream = (hipStream_t)stream_;
-  if (N <= 0) return SD_OK;
-  colsum_kernel<<<(N + 63) / 64, 256, 0, stream>>>(in, out, R, N, ld, accumulate);
-  SD_LAUNCH_CHECK();
-  return SD_OK;
+  return sd_colsum_ws(in, out, R, N, ld, accumulate, nullptr, stream_);
 }

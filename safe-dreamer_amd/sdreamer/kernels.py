@@ -52,6 +52,13 @@ def _layout(t, rows_dim, k_dim):
     raise ValueError(f"GEMM operand needs a unit stride, got strides {t.stride()} shape {tuple(t.shape)}")
 
 
+def _skinny_split(M, N, K, batch):
+    """K split for the M <= 32 kernel: ~256 workgroups, >= 128-deep K chunks."""
+    tiles = -(-N // 32) * batch
+    ks = min(max(K // 128, 1), max(1, -(-256 // tiles)))
+    return max(1, min(ks, 64))
+
+
 def _auto_split(M, N, K, batch):
     tiles = -(-M // 64) * -(-N // 64) * batch
     if tiles >= 256 or K < 512:
@@ -93,7 +100,7 @@ def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1):
     if M == 0 or Nn == 0:
         return out
     if ksplit is None:
-        ksplit = _auto_split(M, Nn, K, Bt)
+        ksplit = _skinny_split(M, Nn, K, Bt) if (M <= 32 and ak and tile < 0) else _auto_split(M, Nn, K, Bt)
     d = nat.GemmDesc()
     d.A, d.B, d.C, d.bias = p(a), p(b), p(out), (p(bias) if bias is not None else None)
     d.lda, d.ldb, d.ldc = lda, ldb, ldc
@@ -151,7 +158,10 @@ def colsum(x2d, out, accumulate=True):
     R, Nn = x2d.shape
     if x2d.stride(1) != 1:
         raise ValueError("colsum needs unit column stride")
-    nat.call("sd_colsum", p(x2d), p(out), R, Nn, x2d.stride(0) if R > 1 else Nn, int(accumulate), stream())
+    chunks = nat.fns["sd_colsum_chunks"](R)
+    ws = torch.empty(chunks * Nn, dtype=torch.float32, device=x2d.device) if chunks > 1 else None
+    nat.call("sd_colsum_ws", p(x2d), p(out), R, Nn, x2d.stride(0) if R > 1 else Nn, int(accumulate), p(ws),
+             stream())
     return out
 
 

@@ -34,6 +34,32 @@ def test_gemm_layouts(M, N, K, ak, bk):
     assert err <= 2e-6 * scale, err
 
 
+@pytest.mark.parametrize("M,N,K", [(16, 256, 2048), (16, 2048, 768), (1, 255, 256), (32, 512, 256), (16, 6, 2560),
+                                   (3, 100, 77)])
+@pytest.mark.parametrize("bk", [True, False])
+def test_gemm_skinny(M, N, K, bk):
+    from sdreamer import kernels as k
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g).to("cuda")
+    w = torch.randn(N, K, generator=g).to("cuda")
+    b = w.t() if bk else w.t().contiguous()
+    bias = torch.randn(N, generator=g).to("cuda")
+    c0 = torch.randn(M, N, generator=g).to("cuda")
+    out = c0.clone()
+    k.gemm(a, b, out, bias=bias, beta=1.0)
+    ref = a.double() @ w.double().t() + bias.double() + c0.double()
+    assert (out.double() - ref).abs().max().item() < 2e-6 * (a.abs().double() @ w.abs().double().t()).max().item() + 1e-5
+
+
+def test_colsum_long():
+    from sdreamer import kernels as k
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(20000, 255, generator=g).to("cuda")
+    out = torch.ones(255, device="cuda")
+    k.colsum(x, out, accumulate=True)
+    assert (out.double().cpu() - (x.double().sum(0).cpu() + 1)).abs().max().item() < 1e-3
+
+
 @pytest.mark.parametrize("ks", [1, 3, 8])
 def test_gemm_splitk_beta_batched(ks):
     from sdreamer import kernels as k
