@@ -56,6 +56,9 @@ int sd_gemm_f32(const sd_gemm_desc* d, float* workspace, long workspace_floats, 
  * and RMSNorm2D on channels-last conv activations (networks.py:88-96). N <= 4096. */
 int sd_rmsnorm_fwd(const float* x, const float* w, float* y, float* rstd, int M, int N, float eps, int act,
                    sd_stream stream);
+/* same with an output row stride ldy (writes straight into a column slice of a wider activation) */
+int sd_rmsnorm_fwd_ld(const float* x, const float* w, float* y, long ldy, float* rstd, int M, int N, float eps,
+                      int act, sd_stream stream);
 /* number of dw partial rows sd_rmsnorm_bwd writes (size dw_partial >= blocks * N) */
 int sd_rmsnorm_bwd_blocks(int M, int N);
 int sd_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* dy, float* dx, float* dw,
@@ -70,13 +73,16 @@ int sd_colsum_ws(const float* in, float* out, int R, int N, long ld, int accumul
 /* ---------------------------------------------------------------- categorical latents
  * Straight-through one-hot sample of unimix categoricals (OneHotDist.__init__/rsample, distributions.py:16-33;
  * RSSM.get_dist(...).rsample(), rssm.py:177,194,219-220). groups = rows*S categoricals of K logits each.
- * Gumbel noise = Philox(seed, stream_id, step, (group + group_offset)*K + k) (see oracle/noise.py).
+ * Gumbel noise = Philox(seed, stream_id, step, (group + group_offset)*K + k) (see oracle/noise.py); when seed_ptr
+ * is non-NULL the effective seed is seed + *seed_ptr (device-resident: a captured HIP graph replays fresh noise).
  * out = onehot(argmax) - y_soft + y_soft; index (groups) optional; entropy (groups) optional (metrics). */
 int sd_onehot_sample_fwd(const float* logits, float* out, int* index, float* entropy, long groups, int K,
-                         float unimix, uint64_t seed, int stream_id, int step, long group_offset, sd_stream stream);
+                         float unimix, uint64_t seed, int stream_id, int step, long group_offset,
+                         const uint64_t* seed_ptr, sd_stream stream);
 /* straight-through gradient: d logits (+)= d/dlogits <dout, y_soft> (recomputes y_soft from logits+noise) */
 int sd_onehot_sample_bwd(const float* logits, const float* dout, float* dlogits, long groups, int K, float unimix,
-                         uint64_t seed, int stream_id, int step, long group_offset, int accumulate, sd_stream stream);
+                         uint64_t seed, int stream_id, int step, long group_offset, int accumulate,
+                         const uint64_t* seed_ptr, sd_stream stream);
 /* discrete actor: log_prob(action one-hot) and entropy of the unimix categorical (OneHotDist, distributions.py:16-36) */
 int sd_onehot_logp_ent_fwd(const float* logits, const float* action, float* logp, float* ent, long rows, int K,
                            float unimix, sd_stream stream);
@@ -98,7 +104,7 @@ int sd_twohot_logp_bwd(const float* logits, const float* bins, const float* targ
                        float* dlogits, long rows, int NB, int accumulate, sd_stream stream);
 /* bounded normal actor (bounded_normal, distributions.py:217-222): x (rows, 2A) = [mean | std-logit] */
 int sd_bnormal_sample(const float* x, float* action, long rows, int A, float min_std, float max_std, uint64_t seed,
-                      int stream_id, int step, long row_offset, sd_stream stream);
+                      int stream_id, int step, long row_offset, const uint64_t* seed_ptr, sd_stream stream);
 int sd_bnormal_logp_ent_fwd(const float* x, const float* action, float* logp, float* ent, long rows, int A,
                             float min_std, float max_std, sd_stream stream);
 int sd_bnormal_logp_ent_bwd(const float* x, const float* action, const float* glogp, const float* gent, float* dx,

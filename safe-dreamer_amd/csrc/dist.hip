@@ -66,7 +66,8 @@ SD_DEV void st_soft(float nl, float g, bool act, float& ys, int& idx, int lane_i
 template <int T>
 __global__ void onehot_sample_fwd(const float* __restrict__ logits, float* __restrict__ out, int* __restrict__ index,
                                   float* __restrict__ entropy, long groups, int K, float unimix, uint64_t seed,
-                                  uint32_t stream, uint32_t step, long group_offset) {
+                                  uint32_t stream, uint32_t step, long group_offset, const uint64_t* seed_ptr) {
+  if (seed_ptr) seed += *seed_ptr;
   const int lt = threadIdx.x % T;
   const long g = ((long)blockIdx.x * blockDim.x + threadIdx.x) / T;
   if (g >= groups) return;  // whole teams exit together (groups are team-aligned)
@@ -93,7 +94,9 @@ __global__ void onehot_sample_fwd(const float* __restrict__ logits, float* __res
 template <int T>
 __global__ void onehot_sample_bwd(const float* __restrict__ logits, const float* __restrict__ dout,
                                   float* __restrict__ dlogits, long groups, int K, float unimix, uint64_t seed,
-                                  uint32_t stream, uint32_t step, long group_offset, int accumulate) {
+                                  uint32_t stream, uint32_t step, long group_offset, int accumulate,
+                                  const uint64_t* seed_ptr) {
+  if (seed_ptr) seed += *seed_ptr;
   const int lt = threadIdx.x % T;
   const long g = ((long)blockIdx.x * blockDim.x + threadIdx.x) / T;
   if (g >= groups) return;
@@ -340,7 +343,9 @@ __global__ void twohot_logp_bwd(const float* __restrict__ logits, const float* _
 
 // ---------------------------------------------------------------- bounded normal actor
 __global__ void bnormal_sample(const float* __restrict__ x, float* __restrict__ action, long rows, int A, float min_std,
-                               float max_std, uint64_t seed, uint32_t stream, uint32_t step, long row_offset) {
+                               float max_std, uint64_t seed, uint32_t stream, uint32_t step, long row_offset,
+                               const uint64_t* seed_ptr) {
+  if (seed_ptr) seed += *seed_ptr;
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= rows * A) return;
   const long r = t / A;
@@ -465,27 +470,27 @@ int blocks_for(long n, int per) { long b = (n + per - 1) / per; return (int)b; }
 
 extern "C" int sd_onehot_sample_fwd(const float* logits, float* out, int* index, float* entropy, long groups, int K,
                                     float unimix, uint64_t seed, int stream_id, int step, long group_offset,
-                                    sd_stream s) {
+                                    const uint64_t* seed_ptr, sd_stream s) {
   if (groups <= 0) return SD_OK;
   if (K < 1 || K > 64) return SD_ESHAPE;
   const int T = team_pow2(K);
   const int grid = blocks_for(groups * T, 256);
   SD_TEAM_SWITCH(T, onehot_sample_fwd<TT><<<grid, 256, 0, (hipStream_t)s>>>(logits, out, index, entropy, groups, K,
-                                                                          unimix, seed, stream_id, step, group_offset))
+                                                                          unimix, seed, stream_id, step, group_offset, seed_ptr))
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
 
 extern "C" int sd_onehot_sample_bwd(const float* logits, const float* dout, float* dlogits, long groups, int K,
                                     float unimix, uint64_t seed, int stream_id, int step, long group_offset,
-                                    int accumulate, sd_stream s) {
+                                    int accumulate, const uint64_t* seed_ptr, sd_stream s) {
   if (groups <= 0) return SD_OK;
   if (K < 1 || K > 64) return SD_ESHAPE;
   const int T = team_pow2(K);
   const int grid = blocks_for(groups * T, 256);
   SD_TEAM_SWITCH(T, onehot_sample_bwd<TT><<<grid, 256, 0, (hipStream_t)s>>>(logits, dout, dlogits, groups, K, unimix,
                                                                           seed, stream_id, step, group_offset,
-                                                                          accumulate))
+                                                                          accumulate, seed_ptr))
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
@@ -565,10 +570,11 @@ extern "C" int sd_twohot_logp_bwd(const float* logits, const float* bins, const 
 }
 
 extern "C" int sd_bnormal_sample(const float* x, float* action, long rows, int A, float min_std, float max_std,
-                                 uint64_t seed, int stream_id, int step, long row_offset, sd_stream s) {
+                                 uint64_t seed, int stream_id, int step, long row_offset, const uint64_t* seed_ptr,
+                                 sd_stream s) {
   if (rows <= 0) return SD_OK;
   bnormal_sample<<<blocks_for(rows * A, 256), 256, 0, (hipStream_t)s>>>(x, action, rows, A, min_std, max_std, seed,
-                                                                        stream_id, step, row_offset);
+                                                                        stream_id, step, row_offset, seed_ptr);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

@@ -123,6 +123,97 @@ __global__ __launch_bounds__(256) void gemm_skinny(GemmArgs g) {
   }
 }
 
+
+// ---------------------------------------------------------------- 16-row GEMM (M <= 16) on v_mfma_f32_16x16x4_f32
+// One workgroup = 8 waves = one 16-column tile over the whole K (no split-K launch): wave w streams k chunks
+// w, w+8, ... (16 k per chunk: lane group q = lane>>4 holds k = 4q..4q+3 of its A row / B column as one float4),
+// 4 chunks in flight per lane; the 8 partial 16x16 tiles are summed through LDS. Used by the observe scan
+// (M = B rows per GPU) where every step streams the RSSM weights once from L2 / Infinity Cache.
+template <bool BKC, bool VA, bool VB>
+__global__ __launch_bounds__(512) void gemm_m16(GemmArgs g) {
+  constexpr int U = 4, NW = 8;
+  __shared__ float red[NW][4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l16 = lane & 15, q = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int split = blockIdx.y, b = blockIdx.z;
+  const int kbeg = split * g.kchunk, kend = min(g.K, kbeg + g.kchunk);
+  const float* A = g.A + (long)b * g.sA;
+  const float* Bp = g.B + (long)b * g.sB;
+  const int m = l16, n = n0 + l16;
+  const bool mv = m < g.M, nv = n < g.N;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k = kbeg + 16 * wave; k < kend; k += 16 * NW * U) {
+    f32x4 a[U], bb[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
+      const int kk = k + 16 * NW * i + 4 * q;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f}, y = {0.f, 0.f, 0.f, 0.f};
+      if (kk < kend) {
+        if (mv) {
+          const float* p = A + (long)m * g.lda + kk;
+          if (VA && kk + 3 < kend) x = *reinterpret_cast<const f32x4*>(p);
+          else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) if (kk + j < kend) x[j] = p[j];
+          }
+        }
+        if (nv) {
+          if (BKC) {
+            const float* p = Bp + (long)n * g.ldb + kk;
+            if (VB && kk + 3 < kend) y = *reinterpret_cast<const f32x4*>(p);
+            else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) if (kk + j < kend) y[j] = p[j];
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) if (kk + j < kend) y[j] = Bp[(long)(kk + j) * g.ldb + n];
+          }
+        }
+      }
+      a[i] = x;
+      bb[i] = y;
+    }
+#pragma unroll
+    for (int i = 0; i < U; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], bb[i][j], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][r][lane] = acc[r];
+  __syncthreads();
+  if (wave < 4) {  // wave w finalises accumulator register r = w: row = 4*(lane>>4) + r, col = lane & 15
+    const int r = wave;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][r][lane];
+    const int row = 4 * q + r;
+    if (row < g.M && nv) {
+      if (g.ksplit > 1) {
+        g.ws[((long)split * g.batch + b) * (long)g.M * g.N + (long)row * g.N + n] = g.alpha * v;
+      } else {
+        float o = g.alpha * v + (g.bias ? g.bias[(long)b * g.sBias + n] : 0.f);
+        float* c = g.C + (long)b * g.sC + (long)row * g.ldc + n;
+        if (g.beta != 0.f) o += g.beta * *c;
+        *c = o;
+      }
+    }
+  }
+}
+
+void launch_m16(const GemmArgs& g, bool bk, bool va, bool vb, hipStream_t st) {
+  dim3 grid(sd_cdiv(g.N, 16), g.ksplit, g.batch);
+#define M16_L(B_, A_, V_) gemm_m16<B_, A_, V_><<<grid, 512, 0, st>>>(g)
+  if (bk) {
+    if (va && vb) M16_L(true, true, true); else if (va) M16_L(true, true, false);
+    else if (vb) M16_L(true, false, true); else M16_L(true, false, false);
+  } else {
+    if (va) M16_L(false, true, false); else M16_L(false, false, false);
+  }
+#undef M16_L
+}
+
 void launch_skinny(const GemmArgs& g, bool bk, bool va, bool vb, hipStream_t st) {
   dim3 grid(sd_cdiv(g.N, 32), g.ksplit, g.batch);
 #define SK_L(B_, A_, V_) gemm_skinny<B_, A_, V_><<<grid, 256, 0, st>>>(g)
@@ -152,7 +243,8 @@ extern "C" int sd_gemm_f32(const sd_gemm_desc* d, float* workspace, long workspa
   if (ks > 1 && (!workspace || workspace_floats < (long)ks * d->batch * d->M * d->N)) return SD_EARG;
   g.ksplit = ks;
   const bool skinny = d->M <= 32 && d->a_kcontig && d->tile < 0;
-  const int kgran = skinny ? 32 : BK;
+  const bool m16 = skinny && d->M <= 16;
+  const int kgran = m16 ? 16 : skinny ? 32 : BK;
   long kc = ((long)(d->K > 0 ? d->K : 1) + ks - 1) / ks;
   kc = (kc + kgran - 1) / kgran * kgran;
   g.kchunk = (int)kc;
@@ -161,7 +253,8 @@ extern "C" int sd_gemm_f32(const sd_gemm_desc* d, float* workspace, long workspa
   const bool va = aligned16(d->A) && d->lda % 4 == 0 && (d->batch == 1 || d->strideA % 4 == 0);
   const bool vb = aligned16(d->B) && d->ldb % 4 == 0 && (d->batch == 1 || d->strideB % 4 == 0);
   if (skinny) {
-    launch_skinny(g, bk, va, vb, stream);
+    if (m16) launch_m16(g, bk, va, vb, stream);
+    else launch_skinny(g, bk, va, vb, stream);
     SD_LAUNCH_CHECK();
     if (ks > 1) {
       long total = (long)d->batch * d->M * d->N;

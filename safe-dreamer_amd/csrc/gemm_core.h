@@ -7,8 +7,8 @@
 namespace sdg {
 namespace {  // internal linkage: the core is instantiated per translation unit
 
-constexpr int BK = 16;
-constexpr int LDS_ROW = BK + 4;  // floats
+constexpr int BK = 32;
+constexpr int LDS_ROW = BK + 4;  // floats (144-B rows: 9 is odd -> conflict-free b128 reads)
 
 struct GemmArgs {
   const float* A;
@@ -133,25 +133,30 @@ SD_DEV void gemm_block(const GemmArgs& g, OpA& la, OpB& lb, int bm0, int bn0, in
       la.load(kbeg + (kt + 1) * BK, kend);
       lb.load(kbeg + (kt + 1) * BK, kend);
     }
-    float af[TM][8], bf[TN][8];
+    constexpr int KH = BK / 2;  // k values per lane half per tile
+    float af[TM][KH], bf[TN][KH];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const float* q = smem + cur * STAGE + (wr * WM + 32 * i + l32) * LDS_ROW + 8 * h;
-      f32x4 x0 = *reinterpret_cast<const f32x4*>(q);
-      f32x4 x1 = *reinterpret_cast<const f32x4*>(q + 4);
+      const float* q = smem + cur * STAGE + (wr * WM + 32 * i + l32) * LDS_ROW + KH * h;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) { af[i][s] = x0[s]; af[i][s + 4] = x1[s]; }
+      for (int v = 0; v < KH / 4; ++v) {
+        f32x4 x = *reinterpret_cast<const f32x4*>(q + 4 * v);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) af[i][4 * v + s] = x[s];
+      }
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const float* q = smem + cur * STAGE + BM * LDS_ROW + (wc * WN + 32 * j + l32) * LDS_ROW + 8 * h;
-      f32x4 x0 = *reinterpret_cast<const f32x4*>(q);
-      f32x4 x1 = *reinterpret_cast<const f32x4*>(q + 4);
+      const float* q = smem + cur * STAGE + BM * LDS_ROW + (wc * WN + 32 * j + l32) * LDS_ROW + KH * h;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) { bf[j][s] = x0[s]; bf[j][s + 4] = x1[s]; }
+      for (int v = 0; v < KH / 4; ++v) {
+        f32x4 x = *reinterpret_cast<const f32x4*>(q + 4 * v);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) bf[j][4 * v + s] = x[s];
+      }
     }
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
+    for (int s = 0; s < KH; ++s)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll

@@ -23,7 +23,7 @@ SD_DEV float team_sum(float v, float* red) {
 template <int TEAM, int VPT>
 __global__ __launch_bounds__(256) void rms_fwd(const float* __restrict__ x, const float* __restrict__ w,
                                                float* __restrict__ y, float* __restrict__ rstd, int M, int N,
-                                               float eps, int act) {
+                                               float eps, int act, long ldy) {
   constexpr int TPB = 256 / TEAM;  // teams per block
   __shared__ float red[4];
   const int team = threadIdx.x / TEAM, t = threadIdx.x % TEAM;
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void rms_fwd(const float* __restrict__ x, cons
     ss = team_sum<TEAM>(ss, red);
     const float r = rsqrtf(ss / (float)N + eps);
     if (t == 0 && rstd) rstd[row] = r;
-    float* yr = y + row * N;
+    float* yr = y + row * ldy;
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
       const int c = t + j * TEAM;
@@ -226,13 +226,18 @@ int team_for(int N) {
 
 extern "C" int sd_rmsnorm_fwd(const float* x, const float* w, float* y, float* rstd, int M, int N, float eps,
                               int act, sd_stream stream_) {
+  return sd_rmsnorm_fwd_ld(x, w, y, N, rstd, M, N, eps, act, stream_);
+}
+
+extern "C" int sd_rmsnorm_fwd_ld(const float* x, const float* w, float* y, long ldy, float* rstd, int M, int N,
+                                 float eps, int act, sd_stream stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (M <= 0) return SD_OK;
   if (N <= 0 || N > 4096) return SD_ESHAPE;
   const int team = team_for(N);
-  if (team == 16) { int grid = grid_for<16>(M); SD_RMS_DISPATCH(rms_fwd, 16, x, w, y, rstd, M, N, eps, act) }
-  else if (team == 64) { int grid = grid_for<64>(M); SD_RMS_DISPATCH(rms_fwd, 64, x, w, y, rstd, M, N, eps, act) }
-  else { int grid = grid_for<256>(M); SD_RMS_DISPATCH(rms_fwd, 256, x, w, y, rstd, M, N, eps, act) }
+  if (team == 16) { int grid = grid_for<16>(M); SD_RMS_DISPATCH(rms_fwd, 16, x, w, y, rstd, M, N, eps, act, ldy) }
+  else if (team == 64) { int grid = grid_for<64>(M); SD_RMS_DISPATCH(rms_fwd, 64, x, w, y, rstd, M, N, eps, act, ldy) }
+  else { int grid = grid_for<256>(M); SD_RMS_DISPATCH(rms_fwd, 256, x, w, y, rstd, M, N, eps, act, ldy) }
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

@@ -129,6 +129,9 @@ class Dreamer(nn.Module):
         self.rbins = _symexp_bins(int(config.reward.dist.bin_num), self.device)
         self.vbins = _symexp_bins(int(config.critic.dist.bin_num), self.device)
         self._updates = 0
+        self.use_graphs = True
+        self._graph = None
+        self._eager_updates = 0
         self._seed_base = int(getattr(config, "seed", 0) or 0) * 1_000_003 + 12345
         self.train()
 
@@ -149,8 +152,11 @@ class Dreamer(nn.Module):
 
     def _update_slow_target(self):  # dreamer.py:242-249
         if self._slow_value_updates % self.slow_target_update == 0:
-            K.polyak(self._optimizer.arena.data[self._v_lo:self._v_hi], self._slow_arena, self.slow_target_fraction)
+            self._polyak()
         self._slow_value_updates += 1
+
+    def _polyak(self):
+        K.polyak(self._optimizer.arena.data[self._v_lo:self._v_hi], self._slow_arena, self.slow_target_fraction)
 
     @torch.no_grad()
     def preprocess(self, data):  # dreamer.py:709-713
@@ -192,8 +198,9 @@ class Dreamer(nn.Module):
             return K.onehot_sample(logits.contiguous(), self.act_dim, float(d.unimix_ratio), seed, stream_id, step,
                                    row_offset)
         out = torch.empty(logits.shape[0], self.act_dim, dtype=torch.float32, device=logits.device)
+        sh, sp = K.seed_args(seed)
         K.nat.call("sd_bnormal_sample", K.p(logits.contiguous()), K.p(out), logits.shape[0], self.act_dim,
-                   float(d.min_std), float(d.max_std), int(seed), stream_id, int(step), int(row_offset), K.stream())
+                   float(d.min_std), float(d.max_std), sh, stream_id, int(step), int(row_offset), sp, K.stream())
         return out
 
     # ------------------------------------------------------------------ update
@@ -206,10 +213,16 @@ class Dreamer(nn.Module):
         return mets
 
     def update_batch(self, data, initial, seed, row_offset=None):
+        """One optimisation step on a given batch. Single-GPU runs are captured into a HIP graph after two eager
+        warm-up updates (set `use_graphs = False` to stay eager); multi-GPU runs stay eager (RCCL collectives)."""
+        ro = self.rank * data["action"].shape[0] if row_offset is None else row_offset
+        if self.use_graphs and self.world == 1 and self.slow_target_update == 1:
+            if self._graph is not None or self._eager_updates >= 2:
+                return self._update_graphed(data, initial, seed, ro)
+        self._eager_updates += 1
         p_data = self.preprocess(dict(data))
         self._update_slow_target()
         self._optimizer.zero_grad()
-        ro = self.rank * p_data["action"].shape[0] if row_offset is None else row_offset
         post, mets = self._cal_grad(p_data, initial, seed, ro)
         if self.world > 1:
             parallel.allreduce_mean_(self._optimizer.arena.grad)
@@ -219,6 +232,42 @@ class Dreamer(nn.Module):
         mets["opt/grad_scale"] = 1.0
         self._updates += 1
         return post, mets
+
+    def _core(self, data, initial, seed, ro):
+        """Device-only work of one update (captured once, replayed every update)."""
+        p_data = self.preprocess(dict(data))
+        self._polyak()
+        self._optimizer.zero_grad()
+        post, mets = self._cal_grad(p_data, initial, seed, ro)
+        self._optimizer.launch_step()
+        return post, mets
+
+    def _update_graphed(self, data, initial, seed, ro):
+        if self._graph is None:
+            self._g_in = {k: v.clone() for k, v in data.items()}
+            self._g_init = tuple(t.clone() for t in initial)
+            self._seed_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                post, mets = self._core(self._g_in, self._g_init, self._seed_dev, ro)
+                keys = [k for k, v in mets.items() if isinstance(v, torch.Tensor)]
+                self._g_mvec = torch.stack([mets[k].float().reshape(()) for k in keys])
+            self._graph, self._g_post, self._g_keys = g, post, keys
+        for k, v in data.items():
+            self._g_in[k].copy_(v)
+        for dst, src in zip(self._g_init, initial):
+            dst.copy_(src)
+        self._seed_dev.fill_(int(seed) & 0x7FFFFFFFFFFFFFFF)
+        self._graph.replay()
+        self._slow_value_updates += 1
+        self._optimizer.host_steps += 1
+        self._updates += 1
+        vec = self._g_mvec.clone()
+        mets = {k: vec[i] for i, k in enumerate(self._g_keys)}
+        mets["opt/lr"] = self._scheduler.get_lr()[0]
+        mets["opt/grad_scale"] = 1.0
+        return self._g_post, mets
 
     def _cal_grad(self, data, initial, seed=0, row_offset=0):
         """dreamer.py:453-671 (fp32). data: dict of (B, T, *) device tensors, image float in [0, 1]."""

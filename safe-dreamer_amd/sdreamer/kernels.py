@@ -53,7 +53,12 @@ def _layout(t, rows_dim, k_dim):
 
 
 def _skinny_split(M, N, K, batch):
-    """K split for the M <= 32 kernel: ~256 workgroups, >= 128-deep K chunks."""
+    """K split for the skinny kernels: single launch when there are enough column tiles, else up to ~64 WGs."""
+    if M <= 16:
+        tiles = -(-N // 16) * batch
+        if tiles >= 16 or K < 1024:
+            return 1
+        return max(1, min(-(-64 // tiles), K // 512))
     tiles = -(-N // 32) * batch
     ks = min(max(K // 128, 1), max(1, -(-256 // tiles)))
     return max(1, min(ks, 64))
@@ -131,12 +136,18 @@ def linear(x, w, b=None, out=None, beta=0.0):
 
 # ------------------------------------------------------------------------------------------------- row norms
 def rmsnorm_fwd(x, w, act=1, y=None, rstd=None):
+    """y may be a column slice of a wider row-major tensor (unit column stride)."""
     x = _c(x)
     N = x.shape[-1]
     M = x.numel() // N
     y = torch.empty_like(x) if y is None else y
     rstd = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device) if rstd is None else rstd
-    nat.call("sd_rmsnorm_fwd", p(x), p(w), p(y), p(rstd), M, N, EPS, int(act), stream())
+    if y.is_contiguous():
+        nat.call("sd_rmsnorm_fwd", p(x), p(w), p(y), p(rstd), M, N, EPS, int(act), stream())
+    else:
+        if y.dim() != 2 or y.stride(1) != 1:
+            raise ValueError("strided rmsnorm output must be a 2-D row-major slice")
+        nat.call("sd_rmsnorm_fwd_ld", p(x), p(w), p(y), y.stride(0), p(rstd), M, N, EPS, int(act), stream())
     return y, rstd
 
 
@@ -166,27 +177,36 @@ def colsum(x2d, out, accumulate=True):
 
 
 # ------------------------------------------------------------------------------------------------- latents
+def seed_args(seed):
+    """A sampling seed is an int, or a device int64 tensor (graph-replayable): -> (host part, device pointer)."""
+    if isinstance(seed, torch.Tensor):
+        return 0, seed.data_ptr()
+    return int(seed) & 0xFFFFFFFFFFFFFFFF, 0
+
+
 def onehot_sample(logits, K, unimix, seed, stream_id, step, group_offset, out=None, index=None, entropy=None):
     logits = _c(logits)
     groups = logits.numel() // K
     out = torch.empty_like(logits) if out is None else out
+    sh, sp = seed_args(seed)
     nat.call("sd_onehot_sample_fwd", p(logits), p(out), p(index), p(entropy), groups, K, float(unimix),
-             int(seed), int(stream_id), int(step), int(group_offset), stream())
+             sh, int(stream_id), int(step), int(group_offset), sp, stream())
     return out
 
 
 def onehot_entropy(logits, K, unimix):
     groups = logits.numel() // K
     ent = torch.empty(groups, dtype=torch.float32, device=logits.device)
-    nat.call("sd_onehot_sample_fwd", p(_c(logits)), 0, 0, p(ent), groups, K, float(unimix), 0, 0, 0, 0, stream())
+    nat.call("sd_onehot_sample_fwd", p(_c(logits)), 0, 0, p(ent), groups, K, float(unimix), 0, 0, 0, 0, 0, stream())
     return ent
 
 
 def onehot_sample_bwd(logits, dout, K, unimix, seed, stream_id, step, group_offset, dlogits=None, accumulate=False):
     groups = logits.numel() // K
     dlogits = torch.empty_like(logits) if dlogits is None else dlogits
-    nat.call("sd_onehot_sample_bwd", p(_c(logits)), p(_c(dout)), p(dlogits), groups, K, float(unimix), int(seed),
-             int(stream_id), int(step), int(group_offset), int(accumulate), stream())
+    sh, sp = seed_args(seed)
+    nat.call("sd_onehot_sample_bwd", p(_c(logits)), p(_c(dout)), p(dlogits), groups, K, float(unimix), sh,
+             int(stream_id), int(step), int(group_offset), int(accumulate), sp, stream())
     return dlogits
 
 
@@ -357,14 +377,38 @@ class LaunchProbe:
     def match(self, name, args):
         return name == self.name and self.pred(args)
 
+    def end(self, args):
+        e = torch.cuda.Event(enable_timing=True)
+        if torch.cuda.is_current_stream_capturing():
+            self.captured_args = args  # inside a HIP-graph capture: remember the launch, time it by replay()
+            self._start = None
+            return
+        e.record()
+        self.records.append((self._start, e, self.work_fn(args)))
+        self.captured_args = args
+
     def begin(self):
+        if torch.cuda.is_current_stream_capturing():
+            return
         self._start = torch.cuda.Event(enable_timing=True)
         self._start.record()
 
-    def end(self, args):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        self.records.append((self._start, e, self.work_fn(args)))
+    def replay(self, n=20):
+        """Re-issue the last recorded launch (same buffers, same shapes) n times, each bracketed by HIP events on
+        the current stream (graph-replayed steps are invisible to Python-side hooks)."""
+        args = getattr(self, "captured_args", None)
+        if args is None:
+            return
+        args = tuple(args[:-1]) + (stream(),)  # launch on the stream the events are recorded on
+        self.records = []
+        for _ in range(n):
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            nat.check(nat.fns[self.name](*args), self.name)
+            e.record()
+            self.records.append((s, e, self.work_fn(args)))
+        torch.cuda.synchronize()
 
     def stop(self):
         if self in nat.PROBES:

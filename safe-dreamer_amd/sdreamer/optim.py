@@ -86,12 +86,17 @@ class LaProp(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        self.launch_step()
+        self.host_steps += 1
+
+    @torch.no_grad()
+    def launch_step(self):
+        """Device part of step() (graph-capturable; host bookkeeping is in step())."""
         a = self.arena
         nat.call("sd_agc_laprop_step", K.p(a.data), K.p(a.grad), K.p(self.exp_avg), K.p(self.exp_avg_sq),
                  K.p(a.chunk_beg), K.p(a.chunk_end), K.p(a.chunk_tensor), K.p(a.tensor_chunk0), a.nchunks,
                  a.ntensors, K.p(self.workspace), K.p(self.scalars), K.p(self.grad_norms), self.agc, self.pmin,
                  self.base_lr, self.warmup, self.betas[0], self.betas[1], self.eps, K.stream())
-        self.host_steps += 1
 
     def current_lr(self):
         """lr the NEXT step will use (LambdaLR semantics; host-side bookkeeping, no device sync)."""

@@ -120,7 +120,7 @@ class RSSM(nn.Module):
         r = reset.reshape(B, T).to(torch.uint8)
         stoch0, deter0 = initial
         return ObserveScan.apply(embed, action, r, stoch0.reshape(B, -1).contiguous(), deter0.contiguous(), self,
-                                 int(seed), int(row_offset))
+                                 seed, int(row_offset))
 
     @torch.no_grad()
     def obs_step(self, stoch, deter, prev_action, embed, reset, seed=0, step=0, row_offset=0,
@@ -192,11 +192,12 @@ class RSSM(nn.Module):
         D, G, U = self._deter, self._blocks, self._hidden
         Dg = D // G
         xcat = torch.empty(M, 3 * U, dtype=torch.float32, device=h_in.device)
-        xcat[:, :U] = K.rmsnorm_fwd(K.linear(h_in, P["W0"], P["b0"]), P["n0"])[0]
-        xcat[:, U:2 * U] = K.rmsnorm_fwd(K.linear(s_in, P["W1"], P["b1"]), P["n1"])[0]
+        K.rmsnorm_fwd(K.linear(h_in, P["W0"], P["b0"]), P["n0"], y=xcat[:, :U])
+        K.rmsnorm_fwd(K.linear(s_in, P["W1"], P["b1"]), P["n1"], y=xcat[:, U:2 * U])
         if x2 is None:
-            x2 = K.rmsnorm_fwd(K.linear(a_n, P["W2"], P["b2"]), P["n2"])[0]
-        xcat[:, 2 * U:] = x2
+            K.rmsnorm_fwd(K.linear(a_n, P["W2"], P["b2"]), P["n2"], y=xcat[:, 2 * U:])
+        else:
+            xcat[:, 2 * U:] = x2
         hp = K.mm(xcat, P["Wsh"].t(), bias=P["bh"])
         K.gemm(h_in.view(M, G, Dg).permute(1, 0, 2), P["Wbd"].transpose(1, 2), hp.view(M, G, Dg).permute(1, 0, 2),
                beta=1.0)
@@ -267,9 +268,9 @@ class ObserveScan(torch.autograd.Function):
             K.mask_rows(prev_s, m, out=s_in[t])
             K.mask_rows(prev_h, m, out=h_in[t])
             K.linear(h_in[t], P["W0"], P["b0"], out=x0p[t])
-            xcat[t, :, :U] = K.rmsnorm_fwd(x0p[t], P["n0"], rstd=r0[t])[0]
+            K.rmsnorm_fwd(x0p[t], P["n0"], y=xcat[t, :, :U], rstd=r0[t])
             K.linear(s_in[t], P["W1"], P["b1"], out=x1p[t])
-            xcat[t, :, U:2 * U] = K.rmsnorm_fwd(x1p[t], P["n1"], rstd=r1[t])[0]
+            K.rmsnorm_fwd(x1p[t], P["n1"], y=xcat[t, :, U:2 * U], rstd=r1[t])
             K.gemm(xcat[t], P["Wsh"].t(), hp[t], bias=P["bh"])
             K.gemm(h_in[t].view(B, G, Dg).permute(1, 0, 2), P["Wbd"].transpose(1, 2),
                    hp[t].view(B, G, Dg).permute(1, 0, 2), beta=1.0)

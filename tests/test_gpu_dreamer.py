@@ -102,3 +102,28 @@ def test_update_matches_reference(name):
             ref = z[f"u{u}_p_{k}__s"]
             step = 4e-5 * (u + 1) / 1000 * 5  # |dp| <= lr * O(1) for LaProp; compare to the step scale
             assert np.abs(got - ref).max() <= max(2e-3 * step, 1e-6 * np.abs(ref).max()), k
+
+
+def test_graph_replay_matches_eager():
+    """HIP-graph replays (update 3+) produce exactly the eager results: same kernels, device-resident seed."""
+    name = "walker_r2"
+    runs = []
+    for graphs in (False, True):
+        ag, z, spec, obs = build_agent(name)
+        ag.use_graphs = graphs
+        out = []
+        for u in range(5):
+            data = batch(z, u % 2, obs, DEV)
+            init = initial(z, u % 2, spec, DEV)
+            (ps, pd), mets = ag.update_batch(data, init, 500 + u)
+            out.append((float(mets["loss/dyn"]), float(mets["loss/value"]), float(mets["opt/loss"]),
+                        pd.detach().clone(), ps.argmax(-1).clone()))
+        sd = ag.state_dict()
+        out.append(torch.cat([sd[k].reshape(-1) for k in spec.shapes]).clone())
+        runs.append(out)
+    (e, g) = runs
+    assert ag._graph is not None
+    for u in range(5):
+        assert e[u][:3] == g[u][:3], (u, e[u][:3], g[u][:3])
+        assert torch.equal(e[u][3], g[u][3]) and torch.equal(e[u][4], g[u][4])
+    assert torch.equal(e[5], g[5])
