@@ -187,6 +187,47 @@ int sd_standardize_bwd(const float* x, const float* mean, const float* stdv, con
 int sd_barlow_loss(const float* c, int E, float lambd, float* partial, int nblocks, float* loss, sd_stream stream);
 int sd_barlow_dc(const float* c, const float* g, float* dc, int E, float lambd, sd_stream stream);
 
+/* ---------------------------------------------------------------- fused RSSM posterior scan (ObserveScan)
+ * RSSM.observe's recurrence (rssm.py:140-178 + Deter.forward rssm.py:36-75) for B <= 16 rows per step, as
+ * 5 fused launches per step forward and 6 per step backward (instead of ~15 / ~20 separate kernels): every launch is
+ * an M=16 MFMA contraction whose A panel is built in LDS by a fused prologue (split-K slab reduction, RMSNorm+SiLU,
+ * straight-through sampler backward, RMSNorm backward) and whose epilogue fuses bias, the GRU gate fwd/bwd, the
+ * unimix sampler and the reset masks. Recurrence-free work (action branch, embed half of obs_net_0, all weight
+ * gradients) stays outside as (T*B)-row GEMMs. Weight operands are k-contiguous (row n of a [N][K] matrix);
+ * the backward uses transposed copies the caller prepares once per update. Time-major (T,B,.) activations.
+ * Requirements: B <= 16; D % G == 0; U, D/G, S*Kd multiples of 64; Kd in {16, 32, 64}. */
+typedef struct sd_rssm_scan {
+  int B, T, D, U, SK, Kd, G;
+  int ks_d, ks_s;              /* K splits of the D-wide and SK-wide step GEMMs (slabs summed by the consumer) */
+  float eps, unimix;
+  uint64_t seed;
+  const uint64_t* seed_ptr;    /* optional device seed offset (graph replay) */
+  int stream_id;
+  long group_offset;           /* global categorical index of row 0 (data-parallel row offset * S) */
+  /* parameters */
+  const float *W0, *b0, *n0;   /* _dyn_in0: (U,D) (U) (U) */
+  const float *W1, *b1, *n1;   /* _dyn_in1: (U,SK) */
+  const float *Wh, *bh, *nh;   /* _dyn_hid: (G, D/G, D/G+3U) (D) (D) */
+  const float *Wg, *bg;        /* _dyn_gru: (G, 3D/G, D/G) (3D) */
+  const float *WoD, *no;       /* obs_net_0 weight[:, :D] as a contiguous (U,D); obs_net_n_0 (U) */
+  const float *Wl, *bl;        /* obs_net_logit: (SK,U) (SK) */
+  const float *W0T, *W1T, *WshT, *WbdT, *WgT, *WoDT, *WlT;  /* backward: (D,U) (SK,U) (3U,D) (G,Dg,Dg) (G,Dg,3Dg) (D,U) (U,SK) */
+  /* inputs */
+  const unsigned char* reset;  /* (T,B) */
+  const float *stoch0, *deter0;/* (B,SK) (B,D) */
+  const float *x2, *eproj;     /* (T,B,U): action branch output; embed half of obs_net_0 + bias */
+  /* saved activations (written by fwd, read by bwd) */
+  float *s_in, *h_in, *x0p, *x1p, *r0, *r1, *xcat, *hp, *hh, *rh, *gates, *deter, *op, *oo, *ro, *logit, *stoch;
+  /* backward */
+  const float *d_stoch, *d_deter, *d_logit;  /* (T,B,SK) (T,B,D) (T,B,SK) incoming grads; each may be NULL */
+  float* dl;                       /* out (T,B,SK): total d logit (incl. the straight-through sample gradient) */
+  float *d_o, *d_op, *d_gates, *d_hh, *d_hp, *d_xcat, *d_x0p, *d_x1p;  /* (T,B,.) */
+  float* work;                     /* >= sd_rssm_scan_work_floats(d) floats */
+} sd_rssm_scan;
+int sd_rssm_scan_work_floats(const sd_rssm_scan* d);
+int sd_rssm_scan_fwd(const sd_rssm_scan* d, sd_stream stream);
+int sd_rssm_scan_bwd(const sd_rssm_scan* d, sd_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

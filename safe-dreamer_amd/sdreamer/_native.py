@@ -39,6 +39,30 @@ class GemmDesc(ctypes.Structure):
 
 HEADER = os.environ.get("SDHIP_HEADER", os.path.join(_HERE, "..", "..", "include", "sdhip.h"))
 
+
+def _parse_struct(path, name):
+    """ctypes.Structure for `typedef struct <name> {...} <name>;` in the header (fields in declaration order)."""
+    import re
+    text = re.sub(r"/\*.*?\*/", " ", open(path).read(), flags=re.S)
+    body = re.search(r"typedef struct " + name + r"\s*\{(.*?)\}\s*" + name + r"\s*;", text, flags=re.S).group(1)
+    scalars = {"int": c_int, "long": c_long, "float": c_float, "double": ctypes.c_double, "uint64_t": ctypes.c_uint64}
+    fields = []
+    for decl in body.split(";"):
+        decl = " ".join(decl.split())
+        if not decl:
+            continue
+        is_ptr = "*" in decl
+        toks = decl.replace("const ", "").replace("*", " ").replace(",", " , ").split()
+        if toks[0] == "unsigned":
+            toks = toks[1:]
+        base, names = toks[0], [t for t in toks[1:] if t != ","]
+        for n in names:
+            fields.append((n, c_ptr if is_ptr else scalars[base]))
+    return type(name, (ctypes.Structure,), {"_fields_": fields})
+
+
+ScanDesc = _parse_struct(HEADER, "sd_rssm_scan")
+
 _CTYPES = {
     "int": c_int, "long": c_long, "float": c_float, "double": ctypes.c_double, "uint64_t": ctypes.c_uint64,
     "sd_stream": c_ptr, "void": None,

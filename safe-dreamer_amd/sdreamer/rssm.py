@@ -15,14 +15,60 @@ Same module tree / parameter names as the reference (`_deter_net._dyn_in{0,1,2}`
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import torch
 from torch import nn
 
+from . import _native as nat
 from . import kernels as K
 from . import ops
 from .networks import Act, BlockLinear, Lambda, Linear, RMSNorm
 
 STREAM_OBS, STREAM_IMG, STREAM_ACT, STREAM_POLICY = 1, 2, 3, 4
+# the fused scan (csrc/scan.hip) is the default; SDREAMER_FUSED_SCAN=0 selects the per-op HIP kernels (tests compare)
+FUSED_SCAN = os.environ.get("SDREAMER_FUSED_SCAN", "1") != "0"
+
+
+def _fused_scan_ok(rssm, B):
+    D, U, G, SK, Kd = rssm._deter, rssm._hidden, rssm._blocks, rssm.flat_stoch, rssm._discrete
+    if not FUSED_SCAN or B > 16 or D % G:
+        return False
+    Dg = D // G
+    return U % 64 == 0 and Dg % 64 == 0 and SK % 64 == 0 and D % 64 == 0 and Kd in (16, 32, 64) and \
+        SK % Kd == 0 and Dg + 3 * U <= 2048 and D // _ks(D, 512) <= 2048 and SK <= 2048
+
+
+def _ks(K_, span):
+    """K split with ~`span`-deep slabs (span a multiple of 16 dividing K)."""
+    ks = max(1, K_ // span)
+    while K_ % (ks * 16):
+        ks -= 1
+    return ks
+
+
+def _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, work):
+    d = nat.ScanDesc()
+    D, U, SK, Kd, G = rssm._deter, rssm._hidden, rssm.flat_stoch, rssm._discrete, rssm._blocks
+    d.B, d.T, d.D, d.U, d.SK, d.Kd, d.G = B, T, D, U, SK, Kd, G
+    d.ks_d, d.ks_s = _ks(D, 512), _ks(SK, 256)
+    d.eps, d.unimix = K.EPS, rssm._unimix_ratio
+    sh, sp = K.seed_args(seed)
+    d.seed, d.seed_ptr, d.stream_id, d.group_offset = sh, sp, STREAM_OBS, int(row_offset) * rssm._stoch
+    for k in ("W0", "b0", "n0", "W1", "b1", "n1", "Wh", "bh", "nh", "Wg", "bg", "Wl", "bl"):
+        setattr(d, k, P[k].data_ptr())
+    d.no = P["no"].data_ptr()
+    d.reset, d.x2, d.eproj = rt.data_ptr(), x2.data_ptr(), eproj.data_ptr()
+    d.work = K.p(work)
+    return d
+
+
+def _scan_work(d):
+    n = nat.fns["sd_rssm_scan_work_floats"](ctypes.addressof(d))
+    if n < 0:
+        raise nat.NativeError(f"sd_rssm_scan_work_floats failed with status {n}")
+    return n
 
 
 class Deter(nn.Module):
@@ -261,9 +307,24 @@ class ObserveScan(torch.autograd.Function):
         ro = torch.empty(T, B, dtype=f32, device=dev)
         logit = torch.empty(T, B, SK, dtype=f32, device=dev)
         stoch = torch.empty(T, B, SK, dtype=f32, device=dev)
-        xcat[:, :, 2 * U:] = x2.view(T, B, U)
+        fused = _fused_scan_ok(rssm, B)
+        if fused:
+            WoD = P["Wo"][:, :D].contiguous()
+            d = _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, None)
+            work = torch.empty(_scan_work(d), dtype=f32, device=dev)
+            d.work, d.WoD = work.data_ptr(), WoD.data_ptr()
+            d.stoch0, d.deter0 = stoch0.data_ptr(), deter0.data_ptr()
+            for k, v in (("s_in", s_in), ("h_in", h_in), ("x0p", x0p), ("x1p", x1p), ("r0", r0), ("r1", r1),
+                         ("xcat", xcat), ("hp", hp), ("hh", hh), ("rh", rh), ("gates", gates), ("deter", deter),
+                         ("op", op), ("oo", oo), ("ro", ro), ("logit", logit), ("stoch", stoch)):
+                setattr(d, k, v.data_ptr())
+            op = torch.empty(T, B, U, dtype=f32, device=dev)  # eproj stays the (embed half + bias) input
+            d.op = op.data_ptr()
+            nat.call("sd_rssm_scan_fwd", ctypes.addressof(d), K.stream())
+        else:
+            xcat[:, :, 2 * U:] = x2.view(T, B, U)
         prev_s, prev_h = stoch0, deter0
-        for t in range(T):
+        for t in (range(0) if fused else range(T)):
             m = rt[t]
             K.mask_rows(prev_s, m, out=s_in[t])
             K.mask_rows(prev_h, m, out=h_in[t])
@@ -287,6 +348,9 @@ class ObserveScan(torch.autograd.Function):
                               op, oo, ro, logit)
         ctx.rssm, ctx.seed, ctx.row_offset = rssm, seed, row_offset
         ctx.dims = (B, T, A, E)
+        ctx.fused = fused
+        if fused:
+            ctx.x2 = x2
         post_stoch = stoch.transpose(0, 1).reshape(B, T, S, Kd).contiguous()
         post_deter = deter.transpose(0, 1).contiguous()
         post_logit = logit.transpose(0, 1).reshape(B, T, S, Kd).contiguous()
@@ -310,6 +374,12 @@ class ObserveScan(torch.autograd.Function):
                 return torch.zeros(T, B, width, dtype=f32, device=dev)
             return x.reshape(B, T, width).transpose(0, 1).contiguous()
 
+        gb = ops.grad_buf
+        if ctx.fused:
+            dl_all, d_op, d_gates, d_hp, d_x0p, d_x1p, d_x2 = ObserveScan._bwd_fused(
+                ctx, d_stoch, d_deter, d_logit, rt, s_in, h_in, x0p, x1p, r0, r1, hp, rh, gates, op, ro, logit)
+            return ObserveScan._wgrads(ctx, P, rt, a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all,
+                                       d_op, d_gates, d_hp, d_x0p, d_x1p, d_x2)
         ds_out = tm(d_stoch, SK)
         dd_out = tm(d_deter, D)
         dl_all = tm(d_logit, SK)  # becomes d logit (incl. the straight-through sample gradient) in place
@@ -321,7 +391,6 @@ class ObserveScan(torch.autograd.Function):
         d_x2 = torch.empty(T, B, U, dtype=f32, device=dev)
         carry_s = torch.zeros(B, SK, dtype=f32, device=dev)
         carry_h = torch.zeros(B, D, dtype=f32, device=dev)
-        gb = ops.grad_buf
         for t in reversed(range(T)):
             ds = ds_out[t] + carry_s
             K.onehot_sample_bwd(logit[t], ds, Kd, rssm._unimix_ratio, ctx.seed, STREAM_OBS, t, ctx.row_offset * S,
@@ -345,7 +414,64 @@ class ObserveScan(torch.autograd.Function):
             m = rt[t]
             carry_h = K.mask_rows(d_hin, m)
             carry_s = K.mask_rows(d_sin, m)
-        # ---- deferred weight gradients: one GEMM over all T*B rows each
+        return ObserveScan._wgrads(ctx, P, rt, a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all, d_op,
+                                   d_gates, d_hp, d_x0p, d_x1p, d_x2)
+
+    @staticmethod
+    def _bwd_fused(ctx, d_stoch, d_deter, d_logit, rt, s_in, h_in, x0p, x1p, r0, r1, hp, rh, gates, op, ro, logit):
+        """Serial part of the backward as sd_rssm_scan_bwd (6 fused launches per step) + the RMSNorm weight
+        gradients of the four in-loop norms as (T*B)-row reductions."""
+        rssm = ctx.rssm
+        P = rssm._p()
+        B, T, A, E = ctx.dims
+        S, Kd, D, U, G = rssm._stoch, rssm._discrete, rssm._deter, rssm._hidden, rssm._blocks
+        SK = S * Kd
+        M = T * B
+        dev = logit.device
+        f32 = torch.float32
+
+        def tm(x, width):
+            return None if x is None else x.reshape(B, T, width).transpose(0, 1).contiguous()
+
+        ds_out, dd_out, dl_in = tm(d_stoch, SK), tm(d_deter, D), tm(d_logit, SK)
+        e = lambda *shape: torch.empty(*shape, dtype=f32, device=dev)  # noqa: E731
+        dl, d_o, d_op, d_x0p, d_x1p = e(T, B, SK), e(T, B, U), e(T, B, U), e(T, B, U), e(T, B, U)
+        d_gates, d_hh, d_hp, d_xcat = e(T, B, 3 * D), e(T, B, D), e(T, B, D), e(T, B, 3 * U)
+        Wo_d = P["Wo"][:, :D]
+        tr = dict(W0T=P["W0"].t().contiguous(), W1T=P["W1"].t().contiguous(), WshT=P["Wsh"].t().contiguous(),
+                  WbdT=P["Wbd"].transpose(1, 2).contiguous(), WgT=P["Wg"].transpose(1, 2).contiguous(),
+                  WoDT=Wo_d.t().contiguous(), WlT=P["Wl"].t().contiguous())
+        x2 = ctx.x2
+        d = _scan_desc(rssm, P, B, T, ctx.seed, ctx.row_offset, rt, x2, x2, None)
+        work = e(_scan_work(d))
+        d.work = work.data_ptr()
+        for k, v in list(tr.items()) + [("s_in", s_in), ("h_in", h_in), ("x0p", x0p), ("x1p", x1p), ("r0", r0),
+                                         ("r1", r1), ("hp", hp), ("rh", rh), ("gates", gates), ("op", op),
+                                         ("ro", ro), ("logit", logit), ("dl", dl), ("d_o", d_o), ("d_op", d_op),
+                                         ("d_gates", d_gates), ("d_hh", d_hh), ("d_hp", d_hp),
+                                         ("d_xcat", d_xcat), ("d_x0p", d_x0p), ("d_x1p", d_x1p)]:
+            setattr(d, k, v.data_ptr())
+        d.d_stoch, d.d_deter, d.d_logit = K.p(ds_out), K.p(dd_out), K.p(dl_in)
+        nat.call("sd_rssm_scan_bwd", ctypes.addressof(d), K.stream())
+        gb = ops.grad_buf
+        f = lambda x: x.reshape(M, -1)  # noqa: E731
+        K.rmsnorm_bwd(f(op), P["no"], ro.reshape(M), f(d_o), dw=gb(P["no"]))
+        K.rmsnorm_bwd(f(hp), P["nh"], rh.reshape(M), f(d_hh), dw=gb(P["nh"]))
+        K.rmsnorm_bwd(f(x0p), P["n0"], r0.reshape(M), f(d_xcat)[:, :U].contiguous(), dw=gb(P["n0"]))
+        K.rmsnorm_bwd(f(x1p), P["n1"], r1.reshape(M), f(d_xcat)[:, U:2 * U].contiguous(), dw=gb(P["n1"]))
+        d_x2 = d_xcat[:, :, 2 * U:].contiguous()
+        return dl, d_op, d_gates, d_hp, d_x0p, d_x1p, d_x2
+
+    @staticmethod
+    def _wgrads(ctx, P, rt, a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all, d_op, d_gates, d_hp,
+                d_x0p, d_x1p, d_x2):
+        """Deferred weight gradients: one GEMM (or column sum) over all T*B time-major rows each."""
+        rssm = ctx.rssm
+        B, T, A, E = ctx.dims
+        D, G = rssm._deter, rssm._blocks
+        Dg = D // G
+        M = T * B
+        gb = ops.grad_buf
         f = lambda x: x.reshape(M, -1)  # noqa: E731
         K.gemm(f(dl_all).t(), f(oo), gb(P["Wl"]), beta=1.0)
         K.colsum(f(dl_all), gb(P["bl"]))

@@ -42,6 +42,22 @@ def test_gemm_desc_layout_matches_c():
     assert [int(x) for x in out] == [ctypes.sizeof(G), G.M.offset, G.ksplit.offset, G.beta.offset]
 
 
+def test_scan_desc_layout_matches_c():
+    from sdreamer import _native as nat
+    S = nat.ScanDesc
+    probe = ["B", "eps", "seed", "seed_ptr", "group_offset", "W0", "WlT", "reset", "stoch", "dl", "work"]
+    fmt = " ".join(["%zu"] * (len(probe) + 1))
+    args = ", ".join(["sizeof(sd_rssm_scan)"] + [f"offsetof(sd_rssm_scan, {f})" for f in probe])
+    src = f'#include <stdio.h>\n#include <stddef.h>\n#include "sdhip.h"\nint main(void){{printf("{fmt}", {args}); return 0;}}\n'
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        subprocess.run(["gcc", "-I", os.path.dirname(HEADER), c, "-o", exe], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
+    assert [int(x) for x in out] == [ctypes.sizeof(S)] + [getattr(S, f).offset for f in probe]
+
+
 def test_kernels_refuse_cpu_tensors():
     import torch
     from sdreamer import kernels as K
