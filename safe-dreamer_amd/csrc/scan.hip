@@ -106,89 +106,81 @@ constexpr int core_lds_floats() { return NW * NT * 256 + MR * 16 * NT; }
   const int l16 = lane & 15, q = lane >> 4;                \
   (void)l16; (void)q;
 
-// ------------------------------------------------------------------------------------------- prologue pieces
-// 32 threads per row (16 rows). x = sum_s slab[s] (+ bias) (+ add); y = silu(x * rsqrt(mean(x^2)+eps) * w) into the
-// LDS panel P (stride ldp). Rows >= M are zero. Saves x / y (row stride ldys) / r when the pointers are non-null.
-SD_DEV void pro_rms(const float* slab, int ks, long sstride, const float* bias, const float* add, int N, int M,
-                    const float* w, float eps, float* P, int ldp, float* sx, float* sy, long ldys, float* sr, int tid) {
-  const int row = tid >> 5, t32 = tid & 31;
-  const bool rv = row < M;
-  float ss = 0.f;
-  for (int c = 4 * t32; c < N; c += 128) {
-    f32x4 x = zero4();
-    if (rv) {
-      for (int s = 0; s < ks; ++s) x += ld4(slab + s * sstride + (long)row * N + c);
-      if (bias) x += ld4(bias + c);
-      if (add) x += ld4(add + (long)row * N + c);
-      if (sx) st4(sx + (long)row * N + c, x);
-    }
-    st4(P + row * ldp + c, x);
-    ss += x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
-  }
-  ss = group_sum<32>(ss);
-  const float r = rsqrtf(ss / (float)N + eps);
-  if (sr && rv && t32 == 0) sr[row] = r;
-  for (int c = 4 * t32; c < N; c += 128) {
-    const f32x4 x = ld4(P + row * ldp + c), wv = ld4(w + c);
-    f32x4 y;
+// ------------------------------------------------------------------------------------------- load helpers
+// Prologues use 32 threads per row (16 rows): thread t32 owns the float4 columns c = 4*t32 + 128*i. Every load a
+// launch needs is issued before the first use (compile-time trip counts, predicated), so a prologue costs one
+// memory round trip instead of one per slab / per column block.
+template <int NI>
+SD_DEV void ld_row(f32x4 (&v)[NI], const float* rowp, int N, bool rv, int t32) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) y[j] = rv ? siluf_(x[j] * r * wv[j]) : 0.f;
-    st4(P + row * ldp + c, y);
-    if (sy && rv) st4(sy + (long)row * ldys + c, y);
+  for (int i = 0; i < NI; ++i) {
+    const int c = 4 * t32 + 128 * i;
+    v[i] = (rv && c < N) ? ld4(rowp + c) : zero4();
   }
 }
-
-// RMSNorm+SiLU backward of full rows: dx = r (g - xh mean(g xh)), g = dy silu'(xh w) w, xh = x r.  dy, x: (M,N).
-// Result into P (stride ldp); saved to sdx when non-null.
-SD_DEV void pro_rms_bwd(const float* x, const float* rstd, const float* w, const float* dy, int N, int M, float* P,
-                        int ldp, float* sdx, int tid) {
-  const int row = tid >> 5, t32 = tid & 31;
-  const bool rv = row < M;
-  const float r = rv ? rstd[row] : 0.f;
-  float dot = 0.f;
-  for (int c = 4 * t32; c < N; c += 128) {
-    f32x4 g = zero4();
-    if (rv) {
-      const f32x4 xv = ld4(x + (long)row * N + c), wv = ld4(w + c), d = ld4(dy + (long)row * N + c);
+// sum of ks <= KS split-K slabs (fixed order)
+template <int NI, int KS>
+SD_DEV void ld_slabs(f32x4 (&v)[NI], const float* rowp, long sstride, int ks, int N, bool rv, int t32) {
+  f32x4 part[KS][NI];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float xh = xv[j] * r;
-        g[j] = d[j] * dsilu(xh * wv[j]) * wv[j];
-        dot += g[j] * xh;
-      }
-    }
-    st4(P + row * ldp + c, g);
-  }
-  dot = group_sum<32>(dot) / (float)N;
-  for (int c = 4 * t32; c < N; c += 128) {
-    f32x4 o = zero4();
-    if (rv) {
-      const f32x4 g = ld4(P + row * ldp + c), xv = ld4(x + (long)row * N + c);
+  for (int s = 0; s < KS; ++s)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = r * (g[j] - xv[j] * r * dot);
-      if (sdx) st4(sdx + (long)row * N + c, o);
+    for (int i = 0; i < NI; ++i) {
+      const int c = 4 * t32 + 128 * i;
+      part[s][i] = (rv && s < ks && c < N) ? ld4(rowp + s * sstride + c) : zero4();
     }
-    st4(P + row * ldp + c, o);
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    v[i] = part[0][i];
+#pragma unroll
+    for (int s = 1; s < KS; ++s) v[i] += part[s][i];
   }
 }
-
-// per-row sum of `tiles` partials part[i*16 + row] (fixed order per thread + fixed tree): 32 threads per row
-SD_DEV float row_partials(const float* part, int tiles, int tid) {
-  const int row = tid >> 5, t32 = tid & 31;
+// per-tile row partials part[i*16 + row], i < tiles <= 32*NP
+template <int NP>
+SD_DEV void ld_parts(float (&v)[NP], const float* part, int tiles, int row, int t32) {
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int i = t32 + 32 * j;
+    v[j] = i < tiles ? part[i * MR + row] : 0.f;
+  }
+}
+template <int NP>
+SD_DEV float sum_parts(const float (&v)[NP]) {
   float s = 0.f;
-  for (int i = t32; i < tiles; i += 32) s += part[i * MR + row];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) s += v[j];
   return group_sum<32>(s);
 }
+SD_DEV float sumsq4(f32x4 x) { return x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]; }
 
-// rows [0, M) of a (M, ld) global matrix, columns [0, N) -> LDS panel; rows >= M zero
-SD_DEV void pro_copy(const float* src, long ld, int N, int M, float* P, int ldp, int tid) {
-  const int row = tid >> 5, t32 = tid & 31;
-  for (int c = 4 * t32; c < N; c += 128) st4(P + row * ldp + c, row < M ? ld4(src + (long)row * ld + c) : zero4());
+// y = silu(x * r * w) (rows >= M -> 0), x already holds the row (incl. bias)
+template <int NI>
+SD_DEV float rms_silu_rows(f32x4 (&x)[NI], const f32x4 (&w)[NI], int N, float eps, bool rv, f32x4 (&y)[NI]) {
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) ss += sumsq4(x[i]);
+  ss = group_sum<32>(ss);
+  const float r = rsqrtf(ss / (float)N + eps);
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[i][j] = rv ? siluf_(x[i][j] * r * w[i][j]) : 0.f;
+  return r;
+}
+
+template <int NI>
+SD_DEV void st_row(float* rowp, const f32x4 (&v)[NI], int N, int t32) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int c = 4 * t32 + 128 * i;
+    if (c < N) st4(rowp + c, v[i]);
+  }
 }
 
 // ------------------------------------------------------------------------------------------- scratch layout
 struct Work {
-  float *x0s, *x1s, *ops, *ssh, *dotp, *dxs, *dhin, *gq, *cs, *ch;
+  float *x0s, *x1s, *ops, *ssh, *dotp, *dxs, *dhin, *gq, *ch;
   long total;
 };
 long al64(long n) { return (n + 63) / 64 * 64; }
@@ -205,11 +197,14 @@ Work work_layout(const sd_rssm_scan& d, float* base) {
   w.dxs = take((long)d.G * d.B * 3 * d.U);
   w.dhin = take((long)d.B * d.D);
   w.gq = take((long)d.B * d.D);
-  w.cs = take((long)d.B * d.SK);
   w.ch = take((long)d.B * d.D);
   w.total = o;
   return w;
 }
+
+constexpr int UH = 256;        // hidden width of the fused path (base.yaml: hidden 256)
+constexpr int NU = UH / 128;   // float4 columns per prologue thread over a hidden row
+constexpr int KSM = 4;         // max split-K slabs
 
 // ------------------------------------------------------------------------------------------- forward kernels
 struct SlabProb {
@@ -231,16 +226,14 @@ __global__ __launch_bounds__(NTHR) void k_slab(SlabProb p0, SlabProb p1, int M, 
   Core<1, CPW> core;
   const float* wt[1] = {p.W + (long)(n0 + l16) * p.ldw + kb};
   core.load_b(wt, nch, wave, q);
+  const int erow = tid >> 4;
+  const bool masked = tid < 256 && erow < M && p.mask && p.mask[erow];
   core.run_glb(p.A + kb, p.lda, M, nch, wave, l16, q);
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
-  if (tid < 256) {
-    const int row = tid >> 4, c = tid & 15;
-    if (row < M) {
-      float v = C[row * 16 + c];
-      if (p.mask && p.mask[row]) v = 0.f;
-      p.out[(long)s * M * N + (long)row * N + n0 + c] = v;
-    }
+  if (tid < 256 && erow < M) {
+    const int c = tid & 15;
+    p.out[(long)s * M * N + (long)erow * N + n0 + c] = masked ? 0.f : C[erow * 16 + c];
   }
 }
 
@@ -261,46 +254,71 @@ __global__ void k_init(sd_rssm_scan d) {
 
 // hp[t] = BlockLinear(dyn_hid_0)([h_g | x0 | x1 | x2]) + bh, with x0 = silu(rms(x0p)), x1 = silu(rms(x1p)) built
 // in the prologue (rssm.py:52-63). grid (D/16); also the per-tile row sums of hp^2 for the next norm.
-template <int CPW>
+template <int CPW, int NG>
 __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_THREAD_IDS
-  const int B = d.B, U = d.U, D = d.D, Dg = D / d.G, Ig = Dg + 3 * U, ldp = Ig + 4;
+  const int B = d.B, D = d.D, Dg = D / d.G, Ig = Dg + 3 * UH, ldp = Ig + 4;
   const int tile = blockIdx.x, n0 = tile * 16, g = n0 / Dg;
   Core<1, CPW> core;
   const float* wt[1] = {d.Wh + (long)(n0 + l16) * Ig};
   core.load_b(wt, Ig / 16, wave, q);
-  float* P = smem + core_lds_floats<1>();
-  const long tBU = (long)t * B * U;
-  pro_copy(d.h_in + (long)t * B * D + (long)g * Dg, D, Dg, B, P, ldp, tid);
-  pro_rms(w.x0s, d.ks_d, (long)B * U, d.b0, nullptr, U, B, d.n0, d.eps, P + Dg, ldp,
-          tile == 0 ? d.x0p + tBU : nullptr, tile == 0 ? d.xcat + 3 * tBU : nullptr, 3 * U,
-          tile == 0 ? d.r0 + (long)t * B : nullptr, tid);
-  pro_rms(w.x1s, d.ks_s, (long)B * U, d.b1, nullptr, U, B, d.n1, d.eps, P + Dg + U, ldp,
-          tile == 1 ? d.x1p + tBU : nullptr, tile == 1 ? d.xcat + 3 * tBU + U : nullptr, 3 * U,
-          tile == 1 ? d.r1 + (long)t * B : nullptr, tid);
-  pro_copy(d.x2 + tBU, U, U, B, P + Dg + 2 * U, ldp, tid);
-  if (tile == 2) {
-    const int row = tid >> 5, t32 = tid & 31;
-    if (row < B)
-      for (int c = 4 * t32; c < U; c += 128) st4(d.xcat + 3 * tBU + (long)row * 3 * U + 2 * U + c, ld4(P + row * ldp + Dg + 2 * U + c));
+  const int row = tid >> 5, t32 = tid & 31;
+  const bool rv = row < B;
+  const long tBU = (long)t * B * UH;
+  f32x4 h[NG], x0[NU], x1[NU], x2v[NU], b0v[NU], b1v[NU], n0v[NU], n1v[NU];
+  ld_row(h, d.h_in + (long)t * B * D + (long)row * D + (long)g * Dg, Dg, rv, t32);
+  ld_slabs<NU, KSM>(x0, w.x0s + (long)row * UH, (long)B * UH, d.ks_d, UH, rv, t32);
+  ld_slabs<NU, KSM>(x1, w.x1s + (long)row * UH, (long)B * UH, d.ks_s, UH, rv, t32);
+  ld_row(x2v, d.x2 + tBU + (long)row * UH, UH, rv, t32);
+  ld_row(b0v, d.b0, UH, true, t32);
+  ld_row(b1v, d.b1, UH, true, t32);
+  ld_row(n0v, d.n0, UH, true, t32);
+  ld_row(n1v, d.n1, UH, true, t32);
+  const float bhv = d.bh[n0 + (tid & 15)];
+#pragma unroll
+  for (int i = 0; i < NU; ++i) {
+    x0[i] += b0v[i];
+    x1[i] += b1v[i];
+  }
+  f32x4 y0[NU], y1[NU];
+  const float r0 = rms_silu_rows(x0, n0v, UH, d.eps, rv, y0);
+  const float r1 = rms_silu_rows(x1, n1v, UH, d.eps, rv, y1);
+  float* P = smem + core_lds_floats<1>() + row * ldp;
+  st_row(P, h, Dg, t32);
+  st_row(P + Dg, y0, UH, t32);
+  st_row(P + Dg + UH, y1, UH, t32);
+  st_row(P + Dg + 2 * UH, x2v, UH, t32);
+  if (rv && tile < 3) {
+    float* xc = d.xcat + 3 * tBU + (long)row * 3 * UH;
+    if (tile == 0) {
+      st_row(d.x0p + tBU + (long)row * UH, x0, UH, t32);
+      st_row(xc, y0, UH, t32);
+      if (t32 == 0) d.r0[(long)t * B + row] = r0;
+    } else if (tile == 1) {
+      st_row(d.x1p + tBU + (long)row * UH, x1, UH, t32);
+      st_row(xc + UH, y1, UH, t32);
+      if (t32 == 0) d.r1[(long)t * B + row] = r1;
+    } else {
+      st_row(xc + 2 * UH, x2v, UH, t32);
+    }
   }
   __syncthreads();
-  core.run_lds(P, ldp, Ig / 16, wave, l16, q);
+  core.run_lds(smem + core_lds_floats<1>(), ldp, Ig / 16, wave, l16, q);
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
   if (tid < 256) {
-    const int row = tid >> 4, c = tid & 15;
-    const float v = C[row * 16 + c] + d.bh[n0 + c];
-    if (row < B) d.hp[(long)t * B * D + (long)row * D + n0 + c] = v;
-    const float ss = group_sum<16>(row < B ? v * v : 0.f);
-    if (c == 0) w.ssh[tile * MR + row] = ss;
+    const int er = tid >> 4, c = tid & 15;
+    const float v = C[er * 16 + c] + bhv;
+    if (er < B) d.hp[(long)t * B * D + (long)er * D + n0 + c] = v;
+    const float ss = group_sum<16>(er < B ? v * v : 0.f);
+    if (c == 0) w.ssh[tile * MR + er] = ss;
   }
 }
 
 // gates = BlockLinear(dyn_gru)(silu(rms(hp))) + bg; deter = GRU(gates, h_in) (rssm.py:65-75); h_in[t+1] masked.
 // grid (D/16): workgroup = 16 deter columns of one block, with their r / c / u gate rows (3 tiles).
-template <int CPW>
+template <int CPW, int NG>
 __global__ __launch_bounds__(NTHR) void k_gate(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_THREAD_IDS
@@ -310,178 +328,240 @@ __global__ __launch_bounds__(NTHR) void k_gate(sd_rssm_scan d, Work w, int t) {
   const float* wg = d.Wg + (long)g * 3 * Dg * Dg;
   const float* wt[3] = {wg + (long)(j0 + l16) * Dg, wg + (long)(Dg + j0 + l16) * Dg, wg + (long)(2 * Dg + j0 + l16) * Dg};
   core.load_b(wt, Dg / 16, wave, q);
-  float* P = smem + core_lds_floats<3>();
-  {
-    const int row = tid >> 5, t32 = tid & 31;
-    const float ss = row_partials(w.ssh, D / 16, tid);
-    const float r = rsqrtf(ss / (float)D + d.eps);
-    const bool rv = row < B;
-    if (rv && t32 == 0 && tile == 0) d.rh[(long)t * B + row] = r;
-    const float* hrow = d.hp + (long)t * B * D + (long)row * D + (long)g * Dg;
-    float* hhrow = d.hh + (long)t * B * D + (long)row * D + (long)g * Dg;
-    for (int c = 4 * t32; c < Dg; c += 128) {
-      f32x4 y = zero4();
-      if (rv) {
-        const f32x4 x = ld4(hrow + c), wv = ld4(d.nh + (long)g * Dg + c);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) y[j] = siluf_(x[j] * r * wv[j]);
-        if (j0 == 0) st4(hhrow + c, y);
-      }
-      st4(P + row * ldp + c, y);
-    }
+  const int row = tid >> 5, t32 = tid & 31;
+  const bool rv = row < B;
+  float pv[8];
+  ld_parts(pv, w.ssh, D / 16, row, t32);
+  f32x4 hv[NG], nv[NG];
+  ld_row(hv, d.hp + (long)t * B * D + (long)row * D + (long)g * Dg, Dg, rv, t32);
+  ld_row(nv, d.nh + (long)g * Dg, Dg, true, t32);
+  // epilogue operands (thread = (row er, column c))
+  const int er = (tid >> 4) & 15, c = tid & 15, j = j0 + c, col = n0 + c;
+  const bool ev = tid < 256 && er < B;
+  const float* bg = d.bg + (long)g * 3 * Dg;
+  float bra = 0.f, bca = 0.f, bua = 0.f, hprev = 0.f;
+  bool rnext = false;
+  if (ev) {
+    bra = bg[j];
+    bca = bg[Dg + j];
+    bua = bg[2 * Dg + j];
+    hprev = d.h_in[(long)t * B * D + (long)er * D + col];
+    rnext = t + 1 < d.T && d.reset[(t + 1) * B + er];
   }
+  const float r = rsqrtf(sum_parts(pv) / (float)D + d.eps);
+  if (rv && t32 == 0 && tile == 0) d.rh[(long)t * B + row] = r;
+  f32x4 y[NG];
+#pragma unroll
+  for (int i = 0; i < NG; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) y[i][k] = rv ? siluf_(hv[i][k] * r * nv[i][k]) : 0.f;
+  st_row(smem + core_lds_floats<3>() + row * ldp, y, Dg, t32);
+  if (rv && j0 == 0) st_row(d.hh + (long)t * B * D + (long)row * D + (long)g * Dg, y, Dg, t32);
   __syncthreads();
-  core.run_lds(P, ldp, Dg / 16, wave, l16, q);
+  core.run_lds(smem + core_lds_floats<3>(), ldp, Dg / 16, wave, l16, q);
   float* C = smem + NW * 3 * 256;
   core.reduce(smem, C, tid, wave, lane);
-  if (tid < 256) {
-    const int row = tid >> 4, c = tid & 15;
-    if (row < B) {
-      const int j = j0 + c, col = n0 + c;
-      const float* bg = d.bg + (long)g * 3 * Dg;
-      const float ra = C[row * 48 + c] + bg[j];
-      const float ca = C[row * 48 + 16 + c] + bg[Dg + j];
-      const float ua = C[row * 48 + 32 + c] + bg[2 * Dg + j];
-      float* gr = d.gates + (long)t * B * 3 * D + (long)row * 3 * D + (long)g * 3 * Dg;
-      gr[j] = ra;
-      gr[Dg + j] = ca;
-      gr[2 * Dg + j] = ua;
-      const float rs = sigmoidf_(ra);
-      const float cc = tanhf(rs * ca);
-      const float u = sigmoidf_(ua - 1.f);
-      const float h = d.h_in[(long)t * B * D + (long)row * D + col];
-      const float out = u * cc + (1.f - u) * h;
-      d.deter[(long)t * B * D + (long)row * D + col] = out;
-      if (t + 1 < d.T) d.h_in[(long)(t + 1) * B * D + (long)row * D + col] = d.reset[(t + 1) * B + row] ? 0.f : out;
-    }
+  if (ev) {
+    const float ra = C[er * 48 + c] + bra;
+    const float ca = C[er * 48 + 16 + c] + bca;
+    const float ua = C[er * 48 + 32 + c] + bua;
+    float* gr = d.gates + (long)t * B * 3 * D + (long)er * 3 * D + (long)g * 3 * Dg;
+    gr[j] = ra;
+    gr[Dg + j] = ca;
+    gr[2 * Dg + j] = ua;
+    const float rs = sigmoidf_(ra);
+    const float cc = tanhf(rs * ca);
+    const float u = sigmoidf_(ua - 1.f);
+    const float out = u * cc + (1.f - u) * hprev;
+    d.deter[(long)t * B * D + (long)er * D + col] = out;
+    if (t + 1 < d.T) d.h_in[(long)(t + 1) * B * D + (long)er * D + col] = rnext ? 0.f : out;
   }
 }
 
 // logits = obs_net_logit(silu(rms(op))) and the straight-through unimix one-hot sample (rssm.py:172-177,
 // distributions.py:16-33); op = sum of the obs_net_0 slabs + (embed half + bias). grid (S): one categorical / WG.
-template <int CPW, int KD>
+template <int KD>
 __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_THREAD_IDS
-  constexpr int NT = KD / 16;
-  const int B = d.B, U = d.U, SK = d.SK, S = SK / KD, ldp = U + 4;
+  constexpr int NT = KD / 16, NE = (MR * KD + NTHR - 1) / NTHR;
+  const int B = d.B, SK = d.SK, S = SK / KD, ldp = UH + 4;
   const int s = blockIdx.x, n0 = s * KD;
-  Core<NT, CPW> core;
+  Core<NT, 2> core;
   const float* wt[NT];
 #pragma unroll
-  for (int i = 0; i < NT; ++i) wt[i] = d.Wl + (long)(n0 + 16 * i + l16) * U;
-  core.load_b(wt, U / 16, wave, q);
-  float* P = smem + core_lds_floats<NT>();
-  const long tBU = (long)t * B * U;
-  const bool sv = s == 0;
-  pro_rms(w.ops, d.ks_d, (long)B * U, nullptr, d.eproj + tBU, U, B, d.no, d.eps, P, ldp, sv ? d.op + tBU : nullptr,
-          sv ? d.oo + tBU : nullptr, U, sv ? d.ro + (long)t * B : nullptr, tid);
+  for (int i = 0; i < NT; ++i) wt[i] = d.Wl + (long)(n0 + 16 * i + l16) * UH;
+  core.load_b(wt, UH / 16, wave, q);
+  const int row = tid >> 5, t32 = tid & 31;
+  const bool rv = row < B;
+  const long tBU = (long)t * B * UH;
+  f32x4 x[NU], e[NU], nv[NU];
+  ld_slabs<NU, KSM>(x, w.ops + (long)row * UH, (long)B * UH, d.ks_d, UH, rv, t32);
+  ld_row(e, d.eproj + tBU + (long)row * UH, UH, rv, t32);
+  ld_row(nv, d.no, UH, true, t32);
+  // sampler operands + noise, independent of the contraction
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+  float blv[NE], gn[NE];
+  bool rnext[NE];
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {
+    const int i = tid + NTHR * k, er = (i / KD) & 15, lt = i % KD;
+    blv[k] = d.bl[n0 + lt];
+    gn[k] = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)t, (uint64_t)((long)er * S + s + d.group_offset) * KD + lt);
+    rnext[k] = er < B && t + 1 < d.T && d.reset[(t + 1) * B + er];
+  }
+#pragma unroll
+  for (int i = 0; i < NU; ++i) x[i] += e[i];
+  f32x4 y[NU];
+  const float r = rms_silu_rows(x, nv, UH, d.eps, rv, y);
+  st_row(smem + core_lds_floats<NT>() + row * ldp, y, UH, t32);
+  if (rv && s == 0) {
+    st_row(d.op + tBU + (long)row * UH, x, UH, t32);
+    st_row(d.oo + tBU + (long)row * UH, y, UH, t32);
+    if (t32 == 0) d.ro[(long)t * B + row] = r;
+  }
   __syncthreads();
-  core.run_lds(P, ldp, U / 16, wave, l16, q);
+  core.run_lds(smem + core_lds_floats<NT>(), ldp, UH / 16, wave, l16, q);
   float* C = smem + NW * NT * 256;
   core.reduce(smem, C, tid, wave, lane);
-  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
-  for (int i = tid; i < MR * KD; i += NTHR) {  // team of KD lanes per (row, categorical)
-    const int row = i / KD, lt = i % KD;
-    const float l = C[row * KD + lt] + d.bl[n0 + lt];
-    float p, pp, nl;
-    unimix_forward<KD>(l, true, KD, d.unimix, p, pp, nl);
-    const float gn = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)t,
-                               (uint64_t)((long)row * S + s + d.group_offset) * KD + lt);
-    float ys;
-    int idx;
-    st_soft<KD>(nl, gn, true, ys, idx, lt);
-    if (row < B) {
-      const float y = ((lt == idx ? 1.f : 0.f) - ys) + ys;
-      const long o = (long)t * B * SK + (long)row * SK + n0 + lt;
-      d.logit[o] = l;
-      d.stoch[o] = y;
-      if (t + 1 < d.T) d.s_in[o + (long)B * SK] = d.reset[(t + 1) * B + row] ? 0.f : y;
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {  // team of KD lanes per (row, categorical)
+    const int i = tid + NTHR * k;
+    if (i < MR * KD) {
+      const int er = i / KD, lt = i % KD;
+      const float l = C[er * KD + lt] + blv[k];
+      float p, pp, nl;
+      unimix_forward<KD>(l, true, KD, d.unimix, p, pp, nl);
+      float ys;
+      int idx;
+      st_soft<KD>(nl, gn[k], true, ys, idx, lt);
+      if (er < B) {
+        const float yv = ((lt == idx ? 1.f : 0.f) - ys) + ys;
+        const long o = (long)t * B * SK + (long)er * SK + n0 + lt;
+        d.logit[o] = l;
+        d.stoch[o] = yv;
+        if (t + 1 < d.T) d.s_in[o + (long)B * SK] = rnext[k] ? 0.f : yv;
+      }
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------- backward kernels
-// dl = d_logit + ST-sampler backward(logit, d_stoch + carry_s) (prologue, noise recomputed);  d_o = dl . Wl.
-// grid (U/16)
-template <int CPW, int KD>
+// straight-through sampler backward of one categorical (team of KD lanes): d logits += d/dl <ds, y_soft>
+template <int KD>
+SD_DEV float sampler_bwd(float l, float gn, float ds, float unimix, int lt) {
+  float p, pp, nl;
+  unimix_forward<KD>(l, true, KD, unimix, p, pp, nl);
+  float ys;
+  int idx;
+  st_soft<KD>(nl, gn, true, ys, idx, lt);
+  const float sd = group_sum<KD>(ds * ys);
+  return unimix_backward<KD>(ys * (ds - sd), p, pp, nl, true, unimix);
+}
+
+// dl[T-1] = d_logit + sampler backward (no carry yet). Elementwise, teams of KD lanes.
+template <int KD>
+__global__ __launch_bounds__(256) void k_sbwd_last(sd_rssm_scan d) {
+  const int t = d.T - 1, SK = d.SK, S = SK / KD;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int row = (int)(i / SK), k = (int)(i % SK), lt = k % KD, s = k / KD;
+  const bool v = row < d.B;
+  const long o = (long)t * d.B * SK + (long)row * SK + k;
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+  const float l = v ? d.logit[o] : 0.f;
+  const float gn = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)t, (uint64_t)((long)row * S + s + d.group_offset) * KD + lt);
+  const float ds = v && d.d_stoch ? d.d_stoch[o] : 0.f;
+  const float dl = sampler_bwd<KD>(l, gn, ds, d.unimix, lt);
+  if (v) d.dl[o] = (d.d_logit ? d.d_logit[o] : 0.f) + dl;
+}
+
+// d_o = dl[t] . Wl   (dl built by the previous launch). grid (U/16)
+template <int CPW, int NS>
 __global__ __launch_bounds__(NTHR) void k_dlogit(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_THREAD_IDS
-  const int B = d.B, U = d.U, SK = d.SK, S = SK / KD, ldp = SK + 4;
+  const int B = d.B, SK = d.SK, ldp = SK + 4;
   const int n0 = blockIdx.x * 16;
   Core<1, CPW> core;
   const float* wt[1] = {d.WlT + (long)(n0 + l16) * SK};
   core.load_b(wt, SK / 16, wave, q);
-  float* P = smem + core_lds_floats<1>();
-  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
-  const long tBS = (long)t * B * SK;
-  for (int i = tid; i < MR * SK; i += NTHR) {
-    const int row = i / SK, k = i % SK, lt = k % KD, s = k / KD;
-    const bool rv = row < B;
-    const long o = tBS + (long)row * SK + k;
-    const float l = rv ? d.logit[o] : 0.f;
-    float p, pp, nl;
-    unimix_forward<KD>(l, true, KD, d.unimix, p, pp, nl);
-    const float gn = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)t,
-                               (uint64_t)((long)row * S + s + d.group_offset) * KD + lt);
-    float ys;
-    int idx;
-    st_soft<KD>(nl, gn, true, ys, idx, lt);
-    const float ds = rv ? (d.d_stoch ? d.d_stoch[o] : 0.f) + w.cs[(long)row * SK + k] : 0.f;
-    const float sd = group_sum<KD>(ds * ys);
-    const float dlv = unimix_backward<KD>(ys * (ds - sd), p, pp, nl, true, d.unimix);
-    const float v = rv ? (d.d_logit ? d.d_logit[o] : 0.f) + dlv : 0.f;
-    P[row * ldp + k] = v;
-    if (rv && blockIdx.x == 0) d.dl[o] = v;
-  }
+  const int row = tid >> 5, t32 = tid & 31;
+  f32x4 v[NS];
+  ld_row(v, d.dl + (long)t * B * SK + (long)row * SK, SK, row < B, t32);
+  st_row(smem + core_lds_floats<1>() + row * ldp, v, SK, t32);
   __syncthreads();
-  core.run_lds(P, ldp, SK / 16, wave, l16, q);
+  core.run_lds(smem + core_lds_floats<1>(), ldp, SK / 16, wave, l16, q);
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
   if (tid < 256) {
-    const int row = tid >> 4, c = tid & 15;
-    if (row < B) d.d_o[(long)t * B * U + (long)row * U + n0 + c] = C[row * 16 + c];
+    const int er = tid >> 4, c = tid & 15;
+    if (er < B) d.d_o[(long)t * B * UH + (long)er * UH + n0 + c] = C[er * 16 + c];
   }
 }
 
 // d_op = RMSNorm-SiLU backward (prologue); dh = d_deter + carry_h + d_op . Wo[:, :D]; GRU backward (epilogue).
 // grid (D/16)
-template <int CPW>
 __global__ __launch_bounds__(NTHR) void k_dgru(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_THREAD_IDS
-  const int B = d.B, U = d.U, D = d.D, Dg = D / d.G, ldp = U + 4;
+  const int B = d.B, D = d.D, Dg = D / d.G, ldp = UH + 4;
   const int tile = blockIdx.x, n0 = tile * 16;
-  Core<1, CPW> core;
-  const float* wt[1] = {d.WoDT + (long)(n0 + l16) * U};
-  core.load_b(wt, U / 16, wave, q);
-  float* P = smem + core_lds_floats<1>();
-  const long tBU = (long)t * B * U;
-  pro_rms_bwd(d.op + tBU, d.ro + (long)t * B, d.no, d.d_o + tBU, U, B, P, ldp, tile == 0 ? d.d_op + tBU : nullptr,
-              tid);
+  Core<1, 2> core;
+  const float* wt[1] = {d.WoDT + (long)(n0 + l16) * UH};
+  core.load_b(wt, UH / 16, wave, q);
+  const int row = tid >> 5, t32 = tid & 31;
+  const bool rv = row < B;
+  const long tBU = (long)t * B * UH;
+  f32x4 xv[NU], dy[NU], nv[NU];
+  ld_row(xv, d.op + tBU + (long)row * UH, UH, rv, t32);
+  ld_row(dy, d.d_o + tBU + (long)row * UH, UH, rv, t32);
+  ld_row(nv, d.no, UH, true, t32);
+  const float r = rv ? d.ro[(long)t * B + row] : 0.f;
+  // epilogue operands
+  const int er = (tid >> 4) & 15, c = tid & 15, col = n0 + c, g = col / Dg, j = col % Dg;
+  const bool ev = tid < 256 && er < B;
+  const long od = (long)t * B * D + (long)er * D + col;
+  const long gb = (long)t * B * 3 * D + (long)er * 3 * D + (long)g * 3 * Dg;
+  float dh0 = 0.f, ra = 0.f, ca = 0.f, ua = 0.f, hv = 0.f;
+  if (ev) {
+    dh0 = (d.d_deter ? d.d_deter[od] : 0.f) + w.ch[(long)er * D + col];
+    ra = d.gates[gb + j];
+    ca = d.gates[gb + Dg + j];
+    ua = d.gates[gb + 2 * Dg + j];
+    hv = d.h_in[od];
+  }
+  float dot = 0.f;
+  f32x4 gq[NU];
+#pragma unroll
+  for (int i = 0; i < NU; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float xh = xv[i][k] * r;
+      gq[i][k] = dy[i][k] * dsilu(xh * nv[i][k]) * nv[i][k];
+      dot += gq[i][k] * xh;
+    }
+  dot = group_sum<32>(dot) / (float)UH;
+  f32x4 o[NU];
+#pragma unroll
+  for (int i = 0; i < NU; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[i][k] = rv ? r * (gq[i][k] - xv[i][k] * r * dot) : 0.f;
+  st_row(smem + core_lds_floats<1>() + row * ldp, o, UH, t32);
+  if (rv && tile == 0) st_row(d.d_op + tBU + (long)row * UH, o, UH, t32);
   __syncthreads();
-  core.run_lds(P, ldp, U / 16, wave, l16, q);
+  core.run_lds(smem + core_lds_floats<1>(), ldp, UH / 16, wave, l16, q);
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
-  if (tid < 256) {
-    const int row = tid >> 4, c = tid & 15;
-    if (row < B) {
-      const int col = n0 + c, g = col / Dg, j = col % Dg;
-      const long od = (long)t * B * D + (long)row * D + col;
-      const float dh = (d.d_deter ? d.d_deter[od] : 0.f) + w.ch[(long)row * D + col] + C[row * 16 + c];
-      const long gb = (long)t * B * 3 * D + (long)row * 3 * D + (long)g * 3 * Dg;
-      const float ra = d.gates[gb + j], ca = d.gates[gb + Dg + j], ua = d.gates[gb + 2 * Dg + j];
-      const float rs = sigmoidf_(ra);
-      const float cc = tanhf(rs * ca);
-      const float u = sigmoidf_(ua - 1.f);
-      const float hv = d.h_in[od];
-      const float dtc = dh * u * (1.f - cc * cc);
-      d.d_gates[gb + j] = dtc * ca * rs * (1.f - rs);
-      d.d_gates[gb + Dg + j] = dtc * rs;
-      d.d_gates[gb + 2 * Dg + j] = dh * (cc - hv) * u * (1.f - u);
-      w.dhin[(long)row * D + col] = dh * (1.f - u);
-    }
+  if (ev) {
+    const float dh = dh0 + C[er * 16 + c];
+    const float rs = sigmoidf_(ra);
+    const float cc = tanhf(rs * ca);
+    const float u = sigmoidf_(ua - 1.f);
+    const float dtc = dh * u * (1.f - cc * cc);
+    d.d_gates[gb + j] = dtc * ca * rs * (1.f - rs);
+    d.d_gates[gb + Dg + j] = dtc * rs;
+    d.d_gates[gb + 2 * Dg + j] = dh * (cc - hv) * u * (1.f - u);
+    w.dhin[(long)er * D + col] = dh * (1.f - u);
   }
 }
 
@@ -496,34 +576,39 @@ __global__ __launch_bounds__(NTHR) void k_dhh(sd_rssm_scan d, Work w, int t) {
   Core<1, CPW> core;
   const float* wt[1] = {d.WgT + ((long)g * Dg + j0 + l16) * 3 * Dg};
   core.load_b(wt, 3 * Dg / 16, wave, q);
+  const int er = (tid >> 4) & 15, c = tid & 15, col = n0 + c;
+  const bool ev = tid < 256 && er < B;
+  const long o = (long)t * B * D + (long)er * D + col;
+  float xh = 0.f, wv = 0.f;
+  if (ev) {
+    xh = d.hp[o] * d.rh[(long)t * B + er];
+    wv = d.nh[col];
+  }
   core.run_glb(d.d_gates + (long)t * B * 3 * D + (long)g * 3 * Dg, 3 * (long)D, B, 3 * Dg / 16, wave, l16, q);
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
   if (tid < 256) {
-    const int row = tid >> 4, c = tid & 15, col = n0 + c;
     float part = 0.f;
-    if (row < B) {
-      const float dy = C[row * 16 + c];
-      const long o = (long)t * B * D + (long)row * D + col;
+    if (ev) {
+      const float dy = C[er * 16 + c];
       d.d_hh[o] = dy;
-      const float xh = d.hp[o] * d.rh[(long)t * B + row], wv = d.nh[col];
       const float gq = dy * dsilu(xh * wv) * wv;
-      w.gq[(long)row * D + col] = gq;
+      w.gq[(long)er * D + col] = gq;
       part = gq * xh;
     }
     part = group_sum<16>(part);
-    if (c == 0) w.dotp[tile * MR + row] = part;
+    if (c == 0) w.dotp[tile * MR + er] = part;
   }
 }
 
 // d_hp_g = RMSNorm backward (prologue, from g*w and the row partials); then two problems in one grid:
 //   P0: d_xcat slab g = d_hp_g . Wsh[g-rows]   ((3U/16) * G workgroups)
 //   P1: d_hin[:, g] += d_hp_g . Wbd[g]          (D/16 workgroups)
-template <int CPW>
+template <int CPW, int NG>
 __global__ __launch_bounds__(NTHR) void k_dhp(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_THREAD_IDS
-  const int B = d.B, U = d.U, D = d.D, Dg = D / d.G, ldp = Dg + 4, X = 3 * U;
+  const int B = d.B, D = d.D, Dg = D / d.G, ldp = Dg + 4, X = 3 * UH;
   const int NX = (X / 16) * d.G;
   const int blk = blockIdx.x;
   const bool p0 = blk < NX;
@@ -541,97 +626,133 @@ __global__ __launch_bounds__(NTHR) void k_dhp(sd_rssm_scan d, Work w, int t) {
   Core<1, CPW> core;
   const float* wt[1] = {wrow};
   core.load_b(wt, Dg / 16, wave, q);
-  float* P = smem + core_lds_floats<1>();
-  {
-    const int row = tid >> 5, t32 = tid & 31;
-    const float dot = row_partials(w.dotp, D / 16, tid) / (float)D;
-    const bool rv = row < B;
-    const float r = rv ? d.rh[(long)t * B + row] : 0.f;
-    const bool save = !p0 && (n0 % Dg) == 0;
-    for (int c = 4 * t32; c < Dg; c += 128) {
-      f32x4 o = zero4();
-      if (rv) {
-        const long ob = (long)row * D + (long)g * Dg + c;
-        const f32x4 gq = ld4(w.gq + ob), x = ld4(d.hp + (long)t * B * D + ob);
+  const int row = tid >> 5, t32 = tid & 31;
+  const bool rv = row < B;
+  float pv[8];
+  ld_parts(pv, w.dotp, D / 16, row, t32);
+  const long ob = (long)row * D + (long)g * Dg;
+  f32x4 gq[NG], xv[NG];
+  ld_row(gq, w.gq + ob, Dg, rv, t32);
+  ld_row(xv, d.hp + (long)t * B * D + ob, Dg, rv, t32);
+  const float r = rv ? d.rh[(long)t * B + row] : 0.f;
+  const int er = (tid >> 4) & 15, c = tid & 15;
+  const bool ev = tid < 256 && er < B;
+  const float dh_old = (!p0 && ev) ? w.dhin[(long)er * D + n0 + c] : 0.f;
+  const float dot = sum_parts(pv) / (float)D;
+  f32x4 o[NG];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = r * (gq[j] - x[j] * r * dot);
-        if (save) st4(d.d_hp + (long)t * B * D + ob, o);
-      }
-      st4(P + row * ldp + c, o);
-    }
-  }
+  for (int i = 0; i < NG; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[i][k] = rv ? r * (gq[i][k] - xv[i][k] * r * dot) : 0.f;
+  st_row(smem + core_lds_floats<1>() + row * ldp, o, Dg, t32);
+  if (rv && !p0 && (n0 % Dg) == 0) st_row(d.d_hp + (long)t * B * D + ob, o, Dg, t32);
   __syncthreads();
-  core.run_lds(P, ldp, Dg / 16, wave, l16, q);
+  core.run_lds(smem + core_lds_floats<1>(), ldp, Dg / 16, wave, l16, q);
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
-  if (tid < 256) {
-    const int row = tid >> 4, c = tid & 15;
-    if (row < B) {
-      if (p0) w.dxs[(long)g * B * X + (long)row * X + n0 + c] = C[row * 16 + c];
-      else w.dhin[(long)row * D + n0 + c] += C[row * 16 + c];
-    }
+  if (ev) {
+    if (p0) w.dxs[(long)g * B * X + (long)er * X + n0 + c] = C[er * 16 + c];
+    else w.dhin[(long)er * D + n0 + c] = dh_old + C[er * 16 + c];
   }
 }
 
 // d_xcat = sum over blocks of the slabs; d_x0p / d_x1p = RMSNorm-SiLU backward of the _dyn_in0 / _dyn_in1 norms.
-// grid (B): one workgroup per row; waves 0-3 take x0, waves 4-7 x1.
+// grid (B): one workgroup per row; waves 0-3 take x0, waves 4-7 x1 (one column per thread).
 __global__ __launch_bounds__(NTHR) void k_dx01(sd_rssm_scan d, Work w, int t) {
   __shared__ float red[NW];
-  extern __shared__ float smem[];
+  __shared__ float dx[3 * UH];
+  constexpr int X = 3 * UH, NC = (X + NTHR - 1) / NTHR, GM = 8;
   const int tid = threadIdx.x, wave = tid >> 6;
-  const int B = d.B, U = d.U, X = 3 * U, b = blockIdx.x;
+  const int B = d.B, b = blockIdx.x;
   const long tB = (long)t * B;
-  float* dx = smem;
-  for (int c = tid; c < X; c += NTHR) {
-    float v = 0.f;
-    for (int g = 0; g < d.G; ++g) v += w.dxs[(long)g * B * X + (long)b * X + c];
-    dx[c] = v;
-    d.d_xcat[(tB + b) * X + c] = v;
+  float part[GM][NC];
+#pragma unroll
+  for (int g = 0; g < GM; ++g)
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = tid + NTHR * k;
+      part[g][k] = (g < d.G && c < X) ? w.dxs[(long)g * B * X + (long)b * X + c] : 0.f;
+    }
+  const int half = wave >> 2, ht = tid & 255;
+  const float* x = (half ? d.x1p : d.x0p) + (tB + b) * UH;
+  const float xv = x[ht], wv = (half ? d.n1 : d.n0)[ht];
+  const float r = (half ? d.r1 : d.r0)[tB + b];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    const int c = tid + NTHR * k;
+    float v = part[0][k];
+#pragma unroll
+    for (int g = 1; g < GM; ++g) v += part[g][k];
+    if (c < X) {
+      dx[c] = v;
+      d.d_xcat[(tB + b) * X + c] = v;
+    }
   }
   __syncthreads();
-  const int half = wave >> 2, ht = tid & 255;
-  const float* x = (half ? d.x1p : d.x0p) + (tB + b) * U;
-  const float* wn = half ? d.n1 : d.n0;
-  const float r = (half ? d.r1 : d.r0)[tB + b];
-  float* out = (half ? d.d_x1p : d.d_x0p) + (tB + b) * U;
-  float dot = 0.f;
-  for (int c = ht; c < U; c += 256) {
-    const float xh = x[c] * r, wv = wn[c];
-    const float gg = dx[half * U + c] * dsilu(xh * wv) * wv;
-    dx[X + half * U + c] = gg;
-    dot += gg * xh;
-  }
-  dot = wave_sum(dot);
+  const float xh = xv * r;
+  const float gg = dx[half * UH + ht] * dsilu(xh * wv) * wv;
+  float dot = wave_sum(gg * xh);
   if ((tid & 63) == 0) red[wave] = dot;
   __syncthreads();
-  dot = (red[4 * half] + red[4 * half + 1] + red[4 * half + 2] + red[4 * half + 3]) / (float)U;
-  for (int c = ht; c < U; c += 256) out[c] = r * (dx[X + half * U + c] - x[c] * r * dot);
+  dot = (red[4 * half] + red[4 * half + 1] + red[4 * half + 2] + red[4 * half + 3]) / (float)UH;
+  ((half ? d.d_x1p : d.d_x0p) + (tB + b) * UH)[ht] = r * (gg - xh * dot);
 }
 
-// carry_h = mask(d_hin + d_x0p . W0), carry_s = mask(d_x1p . W1) for step t-1 (rssm.py:161-165 backward).
-// grid (D/16 + SK/16)
-template <int CPW>
+// carry_h = mask(d_hin + d_x0p . W0) and carry_s = mask(d_x1p . W1) into step t-1 (rssm.py:161-165 backward); the
+// carry_s workgroups (one categorical each) then run the sampler backward of step t-1:
+// dl[t-1] = d_logit[t-1] + ST-backward(logit[t-1], d_stoch[t-1] + carry_s). grid (D/KD + S)
+template <int KD>
 __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_THREAD_IDS
-  const int B = d.B, U = d.U, D = d.D, SK = d.SK;
-  const bool p0 = (int)blockIdx.x < D / 16;
-  const int n0 = p0 ? blockIdx.x * 16 : (blockIdx.x - D / 16) * 16;
-  Core<1, CPW> core;
-  const float* wt[1] = {(p0 ? d.W0T : d.W1T) + (long)(n0 + l16) * U};
-  core.load_b(wt, U / 16, wave, q);
-  core.run_glb((p0 ? d.d_x0p : d.d_x1p) + (long)t * B * U, U, B, U / 16, wave, l16, q);
-  float* C = smem + NW * 256;
+  constexpr int NT = KD / 16, NE = (MR * KD + NTHR - 1) / NTHR;
+  const int B = d.B, D = d.D, SK = d.SK, S = SK / KD;
+  const bool p0 = (int)blockIdx.x < D / KD;
+  const int n0 = (p0 ? blockIdx.x : blockIdx.x - D / KD) * KD;
+  Core<NT, 2> core;
+  const float* wt[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) wt[i] = (p0 ? d.W0T : d.W1T) + (long)(n0 + 16 * i + l16) * UH;
+  core.load_b(wt, UH / 16, wave, q);
+  // epilogue operands: element i = (row er, column lt) of the 16 x KD tile
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+  const int tp = t - 1;
+  float e0[NE], e1[NE], e2[NE], gn[NE];
+  bool rs[NE];
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {
+    const int i = tid + NTHR * k, er = (i / KD) & 15, lt = i % KD;
+    const bool ev = i < MR * KD && er < B;
+    rs[k] = ev && d.reset[t * B + er];
+    e0[k] = e1[k] = e2[k] = gn[k] = 0.f;
+    if (p0) {
+      if (ev) e0[k] = w.dhin[(long)er * D + n0 + lt];
+    } else {
+      const long o = (long)tp * B * SK + (long)er * SK + n0 + lt;
+      if (ev) {
+        e0[k] = d.logit[o];
+        e1[k] = d.d_stoch ? d.d_stoch[o] : 0.f;
+        e2[k] = d.d_logit ? d.d_logit[o] : 0.f;
+      }
+      gn[k] = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)tp,
+                        (uint64_t)((long)er * S + n0 / KD + d.group_offset) * KD + lt);
+    }
+  }
+  core.run_glb((p0 ? d.d_x0p : d.d_x1p) + (long)t * B * UH, UH, B, UH / 16, wave, l16, q);
+  float* C = smem + NW * NT * 256;
   core.reduce(smem, C, tid, wave, lane);
-  if (tid < 256) {
-    const int row = tid >> 4, c = tid & 15;
-    if (row < B) {
-      const bool rs = d.reset[t * B + row] != 0;
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {
+    const int i = tid + NTHR * k;
+    if (i < MR * KD) {
+      const int er = i / KD, lt = i % KD;
+      const bool ev = er < B;
       if (p0) {
-        const long o = (long)row * D + n0 + c;
-        w.ch[o] = rs ? 0.f : w.dhin[o] + C[row * 16 + c];
+        if (ev) w.ch[(long)er * D + n0 + lt] = rs[k] ? 0.f : e0[k] + C[er * KD + lt];
       } else {
-        w.cs[(long)row * SK + n0 + c] = rs ? 0.f : C[row * 16 + c];
+        const float cs = rs[k] ? 0.f : C[er * KD + lt];
+        const float dlv = sampler_bwd<KD>(e0[k], gn[k], ev ? e1[k] + cs : 0.f, d.unimix, lt);
+        if (ev) d.dl[(long)tp * B * SK + (long)er * SK + n0 + lt] = e2[k] + dlv;
       }
     }
   }
@@ -676,15 +797,24 @@ bool raise_lds(size_t bytes) {
 
 int check(const sd_rssm_scan* d) {
   if (!d) return SD_EARG;
-  if (d->B < 1 || d->B > MR || d->T < 1 || d->G < 1 || d->D % d->G) return SD_ESHAPE;
+  if (d->B < 1 || d->B > MR || d->T < 1 || d->G < 1 || d->G > 8 || d->D % d->G) return SD_ESHAPE;
   const int Dg = d->D / d->G;
-  if (d->U % 64 || Dg % 64 || d->SK % 64 || d->D % 64) return SD_ESHAPE;
+  if (d->U != UH || (Dg != 256 && Dg != 512) || (d->SK != 512 && d->SK != 1024) || d->D > 4096) return SD_ESHAPE;
   if (d->Kd != 16 && d->Kd != 32 && d->Kd != 64) return SD_ESHAPE;
-  if (d->SK % d->Kd) return SD_ESHAPE;
-  if (d->ks_d < 1 || d->ks_s < 1 || d->D % (d->ks_d * 16) || d->SK % (d->ks_s * 16)) return SD_ESHAPE;
+  if (d->SK % d->Kd || d->D % d->Kd) return SD_ESHAPE;
+  if (d->ks_d < 1 || d->ks_s < 1 || d->ks_d > KSM || d->ks_s > KSM || d->D % (d->ks_d * 16) ||
+      d->SK % (d->ks_s * 16))
+    return SD_ESHAPE;
   if (!d->work) return SD_EARG;
   return SD_OK;
 }
+
+#define SD_NG_SWITCH(dg, ...)                                 \
+  switch (dg) {                                               \
+    case 256: { constexpr int NG = 2; __VA_ARGS__; } break;   \
+    case 512: { constexpr int NG = 4; __VA_ARGS__; } break;   \
+    default: return SD_ESHAPE;                                \
+  }
 
 }  // namespace
 
@@ -699,51 +829,48 @@ extern "C" int sd_rssm_scan_fwd(const sd_rssm_scan* dp, sd_stream stream_) {
   hipStream_t st = (hipStream_t)stream_;
   const sd_rssm_scan& d = *dp;
   const Work w = work_layout(d, d.work);
-  const int B = d.B, U = d.U, D = d.D, SK = d.SK, Dg = D / d.G, Ig = Dg + 3 * U;
+  const int B = d.B, D = d.D, SK = d.SK, Dg = D / d.G, Ig = Dg + 3 * UH;
   const int span_d = D / d.ks_d, span_s = SK / d.ks_s;
-  const int cp_d = cpw_for(span_d), cp_s = cpw_for(span_s), cp_h = cpw_for(Ig), cp_g = cpw_for(Dg),
-            cp_u = cpw_for(U);
-  if (cp_d < 0 || cp_s < 0 || cp_h < 0 || cp_g < 0 || cp_u < 0) return SD_ESHAPE;
+  const int cp_d = cpw_for(span_d), cp_s = cpw_for(span_s), cp_h = cpw_for(Ig);
+  if (cp_d < 0 || cp_s < 0 || cp_h < 0) return SD_ESHAPE;
   const size_t core1 = core_lds_floats<1>() * 4;
   const size_t lds_hid = core1 + (size_t)MR * (Ig + 4) * 4;
   const size_t lds_gate = core_lds_floats<3>() * 4 + (size_t)MR * (Dg + 4) * 4;
-  const long BD = (long)B * D, BS = (long)B * SK, BU = (long)B * U;
+  const long BD = (long)B * D, BS = (long)B * SK;
 
   k_init<<<64, 256, 0, st>>>(d);
   SD_LAUNCH_CHECK();
   {  // x0p(0) = h_in[0] . W0^T
     SlabProb p{d.h_in, D, d.W0, D, w.x0s, nullptr};
-    SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(U / 16, d.ks_d, 1), NTHR, core1, st>>>(p, p, B, U, span_d));
+    SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, 1), NTHR, core1, st>>>(p, p, B, UH, span_d));
     SD_LAUNCH_CHECK();
   }
   for (int t = 0; t < d.T; ++t) {
     {
       SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr};
-      SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(U / 16, d.ks_s, 1), NTHR, core1, st>>>(p, p, B, U, span_s));
+      SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(UH / 16, d.ks_s, 1), NTHR, core1, st>>>(p, p, B, UH, span_s));
       SD_LAUNCH_CHECK();
     }
-    SD_CPW_SWITCH(cp_h, if (!raise_lds<k_hid<CP>>(lds_hid)) return SD_EARG;
-                  k_hid<CP><<<D / 16, NTHR, lds_hid, st>>>(d, w, t));
+    SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG>>(lds_hid))) return SD_EARG;
+                                   k_hid<CP, NG><<<D / 16, NTHR, lds_hid, st>>>(d, w, t)));
     SD_LAUNCH_CHECK();
-    SD_CPW_SWITCH(cp_g, if (!raise_lds<k_gate<CP>>(lds_gate)) return SD_EARG;
-                  k_gate<CP><<<D / 16, NTHR, lds_gate, st>>>(d, w, t));
+    SD_NG_SWITCH(Dg, if (!(raise_lds<k_gate<NG, NG>>(lds_gate))) return SD_EARG;
+                 k_gate<NG, NG><<<D / 16, NTHR, lds_gate, st>>>(d, w, t));
     SD_LAUNCH_CHECK();
     {
       SlabProb po{d.deter + t * BD, D, d.WoD, D, w.ops, nullptr};
       SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset + (t + 1) * B};
       const int np = t + 1 < d.T ? 2 : 1;
-      SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(U / 16, d.ks_d, np), NTHR, core1, st>>>(po, px, B, U, span_d));
+      SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, np), NTHR, core1, st>>>(po, px, B, UH, span_d));
       SD_LAUNCH_CHECK();
     }
     SD_KD_SWITCH(d.Kd, {
-      constexpr int NT = KD / 16;
-      const size_t lds = core_lds_floats<NT>() * 4 + (size_t)MR * (U + 4) * 4;
-      SD_CPW_SWITCH(cp_u, if (!(raise_lds<k_logit<CP, KD>>(lds))) return SD_EARG;
-                    k_logit<CP, KD><<<SK / KD, NTHR, lds, st>>>(d, w, t));
+      const size_t lds = core_lds_floats<KD / 16>() * 4 + (size_t)MR * (UH + 4) * 4;
+      if (!(raise_lds<k_logit<KD>>(lds))) return SD_EARG;
+      k_logit<KD><<<SK / KD, NTHR, lds, st>>>(d, w, t);
     });
     SD_LAUNCH_CHECK();
   }
-  (void)BU;
   return SD_OK;
 }
 
@@ -753,34 +880,38 @@ extern "C" int sd_rssm_scan_bwd(const sd_rssm_scan* dp, sd_stream stream_) {
   hipStream_t st = (hipStream_t)stream_;
   const sd_rssm_scan& d = *dp;
   const Work w = work_layout(d, d.work);
-  const int B = d.B, U = d.U, D = d.D, SK = d.SK, Dg = D / d.G;
-  const int cp_sk = cpw_for(SK), cp_u = cpw_for(U), cp_g3 = cpw_for(3 * Dg), cp_g = cpw_for(Dg);
-  if (cp_sk < 0 || cp_u < 0 || cp_g3 < 0 || cp_g < 0) return SD_ESHAPE;
+  const int B = d.B, D = d.D, SK = d.SK, Dg = D / d.G;
+  const int cp_g3 = cpw_for(3 * Dg);
+  if (cp_g3 < 0) return SD_ESHAPE;
   const size_t core1 = core_lds_floats<1>() * 4;
   const size_t lds_dl = core1 + (size_t)MR * (SK + 4) * 4;
-  const size_t lds_dgru = core1 + (size_t)MR * (U + 4) * 4;
+  const size_t lds_dgru = core1 + (size_t)MR * (UH + 4) * 4;
   const size_t lds_dhp = core1 + (size_t)MR * (Dg + 4) * 4;
-  const size_t lds_dx = (size_t)(3 * U + 2 * U) * 4;
-  hipError_t e = hipMemsetAsync(w.cs, 0, sizeof(float) * (size_t)B * SK, st);
+  hipError_t e = hipMemsetAsync(w.ch, 0, sizeof(float) * (size_t)B * D, st);
   if (e != hipSuccess) return (int)e;
-  e = hipMemsetAsync(w.ch, 0, sizeof(float) * (size_t)B * D, st);
-  if (e != hipSuccess) return (int)e;
-  const int NX = (3 * U / 16) * d.G;
+  const int NX = (3 * UH / 16) * d.G;
+  SD_KD_SWITCH(d.Kd, k_sbwd_last<KD><<<(int)(((long)B * SK + 255) / 256), 256, 0, st>>>(d));
+  SD_LAUNCH_CHECK();
   for (int t = d.T - 1; t >= 0; --t) {
-    SD_KD_SWITCH(d.Kd, SD_CPW_SWITCH(cp_sk, if (!(raise_lds<k_dlogit<CP, KD>>(lds_dl))) return SD_EARG;
-                                     k_dlogit<CP, KD><<<U / 16, NTHR, lds_dl, st>>>(d, w, t)));
+    if (SK == 512) {
+      if (!(raise_lds<k_dlogit<4, 4>>(lds_dl))) return SD_EARG;
+      k_dlogit<4, 4><<<UH / 16, NTHR, lds_dl, st>>>(d, w, t);
+    } else {
+      if (!(raise_lds<k_dlogit<8, 8>>(lds_dl))) return SD_EARG;
+      k_dlogit<8, 8><<<UH / 16, NTHR, lds_dl, st>>>(d, w, t);
+    }
     SD_LAUNCH_CHECK();
-    SD_CPW_SWITCH(cp_u, k_dgru<CP><<<D / 16, NTHR, lds_dgru, st>>>(d, w, t));
+    k_dgru<<<D / 16, NTHR, lds_dgru, st>>>(d, w, t);
     SD_LAUNCH_CHECK();
     SD_CPW_SWITCH(cp_g3, k_dhh<CP><<<D / 16, NTHR, core1, st>>>(d, w, t));
     SD_LAUNCH_CHECK();
-    SD_CPW_SWITCH(cp_g, if (!raise_lds<k_dhp<CP>>(lds_dhp)) return SD_EARG;
-                  k_dhp<CP><<<NX + D / 16, NTHR, lds_dhp, st>>>(d, w, t));
+    SD_NG_SWITCH(Dg, if (!(raise_lds<k_dhp<NG, NG>>(lds_dhp))) return SD_EARG;
+                 k_dhp<NG, NG><<<NX + D / 16, NTHR, lds_dhp, st>>>(d, w, t));
     SD_LAUNCH_CHECK();
-    k_dx01<<<B, NTHR, lds_dx, st>>>(d, w, t);
+    k_dx01<<<B, NTHR, 0, st>>>(d, w, t);
     SD_LAUNCH_CHECK();
     if (t > 0) {
-      SD_CPW_SWITCH(cp_u, k_carry<CP><<<D / 16 + SK / 16, NTHR, core1, st>>>(d, w, t));
+      SD_KD_SWITCH(d.Kd, k_carry<KD><<<D / KD + SK / KD, NTHR, core_lds_floats<KD / 16>() * 4, st>>>(d, w, t));
       SD_LAUNCH_CHECK();
     }
   }
