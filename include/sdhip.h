@@ -145,6 +145,10 @@ int sd_conv2d_fwd(const float* in, const float* w, const float* bias, float* out
 /* dw_db (Co, kh*kw*Ci + 1) = [dW | d bias]; ksplit > 1 needs workspace >= ksplit*Co*(kh*kw*Ci+1) floats */
 int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db, float* workspace, long ws_floats, int ksplit,
                     int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad, int ups, sd_stream stream);
+/* partial-slab count sd_conv2d_wgrad uses for this request (workspace >= slabs * Co * (kh*kw*Ci + 1) floats when
+ * slabs > 1): stride-1 convs with Co % 16 == 0 take a direct kernel (dy rows + input patch staged in LDS, no im2col
+ * re-reads) whose split is fixed by the library; others use `ksplit` over the im2col implicit GEMM. */
+int sd_conv2d_wgrad_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int ups, int ksplit);
 /* Wf[ci][ky][kx][co] = W[co][kh-1-ky][kw-1-kx][ci]  (input-gradient conv weights) */
 int sd_conv_flip_weight(const float* w, float* wf, int Co, int kh, int kw, int Ci, sd_stream stream);
 /* backward of nearest 2x upsample: din (Nb,H,W,C) = 2x2 sums of du (Nb,2H,2W,C) */
@@ -173,6 +177,9 @@ int sd_polyak(const float* src, float* dst, long n, float mix, sd_stream stream)
 /* ---------------------------------------------------------------- misc
  * Dreamer.preprocess + ConvEncoder's "-0.5": out = in/255 - shift (dreamer.py:710-713, networks.py:224) */
 int sd_u8_to_f32(const uint8_t* in, float* out, long n, float shift, sd_stream stream);
+/* NHWC channel pad + shift: out[p][c] = in[p][c] - shift (c < C), 0 (C <= c < Cp). The ConvEncoder input
+ * (obs - 0.5, networks.py:224) padded 3 -> 4 channels so the first conv takes the float4 / direct-wgrad paths. */
+int sd_pad_channels(const float* in, float* out, long pixels, int C, int Cp, float shift, sd_stream stream);
 /* symlog (distributions.py:8-9) for MLP-encoder inputs (networks.py:333-334) */
 int sd_symlog(const float* x, float* y, long n, sd_stream stream);
 int sd_fill_gumbel(float* out, long n, uint64_t seed, int stream_id, int step, long offset, sd_stream stream);

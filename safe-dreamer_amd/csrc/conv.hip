@@ -10,6 +10,8 @@
 //   bwd-data:   the same kernel on dOut with the flipped/transposed weight Wf[ci][ky][kx][co], pad' = k-1-pad
 //   bwd-weight: dW[co][k]  = sum_m dOut[m][co] im2col(m, k)   (+ a ones column -> d bias), split-K over pixels
 // `ups = 1` reads the input through a nearest 2x upsample (decoder) without materialising it.
+#include <stdlib.h>
+
 #include "gemm_core.h"
 #include "sdhip.h"
 
@@ -37,7 +39,7 @@ SD_DEV bool tap(const Geom& G, int n, int y, int x, int k, long& off) {
 // A operand of fwd / bwd-data: rows = output pixels, k = (ky, kx, ci) contiguous in ci.
 template <int ROWS, bool VEC>
 struct Im2colRows {
-  static constexpr int NV = ROWS * BK / 4 / 256 > 0 ? ROWS * BK / 4 / 256 : 1;
+  static constexpr int NV = (ROWS * BK / 4 + 255) / 256;
   Geom G;
   int pn[NV], py[NV], px[NV];
   f32x4 r[NV];
@@ -84,7 +86,7 @@ struct Im2colRows {
 // B operand of bwd-weight: rows = j = (ky, kx, ci) (+ one ones-row at j == J for the bias), k = pixel.
 template <int ROWS, bool VEC>
 struct Im2colCols {
-  static constexpr int NV = ROWS * BK / 4 / 256 > 0 ? ROWS * BK / 4 / 256 : 1;
+  static constexpr int NV = (ROWS * BK / 4 + 255) / 256;
   Geom G;
   int J, row0;
   TileLoader<ROWS, false, false> st;
@@ -121,6 +123,316 @@ struct Im2colCols {
   }
   SD_DEV void store(float* lds) const { st.store(lds); }
 };
+
+// ---------------------------------------------------------------- tap-table loaders (C % 4 == 0, pow2 grid)
+// The k -> (ky, kx, ci) decode of the implicit-GEMM A operand is table-driven: each workgroup writes one packed
+// int per 4 k's into LDS (ci | ky << 16 | kx << 24) before its first tile, so a float4 of the im2col row costs an
+// LDS read, two compares and an address instead of two runtime integer divisions.
+constexpr int MAX_TAPQ = 512;  // K <= 2048
+constexpr int NW_D = 8;        // waves of the direct bwd-weight kernel
+
+SD_DEV void build_taps(int* tab, const Geom& G, int K) {
+  for (int kq = threadIdx.x; kq < K / 4; kq += blockDim.x) {
+    const int k = 4 * kq, t = k / G.C, c = k - t * G.C;
+    const int ky = t / G.kw, kx = t - ky * G.kw;
+    tab[kq] = c | (ky << 16) | (kx << 24);
+  }
+  __syncthreads();
+}
+
+template <int ROWS>
+struct Im2colRowsT {
+  static constexpr int NV = (ROWS * BK / 4 + 255) / 256;
+  Geom G;
+  const int* tab;
+  int py[NV], px[NV];
+  long pbase[NV];  // n * Hs (row index base) or -1
+  TileLoader<ROWS, true, false> st;
+  SD_DEV Im2colRowsT(const Geom& g, const int* tab_, int M, int row0, int lw, int lhw) : G(g), tab(tab_) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      const int m = row0 + i / (BK / 4);
+      pbase[v] = -1;
+      if (i < ROWS * BK / 4 && m < M) {
+        const int n = m >> lhw, rem = m & ((1 << lhw) - 1);
+        py[v] = rem >> lw;
+        px[v] = rem & ((1 << lw) - 1);
+        pbase[v] = (long)n * G.Hs;
+      }
+    }
+  }
+  SD_DEV void load(int k0, int kend) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      const int gk = k0 + 4 * (i % (BK / 4));
+      if (pbase[v] >= 0 && gk < kend) {
+        const int e = tab[gk >> 2];
+        const int yy = py[v] + ((e >> 16) & 0xff) - G.pad, xx = px[v] + (e >> 24) - G.pad;
+        if (yy >= 0 && yy < G.Hg && xx >= 0 && xx < G.Wg)
+          x = *reinterpret_cast<const f32x4*>(G.in + ((pbase[v] + (yy >> G.ups)) * G.Ws + (xx >> G.ups)) * G.C +
+                                              (e & 0xffff));
+      }
+      st.r[v] = x;
+    }
+  }
+  SD_DEV void store(float* lds) const { st.store(lds); }
+};
+
+// bwd-weight B operand, k-major: rows j = (ky, kx, ci) fixed per thread (decoded once), k = pixel (pow2 grid:
+// shifts). Consecutive lanes take consecutive 4-channel groups of one pixel -> coalesced 16-B loads.
+template <int ROWS>
+struct Im2colColsKM : KMajor<ROWS> {
+  using KMajor<ROWS>::r;
+  using KMajor<ROWS>::NV;
+  Geom G;
+  int J, lw, lhw;
+  int jc[NV], jy[NV], jx[NV], j0v[NV];  // jc < 0: the group straddles J (scalar path incl. the ones column)
+  SD_DEV Im2colColsKM(const Geom& g, int J_, int row0, int lw_, int lhw_) : G(g), J(J_), lw(lw_), lhw(lhw_) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      const int j0 = row0 + 4 * this->rq(i);
+      j0v[v] = j0;
+      jc[v] = -1;
+      jy[v] = jx[v] = 0;
+      if (j0 + 3 < J) {
+        const int t = j0 / G.C;
+        jc[v] = j0 - t * G.C;
+        jy[v] = t / G.kw - G.pad;
+        jx[v] = t - (t / G.kw) * G.kw - G.pad;
+      }
+    }
+  }
+  SD_DEV void load(int k0, int kend) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      const int m = k0 + this->kk(i);
+      if (i < ROWS * BK / 4 && m < kend && j0v[v] <= J) {
+        const int n = m >> lhw, rem = m & ((1 << lhw) - 1);
+        const int y = rem >> lw, xq = rem & ((1 << lw) - 1);
+        if (jc[v] >= 0) {
+          const int yy = y + jy[v], xx = xq + jx[v];
+          if (yy >= 0 && yy < G.Hg && xx >= 0 && xx < G.Wg)
+            x = *reinterpret_cast<const f32x4*>(
+                G.in + (((long)n * G.Hs + (yy >> G.ups)) * G.Ws + (xx >> G.ups)) * G.C + jc[v]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int jj = j0v[v] + j;
+            long off;
+            if (jj < J) {
+              if (tap(G, n, y, xq, jj, off)) x[j] = G.in[off];
+            } else if (jj == J) {
+              x[j] = 1.f;
+            }
+          }
+        }
+      }
+      r[v] = x;
+    }
+  }
+};
+
+// fwd / bwd-data: M = pixels, N = Co (tile = all output channels), 16x16x4 MFMA, 4 waves along M
+template <int BN>
+__global__ __launch_bounds__(256) void conv_fwd16(GemmArgs g, Geom G, int lw, int lhw) {
+  __shared__ int tab[MAX_TAPQ];
+  build_taps(tab, G, g.K);
+  constexpr int BM = 128;
+  const int bm0 = blockIdx.x * BM;
+  Im2colRowsT<BM> la(G, tab, g.M, bm0, lw, lhw);
+  DenseOperand<BN, true, true> lb(g.B, g.ldb, g.N, 0);
+  gemm_block16<BM, BN, 32, BN>(g, la, lb, bm0, 0, 0, 0, 0, g.K);
+}
+
+// bwd-weight: M = Co (one tile), N = kh*kw*Ci + 1, K = pixels (split-K slabs), 4 waves along N
+template <int BM>
+__global__ __launch_bounds__(256) void conv_wgrad16(GemmArgs g, Geom G, int J, int lw, int lhw) {
+  constexpr int BN = 128;
+  const int bn0 = blockIdx.x * BN;
+  const int split = blockIdx.z;
+  const int kbeg = split * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  DenseKM<BM, true> la(g.A, g.lda, g.M, 0);
+  Im2colColsKM<BN> lb(G, J, bn0, lw, lhw);
+  gemm_block16<BM, BN, BM, 32>(g, la, lb, 0, bn0, 0, split, kbeg, kend);
+}
+
+// ---------------------------------------------------------------- direct bwd-weight (stride 1, no upsample)
+// dW[co][j = (ky,kx,ci)] (+ d bias at j = J) = sum over pixels of dy[p][co] * x[p + (ky,kx) - pad][ci].
+// A 512-thread workgroup stages one block of R image rows in LDS — the dy rows (R*W x Co) and the input patch with
+// its halo ((R+kh-1) x (W+kw-1) x Ci, zero padded) — and runs every (co, j) product of that block from LDS, so the
+// 25x im2col expansion is never read from memory (one patch read per row block instead of one per tap).
+// Wave w owns NBW 16-column blocks of j, all TM 16-row blocks of co: acc = TM*NBW 16x16 fp32 tiles in registers,
+// accumulated over the row blocks blockIdx.y, +gridDim.y, ...; the gridDim.y partial slabs are summed by
+// gemm_reduce_kernel. MFMA 16x16x4: lane (l16, q) supplies dy[p = 4s+q][co = l16] and x-patch[p = 4s+q][j = l16].
+// LDS row strides are padded to 16 (mod 64) floats so the 4 lane groups hit distinct banks.
+struct DirectW {
+  const float* x;
+  const float* dy;
+  float* ws;
+  int Nb, H, W, Ci, Co, kh, kw, pad, R, lw;  // lw = log2(W)
+  int J, PW, PH, SA, CP, blocks;
+};
+
+SD_DEV int pad16(int c) { return c % 32 == 0 ? c + 16 : c; }
+
+constexpr int WD_VA = 4, WD_VP = 6;  // max float4 per thread of a staged dy block / input patch
+
+// WS (wave split): for narrow j ranges every wave covers all j blocks over every 8th k step and writes its own slab
+template <int TM, int NBW, bool WS>
+__global__ __launch_bounds__(512) void conv_wgrad_direct(DirectW d) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l16 = lane & 15, q = lane >> 4;
+  const int P = d.R * d.W;
+  float* dyl = lds;                 // [P][SA]
+  float* xp = lds + P * d.SA;       // [PH][PW][CP]; channel Ci holds 1.0 (bias column), Ci+1 holds 0.0
+  // per-lane column decode of this wave's j blocks (j == J -> the ones channel, j > J -> the zero channel)
+  int off[NBW];
+#pragma unroll
+  for (int b = 0; b < NBW; ++b) {
+    const int j = 16 * (WS ? b : (blockIdx.x * NW_D + wave) * NBW + b) + l16;
+    if (j < d.J) {
+      const int t = j / d.Ci, ci = j - t * d.Ci, ky = t / d.kw, kx = t - ky * d.kw;
+      off[b] = (ky * d.PW + kx) * d.CP + ci;
+    } else {
+      off[b] = d.Ci + (j == d.J ? 0 : 1);
+    }
+  }
+  f32x4 acc[TM][NBW];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int b = 0; b < NBW; ++b) acc[i][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int rows_per_img = d.H / d.R, cq = d.Ci / 4, nA = P * d.Co / 4, nP = d.PH * d.PW * cq;
+  f32x4 ra[WD_VA], rp[WD_VP];
+  // global -> registers for row block rb (all loads issued together)
+  auto fetch = [&](int rb) {
+    const int n = rb / rows_per_img, y0 = (rb - n * rows_per_img) * d.R;
+    const float* dsrc = d.dy + ((long)n * d.H + y0) * d.W * d.Co;
+#pragma unroll
+    for (int v = 0; v < WD_VA; ++v) {
+      const int i = tid + 512 * v;
+      ra[v] = i < nA ? *reinterpret_cast<const f32x4*>(dsrc + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int v = 0; v < WD_VP; ++v) {
+      const int i = tid + 512 * v;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (i < nP) {
+        const int pix = i / cq, c = 4 * (i - pix * cq);
+        const int py = pix / d.PW, px = pix - py * d.PW;
+        const int iy = y0 - d.pad + py, ix = px - d.pad;
+        if (iy >= 0 && iy < d.H && ix >= 0 && ix < d.W)
+          x = *reinterpret_cast<const f32x4*>(d.x + (((long)n * d.H + iy) * d.W + ix) * d.Ci + c);
+      }
+      rp[v] = x;
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int v = 0; v < WD_VA; ++v) {
+      const int i = tid + 512 * v;
+      if (i < nA) {
+        const int e = 4 * i, p = e / d.Co, c = e - p * d.Co;
+        *reinterpret_cast<f32x4*>(dyl + p * d.SA + c) = ra[v];
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < WD_VP; ++v) {
+      const int i = tid + 512 * v;
+      if (i < nP) {
+        const int pix = i / cq, c = 4 * (i - pix * cq);
+        *reinterpret_cast<f32x4*>(xp + pix * d.CP + c) = rp[v];
+      }
+    }
+  };
+  // the constant channels never change: write them once
+  for (int pix = tid; pix < d.PH * d.PW; pix += 512) {
+    xp[pix * d.CP + d.Ci] = 1.f;
+    xp[pix * d.CP + d.Ci + 1] = 0.f;
+  }
+  int rb = blockIdx.y;
+  if (rb < d.blocks) fetch(rb);
+  for (; rb < d.blocks; rb += gridDim.y) {
+    __syncthreads();  // previous block's LDS reads are done
+    stage();
+    __syncthreads();
+    if (rb + (int)gridDim.y < d.blocks) fetch(rb + gridDim.y);  // next block's loads overlap this block's MFMAs
+    for (int s = WS ? wave : 0; s < P / 4; s += WS ? NW_D : 1) {
+      const int p = 4 * s + q, py = p >> d.lw, px = p & (d.W - 1);
+      float a[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = dyl[p * d.SA + 16 * i + l16];
+      const float* xb = xp + (py * d.PW + px) * d.CP;
+      float bv[NBW];
+#pragma unroll
+      for (int b = 0; b < NBW; ++b) bv[b] = xb[off[b]];
+#pragma unroll
+      for (int b = 0; b < NBW; ++b)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], bv[b], acc[i][b], 0, 0, 0);
+    }
+  }
+  // partial slab blockIdx.y: ws[split][co][J+1]
+  float* out = d.ws + (long)blockIdx.y * d.Co * (d.J + 1);
+  if (WS) {  // sum the 8 waves' tiles through LDS (the staging area is free now), one 16x16 tile at a time
+#pragma unroll
+    for (int b = 0; b < NBW; ++b)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lds[(wave * 4 + r) * 64 + lane] = acc[i][b][r];
+        __syncthreads();
+        if (tid < 256) {
+          const int r = tid >> 6, ln = tid & 63;
+          float v = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW_D; ++w) v += lds[(w * 4 + r) * 64 + ln];
+          const int j = 16 * b + (ln & 15), co = 16 * i + 4 * (ln >> 4) + r;
+          if (j <= d.J && co < d.Co) out[(long)co * (d.J + 1) + j] = v;
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int b = 0; b < NBW; ++b) {
+    const int j = 16 * ((blockIdx.x * NW_D + wave) * NBW + b) + l16;
+    if (j <= d.J) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = 16 * i + 4 * q + r;
+          if (co < d.Co) out[(long)co * (d.J + 1) + j] = acc[i][b][r];
+        }
+    }
+  }
+}
+
+// SDHIP_CONV_ALGO (benchmarking knob): 0 = auto, 1 = 32x32-tile kernels only, 2 = 16x16 kernels where eligible
+int conv_algo() {
+  static int a = -1;
+  if (a < 0) {
+    const char* e = getenv("SDHIP_CONV_ALGO");
+    a = e ? atoi(e) : 0;
+  }
+  return a;
+}
+
+int ilog2_exact(int v) {  // log2(v) if v is a power of two, else -1
+  if (v <= 0 || (v & (v - 1))) return -1;
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
 
 template <int BM, int BN, int WM, int WN, bool VA, bool VB>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(GemmArgs g, Geom G) {
@@ -309,6 +621,84 @@ int vpt_for(int C, int T) { int v = (C + T - 1) / T; return v <= 1 ? 1 : v <= 2 
 }  // namespace
 
 // out (Nb, Hg, Wg, Co) = conv_same(in (Nb, Hs, Ws, Ci) [upsampled x2 if ups], w (Co, kh, kw, Ci)) + bias
+// host side of the direct bwd-weight: row-block size, j blocking, split count (shared with the workspace query)
+struct DirectPlan {
+  int R, nbw, gx, gy, slabs;
+  bool ws;
+  size_t lds;
+};
+int patch_stride(int Ci) {  // >= Ci + 2 (ones / zero channels), % 4 == 0, 16 or 48 (mod 64) for wide Ci
+  if (Ci < 16) return (Ci + 2 + 3) / 4 * 4;
+  int c = (Ci + 2 + 15) / 16 * 16;
+  while (c % 64 != 16 && c % 64 != 48) c += 16;
+  return c;
+}
+
+bool direct_plan(int Nb, int H, int W, int Ci, int Co, int kh, int kw, int ups, DirectPlan& pl) {
+  if (conv_algo() != 0 || ups != 0 || Co % 16 || Co > 64 || Ci % 4 || ilog2_exact(W) < 0) return false;
+  pl.R = W >= 128 ? 1 : (128 / W < H ? 128 / W : H);
+  if (H % pl.R || (pl.R * W) % 4) return false;
+  const int SA = Co % 32 == 0 ? Co + 16 : Co, CP = patch_stride(Ci);
+  const int PH = pl.R + kh - 1, PW = W + kw - 1;
+  pl.lds = ((size_t)pl.R * W * SA + (size_t)PH * PW * CP) * 4;
+  if (pl.lds > 160 * 1024) return false;
+  if (pl.R * W * Co / 4 > WD_VA * 512 || PH * PW * (Ci / 4) > WD_VP * 512) return false;
+  const int J = kh * kw * Ci, JB = (J + 1 + 15) / 16;
+  pl.ws = JB <= 7;  // few column blocks: split the pixels over the waves instead
+  pl.nbw = pl.ws ? 7 : JB <= 16 ? 2 : JB <= 32 ? 4 : JB <= 56 ? 7 : (Co <= 48 ? 10 : 7);
+  pl.gx = pl.ws ? 1 : (JB + NW_D * pl.nbw - 1) / (NW_D * pl.nbw);
+  const int blocks = Nb * (H / pl.R);
+  pl.gy = 256 / pl.gx;
+  if (pl.gy > blocks) pl.gy = blocks;
+  if (pl.gy < 1) pl.gy = 1;
+  pl.slabs = pl.gy;
+  return true;
+}
+
+int wgrad_direct(const float* in, const float* dout, float* dw_db, float* ws, long ws_floats, int Nb, int H, int W,
+                 int Ci, int Co, int kh, int kw, int pad, int J, int lw, const DirectPlan& pl, hipStream_t s) {
+  DirectW d;
+  d.x = in; d.dy = dout; d.Nb = Nb; d.H = H; d.W = W; d.Ci = Ci; d.Co = Co; d.kh = kh; d.kw = kw; d.pad = pad;
+  d.lw = lw; d.J = J; d.R = pl.R;
+  d.PW = W + kw - 1; d.PH = d.R + kh - 1;
+  d.SA = Co % 32 == 0 ? Co + 16 : Co;
+  d.CP = patch_stride(Ci);
+  d.blocks = Nb * (H / d.R);
+  const size_t lds = pl.lds;
+  const int nbw = pl.nbw, gx = pl.gx, gy = pl.gy;
+  if (!ws || ws_floats < (long)pl.slabs * Co * (J + 1)) return SD_EARG;
+  d.ws = ws;
+  const dim3 grid(gx, gy);
+  const int TM = Co / 16;
+#define SD_WD(TM_, NB_, WS_)                                                                               \
+  if (TM == TM_ && nbw == NB_ && pl.ws == WS_) {                                                           \
+    static bool raised = false;                                                                            \
+    if (!raised && lds > 65536) {                                                                          \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad_direct<TM_, NB_, WS_>),             \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)       \
+        return SD_EARG;                                                                                    \
+      raised = true;                                                                                       \
+    }                                                                                                      \
+    conv_wgrad_direct<TM_, NB_, WS_><<<grid, 512, lds, s>>>(d);                                            \
+    launched = true;                                                                                       \
+  }
+  bool launched = false;
+  SD_WD(1, 7, true) SD_WD(2, 7, true) SD_WD(3, 7, true) SD_WD(4, 7, true)
+  SD_WD(1, 2, false) SD_WD(1, 4, false) SD_WD(1, 7, false) SD_WD(1, 10, false)
+  SD_WD(2, 2, false) SD_WD(2, 4, false) SD_WD(2, 7, false) SD_WD(2, 10, false)
+  SD_WD(3, 2, false) SD_WD(3, 4, false) SD_WD(3, 7, false) SD_WD(3, 10, false)
+  SD_WD(4, 2, false) SD_WD(4, 4, false) SD_WD(4, 7, false)
+#undef SD_WD
+  if (!launched) return SD_ESHAPE;
+  SD_LAUNCH_CHECK();
+  GemmArgs g{};
+  g.C = dw_db; g.ldc = J + 1; g.ws = ws; g.M = Co; g.N = J + 1; g.batch = 1; g.ksplit = pl.slabs; g.alpha = 1.f;
+  const long total = (long)Co * (J + 1);
+  gemm_reduce_kernel<<<(int)((total + 255) / 256), 256, 0, s>>>(g);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
 extern "C" int sd_conv2d_fwd(const float* in, const float* w, const float* bias, float* out, int Nb, int Hs, int Ws,
                              int Ci, int Co, int kh, int kw, int pad, int ups, sd_stream stream_) {
   hipStream_t s = (hipStream_t)stream_;
@@ -319,8 +709,18 @@ extern "C" int sd_conv2d_fwd(const float* in, const float* w, const float* bias,
   g.M = Nb * G.Hg * G.Wg; g.N = Co; g.K = kh * kw * Ci; g.batch = 1; g.ksplit = 1; g.kchunk = g.K;
   g.alpha = 1.f; g.beta = 0.f;
   const bool vb = (((long)kh * kw * Ci) % 4 == 0) && al16(w);
-  const bool va = (Ci % 16 == 0) && al16(in) && vb;
-  if (Co <= 32) fwd_tile<128, 32, 32, 32>(g, G, va, vb, s);
+  const bool va = (Ci % 4 == 0) && al16(in) && vb;
+  const int lw = ilog2_exact(G.Wg), lhw = ilog2_exact(G.Hg * G.Wg);
+  if (conv_algo() != 1 && va && lw >= 0 && lhw >= 0 && g.K / 4 <= MAX_TAPQ &&
+      (Co == 32 || Co == 48 || Co == 64 || Co == 16)) {
+    const dim3 grid(sd_cdiv(g.M, 128));
+    switch (Co) {
+      case 16: conv_fwd16<16><<<grid, 256, 0, s>>>(g, G, lw, lhw); break;
+      case 32: conv_fwd16<32><<<grid, 256, 0, s>>>(g, G, lw, lhw); break;
+      case 48: conv_fwd16<48><<<grid, 256, 0, s>>>(g, G, lw, lhw); break;
+      default: conv_fwd16<64><<<grid, 256, 0, s>>>(g, G, lw, lhw); break;
+    }
+  } else if (Co <= 32) fwd_tile<128, 32, 32, 32>(g, G, va, vb, s);
   else fwd_tile<128, 64, 64, 32>(g, G, va, vb, s);
   SD_LAUNCH_CHECK();
   return SD_OK;
@@ -345,7 +745,19 @@ extern "C" int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db,
   g.alpha = 1.f; g.beta = 0.f;
   const bool va = al16(dout) && Co % 4 == 0;
   const bool vb = (Ci % 4 == 0) && al16(in);
-  if (Co <= 32) wgrad_tile<32, 128, 32, 32>(g, G, J, va, vb, s);
+  const int lw = ilog2_exact(G.Wg), lhw = ilog2_exact(G.Hg * G.Wg);
+  DirectPlan pl;
+  if (va && vb && direct_plan(Nb, Hs, Ws, Ci, Co, kh, kw, ups, pl))
+    return wgrad_direct(in, dout, dw_db, workspace, ws_floats, Nb, Hs, Ws, Ci, Co, kh, kw, pad, J, lw, pl, s);
+  if (conv_algo() == 2 && va && vb && lw >= 0 && lhw >= 0 && (Co == 16 || Co == 32 || Co == 48 || Co == 64)) {
+    const dim3 grid(sd_cdiv(g.N, 128), 1, ks);
+    switch (Co) {
+      case 16: conv_wgrad16<16><<<grid, 256, 0, s>>>(g, G, J, lw, lhw); break;
+      case 32: conv_wgrad16<32><<<grid, 256, 0, s>>>(g, G, J, lw, lhw); break;
+      case 48: conv_wgrad16<48><<<grid, 256, 0, s>>>(g, G, J, lw, lhw); break;
+      default: conv_wgrad16<64><<<grid, 256, 0, s>>>(g, G, J, lw, lhw); break;
+    }
+  } else if (Co <= 32) wgrad_tile<32, 128, 32, 32>(g, G, J, va, vb, s);
   else wgrad_tile<64, 64, 32, 32>(g, G, J, va, vb, s);
   SD_LAUNCH_CHECK();
   if (ks > 1) {
@@ -355,6 +767,13 @@ extern "C" int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db,
     SD_LAUNCH_CHECK();
   }
   return SD_OK;
+}
+
+// number of partial slabs (each Co x (kh*kw*Ci+1) floats) sd_conv2d_wgrad will use with this `ksplit` request
+extern "C" int sd_conv2d_wgrad_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int ups, int ksplit) {
+  DirectPlan pl;
+  if (direct_plan(Nb, Hs, Ws, Ci, Co, kh, kw, ups, pl)) return pl.slabs;
+  return ksplit < 1 ? 1 : ksplit;
 }
 
 extern "C" int sd_conv_flip_weight(const float* w, float* wf, int Co, int kh, int kw, int Ci, sd_stream s) {

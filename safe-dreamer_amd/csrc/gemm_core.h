@@ -26,7 +26,7 @@ struct GemmArgs {
 // KC: k contiguous (row-major in k, `ld` between rows) ; else rows contiguous (`ld` between k's).
 template <int ROWS, bool KC, bool VEC>
 struct TileLoader {
-  static constexpr int NV = ROWS * BK / 4 / 256 > 0 ? ROWS * BK / 4 / 256 : 1;  // float4 per thread
+  static constexpr int NV = (ROWS * BK / 4 + 255) / 256;  // float4 per thread
   f32x4 r[NV];
 
   SD_DEV void load(const float* __restrict__ p, long ld, int row0, int nrows, int k0, int kend) {
@@ -196,6 +196,188 @@ SD_DEV void gemm_block(const GemmArgs& g, OpA& la, OpB& lb, int bm0, int bn0, in
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = bm0 + wr * WM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < g.M && n < g.N) {
+          float v = g.alpha * acc[i][j][r] + bv;
+          float* c = C + (long)m * g.ldc + n;
+          if (g.beta != 0.f) v += g.beta * *c;
+          *c = v;
+        }
+      }
+    }
+}
+
+// k-major LDS image of a ROWS x BK operand tile whose global rows are contiguous along ROWS (A(m,k) at
+// p[k*ld + m]): thread i loads the float4 (k = i / (ROWS/4), rows 4*(i % (ROWS/4)) ..+3) — consecutive lanes read
+// consecutive 16 B of one k-row (coalesced) — and stores it as two 8-B writes into LDS[k][ROWS + 2]; the +2 pad
+// makes the per-lane scalar fragment reads of gemm_block16 (lanes l16 along rows, 4 lane groups 8 k apart) hit
+// 64 distinct banks.
+template <int ROWS>
+struct KMajor {
+  static constexpr bool KMAJOR = true;
+  static constexpr int LD = ROWS + 2;
+  static constexpr int NQ = ROWS / 4;                       // float4 per k-row
+  static constexpr int NV = (ROWS * BK / 4 + 255) / 256;    // float4 per thread
+  f32x4 r[NV];
+  SD_DEV static int kk(int i) { return i / NQ; }
+  SD_DEV static int rq(int i) { return i % NQ; }
+  SD_DEV void store(float* lds) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      if (i < ROWS * BK / 4) {
+        float* d = lds + kk(i) * LD + 4 * rq(i);
+        *reinterpret_cast<float2*>(d) = float2{r[v][0], r[v][1]};
+        *reinterpret_cast<float2*>(d + 2) = float2{r[v][2], r[v][3]};
+      }
+    }
+  }
+};
+
+// dense k-major operand (rows m or n contiguous, `ld` between k's)
+template <int ROWS, bool VEC>
+struct DenseKM : KMajor<ROWS> {
+  using KMajor<ROWS>::r;
+  using KMajor<ROWS>::NV;
+  const float* p;
+  long ld;
+  int nrows, row0;
+  SD_DEV DenseKM(const float* base, long ld_, int nrows_, int row0_) : p(base), ld(ld_), nrows(nrows_), row0(row0_) {}
+  SD_DEV void load(int k0, int kend) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      const int gk = k0 + this->kk(i), gr = row0 + 4 * this->rq(i);
+      if (i < ROWS * BK / 4 && gk < kend) {
+        const float* q = p + (long)gk * ld + gr;
+        if (VEC && gr + 3 < nrows) {
+          x = *reinterpret_cast<const f32x4*>(q);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (gr + j < nrows) x[j] = q[j];
+        }
+      }
+      r[v] = x;
+    }
+  }
+};
+
+// Same pipeline on v_mfma_f32_16x16x4_f32 (wave tiles in multiples of 16: e.g. N = 48 output channels exactly).
+// Row-major LDS operands: lane (l16, q = lane>>4) reads k = 8q .. 8q+7 of its fragment row (two ds_read_b128);
+// k-major operands (OpX::KMAJOR): the same k's as 8 scalar reads. MFMA step s consumes k = 8q + s in lane group q
+// — a fixed k permutation shared by A and B.
+template <class Op, class = void>
+struct is_kmajor { static constexpr bool value = false; };
+template <class Op>
+struct is_kmajor<Op, decltype(void(Op::KMAJOR))> { static constexpr bool value = Op::KMAJOR; };
+
+template <int BM, int BN, int WM, int WN, class OpA, class OpB>
+SD_DEV void gemm_block16(const GemmArgs& g, OpA& la, OpB& lb, int bm0, int bn0, int b, int split, int kbeg,
+                         int kend) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+  constexpr bool AKM = is_kmajor<OpA>::value, BKM = is_kmajor<OpB>::value;
+  constexpr int LDA = AKM ? BM + 2 : LDS_ROW, LDB = BKM ? BN + 2 : LDS_ROW;
+  constexpr int SA = AKM ? BK * LDA : BM * LDS_ROW, SB = BKM ? BK * LDB : BN * LDS_ROW;
+  constexpr int STAGE = SA + SB;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  const int l16 = lane & 15, q = lane >> 4;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    la.load(kbeg, kend);
+    lb.load(kbeg, kend);
+    la.store(smem);
+    lb.store(smem + SA);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      la.load(kbeg + (kt + 1) * BK, kend);
+      lb.load(kbeg + (kt + 1) * BK, kend);
+    }
+    float af[TM][8], bf[TN][8];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wr * WM + 16 * i + l16;
+      if (AKM) {
+        const float* p = smem + cur * STAGE + 8 * q * LDA + row;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) af[i][s] = p[s * LDA];
+      } else {
+        const float* p = smem + cur * STAGE + row * LDS_ROW + 8 * q;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(p), x1 = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) { af[i][s] = x0[s]; af[i][4 + s] = x1[s]; }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wc * WN + 16 * j + l16;
+      if (BKM) {
+        const float* p = smem + cur * STAGE + SA + 8 * q * LDB + row;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) bf[j][s] = p[s * LDB];
+      } else {
+        const float* p = smem + cur * STAGE + SA + row * LDS_ROW + 8 * q;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(p), x1 = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) { bf[j][s] = x0[s]; bf[j][4 + s] = x1[s]; }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    if (kt + 1 < nk) {
+      la.store(smem + (cur ^ 1) * STAGE);
+      lb.store(smem + (cur ^ 1) * STAGE + SA);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: reg r of a 16x16 tile -> row 4q + r, col l16
+  if (g.ksplit > 1) {
+    float* W = g.ws + ((long)split * g.batch + b) * (long)g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = bn0 + wc * WN + 16 * j + l16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = bm0 + wr * WM + 16 * i + 4 * q + r;
+          if (m < g.M && n < g.N) W[(long)m * g.N + n] = g.alpha * acc[i][j][r];
+        }
+      }
+    return;
+  }
+  float* C = g.C + (long)b * g.sC;
+  const float* bias = g.bias ? g.bias + (long)b * g.sBias : nullptr;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = bn0 + wc * WN + 16 * j + l16;
+      const float bv = (bias && n < g.N) ? bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm0 + wr * WM + 16 * i + 4 * q + r;
         if (m < g.M && n < g.N) {
           float v = g.alpha * acc[i][j][r] + bv;
           float* c = C + (long)m * g.ldc + n;

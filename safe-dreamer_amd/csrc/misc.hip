@@ -17,6 +17,16 @@ __global__ void u8_to_f32(const uint8_t* __restrict__ in, float* __restrict__ ou
   if (i < n) out[i] = (float)in[i] / 255.0f - shift;
 }
 
+// out[p][c] = in[p][c] - shift for c < C, 0 for C <= c < Cp (channel-pad an NHWC image to a float4 multiple)
+__global__ void pad_channels_kernel(const float* __restrict__ in, float* __restrict__ out, long pixels, int C, int Cp,
+                                    float shift) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= pixels * Cp) return;
+  const long pix = i / Cp;
+  const int c = (int)(i - pix * Cp);
+  out[i] = c < C ? in[pix * C + c] - shift : 0.f;
+}
+
 __global__ void symlog_kernel(const float* __restrict__ x, float* __restrict__ y, long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
@@ -166,6 +176,13 @@ int nb(long n) { return (int)((n + 255) / 256); }
 extern "C" int sd_u8_to_f32(const uint8_t* in, float* out, long n, float shift, sd_stream s) {
   if (n <= 0) return SD_OK;
   u8_to_f32<<<nb(n), 256, 0, (hipStream_t)s>>>(in, out, n, shift);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_pad_channels(const float* in, float* out, long pixels, int C, int Cp, float shift, sd_stream s) {
+  if (pixels <= 0) return SD_OK;
+  if (C < 1 || Cp < C) return SD_ESHAPE;
+  pad_channels_kernel<<<nb(pixels * Cp), 256, 0, (hipStream_t)s>>>(in, out, pixels, C, Cp, shift);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

@@ -281,6 +281,15 @@ def u8_to_f32(img, shift=0.0, out=None):
     return out
 
 
+def pad_channels(x, Cp, shift=0.0):
+    """NHWC (..., C) -> (..., Cp): x - shift, zero channels appended."""
+    x = _c(x)
+    C = x.shape[-1]
+    out = torch.empty(*x.shape[:-1], Cp, dtype=torch.float32, device=x.device)
+    nat.call("sd_pad_channels", p(x), p(out), x.numel() // C, C, Cp, float(shift), stream())
+    return out
+
+
 def symlog(x):
     y = torch.empty_like(x)
     nat.call("sd_symlog", p(_c(x)), p(y), x.numel(), stream())
@@ -321,6 +330,7 @@ def conv2d_wgrad(x, dout, kh, kw, ups=0, pad=None):
     tiles = -(-Co // 64) * -(-(J + 1) // 64)
     ks = max(1, min(ks, max(1, 1024 // tiles)))
     out = torch.empty(Co, J + 1, dtype=torch.float32, device=x.device)
+    ks = nat.fns["sd_conv2d_wgrad_slabs"](Nb, H, W, Ci, Co, kh, kw, ups, ks)
     ws = torch.empty(ks * Co * (J + 1), dtype=torch.float32, device=x.device) if ks > 1 else None
     nat.call("sd_conv2d_wgrad", p(_c(x)), p(_c(dout)), p(out), p(ws), ws.numel() if ws is not None else 0, ks,
              Nb, H, W, Ci, Co, kh, kw, pad, ups, stream())

@@ -225,7 +225,10 @@ class MultiEncoder(nn.Module):
                 img = torch.cat([obs[k] for k in self.cnn_shapes], -1) if len(self.cnn_shapes) > 1 else obs[next(iter(self.cnn_shapes))]
                 BT = img.shape[:-3]
                 x = img.reshape(-1, *img.shape[-3:])
-                x = x - 0.5  # ConvEncoder.forward, networks.py:224
+                if x.shape[-1] % 4:  # obs - 0.5 (networks.py:224), zero-padded to a float4 channel multiple
+                    x = K.pad_channels(x.contiguous(), (x.shape[-1] + 3) // 4 * 4, 0.5)
+                else:
+                    x = x - 0.5  # ConvEncoder.forward, networks.py:224
                 outs.append(enc(x.contiguous()).reshape(*BT, -1))
             else:
                 x = torch.cat([obs[k] for k in self.mlp_shapes], -1)

@@ -118,7 +118,9 @@ class ConvPoolNormFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, nw, nchw_flat):
-        conv = k.conv2d_fwd(x.contiguous(), w, b)
+        # x may carry zero-padded channels (first layer: 3 -> 4); the weight is padded to match
+        wk = w if x.shape[-1] == w.shape[-1] else torch.nn.functional.pad(w, (0, x.shape[-1] - w.shape[-1])).contiguous()
+        conv = k.conv2d_fwd(x.contiguous(), wk, b)
         y, pooled, amax, rstd = k.pool_rms_fwd(conv, nw, nchw_flat=nchw_flat)
         del conv
         ctx.save_for_backward(x, w, b, nw, pooled, amax, rstd)
@@ -134,10 +136,13 @@ class ConvPoolNormFn(torch.autograd.Function):
         Co, kh, kw, Ci = w.shape
         dconv = k.pool_rms_bwd(pooled, amax, nw, rstd, dy.contiguous(), H, W, grad_buf(nw), nchw_flat=ctx.nchw_flat)
         dwdb = k.conv2d_wgrad(x, dconv, kh, kw)
-        grad_buf(w).add_(dwdb[:, :-1].reshape(w.shape))
+        Cx = x.shape[-1]
+        grad_buf(w).add_(dwdb[:, :-1].reshape(Co, kh, kw, Cx)[..., :Ci])
         grad_buf(b).add_(dwdb[:, -1])
         dx = None
         if ctx.needs_input_grad[0]:
+            if Cx != Ci:
+                raise NotImplementedError("input gradient through a channel-padded conv")
             dx = k.conv2d_fwd(dconv, k.conv_flip_weight(w), None, pad=kh - 1 - (kh - 1) // 2)
         return dx, None, None, None, None
 

@@ -184,7 +184,8 @@ def test_gru_gates():
     close(dh, hr.grad, 1e-6, "dh")
 
 
-@pytest.mark.parametrize("ci,co,hw,nb", [(3, 32, 64, 3), (32, 48, 32, 2), (48, 64, 16, 4), (64, 64, 8, 5)])
+@pytest.mark.parametrize("ci,co,hw,nb", [(3, 32, 64, 3), (4, 32, 64, 3), (32, 48, 32, 2), (48, 64, 16, 4),
+                                        (64, 64, 8, 5)])
 def test_conv_pool_norm(ci, co, hw, nb):
     from sdreamer import ops
     x = torch.rand(nb, hw, hw, ci, generator=_g(ci)) - 0.5
