@@ -235,6 +235,35 @@ int sd_rssm_scan_work_floats(const sd_rssm_scan* d);
 int sd_rssm_scan_fwd(const sd_rssm_scan* d, sd_stream stream);
 int sd_rssm_scan_bwd(const sd_rssm_scan* d, sd_stream stream);
 
+/* ---------------------------------------------------------------- fused imagination (Dreamer._imagine)
+ * Dreamer._imagine (dreamer.py:673-692) over N start states for H1 actor steps: per step the actor MLP
+ * (networks.py:313-377) + action sample (bounded normal / one-hot, distributions.py:217-222 / 16-33), then
+ * RSSM.img_step (rssm.py:180-187: Deter.forward + prior logits + one-hot sample) — 9 launches per step. Every launch
+ * is a row-tiled MFMA contraction whose A loader applies the previous layer's RMSNorm+SiLU on the fly (row rstd from
+ * per-tile partial sums written by the producer's epilogue) and whose epilogue fuses bias, the GRU gate, the
+ * samplers and the action branch (action_norm -> _dyn_in2 -> RMSNorm -> SiLU). Requirements: N % 64 == 0,
+ * U == 256, D/G in {256, 512}, S*Kd % 64 == 0, Kd in {16, 32}, 2A <= 32 (A <= 16 discrete), 1..4 actor layers,
+ * 1..4 img layers. feats (H1, N, S*Kd + D): row block t = 0 holds the start state on entry. */
+typedef struct sd_imagine {
+  int N, H1, D, U, SK, Kd, G, A, act_discrete, actor_layers, img_layers;
+  float eps, unimix, act_unimix, min_std, max_std;
+  uint64_t seed;
+  const uint64_t* seed_ptr;
+  int stream_img, stream_act;
+  long row_offset;
+  const float* Wa[4]; const float* ba[4]; const float* na[4];  /* actor layer i: (U, in_i) (U) (U) */
+  const float *Wao, *bao;                                        /* actor output: (2A or A, U) */
+  const float *W0, *b0, *n0, *W1, *b1, *n1, *W2, *b2, *n2;       /* _dyn_in0/1/2 */
+  const float *Wh, *bh, *nh, *Wg, *bg;                           /* _dyn_hid (G,Dg,Dg+3U), _dyn_gru (G,3Dg,Dg) */
+  const float* Wi[4]; const float* bi[4]; const float* ni[4];    /* img_net layer i */
+  const float *Wl, *bl;                                          /* img_net_logit (SK, U) */
+  float* feats;
+  float* actions;                                                /* (H1, N, A) */
+  float* work;
+} sd_imagine;
+int sd_imagine_work_floats(const sd_imagine* d);
+int sd_imagine_run(const sd_imagine* d, sd_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,6 +55,25 @@ SD_DEV float block_sum(float v, float* red) {
   return s;
 }
 
+// Branch-free bounded loads: a buffer descriptor (range-checked by the hardware) plus a per-lane byte offset; an
+// invalid element gets an offset >= the range (SD_OOB) and reads 0. A "cond ? load : 0" on a runtime condition
+// instead makes hipcc branch around the load and drain vmcnt(0) there, serialising every prefetch behind it.
+// Descriptor inputs go through readfirstlane so hipcc knows they are wave-uniform (no waterfall loops).
+typedef __amdgpu_buffer_rsrc_t sd_rsrc;
+constexpr uint32_t SD_OOB = 0x80000000u;
+SD_DEV sd_rsrc sd_make_rsrc(const void* base, long bytes) {
+  const uint64_t p = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  const uint32_t nb = __builtin_amdgcn_readfirstlane((uint32_t)(bytes < 0x7ffffff0L ? bytes : 0x7ffffff0L));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)nb, 0x00020000);
+}
+SD_DEV f32x4 sd_bload4(sd_rsrc r, uint32_t byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+SD_DEV float sd_bload1(sd_rsrc r, uint32_t byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+
 SD_DEV float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 SD_DEV float siluf_(float x) { return x / (1.f + expf(-x)); }
 

@@ -272,9 +272,13 @@ struct is_kmajor { static constexpr bool value = false; };
 template <class Op>
 struct is_kmajor<Op, decltype(void(Op::KMAJOR))> { static constexpr bool value = Op::KMAJOR; };
 
-template <int BM, int BN, int WM, int WN, class OpA, class OpB>
-SD_DEV void gemm_block16(const GemmArgs& g, OpA& la, OpB& lb, int bm0, int bn0, int b, int split, int kbeg,
-                         int kend) {
+// PF = K-tiles in flight in registers (loader copies la[PF] / lb[PF]); the LDS image is double-buffered. With PF > 1
+// a tile's global loads are issued PF iterations before its LDS store, hiding L2 latency behind PF tiles of MFMA work
+// when a launch has too few waves per SIMD to hide it by occupancy. The k loop is unrolled by PF so every register
+// set is statically indexed.
+template <int BM, int BN, int WM, int WN, int PF = 1, class OpA, class OpB>
+SD_DEV void gemm16_mainloop_pf(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16],
+                               bool accumulate = false) {
   constexpr int WAVES_N = BN / WN;
   constexpr int TM = WM / 16, TN = WN / 16;
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
@@ -288,26 +292,36 @@ SD_DEV void gemm_block16(const GemmArgs& g, OpA& la, OpB& lb, int bm0, int bn0, 
   const int wr = wave / WAVES_N, wc = wave % WAVES_N;
   const int l16 = lane & 15, q = lane >> 4;
 
-  f32x4 acc[TM][TN];
+  // fewer than 4 independent accumulator chains per wave: alternate two banks over the MFMA k steps so
+  // dependent MFMAs do not serialise on the MFMA latency (one wave per SIMD in small-grid launches)
+  constexpr int XC = TM * TN < 4 ? 2 : 1;
+  f32x4 acc2[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) {
+      acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!accumulate) acc[i][j] = acc2[i][j];
+    }
 
   const int nk = (kend - kbeg + BK - 1) / BK;
-  if (nk > 0) {
-    la.load(kbeg, kend);
-    lb.load(kbeg, kend);
-    la.store(smem);
-    lb.store(smem + SA);
-    __syncthreads();
+  if (nk <= 0) return;
+  // tile t's k0; indices past the end are clamped to the last tile (a redundant reload that is never consumed), so
+  // the steady-state body issues every load unconditionally: a load under a branch makes hipcc drain vmcnt(0) at
+  // the merge, which would serialise the whole prefetch pipeline
+  auto ktile = [&](int t) { return kbeg + (t < nk ? t : nk - 1) * BK; };
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    la[u].load(ktile(u), kend);
+    lb[u].load(ktile(u), kend);
   }
-  for (int kt = 0; kt < nk; ++kt) {
+  la[0].store(smem);
+  lb[0].store(smem + SA);
+  __syncthreads();
+  la[0].load(ktile(PF), kend);
+  lb[0].load(ktile(PF), kend);
+  auto step = [&](int kt, int u) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      la.load(kbeg + (kt + 1) * BK, kend);
-      lb.load(kbeg + (kt + 1) * BK, kend);
-    }
     float af[TM][8], bf[TN][8];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -342,14 +356,53 @@ SD_DEV void gemm_block16(const GemmArgs& g, OpA& la, OpB& lb, int bm0, int bn0, 
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
-    if (kt + 1 < nk) {
-      la.store(smem + (cur ^ 1) * STAGE);
-      lb.store(smem + (cur ^ 1) * STAGE + SA);
-    }
+        for (int j = 0; j < TN; ++j) {
+          if (XC == 2 && (s & 1))
+            acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc2[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+        }
+    // tile kt+1 lives in register set (u+1) % PF: stage it, then refill that set with tile kt+1+PF
+    const int nx = (u + 1) % PF;  // static after unrolling
+    la[nx].store(smem + (cur ^ 1) * STAGE);
+    lb[nx].store(smem + (cur ^ 1) * STAGE + SA);
+    la[nx].load(ktile(kt + 1 + PF), kend);
+    lb[nx].load(ktile(kt + 1 + PF), kend);
     __syncthreads();
+  };
+  int kt = 0;
+  for (; kt + PF <= nk; kt += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) step(kt + u, u);
   }
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (kt + u < nk) step(kt + u, u);
+  if (XC == 2) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += acc2[i][j];
+  }
+}
+
+template <int BM, int BN, int WM, int WN, class OpA, class OpB>
+SD_DEV void gemm16_mainloop(OpA& la, OpB& lb, int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16]) {
+  OpA (&a1)[1] = *reinterpret_cast<OpA(*)[1]>(&la);
+  OpB (&b1)[1] = *reinterpret_cast<OpB(*)[1]>(&lb);
+  gemm16_mainloop_pf<BM, BN, WM, WN, 1>(a1, b1, kbeg, kend, acc);
+}
+
+template <int BM, int BN, int WM, int WN, class OpA, class OpB>
+SD_DEV void gemm_block16(const GemmArgs& g, OpA& la, OpB& lb, int bm0, int bn0, int b, int split, int kbeg,
+                         int kend) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  const int l16 = lane & 15, q = lane >> 4;
+  f32x4 acc[TM][TN];
+  gemm16_mainloop<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
 
   // epilogue: reg r of a 16x16 tile -> row 4q + r, col l16
   if (g.ksplit > 1) {

@@ -1,0 +1,548 @@
+// Fused imagination: Dreamer._imagine (dreamer.py:673-692) = for each of H1 steps: actor MLP on feat = [stoch, deter]
+// (networks.py:313-377) -> action sample (bounded normal / one-hot) -> RSSM.img_step (rssm.py:180-187:
+// Deter.forward rssm.py:36-75 + prior img_net + one-hot sample). N (= B*T) independent rows per step.
+//
+// 9 launches per step (the per-op path took ~28): each launch is a row-tiled fp32 MFMA contraction
+// (v_mfma_f32_16x16x4_f32 via gemm16_mainloop) with
+//   * A loaders that apply the previous layer's RMSNorm + SiLU while staging K-tiles into LDS — the per-row rstd
+//     comes from row partial sums of squares that the PRODUCER's epilogue wrote (one float per row per 16*TN
+//     output columns), so no normalised activation is ever materialised and no norm launch exists;
+//   * epilogues that fuse the bias, those row partials, the GRU gate, the unimix one-hot prior sampler, and the
+//     whole action branch (bounded-normal / one-hot action, action_norm, _dyn_in2 Linear + RMSNorm + SiLU);
+//   * independent contractions that share an A operand grouped into one launch (actor layer 0 with _dyn_in1,
+//     img_net_0 with the next step's _dyn_in0).
+// Results land directly in the reference's (H1, N, F) feat and (H1, N, A) action layouts.
+#include "common.h"
+#include "dist_core.h"
+#include "gemm_core.h"
+#include "philox.h"
+#include "sdhip.h"
+
+namespace {
+using namespace sdg;
+
+SD_DEV f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+SD_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// ------------------------------------------------------------------------------------------- A loaders
+// Row-major LDS image of a BM x BK tile; thread i holds row i / 8, k-quad i % 8 (float4 along k).
+template <int BM>
+struct AStage {
+  static constexpr int NV = (BM * BK / 4 + 255) / 256;
+  f32x4 r[NV];
+  SD_DEV static int row(int v) { return (threadIdx.x + 256 * v) / (BK / 4); }
+  SD_DEV static int kq(int v) { return (threadIdx.x + 256 * v) % (BK / 4); }
+  SD_DEV static bool live(int v) { return threadIdx.x + 256 * v < BM * BK / 4; }
+  SD_DEV void store(float* lds) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      if (live(v)) *reinterpret_cast<f32x4*>(lds + row(v) * LDS_ROW + 4 * kq(v)) = r[v];
+  }
+};
+
+// Per-row rstd of the workgroup's BM rows from `np` partial sums of squares part[p*M + m] over `width` columns,
+// into LDS rs[BM]. 256 threads: row = tid % BM, partial group tid / BM; all loads issued at once (MAXP per thread),
+// coalesced along rows. Fixed summation order.
+template <int BM, int MAXP>
+SD_DEV void wg_rstd(const float* part, int np, int M, int m0, int width, float eps, float* rs, float* red) {
+  constexpr int G = 256 / BM;
+  const int tid = threadIdx.x, row = tid % BM, grp = tid / BM;
+  const sd_rsrc rp = sd_make_rsrc(part, (long)np * M * 4);
+  float v[MAXP];
+#pragma unroll
+  for (int k = 0; k < MAXP; ++k) {
+    const int p = grp + G * k;
+    v[k] = sd_bload1(rp, (p < np && m0 + row < M) ? (uint32_t)(((long)p * M + m0 + row) * 4) : SD_OOB);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXP; ++k) s += v[k];
+  red[tid] = s;
+  __syncthreads();
+  if (tid < BM) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) t += red[g * BM + tid];
+    rs[tid] = rsqrtf(t / (float)width + eps);
+  }
+  __syncthreads();
+}
+
+template <int BM>
+struct APlain : AStage<BM> {
+  using AStage<BM>::r;
+  sd_rsrc rx;
+  long ld;
+  int m0, M;
+  SD_DEV APlain(const float* X, long ld_, int m0_, int M_, int K) : ld(ld_), m0(m0_), M(M_) {
+    rx = sd_make_rsrc(X, ((long)(M - 1) * ld + K) * 4);
+  }
+  SD_DEV void load(int k0, int) {
+#pragma unroll
+    for (int v = 0; v < AStage<BM>::NV; ++v) {
+      const int m = m0 + this->row(v);
+      r[v] = sd_bload4(rx, m < M ? (uint32_t)(((long)m * ld + k0 + 4 * this->kq(v)) * 4) : SD_OOB);
+    }
+  }
+};
+
+// A(m, k) = silu(X[m][k] * rstd[m] * w[k]), rstd of the tile's rows in LDS (wg_rstd)
+template <int BM>
+struct ARms : AStage<BM> {
+  using AStage<BM>::r;
+  using AStage<BM>::NV;
+  sd_rsrc rx;
+  const float* w;
+  long ld;
+  int m0, M;
+  float rr[NV];
+  SD_DEV ARms(const float* X, long ld_, const float* w_, const float* rs, int m0_, int M_, int K)
+      : w(w_), ld(ld_), m0(m0_), M(M_) {
+    rx = sd_make_rsrc(X, ((long)(M - 1) * ld + K) * 4);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) rr[v] = rs[this->row(v)];
+  }
+  SD_DEV void load(int k0, int) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int gk = k0 + 4 * this->kq(v), m = m0 + this->row(v);
+      const f32x4 x = sd_bload4(rx, m < M ? (uint32_t)(((long)m * ld + gk) * 4) : SD_OOB), wv = ld4(w + gk);
+      f32x4 y;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] = siluf_(x[j] * rr[v] * wv[j]);
+      r[v] = y;
+    }
+  }
+};
+
+// B operand: rows of a k-contiguous weight matrix; local row lr -> global row base + (lr / seg) * stride + lr % seg
+template <int BN>
+struct BRows {
+  static constexpr int NV = (BN * BK / 4 + 255) / 256;
+  f32x4 r[NV];
+  const float* W;
+  long ld;
+  int base, seg, stride;
+  SD_DEV BRows(const float* W_, long ld_, int base_, int seg_, int stride_) : W(W_), ld(ld_), base(base_), seg(seg_), stride(stride_) {}
+  SD_DEV void load(int k0, int) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + 256 * v;
+      if (i < BN * BK / 4) {
+        const int lr = i / (BK / 4), kq = i % (BK / 4);
+        const long gr = base + (lr / seg) * stride + lr % seg;
+        r[v] = ld4(W + gr * ld + k0 + 4 * kq);
+      }
+    }
+  }
+  SD_DEV void store(float* lds) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + 256 * v;
+      if (i < BN * BK / 4) *reinterpret_cast<f32x4*>(lds + (i / (BK / 4)) * LDS_ROW + 4 * (i % (BK / 4))) = r[v];
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------------- epilogue helpers
+// Wave (wr, wc) of a BM x BN tile owns rows wr*16 + 4q + r and columns wc*WN + 16j + l16 (gemm16_mainloop layout).
+struct Lane {
+  int l16, q, wr, wc;
+};
+template <int BN, int WN>
+SD_DEV Lane lane_ids() {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  return Lane{lane & 15, lane >> 4, wave / (BN / WN), wave % (BN / WN)};
+}
+
+// out[m][n] = acc + bias[n]; part[(n0 + wc*WN)/WN * M + m] = sum over the wave's WN columns of out^2
+template <int BM, int BN, int WN>
+SD_DEV void ep_bias_part(const f32x4 (&acc)[1][WN / 16], const float* bias, float* out, long ldo, float* part, int M,
+                         int m0, int n0) {
+  constexpr int TN = WN / 16;
+  const Lane L = lane_ids<BN, WN>();
+  float ss[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + L.wc * WN + 16 * j + L.l16;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + L.wr * 16 + 4 * L.q + r;
+      const float v = acc[0][j][r] + bv;
+      if (m < M) out[(long)m * ldo + n] = v;
+      ss[r] += v * v;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float s = group_sum<16>(ss[r]);
+    const int m = m0 + L.wr * 16 + 4 * L.q + r;
+    if (L.l16 == 0 && part && m < M) part[(long)((n0 + L.wc * WN) / WN) * M + m] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------- kernels
+struct LinProb {
+  const float* A;
+  long lda;
+  int K;
+  const float* W;  // (N, K) k-contiguous (ld = ldw)
+  long ldw;
+  const float* bias;
+  float* out;
+  long ldo;
+  float* part;
+};
+
+// grouped plain-A linear layers (N = 256 each): out = A . W^T + b, with row partials. grid (N/BN, M/BM, nprob)
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, int M) {
+  constexpr int WN = BN / (4 / (BM / 16));
+  const LinProb p = blockIdx.z ? p1 : p0;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const APlain<BM> a0(p.A, p.lda, m0, M, p.K);
+  const BRows<BN> b0(p.W, p.ldw, n0, BN, 0);
+  APlain<BM> la[3] = {a0, a0, a0};
+  BRows<BN> lb[3] = {b0, b0, b0};
+  f32x4 acc[1][WN / 16];
+  gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, p.K, acc);
+  ep_bias_part<BM, BN, WN>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0);
+}
+
+// out = silu(rms(X)) . W^T + b (MLP hidden layer after the first), with row partials
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw, const float* part_in, int np, int K,
+                                                const float* W, const float* bias, float* out, float* part, int M,
+                                                float eps) {
+  constexpr int WN = BN / (4 / (BM / 16));
+  __shared__ float rs[BM], red[256];
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  wg_rstd<BM, 8>(part_in, np, M, m0, K, eps, rs, red);
+  const ARms<BM> a0(X, K, nw, rs, m0, M, K);
+  const BRows<BN> b0(W, K, n0, BN, 0);
+  ARms<BM> la[3] = {a0, a0, a0};
+  BRows<BN> lb[3] = {b0, b0, b0};
+  f32x4 acc[1][WN / 16];
+  gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, K, acc);
+  ep_bias_part<BM, BN, WN>(acc, bias, out, gridDim.x * BN, part, M, m0, n0);
+}
+
+// hp = BlockLinear(dyn_hid_0)([h_g | x0 | x1 | x2]) + bh with x0 = silu(rms(x0p)), x1 = silu(rms(x1p)) applied by the
+// A loaders (rssm.py:52-63): four main loops over the input segments accumulate into one tile. BM = BN = 64,
+// grid (D/64, M/64); row partials over D for the gate norm.
+__global__ __launch_bounds__(256) void k_hid(sd_imagine d, const float* h, long ldh, const float* x0p, const float* x1p,
+                                             const float* px0, const float* px1, int npx, const float* x2, float* hp,
+                                             float* ph) {
+  constexpr int BM = 64, BN = 64;
+  __shared__ float rs0[BM], rs1[BM], red[256];
+  const int Dg = d.D / d.G, U = d.U, Ig = Dg + 3 * U, M = d.N;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, g = n0 / Dg;
+  wg_rstd<BM, 8>(px0, npx, M, m0, U, d.eps, rs0, red);
+  wg_rstd<BM, 8>(px1, npx, M, m0, U, d.eps, rs1, red);
+  const float* Wseg = d.Wh + (long)n0 * Ig;  // rows n0.. of Wh viewed as (D, Ig)
+  f32x4 acc[1][4];
+  {
+    const APlain<BM> a0(h + (long)g * Dg, ldh, m0, M, Dg);
+    const BRows<BN> b0(Wseg, Ig, 0, BN, 0);
+    APlain<BM> la[3] = {a0, a0, a0};
+    BRows<BN> lb[3] = {b0, b0, b0};
+    gemm16_mainloop_pf<BM, BN, 16, BN, 3>(la, lb, 0, Dg, acc);
+  }
+  {
+    const ARms<BM> a0(x0p, U, d.n0, rs0, m0, M, U);
+    const BRows<BN> b0(Wseg + Dg, Ig, 0, BN, 0);
+    ARms<BM> la[3] = {a0, a0, a0};
+    BRows<BN> lb[3] = {b0, b0, b0};
+    gemm16_mainloop_pf<BM, BN, 16, BN, 3>(la, lb, 0, U, acc, true);
+  }
+  {
+    const ARms<BM> a0(x1p, U, d.n1, rs1, m0, M, U);
+    const BRows<BN> b0(Wseg + Dg + U, Ig, 0, BN, 0);
+    ARms<BM> la[3] = {a0, a0, a0};
+    BRows<BN> lb[3] = {b0, b0, b0};
+    gemm16_mainloop_pf<BM, BN, 16, BN, 3>(la, lb, 0, U, acc, true);
+  }
+  {
+    const APlain<BM> a0(x2, U, m0, M, U);
+    const BRows<BN> b0(Wseg + Dg + 2 * U, Ig, 0, BN, 0);
+    APlain<BM> la[3] = {a0, a0, a0};
+    BRows<BN> lb[3] = {b0, b0, b0};
+    gemm16_mainloop_pf<BM, BN, 16, BN, 3>(la, lb, 0, U, acc, true);
+  }
+  ep_bias_part<BM, BN, BN>(acc, d.bh, hp, d.D, ph, M, m0, n0);
+}
+
+// gates = BlockLinear(dyn_gru)(silu(rms(hp))) + bg; deter' = GRU (rssm.py:65-75) -> feats[t+1][:, SK:].
+// Tile: 64 rows x (r | c | u) for 32 deter columns of block g (BN = 96). grid (D/32, M/64)
+__global__ __launch_bounds__(256) void k_gate(sd_imagine d, const float* hp, const float* ph, int nph,
+                                              const float* hold, float* hnew, long ldf) {
+  constexpr int BM = 64, BN = 96;
+  const int Dg = d.D / d.G;
+  const int c0 = blockIdx.x * 32, m0 = blockIdx.y * BM, g = c0 / Dg, j0 = c0 % Dg;
+  __shared__ float rs[BM], red[256];
+  wg_rstd<BM, 16>(ph, nph, d.N, m0, d.D, d.eps, rs, red);
+  const ARms<BM> a0(hp + (long)g * Dg, d.D, d.nh + (long)g * Dg, rs, m0, d.N, Dg);
+  const BRows<BN> b0(d.Wg + (long)g * 3 * Dg * Dg, Dg, j0, 32, Dg);
+  ARms<BM> la[2] = {a0, a0};
+  BRows<BN> lb[2] = {b0, b0};
+  f32x4 acc[1][6];
+  gemm16_mainloop_pf<BM, BN, 16, BN, 2>(la, lb, 0, Dg, acc);
+  const Lane L = lane_ids<BN, BN>();
+  const float* bg = d.bg + (long)g * 3 * Dg;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = 16 * j + L.l16, jj = j0 + c, col = c0 + c;
+    const float br = bg[jj], bc = bg[Dg + jj], bu = bg[2 * Dg + jj];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long m = m0 + L.wr * 16 + 4 * L.q + r;
+      if (m >= d.N) continue;
+      const float ra = acc[0][j][r] + br, ca = acc[0][2 + j][r] + bc, ua = acc[0][4 + j][r] + bu;
+      const float rs = sigmoidf_(ra);
+      const float cc = tanhf(rs * ca);
+      const float u = sigmoidf_(ua - 1.f);
+      hnew[m * ldf + col] = u * cc + (1.f - u) * hold[m * ldf + col];
+    }
+  }
+}
+
+// prior logits = img_net_logit(silu(rms(x))) and the unimix one-hot ST sample -> feats[t+1][:, :SK].
+// BM = BN = 64, grid (SK/64, M/64); the tile is staged through LDS and sampled by teams of KD threads.
+template <int KD>
+__global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, const float* nw, const float* part_in,
+                                               int np, float* snew, long ldf, int t) {
+  constexpr int BM = 64, BN = 64;
+  __shared__ float tile[BM][BN + 1];
+  __shared__ float rs[BM], red[256];
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, U = d.U, S = d.SK / KD;
+  wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
+  const ARms<BM> a0(X, U, nw, rs, m0, d.N, U);
+  const BRows<BN> b0(d.Wl, U, n0, BN, 0);
+  ARms<BM> la[3] = {a0, a0, a0};
+  BRows<BN> lb[3] = {b0, b0, b0};
+  f32x4 acc[1][4];
+  gemm16_mainloop_pf<BM, BN, 16, BN, 3>(la, lb, 0, U, acc);
+  const Lane L = lane_ids<BN, BN>();
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tile[L.wr * 16 + 4 * L.q + r][16 * j + L.l16] = acc[0][j][r] + d.bl[n0 + 16 * j + L.l16];
+  __syncthreads();
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+  for (int i = threadIdx.x; i < BM * BN; i += 256) {
+    const int rl = i / BN, c = i % BN, lt = c % KD;
+    const long m = m0 + rl;
+    const int s = (n0 + c) / KD;
+    const float l = tile[rl][c];
+    float p, pp, nl;
+    unimix_forward<KD>(l, true, KD, d.unimix, p, pp, nl);
+    const float gn = sd_gumbel(seed, (uint32_t)d.stream_img, (uint32_t)t,
+                               (uint64_t)((m + d.row_offset) * S + s) * KD + lt);
+    float ys;
+    int idx;
+    st_soft<KD>(nl, gn, true, ys, idx, lt);
+    if (m < d.N) snew[m * ldf + n0 + c] = ((lt == idx ? 1.f : 0.f) - ys) + ys;
+  }
+}
+
+// actor output layer + action sample (bounded normal: loc = tanh, scale in [min_std, max_std]; or unimix one-hot),
+// action_norm, and the action branch of the next Deter step: x2 = silu(rms(_dyn_in2(a_n))) (rssm.py:40-46).
+// BM = 32, BN = 32 (2A or A <= 32 columns), grid (1, M/32).
+__global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, const float* nw, const float* part_in,
+                                                int np, float* act, float* x2, int t, int want_x2) {
+  constexpr int BM = 32, BN = 32, WN = 16;
+  __shared__ float tile[BM][BN + 1];
+  __shared__ float an[BM][17];
+  __shared__ float xs[BM][257];
+  __shared__ float rsum[BM][9];
+  const int m0 = blockIdx.y * BM, U = d.U, A = d.A;
+  const int NO = d.act_discrete ? A : 2 * A;
+  __shared__ float rs[BM], red[256];
+  wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
+  const ARms<BM> a0(X, U, nw, rs, m0, d.N, U);
+  const BRows<BN> b0(d.Wao, U, 0, BN, 0);  // 32 rows: the caller passes the output weight zero-padded to 32 rows
+  ARms<BM> la[3] = {a0, a0, a0};
+  BRows<BN> lb[3] = {b0, b0, b0};
+  f32x4 acc[1][1];
+  gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, U, acc);
+  const Lane L = lane_ids<BN, WN>();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int c = L.wc * WN + L.l16;
+    tile[L.wr * 16 + 4 * L.q + r][c] = acc[0][0][r] + (c < NO ? d.bao[c] : 0.f);
+  }
+  __syncthreads();
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+  const int tid = threadIdx.x;
+  if (d.act_discrete) {  // team of 16 lanes per row (A <= 16), one-hot ST sample with the actor's unimix
+    for (int i = tid; i < BM * 16; i += 256) {
+      const int rl = i / 16, lt = i % 16;
+      const bool on = lt < A;
+      const long m = m0 + rl;
+      const float l = on ? tile[rl][lt] : 0.f;
+      float p, pp, nl;
+      unimix_forward<16>(l, on, A, d.act_unimix, p, pp, nl);
+      const float gn = on ? sd_gumbel(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lt)
+                          : 0.f;
+      float ys;
+      int idx;
+      st_soft<16>(nl, gn, on, ys, idx, lt);
+      if (on) {
+        const float a = ((lt == idx ? 1.f : 0.f) - ys) + ys;
+        if (m < d.N) act[m * A + lt] = a;
+        an[rl][lt] = a / fmaxf(fabsf(a), 1.f);
+      }
+    }
+  } else {
+    for (int i = tid; i < BM * A; i += 256) {
+      const int rl = i / A, j = i % A;
+      const long m = m0 + rl;
+      const float loc = tanhf(tile[rl][j]);
+      const float sc = (d.max_std - d.min_std) * sigmoidf_(tile[rl][A + j] + 2.f) + d.min_std;
+      const float a = loc + sd_normal(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + j) * sc;
+      if (m < d.N) act[m * A + j] = a;
+      an[rl][j] = a / fmaxf(fabsf(a), 1.f);
+    }
+  }
+  if (!want_x2) return;
+  __syncthreads();
+  // x2p[row][c] = a_n[row] . W2[c] + b2[c]; thread c = tid (U == 256 columns), all 32 rows
+  {
+    const int c = tid;
+    float w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = j < A ? d.W2[(long)c * A + j] : 0.f;
+    const float b = d.b2[c];
+    for (int rl = 0; rl < BM; ++rl) {
+      float v = b;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j < A) v += an[rl][j] * w[j];
+      xs[rl][c] = v;
+    }
+  }
+  __syncthreads();
+  {  // row sums of squares: 8 threads per row
+    const int rl = tid / 8, part = tid % 8;
+    float s = 0.f;
+    for (int c = part; c < U; c += 8) s += xs[rl][c] * xs[rl][c];
+    rsum[rl][part] = s;
+  }
+  __syncthreads();
+  {
+    const int c = tid;
+    const float wn = d.n2[c];
+    for (int rl = 0; rl < BM; ++rl) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += rsum[rl][k];
+      const float rs = rsqrtf(s / (float)U + d.eps);
+      if (m0 + rl < d.N) x2[(long)(m0 + rl) * U + c] = siluf_(xs[rl][c] * rs * wn);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------- host side
+struct IWork {
+  float *a[2], *pa[2], *x0p, *px0, *x1p, *px1, *x2, *hp, *ph, *i[2], *pi[2];
+  long total;
+};
+long al64(long n) { return (n + 63) / 64 * 64; }
+IWork iwork(const sd_imagine& d, float* base) {
+  IWork w;
+  long o = 0;
+  auto take = [&](long n) { float* p = base ? base + o : nullptr; o += al64(n); return p; };
+  const long NU = (long)d.N * d.U, NP = (long)d.N * (d.U / 32);
+  for (int k = 0; k < 2; ++k) { w.a[k] = take(NU); w.pa[k] = take(NP); }
+  w.x0p = take(NU); w.px0 = take(NP);
+  w.x1p = take(NU); w.px1 = take(NP);
+  w.x2 = take(NU);
+  w.hp = take((long)d.N * d.D);
+  w.ph = take((long)d.N * (d.D / 64));
+  for (int k = 0; k < 2; ++k) { w.i[k] = take(NU); w.pi[k] = take(NP); }
+  w.total = o;
+  return w;
+}
+
+int icheck(const sd_imagine* d) {
+  if (!d || !d->feats || !d->actions || !d->work) return SD_EARG;
+  if (d->N < 1 || d->H1 < 1 || d->U != 256 || d->G < 1 || d->D % d->G || d->D > 4096) return SD_ESHAPE;
+  const int Dg = d->D / d->G;
+  if (Dg % 32 || Dg < 32 || d->SK % 64 || (d->Kd != 16 && d->Kd != 32) || d->SK % d->Kd) return SD_ESHAPE;
+  if (d->A < 1 || (d->act_discrete ? d->A > 16 : 2 * d->A > 32)) return SD_ESHAPE;
+  if (d->actor_layers < 1 || d->actor_layers > 4 || d->img_layers < 1 || d->img_layers > 4) return SD_ESHAPE;
+  if ((d->SK + d->D) % 32) return SD_ESHAPE;
+  return SD_OK;
+}
+
+}  // namespace
+
+extern "C" int sd_imagine_work_floats(const sd_imagine* d) {
+  if (!d) return SD_EARG;
+  return (int)iwork(*d, nullptr).total;
+}
+
+// BRows reads BN = 32 rows of the actor output weight: the caller passes Wao padded to 32 rows (zero rows)
+extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
+  int rc = icheck(dp);
+  if (rc) return rc;
+  const sd_imagine& d = *dp;
+  hipStream_t st = (hipStream_t)stream_;
+  const IWork w = iwork(d, d.work);
+  const int N = d.N, U = d.U, SK = d.SK, D = d.D, F = SK + D;
+  const long NF = (long)N * F;
+  const int npU = U / 32;  // row partials per hidden row (k_lin / k_rmslin with BM = 32, BN = 64 -> WN = 32)
+  const dim3 g32(U / 64, sd_cdiv(N, 32));
+  auto feats = [&](int t) { return d.feats + t * NF; };
+  {  // x0p(0) = h0 . W0^T + b0
+    LinProb p{feats(0) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0};
+    k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), 1), 256, 0, st>>>(p, p, N);
+    SD_LAUNCH_CHECK();
+  }
+  for (int t = 0; t < d.H1; ++t) {
+    const bool last = t == d.H1 - 1;
+    {  // actor layer 0 on feat = [stoch, deter]; _dyn_in1 on stoch
+      LinProb pa{feats(t), F, F, d.Wa[0], F, d.ba[0], w.a[0], U, w.pa[0]};
+      LinProb px{feats(t), F, SK, d.W1, SK, d.b1, w.x1p, U, w.px1};
+      k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, N);
+      SD_LAUNCH_CHECK();
+    }
+    int cur = 0;
+    for (int l = 1; l < d.actor_layers; ++l) {
+      k_rmslin<32, 64><<<g32, 256, 0, st>>>(w.a[cur], d.na[l - 1], w.pa[cur], npU, U, d.Wa[l], d.ba[l], w.a[cur ^ 1],
+                                            w.pa[cur ^ 1], N, d.eps);
+      SD_LAUNCH_CHECK();
+      cur ^= 1;
+    }
+    k_action<<<dim3(1, sd_cdiv(N, 32)), 256, 0, st>>>(d, w.a[cur], d.na[d.actor_layers - 1], w.pa[cur], npU,
+                                              d.actions + (long)t * N * d.A, w.x2, t, last ? 0 : 1);
+    SD_LAUNCH_CHECK();
+    if (last) break;
+    k_hid<<<dim3(D / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, npU, w.x2, w.hp, w.ph);
+    SD_LAUNCH_CHECK();
+    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / 64, feats(t) + SK, feats(t + 1) + SK, F);
+    SD_LAUNCH_CHECK();
+    {  // img_net_0 and the next step's _dyn_in0 share A = deter'
+      LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0]};
+      LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0};
+      k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), 2), 256, 0, st>>>(pi, px, N);
+      SD_LAUNCH_CHECK();
+    }
+    int ci = 0;
+    for (int l = 1; l < d.img_layers; ++l) {
+      k_rmslin<32, 64><<<g32, 256, 0, st>>>(w.i[ci], d.ni[l - 1], w.pi[ci], npU, U, d.Wi[l], d.bi[l], w.i[ci ^ 1],
+                                            w.pi[ci ^ 1], N, d.eps);
+      SD_LAUNCH_CHECK();
+      ci ^= 1;
+    }
+    if (d.Kd == 16)
+      k_prior<16><<<dim3(SK / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npU,
+                                                          feats(t + 1), F, t);
+    else
+      k_prior<32><<<dim3(SK / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npU,
+                                                          feats(t + 1), F, t);
+    SD_LAUNCH_CHECK();
+  }
+  return SD_OK;
+}

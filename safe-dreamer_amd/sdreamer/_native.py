@@ -57,11 +57,16 @@ def _parse_struct(path, name):
             toks = toks[1:]
         base, names = toks[0], [t for t in toks[1:] if t != ","]
         for n in names:
-            fields.append((n, c_ptr if is_ptr else scalars[base]))
+            typ = c_ptr if is_ptr else scalars[base]
+            m = re.match(r"(\w+)\[(\d+)\]$", n)
+            if m:
+                n, typ = m.group(1), typ * int(m.group(2))
+            fields.append((n, typ))
     return type(name, (ctypes.Structure,), {"_fields_": fields})
 
 
 ScanDesc = _parse_struct(HEADER, "sd_rssm_scan")
+ImagineDesc = _parse_struct(HEADER, "sd_imagine")
 
 _CTYPES = {
     "int": c_int, "long": c_long, "float": c_float, "double": ctypes.c_double, "uint64_t": ctypes.c_uint64,

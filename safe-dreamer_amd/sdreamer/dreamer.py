@@ -16,18 +16,25 @@ Differences by design (documented in DESIGN.md):
 from __future__ import annotations
 
 import copy
+import ctypes
 import math
+import os
 from collections import OrderedDict
 
 import torch
 from torch import nn
 
+from . import _native as nat
 from . import kernels as K
 from . import ops
 from . import parallel
 from .networks import MLPHead, MultiDecoder, MultiEncoder, Projector, ReturnEMA
 from .optim import LaProp, WarmupSchedule
 from .rssm import RSSM, STREAM_ACT, STREAM_IMG, STREAM_POLICY
+
+# csrc/img.hip runs the whole imagination as 9 fused launches per step; SDREAMER_FUSED_IMAG=0 selects the per-op
+# HIP kernels (tests compare the two)
+FUSED_IMAG = os.environ.get("SDREAMER_FUSED_IMAG", "1") != "0"
 
 
 def _symexp_bins(n, device):  # symexp_twohot bins, distributions.py:242-251
@@ -383,6 +390,54 @@ class Dreamer(nn.Module):
         return (post_stoch, post_deter), metrics
 
     @torch.no_grad()
+    def _fused_imag_ok(self):
+        r, a = self.rssm, self.actor
+        if not FUSED_IMAG or a.mlp._symlog_inputs or a.mlp.out_dim != r._hidden or r._hidden != 256:
+            return False
+        if a.dist_name not in ("bounded_normal", "onehot") or r._deter % r._blocks or r._deter > 4096:
+            return False
+        A = self.act_dim
+        return (r._deter // r._blocks) % 32 == 0 and r.flat_stoch % 64 == 0 and r._discrete in (16, 32) and \
+            (A <= 16 if self.act_discrete else 2 * A <= 32) and 1 <= a.mlp.n <= 4 and 1 <= r._img_layers <= 4 and \
+            a.last.weight.shape[0] <= 32
+
+    def _imagine_fused(self, feats, actions, H1, seed, row_offset):
+        """sd_imagine_run (csrc/img.hip): feats[0] holds the start state."""
+        r, a = self.rssm, self.actor
+        N = feats.shape[1]
+        P = r._p()
+        d = nat.ImagineDesc()
+        d.N, d.H1, d.D, d.U, d.SK, d.Kd, d.G, d.A = N, H1, r._deter, r._hidden, r.flat_stoch, r._discrete, r._blocks, \
+            self.act_dim
+        d.act_discrete, d.actor_layers, d.img_layers = int(self.act_discrete), a.mlp.n, r._img_layers
+        dist = self.config.actor.dist
+        d.eps, d.unimix = K.EPS, r._unimix_ratio
+        if self.act_discrete:
+            d.act_unimix = float(dist.unimix_ratio)
+        else:
+            d.min_std, d.max_std = float(dist.min_std), float(dist.max_std)
+        d.seed, d.seed_ptr = K.seed_args(seed)
+        d.stream_img, d.stream_act, d.row_offset = STREAM_IMG, STREAM_ACT, int(row_offset)
+        for i, (lin, norm) in enumerate(a.mlp._mods):
+            d.Wa[i], d.ba[i], d.na[i] = lin.weight.data_ptr(), lin.bias.data_ptr(), norm.weight.data_ptr()
+        wo = a.last.weight
+        wpad = torch.zeros(32, wo.shape[1], dtype=torch.float32, device=wo.device)  # the action tile reads 32 rows
+        wpad[:wo.shape[0]] = wo
+        d.Wao, d.bao = wpad.data_ptr(), a.last.bias.data_ptr()
+        for k in ("W0", "b0", "n0", "W1", "b1", "n1", "W2", "b2", "n2", "Wh", "bh", "nh", "Wg", "bg"):
+            setattr(d, k, P[k].data_ptr())
+        mods, last = r._img_mods()
+        for i, (lin, norm) in enumerate(mods):
+            d.Wi[i], d.bi[i], d.ni[i] = lin.weight.data_ptr(), lin.bias.data_ptr(), norm.weight.data_ptr()
+        d.Wl, d.bl = last.weight.data_ptr(), last.bias.data_ptr()
+        d.feats, d.actions = feats.data_ptr(), actions.data_ptr()
+        nwork = nat.fns["sd_imagine_work_floats"](ctypes.addressof(d))
+        if nwork < 0:
+            raise nat.NativeError(f"sd_imagine_work_floats failed with status {nwork}")
+        work = torch.empty(nwork, dtype=torch.float32, device=feats.device)
+        d.work = work.data_ptr()
+        nat.call("sd_imagine_run", ctypes.addressof(d), K.stream())
+
     def _imagine_tm(self, start, H1, seed, row_offset=0):
         """Dreamer._imagine (dreamer.py:673-692), time-major: feats (H1, N, F), actions (H1, N, A).
         The reference's last img_step (whose output is discarded) is skipped."""
@@ -393,6 +448,11 @@ class Dreamer(nn.Module):
         actions = torch.empty(H1, N, self.act_dim, dtype=torch.float32, device=deter.device)
         s = stoch.reshape(N, SK).contiguous()
         h = deter.contiguous()
+        if self._fused_imag_ok():
+            feats[0, :, :SK] = s
+            feats[0, :, SK:] = h
+            self._imagine_fused(feats, actions, H1, seed, row_offset)
+            return feats, actions
         for t in range(H1):
             feats[t, :, :SK] = s
             feats[t, :, SK:] = h

@@ -1,0 +1,63 @@
+"""Fused imagination (csrc/img.hip: 9 launches per step) against the per-op HIP path (pinned end-to-end to the
+reference's golden vectors in test_gpu_dreamer.py), with the golden agents' weights: continuous actor (walker),
+discrete actor + 32x32 latents (atari), deter 4096 (memory maze); N aligned to the 64-row tiles and ragged.
+Tolerances: feats/actions 1e-3 rel + 2e-4 abs (different fp32 summation order); sampled latent indices must agree
+except on near-ties (at most 0.1% of the categoricals)."""
+import pytest
+import torch
+
+from sdreamer import dreamer as DR
+from test_gpu_dreamer import build_agent
+
+pytestmark = pytest.mark.gpu
+
+
+def _start(ag, N, seed):
+    g = torch.Generator().manual_seed(seed)
+    S, Kd, D = ag.rssm._stoch, ag.rssm._discrete, ag.rssm._deter
+    idx = torch.randint(0, Kd, (N, S), generator=g)
+    stoch = torch.nn.functional.one_hot(idx, Kd).float().cuda()
+    deter = (0.5 * torch.randn(N, D, generator=g)).cuda()
+    return stoch, deter
+
+
+def _run(ag, start, H1, fused):
+    DR.FUSED_IMAG = fused
+    try:
+        f, a = ag._imagine_tm(start, H1, seed=77, row_offset=5)
+        torch.cuda.synchronize()
+        return f.clone(), a.clone()
+    finally:
+        DR.FUSED_IMAG = True
+
+
+@pytest.mark.parametrize("name", ["walker_r2", "atari_r2", "maze_r2"])
+@pytest.mark.parametrize("N", [128, 100])
+def test_fused_imagination_matches_per_op(name, N):
+    ag, z, spec, obs = build_agent(name)
+    assert ag._fused_imag_ok()
+    start = _start(ag, N, 3)
+    H1 = 6
+    fr, ar = _run(ag, start, H1, False)
+    ff, af = _run(ag, start, H1, True)
+    SK = ag.rssm.flat_stoch
+    Kd = ag.rssm._discrete
+    ir = fr[:, :, :SK].reshape(H1, N, -1, Kd).argmax(-1)
+    i_f = ff[:, :, :SK].reshape(H1, N, -1, Kd).argmax(-1)
+    mism = (ir != i_f).float().mean().item()
+    assert mism <= 1e-3, mism
+    if mism == 0:
+        torch.testing.assert_close(ff, fr, rtol=1e-3, atol=2e-4)
+        torch.testing.assert_close(af, ar, rtol=1e-3, atol=2e-4)
+    else:  # compare up to the first step with a flipped sample
+        t0 = int((ir != i_f).flatten(1).any(1).nonzero()[0])
+        torch.testing.assert_close(ff[:t0 + 1, :, SK:], fr[:t0 + 1, :, SK:], rtol=1e-3, atol=2e-4)
+        torch.testing.assert_close(af[:t0 + 1], ar[:t0 + 1], rtol=1e-3, atol=2e-4)
+
+
+def test_fused_imagination_deterministic():
+    ag, z, spec, obs = build_agent("walker_r2")
+    start = _start(ag, 192, 5)
+    a = _run(ag, start, 5, True)
+    b = _run(ag, start, 5, True)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
