@@ -137,6 +137,10 @@ class Dreamer(nn.Module):
         self.vbins = _symexp_bins(int(config.critic.dist.bin_num), self.device)
         self._updates = 0
         self.use_graphs = True
+        # the actor-critic branch (imagination, policy/value/replay-value losses and their backward) depends only on the
+        # detached posterior: it runs on this side stream concurrently with the world-model branch (see _cal_grad)
+        self.use_side_stream = True
+        self._side = torch.cuda.Stream(device=self.device)
         self._graph = None
         self._eager_updates = 0
         self._seed_base = int(getattr(config, "seed", 0) or 0) * 1_000_003 + 12345
@@ -277,18 +281,67 @@ class Dreamer(nn.Module):
         return self._g_post, mets
 
     def _cal_grad(self, data, initial, seed=0, row_offset=0):
-        """dreamer.py:453-671 (fp32). data: dict of (B, T, *) device tensors, image float in [0, 1]."""
-        losses, metrics = {}, {}
+        """dreamer.py:453-671 (fp32). data: dict of (B, T, *) device tensors, image float in [0, 1].
+
+        Same losses and gradients as the reference's single backward, scheduled as two concurrent branches after the
+        posterior scan (one process, single GPU; data parallel stays serial):
+          main stream  — world-model head losses (prior/KL, representation, reward, continue) on detached LEAF copies
+                         of the posterior, their backward down to the leaves; then, once the side stream has the
+                         replay-value gradient, one backward from the posterior into the scan and the encoder;
+          side stream  — imagination, lambda-returns, the replay-value loss (kept attached to the world model as in
+                         dreamer.py:652: its feat gradient joins the scan backward), then the policy / value losses
+                         and their backward, overlapping the launch-bound scan backward.
+        Gradient writes of the two streams touch disjoint parameters; value-head gradients come only from the side
+        stream (replay value, then imagined value, in stream order)."""
         B, T = data["action"].shape[:2]
-        S, Kd, SK, D = self.rssm._stoch, self.rssm._discrete, self.rssm.flat_stoch, self.rssm._deter
+        SK = self.rssm.flat_stoch
         embed = self.encoder(data)
         post_stoch, post_deter, post_logit = self.rssm.observe(embed, data["action"], initial, data["is_first"],
                                                                seed=seed, row_offset=row_offset)
+        leaves = [t.detach().requires_grad_(True) for t in (post_stoch, post_deter, post_logit)]
+        feat_l = self.rssm.get_feat(leaves[0], leaves[1])
+        feat_r = feat_l.detach().requires_grad_(True)  # replay-value leaf (side stream)
+        main = torch.cuda.current_stream()
+        side = self._side if (self.use_side_stream and self.world == 1) else main
+        if side is not main:
+            side.wait_stream(main)
+            for t in (post_stoch, post_deter, feat_r, data["reward"], data["is_last"], data["is_terminal"]):
+                t.record_stream(side)
+        with torch.cuda.stream(side):
+            repval_done, ac_total, ac_losses, ac_metrics, ac_last = self._ac_branch(data, post_stoch, post_deter,
+                                                                                   feat_r, seed, row_offset)
+        wm_total, losses, metrics = self._wm_heads(data, embed, leaves, feat_l)
+        # phase 2 (main): posterior gradient = head-loss leaf grads + replay-value feat grad -> scan + encoder
+        if side is not main:
+            main.wait_event(repval_done)
+            feat_r.grad.record_stream(main)
+        g_feat = feat_r.grad
+        lg = [l.grad if l.grad is not None else torch.zeros_like(l) for l in leaves]
+        g_stoch = lg[0] + g_feat[..., :SK].reshape(leaves[0].shape)
+        g_deter = lg[1] + g_feat[..., SK:]
+        torch.autograd.backward([post_stoch, post_deter, post_logit], [g_stoch, g_deter, lg[2]])
+        if side is not main:
+            main.wait_stream(side)
+            for v in list(ac_losses.values()) + list(ac_metrics.values()) + list(ac_last.values()) + [ac_total]:
+                v.record_stream(main)
+        losses.update(ac_losses)
+        metrics.update(ac_metrics)
+        total = wm_total + ac_total
+        metrics.update({f"loss/{k}": v.detach() for k, v in losses.items()})
+        metrics["opt/loss"] = total.detach()
+        self._last = dict(embed=embed, post_logit=post_logit, prior_logit=self._prior_logit, **ac_last)
+        return (post_stoch, post_deter), metrics
+
+    def _wm_heads(self, data, embed, leaves, feat):
+        """World-model losses (dreamer.py:453-576) on the posterior leaves, backward down to the leaves."""
+        losses, metrics = {}, {}
+        B, T = data["action"].shape[:2]
+        post_stoch, post_deter, post_logit = leaves
         prior_logit = self.rssm.prior(post_deter)
+        self._prior_logit = prior_logit
         dyn_loss, rep_loss = self.rssm.kl_loss(post_logit, prior_logit, self.kl_free)
         losses["dyn"] = dyn_loss.mean()
         losses["rep"] = rep_loss.mean()
-        feat = self.rssm.get_feat(post_stoch, post_deter)
         if self.rep_loss == "dreamer":
             recon = self.decoder(post_stoch, post_deter)
             for key, mode in recon.items():
@@ -309,7 +362,17 @@ class Dreamer(nn.Module):
         losses["con"] = -ops.BernoulliLogProbFn.apply(self.cont(feat), cont).mean()
         metrics["dyn_entropy"] = self.rssm.entropy(prior_logit).mean()
         metrics["rep_entropy"] = self.rssm.entropy(post_logit).mean()
+        wm_total = sum(v * self._loss_scales[k] for k, v in losses.items())
+        wm_total.backward()
+        return wm_total, losses, metrics
 
+    def _ac_branch(self, data, post_stoch, post_deter, feat_r, seed, row_offset):
+        """Imagination, lambda-returns, replay value (dreamer.py:578-664) and the policy / value losses with their
+        backward. feat_r: detached posterior feat leaf; its .grad (the replay-value gradient into the world model) is
+        ready when the returned event fires."""
+        losses, metrics = {}, {}
+        B, T = data["action"].shape[:2]
+        S, Kd, D = self.rssm._stoch, self.rssm._discrete, self.rssm._deter
         # ---- imagination (dreamer.py:578-636); time-major (H1, N, .)
         N = B * T
         H1 = self.imag_horizon + 1
@@ -331,6 +394,31 @@ class Dreamer(nn.Module):
             ret_all = parallel.gather_returns(ret, self.world)
             ret_offset, ret_scale = self.return_ema(ret_all)
             adv = (ret - val_n[:, :-1]) / ret_scale
+
+        # ---- replay value (dreamer.py:638-664), attached to the world model through feat_r
+        with torch.no_grad():
+            last = data["is_last"].float().reshape(B, T)
+            term = data["is_terminal"].float().reshape(B, T)
+            reward = data["reward"].float().reshape(B, T)
+            fd = feat_r.detach().reshape(N, -1)
+            value = K.twohot_mode(self.value.logits_nograd(fd), self.vbins).view(B, T)
+            slow_value = K.twohot_mode(self._slow_value.logits_nograd(fd), self.vbins).view(B, T)
+            # boot = imag ret[:, 0] (dreamer.py:645): ret is (N, H) with N = (b, t)
+            rret = K.lambda_return(reward.contiguous(), ret, disc, self.lamb, term=term.contiguous(),
+                                   last=last.contiguous(), boot_row_stride=T * H, boot_t_stride=H)  # (B, T-1)
+        vd = self.value(feat_r[:, :-1])
+        lp_r = ops.TwoHotLogProbFn.apply(vd, self.vbins, rret.reshape(-1))
+        lp_s = ops.TwoHotLogProbFn.apply(vd, self.vbins, slow_value[:, :-1].contiguous().reshape(-1))
+        losses["repval"] = torch.mean((1.0 - last[:, :-1]) * (-lp_r - lp_s))
+        (losses["repval"] * self._loss_scales["repval"]).backward()
+        repval_done = torch.cuda.Event()
+        repval_done.record()
+        with torch.no_grad():
+            metrics.update(_tstats(rret, "ret_replay"))
+            metrics.update(_tstats(value, "value_replay"))
+            metrics.update(_tstats(slow_value, "slow_value_replay"))
+
+        # ---- actor / critic on the imagined trajectories
         pl = self.actor(ifeat[:H].reshape(H * N, -1))
         if self.act_discrete:
             logpi, ent = ops.OneHotLogProbEntFn.apply(pl, iact[:H].reshape(H * N, -1),
@@ -346,6 +434,7 @@ class Dreamer(nn.Module):
         lp_tar = ops.TwoHotLogProbFn.apply(vl, self.vbins, ret.t().contiguous().reshape(-1))
         lp_slow = ops.TwoHotLogProbFn.apply(vl, self.vbins, i_slow[:H].reshape(-1))
         losses["value"] = torch.mean(w * (-lp_tar - lp_slow).view(H, N).t())
+        (losses["policy"] * self._loss_scales["policy"] + losses["value"] * self._loss_scales["value"]).backward()
         with torch.no_grad():
             ret_normed = (ret - ret_offset) / ret_scale
             metrics["ret"] = ret_normed.mean()
@@ -361,33 +450,9 @@ class Dreamer(nn.Module):
             metrics["weight"] = weight.mean()
             metrics["action_entropy"] = ent.detach().mean()
             metrics.update(_tstats(iact, "action"))
-
-        # ---- replay value (dreamer.py:638-664)
-        with torch.no_grad():
-            last = data["is_last"].float().reshape(B, T)
-            term = data["is_terminal"].float().reshape(B, T)
-            reward = data["reward"].float().reshape(B, T)
-            fd = feat.detach().reshape(N, -1)
-            value = K.twohot_mode(self.value.logits_nograd(fd), self.vbins).view(B, T)
-            slow_value = K.twohot_mode(self._slow_value.logits_nograd(fd), self.vbins).view(B, T)
-            # boot = imag ret[:, 0] (dreamer.py:645): ret is (N, H) with N = (b, t)
-            rret = K.lambda_return(reward.contiguous(), ret, disc, self.lamb, term=term.contiguous(),
-                                   last=last.contiguous(), boot_row_stride=T * H, boot_t_stride=H)  # (B, T-1)
-        vd = self.value(feat[:, :-1])
-        lp_r = ops.TwoHotLogProbFn.apply(vd, self.vbins, rret.reshape(-1))
-        lp_s = ops.TwoHotLogProbFn.apply(vd, self.vbins, slow_value[:, :-1].contiguous().reshape(-1))
-        losses["repval"] = torch.mean((1.0 - last[:, :-1]) * (-lp_r - lp_s))
-        with torch.no_grad():
-            metrics.update(_tstats(rret, "ret_replay"))
-            metrics.update(_tstats(value, "value_replay"))
-            metrics.update(_tstats(slow_value, "slow_value_replay"))
-        total = sum(v * self._loss_scales[k] for k, v in losses.items())
-        total.backward()
-        metrics.update({f"loss/{k}": v.detach() for k, v in losses.items()})
-        metrics["opt/loss"] = total.detach()
-        self._last = dict(embed=embed, post_logit=post_logit, prior_logit=prior_logit, imag_feat_tm=ifeat,
-                          imag_action_tm=iact, ret=ret, rret=rret)
-        return (post_stoch, post_deter), metrics
+        ac_total = sum(v.detach() * self._loss_scales[k] for k, v in losses.items())
+        return repval_done, ac_total, losses, metrics, dict(imag_feat_tm=ifeat, imag_action_tm=iact, ret=ret,
+                                                             rret=rret)
 
     @torch.no_grad()
     def _fused_imag_ok(self):
