@@ -139,7 +139,7 @@ class Dreamer(nn.Module):
         self.use_graphs = True
         # the actor-critic branch (imagination, policy/value/replay-value losses and their backward) depends only on the
         # detached posterior: it runs on this side stream concurrently with the world-model branch (see _cal_grad)
-        self.use_side_stream = True
+        self.use_side_stream = os.environ.get("SDREAMER_SIDE_STREAM", "1") != "0"
         self._side = torch.cuda.Stream(device=self.device)
         self._graph = None
         self._eager_updates = 0
