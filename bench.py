@@ -100,8 +100,8 @@ def dominant_probe(K):
         Nb, Hs, Ws, Ci, Co, kh, kw, ups = a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[12]
         return 2.0 * Nb * (Hs << ups) * (Ws << ups) * Co * kh * kw * Ci
     return K.LaunchProbe("sd_conv2d_fwd", lambda a: a[7] == 32 and a[8] == 48 and a[12] == 0, flops,
-                         label="conv_fwd_kernel (encoder conv2: 32->48 ch, 32x32, 5x5; implicit GEMM on "
-                               "v_mfma_f32_32x32x2_f32)")
+                         label="conv_fwd16<48> (encoder conv2: 32->48 ch, 32x32, 5x5; implicit GEMM, "
+                               "v_mfma_f32_16x16x4_f32, N tile = 48 channels)")
 
 
 def main():
@@ -169,6 +169,15 @@ def main():
     }
     if probe is not None:
         out["roofline"] = probe.report()
+        # HBM bytes per launch of the same kernel from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+        # (tools/roofline_traffic.py: gfx950 FETCH_SIZE x2 correction), committed under profiles/
+        tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_roofline_traffic.json")
+        if os.path.exists(tf):
+            t = json.load(open(tf))
+            if t.get("kernel") == "conv_fwd16<48>" and t.get("traffic_bytes"):
+                out["roofline"]["traffic"] = t["traffic_bytes"]
+                out["roofline"]["traffic_source"] = "profiles/r01_roofline_traffic.json (rocprofv3 --pmc)"
+                out["roofline"]["algorithmic_bytes"] = 4.0 * 1024 * 32 * 32 * (32 + 48)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(len(os.sched_getaffinity(0)), 16)
         cfg_cpu = load_config(args.config, ["device=cpu", "model.compile=False"])

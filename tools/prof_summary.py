@@ -22,8 +22,25 @@ def from_csv(path):
     return sorted(rows, key=lambda r: -r[2])
 
 
+def probe_rows(path, name_like="conv_fwd16ILi48E", grid_wgs=8192):
+    """Dispatches of the bench roofline probe kernel (encoder conv2 fwd: 8192 workgroups) — the per-launch average
+    to compare with bench.py's roofline.avg_us."""
+    con = sqlite3.connect(path)
+    q = """select d.end - d.start from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id = s.id
+           where s.kernel_name like ? and d.grid_size_x / d.workgroup_size_x = ?"""
+    try:
+        return [r[0] for r in con.execute(q, (f"%{name_like}%", grid_wgs))]
+    except sqlite3.OperationalError:
+        return []
+
+
 def main(path, top=40, per=1):
     rows = from_db(path) if path.endswith(".db") else from_csv(path)
+    if path.endswith(".db"):
+        pr = probe_rows(path)
+        if pr:
+            print(f"roofline probe kernel conv_fwd16<48> at 8192 workgroups (encoder conv2 fwd): {len(pr)} dispatches, "
+                  f"avg {sum(pr) / len(pr) / 1e3:.1f} us, min {min(pr) / 1e3:.1f} us\n")
     tot = sum(r[2] for r in rows)
     print(f"total kernel time {tot / 1e6:.2f} ms over the profiled run ({tot / 1e6 / per:.2f} ms per step, {per} steps)")
     print("| share | total ms | calls | avg us | kernel |")
