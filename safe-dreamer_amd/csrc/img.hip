@@ -230,47 +230,47 @@ __global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw,
 
 // hp = BlockLinear(dyn_hid_0)([h_g | x0 | x1 | x2]) + bh with x0 = silu(rms(x0p)), x1 = silu(rms(x1p)) applied by the
 // A loaders (rssm.py:52-63): four main loops over the input segments accumulate into one tile. BM = BN = 64,
-// grid (D/64, M/64); row partials over D for the gate norm.
+// grid (D/64, M/64); row partials per 64 columns (D/64 of them) for the gate norm.
 __global__ __launch_bounds__(256) void k_hid(sd_imagine d, const float* h, long ldh, const float* x0p, const float* x1p,
                                              const float* px0, const float* px1, int npx, const float* x2, float* hp,
                                              float* ph) {
-  constexpr int BM = 64, BN = 64;
+  constexpr int BM = 64, BN = 64, WN = 64;
   __shared__ float rs0[BM], rs1[BM], red[256];
   const int Dg = d.D / d.G, U = d.U, Ig = Dg + 3 * U, M = d.N;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, g = n0 / Dg;
   wg_rstd<BM, 8>(px0, npx, M, m0, U, d.eps, rs0, red);
   wg_rstd<BM, 8>(px1, npx, M, m0, U, d.eps, rs1, red);
   const float* Wseg = d.Wh + (long)n0 * Ig;  // rows n0.. of Wh viewed as (D, Ig)
-  f32x4 acc[1][4];
+  f32x4 acc[1][WN / 16];
   {
     const APlain<BM> a0(h + (long)g * Dg, ldh, m0, M, Dg);
     const BRows<BN> b0(Wseg, Ig, 0, BN, 0);
     APlain<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, BN, 3>(la, lb, 0, Dg, acc);
+    gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, Dg, acc);
   }
   {
     const ARms<BM> a0(x0p, U, d.n0, rs0, m0, M, U);
     const BRows<BN> b0(Wseg + Dg, Ig, 0, BN, 0);
     ARms<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, BN, 3>(la, lb, 0, U, acc, true);
+    gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
   }
   {
     const ARms<BM> a0(x1p, U, d.n1, rs1, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + U, Ig, 0, BN, 0);
     ARms<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, BN, 3>(la, lb, 0, U, acc, true);
+    gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
   }
   {
     const APlain<BM> a0(x2, U, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + 2 * U, Ig, 0, BN, 0);
     APlain<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, BN, 3>(la, lb, 0, U, acc, true);
+    gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
   }
-  ep_bias_part<BM, BN, BN>(acc, d.bh, hp, d.D, ph, M, m0, n0);
+  ep_bias_part<BM, BN, WN>(acc, d.bh, hp, d.D, ph, M, m0, n0);
 }
 
 // gates = BlockLinear(dyn_gru)(silu(rms(hp))) + bg; deter' = GRU (rssm.py:65-75) -> feats[t+1][:, SK:].
@@ -308,11 +308,13 @@ __global__ __launch_bounds__(256) void k_gate(sd_imagine d, const float* hp, con
 }
 
 // prior logits = img_net_logit(silu(rms(x))) and the unimix one-hot ST sample -> feats[t+1][:, :SK].
-// BM = BN = 64, grid (SK/64, M/64); the tile is staged through LDS and sampled by teams of KD threads.
+// BM = 16, BN = 64 (4 waves along N), grid (SK/64, M/16): 512 workgroups at the bench shape so the sampler epilogue
+// (Philox noise + unimix softmax per element) runs 4 elements per thread; the tile is staged through LDS and sampled
+// by teams of KD threads.
 template <int KD>
 __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, const float* nw, const float* part_in,
                                                int np, float* snew, long ldf, int t) {
-  constexpr int BM = 64, BN = 64;
+  constexpr int BM = 16, BN = 64, WN = 16;
   __shared__ float tile[BM][BN + 1];
   __shared__ float rs[BM], red[256];
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, U = d.U, S = d.SK / KD;
@@ -321,16 +323,19 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
   const BRows<BN> b0(d.Wl, U, n0, BN, 0);
   ARms<BM> la[3] = {a0, a0, a0};
   BRows<BN> lb[3] = {b0, b0, b0};
-  f32x4 acc[1][4];
-  gemm16_mainloop_pf<BM, BN, 16, BN, 3>(la, lb, 0, U, acc);
-  const Lane L = lane_ids<BN, BN>();
+  f32x4 acc[1][1];
+  gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, U, acc);
+  const Lane L = lane_ids<BN, WN>();
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) tile[L.wr * 16 + 4 * L.q + r][16 * j + L.l16] = acc[0][j][r] + d.bl[n0 + 16 * j + L.l16];
+  for (int r = 0; r < 4; ++r) {
+    const int c = L.wc * WN + L.l16;
+    tile[4 * L.q + r][c] = acc[0][0][r] + d.bl[n0 + c];
+  }
   __syncthreads();
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
-  for (int i = threadIdx.x; i < BM * BN; i += 256) {
+#pragma unroll
+  for (int k = 0; k < BM * BN / 256; ++k) {
+    const int i = threadIdx.x + 256 * k;
     const int rl = i / BN, c = i % BN, lt = c % KD;
     const long m = m0 + rl;
     const int s = (n0 + c) / KD;
@@ -537,10 +542,10 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       ci ^= 1;
     }
     if (d.Kd == 16)
-      k_prior<16><<<dim3(SK / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npU,
+      k_prior<16><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npU,
                                                           feats(t + 1), F, t);
     else
-      k_prior<32><<<dim3(SK / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npU,
+      k_prior<32><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npU,
                                                           feats(t + 1), F, t);
     SD_LAUNCH_CHECK();
   }
