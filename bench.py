@@ -93,15 +93,23 @@ def cpu_baseline(cfg, n_updates, threads):
 
 
 def dominant_probe(K):
-    """Roofline probe on the dominant kernel of the step: the encoder's second convolution forward
-    (implicit GEMM, M = B*L*32*32 pixels, N = 48, K = 5*5*32), the largest MFMA launch of the update
-    (see DESIGN.md §Roofline). Algorithmic work = 2*M*N*K FLOP per launch."""
-    def flops(a):  # sd_conv2d_fwd(in, w, b, out, Nb, Hs, Ws, Ci, Co, kh, kw, pad, ups, stream)
-        Nb, Hs, Ws, Ci, Co, kh, kw, ups = a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[12]
-        return 2.0 * Nb * (Hs << ups) * (Ws << ups) * Co * kh * kw * Ci
-    return K.LaunchProbe("sd_conv2d_fwd", lambda a: a[7] == 32 and a[8] == 48 and a[12] == 0, flops,
-                         label="conv_fwd16<48> (encoder conv2: 32->48 ch, 32x32, 5x5; implicit GEMM, "
-                               "v_mfma_f32_16x16x4_f32, N tile = 48 channels)")
+    """Roofline probe on the dominant kernel of the step: the encoder's second stage forward, conv + MaxPool2d(2) +
+    RMSNorm2D + SiLU in one launch (implicit GEMM, M = B*L*32*32 pixels, N = 48, K = 5*5*32), the largest MFMA launch
+    of the update. Algorithmic work = 2*M*N*K FLOP per launch."""
+    if not K.ops_fused_pool():
+        def flops(a):  # sd_conv2d_fwd(in, w, b, out, Nb, Hs, Ws, Ci, Co, kh, kw, pad, ups, stream)
+            Nb, Hs, Ws, Ci, Co, kh, kw, ups = a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[12]
+            return 2.0 * Nb * (Hs << ups) * (Ws << ups) * Co * kh * kw * Ci
+        return K.LaunchProbe("sd_conv2d_fwd", lambda a: a[7] == 32 and a[8] == 48 and a[12] == 0, flops,
+                             label="conv_fwd16<48> (encoder conv2: 32->48 ch, 32x32, 5x5; implicit GEMM, "
+                                   "v_mfma_f32_16x16x4_f32, N tile = 48 channels)")
+
+    def flops(a):  # sd_conv2d_fwd_pool(in, w, b, nw, pooled, amax, y, rstd, Nb, Hs, Ws, Ci, Co, kh, kw, ...)
+        Nb, Hs, Ws, Ci, Co, kh, kw = a[8], a[9], a[10], a[11], a[12], a[13], a[14]
+        return 2.0 * Nb * Hs * Ws * Co * kh * kw * Ci
+    return K.LaunchProbe("sd_conv2d_fwd_pool", lambda a: a[11] == 32 and a[12] == 48, flops,
+                         label="conv_fwd16_pool<48> (encoder stage 2: 32->48 ch, 32x32, 5x5 conv + 2x2 max-pool + "
+                               "RMSNorm + SiLU epilogue; implicit GEMM, v_mfma_f32_16x16x4_f32, N tile = 48)")
 
 
 def main():
@@ -174,10 +182,11 @@ def main():
         tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_roofline_traffic.json")
         if os.path.exists(tf):
             t = json.load(open(tf))
-            if t.get("kernel") == "conv_fwd16<48>" and t.get("traffic_bytes"):
+            if out["roofline"] and out["roofline"]["kernel"].startswith(t.get("kernel", "?") + " ") \
+                    and t.get("traffic_bytes"):
                 out["roofline"]["traffic"] = t["traffic_bytes"]
                 out["roofline"]["traffic_source"] = "profiles/r01_roofline_traffic.json (rocprofv3 --pmc)"
-                out["roofline"]["algorithmic_bytes"] = 4.0 * 1024 * 32 * 32 * (32 + 48)
+                out["roofline"]["algorithmic_bytes"] = t.get("algorithmic_bytes")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(len(os.sched_getaffinity(0)), 16)
         cfg_cpu = load_config(args.config, ["device=cpu", "model.compile=False"])

@@ -155,6 +155,13 @@ int sd_conv_flip_weight(const float* w, float* wf, int Co, int kh, int kw, int C
 int sd_sumpool2(const float* du, float* din, int Nb, int H, int W, int C, sd_stream stream);
 /* ConvEncoder layer tail: y = SiLU(RMSNorm2D(MaxPool2d(2)(x))) (networks.py:211-214); pooled/amax/rstd saved.
  * nchw_flat: write y in the reference's NCHW flatten order (networks.py:232). C <= 128. */
+/* ConvEncoder stage fused (networks.py:201-216): conv -> MaxPool2d(2) -> RMSNorm2D(nw) -> SiLU in one launch, writing
+ * only the pooled outputs (pooled pre-norm values, 2x2 argmax, rstd: the inputs of sd_pool_rms_bwd). Returns
+ * SD_ESHAPE (nothing launched) outside its instantiations: Co in {16,32,48,64}, Ci % 4 == 0, W a power of two <= 64,
+ * H even, Nb*H*W % 128 == 0 — the caller then runs sd_conv2d_fwd + sd_pool_rms_fwd. */
+int sd_conv2d_fwd_pool(const float* in, const float* w, const float* bias, const float* nw, float* pooled,
+                       uint8_t* amax, float* y, float* rstd, int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw,
+                       int pad, float eps, int nchw_flat, sd_stream stream);
 int sd_pool_rms_fwd(const float* x, const float* w, float* pooled, uint8_t* amax, float* y, float* rstd, int Nb,
                     int H, int W, int C, float eps, int nchw_flat, sd_stream stream);
 int sd_pool_rms_bwd_blocks(int Nb, int H, int W);

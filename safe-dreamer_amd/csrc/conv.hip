@@ -250,6 +250,78 @@ __global__ __launch_bounds__(256) void conv_fwd16(GemmArgs g, Geom G, int lw, in
   gemm_block16<BM, BN, 32, BN>(g, la, lb, bm0, 0, 0, 0, 0, g.K);
 }
 
+// ConvEncoder stage fused: conv (fwd16 main loop) -> MaxPool2d(2) -> RMSNorm2D -> SiLU (networks.py:201-216).
+// A 128-pixel M tile holds whole 2x2 windows (128 % 2W == 0, image rows come in pairs), so the epilogue stages the
+// conv tile in the main loop's LDS area, pools it, normalises over the Co channels (8 threads per pooled pixel) and
+// writes only the pooled outputs (pooled pre-norm values, argmax, rstd for the backward; y NHWC or NCHW-flat).
+template <int BN>
+__global__ __launch_bounds__(256) void conv_fwd16_pool(GemmArgs g, Geom G, int lw, int lhw, const float* nw,
+                                                       float* pooled, uint8_t* amax, float* y, float* rstd, float eps,
+                                                       int nchw_flat) {
+  __shared__ int tab[MAX_TAPQ];
+  build_taps(tab, G, g.K);
+  constexpr int BM = 128, WM = 32, LDC = BN + 1;
+  const int bm0 = blockIdx.x * BM;
+  Im2colRowsT<BM> la(G, tab, g.M, bm0, lw, lhw);
+  DenseOperand<BN, true, true> lb(g.B, g.ldb, g.N, 0);
+  f32x4 acc[WM / 16][BN / 16];
+  gemm16_mainloop<BM, BN, WM, BN>(la, lb, 0, g.K, acc);
+  __syncthreads();  // every wave is done reading the staging area
+  float* C = sd_smem<gemm16_smem_floats<BM, BN>()>();
+  static_assert(BM * LDC <= gemm16_smem_floats<BM, BN>(), "tile fits the staging area");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < WM / 16; ++i)
+#pragma unroll
+    for (int j = 0; j < BN / 16; ++j) {
+      const int col = 16 * j + l16;
+      const float bv = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) C[(wave * WM + 16 * i + 4 * q + r) * LDC + col] = acc[i][j][r] + bv;
+    }
+  __syncthreads();
+  constexpr int NK = BN / 8;
+  const int tid = threadIdx.x, pp = tid >> 3, t8 = tid & 7;  // 32 pooled pixels x 8 threads
+  const int W = G.Wg, Wo = W >> 1, lwo = lw - 1;
+  const int yo = pp >> lwo, xo = pp & (Wo - 1);
+  const int l0 = (2 * yo) * W + 2 * xo;                     // local pixel of the window's top-left
+  const int gp = bm0 + l0;                                    // global conv pixel
+  const int n = gp >> lhw, rem = gp & ((1 << lhw) - 1), yy = rem >> lw, xx = rem & (W - 1);
+  const int Ho = G.Hg >> 1;
+  const long gpp = ((long)n * Ho + (yy >> 1)) * Wo + (xx >> 1);  // global pooled pixel
+  const bool valid = gp < g.M;
+  float v[NK];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c = t8 + 8 * k;
+    float best = -INFINITY;
+    int bi = 0;
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+      const float val = C[(l0 + (qd >> 1) * W + (qd & 1)) * LDC + c];
+      if (val > best || isnan(val)) { best = val; bi = qd; }
+    }
+    v[k] = best;
+    ss += best * best;
+    if (valid) {
+      pooled[gpp * BN + c] = best;
+      amax[gpp * BN + c] = (uint8_t)bi;
+    }
+  }
+  ss = group_sum<8>(ss);
+  const float r = rsqrtf(ss / (float)BN + eps);
+  if (valid && t8 == 0) rstd[gpp] = r;
+  const long prem = gpp - (long)n * Ho * Wo;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c = t8 + 8 * k;
+    const float z = v[k] * r * nw[c];
+    const long o = nchw_flat ? (long)n * BN * Ho * Wo + (long)c * Ho * Wo + prem : gpp * BN + c;
+    if (valid) y[o] = siluf_(z);
+  }
+}
+
 // bwd-weight: M = Co (one tile), N = kh*kw*Ci + 1, K = pixels (split-K slabs), 4 waves along N
 template <int BM>
 __global__ __launch_bounds__(256) void conv_wgrad16(GemmArgs g, Geom G, int J, int lw, int lhw) {
@@ -727,6 +799,35 @@ extern "C" int sd_conv2d_fwd(const float* in, const float* w, const float* bias,
 }
 
 // dw_db (Co, kh*kw*Ci + 1) = [dW | d bias] = sum over pixels of dout (Nb,Hg,Wg,Co) x im2col(in)
+// fused ConvEncoder stage forward; SD_ESHAPE when the shape is outside the fused kernel (caller: conv + pool)
+extern "C" int sd_conv2d_fwd_pool(const float* in, const float* w, const float* bias, const float* nw, float* pooled,
+                                  uint8_t* amax, float* y, float* rstd, int Nb, int Hs, int Ws, int Ci, int Co, int kh,
+                                  int kw, int pad, float eps, int nchw_flat, sd_stream stream_) {
+  hipStream_t s = (hipStream_t)stream_;
+  if (Nb <= 0) return SD_OK;
+  Geom G{in, Nb, Hs, Ws, Ci, Hs, Ws, kh, kw, pad, 0};
+  GemmArgs g{};
+  g.B = w; g.bias = bias; g.ldb = (long)kh * kw * Ci; g.ldc = Co;
+  g.M = Nb * Hs * Ws; g.N = Co; g.K = kh * kw * Ci; g.batch = 1; g.ksplit = 1; g.kchunk = g.K;
+  g.alpha = 1.f; g.beta = 0.f;
+  const bool vb = (((long)kh * kw * Ci) % 4 == 0) && al16(w);
+  const bool va = (Ci % 4 == 0) && al16(in) && vb;
+  const int lw = ilog2_exact(Ws), lhw = ilog2_exact(Hs * Ws);
+  if (conv_algo() == 1 || !va || lw < 1 || lhw < 0 || g.K / 4 > MAX_TAPQ || Hs % 2 || 128 % (2 * Ws) ||
+      g.M % 128)
+    return SD_ESHAPE;
+  const dim3 grid(g.M / 128);
+  switch (Co) {
+    case 16: conv_fwd16_pool<16><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat); break;
+    case 32: conv_fwd16_pool<32><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat); break;
+    case 48: conv_fwd16_pool<48><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat); break;
+    case 64: conv_fwd16_pool<64><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat); break;
+    default: return SD_ESHAPE;
+  }
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
 extern "C" int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db, float* workspace, long ws_floats,
                                int ksplit, int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad, int ups,
                                sd_stream stream_) {

@@ -276,6 +276,18 @@ struct is_kmajor<Op, decltype(void(Op::KMAJOR))> { static constexpr bool value =
 // a tile's global loads are issued PF iterations before its LDS store, hiding L2 latency behind PF tiles of MFMA work
 // when a launch has too few waves per SIMD to hide it by occupancy. The k loop is unrolled by PF so every register
 // set is statically indexed.
+// Static LDS block of N floats, one per (kernel, N): lets an epilogue reuse a main loop's staging area.
+template <int N>
+SD_DEV float* sd_smem() {
+  __shared__ __attribute__((aligned(16))) float s[N];
+  return s;
+}
+// floats of gemm16_mainloop_pf's double-buffered staging area
+template <int BM, int BN, bool AKM = false, bool BKM = false>
+constexpr int gemm16_smem_floats() {
+  return 2 * ((AKM ? BK * (BM + 2) : BM * LDS_ROW) + (BKM ? BK * (BN + 2) : BN * LDS_ROW));
+}
+
 template <int BM, int BN, int WM, int WN, int PF = 1, class OpA, class OpB>
 SD_DEV void gemm16_mainloop_pf(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16],
                                bool accumulate = false) {
@@ -286,7 +298,8 @@ SD_DEV void gemm16_mainloop_pf(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend,
   constexpr int LDA = AKM ? BM + 2 : LDS_ROW, LDB = BKM ? BN + 2 : LDS_ROW;
   constexpr int SA = AKM ? BK * LDA : BM * LDS_ROW, SB = BKM ? BK * LDB : BN * LDS_ROW;
   constexpr int STAGE = SA + SB;
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  static_assert(2 * STAGE == gemm16_smem_floats<BM, BN, AKM, BKM>(), "staging size");
+  float* smem = sd_smem<2 * STAGE>();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave / WAVES_N, wc = wave % WAVES_N;

@@ -123,6 +123,9 @@ class NativeError(RuntimeError):
     pass
 
 
+SD_ESHAPE = -2  # common.h
+
+
 def check(rc, name=""):
     if rc != 0:
         raise NativeError(f"{name} failed with status {rc}")
@@ -141,6 +144,27 @@ def call(name, *args):
             pr.end(args)
         return
     check(fns[name](*args), name)
+
+
+def call_shaped(name, *args):
+    """Like call(), but returns False (nothing launched) when the entry point reports SD_ESHAPE, i.e. the shape is
+    outside a specialised kernel and the caller runs its general path."""
+    if PROBES:
+        hit = [pr for pr in PROBES if pr.match(name, args)]
+        for pr in hit:
+            pr.begin()
+        rc = fns[name](*args)
+        if rc == SD_ESHAPE:
+            return False
+        check(rc, name)
+        for pr in hit:
+            pr.end(args)
+        return True
+    rc = fns[name](*args)
+    if rc == SD_ESHAPE:
+        return False
+    check(rc, name)
+    return True
 
 
 def exported_symbols():

@@ -362,6 +362,26 @@ def pool_rms_fwd(x, w, nchw_flat=False):
     return y, pooled, amax, rstd
 
 
+def ops_fused_pool():
+    from . import ops
+    return ops.FUSED_POOL
+
+
+def conv2d_fwd_pool(x, w, b, nw, nchw_flat=False):
+    """Fused ConvEncoder stage forward (sd_conv2d_fwd_pool): x (Nb, H, W, Ci) NHWC, w (Co, kh, kw, Ci) ->
+    (y, pooled, amax, rstd) as pool_rms_fwd(conv2d_fwd(x, w, b), nw) returns them, or None when the shape is outside
+    the fused kernel."""
+    Nb, H, W, Ci = x.shape
+    Co, kh, kw, _ = w.shape
+    pooled = torch.empty(Nb, H // 2, W // 2, Co, dtype=torch.float32, device=x.device)
+    amax = torch.empty(Nb, H // 2, W // 2, Co, dtype=torch.uint8, device=x.device)
+    y = torch.empty_like(pooled)
+    rstd = torch.empty(Nb, H // 2, W // 2, dtype=torch.float32, device=x.device)
+    ok = nat.call_shaped("sd_conv2d_fwd_pool", p(_c(x)), p(_c(w)), p(b), p(nw), p(pooled), p(amax), p(y), p(rstd),
+                         Nb, H, W, Ci, Co, kh, kw, (kh - 1) // 2, EPS, int(nchw_flat), stream())
+    return (y, pooled, amax, rstd) if ok else None
+
+
 def pool_rms_bwd(pooled, amax, w, rstd, dy, H, W, dw, nchw_flat=False):
     Nb, Ho, Wo, C = pooled.shape
     dx = torch.empty(Nb, H, W, C, dtype=torch.float32, device=pooled.device)

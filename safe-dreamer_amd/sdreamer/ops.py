@@ -6,9 +6,15 @@ autograd, so weight gradients never take an extra allocation + add pass. Input g
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import kernels as k
+
+
+# ConvEncoder stages run conv + pool + norm as one launch where the shape allows (SDREAMER_FUSED_POOL=0: two launches)
+FUSED_POOL = os.environ.get("SDREAMER_FUSED_POOL", "1") != "0"
 
 
 def grad_buf(param):
@@ -120,9 +126,12 @@ class ConvPoolNormFn(torch.autograd.Function):
     def forward(ctx, x, w, b, nw, nchw_flat):
         # x may carry zero-padded channels (first layer: 3 -> 4); the weight is padded to match
         wk = w if x.shape[-1] == w.shape[-1] else torch.nn.functional.pad(w, (0, x.shape[-1] - w.shape[-1])).contiguous()
-        conv = k.conv2d_fwd(x.contiguous(), wk, b)
-        y, pooled, amax, rstd = k.pool_rms_fwd(conv, nw, nchw_flat=nchw_flat)
-        del conv
+        fused = k.conv2d_fwd_pool(x.contiguous(), wk, b, nw, nchw_flat=nchw_flat) if FUSED_POOL else None
+        if fused is None:
+            conv = k.conv2d_fwd(x.contiguous(), wk, b)
+            fused = k.pool_rms_fwd(conv, nw, nchw_flat=nchw_flat)
+            del conv
+        y, pooled, amax, rstd = fused
         ctx.save_for_backward(x, w, b, nw, pooled, amax, rstd)
         ctx.nchw_flat = nchw_flat
         if nchw_flat:

@@ -18,12 +18,20 @@ def per_launch(path, counter, name_like, grid_wgs):
     return (sum(vals) / len(vals) if vals else None), len(vals), desc
 
 
-def main(fetch_db, write_db, out):
-    name, wgs = "conv_fwd16<48>", 8192
+# algorithmic bytes per launch: the conv input read once + the stage's outputs written once
+ALGO = {
+    "conv_fwd16<48>": 4.0 * 1024 * 32 * 32 * (32 + 48),  # NHWC input, full-resolution conv output
+    # input + pooled (f32) + y (f32) + argmax (u8) + rstd (f32 per pooled pixel)
+    "conv_fwd16_pool<48>": 4.0 * 1024 * 32 * 32 * 32 + 1024 * 16 * 16 * (48 * (4 + 4 + 1) + 4),
+}
+
+
+def main(fetch_db, write_db, out, name="conv_fwd16_pool<48>"):
+    wgs = 8192
     f, nf, fdesc = per_launch(fetch_db, "FETCH_SIZE", name, wgs)
     w, nw, wdesc = per_launch(write_db, "WRITE_SIZE", name, wgs)
     kb = 1024.0  # rocprofv3 FETCH_SIZE / WRITE_SIZE are in kilobytes
-    res = {"kernel": name, "grid_workgroups": wgs, "dispatches": [nf, nw],
+    res = {"kernel": name, "grid_workgroups": wgs, "algorithmic_bytes": ALGO[name], "dispatches": [nf, nw],
            "fetch_bytes_raw": f * kb if f is not None else None,
            "fetch_bytes": 2 * f * kb if f is not None else None,  # gfx950: FETCH_SIZE = 1/2 of wide reads
            "write_bytes": w * kb if w is not None else None,
@@ -34,4 +42,4 @@ def main(fetch_db, write_db, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
