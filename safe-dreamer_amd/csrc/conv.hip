@@ -181,6 +181,66 @@ struct Im2colRowsT {
   SD_DEV void store(float* lds) const { st.store(lds); }
 };
 
+// Branch-free variant of Im2colRowsT on buffer loads (out-of-image taps and the K tail read 0 through the
+// descriptor's range check), for gemm16_mainloop_es. Input must be < 2 GiB (checked by the launcher).
+template <int ROWS>
+struct Im2colRowsB {
+  static constexpr int NV = (ROWS * BK / 4 + 255) / 256;
+  Geom G;
+  const int* tab;
+  sd_rsrc rs;
+  int py[NV], px[NV], pb[NV];  // pb: n * Hs, or a large negative value for rows past M
+  TileLoader<ROWS, true, false> st;
+  SD_DEV Im2colRowsB(const Geom& g, const int* tab_, int M, int row0, int lw, int lhw) : G(g), tab(tab_) {
+    rs = sd_make_rsrc(g.in, (long)g.Nb * g.Hs * g.Ws * g.C * 4);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      const int m = row0 + i / (BK / 4);
+      const int n = m >> lhw, rem = m & ((1 << lhw) - 1);
+      py[v] = rem >> lw;
+      px[v] = rem & ((1 << lw) - 1);
+      pb[v] = (i < ROWS * BK / 4 && m < M) ? n * G.Hs : -(1 << 28);
+    }
+  }
+  SD_DEV void load(int k0, int kend) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      const int gk = k0 + 4 * (i % (BK / 4));
+      const int e = tab[min(gk >> 2, MAX_TAPQ - 1)];
+      const int yy = py[v] + ((e >> 16) & 0xff) - G.pad, xx = px[v] + (e >> 24) - G.pad;
+      const bool ok = pb[v] >= 0 && gk < kend && (unsigned)yy < (unsigned)G.Hg && (unsigned)xx < (unsigned)G.Wg;
+      const uint32_t off = (uint32_t)((((pb[v] + (yy >> G.ups)) * G.Ws + (xx >> G.ups)) * G.C + (e & 0xffff)) * 4);
+      st.r[v] = sd_bload4(rs, ok ? off : SD_OOB);
+    }
+  }
+  SD_DEV void store(float* lds) const { st.store(lds); }
+};
+
+// Branch-free dense operand, k contiguous, ROWS x BK tiles of a (nrows x K) matrix with K % 4 == 0 (buffer loads)
+template <int ROWS>
+struct DenseKCB {
+  static constexpr int NV = (ROWS * BK / 4 + 255) / 256;
+  sd_rsrc rs;
+  long ld;
+  int nrows, row0;
+  TileLoader<ROWS, true, false> st;
+  SD_DEV DenseKCB(const float* base, long ld_, int nrows_, int row0_) : ld(ld_), nrows(nrows_), row0(row0_) {
+    rs = sd_make_rsrc(base, (long)nrows_ * ld_ * 4);
+  }
+  SD_DEV void load(int k0, int kend) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      const int row = row0 + i / (BK / 4), gk = k0 + 4 * (i % (BK / 4));
+      const bool ok = i < ROWS * BK / 4 && row < nrows && gk < kend;
+      st.r[v] = sd_bload4(rs, ok ? (uint32_t)((row * ld + gk) * 4) : SD_OOB);
+    }
+  }
+  SD_DEV void store(float* lds) const { st.store(lds); }
+};
+
 // bwd-weight B operand, k-major: rows j = (ky, kx, ci) fixed per thread (decoded once), k = pixel (pow2 grid:
 // shifts). Consecutive lanes take consecutive 4-channel groups of one pixel -> coalesced 16-B loads.
 template <int ROWS>
@@ -239,22 +299,28 @@ struct Im2colColsKM : KMajor<ROWS> {
 };
 
 // fwd / bwd-data: M = pixels, N = Co (tile = all output channels), 16x16x4 MFMA, 4 waves along M
-template <int BN>
+template <int BN, bool ES>
 __global__ __launch_bounds__(256) void conv_fwd16(GemmArgs g, Geom G, int lw, int lhw) {
   __shared__ int tab[MAX_TAPQ];
   build_taps(tab, G, g.K);
   constexpr int BM = 128;
   const int bm0 = blockIdx.x * BM;
-  Im2colRowsT<BM> la(G, tab, g.M, bm0, lw, lhw);
-  DenseOperand<BN, true, true> lb(g.B, g.ldb, g.N, 0);
-  gemm_block16<BM, BN, 32, BN>(g, la, lb, bm0, 0, 0, 0, 0, g.K);
+  if constexpr (ES) {
+    Im2colRowsB<BM> la(G, tab, g.M, bm0, lw, lhw);
+    DenseKCB<BN> lb(g.B, g.ldb, g.N, 0);
+    gemm_block16<BM, BN, 32, BN, true>(g, la, lb, bm0, 0, 0, 0, 0, g.K);
+  } else {
+    Im2colRowsT<BM> la(G, tab, g.M, bm0, lw, lhw);
+    DenseOperand<BN, true, true> lb(g.B, g.ldb, g.N, 0);
+    gemm_block16<BM, BN, 32, BN>(g, la, lb, bm0, 0, 0, 0, 0, g.K);
+  }
 }
 
 // ConvEncoder stage fused: conv (fwd16 main loop) -> MaxPool2d(2) -> RMSNorm2D -> SiLU (networks.py:201-216).
 // A 128-pixel M tile holds whole 2x2 windows (128 % 2W == 0, image rows come in pairs), so the epilogue stages the
 // conv tile in the main loop's LDS area, pools it, normalises over the Co channels (8 threads per pooled pixel) and
 // writes only the pooled outputs (pooled pre-norm values, argmax, rstd for the backward; y NHWC or NCHW-flat).
-template <int BN>
+template <int BN, bool ES>
 __global__ __launch_bounds__(256) void conv_fwd16_pool(GemmArgs g, Geom G, int lw, int lhw, const float* nw,
                                                        float* pooled, uint8_t* amax, float* y, float* rstd, float eps,
                                                        int nchw_flat) {
@@ -262,10 +328,16 @@ __global__ __launch_bounds__(256) void conv_fwd16_pool(GemmArgs g, Geom G, int l
   build_taps(tab, G, g.K);
   constexpr int BM = 128, WM = 32, LDC = BN + 1;
   const int bm0 = blockIdx.x * BM;
-  Im2colRowsT<BM> la(G, tab, g.M, bm0, lw, lhw);
-  DenseOperand<BN, true, true> lb(g.B, g.ldb, g.N, 0);
   f32x4 acc[WM / 16][BN / 16];
-  gemm16_mainloop<BM, BN, WM, BN>(la, lb, 0, g.K, acc);
+  if constexpr (ES) {
+    Im2colRowsB<BM> la(G, tab, g.M, bm0, lw, lhw);
+    DenseKCB<BN> lb(g.B, g.ldb, g.N, 0);
+    gemm16_mainloop_es<BM, BN, WM, BN>(la, lb, 0, g.K, acc);
+  } else {
+    Im2colRowsT<BM> la(G, tab, g.M, bm0, lw, lhw);
+    DenseOperand<BN, true, true> lb(g.B, g.ldb, g.N, 0);
+    gemm16_mainloop<BM, BN, WM, BN>(la, lb, 0, g.K, acc);
+  }
   __syncthreads();  // every wave is done reading the staging area
   float* C = sd_smem<gemm16_smem_floats<BM, BN>()>();
   static_assert(BM * LDC <= gemm16_smem_floats<BM, BN>(), "tile fits the staging area");
@@ -497,6 +569,17 @@ int conv_algo() {
     a = e ? atoi(e) : 0;
   }
   return a;
+}
+
+// SDHIP_CONV_ES (benchmarking knob): 1 (default) = 16x16 conv kernels on the early-store main loop with buffer-load
+// operands, 0 = the double-buffered main loop with branchy loaders
+bool conv_es() {
+  static int a = -1;
+  if (a < 0) {
+    const char* e = getenv("SDHIP_CONV_ES");
+    a = e ? atoi(e) : 1;
+  }
+  return a != 0;
 }
 
 int ilog2_exact(int v) {  // log2(v) if v is a power of two, else -1
@@ -786,12 +869,16 @@ extern "C" int sd_conv2d_fwd(const float* in, const float* w, const float* bias,
   if (conv_algo() != 1 && va && lw >= 0 && lhw >= 0 && g.K / 4 <= MAX_TAPQ &&
       (Co == 32 || Co == 48 || Co == 64 || Co == 16)) {
     const dim3 grid(sd_cdiv(g.M, 128));
+    const bool es = conv_es() && (long)Nb * Hs * Ws * Ci < (1L << 29);  // buffer offsets < 2 GiB
+#define SD_FWD16(BN) (es ? conv_fwd16<BN, true><<<grid, 256, 0, s>>>(g, G, lw, lhw) \
+                         : conv_fwd16<BN, false><<<grid, 256, 0, s>>>(g, G, lw, lhw))
     switch (Co) {
-      case 16: conv_fwd16<16><<<grid, 256, 0, s>>>(g, G, lw, lhw); break;
-      case 32: conv_fwd16<32><<<grid, 256, 0, s>>>(g, G, lw, lhw); break;
-      case 48: conv_fwd16<48><<<grid, 256, 0, s>>>(g, G, lw, lhw); break;
-      default: conv_fwd16<64><<<grid, 256, 0, s>>>(g, G, lw, lhw); break;
+      case 16: SD_FWD16(16); break;
+      case 32: SD_FWD16(32); break;
+      case 48: SD_FWD16(48); break;
+      default: SD_FWD16(64); break;
     }
+#undef SD_FWD16
   } else if (Co <= 32) fwd_tile<128, 32, 32, 32>(g, G, va, vb, s);
   else fwd_tile<128, 64, 64, 32>(g, G, va, vb, s);
   SD_LAUNCH_CHECK();
@@ -817,13 +904,18 @@ extern "C" int sd_conv2d_fwd_pool(const float* in, const float* w, const float* 
       g.M % 128)
     return SD_ESHAPE;
   const dim3 grid(g.M / 128);
+  const bool es = conv_es() && (long)Nb * Hs * Ws * Ci < (1L << 29);  // buffer offsets < 2 GiB
+#define SD_FWDP(BN)                                                                                          \
+  (es ? conv_fwd16_pool<BN, true><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat) \
+      : conv_fwd16_pool<BN, false><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat))
   switch (Co) {
-    case 16: conv_fwd16_pool<16><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat); break;
-    case 32: conv_fwd16_pool<32><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat); break;
-    case 48: conv_fwd16_pool<48><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat); break;
-    case 64: conv_fwd16_pool<64><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat); break;
+    case 16: SD_FWDP(16); break;
+    case 32: SD_FWDP(32); break;
+    case 48: SD_FWDP(48); break;
+    case 64: SD_FWDP(64); break;
     default: return SD_ESHAPE;
   }
+#undef SD_FWDP
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

@@ -73,7 +73,8 @@ struct TileLoader {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int i = tid + v * 256;
-      if (i < ROWS * BK / 4) {
+      // (v + 1) * 256 <= ROWS * BK / 4: every thread's slot is inside the tile (static; hipcc cannot see tid < 256)
+      if ((v + 1) * 256 <= ROWS * BK / 4 || i < ROWS * BK / 4) {
         if (KC) {
           const int row = i / (BK / 4), kq = i % (BK / 4);
           *reinterpret_cast<f32x4*>(lds + row * LDS_ROW + 4 * kq) = r[v];
@@ -375,6 +376,9 @@ SD_DEV void gemm16_mainloop_pf(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend,
           else
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
         }
+    // keep the LDS store of the next tile behind this tile's MFMAs: hoisted into them, its vmcnt(0) wait would
+    // cut the window in which the global loads land from the whole k tile to a few MFMAs
+    __builtin_amdgcn_sched_barrier(0);
     // tile kt+1 lives in register set (u+1) % PF: stage it, then refill that set with tile kt+1+PF
     const int nx = (u + 1) % PF;  // static after unrolling
     la[nx].store(smem + (cur ^ 1) * STAGE);
@@ -399,6 +403,70 @@ SD_DEV void gemm16_mainloop_pf(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend,
   }
 }
 
+// Early-store variant for row-major LDS operands (one register set): iteration kt reads its fragments from
+// LDS[kt&1], stages tile kt+1 (loaded during iteration kt-1, so its loads had a whole MFMA phase to land) into the
+// other buffer, issues the loads of tile kt+2, and only then runs its MFMAs — the loads are in flight under the
+// MFMAs and their address arithmetic can fill the MFMA issue gaps. One barrier per k tile. Loaders should be
+// branch-free (buffer loads) so the body stays one basic block the scheduler can interleave.
+template <int BM, int BN, int WM, int WN, class OpA, class OpB>
+SD_DEV void gemm16_mainloop_es(OpA& la, OpB& lb, int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16]) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+  static_assert(!is_kmajor<OpA>::value && !is_kmajor<OpB>::value, "row-major LDS operands");
+  constexpr int SA = BM * LDS_ROW, STAGE = (BM + BN) * LDS_ROW;
+  static_assert(2 * STAGE == gemm16_smem_floats<BM, BN>(), "staging size");
+  float* smem = sd_smem<2 * STAGE>();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  const int l16 = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk <= 0) return;
+  auto ktile = [&](int t) { return kbeg + (t < nk ? t : nk - 1) * BK; };
+  la.load(ktile(0), kend);
+  lb.load(ktile(0), kend);
+  la.store(smem);
+  lb.store(smem + SA);
+  la.load(ktile(1), kend);
+  lb.load(ktile(1), kend);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const float* cur = smem + (kt & 1) * STAGE;
+    float* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+    float af[TM][8], bf[TN][8];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* p = cur + (wr * WM + 16 * i + l16) * LDS_ROW + 8 * q;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(p), x1 = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) { af[i][s] = x0[s]; af[i][4 + s] = x1[s]; }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* p = cur + SA + (wc * WN + 16 * j + l16) * LDS_ROW + 8 * q;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(p), x1 = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) { bf[j][s] = x0[s]; bf[j][4 + s] = x1[s]; }
+    }
+    la.store(nxt);
+    lb.store(nxt + SA);
+    la.load(ktile(kt + 2), kend);
+    lb.load(ktile(kt + 2), kend);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    __syncthreads();
+  }
+}
+
 template <int BM, int BN, int WM, int WN, class OpA, class OpB>
 SD_DEV void gemm16_mainloop(OpA& la, OpB& lb, int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16]) {
   OpA (&a1)[1] = *reinterpret_cast<OpA(*)[1]>(&la);
@@ -406,7 +474,7 @@ SD_DEV void gemm16_mainloop(OpA& la, OpB& lb, int kbeg, int kend, f32x4 (&acc)[W
   gemm16_mainloop_pf<BM, BN, WM, WN, 1>(a1, b1, kbeg, kend, acc);
 }
 
-template <int BM, int BN, int WM, int WN, class OpA, class OpB>
+template <int BM, int BN, int WM, int WN, bool ES = false, class OpA, class OpB>
 SD_DEV void gemm_block16(const GemmArgs& g, OpA& la, OpB& lb, int bm0, int bn0, int b, int split, int kbeg,
                          int kend) {
   constexpr int WAVES_N = BN / WN;
@@ -415,7 +483,10 @@ SD_DEV void gemm_block16(const GemmArgs& g, OpA& la, OpB& lb, int bm0, int bn0, 
   const int wr = wave / WAVES_N, wc = wave % WAVES_N;
   const int l16 = lane & 15, q = lane >> 4;
   f32x4 acc[TM][TN];
-  gemm16_mainloop<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
+  if constexpr (ES)
+    gemm16_mainloop_es<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
+  else
+    gemm16_mainloop<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
 
   // epilogue: reg r of a 16x16 tile -> row 4q + r, col l16
   if (g.ksplit > 1) {

@@ -32,7 +32,9 @@ def main():
         dy = torch.randn(Nb, H, H, Co, device="cuda")
         fl = 2.0 * Nb * H * H * Co * 25 * Ci
         wf = K.conv_flip_weight(w)
-        for name, fn in (("fwd", lambda: K.conv2d_fwd(x, w, b)), ("dgrad", lambda: K.conv2d_fwd(dy, wf, None)),
+        nw = torch.ones(Co, device="cuda")
+        for name, fn in (("fwd", lambda: K.conv2d_fwd(x, w, b)), ("fpool", lambda: K.conv2d_fwd_pool(x, w, b, nw)),
+                         ("dgrad", lambda: K.conv2d_fwd(dy, wf, None)),
                          ("wgrad", lambda: K.conv2d_wgrad(x, dy, 5, 5))):
             us = timeit(fn)
             tot[name] = tot.get(name, 0) + us
