@@ -289,7 +289,9 @@ constexpr int gemm16_smem_floats() {
   return 2 * ((AKM ? BK * (BM + 2) : BM * LDS_ROW) + (BKM ? BK * (BN + 2) : BN * LDS_ROW));
 }
 
-template <int BM, int BN, int WM, int WN, int PF = 1, class OpA, class OpB>
+// ES (early store): stage tile kt+1 and issue the loads of tile kt+1+PF BEFORE this tile's MFMAs (after its fragment
+// reads), so the loads' address arithmetic fills the MFMA issue gaps; otherwise after them.
+template <int BM, int BN, int WM, int WN, int PF = 1, bool ES = false, class OpA, class OpB>
 SD_DEV void gemm16_mainloop_pf(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16],
                                bool accumulate = false) {
   constexpr int WAVES_N = BN / WN;
@@ -365,6 +367,14 @@ SD_DEV void gemm16_mainloop_pf(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend,
         for (int s = 0; s < 4; ++s) { bf[j][s] = x0[s]; bf[j][4 + s] = x1[s]; }
       }
     }
+    // tile kt+1 lives in register set (u+1) % PF: stage it, then refill that set with tile kt+1+PF
+    const int nx = (u + 1) % PF;  // static after unrolling
+    if constexpr (ES) {
+      la[nx].store(smem + (cur ^ 1) * STAGE);
+      lb[nx].store(smem + (cur ^ 1) * STAGE + SA);
+      la[nx].load(ktile(kt + 1 + PF), kend);
+      lb[nx].load(ktile(kt + 1 + PF), kend);
+    }
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -376,15 +386,17 @@ SD_DEV void gemm16_mainloop_pf(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend,
           else
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
         }
-    // keep the LDS store of the next tile behind this tile's MFMAs: hoisted into them, its vmcnt(0) wait would
-    // cut the window in which the global loads land from the whole k tile to a few MFMAs
-    __builtin_amdgcn_sched_barrier(0);
-    // tile kt+1 lives in register set (u+1) % PF: stage it, then refill that set with tile kt+1+PF
-    const int nx = (u + 1) % PF;  // static after unrolling
-    la[nx].store(smem + (cur ^ 1) * STAGE);
-    lb[nx].store(smem + (cur ^ 1) * STAGE + SA);
-    la[nx].load(ktile(kt + 1 + PF), kend);
-    lb[nx].load(ktile(kt + 1 + PF), kend);
+    if constexpr (!ES) {
+      // keep the LDS store of the next tile behind this tile's MFMAs: hoisted into them, its vmcnt(0) wait would
+      // cut the window in which the global loads land from the whole k tile to a few MFMAs
+#ifndef SD_NO_SCHED_BARRIER
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+      la[nx].store(smem + (cur ^ 1) * STAGE);
+      lb[nx].store(smem + (cur ^ 1) * STAGE + SA);
+      la[nx].load(ktile(kt + 1 + PF), kend);
+      lb[nx].load(ktile(kt + 1 + PF), kend);
+    }
     __syncthreads();
   };
   int kt = 0;

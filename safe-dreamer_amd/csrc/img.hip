@@ -18,6 +18,7 @@
 #include "philox.h"
 #include "sdhip.h"
 
+
 namespace {
 using namespace sdg;
 
@@ -32,7 +33,8 @@ struct AStage {
   f32x4 r[NV];
   SD_DEV static int row(int v) { return (threadIdx.x + 256 * v) / (BK / 4); }
   SD_DEV static int kq(int v) { return (threadIdx.x + 256 * v) % (BK / 4); }
-  SD_DEV static bool live(int v) { return threadIdx.x + 256 * v < BM * BK / 4; }
+  // static when slot v is full for every thread (hipcc cannot see threadIdx.x < 256): no branch in the k loop
+  SD_DEV static bool live(int v) { return 256 * (v + 1) <= BM * BK / 4 || threadIdx.x + 256 * v < BM * BK / 4; }
   SD_DEV void store(float* lds) const {
 #pragma unroll
     for (int v = 0; v < NV; ++v)
@@ -128,7 +130,7 @@ struct BRows {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int i = threadIdx.x + 256 * v;
-      if (i < BN * BK / 4) {
+      if (256 * (v + 1) <= BN * BK / 4 || i < BN * BK / 4) {
         const int lr = i / (BK / 4), kq = i % (BK / 4);
         const long gr = base + (lr / seg) * stride + lr % seg;
         r[v] = ld4(W + gr * ld + k0 + 4 * kq);
@@ -139,7 +141,8 @@ struct BRows {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int i = threadIdx.x + 256 * v;
-      if (i < BN * BK / 4) *reinterpret_cast<f32x4*>(lds + (i / (BK / 4)) * LDS_ROW + 4 * (i % (BK / 4))) = r[v];
+      if (256 * (v + 1) <= BN * BK / 4 || i < BN * BK / 4)
+        *reinterpret_cast<f32x4*>(lds + (i / (BK / 4)) * LDS_ROW + 4 * (i % (BK / 4))) = r[v];
     }
   }
 };
@@ -155,10 +158,10 @@ SD_DEV Lane lane_ids() {
   return Lane{lane & 15, lane >> 4, wave / (BN / WN), wave % (BN / WN)};
 }
 
-// out[m][n] = acc + bias[n]; part[(n0 + wc*WN)/WN * M + m] = sum over the wave's WN columns of out^2
+// out[m][n] = acc + bias[n] (+ add[m][n]); part[(n0 + wc*WN)/WN * M + m] = sum over the wave's WN columns of out^2
 template <int BM, int BN, int WN>
 SD_DEV void ep_bias_part(const f32x4 (&acc)[1][WN / 16], const float* bias, float* out, long ldo, float* part, int M,
-                         int m0, int n0) {
+                         int m0, int n0, const float* add = nullptr) {
   constexpr int TN = WN / 16;
   const Lane L = lane_ids<BN, WN>();
   float ss[4] = {0.f, 0.f, 0.f, 0.f};
@@ -169,7 +172,8 @@ SD_DEV void ep_bias_part(const f32x4 (&acc)[1][WN / 16], const float* bias, floa
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + L.wr * 16 + 4 * L.q + r;
-      const float v = acc[0][j][r] + bv;
+      float v = acc[0][j][r] + bv;
+      if (add && m < M) v += add[(long)m * ldo + n];
       if (m < M) out[(long)m * ldo + n] = v;
       ss[r] += v * v;
     }
@@ -193,24 +197,26 @@ struct LinProb {
   float* out;
   long ldo;
   float* part;
+  const float* add;  // optional (M, ldo) term added before the row partials (a K-split layer's first part)
 };
 
-// grouped plain-A linear layers (N = 256 each): out = A . W^T + b, with row partials. grid (N/BN, M/BM, nprob)
+// grouped plain-A linear layers (N = 256 each): out = A . W^T + b (+ add), with row partials. grid (N/BN, M/BM, nprob)
 template <int BM, int BN>
-__global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, int M) {
+__global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2, int M) {
   constexpr int WN = BN / (4 / (BM / 16));
-  const LinProb p = blockIdx.z ? p1 : p0;
+  const LinProb p = blockIdx.z == 0 ? p0 : (blockIdx.z == 1 ? p1 : p2);
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const APlain<BM> a0(p.A, p.lda, m0, M, p.K);
   const BRows<BN> b0(p.W, p.ldw, n0, BN, 0);
   APlain<BM> la[3] = {a0, a0, a0};
   BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][WN / 16];
-  gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, p.K, acc);
-  ep_bias_part<BM, BN, WN>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0);
+  gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, p.K, acc);
+  ep_bias_part<BM, BN, WN>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
 }
 
 // out = silu(rms(X)) . W^T + b (MLP hidden layer after the first), with row partials
+// early-store main loop order (gemm16_mainloop_pf ES): measured faster here, slower in the other imagination kernels
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw, const float* part_in, int np, int K,
                                                 const float* W, const float* bias, float* out, float* part, int M,
@@ -224,7 +230,7 @@ __global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw,
   ARms<BM> la[3] = {a0, a0, a0};
   BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][WN / 16];
-  gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, K, acc);
+  gemm16_mainloop_pf<BM, BN, 16, WN, 3, true>(la, lb, 0, K, acc);
   ep_bias_part<BM, BN, WN>(acc, bias, out, gridDim.x * BN, part, M, m0, n0);
 }
 
@@ -247,28 +253,28 @@ __global__ __launch_bounds__(256) void k_hid(sd_imagine d, const float* h, long 
     const BRows<BN> b0(Wseg, Ig, 0, BN, 0);
     APlain<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, Dg, acc);
+    gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, Dg, acc);
   }
   {
     const ARms<BM> a0(x0p, U, d.n0, rs0, m0, M, U);
     const BRows<BN> b0(Wseg + Dg, Ig, 0, BN, 0);
     ARms<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
+    gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, U, acc, true);
   }
   {
     const ARms<BM> a0(x1p, U, d.n1, rs1, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + U, Ig, 0, BN, 0);
     ARms<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
+    gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, U, acc, true);
   }
   {
     const APlain<BM> a0(x2, U, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + 2 * U, Ig, 0, BN, 0);
     APlain<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
+    gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, U, acc, true);
   }
   ep_bias_part<BM, BN, WN>(acc, d.bh, hp, d.D, ph, M, m0, n0);
 }
@@ -287,7 +293,7 @@ __global__ __launch_bounds__(256) void k_gate(sd_imagine d, const float* hp, con
   ARms<BM> la[2] = {a0, a0};
   BRows<BN> lb[2] = {b0, b0};
   f32x4 acc[1][6];
-  gemm16_mainloop_pf<BM, BN, 16, BN, 2>(la, lb, 0, Dg, acc);
+  gemm16_mainloop_pf<BM, BN, 16, BN, 2, false>(la, lb, 0, Dg, acc);
   const Lane L = lane_ids<BN, BN>();
   const float* bg = d.bg + (long)g * 3 * Dg;
 #pragma unroll
@@ -324,7 +330,7 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
   ARms<BM> la[3] = {a0, a0, a0};
   BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][1];
-  gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, U, acc);
+  gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, U, acc);
   const Lane L = lane_ids<BN, WN>();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -370,7 +376,7 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
   ARms<BM> la[3] = {a0, a0, a0};
   BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][1];
-  gemm16_mainloop_pf<BM, BN, 16, WN, 3>(la, lb, 0, U, acc);
+  gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, U, acc);
   const Lane L = lane_ids<BN, WN>();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -450,7 +456,7 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
 
 // ------------------------------------------------------------------------------------------- host side
 struct IWork {
-  float *a[2], *pa[2], *x0p, *px0, *x1p, *px1, *x2, *hp, *ph, *i[2], *pi[2];
+  float *a[2], *pa[2], *ad, *x0p, *px0, *x1p, *px1, *x2, *hp, *ph, *i[2], *pi[2];
   long total;
 };
 long al64(long n) { return (n + 63) / 64 * 64; }
@@ -460,6 +466,7 @@ IWork iwork(const sd_imagine& d, float* base) {
   auto take = [&](long n) { float* p = base ? base + o : nullptr; o += al64(n); return p; };
   const long NU = (long)d.N * d.U, NP = (long)d.N * (d.U / 32);
   for (int k = 0; k < 2; ++k) { w.a[k] = take(NU); w.pa[k] = take(NP); }
+  w.ad = take(NU);
   w.x0p = take(NU); w.px0 = take(NP);
   w.x1p = take(NU); w.px1 = take(NP);
   w.x2 = take(NU);
@@ -500,17 +507,21 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   const int npU = U / 32;  // row partials per hidden row (k_lin / k_rmslin with BM = 32, BN = 64 -> WN = 32)
   const dim3 g32(U / 64, sd_cdiv(N, 32));
   auto feats = [&](int t) { return d.feats + t * NF; };
-  {  // x0p(0) = h0 . W0^T + b0
-    LinProb p{feats(0) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0};
-    k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), 1), 256, 0, st>>>(p, p, N);
+  // actor layer 0 on feat = [stoch, deter] is K-split: the deter part (no bias) runs in the launch that already
+  // reads deter' (img_net_0 / _dyn_in0), the stoch part (+ bias + deter part, row partials) after the prior sample
+  const float* Wa0d = d.Wa[0] + SK;  // (U, F) columns SK.. of the actor's first weight
+  {  // x0p(0) = h0 . W0^T + b0 and the deter part of actor layer 0 at t = 0
+    LinProb p{feats(0) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
+    LinProb pd{feats(0) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
+    k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), 2), 256, 0, st>>>(p, pd, pd, N);
     SD_LAUNCH_CHECK();
   }
   for (int t = 0; t < d.H1; ++t) {
     const bool last = t == d.H1 - 1;
-    {  // actor layer 0 on feat = [stoch, deter]; _dyn_in1 on stoch
-      LinProb pa{feats(t), F, F, d.Wa[0], F, d.ba[0], w.a[0], U, w.pa[0]};
-      LinProb px{feats(t), F, SK, d.W1, SK, d.b1, w.x1p, U, w.px1};
-      k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, N);
+    {  // actor layer 0, stoch part (+ deter part); _dyn_in1 on stoch
+      LinProb pa{feats(t), F, SK, d.Wa[0], F, d.ba[0], w.a[0], U, w.pa[0], w.ad};
+      LinProb px{feats(t), F, SK, d.W1, SK, d.b1, w.x1p, U, w.px1, nullptr};
+      k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, px, N);
       SD_LAUNCH_CHECK();
     }
     int cur = 0;
@@ -528,10 +539,11 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     SD_LAUNCH_CHECK();
     k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / 64, feats(t) + SK, feats(t + 1) + SK, F);
     SD_LAUNCH_CHECK();
-    {  // img_net_0 and the next step's _dyn_in0 share A = deter'
-      LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0]};
-      LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0};
-      k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), 2), 256, 0, st>>>(pi, px, N);
+    {  // img_net_0, the next step's _dyn_in0 and the deter part of its actor layer 0 share A = deter'
+      LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};
+      LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
+      LinProb pd{feats(t + 1) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
+      k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), 3), 256, 0, st>>>(pi, px, pd, N);
       SD_LAUNCH_CHECK();
     }
     int ci = 0;
