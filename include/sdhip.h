@@ -267,9 +267,15 @@ typedef struct sd_imagine {
   float* feats;
   float* actions;                                                /* (H1, N, A) */
   float* work;
+  int t_begin, t_end; /* run steps [t_begin, t_end) (t_end <= 0: H1); chunks share `work` and run in order */
 } sd_imagine;
 int sd_imagine_work_floats(const sd_imagine* d);
 int sd_imagine_run(const sd_imagine* d, sd_stream stream);
+
+/* Profiling aid: store the device wall clock (constant rate, sd_wall_clock_khz) into buf[idx] when `stream` reaches
+ * this point; capturable into a HIP graph. Not part of the reference interface. */
+int sd_mark(uint64_t* buf, int idx, sd_stream stream);
+int sd_wall_clock_khz(int device);
 
 #ifdef __cplusplus
 }

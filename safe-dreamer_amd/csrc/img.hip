@@ -485,6 +485,7 @@ int icheck(const sd_imagine* d) {
   if (d->A < 1 || (d->act_discrete ? d->A > 16 : 2 * d->A > 32)) return SD_ESHAPE;
   if (d->actor_layers < 1 || d->actor_layers > 4 || d->img_layers < 1 || d->img_layers > 4) return SD_ESHAPE;
   if ((d->SK + d->D) % 32) return SD_ESHAPE;
+  if (d->t_begin < 0 || d->t_begin >= (d->t_end > 0 ? d->t_end : d->H1) || d->t_end > d->H1) return SD_EARG;
   return SD_OK;
 }
 
@@ -510,13 +511,14 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   // actor layer 0 on feat = [stoch, deter] is K-split: the deter part (no bias) runs in the launch that already
   // reads deter' (img_net_0 / _dyn_in0), the stoch part (+ bias + deter part, row partials) after the prior sample
   const float* Wa0d = d.Wa[0] + SK;  // (U, F) columns SK.. of the actor's first weight
-  {  // x0p(0) = h0 . W0^T + b0 and the deter part of actor layer 0 at t = 0
+  const int t_end = d.t_end > 0 ? d.t_end : d.H1;
+  if (d.t_begin == 0) {  // x0p(0) = h0 . W0^T + b0 and the deter part of actor layer 0 at t = 0
     LinProb p{feats(0) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
     LinProb pd{feats(0) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
     k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), 2), 256, 0, st>>>(p, pd, pd, N);
     SD_LAUNCH_CHECK();
   }
-  for (int t = 0; t < d.H1; ++t) {
+  for (int t = d.t_begin; t < t_end; ++t) {
     const bool last = t == d.H1 - 1;
     {  // actor layer 0, stoch part (+ deter part); _dyn_in1 on stoch
       LinProb pa{feats(t), F, SK, d.Wa[0], F, d.ba[0], w.a[0], U, w.pa[0], w.ad};

@@ -250,3 +250,22 @@ extern "C" int sd_barlow_dc(const float* c, const float* g, float* dc, int E, fl
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
+
+// ---- timeline marks (profiling aid): one thread stores the constant-rate wall clock into buf[idx]; enqueued on a
+// stream (and capturable into a HIP graph) it timestamps the point the stream has reached
+namespace {
+__global__ void mark_kernel(unsigned long long* buf, int idx) { buf[idx] = wall_clock64(); }
+}  // namespace
+
+extern "C" int sd_mark(uint64_t* buf, int idx, sd_stream stream) {
+  if (!buf || idx < 0) return SD_EARG;
+  mark_kernel<<<1, 1, 0, (hipStream_t)stream>>>(reinterpret_cast<unsigned long long*>(buf), idx);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_wall_clock_khz(int device) {
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, device) != hipSuccess) return SD_EARG;
+  return v;
+}

@@ -238,6 +238,11 @@ __global__ __launch_bounds__(NTHR) void k_slab(SlabProb p0, SlabProb p1, int M, 
 }
 
 // s_in[0] = mask(stoch0), h_in[0] = mask(deter0)   (rssm.py:161-165 on the initial state)
+__global__ void k_zero(float* p, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0.f;
+}
+
 __global__ void k_init(sd_rssm_scan d) {
   const long nS = (long)d.B * d.SK, nD = (long)d.B * d.D;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nS + nD; i += (long)gridDim.x * blockDim.x) {
@@ -887,8 +892,10 @@ extern "C" int sd_rssm_scan_bwd(const sd_rssm_scan* dp, sd_stream stream_) {
   const size_t lds_dl = core1 + (size_t)MR * (SK + 4) * 4;
   const size_t lds_dgru = core1 + (size_t)MR * (UH + 4) * 4;
   const size_t lds_dhp = core1 + (size_t)MR * (Dg + 4) * 4;
-  hipError_t e = hipMemsetAsync(w.ch, 0, sizeof(float) * (size_t)B * D, st);
-  if (e != hipSuccess) return (int)e;
+  // carry of the step after T-1 is zero. A kernel, not hipMemsetAsync: in a captured HIP graph the memset node was
+  // observed not to be ordered before the first k_dgru (garbage carry in replays)
+  k_zero<<<sd_cdiv(B * D, 256), 256, 0, st>>>(w.ch, (long)B * D);
+  SD_LAUNCH_CHECK();
   const int NX = (3 * UH / 16) * d.G;
   SD_KD_SWITCH(d.Kd, k_sbwd_last<KD><<<(int)(((long)B * SK + 255) / 256), 256, 0, st>>>(d));
   SD_LAUNCH_CHECK();

@@ -140,6 +140,8 @@ class Dreamer(nn.Module):
         # the actor-critic branch (imagination, policy/value/replay-value losses and their backward) depends only on the
         # detached posterior: it runs on this side stream concurrently with the world-model branch (see _cal_grad)
         self.use_side_stream = os.environ.get("SDREAMER_SIDE_STREAM", "1") != "0"
+        # SDREAMER_MARKS=1: device timestamps at the phase boundaries of every update (kernels.Marks)
+        self.marks = K.Marks(self.device) if os.environ.get("SDREAMER_MARKS", "0") != "0" else None
         self._side = torch.cuda.Stream(device=self.device)
         self._graph = None
         self._eager_updates = 0
@@ -231,6 +233,8 @@ class Dreamer(nn.Module):
             if self._graph is not None or self._eager_updates >= 2:
                 return self._update_graphed(data, initial, seed, ro)
         self._eager_updates += 1
+        if self.marks is not None:
+            self.marks.reset()
         p_data = self.preprocess(dict(data))
         self._update_slow_target()
         self._optimizer.zero_grad()
@@ -238,39 +242,90 @@ class Dreamer(nn.Module):
         if self.world > 1:
             parallel.allreduce_mean_(self._optimizer.arena.grad)
         self._optimizer.step()
+        self._mark("optimizer")
         self._scheduler.step()
         mets["opt/lr"] = self._scheduler.get_lr()[0]
         mets["opt/grad_scale"] = 1.0
         self._updates += 1
         return post, mets
 
-    def _core(self, data, initial, seed, ro):
-        """Device-only work of one update (captured once, replayed every update)."""
+    def _mark(self, tag):
+        if self.marks is not None:
+            self.marks(tag)
+
+    def _core_forward(self, data, initial, seed, ro):
+        """Graph phase P (main): preprocess, Polyak, zero_grad, encoder + posterior scan."""
+        if self.marks is not None:
+            self.marks.reset()
         p_data = self.preprocess(dict(data))
         self._polyak()
         self._optimizer.zero_grad()
-        post, mets = self._cal_grad(p_data, initial, seed, ro)
+        return self._ph_forward(p_data, initial, seed, ro)
+
+    def _core_finish(self, st):
+        """Graph phase M3 (main): merged metrics, optimizer step, metric vector."""
+        post, mets = self._ph_finish(st)
         self._optimizer.launch_step()
-        return post, mets
+        self._mark("optimizer")
+        keys = [k for k, v in mets.items() if isinstance(v, torch.Tensor)]
+        mvec = torch.stack([mets[k].float().reshape(()) for k in keys])
+        return post, keys, mvec
 
     def _update_graphed(self, data, initial, seed, ro):
+        """Replay of the update as six single-stream HIP graphs (captured once) joined by stream events:
+
+            main: P (encoder, scan fwd) ─┬─ M1 (world-model heads) ─ wait(S1) ─ M2 (posterior bwd) ─ wait(S2) ─ M3
+            side:                        └─ S1 (imagination, returns, replay value) ─ S2 (actor / critic)
+
+        One graph per stream phase keeps every graph linear: the HIP runtime launches a linear graph as a batch
+        (~0.5 ms of host time for the whole update) and the cross-stream edges become device-side event waits.
+        A single two-stream graph instead costs ~12 ms of host time per launch, stalling on each cross-stream
+        edge. Every graph has its own memory pool; tensors that cross phases are held by `self._gst`."""
         if self._graph is None:
             self._g_in = {k: v.clone() for k, v in data.items()}
             self._g_init = tuple(t.clone() for t in initial)
             self._seed_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+            side_cap = torch.cuda.Stream(device=self.device)
             torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                post, mets = self._core(self._g_in, self._g_init, self._seed_dev, ro)
-                keys = [k for k, v in mets.items() if isinstance(v, torch.Tensor)]
-                self._g_mvec = torch.stack([mets[k].float().reshape(()) for k in keys])
-            self._graph, self._g_post, self._g_keys = g, post, keys
+
+            def cap(fn, stream=None):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=stream):
+                    out = fn()
+                return g, out
+
+            gP, st = cap(lambda: self._core_forward(self._g_in, self._g_init, self._seed_dev, ro))
+            gS1, _ = cap(lambda: self._ph_side_returns(st), side_cap)
+            gM1, _ = cap(lambda: self._ph_wm(st))
+            gM2, _ = cap(lambda: self._ph_posterior_bwd(st))
+            gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
+            gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st))
+            torch.cuda.synchronize()
+            self._graph = (gP, gS1, gM1, gM2, gS2, gM3)
+            self._gst, self._g_post, self._g_keys, self._g_mvec = st, post, keys, mvec
         for k, v in data.items():
             self._g_in[k].copy_(v)
         for dst, src in zip(self._g_init, initial):
             dst.copy_(src)
         self._seed_dev.fill_(int(seed) & 0x7FFFFFFFFFFFFFFF)
-        self._graph.replay()
+        gP, gS1, gM1, gM2, gS2, gM3 = self._graph
+        main = torch.cuda.current_stream()
+        side = self._side if self.use_side_stream else main
+        gP.replay()
+        if side is not main:
+            side.wait_stream(main)
+        with torch.cuda.stream(side):
+            gS1.replay()
+            ev_s1 = torch.cuda.Event()
+            ev_s1.record()
+        gM1.replay()
+        main.wait_event(ev_s1)
+        gM2.replay()
+        with torch.cuda.stream(side):
+            gS2.replay()
+        if side is not main:
+            main.wait_stream(side)
+        gM3.replay()
         self._slow_value_updates += 1
         self._optimizer.host_steps += 1
         self._updates += 1
@@ -283,54 +338,118 @@ class Dreamer(nn.Module):
     def _cal_grad(self, data, initial, seed=0, row_offset=0):
         """dreamer.py:453-671 (fp32). data: dict of (B, T, *) device tensors, image float in [0, 1].
 
-        Same losses and gradients as the reference's single backward, scheduled as two concurrent branches after the
-        posterior scan (one process, single GPU; data parallel stays serial):
-          main stream  — world-model head losses (prior/KL, representation, reward, continue) on detached LEAF copies
-                         of the posterior, their backward down to the leaves; then, once the side stream has the
-                         replay-value gradient, one backward from the posterior into the scan and the encoder;
-          side stream  — imagination, lambda-returns, the replay-value loss (kept attached to the world model as in
-                         dreamer.py:652: its feat gradient joins the scan backward), then the policy / value losses
-                         and their backward, overlapping the launch-bound scan backward.
+        Same losses and gradients as the reference's single backward, scheduled as stream phases after the posterior
+        scan (single GPU; data parallel stays on one stream):
+          main — world-model head losses (prior/KL, representation, reward, continue) on detached LEAF copies of the
+                 posterior and their backward down to the leaves; then, once the side stream has the replay-value
+                 gradient, one backward from the posterior into the scan and the encoder;
+          side — imagination, imagined heads, lambda-returns + ReturnEMA, the replay-value loss (kept attached to the
+                 world model as in dreamer.py:652: its feat gradient joins the scan backward) and its backward, then
+                 the policy / value losses and their backward, overlapping the launch-bound scan backward.
         Gradient writes of the two streams touch disjoint parameters; value-head gradients come only from the side
-        stream (replay value, then imagined value, in stream order)."""
-        B, T = data["action"].shape[:2]
-        SK = self.rssm.flat_stoch
-        embed = self.encoder(data)
-        post_stoch, post_deter, post_logit = self.rssm.observe(embed, data["action"], initial, data["is_first"],
-                                                               seed=seed, row_offset=row_offset)
-        leaves = [t.detach().requires_grad_(True) for t in (post_stoch, post_deter, post_logit)]
-        feat_l = self.rssm.get_feat(leaves[0], leaves[1])
-        feat_r = feat_l.detach().requires_grad_(True)  # replay-value leaf (side stream)
+        stream (replay value, then imagined value, in stream order). Graph mode captures each phase separately
+        (_update_graphed)."""
+        st = self._ph_forward(data, initial, seed, row_offset)
         main = torch.cuda.current_stream()
         side = self._side if (self.use_side_stream and self.world == 1) else main
         if side is not main:
             side.wait_stream(main)
-            for t in (post_stoch, post_deter, feat_r, data["reward"], data["is_last"], data["is_terminal"]):
+            for t in (st["post_stoch"], st["post_deter"], st["feat_r"], data["reward"], data["is_last"],
+                      data["is_terminal"]):
                 t.record_stream(side)
         with torch.cuda.stream(side):
-            repval_done, ac_total, ac_losses, ac_metrics, ac_last = self._ac_branch(data, post_stoch, post_deter,
-                                                                                   feat_r, seed, row_offset)
-        wm_total, losses, metrics = self._wm_heads(data, embed, leaves, feat_l)
-        # phase 2 (main): posterior gradient = head-loss leaf grads + replay-value feat grad -> scan + encoder
+            self._ph_side_returns(st)
+            ev_s1 = torch.cuda.Event()
+            ev_s1.record()
+        self._ph_wm(st)
         if side is not main:
-            main.wait_event(repval_done)
-            feat_r.grad.record_stream(main)
-        g_feat = feat_r.grad
+            main.wait_event(ev_s1)
+            st["feat_r"].grad.record_stream(main)
+        self._ph_posterior_bwd(st)
+        with torch.cuda.stream(side):
+            self._ph_side_ac(st)
+        if side is not main:
+            main.wait_stream(side)
+            for k in ("ac_losses", "ac_metrics", "rv_metrics"):
+                for v in st[k].values():
+                    v.record_stream(main)
+            st["repval"].record_stream(main)
+        return self._ph_finish(st)
+
+    def _ph_forward(self, data, initial, seed, ro):
+        """main: encoder + posterior scan (dreamer.py:453-470); detached leaves for the two branches."""
+        mk = self._mark
+        mk("start")
+        embed = self.encoder(data)
+        mk("encoder_fwd")
+        post_stoch, post_deter, post_logit = self.rssm.observe(embed, data["action"], initial, data["is_first"],
+                                                               seed=seed, row_offset=ro)
+        mk("scan_fwd")
+        if self.marks is not None and embed.requires_grad:
+            embed.register_hook(lambda g: mk("scan_bwd"))
+        leaves = [t.detach().requires_grad_(True) for t in (post_stoch, post_deter, post_logit)]
+        feat_l = self.rssm.get_feat(leaves[0], leaves[1])
+        feat_r = feat_l.detach().requires_grad_(True)  # replay-value leaf (side stream)
+        return dict(data=data, seed=seed, ro=ro, embed=embed, post_stoch=post_stoch, post_deter=post_deter,
+                    post_logit=post_logit, leaves=leaves, feat_l=feat_l, feat_r=feat_r)
+
+    def _ph_side_returns(self, st):
+        """side: imagination (dreamer.py:578-597), imagined heads, lambda-returns + ReturnEMA (598-636), replay value
+        (638-652) and its backward."""
+        data = st["data"]
+        B, T = data["action"].shape[:2]
+        N, H1 = B * T, self.imag_horizon + 1
+        self._mark("side:fork")
+        start = (st["post_stoch"].detach().reshape(N, self.rssm._stoch, self.rssm._discrete),
+                 st["post_deter"].detach().reshape(N, self.rssm._deter))
+        ifeat, iact = self._imagine_tm(start, H1, st["seed"], st["ro"] * T)
+        self._mark("side:imagine")
+        rr = self._heads_returns(ifeat)
+        self._mark("side:heads_returns")
+        rv = self._repval_pre(data, st["feat_r"])
+        loss, rv_metrics, rret = self._repval_post(data, rv, rr["ret"])
+        (loss * self._loss_scales["repval"]).backward()
+        self._mark("side:repval")
+        st.update(ifeat=ifeat, iact=iact, rr=rr, repval=loss, rv_metrics=rv_metrics, rret=rret)
+
+    def _ph_wm(self, st):
+        """main: world-model head losses and their backward down to the posterior leaves."""
+        st["wm_total"], st["wm_losses"], st["wm_metrics"] = self._wm_heads(st["data"], st["embed"], st["leaves"],
+                                                                           st["feat_l"])
+        self._mark("wm_heads")
+
+    def _ph_posterior_bwd(self, st):
+        """main: posterior gradient = head-loss leaf grads + replay-value feat grad -> scan + encoder backward."""
+        SK = self.rssm.flat_stoch
+        leaves = st["leaves"]
+        self._mark("repval_wait")
+        g_feat = st["feat_r"].grad
         lg = [l.grad if l.grad is not None else torch.zeros_like(l) for l in leaves]
         g_stoch = lg[0] + g_feat[..., :SK].reshape(leaves[0].shape)
         g_deter = lg[1] + g_feat[..., SK:]
-        torch.autograd.backward([post_stoch, post_deter, post_logit], [g_stoch, g_deter, lg[2]])
-        if side is not main:
-            main.wait_stream(side)
-            for v in list(ac_losses.values()) + list(ac_metrics.values()) + list(ac_last.values()) + [ac_total]:
-                v.record_stream(main)
-        losses.update(ac_losses)
-        metrics.update(ac_metrics)
-        total = wm_total + ac_total
+        torch.autograd.backward([st["post_stoch"], st["post_deter"], st["post_logit"]], [g_stoch, g_deter, lg[2]])
+        self._mark("encoder_bwd")
+
+    def _ph_side_ac(self, st):
+        """side: policy / value losses on the imagined trajectories and their backward."""
+        st["ac_losses"], st["ac_metrics"] = self._ac_losses(st["ifeat"], st["iact"], st["rr"])
+        self._mark("side:actor_critic")
+
+    def _ph_finish(self, st):
+        losses, metrics = dict(st["wm_losses"]), dict(st["wm_metrics"])
+        self._mark("join")
+        losses["repval"] = st["repval"]
+        losses.update(st["ac_losses"])
+        metrics.update(st["rv_metrics"])
+        metrics.update(st["ac_metrics"])
+        total = st["wm_total"] + sum(v.detach() * self._loss_scales[k] for k, v in losses.items()
+                                     if k in ("repval", "policy", "value"))
         metrics.update({f"loss/{k}": v.detach() for k, v in losses.items()})
         metrics["opt/loss"] = total.detach()
-        self._last = dict(embed=embed, post_logit=post_logit, prior_logit=self._prior_logit, **ac_last)
-        return (post_stoch, post_deter), metrics
+        rr = st["rr"]
+        self._last = dict(embed=st["embed"], post_logit=st["post_logit"], prior_logit=self._prior_logit,
+                          imag_feat_tm=st["ifeat"], imag_action_tm=st["iact"], ret=rr["ret"], rret=st["rret"])
+        return (st["post_stoch"], st["post_deter"]), metrics
 
     def _wm_heads(self, data, embed, leaves, feat):
         """World-model losses (dreamer.py:453-576) on the posterior leaves, backward down to the leaves."""
@@ -366,59 +485,69 @@ class Dreamer(nn.Module):
         wm_total.backward()
         return wm_total, losses, metrics
 
-    def _ac_branch(self, data, post_stoch, post_deter, feat_r, seed, row_offset):
-        """Imagination, lambda-returns, replay value (dreamer.py:578-664) and the policy / value losses with their
-        backward. feat_r: detached posterior feat leaf; its .grad (the replay-value gradient into the world model) is
-        ready when the returned event fires."""
-        losses, metrics = {}, {}
+    def _repval_pre(self, data, feat_r):
+        """Replay-value parts that do not need the imagined returns (dreamer.py:638-652): value / slow-value modes on
+        the replay posterior, the value head forward (with grad) and the slow-target log-prob."""
         B, T = data["action"].shape[:2]
-        S, Kd, D = self.rssm._stoch, self.rssm._discrete, self.rssm._deter
-        # ---- imagination (dreamer.py:578-636); time-major (H1, N, .)
         N = B * T
-        H1 = self.imag_horizon + 1
-        H = H1 - 1
-        start = (post_stoch.detach().reshape(N, S, Kd), post_deter.detach().reshape(N, D))
-        ifeat, iact = self._imagine_tm(start, H1, seed, row_offset * T)
-        flat = ifeat.reshape(H1 * N, -1)
         with torch.no_grad():
-            i_rew = K.twohot_mode(self.reward.logits_nograd(flat), self.rbins).view(H1, N)
-            i_contl = self.cont.logits_nograd(flat).view(H1, N)
-            i_val = K.twohot_mode(self.value.logits_nograd(flat), self.vbins).view(H1, N)
-            i_slow = K.twohot_mode(self._slow_value.logits_nograd(flat), self.vbins).view(H1, N)
-            disc = 1 - 1 / self.horizon
-            rew_n, contl_n, val_n = i_rew.t().contiguous(), i_contl.t().contiguous(), i_val.t().contiguous()
-            i_cont = torch.empty(N, H1, device=self.device)
-            weight = torch.empty(N, H1, device=self.device)
-            ret = K.lambda_return(rew_n, val_n, disc, self.lamb, cont_logit=contl_n, cont_out=i_cont,
-                                  weight_out=weight)  # (N, H)
-            ret_all = parallel.gather_returns(ret, self.world)
-            ret_offset, ret_scale = self.return_ema(ret_all)
-            adv = (ret - val_n[:, :-1]) / ret_scale
+            fd = feat_r.detach().reshape(N, -1)
+            value = K.twohot_mode(self.value.logits_nograd(fd), self.vbins).view(B, T)
+            slow_value = K.twohot_mode(self._slow_value.logits_nograd(fd), self.vbins).view(B, T)
+        vd = self.value(feat_r[:, :-1])
+        lp_s = ops.TwoHotLogProbFn.apply(vd, self.vbins, slow_value[:, :-1].contiguous().reshape(-1))
+        return dict(value=value, slow_value=slow_value, vd=vd, lp_s=lp_s)
 
-        # ---- replay value (dreamer.py:638-664), attached to the world model through feat_r
+    def _repval_post(self, data, rv, ret):
+        """Replay lambda-return bootstrapped from the imagined return (dreamer.py:645) and the replay-value loss."""
+        B, T = data["action"].shape[:2]
+        H = self.imag_horizon
+        disc = 1 - 1 / self.horizon
         with torch.no_grad():
             last = data["is_last"].float().reshape(B, T)
             term = data["is_terminal"].float().reshape(B, T)
             reward = data["reward"].float().reshape(B, T)
-            fd = feat_r.detach().reshape(N, -1)
-            value = K.twohot_mode(self.value.logits_nograd(fd), self.vbins).view(B, T)
-            slow_value = K.twohot_mode(self._slow_value.logits_nograd(fd), self.vbins).view(B, T)
-            # boot = imag ret[:, 0] (dreamer.py:645): ret is (N, H) with N = (b, t)
+            # boot = imag ret[:, 0]: ret is (N, H) with N = (b, t)
             rret = K.lambda_return(reward.contiguous(), ret, disc, self.lamb, term=term.contiguous(),
                                    last=last.contiguous(), boot_row_stride=T * H, boot_t_stride=H)  # (B, T-1)
-        vd = self.value(feat_r[:, :-1])
-        lp_r = ops.TwoHotLogProbFn.apply(vd, self.vbins, rret.reshape(-1))
-        lp_s = ops.TwoHotLogProbFn.apply(vd, self.vbins, slow_value[:, :-1].contiguous().reshape(-1))
-        losses["repval"] = torch.mean((1.0 - last[:, :-1]) * (-lp_r - lp_s))
-        (losses["repval"] * self._loss_scales["repval"]).backward()
-        repval_done = torch.cuda.Event()
-        repval_done.record()
+        lp_r = ops.TwoHotLogProbFn.apply(rv["vd"], self.vbins, rret.reshape(-1))
+        loss = torch.mean((1.0 - last[:, :-1]) * (-lp_r - rv["lp_s"]))
+        metrics = {}
         with torch.no_grad():
             metrics.update(_tstats(rret, "ret_replay"))
-            metrics.update(_tstats(value, "value_replay"))
-            metrics.update(_tstats(slow_value, "slow_value_replay"))
+            metrics.update(_tstats(rv["value"], "value_replay"))
+            metrics.update(_tstats(rv["slow_value"], "slow_value_replay"))
+        return loss, metrics, rret
 
-        # ---- actor / critic on the imagined trajectories
+    @torch.no_grad()
+    def _heads_returns(self, ifeat):
+        """Imagined reward / continue / value / slow-value heads (dreamer.py:598-622), lambda-returns, ReturnEMA and
+        the advantage (dreamer.py:623-636)."""
+        H1, N = ifeat.shape[:2]
+        dev = ifeat.device
+        flat = ifeat.reshape(H1 * N, -1)
+        i_rew = K.twohot_mode(self.reward.logits_nograd(flat), self.rbins).view(H1, N)
+        i_contl = self.cont.logits_nograd(flat).view(H1, N)
+        i_val = K.twohot_mode(self.value.logits_nograd(flat), self.vbins).view(H1, N)
+        i_slow = K.twohot_mode(self._slow_value.logits_nograd(flat), self.vbins).view(H1, N)
+        disc = 1 - 1 / self.horizon
+        rew_n, contl_n, val_n = i_rew.t().contiguous(), i_contl.t().contiguous(), i_val.t().contiguous()
+        i_cont = torch.empty(N, H1, device=dev)
+        weight = torch.empty(N, H1, device=dev)
+        ret = K.lambda_return(rew_n, val_n, disc, self.lamb, cont_logit=contl_n, cont_out=i_cont,
+                              weight_out=weight)  # (N, H)
+        ret_all = parallel.gather_returns(ret, self.world)
+        ret_offset, ret_scale = self.return_ema(ret_all)
+        adv = (ret - val_n[:, :-1]) / ret_scale
+        return dict(ret=ret, weight=weight, adv=adv, i_cont=i_cont, i_rew=i_rew, i_val=i_val, i_slow=i_slow,
+                    ret_offset=ret_offset, ret_scale=ret_scale)
+
+    def _ac_losses(self, ifeat, iact, rr):
+        """Policy and value losses on the imagined trajectories (dreamer.py:653-671) and their backward."""
+        losses, metrics = {}, {}
+        H1, N = ifeat.shape[:2]
+        H = H1 - 1
+        ret, weight, adv, i_slow = rr["ret"], rr["weight"], rr["adv"], rr["i_slow"]
         pl = self.actor(ifeat[:H].reshape(H * N, -1))
         if self.act_discrete:
             logpi, ent = ops.OneHotLogProbEntFn.apply(pl, iact[:H].reshape(H * N, -1),
@@ -436,23 +565,21 @@ class Dreamer(nn.Module):
         losses["value"] = torch.mean(w * (-lp_tar - lp_slow).view(H, N).t())
         (losses["policy"] * self._loss_scales["policy"] + losses["value"] * self._loss_scales["value"]).backward()
         with torch.no_grad():
-            ret_normed = (ret - ret_offset) / ret_scale
+            ret_normed = (ret - rr["ret_offset"]) / rr["ret_scale"]
             metrics["ret"] = ret_normed.mean()
             metrics["ret_005"] = self.return_ema.ema_vals[0].clone()
             metrics["ret_095"] = self.return_ema.ema_vals[1].clone()
             metrics["adv"] = adv.mean()
             metrics["adv_std"] = adv.std()
-            metrics["con"] = i_cont.mean()
-            metrics["rew"] = i_rew.mean()
-            metrics["val"] = i_val.mean()
+            metrics["con"] = rr["i_cont"].mean()
+            metrics["rew"] = rr["i_rew"].mean()
+            metrics["val"] = rr["i_val"].mean()
             metrics["tar"] = ret.mean()
             metrics["slowval"] = i_slow.mean()
             metrics["weight"] = weight.mean()
             metrics["action_entropy"] = ent.detach().mean()
             metrics.update(_tstats(iact, "action"))
-        ac_total = sum(v.detach() * self._loss_scales[k] for k, v in losses.items())
-        return repval_done, ac_total, losses, metrics, dict(imag_feat_tm=ifeat, imag_action_tm=iact, ret=ret,
-                                                             rret=rret)
+        return losses, metrics
 
     @torch.no_grad()
     def _fused_imag_ok(self):
@@ -466,8 +593,10 @@ class Dreamer(nn.Module):
             (A <= 16 if self.act_discrete else 2 * A <= 32) and 1 <= a.mlp.n <= 4 and 1 <= r._img_layers <= 4 and \
             a.last.weight.shape[0] <= 32
 
-    def _imagine_fused(self, feats, actions, H1, seed, row_offset):
-        """sd_imagine_run (csrc/img.hip): feats[0] holds the start state."""
+    def _imagine_fused(self, feats, actions, H1, seed, row_offset, chunks=None):
+        """sd_imagine_run (csrc/img.hip): feats[0] holds the start state. chunks: step boundaries [t0, t1, ..., H1];
+        the steps run as one launch sequence per chunk with an event recorded after each (returned), so consumers on
+        other streams can start on a chunk's feats while the next chunk is imagined."""
         r, a = self.rssm, self.actor
         N = feats.shape[1]
         P = r._p()
@@ -501,11 +630,21 @@ class Dreamer(nn.Module):
             raise nat.NativeError(f"sd_imagine_work_floats failed with status {nwork}")
         work = torch.empty(nwork, dtype=torch.float32, device=feats.device)
         d.work = work.data_ptr()
-        nat.call("sd_imagine_run", ctypes.addressof(d), K.stream())
+        bounds = list(chunks) if chunks else [0, H1]
+        events = []
+        for t0, t1 in zip(bounds[:-1], bounds[1:]):
+            d.t_begin, d.t_end = int(t0), int(t1)
+            nat.call("sd_imagine_run", ctypes.addressof(d), K.stream())
+            if chunks:
+                ev = torch.cuda.Event()
+                ev.record()
+                events.append(ev)
+        return events
 
-    def _imagine_tm(self, start, H1, seed, row_offset=0):
+    def _imagine_tm(self, start, H1, seed, row_offset=0, chunks=None):
         """Dreamer._imagine (dreamer.py:673-692), time-major: feats (H1, N, F), actions (H1, N, A).
-        The reference's last img_step (whose output is discarded) is skipped."""
+        The reference's last img_step (whose output is discarded) is skipped. With `chunks` (step boundaries) returns
+        (feats, actions, events) with one event per chunk (see _imagine_fused)."""
         stoch, deter = start
         N = deter.shape[0]
         SK = self.rssm.flat_stoch
@@ -516,8 +655,8 @@ class Dreamer(nn.Module):
         if self._fused_imag_ok():
             feats[0, :, :SK] = s
             feats[0, :, SK:] = h
-            self._imagine_fused(feats, actions, H1, seed, row_offset)
-            return feats, actions
+            events = self._imagine_fused(feats, actions, H1, seed, row_offset, chunks)
+            return (feats, actions, events) if chunks else (feats, actions)
         for t in range(H1):
             feats[t, :, :SK] = s
             feats[t, :, SK:] = h
@@ -527,6 +666,10 @@ class Dreamer(nn.Module):
                 break
             h = self.rssm._deter_fwd(s, h, K.action_norm(actions[t]))
             s, _ = self.rssm._prior_nograd(h, seed, t, row_offset, STREAM_IMG)
+        if chunks:
+            ev = torch.cuda.Event()
+            ev.record()
+            return feats, actions, [ev] * (len(chunks) - 1)
         return feats, actions
 
     @torch.no_grad()

@@ -392,6 +392,31 @@ def pool_rms_bwd(pooled, amax, w, rstd, dy, H, W, dw, nchw_flat=False):
     return dx
 
 
+# ------------------------------------------------------------------------------------------------- timeline marks
+class Marks:
+    """Device timestamps (sd_mark) at tagged points of the update, on whatever stream is current — captured into the
+    HIP graph like any launch, so replayed updates report the real two-stream timeline. Profiling aid only."""
+
+    def __init__(self, device, slots=256):
+        self.buf = torch.zeros(slots, dtype=torch.int64, device=device)
+        self.tags = []
+        self.khz = nat.fns["sd_wall_clock_khz"](torch.device(device).index or 0)
+
+    def reset(self):
+        self.tags = []
+
+    def __call__(self, tag):
+        if len(self.tags) >= self.buf.numel():
+            return
+        nat.call("sd_mark", p(self.buf), len(self.tags), stream())
+        self.tags.append(tag)
+
+    def report(self):
+        """[(tag, microseconds since the first mark)] of the last completed update"""
+        v = self.buf[:len(self.tags)].cpu().tolist()
+        return [(t, (x - v[0]) * 1e3 / self.khz) for t, x in zip(self.tags, v)]
+
+
 # ------------------------------------------------------------------------------------------------- launch probe
 class LaunchProbe:
     """Times every launch of one C-ABI entry point (filtered by its arguments) with HIP events recorded on the

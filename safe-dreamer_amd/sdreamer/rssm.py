@@ -29,6 +29,8 @@ from .networks import Act, BlockLinear, Lambda, Linear, RMSNorm
 STREAM_OBS, STREAM_IMG, STREAM_ACT, STREAM_POLICY = 1, 2, 3, 4
 # the fused scan (csrc/scan.hip) is the default; SDREAMER_FUSED_SCAN=0 selects the per-op HIP kernels (tests compare)
 FUSED_SCAN = os.environ.get("SDREAMER_FUSED_SCAN", "1") != "0"
+# debugging aid: fill the fused backward's scratch tensors with NaN so any element read before it is written shows
+_POISON = os.environ.get("SDREAMER_DEBUG_POISON", "0") != "0"
 
 
 def _fused_scan_ok(rssm, B):
@@ -426,7 +428,8 @@ class ObserveScan(torch.autograd.Function):
             return None if x is None else x.reshape(B, T, width).transpose(0, 1).contiguous()
 
         ds_out, dd_out, dl_in = tm(d_stoch, SK), tm(d_deter, D), tm(d_logit, SK)
-        e = lambda *shape: torch.empty(*shape, dtype=f32, device=dev)  # noqa: E731
+        e = lambda *shape: (torch.full(shape, float("nan"), dtype=f32, device=dev) if _POISON  # noqa: E731
+                            else torch.empty(*shape, dtype=f32, device=dev))
         dl, d_o, d_op, d_x0p, d_x1p = e(T, B, SK), e(T, B, U), e(T, B, U), e(T, B, U), e(T, B, U)
         d_gates, d_hh, d_hp, d_xcat = e(T, B, 3 * D), e(T, B, D), e(T, B, D), e(T, B, 3 * U)
         Wo_d = P["Wo"][:, :D]
