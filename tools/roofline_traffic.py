@@ -28,8 +28,9 @@ ALGO = {
 
 def main(fetch_db, write_db, out, name="conv_fwd16_pool<48>"):
     wgs = 8192
-    f, nf, fdesc = per_launch(fetch_db, "FETCH_SIZE", name, wgs)
-    w, nw, wdesc = per_launch(write_db, "WRITE_SIZE", name, wgs)
+    pat = name.rstrip(">")  # demangled names carry further template arguments (e.g. conv_fwd16_pool<48, true>)
+    f, nf, fdesc = per_launch(fetch_db, "FETCH_SIZE", pat, wgs)
+    w, nw, wdesc = per_launch(write_db, "WRITE_SIZE", pat, wgs)
     kb = 1024.0  # rocprofv3 FETCH_SIZE / WRITE_SIZE are in kilobytes
     res = {"kernel": name, "grid_workgroups": wgs, "algorithmic_bytes": ALGO[name], "dispatches": [nf, nw],
            "fetch_bytes_raw": f * kb if f is not None else None,
