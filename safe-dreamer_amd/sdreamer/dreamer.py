@@ -272,10 +272,11 @@ class Dreamer(nn.Module):
         return post, keys, mvec
 
     def _update_graphed(self, data, initial, seed, ro):
-        """Replay of the update as six single-stream HIP graphs (captured once) joined by stream events:
+        """Replay of the update as seven single-stream HIP graphs (captured once) joined by stream events:
 
-            main: P (encoder, scan fwd) ─┬─ M1 (world-model heads) ─ wait(S1) ─ M2 (posterior bwd) ─ wait(S2) ─ M3
-            side:                        └─ S1 (imagination, returns, replay value) ─ S2 (actor / critic)
+            main: P (encoder, scan fwd) ─┬─ M1 (world-model heads, replay-value fwd) ─ wait(S1) ─ R (replay-value
+                                         │   loss + bwd) ─┬─ M2 (posterior bwd) ─ wait(S2) ─ M3
+            side:                        └─ S1 (imagination, heads, returns) ─ wait(R) ─ S2 (actor / critic)
 
         One graph per stream phase keeps every graph linear: the HIP runtime launches a linear graph as a batch
         (~0.5 ms of host time for the whole update) and the cross-stream edges become device-side event waits.
@@ -297,18 +298,19 @@ class Dreamer(nn.Module):
             gP, st = cap(lambda: self._core_forward(self._g_in, self._g_init, self._seed_dev, ro))
             gS1, _ = cap(lambda: self._ph_side_returns(st), side_cap)
             gM1, _ = cap(lambda: self._ph_wm(st))
+            gR, _ = cap(lambda: self._ph_repval(st))
             gM2, _ = cap(lambda: self._ph_posterior_bwd(st))
             gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
             gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st))
             torch.cuda.synchronize()
-            self._graph = (gP, gS1, gM1, gM2, gS2, gM3)
+            self._graph = (gP, gS1, gM1, gR, gM2, gS2, gM3)
             self._gst, self._g_post, self._g_keys, self._g_mvec = st, post, keys, mvec
         for k, v in data.items():
             self._g_in[k].copy_(v)
         for dst, src in zip(self._g_init, initial):
             dst.copy_(src)
         self._seed_dev.fill_(int(seed) & 0x7FFFFFFFFFFFFFFF)
-        gP, gS1, gM1, gM2, gS2, gM3 = self._graph
+        gP, gS1, gM1, gR, gM2, gS2, gM3 = self._graph
         main = torch.cuda.current_stream()
         side = self._side if self.use_side_stream else main
         gP.replay()
@@ -320,8 +322,12 @@ class Dreamer(nn.Module):
             ev_s1.record()
         gM1.replay()
         main.wait_event(ev_s1)
+        gR.replay()
+        ev_rep = torch.cuda.Event()
+        ev_rep.record()
         gM2.replay()
         with torch.cuda.stream(side):
+            side.wait_event(ev_rep)
             gS2.replay()
         if side is not main:
             main.wait_stream(side)
@@ -340,15 +346,15 @@ class Dreamer(nn.Module):
 
         Same losses and gradients as the reference's single backward, scheduled as stream phases after the posterior
         scan (single GPU; data parallel stays on one stream):
+          side — imagination, imagined heads, lambda-returns + ReturnEMA; later (after the replay-value backward) the
+                 policy / value losses and their backward, overlapping the posterior backward;
           main — world-model head losses (prior/KL, representation, reward, continue) on detached LEAF copies of the
-                 posterior and their backward down to the leaves; then, once the side stream has the replay-value
-                 gradient, one backward from the posterior into the scan and the encoder;
-          side — imagination, imagined heads, lambda-returns + ReturnEMA, the replay-value loss (kept attached to the
-                 world model as in dreamer.py:652: its feat gradient joins the scan backward) and its backward, then
-                 the policy / value losses and their backward, overlapping the launch-bound scan backward.
-        Gradient writes of the two streams touch disjoint parameters; value-head gradients come only from the side
-        stream (replay value, then imagined value, in stream order). Graph mode captures each phase separately
-        (_update_graphed)."""
+                 posterior and their backward down to the leaves, the replay-value forward; once the returns exist,
+                 the replay-value loss (kept attached to the world model as in dreamer.py:652) and its backward; then
+                 one backward from the posterior into the scan and the encoder.
+        Gradient writes of the two streams touch disjoint parameters except the value head, whose two contributions
+        are ordered by an event (replay value on main first, then the imagined value loss on side). Graph mode
+        captures each phase separately (_update_graphed)."""
         st = self._ph_forward(data, initial, seed, row_offset)
         main = torch.cuda.current_stream()
         side = self._side if (self.use_side_stream and self.world == 1) else main
@@ -364,16 +370,22 @@ class Dreamer(nn.Module):
         self._ph_wm(st)
         if side is not main:
             main.wait_event(ev_s1)
-            st["feat_r"].grad.record_stream(main)
+            for t in (st["ifeat"], st["iact"]):
+                t.record_stream(main)
+            for v in st["rr"].values():
+                v.record_stream(main)
+        self._ph_repval(st)
+        ev_rep = torch.cuda.Event()
+        ev_rep.record()
         self._ph_posterior_bwd(st)
         with torch.cuda.stream(side):
+            side.wait_event(ev_rep)
             self._ph_side_ac(st)
         if side is not main:
             main.wait_stream(side)
-            for k in ("ac_losses", "ac_metrics", "rv_metrics"):
+            for k in ("ac_losses", "ac_metrics"):
                 for v in st[k].values():
                     v.record_stream(main)
-            st["repval"].record_stream(main)
         return self._ph_finish(st)
 
     def _ph_forward(self, data, initial, seed, ro):
@@ -394,8 +406,7 @@ class Dreamer(nn.Module):
                     post_logit=post_logit, leaves=leaves, feat_l=feat_l, feat_r=feat_r)
 
     def _ph_side_returns(self, st):
-        """side: imagination (dreamer.py:578-597), imagined heads, lambda-returns + ReturnEMA (598-636), replay value
-        (638-652) and its backward."""
+        """side: imagination (dreamer.py:578-597), imagined heads, lambda-returns + ReturnEMA (598-636)."""
         data = st["data"]
         B, T = data["action"].shape[:2]
         N, H1 = B * T, self.imag_horizon + 1
@@ -406,17 +417,24 @@ class Dreamer(nn.Module):
         self._mark("side:imagine")
         rr = self._heads_returns(ifeat)
         self._mark("side:heads_returns")
-        rv = self._repval_pre(data, st["feat_r"])
-        loss, rv_metrics, rret = self._repval_post(data, rv, rr["ret"])
-        (loss * self._loss_scales["repval"]).backward()
-        self._mark("side:repval")
-        st.update(ifeat=ifeat, iact=iact, rr=rr, repval=loss, rv_metrics=rv_metrics, rret=rret)
+        st.update(ifeat=ifeat, iact=iact, rr=rr)
 
     def _ph_wm(self, st):
-        """main: world-model head losses and their backward down to the posterior leaves."""
+        """main: world-model head losses and their backward down to the posterior leaves; the replay-value parts
+        that do not need the imagined returns."""
         st["wm_total"], st["wm_losses"], st["wm_metrics"] = self._wm_heads(st["data"], st["embed"], st["leaves"],
                                                                            st["feat_l"])
         self._mark("wm_heads")
+        st["rv"] = self._repval_pre(st["data"], st["feat_r"])
+        self._mark("repval_fwd")
+
+    def _ph_repval(self, st):
+        """main (after the returns): replay-value loss (dreamer.py:638-652, attached to the world model through
+        feat_r) and its backward."""
+        loss, rv_metrics, rret = self._repval_post(st["data"], st["rv"], st["rr"]["ret"])
+        (loss * self._loss_scales["repval"]).backward()
+        self._mark("repval_bwd")
+        st.update(repval=loss, rv_metrics=rv_metrics, rret=rret)
 
     def _ph_posterior_bwd(self, st):
         """main: posterior gradient = head-loss leaf grads + replay-value feat grad -> scan + encoder backward."""
