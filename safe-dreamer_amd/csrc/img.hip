@@ -88,7 +88,9 @@ struct APlain : AStage<BM> {
   }
 };
 
-// A(m, k) = silu(X[m][k] * rstd[m] * w[k]), rstd of the tile's rows in LDS (wg_rstd)
+// A(m, k) = silu(X[m][k] * rstd[m] * w[k]), rstd of the tile's rows in LDS (wg_rstd). The loads only fill
+// registers; the RMSNorm + SiLU is applied when the tile is staged into LDS (store), PF k tiles later, so the
+// loads stay in flight behind the MFMAs instead of being waited for at issue.
 template <int BM>
 struct ARms : AStage<BM> {
   using AStage<BM>::r;
@@ -98,6 +100,7 @@ struct ARms : AStage<BM> {
   long ld;
   int m0, M;
   float rr[NV];
+  f32x4 wr[NV];
   SD_DEV ARms(const float* X, long ld_, const float* w_, const float* rs, int m0_, int M_, int K)
       : w(w_), ld(ld_), m0(m0_), M(M_) {
     rx = sd_make_rsrc(X, ((long)(M - 1) * ld + K) * 4);
@@ -108,12 +111,19 @@ struct ARms : AStage<BM> {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int gk = k0 + 4 * this->kq(v), m = m0 + this->row(v);
-      const f32x4 x = sd_bload4(rx, m < M ? (uint32_t)(((long)m * ld + gk) * 4) : SD_OOB), wv = ld4(w + gk);
-      f32x4 y;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) y[j] = siluf_(x[j] * rr[v] * wv[j]);
-      r[v] = y;
+      r[v] = sd_bload4(rx, m < M ? (uint32_t)(((long)m * ld + gk) * 4) : SD_OOB);
+      wr[v] = ld4(w + gk);
     }
+  }
+  SD_DEV void store(float* lds) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      if (this->live(v)) {
+        f32x4 y;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = siluf_(r[v][j] * rr[v] * wr[v][j]);
+        *reinterpret_cast<f32x4*>(lds + this->row(v) * LDS_ROW + 4 * this->kq(v)) = y;
+      }
   }
 };
 
