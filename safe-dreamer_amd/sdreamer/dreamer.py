@@ -22,6 +22,7 @@ import os
 from collections import OrderedDict
 
 import torch
+import torch.distributed as dist
 from torch import nn
 
 from . import _native as nat
@@ -226,10 +227,11 @@ class Dreamer(nn.Module):
         return mets
 
     def update_batch(self, data, initial, seed, row_offset=None):
-        """One optimisation step on a given batch. Single-GPU runs are captured into a HIP graph after two eager
-        warm-up updates (set `use_graphs = False` to stay eager); multi-GPU runs stay eager (RCCL collectives)."""
+        """One optimisation step on a given batch. After two eager warm-up updates the update is captured into HIP
+        graphs (set `use_graphs = False` to stay eager); multi-GPU runs split the graphs at the RCCL exchange steps
+        (parallel.collective) and issue those eagerly between graph replays."""
         ro = self.rank * data["action"].shape[0] if row_offset is None else row_offset
-        if self.use_graphs and self.world == 1 and self.slow_target_update == 1:
+        if self.use_graphs and self.slow_target_update == 1:
             if self._graph is not None or self._eager_updates >= 2:
                 return self._update_graphed(data, initial, seed, ro)
         self._eager_updates += 1
@@ -265,6 +267,8 @@ class Dreamer(nn.Module):
     def _core_finish(self, st):
         """Graph phase M3 (main): merged metrics, optimizer step, metric vector."""
         post, mets = self._ph_finish(st)
+        if self.world > 1:  # the arena was sum-all-reduced between the phase graphs (_update_graphed)
+            self._optimizer.arena.grad.mul_(1.0 / self.world)
         self._optimizer.launch_step()
         self._mark("optimizer")
         keys = [k for k, v in mets.items() if isinstance(v, torch.Tensor)]
@@ -272,37 +276,46 @@ class Dreamer(nn.Module):
         return post, keys, mvec
 
     def _update_graphed(self, data, initial, seed, ro):
-        """Replay of the update as seven single-stream HIP graphs (captured once) joined by stream events:
+        """Replay of the update as seven single-stream phases (captured once) joined by stream events:
 
             main: P (encoder, scan fwd) ─┬─ M1 (world-model heads, replay-value fwd) ─ wait(S1) ─ R (replay-value
-                                         │   loss + bwd) ─┬─ M2 (posterior bwd) ─ wait(S2) ─ M3
+                                         │   loss + bwd) ─┬─ M2 (posterior bwd) ─ wait(S2) ─ [grad all-reduce] ─ M3
             side:                        └─ S1 (imagination, heads, returns) ─ wait(R) ─ S2 (actor / critic)
 
         One graph per stream phase keeps every graph linear: the HIP runtime launches a linear graph as a batch
         (~0.5 ms of host time for the whole update) and the cross-stream edges become device-side event waits.
         A single two-stream graph instead costs ~12 ms of host time per launch, stalling on each cross-stream
-        edge. Every graph has its own memory pool; tensors that cross phases are held by `self._gst`."""
+        edge. Every graph has its own memory pool; tensors that cross phases are held by `self._gst`.
+
+        Data parallel: a phase that exchanges data (Barlow statistics in M1, the returns gather in S1) is a chain
+        graph → collective → graph (parallel.PhaseGraph); the collectives are issued eagerly on the phase's stream,
+        in the same order on every rank: M1's before S1's, so RCCL's single stream never queues the world-model
+        branch behind the imagination. The gradient arena is sum-all-reduced between the joins and M3 (which
+        scales it by 1/world before AGC + LaProp)."""
         if self._graph is None:
             self._g_in = {k: v.clone() for k, v in data.items()}
             self._g_init = tuple(t.clone() for t in initial)
             self._seed_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+            main_cap = torch.cuda.Stream(device=self.device)
             side_cap = torch.cuda.Stream(device=self.device)
+            # thread-local capture: RCCL's watchdog thread queries events while a multi-GPU phase is captured
+            mode = "global" if self.world == 1 else "thread_local"
             torch.cuda.synchronize()
 
-            def cap(fn, stream=None):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=stream):
-                    out = fn()
-                return g, out
+            def cap(fn, stream):
+                return parallel.capture_phase(fn, stream, mode)
 
-            gP, st = cap(lambda: self._core_forward(self._g_in, self._g_init, self._seed_dev, ro))
+            gP, st = cap(lambda: self._core_forward(self._g_in, self._g_init, self._seed_dev, ro), main_cap)
             gS1, _ = cap(lambda: self._ph_side_returns(st), side_cap)
-            gM1, _ = cap(lambda: self._ph_wm(st))
-            gR, _ = cap(lambda: self._ph_repval(st))
-            gM2, _ = cap(lambda: self._ph_posterior_bwd(st))
+            gM1, _ = cap(lambda: self._ph_wm(st), main_cap)
+            gR, _ = cap(lambda: self._ph_repval(st), main_cap)
+            gM2, _ = cap(lambda: self._ph_posterior_bwd(st), main_cap)
             gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
-            gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st))
+            gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st), main_cap)
             torch.cuda.synchronize()
+            for g in (gP, gR, gM2, gS2, gM3):
+                if g.n_collectives:
+                    raise RuntimeError("unexpected exchange step in a single-graph phase")
             self._graph = (gP, gS1, gM1, gR, gM2, gS2, gM3)
             self._gst, self._g_post, self._g_keys, self._g_mvec = st, post, keys, mvec
         for k, v in data.items():
@@ -316,11 +329,14 @@ class Dreamer(nn.Module):
         gP.replay()
         if side is not main:
             side.wait_stream(main)
+        k1 = gS1.first_collective()
         with torch.cuda.stream(side):
-            gS1.replay()
+            gS1.replay(0, k1)
+        gM1.replay()
+        with torch.cuda.stream(side):
+            gS1.replay(k1)
             ev_s1 = torch.cuda.Event()
             ev_s1.record()
-        gM1.replay()
         main.wait_event(ev_s1)
         gR.replay()
         ev_rep = torch.cuda.Event()
@@ -331,6 +347,8 @@ class Dreamer(nn.Module):
             gS2.replay()
         if side is not main:
             main.wait_stream(side)
+        if self.world > 1:
+            parallel.collective(lambda: dist.all_reduce(self._optimizer.arena.grad))
         gM3.replay()
         self._slow_value_updates += 1
         self._optimizer.host_steps += 1
@@ -354,10 +372,11 @@ class Dreamer(nn.Module):
                  one backward from the posterior into the scan and the encoder.
         Gradient writes of the two streams touch disjoint parameters except the value head, whose two contributions
         are ordered by an event (replay value on main first, then the imagined value loss on side). Graph mode
-        captures each phase separately (_update_graphed)."""
+        captures each phase separately (_update_graphed). Data parallel runs the same two streams; the exchange steps
+        (parallel.collective) are issued on the stream of the phase that needs them."""
         st = self._ph_forward(data, initial, seed, row_offset)
         main = torch.cuda.current_stream()
-        side = self._side if (self.use_side_stream and self.world == 1) else main
+        side = self._side if self.use_side_stream else main
         if side is not main:
             side.wait_stream(main)
             for t in (st["post_stoch"], st["post_deter"], st["feat_r"], data["reward"], data["is_last"],

@@ -39,7 +39,7 @@ def _worker(rank, world, port, q):
         x1 = torch.randn(64, 16, generator=gen)
         x2 = torch.randn(64, 16, generator=gen)
         xs = x1[32 * rank: 32 * (rank + 1)].clone().requires_grad_()
-        loss = parallel.DistBarlowFn.apply(xs, x2[32 * rank: 32 * (rank + 1)], 5e-4)
+        loss = parallel.barlow_dist(xs, x2[32 * rank: 32 * (rank + 1)], 5e-4, world)
         loss.backward()
         xr = x1.clone().requires_grad_()
         n1 = (xr - xr.mean(0)) / (xr.std(0) + 1e-8)
@@ -49,7 +49,7 @@ def _worker(rank, world, port, q):
         ref = (torch.diagonal(c) - 1).pow(2).sum() + 5e-4 * c[off].pow(2).sum()
         ref.backward()
         ok_b = abs(float(loss) - float(ref)) < 1e-4 * abs(float(ref)) and torch.allclose(
-            xs.grad, xr.grad[32 * rank: 32 * (rank + 1)], atol=1e-6, rtol=1e-4)
+            xs.grad / world, xr.grad[32 * rank: 32 * (rank + 1)], atol=1e-6, rtol=1e-4)  # x world: see _DistBarlowLoss
         q.put((rank, ok_ar, ok_g, ok_b))
     finally:
         dist.destroy_process_group()
