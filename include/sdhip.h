@@ -49,6 +49,10 @@ typedef struct sd_gemm_desc {
   float alpha, beta;
 } sd_gemm_desc;
 int sd_gemm_f32(const sd_gemm_desc* d, float* workspace, long workspace_floats, sd_stream stream);
+/* Same contract on the split-bf16 path (csrc/gemm3_core.h): a = hi + lo (bf16 each), a*b = hi*hi + hi*lo + lo*hi on
+ * v_mfma_f32_16x16x32_bf16 with f32 accumulation, ~1e-5 relative to the typical |term| * sqrt(K), 5.3x the f32 MFMA
+ * rate. For gradient contractions and frozen heads (no sampled index depends on them). M, N or K < 64 -> f32 path. */
+int sd_gemm_bf16x3(const sd_gemm_desc* d, float* workspace, long workspace_floats, sd_stream stream);
 
 /* ---------------------------------------------------------------- row norms
  * y = act(x * rsqrt(mean(x^2) + eps) * w) per row; act 0 = none, 1 = SiLU. rstd (M) saved for backward.

@@ -1,0 +1,86 @@
+// Dense split-bf16 GEMM (gemm3_core.h): same contract as sd_gemm_f32 (gemm.hip) — C[b] = alpha * A[b] . B[b]
+// (+ bias) (+ beta * C[b]), strided batch, either unit stride per operand, split-K slabs summed in a fixed order —
+// at ~1e-5 relative accuracy instead of f32's ~1e-7. Shapes below one 64x64 tile per operand side go to the f32
+// kernels (they are latency-bound there anyway).
+#include "common.h"
+#include "sdhip.h"
+
+#include "gemm3_core.h"
+
+namespace {
+using namespace sdb;
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool VA, bool VB>
+__global__ __launch_bounds__(256, 2) void gemm3_kernel(GemmArgs g) {
+  const int bn0 = blockIdx.x * BN, bm0 = blockIdx.y * BM;
+  const int b = blockIdx.z / g.ksplit, split = blockIdx.z % g.ksplit;
+  const int kbeg = split * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const float* A = g.A + (long)b * g.sA;
+  const float* Bp = g.B + (long)b * g.sB;
+  using OA = typename std::conditional<AK, KC3<BM, VA>, KM3<BM, VA>>::type;
+  using OB = typename std::conditional<BKC, KC3<BN, VB>, KM3<BN, VB>>::type;
+  OA la(A, g.lda, g.M, bm0);
+  OB lb(Bp, g.ldb, g.N, bn0);
+  f32x4 acc[WM / 16][WN / 16];
+  gemm3_mainloop<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
+  gemm3_epilogue<BM, BN, WM, WN>(g, acc, bm0, bn0, b, split);
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC>
+void launch3_tile(const GemmArgs& g, bool va, bool vb, hipStream_t st) {
+  dim3 grid(sd_cdiv(g.N, BN), sd_cdiv(g.M, BM), g.batch * g.ksplit);
+  if (va && vb) gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, true><<<grid, 256, 0, st>>>(g);
+  else if (va) gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, false><<<grid, 256, 0, st>>>(g);
+  else if (vb) gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, true><<<grid, 256, 0, st>>>(g);
+  else gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, false><<<grid, 256, 0, st>>>(g);
+}
+
+template <bool AK, bool BKC>
+void launch3_layout(const GemmArgs& g, int tile, bool va, bool vb, hipStream_t st) {
+  if (tile == 0) launch3_tile<128, 128, 64, 64, AK, BKC>(g, va, vb, st);
+  else launch3_tile<64, 64, 32, 32, AK, BKC>(g, va, vb, st);
+}
+
+bool al16_3(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" int sd_gemm_bf16x3(const sd_gemm_desc* d, float* workspace, long workspace_floats, sd_stream stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  if (!d || !d->A || !d->B || !d->C) return SD_EARG;
+  if (d->M <= 0 || d->N <= 0 || d->batch <= 0) return SD_OK;
+  if (d->M < 64 || d->N < 64 || d->K < 64) return sd_gemm_f32(d, workspace, workspace_floats, stream_);
+  GemmArgs g;
+  g.A = d->A; g.B = d->B; g.C = d->C; g.bias = d->bias; g.ws = workspace;
+  g.lda = d->lda; g.ldb = d->ldb; g.ldc = d->ldc;
+  g.sA = d->strideA; g.sB = d->strideB; g.sC = d->strideC; g.sBias = d->strideBias;
+  g.M = d->M; g.N = d->N; g.K = d->K; g.batch = d->batch;
+  g.alpha = d->alpha; g.beta = d->beta;
+  int ks = d->ksplit < 1 ? 1 : d->ksplit;
+  if (ks > 1 && (!workspace || workspace_floats < (long)ks * d->batch * d->M * d->N)) return SD_EARG;
+  g.ksplit = ks;
+  long kc = ((long)d->K + ks - 1) / ks;
+  g.kchunk = (int)((kc + BK - 1) / BK * BK);
+  const bool va = al16_3(d->A) && d->lda % 4 == 0 && (d->batch == 1 || d->strideA % 4 == 0);
+  const bool vb = al16_3(d->B) && d->ldb % 4 == 0 && (d->batch == 1 || d->strideB % 4 == 0);
+  int tile = d->tile;
+  if (tile != 0 && tile != 1) {
+    const long tiles128 = (long)sd_cdiv(d->M, 128) * sd_cdiv(d->N, 128) * d->batch * ks;
+    tile = tiles128 >= 256 ? 0 : 1;
+  }
+  const bool ak = d->a_kcontig != 0, bk = d->b_kcontig != 0;
+  if (ak && bk) launch3_layout<true, true>(g, tile, va, vb, stream);
+  else if (ak) launch3_layout<true, false>(g, tile, va, vb, stream);
+  else if (bk) launch3_layout<false, true>(g, tile, va, vb, stream);
+  else launch3_layout<false, false>(g, tile, va, vb, stream);
+  SD_LAUNCH_CHECK();
+  if (ks > 1) {
+    long total = (long)d->batch * d->M * d->N;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    sdg::gemm_reduce_kernel<<<blocks, 256, 0, stream>>>(g);
+    SD_LAUNCH_CHECK();
+  }
+  return SD_OK;
+}

@@ -1,0 +1,233 @@
+// Split-bf16 ("bf16x3") GEMM core on v_mfma_f32_16x16x32_bf16 (gfx950: 1024 FLOP/clk/SIMD, 16x the f32 MFMA).
+//
+// Every fp32 operand is split when it is staged into LDS: a = hi + lo with hi = bf16(a), lo = bf16(a - hi)
+// (|a - hi - lo| <= 2^-17 |a|). The product a*b is taken as hi_a*hi_b + hi_a*lo_b + lo_a*hi_b — three bf16 MFMAs
+// with exact products, accumulated in fp32 — dropping lo_a*lo_b (<= 2^-18 |ab|). A K-term dot product carries
+// ~1e-5 relative error of the typical |term| * sqrt(K) (f32 MFMA: ~1e-7) at 16/3 = 5.3x the f32 MFMA rate.
+// Used for the contractions whose results feed no sampled index: gradients (input and weight) of every linear
+// and convolution, and the frozen imagined heads. Sampled latents and actions stay on the exact f32 path.
+//
+// LDS image per operand tile: [row][hi k0..31 | lo k0..31 | pad 8] bf16 (144-B rows, 36 banks: the 16 rows of a
+// fragment read hit 16 distinct 4-bank groups). MFMA operand per lane: row l16 (A: m, B: n), k = 8q .. 8q+7
+// (q = lane >> 4) as one ds_read_b128 per plane; accumulator reg r of a 16x16 tile -> row 4q + r, column l16.
+#pragma once
+#include "common.h"
+#include "gemm_core.h"
+
+namespace sdb {
+namespace {
+using sdg::GemmArgs;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 32;
+constexpr int LROW = 2 * BK + 8;  // bf16 per LDS row
+
+SD_DEV void split_store(__bf16* dst, f32x4 v) {
+  const bf16x4 hi = __builtin_convertvector(v, bf16x4);
+  const f32x4 r = v - __builtin_convertvector(hi, f32x4);
+  *reinterpret_cast<bf16x4*>(dst) = hi;
+  *reinterpret_cast<bf16x4*>(dst + BK) = __builtin_convertvector(r, bf16x4);
+}
+
+// Operand with k contiguous (row r, k at p[r * ld + k]): thread loads float4 runs along k.
+template <int ROWS, bool VEC>
+struct KC3 {
+  static constexpr int NV = (ROWS * BK / 4 + 255) / 256;
+  f32x4 r[NV];
+  const float* p;
+  long ld;
+  int nrows, row0;
+  SD_DEV KC3(const float* base, long ld_, int nrows_, int row0_) : p(base), ld(ld_), nrows(nrows_), row0(row0_) {}
+  SD_DEV void load(int k0, int kend) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      const int row = i / (BK / 4), gk = k0 + 4 * (i % (BK / 4)), gr = row0 + row;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (i < ROWS * BK / 4 && gr < nrows) {
+        const float* q = p + (long)gr * ld + gk;
+        if (VEC && gk + 3 < kend) {
+          x = *reinterpret_cast<const f32x4*>(q);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (gk + j < kend) x[j] = q[j];
+        }
+      }
+      r[v] = x;
+    }
+  }
+  SD_DEV void store(__bf16* lds) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      if ((v + 1) * 256 <= ROWS * BK / 4 || i < ROWS * BK / 4)
+        split_store(lds + (i / (BK / 4)) * LROW + 4 * (i % (BK / 4)), r[v]);
+    }
+  }
+};
+
+// Operand with rows contiguous (row r, k at p[k * ld + r]): thread loads a 4 (k) x 4 (rows) block as four float4
+// runs along the rows (coalesced), transposes it in registers and stores four k-runs.
+template <int ROWS, bool VEC>
+struct KM3 {
+  static constexpr int NBLK = ROWS * BK / 16;
+  static constexpr int NV = (NBLK + 255) / 256;
+  f32x4 r[NV][4];
+  const float* p;
+  long ld;
+  int nrows, row0;
+  SD_DEV KM3(const float* base, long ld_, int nrows_, int row0_) : p(base), ld(ld_), nrows(nrows_), row0(row0_) {}
+  SD_DEV void load(int k0, int kend) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      const int rq = i % (ROWS / 4), kq = i / (ROWS / 4);
+      const int gr = row0 + 4 * rq;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int gk = k0 + 4 * kq + kk;
+        f32x4 x = {0.f, 0.f, 0.f, 0.f};
+        if (i < NBLK && gk < kend) {
+          const float* q = p + (long)gk * ld + gr;
+          if (VEC && gr + 3 < nrows) {
+            x = *reinterpret_cast<const f32x4*>(q);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (gr + j < nrows) x[j] = q[j];
+          }
+        }
+        r[v][kk] = x;
+      }
+    }
+  }
+  SD_DEV void store(__bf16* lds) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      if ((v + 1) * 256 <= NBLK || i < NBLK) {
+        const int rq = i % (ROWS / 4), kq = i / (ROWS / 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 t = {r[v][0][j], r[v][1][j], r[v][2][j], r[v][3][j]};
+          split_store(lds + (4 * rq + j) * LROW + 4 * kq, t);
+        }
+      }
+    }
+  }
+};
+
+template <int BM, int BN>
+constexpr int gemm3_smem_bf16() {
+  return 2 * (BM + BN) * LROW;
+}
+
+// Double-buffered main loop: the next k tile's global loads are issued before this tile's MFMAs and staged (split)
+// into the other LDS buffer after them; one barrier per k tile.
+template <int BM, int BN, int WM, int WN, class OpA, class OpB>
+SD_DEV void gemm3_mainloop(OpA& la, OpB& lb, int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16]) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+  constexpr int SA = BM * LROW, STAGE = (BM + BN) * LROW;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  const int l16 = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk <= 0) return;
+  la.load(kbeg, kend);
+  lb.load(kbeg, kend);
+  la.store(smem);
+  lb.store(smem + SA);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const __bf16* cur = smem + (kt & 1) * STAGE;
+    if (kt + 1 < nk) {
+      la.load(kbeg + (kt + 1) * BK, kend);
+      lb.load(kbeg + (kt + 1) * BK, kend);
+    }
+    bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const __bf16* p = cur + (wr * WM + 16 * i + l16) * LROW + 8 * q;
+      ah[i] = *reinterpret_cast<const bf16x8*>(p);
+      al[i] = *reinterpret_cast<const bf16x8*>(p + BK);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const __bf16* p = cur + SA + (wc * WN + 16 * j + l16) * LROW + 8 * q;
+      bh[j] = *reinterpret_cast<const bf16x8*>(p);
+      bl[j] = *reinterpret_cast<const bf16x8*>(p + BK);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+    if (kt + 1 < nk) {
+      __bf16* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+      la.store(nxt);
+      lb.store(nxt + SA);
+    }
+    __syncthreads();
+  }
+}
+
+// C tile epilogue (alpha, bias, beta; or a split-K partial slab)
+template <int BM, int BN, int WM, int WN>
+SD_DEV void gemm3_epilogue(const GemmArgs& g, const f32x4 (&acc)[WM / 16][WN / 16], int bm0, int bn0, int b,
+                           int split) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  const int l16 = lane & 15, q = lane >> 4;
+  if (g.ksplit > 1) {
+    float* W = g.ws + ((long)split * g.batch + b) * (long)g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = bn0 + wc * WN + 16 * j + l16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = bm0 + wr * WM + 16 * i + 4 * q + r;
+          if (m < g.M && n < g.N) W[(long)m * g.N + n] = g.alpha * acc[i][j][r];
+        }
+      }
+    return;
+  }
+  float* C = g.C + (long)b * g.sC;
+  const float* bias = g.bias ? g.bias + (long)b * g.sBias : nullptr;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = bn0 + wc * WN + 16 * j + l16;
+      const float bv = (bias && n < g.N) ? bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm0 + wr * WM + 16 * i + 4 * q + r;
+        if (m < g.M && n < g.N) {
+          float v = g.alpha * acc[i][j][r] + bv;
+          float* c = C + (long)m * g.ldc + n;
+          if (g.beta != 0.f) v += g.beta * *c;
+          *c = v;
+        }
+      }
+    }
+}
+
+}  // namespace
+}  // namespace sdb

@@ -563,10 +563,11 @@ class Dreamer(nn.Module):
         H1, N = ifeat.shape[:2]
         dev = ifeat.device
         flat = ifeat.reshape(H1 * N, -1)
-        i_rew = K.twohot_mode(self.reward.logits_nograd(flat), self.rbins).view(H1, N)
-        i_contl = self.cont.logits_nograd(flat).view(H1, N)
-        i_val = K.twohot_mode(self.value.logits_nograd(flat), self.vbins).view(H1, N)
-        i_slow = K.twohot_mode(self._slow_value.logits_nograd(flat), self.vbins).view(H1, N)
+        # frozen heads on the imagined trajectories: split-bf16 contractions (no sampled index depends on them)
+        i_rew = K.twohot_mode(self.reward.logits_nograd(flat, True), self.rbins).view(H1, N)
+        i_contl = self.cont.logits_nograd(flat, True).view(H1, N)
+        i_val = K.twohot_mode(self.value.logits_nograd(flat, True), self.vbins).view(H1, N)
+        i_slow = K.twohot_mode(self._slow_value.logits_nograd(flat, True), self.vbins).view(H1, N)
         disc = 1 - 1 / self.horizon
         rew_n, contl_n, val_n = i_rew.t().contiguous(), i_contl.t().contiguous(), i_val.t().contiguous()
         i_cont = torch.empty(N, H1, device=dev)
@@ -585,7 +586,7 @@ class Dreamer(nn.Module):
         H1, N = ifeat.shape[:2]
         H = H1 - 1
         ret, weight, adv, i_slow = rr["ret"], rr["weight"], rr["adv"], rr["i_slow"]
-        pl = self.actor(ifeat[:H].reshape(H * N, -1))
+        pl = self.actor(ifeat[:H].reshape(H * N, -1), fast=True)
         if self.act_discrete:
             logpi, ent = ops.OneHotLogProbEntFn.apply(pl, iact[:H].reshape(H * N, -1),
                                                        float(self.config.actor.dist.unimix_ratio))
@@ -596,7 +597,7 @@ class Dreamer(nn.Module):
         logpi, ent = logpi.view(H, N).t(), ent.view(H, N).t()
         w = weight[:, :H]
         losses["policy"] = torch.mean(w * -(logpi * adv + self.act_entropy * ent))
-        vl = self.value(ifeat[:H].reshape(H * N, -1))
+        vl = self.value(ifeat[:H].reshape(H * N, -1), fast=True)
         lp_tar = ops.TwoHotLogProbFn.apply(vl, self.vbins, ret.t().contiguous().reshape(-1))
         lp_slow = ops.TwoHotLogProbFn.apply(vl, self.vbins, i_slow[:H].reshape(-1))
         losses["value"] = torch.mean(w * (-lp_tar - lp_slow).view(H, N).t())

@@ -6,6 +6,7 @@ there is no CPU fallback anywhere in the product path.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -72,9 +73,23 @@ def _auto_split(M, N, K, batch):
     return max(1, min(ks, 32))
 
 
-def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1):
+# SDREAMER_FAST_GEMM=0 keeps every contraction on the exact f32 MFMA path (A/B and precision studies)
+FAST_GEMM = os.environ.get("SDREAMER_FAST_GEMM", "1") != "0"
+
+
+def _fast_split(M, N, K, batch):
+    """K split for the split-bf16 kernel: ~512 workgroups of 128x128 tiles (2 per CU) when K is long; the launcher
+    falls back to 64x64 tiles below 256 workgroups."""
+    tiles = -(-M // 128) * -(-N // 128) * batch
+    if tiles >= 256 or K < 1024:
+        return 1
+    return max(1, min(K // 512, -(-512 // tiles), 32))
+
+
+def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1, fast=False):
     """out[M,N] = alpha * a[M,K] @ b[K,N] (+ bias[N]) (+ beta*out). Strided views allowed (one unit stride each);
-    3-D operands are a strided batch over dim 0."""
+    3-D operands are a strided batch over dim 0. fast=True: split-bf16 MFMA path (sd_gemm_bf16x3, ~1e-5 relative)
+    for contractions no sampled index depends on (gradients, frozen heads)."""
     _chk(a, b, out, bias)
     if a.dtype != torch.float32 or b.dtype != torch.float32 or out.dtype != torch.float32:
         raise TypeError("fp32 GEMM")
@@ -104,8 +119,12 @@ def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1):
         ldc = out.stride(0) if M > 1 else max(Nn, 1)
     if M == 0 or Nn == 0:
         return out
+    fast = fast and FAST_GEMM and M >= 64 and Nn >= 64 and K >= 64
     if ksplit is None:
-        ksplit = _skinny_split(M, Nn, K, Bt) if (M <= 32 and ak and tile < 0) else _auto_split(M, Nn, K, Bt)
+        if fast:
+            ksplit = _fast_split(M, Nn, K, Bt)
+        else:
+            ksplit = _skinny_split(M, Nn, K, Bt) if (M <= 32 and ak and tile < 0) else _auto_split(M, Nn, K, Bt)
     d = nat.GemmDesc()
     d.A, d.B, d.C, d.bias = p(a), p(b), p(out), (p(bias) if bias is not None else None)
     d.lda, d.ldb, d.ldc = lda, ldb, ldc
@@ -117,7 +136,8 @@ def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1):
     ws = None
     if ksplit > 1:
         ws = torch.empty(ksplit * Bt * M * Nn, dtype=torch.float32, device=out.device)
-    nat.call("sd_gemm_f32", ctypes.byref(d), p(ws), ws.numel() if ws is not None else 0, stream())
+    nat.call("sd_gemm_bf16x3" if fast else "sd_gemm_f32", ctypes.byref(d), p(ws), ws.numel() if ws is not None else 0,
+             stream())
     return out
 
 
@@ -129,9 +149,9 @@ def mm(a, b, bias=None, out=None, **kw):
     return gemm(a, b, out, bias=bias, **kw)
 
 
-def linear(x, w, b=None, out=None, beta=0.0):
+def linear(x, w, b=None, out=None, beta=0.0, fast=False):
     """x (M, I) @ w(O, I)^T + b  — nn.Linear forward."""
-    return mm(x, w.t(), bias=b, out=out, beta=beta)
+    return mm(x, w.t(), bias=b, out=out, beta=beta, fast=fast)
 
 
 # ------------------------------------------------------------------------------------------------- row norms

@@ -125,19 +125,20 @@ class MLP(nn.Module):
         self.out_dim = int(config.units)
         self._mods = [(self.layers[3 * i], self.layers[3 * i + 1]) for i in range(self.n)]
 
-    def forward(self, x):
+    def forward(self, x, fast=False):
         if self._symlog_inputs:
             x = K.symlog(x.contiguous())
         for lin, norm in self._mods:
-            x = ops.rms_silu(ops.linear(x, lin.weight, lin.bias), norm.weight)
+            x = ops.rms_silu(ops.linear(x, lin.weight, lin.bias, fast), norm.weight)
         return x
 
     @torch.no_grad()
-    def forward_nograd(self, x):
+    def forward_nograd(self, x, fast=False):
         if self._symlog_inputs:
             x = K.symlog(x.contiguous())
         for lin, norm in self._mods:
-            x = K.rmsnorm_fwd(K.linear(x.reshape(-1, x.shape[-1]), lin.weight, lin.bias), norm.weight, act=1)[0]
+            x = K.rmsnorm_fwd(K.linear(x.reshape(-1, x.shape[-1]), lin.weight, lin.bias, fast=fast), norm.weight,
+                              act=1)[0]
         return x
 
 
@@ -154,13 +155,14 @@ class MLPHead(nn.Module):
         outscale = float(config.outscale) if config.outscale is not None else 1.0
         self.last = Linear(self.mlp.out_dim, out, outscale=outscale)
 
-    def forward(self, x):
-        return ops.linear(self.mlp(x), self.last.weight, self.last.bias)
+    def forward(self, x, fast=False):
+        """fast: split-bf16 contractions (imagined trajectories; see ops.LinearFn)."""
+        return ops.linear(self.mlp(x, fast), self.last.weight, self.last.bias, fast)
 
     @torch.no_grad()
-    def logits_nograd(self, x):
-        h = self.mlp.forward_nograd(x.reshape(-1, x.shape[-1]))
-        return K.linear(h, self.last.weight, self.last.bias)
+    def logits_nograd(self, x, fast=False):
+        h = self.mlp.forward_nograd(x.reshape(-1, x.shape[-1]), fast)
+        return K.linear(h, self.last.weight, self.last.bias, fast=fast)
 
 
 class ConvEncoder(nn.Module):

@@ -29,12 +29,13 @@ def _flat(x):
 
 # ------------------------------------------------------------------------------------------------- dense layers
 class LinearFn(torch.autograd.Function):
-    """nn.Linear (y = x W^T + b)."""
+    """nn.Linear (y = x W^T + b). Gradients on the split-bf16 GEMM (k.gemm fast=True, ~1e-5 relative); the forward
+    too when `fast` (imagined-trajectory heads: no sampled index depends on them)."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, fast=False):
         x2 = _flat(x).contiguous()
-        y = k.mm(x2, w.t(), bias=b)
+        y = k.mm(x2, w.t(), bias=b, fast=fast)
         ctx.save_for_backward(x2, w, b)
         ctx.in_shape = x.shape
         return y.view(*x.shape[:-1], w.shape[0])
@@ -45,12 +46,12 @@ class LinearFn(torch.autograd.Function):
         dy2 = _flat(dy).contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = k.mm(dy2, w).view(ctx.in_shape)
+            dx = k.mm(dy2, w, fast=True).view(ctx.in_shape)
         if w.requires_grad:
-            k.gemm(dy2.t(), x2, grad_buf(w), beta=1.0)
+            k.gemm(dy2.t(), x2, grad_buf(w), beta=1.0, fast=True)
         if b is not None and b.requires_grad:
             k.colsum(dy2, grad_buf(b), accumulate=True)
-        return dx, None, None
+        return dx, None, None, None
 
 
 class RmsSiluFn(torch.autograd.Function):
@@ -97,17 +98,17 @@ class BlockLinearFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, G * Ig, dtype=torch.float32, device=dy.device)
-            k.gemm(dyv, wp, dx.view(M, G, Ig).permute(1, 0, 2))
+            k.gemm(dyv, wp, dx.view(M, G, Ig).permute(1, 0, 2), fast=True)
             dx = dx.view(ctx.in_shape)
         if wp.requires_grad:
-            k.gemm(dyv.transpose(1, 2), x2.view(M, G, Ig).permute(1, 0, 2), grad_buf(wp), beta=1.0)
+            k.gemm(dyv.transpose(1, 2), x2.view(M, G, Ig).permute(1, 0, 2), grad_buf(wp), beta=1.0, fast=True)
         if b.requires_grad:
             k.colsum(dy2, grad_buf(b), accumulate=True)
         return dx, None, None
 
 
-def linear(x, w, b=None):
-    return LinearFn.apply(x, w, b)
+def linear(x, w, b=None, fast=False):
+    return LinearFn.apply(x, w, b, fast)
 
 
 def rms_silu(x, w, act=1):

@@ -76,3 +76,42 @@ def test_gemm_splitk_beta_batched(ks):
     k.gemm(av, bv, ov, alpha=0.5, beta=1.0, ksplit=ks)
     ref = 0.5 * torch.einsum("mbk,bnk->mbn", a.view(M, Bt, K).double(), w.double()).reshape(M, Bt * N) + c0.double()
     assert (out.double() - ref).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (1024, 256, 2560), (300, 129, 1000), (15360, 256, 2560),
+                                   (256, 2560, 15360), (2048, 1024, 512), (4096, 65, 1600), (100, 200, 3000)])
+@pytest.mark.parametrize("ak", [True, False])
+@pytest.mark.parametrize("bk", [True, False])
+def test_gemm_bf16x3_layouts(M, N, K, ak, bk):
+    """Split-bf16 path: |err_ij| <= 4e-5 * sum_k |a_ik||b_kj| (per-product split error <= 3 * 2^-17, f32 sums)."""
+    from sdreamer import kernels as k
+    dev = "cuda"
+    g = torch.Generator(device="cpu").manual_seed(M * 5 + N * 3 + K)
+    a0 = torch.randn(M, K, generator=g).to(dev)
+    b0 = torch.randn(K, N, generator=g).to(dev)
+    a = a0 if ak else a0.t().contiguous().t()
+    b = b0.t().contiguous().t() if bk else b0
+    bias = torch.randn(N, generator=g).to(dev)
+    c0 = torch.randn(M, N, generator=g).to(dev)
+    out = c0.clone()
+    k.gemm(a, b, out, bias=bias, alpha=0.5, beta=1.0, fast=True)
+    ref = _ref(a0, b0, bias, c0, alpha=0.5, beta=1.0)
+    bound = 0.5 * (a0.double().abs() @ b0.double().abs()) * 4e-5 + 1e-5 * (1 + c0.double().abs() + bias.double().abs())
+    excess = ((out.double() - ref).abs() - bound).max().item()
+    assert excess <= 0, excess
+    # and it is not the f32 path in disguise: the error is that of a split-bf16 product (> f32's ~1e-7)
+    if M >= 64 and N >= 64 and K >= 64:
+        rel = ((out.double() - ref).abs().max() / (a0.double().abs() @ b0.double().abs()).max()).item()
+        assert rel > 1e-9, rel
+
+
+def test_gemm_bf16x3_batched_split():
+    from sdreamer import kernels as k
+    g = torch.Generator(device="cpu").manual_seed(11)
+    a = torch.randn(8, 256, 1024, generator=g).cuda()
+    b = torch.randn(8, 1024, 768, generator=g).cuda()
+    out = torch.empty(8, 256, 768, device="cuda")
+    k.gemm(a, b, out, ksplit=4, fast=True)
+    ref = a.double() @ b.double()
+    bound = 4e-5 * (a.double().abs() @ b.double().abs()) + 1e-6
+    assert ((out.double() - ref).abs() - bound).max().item() <= 0
