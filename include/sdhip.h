@@ -153,6 +153,16 @@ int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db, float* wor
  * slabs > 1): stride-1 convs with Co % 16 == 0 take a direct kernel (dy rows + input patch staged in LDS, no im2col
  * re-reads) whose split is fixed by the library; others use `ksplit` over the im2col implicit GEMM. */
 int sd_conv2d_wgrad_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int ups, int ksplit);
+/* Split-bf16 (bf16x3, ~1e-5 relative) backward convolutions (csrc/conv.hip, gemm3_core.h). SD_ESHAPE when the
+ * shape is outside the kernels (the caller then takes the f32 path). dgrad: same arguments as sd_conv2d_fwd with
+ * in = dOut (Ci channels), w = the flipped weight (sd_conv_flip_weight), out = dIn (Co channels), ups = 0.
+ * wgrad: [dW | db] as sd_conv2d_wgrad (ups = 0); workspace >= slabs * Co * (kh*kw*Ci + 1) floats, slabs from
+ * sd_conv2d_wgrad_bf16x3_slabs. Replace the backward of Conv2dSamePad (networks.py:59-85). */
+int sd_conv2d_dgrad_bf16x3(const float* dout, const float* wflip, float* din, int Nb, int Hs, int Ws, int Ci, int Co,
+                           int kh, int kw, int pad, sd_stream stream);
+int sd_conv2d_wgrad_bf16x3_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int ups);
+int sd_conv2d_wgrad_bf16x3(const float* in, const float* dout, float* dw_db, float* workspace, long ws_floats,
+                           int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad, sd_stream stream);
 /* Wf[ci][ky][kx][co] = W[co][kh-1-ky][kw-1-kx][ci]  (input-gradient conv weights) */
 int sd_conv_flip_weight(const float* w, float* wf, int Co, int kh, int kw, int Ci, sd_stream stream);
 /* backward of nearest 2x upsample: din (Nb,H,W,C) = 2x2 sums of du (Nb,2H,2W,C) */

@@ -339,12 +339,37 @@ def conv2d_fwd(x, w, b, ups=0, pad=None, out=None):
     return out
 
 
-def conv2d_wgrad(x, dout, kh, kw, ups=0, pad=None):
-    """returns (Co, kh*kw*Ci + 1) = [dW | db]"""
+def conv2d_dgrad(dout, w, pad=None, fast=True):
+    """Input gradient of a stride-1 conv: conv_same(dOut, flipped W). dout (Nb, H, W, Co), w (Co, kh, kw, Ci) ->
+    (Nb, H, W, Ci). fast: split-bf16 MFMA kernel (sd_conv2d_dgrad_bf16x3) where its shape constraints hold."""
+    Co, kh, kw, Ci = w.shape
+    pad = kh - 1 - (kh - 1) // 2 if pad is None else pad
+    wf = conv_flip_weight(w)
+    if fast and FAST_GEMM:
+        Nb, H, W, _ = dout.shape
+        din = torch.empty(Nb, H, W, Ci, dtype=torch.float32, device=dout.device)
+        if nat.call_shaped("sd_conv2d_dgrad_bf16x3", p(_c(dout)), p(wf), p(din), Nb, H, W, Co, Ci, kh, kw, pad,
+                           stream()):
+            return din
+    return conv2d_fwd(dout, wf, None, pad=pad)
+
+
+def conv2d_wgrad(x, dout, kh, kw, ups=0, pad=None, fast=False):
+    """returns (Co, kh*kw*Ci + 1) = [dW | db]. fast: split-bf16 implicit-GEMM kernel (sd_conv2d_wgrad_bf16x3) where
+    eligible. Off by default: its im2col operand is gathered from memory per k tile, and at the encoder shapes the
+    f32 direct kernel (input patch staged once per row block in LDS) is faster (tools/conv_bench.py)."""
     Nb, H, W, Ci = x.shape
     Co = dout.shape[-1]
     pad = (kh - 1) // 2 if pad is None else pad
     J = kh * kw * Ci
+    if fast and FAST_GEMM:
+        ks = nat.fns["sd_conv2d_wgrad_bf16x3_slabs"](Nb, H, W, Ci, Co, kh, kw, ups)
+        if ks > 0:
+            out = torch.empty(Co, J + 1, dtype=torch.float32, device=x.device)
+            ws = torch.empty(ks * Co * (J + 1), dtype=torch.float32, device=x.device) if ks > 1 else None
+            if nat.call_shaped("sd_conv2d_wgrad_bf16x3", p(_c(x)), p(_c(dout)), p(out), p(ws),
+                               ws.numel() if ws is not None else 0, Nb, H, W, Ci, Co, kh, kw, pad, stream()):
+                return out
     pixels = dout.numel() // Co
     ks = max(1, min(256, pixels // 4096))
     tiles = -(-Co // 64) * -(-(J + 1) // 64)

@@ -121,7 +121,9 @@ def block_linear(x, wp, b):
 
 # ------------------------------------------------------------------------------------------------- conv
 class ConvPoolNormFn(torch.autograd.Function):
-    """One ConvEncoder stage: Conv2dSamePad -> MaxPool2d(2) -> RMSNorm2D -> SiLU (networks.py:201-216), NHWC."""
+    """One ConvEncoder stage: Conv2dSamePad -> MaxPool2d(2) -> RMSNorm2D -> SiLU (networks.py:201-216), NHWC.
+    Forward on the exact f32 MFMA kernels (the posterior samples depend on it); both backward contractions on the
+    split-bf16 kernels (k.conv2d_wgrad / k.conv2d_dgrad, ~1e-5 relative)."""
 
     @staticmethod
     def forward(ctx, x, w, b, nw, nchw_flat):
@@ -153,7 +155,7 @@ class ConvPoolNormFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if Cx != Ci:
                 raise NotImplementedError("input gradient through a channel-padded conv")
-            dx = k.conv2d_fwd(dconv, k.conv_flip_weight(w), None, pad=kh - 1 - (kh - 1) // 2)
+            dx = k.conv2d_dgrad(dconv, w)
         return dx, None, None, None, None
 
 
@@ -176,7 +178,7 @@ class UpConvFn(torch.autograd.Function):
         grad_buf(b).add_(dwdb[:, -1])
         dx = None
         if ctx.needs_input_grad[0]:
-            du = k.conv2d_fwd(dy, k.conv_flip_weight(w), None, pad=kh - 1 - (kh - 1) // 2)
+            du = k.conv2d_dgrad(dy, w)
             dx = k.sumpool2(du)
         return dx, None, None
 

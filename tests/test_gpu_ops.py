@@ -334,3 +334,25 @@ def test_laprop_agc_step():
         ag.opt_step += 1
         for i in range(len(shapes)):
             close(params[i].data, ag.P[str(i)].data, 1e-6, f"param {i} step {it}")
+
+
+@pytest.mark.parametrize("ci,co,hw,nb", [(4, 32, 64, 3), (32, 48, 32, 8), (48, 64, 16, 16), (64, 64, 8, 40),
+                                        (16, 32, 16, 2), (64, 16, 32, 1)])
+def test_conv_backward_bf16x3(ci, co, hw, nb):
+    """Split-bf16 conv backward (sd_conv2d_dgrad_bf16x3 / sd_conv2d_wgrad_bf16x3) vs the f32 kernels:
+    |err| <= 4e-5 * (the same contraction on |operands|) elementwise (per-product split error <= 3 * 2^-17)."""
+    from sdreamer import kernels as K
+    x = (torch.rand(nb, hw, hw, ci, generator=_g(ci + hw)) - 0.5).to(DEV)
+    w = (torch.randn(co, 5, 5, ci, generator=_g(co)) / (ci * 25) ** 0.5).to(DEV)
+    dy = torch.randn(nb, hw, hw, co, generator=_g(7)).to(DEV)
+    dx = K.conv2d_dgrad(dy, w, fast=True)
+    dx_ref = K.conv2d_dgrad(dy, w, fast=False)
+    bound = 4e-5 * K.conv2d_dgrad(dy.abs(), w.abs(), fast=False) + 1e-6
+    assert ((dx - dx_ref).abs() - bound).max().item() <= 0, "dgrad"
+    if ci in (16, 32, 48, 64):  # the split kernel's output-channel tiles; other widths take the f32 kernel
+        assert (dx - dx_ref).abs().max().item() > 0, "dgrad took the f32 path"
+    dw = K.conv2d_wgrad(x, dy, 5, 5, fast=True)
+    dw_ref = K.conv2d_wgrad(x, dy, 5, 5, fast=False)
+    bound = 4e-5 * K.conv2d_wgrad(x.abs(), dy.abs(), 5, 5, fast=False) + 1e-5
+    assert ((dw - dw_ref).abs() - bound).max().item() <= 0, "wgrad"
+    assert (dw - dw_ref).abs().max().item() > 0, "wgrad took the f32 path"

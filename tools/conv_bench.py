@@ -35,7 +35,9 @@ def main():
         nw = torch.ones(Co, device="cuda")
         for name, fn in (("fwd", lambda: K.conv2d_fwd(x, w, b)), ("fpool", lambda: K.conv2d_fwd_pool(x, w, b, nw)),
                          ("dgrad", lambda: K.conv2d_fwd(dy, wf, None)),
-                         ("wgrad", lambda: K.conv2d_wgrad(x, dy, 5, 5))):
+                         ("dgrad3", lambda: K.conv2d_dgrad(dy, w, pad=2, fast=True)),
+                         ("wgrad", lambda: K.conv2d_wgrad(x, dy, 5, 5, fast=False)),
+                         ("wgrad3", lambda: K.conv2d_wgrad(x, dy, 5, 5, fast=True))):
             us = timeit(fn)
             tot[name] = tot.get(name, 0) + us
             print(f"H{H:3d} Ci{Ci:3d} Co{Co:3d} {name:6s} {us:9.1f} us {fl / us / 1e6:7.1f} TF/s", flush=True)
