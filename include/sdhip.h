@@ -156,8 +156,9 @@ int sd_conv2d_wgrad_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw
 /* Split-bf16 (bf16x3, ~1e-5 relative) backward convolutions (csrc/conv.hip, gemm3_core.h). SD_ESHAPE when the
  * shape is outside the kernels (the caller then takes the f32 path). dgrad: same arguments as sd_conv2d_fwd with
  * in = dOut (Ci channels), w = the flipped weight (sd_conv_flip_weight), out = dIn (Co channels), ups = 0.
- * wgrad: [dW | db] as sd_conv2d_wgrad (ups = 0); workspace >= slabs * Co * (kh*kw*Ci + 1) floats, slabs from
- * sd_conv2d_wgrad_bf16x3_slabs. Replace the backward of Conv2dSamePad (networks.py:59-85). */
+ * wgrad: [dW | db] as sd_conv2d_wgrad (ups = 0, Ci % 4 == 0, Ci >= 16, Co <= 64, power-of-two W >= 8);
+ * workspace >= slabs * Co * (kh*kw*Ci + 1) floats, slabs from sd_conv2d_wgrad_bf16x3_slabs (SD_ESHAPE: not
+ * eligible). Replace the backward of Conv2dSamePad (networks.py:59-85). */
 int sd_conv2d_dgrad_bf16x3(const float* dout, const float* wflip, float* din, int Nb, int Hs, int Ws, int Ci, int Co,
                            int kh, int kw, int pad, sd_stream stream);
 int sd_conv2d_wgrad_bf16x3_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int ups);

@@ -599,85 +599,6 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad3(GemmArgs g, Geom G, int lw
   sdb::gemm3_epilogue<BM, BN, 32, BN>(g, acc, bm0, 0, 0, 0);
 }
 
-// bwd-weight B operand on the split path: rows j = (ky, kx, ci .. ci+3) (+ the ones row j == J for d bias), k = pixel.
-// A thread owns one 4 (pixels) x 4 (j) block: four buffer loads of 4 channels at 4 consecutive pixels (out-of-image
-// taps read 0), transposed in registers into four j rows of 4 pixels (sdb::KM3's store).
-template <int ROWS>
-struct Im2colColsKM3 {
-  static constexpr int NBLK = ROWS * BK / 16;
-  static constexpr int NV = (NBLK + 255) / 256;
-  f32x4 r[NV][4];
-  Geom G;
-  sd_rsrc rs;
-  int lw, lhw;
-  int jy[NV], jx[NV], jc[NV], kind[NV];  // kind 0: image taps, 1: the ones row (j0 == J), 2: zero rows
-  SD_DEV Im2colColsKM3(const Geom& g, int J, int row0, int lw_, int lhw_) : G(g), lw(lw_), lhw(lhw_) {
-    rs = sd_make_rsrc(g.in, (long)g.Nb * g.Hs * g.Ws * g.C * 4);
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int i = threadIdx.x + v * 256;
-      const int j0 = row0 + 4 * (i % (ROWS / 4));
-      jy[v] = jx[v] = jc[v] = 0;
-      kind[v] = j0 < J ? 0 : (j0 == J ? 1 : 2);
-      if (j0 < J) {
-        const int t = j0 / G.C;
-        jc[v] = j0 - t * G.C;
-        jy[v] = t / G.kw - G.pad;
-        jx[v] = t - (t / G.kw) * G.kw - G.pad;
-      }
-    }
-  }
-  SD_DEV void load(int k0, int kend) {
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int i = threadIdx.x + v * 256;
-      const int kq = i / (ROWS / 4);
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int m = k0 + 4 * kq + kk;
-        const int n = m >> lhw, rem = m & ((1 << lhw) - 1);
-        const int yy = (rem >> lw) + jy[v], xx = (rem & ((1 << lw) - 1)) + jx[v];
-        const bool live = i < NBLK && m < kend;
-        const bool ok = live && kind[v] == 0 && (unsigned)yy < (unsigned)G.Hg && (unsigned)xx < (unsigned)G.Wg;
-        const uint32_t off = (uint32_t)(((((long)n * G.Hs + yy) * G.Ws + xx) * G.C + jc[v]) * 4);
-        f32x4 x = sd_bload4(rs, ok ? off : SD_OOB);
-        if (live && kind[v] == 1) x = f32x4{1.f, 0.f, 0.f, 0.f};
-        r[v][kk] = x;
-      }
-    }
-  }
-  SD_DEV void store(__bf16* lds) const {
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int i = threadIdx.x + v * 256;
-      if ((v + 1) * 256 <= NBLK || i < NBLK) {
-        const int rq = i % (ROWS / 4), kq = i / (ROWS / 4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x4 t = {r[v][0][j], r[v][1][j], r[v][2][j], r[v][3][j]};
-          sdb::split_store(lds + (4 * rq + j) * sdb::LROW + 4 * kq, t);
-        }
-      }
-    }
-  }
-};
-
-// bwd-weight: [dW | db] (Co x J+1) = dOut^T (Co x pixels) . im2col(in) (pixels x J+1); M = Co (one tile), N = j
-// (128 per workgroup), K = pixels split over blockIdx.z into partial slabs (slab_reduce sums them in a fixed order).
-template <int BM, int WM, int WN>
-__global__ __launch_bounds__(256, 2) void conv_wgrad3(GemmArgs g, Geom G, int J, int lw, int lhw) {
-  constexpr int BN = 128;
-  const int bn0 = blockIdx.x * BN;
-  const int split = blockIdx.z;
-  const int kbeg = split * g.kchunk;
-  const int kend = min(g.K, kbeg + g.kchunk);
-  sdb::KM3<BM, true> la(g.A, g.lda, g.M, 0);
-  Im2colColsKM3<BN> lb(G, J, bn0, lw, lhw);
-  f32x4 acc[WM / 16][WN / 16];
-  sdb::gemm3_mainloop<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
-  sdb::gemm3_epilogue<BM, BN, WM, WN>(g, acc, 0, bn0, 0, split);
-}
-
 // out[e] = sum_s ws[s * n + e] in a fixed order; 64 outputs per workgroup (one per lane), the 4 waves take every
 // 4th slab and are summed through LDS.
 __global__ __launch_bounds__(256) void slab_reduce(const float* __restrict__ ws, int slabs, long n,
@@ -698,6 +619,161 @@ __global__ __launch_bounds__(256) void slab_reduce(const float* __restrict__ ws,
   part[wave][lane] = v;
   __syncthreads();
   if (wave == 0 && e < n) out[e] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+}
+
+// ---------------------------------------------------------------- direct split-bf16 bwd-weight
+// conv_wgrad_direct's structure (one block of R image rows per step: the input patch with its halo staged in LDS
+// once, every (co, j) product of the block taken from LDS, partial slabs per blockIdx.y) on v_mfma_f32_16x16x32_bf16.
+// k = pixels, 32 per MFMA step: lane group q supplies pixels 4i + q (i = 0..7) of the step, so the 4 lane groups read
+// neighbouring pixels of the patch (CP floats apart: conflict-free) and each lane's 8 B-values are 8 ds_read_b32 at
+// precomputed pixel offsets + its column's tap offset, split to (hi, lo) in registers. dy of the block is staged
+// transposed and pre-split, [co][pos] per plane with pos = 8 (p % 4) + (p / 4) % 8 inside each 32-pixel step, so a
+// lane's 8 A-values (the same pixels) are one ds_read_b128 per plane. Wave w owns NBW 16-column blocks of j and all
+// TM 16-row blocks of co (rows >= Co read zero rows).
+struct DirectW3 {
+  const float* x;
+  const float* dy;
+  float* ws;
+  int Nb, H, W, Ci, Co, kh, kw, pad, R, lw;
+  int J, PW, PH, CP, PS, blocks;
+};
+
+template <int TM, int NBW>
+__global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l16 = lane & 15, q = lane >> 4;
+  const int P = d.R * d.W;
+  float* xp = lds;  // [PH][PW][CP]; channel Ci holds 1.0 (bias column), Ci+1 holds 0.0
+  __bf16* dyh = reinterpret_cast<__bf16*>(lds + d.PH * d.PW * d.CP);  // [TM*16][PS]
+  __bf16* dyl = dyh + TM * 16 * d.PS;
+  for (int e = tid; e < TM * 16 * d.PS; e += 512) {  // rows >= Co stay zero; rows < Co are overwritten per block
+    dyh[e] = (__bf16)0.f;
+    dyl[e] = (__bf16)0.f;
+  }
+  int off[NBW];
+#pragma unroll
+  for (int b = 0; b < NBW; ++b) {
+    const int j = 16 * ((blockIdx.x * NW_D + wave) * NBW + b) + l16;
+    if (j < d.J) {
+      const int t = j / d.Ci, ci = j - t * d.Ci, ky = t / d.kw, kx = t - ky * d.kw;
+      off[b] = (ky * d.PW + kx) * d.CP + ci;
+    } else {
+      off[b] = d.Ci + (j == d.J ? 0 : 1);
+    }
+  }
+  f32x4 acc[TM][NBW];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int b = 0; b < NBW; ++b) acc[i][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int rows_per_img = d.H / d.R, cq = d.Ci / 4, nP = d.PH * d.PW * cq;
+  const int c4 = d.Co / 4, nD = c4 * (P / 4);  // 4x4 blocks: 8 pixel groups per 32-pixel step
+  // this thread's dy block: 4 channels x 4 pixels (pixels c + 4 (4 ih + t) of 32-pixel step sb, t = 0..3)
+  const int dq4 = tid % c4, drest = tid / c4;
+  const int dc = drest % 4, dih = (drest / 4) % 2, dsb = drest / 8;
+  f32x4 rd[4], rp[WD_VP];
+  auto fetch = [&](int rb) {
+    const int n = rb / rows_per_img, y0 = (rb - n * rows_per_img) * d.R;
+    const float* dsrc = d.dy + ((long)n * d.H + y0) * d.W * d.Co;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int px = 32 * dsb + dc + 4 * (4 * dih + t);
+      rd[t] = tid < nD ? *reinterpret_cast<const f32x4*>(dsrc + (long)px * d.Co + 4 * dq4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int v = 0; v < WD_VP; ++v) {
+      const int i = tid + 512 * v;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (i < nP) {
+        const int pix = i / cq, c = 4 * (i - pix * cq);
+        const int py = pix / d.PW, px = pix - py * d.PW;
+        const int iy = y0 - d.pad + py, ix = px - d.pad;
+        if (iy >= 0 && iy < d.H && ix >= 0 && ix < d.W)
+          x = *reinterpret_cast<const f32x4*>(d.x + (((long)n * d.H + iy) * d.W + ix) * d.Ci + c);
+      }
+      rp[v] = x;
+    }
+  };
+  auto stage = [&]() {
+    if (tid < nD) {
+      const int pos = 32 * dsb + 8 * dc + 4 * dih;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const f32x4 t = {rd[0][jj], rd[1][jj], rd[2][jj], rd[3][jj]};
+        const sdb::bf16x4 hi = __builtin_convertvector(t, sdb::bf16x4);
+        const f32x4 r = t - __builtin_convertvector(hi, f32x4);
+        const int o = (4 * dq4 + jj) * d.PS + pos;
+        *reinterpret_cast<sdb::bf16x4*>(dyh + o) = hi;
+        *reinterpret_cast<sdb::bf16x4*>(dyl + o) = __builtin_convertvector(r, sdb::bf16x4);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < WD_VP; ++v) {
+      const int i = tid + 512 * v;
+      if (i < nP) {
+        const int pix = i / cq, c = 4 * (i - pix * cq);
+        *reinterpret_cast<f32x4*>(xp + pix * d.CP + c) = rp[v];
+      }
+    }
+  };
+  for (int pix = tid; pix < d.PH * d.PW; pix += 512) {
+    xp[pix * d.CP + d.Ci] = 1.f;
+    xp[pix * d.CP + d.Ci + 1] = 0.f;
+  }
+  int rb = blockIdx.y;
+  if (rb < d.blocks) fetch(rb);
+  for (; rb < d.blocks; rb += gridDim.y) {
+    __syncthreads();  // previous block's LDS reads are done
+    stage();
+    __syncthreads();
+    if (rb + (int)gridDim.y < d.blocks) fetch(rb + gridDim.y);  // next block's loads overlap this block's MFMAs
+    for (int s = 0; s < P / 32; ++s) {
+      sdb::bf16x8 ah[TM], al[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int o = (16 * i + l16) * d.PS + 32 * s + 8 * q;
+        ah[i] = *reinterpret_cast<const sdb::bf16x8*>(dyh + o);
+        al[i] = *reinterpret_cast<const sdb::bf16x8*>(dyl + o);
+      }
+      int pb[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int p = 32 * s + 4 * i + q, py = p >> d.lw, px = p & (d.W - 1);
+        pb[i] = (py * d.PW + px) * d.CP;
+      }
+#pragma unroll
+      for (int b = 0; b < NBW; ++b) {
+        const f32x4 v0 = {xp[pb[0] + off[b]], xp[pb[1] + off[b]], xp[pb[2] + off[b]], xp[pb[3] + off[b]]};
+        const f32x4 v1 = {xp[pb[4] + off[b]], xp[pb[5] + off[b]], xp[pb[6] + off[b]], xp[pb[7] + off[b]]};
+        const sdb::bf16x4 h0 = __builtin_convertvector(v0, sdb::bf16x4), h1 = __builtin_convertvector(v1, sdb::bf16x4);
+        const sdb::bf16x4 e0 = __builtin_convertvector(v0 - __builtin_convertvector(h0, f32x4), sdb::bf16x4);
+        const sdb::bf16x4 e1 = __builtin_convertvector(v1 - __builtin_convertvector(h1, f32x4), sdb::bf16x4);
+        const sdb::bf16x8 bh = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+        const sdb::bf16x8 bl = __builtin_shufflevector(e0, e1, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          acc[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, acc[i][b], 0, 0, 0);
+          acc[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, acc[i][b], 0, 0, 0);
+          acc[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, acc[i][b], 0, 0, 0);
+        }
+      }
+    }
+  }
+  float* out = d.ws + (long)blockIdx.y * d.Co * (d.J + 1);
+#pragma unroll
+  for (int b = 0; b < NBW; ++b) {
+    const int j = 16 * ((blockIdx.x * NW_D + wave) * NBW + b) + l16;
+    if (j <= d.J) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = 16 * i + 4 * q + r;
+          if (co < d.Co) out[(long)co * (d.J + 1) + j] = acc[i][b][r];
+        }
+    }
+  }
 }
 
 // SDHIP_CONV_ALGO (benchmarking knob): 0 = auto, 1 = 32x32-tile kernels only, 2 = 16x16 kernels where eligible
@@ -1162,18 +1238,76 @@ extern "C" int sd_pool_rms_bwd(const float* pooled, const uint8_t* amax, const f
 
 // ---------------------------------------------------------------- split-bf16 backward entry points
 namespace {
-bool wgrad3_ok(int Hs, int Ws, int Ci, int Co, int kh, int ups) {
-  return ups == 0 && Ci % 4 == 0 && Co <= 64 && Co % 4 == 0 && ilog2_exact(Ws) >= 0 && ilog2_exact(Hs * Ws) >= 0 &&
-         kh * kh * Ci / 4 <= 1 << 20;
+}  // namespace
+
+
+namespace {
+bool direct3_plan(int Nb, int H, int W, int Ci, int Co, int kh, int kw, int ups, DirectPlan& pl) {
+  if (ups != 0 || Co % 4 || Co > 64 || Ci % 4 || Ci < 16 || W < 8 || ilog2_exact(W) < 0 || W > 128) return false;
+  pl.R = 128 / W < H ? 128 / W : H;
+  const int P = pl.R * W;
+  if (H % pl.R || P % 32) return false;
+  const int TM = (Co + 15) / 16, CP = patch_stride(Ci);
+  const int PH = pl.R + kh - 1, PW = W + kw - 1;
+  pl.lds = (size_t)PH * PW * CP * 4 + (size_t)TM * 16 * (P + 8) * 2 * 2;
+  if (pl.lds > 160 * 1024 || PH * PW * (Ci / 4) > WD_VP * 512 || (Co / 4) * (P / 4) > 512) return false;
+  const int J = kh * kw * Ci, JB = (J + 1 + 15) / 16;
+  pl.ws = false;
+  // column blocks per wave: the accumulators (TM * NBW * 4 VGPRs) bound it; SDHIP_WGRAD3_NBW overrides (tuning knob)
+  static int nbw_env = -1;
+  if (nbw_env < 0) {
+    const char* e = getenv("SDHIP_WGRAD3_NBW");
+    nbw_env = e ? atoi(e) : 0;
+  }
+  const int nmax = nbw_env > 0 ? nbw_env : (TM <= 3 ? 7 : 4);
+  pl.gx = (JB + NW_D * nmax - 1) / (NW_D * nmax);
+  const int need = (JB + NW_D * pl.gx - 1) / (NW_D * pl.gx);
+  pl.nbw = need <= 2 ? 2 : need <= 4 ? 4 : need <= 5 ? 5 : 7;
+  const int blocks = Nb * (H / pl.R);
+  pl.gy = 256 / pl.gx;
+  if (pl.gy > blocks) pl.gy = blocks;
+  if (pl.gy < 1) pl.gy = 1;
+  pl.slabs = pl.gy;
+  return true;
 }
-int wgrad3_slabs(int Nb, int Hs, int Ws, int Ci, int kh, int kw) {
-  const long K = (long)Nb * Hs * Ws;
-  const int ntiles = sd_cdiv((long)kh * kw * Ci + 1, 128);
-  long ks = (512 + ntiles - 1) / ntiles;
-  const long kmax = K / (8 * BK);  // >= 8 k tiles per slab
-  if (ks > kmax) ks = kmax;
-  if (ks > 256) ks = 256;
-  return ks < 1 ? 1 : (int)ks;
+
+int wgrad3_direct(const float* in, const float* dout, float* dw_db, float* ws, long ws_floats, int Nb, int H, int W,
+                  int Ci, int Co, int kh, int kw, int pad, const DirectPlan& pl, hipStream_t s) {
+  DirectW3 d;
+  d.x = in; d.dy = dout; d.Nb = Nb; d.H = H; d.W = W; d.Ci = Ci; d.Co = Co; d.kh = kh; d.kw = kw; d.pad = pad;
+  d.lw = ilog2_exact(W); d.J = kh * kw * Ci; d.R = pl.R;
+  d.PW = W + kw - 1; d.PH = d.R + kh - 1;
+  d.CP = patch_stride(Ci);
+  d.PS = d.R * W + 8;
+  d.blocks = Nb * (H / d.R);
+  if (!ws || ws_floats < (long)pl.slabs * Co * (d.J + 1)) return SD_EARG;
+  d.ws = ws;
+  const dim3 grid(pl.gx, pl.gy);
+  const int TM = (Co + 15) / 16;
+  bool launched = false;
+#define SD_WD3(TM_, NB_)                                                                                   \
+  if (TM == TM_ && pl.nbw == NB_) {                                                                       \
+    static bool raised = false;                                                                            \
+    if (!raised && pl.lds > 65536) {                                                                       \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad3_direct<TM_, NB_>),                 \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)       \
+        return SD_EARG;                                                                                    \
+      raised = true;                                                                                       \
+    }                                                                                                      \
+    conv_wgrad3_direct<TM_, NB_><<<grid, 512, pl.lds, s>>>(d);                                            \
+    launched = true;                                                                                       \
+  }
+  SD_WD3(1, 2) SD_WD3(1, 4) SD_WD3(1, 5) SD_WD3(1, 7)
+  SD_WD3(2, 2) SD_WD3(2, 4) SD_WD3(2, 5) SD_WD3(2, 7)
+  SD_WD3(3, 2) SD_WD3(3, 4) SD_WD3(3, 5) SD_WD3(3, 7)
+  SD_WD3(4, 2) SD_WD3(4, 4) SD_WD3(4, 5) SD_WD3(4, 7)
+#undef SD_WD3
+  if (!launched) return SD_ESHAPE;
+  SD_LAUNCH_CHECK();
+  const long n = (long)Co * (d.J + 1);
+  slab_reduce<<<(int)((n + 63) / 64), 256, 0, s>>>(ws, pl.slabs, n, dw_db);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
 }
 }  // namespace
 
@@ -1203,8 +1337,9 @@ extern "C" int sd_conv2d_dgrad_bf16x3(const float* dout, const float* wflip, flo
 }
 
 extern "C" int sd_conv2d_wgrad_bf16x3_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int ups) {
-  if (!wgrad3_ok(Hs, Ws, Ci, Co, kh, ups)) return SD_ESHAPE;
-  return wgrad3_slabs(Nb, Hs, Ws, Ci, kh, kw);
+  DirectPlan pl;
+  if (!direct3_plan(Nb, Hs, Ws, Ci, Co, kh, kw, ups, pl)) return SD_ESHAPE;
+  return pl.slabs;
 }
 
 extern "C" int sd_conv2d_wgrad_bf16x3(const float* in, const float* dout, float* dw_db, float* workspace,
@@ -1212,27 +1347,7 @@ extern "C" int sd_conv2d_wgrad_bf16x3(const float* in, const float* dout, float*
                                       sd_stream stream_) {
   hipStream_t s = (hipStream_t)stream_;
   if (Nb <= 0) return SD_OK;
-  if (!wgrad3_ok(Hs, Ws, Ci, Co, kh, 0) || !al16(in) || !al16(dout) || (long)Nb * Hs * Ws * Ci >= (1L << 29))
-    return SD_ESHAPE;
-  const int J = kh * kw * Ci;
-  const int ks = wgrad3_slabs(Nb, Hs, Ws, Ci, kh, kw);
-  if (ks > 1 && (!workspace || ws_floats < (long)ks * Co * (J + 1))) return SD_EARG;
-  Geom G{in, Nb, Hs, Ws, Ci, Hs, Ws, kh, kw, pad, 0};
-  GemmArgs g{};
-  g.A = dout; g.lda = Co; g.C = dw_db; g.ldc = J + 1; g.ws = workspace;
-  g.M = Co; g.N = J + 1; g.K = Nb * Hs * Ws; g.batch = 1; g.ksplit = ks;
-  const long kc = ((long)g.K + ks - 1) / ks;
-  g.kchunk = (int)((kc + BK - 1) / BK * BK);
-  g.alpha = 1.f; g.beta = 0.f;
-  const int lw = ilog2_exact(Ws), lhw = ilog2_exact(Hs * Ws);
-  const dim3 grid(sd_cdiv(g.N, 128), 1, ks);
-  if (Co <= 32) conv_wgrad3<32, 32, 32><<<grid, 256, 0, s>>>(g, G, J, lw, lhw);
-  else conv_wgrad3<64, 32, 64><<<grid, 256, 0, s>>>(g, G, J, lw, lhw);
-  SD_LAUNCH_CHECK();
-  if (ks > 1) {
-    const long n = (long)Co * (J + 1);
-    slab_reduce<<<(int)((n + 63) / 64), 256, 0, s>>>(workspace, ks, n, dw_db);
-    SD_LAUNCH_CHECK();
-  }
-  return SD_OK;
+  DirectPlan pl;
+  if (!direct3_plan(Nb, Hs, Ws, Ci, Co, kh, kw, 0, pl) || !al16(in) || !al16(dout)) return SD_ESHAPE;
+  return wgrad3_direct(in, dout, dw_db, workspace, ws_floats, Nb, Hs, Ws, Ci, Co, kh, kw, pad, pl, s);
 }

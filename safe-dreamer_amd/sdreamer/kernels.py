@@ -354,10 +354,9 @@ def conv2d_dgrad(dout, w, pad=None, fast=True):
     return conv2d_fwd(dout, wf, None, pad=pad)
 
 
-def conv2d_wgrad(x, dout, kh, kw, ups=0, pad=None, fast=False):
-    """returns (Co, kh*kw*Ci + 1) = [dW | db]. fast: split-bf16 implicit-GEMM kernel (sd_conv2d_wgrad_bf16x3) where
-    eligible. Off by default: its im2col operand is gathered from memory per k tile, and at the encoder shapes the
-    f32 direct kernel (input patch staged once per row block in LDS) is faster (tools/conv_bench.py)."""
+def conv2d_wgrad(x, dout, kh, kw, ups=0, pad=None, fast=True):
+    """returns (Co, kh*kw*Ci + 1) = [dW | db]. fast: split-bf16 direct kernel (sd_conv2d_wgrad_bf16x3) where eligible
+    (Ci >= 16; the 4-channel first layer keeps the f32 direct kernel)."""
     Nb, H, W, Ci = x.shape
     Co = dout.shape[-1]
     pad = (kh - 1) // 2 if pad is None else pad

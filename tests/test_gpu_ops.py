@@ -355,4 +355,5 @@ def test_conv_backward_bf16x3(ci, co, hw, nb):
     dw_ref = K.conv2d_wgrad(x, dy, 5, 5, fast=False)
     bound = 4e-5 * K.conv2d_wgrad(x.abs(), dy.abs(), 5, 5, fast=False) + 1e-5
     assert ((dw - dw_ref).abs() - bound).max().item() <= 0, "wgrad"
-    assert (dw - dw_ref).abs().max().item() > 0, "wgrad took the f32 path"
+    if K.nat.fns["sd_conv2d_wgrad_bf16x3_slabs"](nb, hw, hw, ci, co, 5, 5, 0) > 0:  # the split kernel's range
+        assert (dw - dw_ref).abs().max().item() > 0, "wgrad took the f32 path"
