@@ -29,7 +29,7 @@ from . import _native as nat
 from . import kernels as K
 from . import ops
 from . import parallel
-from .networks import MLPHead, MultiDecoder, MultiEncoder, Projector, ReturnEMA
+from .networks import MLPHead, MultiDecoder, MultiEncoder, Projector, ReturnEMA, heads_nograd
 from .optim import LaProp, WarmupSchedule
 from .rssm import RSSM, STREAM_ACT, STREAM_IMG, STREAM_POLICY
 
@@ -563,11 +563,13 @@ class Dreamer(nn.Module):
         H1, N = ifeat.shape[:2]
         dev = ifeat.device
         flat = ifeat.reshape(H1 * N, -1)
-        # frozen heads on the imagined trajectories: split-bf16 contractions (no sampled index depends on them)
-        i_rew = K.twohot_mode(self.reward.logits_nograd(flat, True), self.rbins).view(H1, N)
-        i_contl = self.cont.logits_nograd(flat, True).view(H1, N)
-        i_val = K.twohot_mode(self.value.logits_nograd(flat, True), self.vbins).view(H1, N)
-        i_slow = K.twohot_mode(self._slow_value.logits_nograd(flat, True), self.vbins).view(H1, N)
+        # frozen heads on the imagined trajectories: split-bf16 contractions (no sampled index depends on them), the
+        # four first layers as one batched launch
+        l_rew, l_cont, l_val, l_slow = heads_nograd((self.reward, self.cont, self.value, self._slow_value), flat, True)
+        i_rew = K.twohot_mode(l_rew, self.rbins).view(H1, N)
+        i_contl = l_cont.view(H1, N)
+        i_val = K.twohot_mode(l_val, self.vbins).view(H1, N)
+        i_slow = K.twohot_mode(l_slow, self.vbins).view(H1, N)
         disc = 1 - 1 / self.horizon
         rew_n, contl_n, val_n = i_rew.t().contiguous(), i_contl.t().contiguous(), i_val.t().contiguous()
         i_cont = torch.empty(N, H1, device=dev)

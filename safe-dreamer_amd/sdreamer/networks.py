@@ -164,6 +164,33 @@ class MLPHead(nn.Module):
         h = self.mlp.forward_nograd(x.reshape(-1, x.shape[-1]), fast)
         return K.linear(h, self.last.weight, self.last.bias, fast=fast)
 
+    @torch.no_grad()
+    def logits_from_first(self, h0, fast=False):
+        """logits given the first layer's pre-norm output h0 = x . W0^T + b0 (see heads_nograd)."""
+        (_, norm0), rest = self.mlp._mods[0], self.mlp._mods[1:]
+        h = K.rmsnorm_fwd(h0, norm0.weight, act=1)[0]
+        for lin, norm in rest:
+            h = K.rmsnorm_fwd(K.linear(h, lin.weight, lin.bias, fast=fast), norm.weight, act=1)[0]
+        return K.linear(h, self.last.weight, self.last.bias, fast=fast)
+
+
+@torch.no_grad()
+def heads_nograd(heads, x, fast=False):
+    """Frozen logits of several MLPHeads on the same input rows x (M, F) with ONE batched launch for their first
+    layers (the contraction over F dominates: A is read once per column tile for all heads, 4x the workgroups of
+    one head's launch). Falls back to per-head forwards when the first layers differ in shape or use symlog."""
+    firsts = [h.mlp._mods[0][0] for h in heads]
+    shape = tuple(firsts[0].weight.shape)
+    if any(h.mlp._symlog_inputs or h.mlp.n < 1 for h in heads) or any(tuple(f.weight.shape) != shape for f in firsts):
+        return [h.logits_nograd(x, fast) for h in heads]
+    x = x.reshape(-1, x.shape[-1])
+    M, n = x.shape[0], len(heads)
+    w = torch.stack([f.weight for f in firsts])  # (n, U, F)
+    b = torch.stack([f.bias for f in firsts])  # (n, U)
+    h0 = torch.empty(n, M, shape[0], dtype=torch.float32, device=x.device)
+    K.gemm(x.expand(n, M, x.shape[1]), w.transpose(1, 2), h0, bias=b, fast=fast)
+    return [h.logits_from_first(h0[i], fast) for i, h in enumerate(heads)]
+
 
 class ConvEncoder(nn.Module):
     """networks.py:192-234. Input NHWC float in [0, 1] (B*T, 64, 64, 3); output (B*T, C*h*w) in NCHW flatten order."""
