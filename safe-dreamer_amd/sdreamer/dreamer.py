@@ -33,6 +33,10 @@ from .networks import MLPHead, MultiDecoder, MultiEncoder, Projector, ReturnEMA,
 from .optim import LaProp, WarmupSchedule
 from .rssm import RSSM, STREAM_ACT, STREAM_IMG, STREAM_POLICY
 
+# SDREAMER_S2_AFTER_SCAN=1 (schedule knob): the actor/critic phase starts after the scan backward (beside the encoder
+# backward) instead of right after the replay-value backward (beside the scan backward)
+S2_AFTER_SCAN = os.environ.get("SDREAMER_S2_AFTER_SCAN", "0") == "1"
+
 # csrc/img.hip runs the whole imagination as 9 fused launches per step; SDREAMER_FUSED_IMAG=0 selects the per-op
 # HIP kernels (tests compare the two)
 FUSED_IMAG = os.environ.get("SDREAMER_FUSED_IMAG", "1") != "0"
@@ -309,21 +313,22 @@ class Dreamer(nn.Module):
             gS1, _ = cap(lambda: self._ph_side_returns(st), side_cap)
             gM1, _ = cap(lambda: self._ph_wm(st), main_cap)
             gR, _ = cap(lambda: self._ph_repval(st), main_cap)
-            gM2, _ = cap(lambda: self._ph_posterior_bwd(st), main_cap)
+            gM2a, _ = cap(lambda: self._ph_scan_bwd(st), main_cap)
+            gM2b, _ = cap(lambda: self._ph_encoder_bwd(st), main_cap)
             gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
             gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st), main_cap)
             torch.cuda.synchronize()
-            for g in (gP, gR, gM2, gS2, gM3):
+            for g in (gP, gR, gM2a, gM2b, gS2, gM3):
                 if g.n_collectives:
                     raise RuntimeError("unexpected exchange step in a single-graph phase")
-            self._graph = (gP, gS1, gM1, gR, gM2, gS2, gM3)
+            self._graph = (gP, gS1, gM1, gR, gM2a, gM2b, gS2, gM3)
             self._gst, self._g_post, self._g_keys, self._g_mvec = st, post, keys, mvec
         for k, v in data.items():
             self._g_in[k].copy_(v)
         for dst, src in zip(self._g_init, initial):
             dst.copy_(src)
         self._seed_dev.fill_(int(seed) & 0x7FFFFFFFFFFFFFFF)
-        gP, gS1, gM1, gR, gM2, gS2, gM3 = self._graph
+        gP, gS1, gM1, gR, gM2a, gM2b, gS2, gM3 = self._graph
         main = torch.cuda.current_stream()
         side = self._side if self.use_side_stream else main
         gP.replay()
@@ -341,7 +346,11 @@ class Dreamer(nn.Module):
         gR.replay()
         ev_rep = torch.cuda.Event()
         ev_rep.record()
-        gM2.replay()
+        gM2a.replay()
+        if S2_AFTER_SCAN:
+            ev_rep = torch.cuda.Event()
+            ev_rep.record()
+        gM2b.replay()
         with torch.cuda.stream(side):
             side.wait_event(ev_rep)
             gS2.replay()
@@ -413,16 +422,17 @@ class Dreamer(nn.Module):
         mk("start")
         embed = self.encoder(data)
         mk("encoder_fwd")
-        post_stoch, post_deter, post_logit = self.rssm.observe(embed, data["action"], initial, data["is_first"],
+        # the scan sees a leaf copy of embed: its backward stops there, so scan and encoder backward are separate
+        # phases (_ph_scan_bwd / _ph_encoder_bwd)
+        embed_l = embed.detach().requires_grad_(embed.requires_grad)
+        post_stoch, post_deter, post_logit = self.rssm.observe(embed_l, data["action"], initial, data["is_first"],
                                                                seed=seed, row_offset=ro)
         mk("scan_fwd")
-        if self.marks is not None and embed.requires_grad:
-            embed.register_hook(lambda g: mk("scan_bwd"))
         leaves = [t.detach().requires_grad_(True) for t in (post_stoch, post_deter, post_logit)]
         feat_l = self.rssm.get_feat(leaves[0], leaves[1])
         feat_r = feat_l.detach().requires_grad_(True)  # replay-value leaf (side stream)
-        return dict(data=data, seed=seed, ro=ro, embed=embed, post_stoch=post_stoch, post_deter=post_deter,
-                    post_logit=post_logit, leaves=leaves, feat_l=feat_l, feat_r=feat_r)
+        return dict(data=data, seed=seed, ro=ro, embed=embed, embed_l=embed_l, post_stoch=post_stoch,
+                    post_deter=post_deter, post_logit=post_logit, leaves=leaves, feat_l=feat_l, feat_r=feat_r)
 
     def _ph_side_returns(self, st):
         """side: imagination (dreamer.py:578-597), imagined heads, lambda-returns + ReturnEMA (598-636)."""
@@ -456,7 +466,11 @@ class Dreamer(nn.Module):
         st.update(repval=loss, rv_metrics=rv_metrics, rret=rret)
 
     def _ph_posterior_bwd(self, st):
-        """main: posterior gradient = head-loss leaf grads + replay-value feat grad -> scan + encoder backward."""
+        self._ph_scan_bwd(st)
+        self._ph_encoder_bwd(st)
+
+    def _ph_scan_bwd(self, st):
+        """main: posterior gradient = head-loss leaf grads + replay-value feat grad -> scan backward (to embed)."""
         SK = self.rssm.flat_stoch
         leaves = st["leaves"]
         self._mark("repval_wait")
@@ -465,6 +479,13 @@ class Dreamer(nn.Module):
         g_stoch = lg[0] + g_feat[..., :SK].reshape(leaves[0].shape)
         g_deter = lg[1] + g_feat[..., SK:]
         torch.autograd.backward([st["post_stoch"], st["post_deter"], st["post_logit"]], [g_stoch, g_deter, lg[2]])
+        self._mark("scan_bwd")
+
+    def _ph_encoder_bwd(self, st):
+        """main: encoder backward from the scan's embed gradient."""
+        g = st["embed_l"].grad
+        if g is not None:
+            st["embed"].backward(g)
         self._mark("encoder_bwd")
 
     def _ph_side_ac(self, st):
