@@ -287,6 +287,15 @@ typedef struct sd_imagine {
 int sd_imagine_work_floats(const sd_imagine* d);
 int sd_imagine_run(const sd_imagine* d, sd_stream stream);
 
+/* InfoNCE representation loss (dreamer.py:533-542): cross_entropy(logits - rowmax(logits), arange) on an (n, ncol)
+ * row-major logits block (ld floats between rows), row r labelled with column r + label_off (data parallel: local
+ * rows against the gathered x2 of every rank). fwd writes per-row losses, the row log-sum-exp (saved for bwd) and the
+ * mean loss (1 float); bwd writes dlogits (n, ncol) = g[0] * scale * (softmax - onehot), g a device scalar. */
+int sd_infonce_fwd(const float* logits, long ld, int n, int ncol, long label_off, float* row_loss, float* lse,
+                   float* loss, sd_stream stream);
+int sd_infonce_bwd(const float* logits, long ld, int n, int ncol, long label_off, const float* lse, const float* g,
+                   float scale, float* dlogits, sd_stream stream);
+
 /* Profiling aid: store the device wall clock (constant rate, sd_wall_clock_khz) into buf[idx] when `stream` reaches
  * this point; capturable into a HIP graph. Not part of the reference interface. */
 int sd_mark(uint64_t* buf, int idx, sd_stream stream);

@@ -627,6 +627,13 @@ class OracleAgent:
             off = ~torch.eye(x1.shape[-1], dtype=torch.bool)
             red = cc[off].pow(2).sum()
             losses["barlow"] = inv + float(c.r2dreamer.lambd) * red
+        elif s.rep_loss == "infonce":  # dreamer.py:533-542
+            x1 = F.linear(feat.reshape(B * T, -1), P["prj.w.weight"])
+            x2 = embed.reshape(B * T, -1).detach()
+            logits = torch.matmul(x1, x2.T)
+            norm_logits = logits - torch.max(logits, 1)[0][:, None]
+            labels = torch.arange(norm_logits.shape[0]).long()
+            losses["infonce"] = F.cross_entropy(norm_logits, labels)
         else:
             raise NotImplementedError(s.rep_loss)
         losses["rew"] = torch.mean(-twohot_log_prob(M.head_logits("reward", feat), M.rbins, data["reward"].float()))

@@ -251,6 +251,69 @@ extern "C" int sd_barlow_dc(const float* c, const float* g, float* dc, int E, fl
   return SD_OK;
 }
 
+// ---- InfoNCE (dreamer.py:533-542): cross_entropy(logits - rowmax, arange) over the rows of x1 x2^T.
+// Row r's label column is r + label_off (data parallel: this rank's rows against every rank's x2). One workgroup
+// per row: max, log-sum-exp (fixed-order block reductions), loss_r = lse_r - l[r][r + off]; the mean over rows is a
+// second single-block kernel (deterministic). Backward: dl[r][c] = g * scale * (softmax(l_r)[c] - [c == r + off]).
+namespace {
+__global__ __launch_bounds__(256) void infonce_rows(const float* __restrict__ l, long ld, int ncol, long off,
+                                                    float* __restrict__ row_loss, float* __restrict__ lse) {
+  __shared__ float red[4];
+  const int r = blockIdx.x;
+  const float* x = l + (long)r * ld;
+  float m = -INFINITY;
+  for (int c = threadIdx.x; c < ncol; c += 256) m = fmaxf(m, x[c]);
+  m = wave_max(m);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float s = 0.f;
+  for (int c = threadIdx.x; c < ncol; c += 256) s += expf(x[c] - m);
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) {
+    const float v = m + logf(s);
+    lse[r] = v;
+    row_loss[r] = v - x[r + off];
+  }
+}
+__global__ __launch_bounds__(256) void mean_kernel(const float* __restrict__ v, int n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += v[i];
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) out[0] = s / (float)n;
+}
+__global__ void infonce_bwd_kernel(const float* __restrict__ l, long ld, int n, int ncol, long off,
+                                   const float* __restrict__ lse, const float* __restrict__ g, float scale,
+                                   float* __restrict__ dl) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)n * ncol) return;
+  const int r = (int)(i / ncol), c = (int)(i - (long)r * ncol);
+  const float p = expf(l[(long)r * ld + c] - lse[r]);
+  dl[(long)r * ncol + c] = g[0] * scale * (p - (c == r + off ? 1.f : 0.f));
+}
+}  // namespace
+
+extern "C" int sd_infonce_fwd(const float* logits, long ld, int n, int ncol, long label_off, float* row_loss,
+                              float* lse, float* loss, sd_stream s) {
+  if (n <= 0) return SD_OK;
+  if (label_off < 0 || label_off + n > ncol) return SD_EARG;
+  infonce_rows<<<n, 256, 0, (hipStream_t)s>>>(logits, ld, ncol, label_off, row_loss, lse);
+  SD_LAUNCH_CHECK();
+  mean_kernel<<<1, 256, 0, (hipStream_t)s>>>(row_loss, n, loss);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_infonce_bwd(const float* logits, long ld, int n, int ncol, long label_off, const float* lse,
+                              const float* g, float scale, float* dlogits, sd_stream s) {
+  if (n <= 0) return SD_OK;
+  infonce_bwd_kernel<<<nb((long)n * ncol), 256, 0, (hipStream_t)s>>>(logits, ld, n, ncol, label_off, lse, g, scale,
+                                                                     dlogits);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
 // ---- timeline marks (profiling aid): one thread stores the constant-rate wall clock into buf[idx]; enqueued on a
 // stream (and capturable into a HIP graph) it timestamps the point the stream has reached
 namespace {

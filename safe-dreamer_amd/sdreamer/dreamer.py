@@ -109,11 +109,11 @@ class Dreamer(nn.Module):
             recon = self._loss_scales.pop("recon")
             self._loss_scales.update({k: recon for k in self.decoder.all_keys})
             modules["decoder"] = self.decoder
-        elif self.rep_loss == "r2dreamer":
+        elif self.rep_loss in ("r2dreamer", "infonce"):
             self.prj = Projector(self.rssm.feat_size, self.embed_size)
             modules["projector"] = self.prj
             self.barlow_lambd = float(config.r2dreamer.lambd)
-            if bool(config.r2dreamer.aug.enabled):
+            if self.rep_loss == "r2dreamer" and bool(config.r2dreamer.aug.enabled):
                 raise NotImplementedError("r2dreamer augmentation is an off-path variant (SURVEY.md §8(f) f4)")
         else:
             raise NotImplementedError(f"rep_loss={self.rep_loss} (off-path variant, SURVEY.md §8(f) f4)")
@@ -529,6 +529,9 @@ class Dreamer(nn.Module):
                     d = (mode - K.symlog(data[key].contiguous())) ** 2.0  # SymlogDist mse, distributions.py:174-190
                     d = torch.where(d < 1e-8, torch.zeros_like(d), d)
                     losses[key] = d.sum(list(range(2, d.dim()))).mean()
+        elif self.rep_loss == "infonce":  # dreamer.py:533-542
+            x1 = self.prj(feat.reshape(B * T, -1))
+            losses["infonce"] = parallel.infonce(x1, embed.reshape(B * T, -1), self.world)
         else:
             x1 = self.prj(feat.reshape(B * T, -1))
             x2 = embed.reshape(B * T, -1).detach()

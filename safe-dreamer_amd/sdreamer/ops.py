@@ -344,3 +344,31 @@ class BarlowFn(torch.autograd.Function):
         dx1 = torch.empty_like(x1)
         k.nat.call("sd_standardize_bwd", k.p(x1), k.p(m1), k.p(s1), k.p(dn1), k.p(dx1), Nr, E, 1e-8, k.stream())
         return dx1, None, None
+
+
+class InfoNCEFn(torch.autograd.Function):
+    """InfoNCE loss (dreamer.py:533-542): logits = x1 x2g^T (f32 GEMM), cross entropy against the diagonal; rows of x1
+    (n, E) with grad, x2g (Nc, E) detached (all ranks' x2 under data parallel), row r labelled Nc-column r + off.
+    Returns the mean over this rank's rows (the DP mean all-reduce of the gradients makes it the global mean)."""
+
+    @staticmethod
+    def forward(ctx, x1, x2g, off):
+        x1 = x1.contiguous()
+        n, nc = x1.shape[0], x2g.shape[0]
+        logits = k.mm(x1, x2g.t())
+        row = torch.empty(n, dtype=torch.float32, device=x1.device)
+        lse = torch.empty(n, dtype=torch.float32, device=x1.device)
+        loss = torch.empty(1, dtype=torch.float32, device=x1.device)
+        k.nat.call("sd_infonce_fwd", k.p(logits), nc, n, nc, int(off), k.p(row), k.p(lse), k.p(loss), k.stream())
+        ctx.save_for_backward(x2g, logits, lse)
+        ctx.off = int(off)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        x2g, logits, lse = ctx.saved_tensors
+        n, nc = logits.shape
+        dl = torch.empty_like(logits)
+        gg = g.reshape(1).contiguous()
+        k.nat.call("sd_infonce_bwd", k.p(logits), nc, n, nc, ctx.off, k.p(lse), k.p(gg), 1.0 / n, k.p(dl), k.stream())
+        return k.mm(dl, x2g, fast=True), None, None

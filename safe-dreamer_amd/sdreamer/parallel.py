@@ -6,7 +6,8 @@ Exchange steps per update (every other stage is row-independent):
   2. ReturnEMA: the imagined λ-returns of every rank are gathered (each rank writes its rows into a zeroed
      (world·N, H) buffer, one sum all-reduce) so every rank computes the same global quantiles
      (networks.py:417 takes the quantile over the whole batch);
-  3. Barlow loss (r2dreamer): two all-reduces per update — column sums, then column sums of squared deviations
+  3. InfoNCE (rep_loss=infonce): x2 of every rank is gathered (the negatives are the whole batch);
+  4. Barlow loss (r2dreamer): two all-reduces per update — column sums, then column sums of squared deviations
      together with the centred E x E cross-product — so loss and gradient equal the single-GPU values
      (dreamer.py:525-532 normalises over all B*T rows). The backward needs no exchange: the two batch sums the
      standardisation backward takes are functions of the global c and column sums (see _DistBarlowLoss).
@@ -188,3 +189,17 @@ def barlow(x1, x2, lambd, world):
     if world > 1 and is_dist():
         return barlow_dist(x1, x2, lambd, world)
     return ops.BarlowFn.apply(x1, x2, lambd)
+
+
+def infonce(x1, x2, world):
+    """InfoNCE (dreamer.py:533-542) with every rank's rows as negatives: x2 of all ranks is gathered (one sum
+    all-reduce of a zero-padded buffer), this rank's rows are labelled with their global column."""
+    x2 = x2.detach().contiguous()
+    if world > 1 and is_dist():
+        n = x2.shape[0]
+        rank = dist.get_rank()
+        x2g = torch.zeros((world * n,) + tuple(x2.shape[1:]), dtype=x2.dtype, device=x2.device)
+        x2g[rank * n:(rank + 1) * n].copy_(x2)
+        collective(lambda: dist.all_reduce(x2g))
+        return ops.InfoNCEFn.apply(x1, x2g, rank * n)
+    return ops.InfoNCEFn.apply(x1, x2, 0)

@@ -38,6 +38,7 @@ CASES = {
     # name: (config, overrides, obs shapes, act_dim, discrete, B, T, H)
     "proprio_dreamer": ("dmc/proprio", [], {"position": (3,), "velocity": (2,)}, 1, False, 4, 16, 8),
     "walker_r2": ("dmc/cnn", [], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
+    "walker_infonce": ("dmc/cnn", ["model.rep_loss=infonce"], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
     "walker_dreamer": ("dmc/walker_dreamer", [], {"image": (64, 64, 3)}, 6, False, 2, 4, 3),
     "atari_r2": ("dmc/atari_breakout", [], {"image": (64, 64, 3)}, 4, True, 2, 4, 3),
     "maze_r2": ("dmc/memory_maze", [], {"image": (64, 64, 3)}, 6, True, 2, 4, 3),

@@ -14,17 +14,23 @@ HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = {
     "proprio_dreamer": ("dmc/proprio", {"position": (3,), "velocity": (2,)}),
     "walker_r2": ("dmc/cnn", {"image": (64, 64, 3)}),
+    "walker_infonce": ("dmc/cnn", {"image": (64, 64, 3)}, ["model.rep_loss=infonce"]),
     "walker_dreamer": ("dmc/walker_dreamer", {"image": (64, 64, 3)}),
     "atari_r2": ("dmc/atari_breakout", {"image": (64, 64, 3)}),
     "maze_r2": ("dmc/memory_maze", {"image": (64, 64, 3)}),
 }
 
 
+def case_overrides(name):
+    """config overrides of a case beyond its config file (e.g. the rep_loss variant)"""
+    return list(CASES[name][2]) if len(CASES[name]) > 2 else []
+
+
 def load_case(name):
     z = dict(np.load(os.path.join(HERE, name + ".npz")))
-    cfg_name, obs = CASES[name]
+    cfg_name, obs = CASES[name][:2]
     H = int(z["meta_H"])
-    cfg = load_config(cfg_name, ["device=cpu", "model.compile=False", f"model.imag_horizon={H}"])
+    cfg = load_config(cfg_name, ["device=cpu", "model.compile=False", f"model.imag_horizon={H}"] + case_overrides(name))
     spec = Spec(cfg.model, obs, int(z["meta_A"]), bool(z["meta_discrete"]))
     params = params_for(spec.shapes, int(z["meta_param_seed"]))
     return z, cfg, spec, params, obs

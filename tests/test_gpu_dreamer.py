@@ -16,12 +16,12 @@ import numpy as np
 import pytest
 import torch
 
-from golden_io import CASES, batch, initial, load_case, sample_idx
+from golden_io import CASES, batch, case_overrides, initial, load_case, sample_idx
 from sdreamer.config import load_config
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-WM_KEYS = ("dyn", "rep", "rew", "con", "barlow", "image", "position", "velocity")
+WM_KEYS = ("dyn", "rep", "rew", "con", "barlow", "infonce", "image", "position", "velocity")
 
 
 class _Sp:
@@ -39,7 +39,8 @@ def build_agent(name):
     z, cfg, spec, params, obs = load_case(name)
     cfg_name = CASES[name][0]
     H = int(z["meta_H"])
-    gcfg = load_config(cfg_name, ["device=cuda:0", "model.compile=False", f"model.imag_horizon={H}"])
+    gcfg = load_config(cfg_name, ["device=cuda:0", "model.compile=False", f"model.imag_horizon={H}"] +
+                       case_overrides(name))
     act = _Sp((int(z["meta_A"]),))
     if bool(z["meta_discrete"]):
         act.discrete = True
