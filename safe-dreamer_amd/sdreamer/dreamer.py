@@ -491,6 +491,10 @@ class Dreamer(nn.Module):
     def _ph_side_ac(self, st):
         """side: policy / value losses on the imagined trajectories and their backward."""
         st["ac_losses"], st["ac_metrics"] = self._ac_losses(st["ifeat"], st["iact"], st["rr"])
+        with torch.no_grad():  # replay-value statistics (dreamer.py:649-651), off the main stream's critical path
+            st["ac_metrics"].update(_tstats(st["rret"], "ret_replay"))
+            st["ac_metrics"].update(_tstats(st["rv"]["value"], "value_replay"))
+            st["ac_metrics"].update(_tstats(st["rv"]["slow_value"], "slow_value_replay"))
         self._mark("side:actor_critic")
 
     def _ph_finish(self, st):
@@ -573,12 +577,7 @@ class Dreamer(nn.Module):
                                    last=last.contiguous(), boot_row_stride=T * H, boot_t_stride=H)  # (B, T-1)
         lp_r = ops.TwoHotLogProbFn.apply(rv["vd"], self.vbins, rret.reshape(-1))
         loss = torch.mean((1.0 - last[:, :-1]) * (-lp_r - rv["lp_s"]))
-        metrics = {}
-        with torch.no_grad():
-            metrics.update(_tstats(rret, "ret_replay"))
-            metrics.update(_tstats(rv["value"], "value_replay"))
-            metrics.update(_tstats(rv["slow_value"], "slow_value_replay"))
-        return loss, metrics, rret
+        return loss, {}, rret  # the replay statistics are logged from the side stream (_ph_side_ac)
 
     @torch.no_grad()
     def _heads_returns(self, ifeat):

@@ -81,9 +81,15 @@ def _fast_split(M, N, K, batch):
     """K split for the split-bf16 kernel: ~512 workgroups of 128x128 tiles (2 per CU) when K is long; the launcher
     falls back to 64x64 tiles below 256 workgroups."""
     tiles = -(-M // 128) * -(-N // 128) * batch
-    if tiles >= 256 or K < 1024:
+    if tiles >= 256:
         return 1
-    return max(1, min(K // 512, -(-512 // tiles), 32))
+    if K >= 1024:
+        return max(1, min(K // 512, -(-512 // tiles), 32))
+    # short K (e.g. the replay-value head on ~1k rows): 64x64 tiles, split so the launch still has ~256 workgroups
+    t64 = -(-M // 64) * -(-N // 64) * batch
+    if t64 >= 128 or K < 256:
+        return 1
+    return max(1, min(K // 128, -(-256 // t64), 16))
 
 
 def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1, fast=False):
