@@ -296,6 +296,25 @@ int sd_infonce_fwd(const float* logits, long ld, int n, int ncol, long label_off
 int sd_infonce_bwd(const float* logits, long ld, int n, int ncol, long label_off, const float* lse, const float* g,
                    float scale, float* dlogits, sd_stream stream);
 
+/* Replay slices (utils/buffer.py:27-53): storage keys laid out (cap, E, row_bytes) in HBM. Slice b starts at
+ * (t0, e) = starts[2 * pick[b]], starts[2 * pick[b] + 1]; key k moves steps j < steps of time (t0 + shift + j) % cap
+ * between storage and batch (B, steps, row_bytes): gather (scatter = 0; also writes the data rows' indices
+ * t_idx / e_idx (B, L) when non-null, time = (t0 + 1 + j) % cap), or the latent write-back (scatter = 1). One launch
+ * for every key. */
+#define SD_MAX_SLICE_KEYS 16
+typedef struct sd_slice_key {
+  void* storage;
+  void* batch;
+  long row_bytes;
+  int steps, shift;
+} sd_slice_key;
+typedef struct sd_slice_keys {
+  sd_slice_key k[SD_MAX_SLICE_KEYS];
+  int n;
+} sd_slice_keys;
+int sd_replay_slices(const sd_slice_keys* keys, const int64_t* starts, const int64_t* pick, int B, int L, long cap,
+                     int E, int64_t* t_idx, int64_t* e_idx, int scatter, sd_stream stream);
+
 /* Profiling aid: store the device wall clock (constant rate, sd_wall_clock_khz) into buf[idx] when `stream` reaches
  * this point; capturable into a HIP graph. Not part of the reference interface. */
 int sd_mark(uint64_t* buf, int idx, sd_stream stream);

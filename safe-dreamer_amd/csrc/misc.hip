@@ -314,6 +314,51 @@ extern "C" int sd_infonce_bwd(const float* logits, long ld, int n, int ncol, lon
   return SD_OK;
 }
 
+// ---- replay slices (utils/buffer.py:27-53 semantics, HBM storage laid out (capacity, env, row)): every key of a
+// batch of B slices gathered in ONE launch straight into the consumer's buffers, and the latent write-back as one
+// scatter. Slice b starts at (t0, e) = starts[pick[b]]; key k copies steps j = 0..steps-1 of time (t0 + shift + j) %
+// cap (data keys: shift 1, the action one step back: shift 0, the initial latent: steps 1, shift 0).
+namespace {
+__global__ __launch_bounds__(256) void slices_kernel(sd_slice_keys ks, const int64_t* __restrict__ starts,
+                                                     const int64_t* __restrict__ pick, int B, int L, long cap, int E,
+                                                     int64_t* __restrict__ t_out, int64_t* __restrict__ e_out,
+                                                     int scatter) {
+  const int row = blockIdx.x, k = blockIdx.y;
+  const sd_slice_key key = ks.k[k];
+  const int b = row / L, j = row - b * L;
+  if (b >= B || j >= key.steps) return;
+  const int64_t t0 = starts[2 * pick[b]], e = starts[2 * pick[b] + 1];
+  const long t = (t0 + key.shift + j) % cap;
+  if (k == 0 && threadIdx.x == 0 && t_out && !scatter) {  // index of the data rows for the write-back
+    const long tt = (t0 + 1 + j) % cap;
+    t_out[(long)b * L + j] = tt;
+    e_out[(long)b * L + j] = e;
+  }
+  char* st = (char*)key.storage + ((long)t * E + e) * key.row_bytes;
+  char* bf = (char*)key.batch + ((long)b * key.steps + j) * key.row_bytes;
+  const char* src = scatter ? bf : st;
+  char* dst = scatter ? st : bf;
+  if ((key.row_bytes & 15) == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    for (long i = threadIdx.x; i < key.row_bytes / 16; i += 256)
+      reinterpret_cast<int4*>(dst)[i] = reinterpret_cast<const int4*>(src)[i];
+  } else {
+    for (long i = threadIdx.x; i < key.row_bytes; i += 256) dst[i] = src[i];
+  }
+}
+}  // namespace
+
+extern "C" int sd_replay_slices(const sd_slice_keys* keys, const int64_t* starts, const int64_t* pick, int B, int L,
+                                long cap, int E, int64_t* t_idx, int64_t* e_idx, int scatter, sd_stream s) {
+  if (!keys || keys->n < 0 || keys->n > SD_MAX_SLICE_KEYS) return SD_EARG;
+  if (B <= 0 || keys->n == 0) return SD_OK;
+  for (int k = 0; k < keys->n; ++k)
+    if (keys->k[k].steps > L || keys->k[k].steps < 0 || !keys->k[k].storage || !keys->k[k].batch) return SD_EARG;
+  slices_kernel<<<dim3(B * L, keys->n), 256, 0, (hipStream_t)s>>>(*keys, starts, pick, B, L, cap, E, t_idx, e_idx,
+                                                                    scatter);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
 // ---- timeline marks (profiling aid): one thread stores the constant-rate wall clock into buf[idx]; enqueued on a
 // stream (and capturable into a HIP graph) it timestamps the point the stream has reached
 namespace {

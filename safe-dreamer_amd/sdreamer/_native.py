@@ -67,6 +67,16 @@ def _parse_struct(path, name):
 
 ScanDesc = _parse_struct(HEADER, "sd_rssm_scan")
 ImagineDesc = _parse_struct(HEADER, "sd_imagine")
+SliceKey = _parse_struct(HEADER, "sd_slice_key")
+
+
+def _define(path, name):
+    import re
+    return int(re.search(r"#define " + name + r"\s+(\d+)", open(path).read()).group(1))
+
+
+class SliceKeys(ctypes.Structure):
+    _fields_ = [("k", SliceKey * _define(HEADER, "SD_MAX_SLICE_KEYS")), ("n", c_int)]
 
 _CTYPES = {
     "int": c_int, "long": c_long, "float": c_float, "double": ctypes.c_double, "uint64_t": ctypes.c_uint64,

@@ -92,8 +92,61 @@ class Buffer:
         index = [t_idx[:, 1:], e_idx[:, 1:]]
         return data, index, initial
 
+    # ---------------------------------------------------------------- fused device path (one launch each way)
+    def _slice_keys(self, pairs):
+        from . import _native as nat
+        ks = nat.SliceKeys()
+        for i, (store, batch, steps, shift) in enumerate(pairs):
+            if batch.dtype != store.dtype or not batch.is_contiguous() or batch.device != store.device:
+                raise ValueError("slice batch buffer must match the storage dtype / device and be contiguous")
+            ks.k[i].storage, ks.k[i].batch = store.data_ptr(), batch.data_ptr()
+            ks.k[i].row_bytes = store[0, 0].numel() * store.element_size()
+            ks.k[i].steps, ks.k[i].shift = steps, shift
+        ks.n = len(pairs)
+        return ks
+
+    def sample_into(self, dst, dst_initial=None):
+        """sample() written straight into caller-owned buffers (dst: the data dict's keys, (B, L, ...) each;
+        dst_initial: (stoch (B, S, K), deter (B, D))), every key in one gather launch (sd_replay_slices). Returns
+        the write-back index, which update() turns into one scatter launch."""
+        import ctypes
+
+        from . import _native as nat
+        from . import kernels as K
+        if self._dirty:
+            self._build_starts()
+        B, L = self.batch_size, self.batch_length
+        pick = torch.randint(0, self._starts.shape[0], (B,), device=self.storage_device, generator=self._gen)
+        pairs = [(v, dst[k], L, 0 if k == "action" else 1) for k, v in self._store.items()
+                 if k not in ("stoch", "deter")]
+        if dst_initial is not None and "stoch" in self._store:
+            pairs += [(self._store["stoch"], dst_initial[0], 1, 0), (self._store["deter"], dst_initial[1], 1, 0)]
+        t_idx = torch.empty(B, L, dtype=torch.int64, device=self.storage_device)
+        e_idx = torch.empty(B, L, dtype=torch.int64, device=self.storage_device)
+        starts = self._starts.contiguous()
+        ks = self._slice_keys(pairs)
+        nat.call("sd_replay_slices", ctypes.addressof(ks), K.p(starts), K.p(pick), B, L, self.cap, self.env_num,
+                 K.p(t_idx), K.p(e_idx), 0, K.stream())
+        index = [t_idx, e_idx]
+        self._last = (index, pick, starts)
+        return index
+
     def update(self, index, stoch, deter):
         """Write posterior latents back to the sampled positions (buffer.py:44-53)."""
+        last = getattr(self, "_last", None)
+        if last is not None and index is last[0] and "stoch" in self._store and "deter" in self._store:
+            import ctypes
+
+            from . import _native as nat
+            from . import kernels as K
+            _, pick, starts = last
+            B, L = self.batch_size, self.batch_length
+            ks = self._slice_keys([(self._store["stoch"], stoch.contiguous(), L, 1),
+                                   (self._store["deter"], deter.contiguous(), L, 1)])
+            nat.call("sd_replay_slices", ctypes.addressof(ks), K.p(starts), K.p(pick), B, L, self.cap,
+                     self.env_num, None, None, 1, K.stream())
+            self._last = None
+            return
         t_idx, e_idx = index
         if "stoch" in self._store:
             self._store["stoch"][t_idx.reshape(-1), e_idx.reshape(-1)] = stoch.reshape(-1, *stoch.shape[2:]).to(

@@ -36,6 +36,8 @@ from .rssm import RSSM, STREAM_ACT, STREAM_IMG, STREAM_POLICY
 # SDREAMER_S2_AFTER_SCAN=1 (schedule knob): the actor/critic phase starts after the scan backward (beside the encoder
 # backward) instead of right after the replay-value backward (beside the scan backward)
 S2_AFTER_SCAN = os.environ.get("SDREAMER_S2_AFTER_SCAN", "0") == "1"
+# SDREAMER_FUSED_SAMPLE=0: replayed updates sample through Buffer.sample() + copies instead of sample_into (A/B knob)
+FUSED_SAMPLE = os.environ.get("SDREAMER_FUSED_SAMPLE", "1") != "0"
 
 # csrc/img.hip runs the whole imagination as 9 fused launches per step; SDREAMER_FUSED_IMAG=0 selects the per-op
 # HIP kernels (tests compare the two)
@@ -224,6 +226,14 @@ class Dreamer(nn.Module):
     # ------------------------------------------------------------------ update
     def update(self, replay_buffer):
         """dreamer.py:402-451."""
+        if self._graph is not None and FUSED_SAMPLE and hasattr(replay_buffer, "sample_into") and \
+                self.slow_target_update == 1:
+            # replayed update: the replay slices are gathered straight into the graphs' input buffers (one launch)
+            index = replay_buffer.sample_into(self._g_in, self._g_init)
+            seed = self._seed_base + self._updates
+            (stoch, deter), mets = self._update_graphed(None, None, seed, self._g_ro)
+            replay_buffer.update(index, stoch.detach(), deter.detach())
+            return mets
         data, index, initial = replay_buffer.sample()
         seed = self._seed_base + self._updates
         (stoch, deter), mets = self.update_batch(data, initial, seed)
@@ -298,6 +308,7 @@ class Dreamer(nn.Module):
         scales it by 1/world before AGC + LaProp)."""
         if self._graph is None:
             self._g_in = {k: v.clone() for k, v in data.items()}
+            self._g_ro = ro
             self._g_init = tuple(t.clone() for t in initial)
             self._seed_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
             main_cap = torch.cuda.Stream(device=self.device)
@@ -323,10 +334,11 @@ class Dreamer(nn.Module):
                     raise RuntimeError("unexpected exchange step in a single-graph phase")
             self._graph = (gP, gS1, gM1, gR, gM2a, gM2b, gS2, gM3)
             self._gst, self._g_post, self._g_keys, self._g_mvec = st, post, keys, mvec
-        for k, v in data.items():
-            self._g_in[k].copy_(v)
-        for dst, src in zip(self._g_init, initial):
-            dst.copy_(src)
+        if data is not None:
+            for k, v in data.items():
+                self._g_in[k].copy_(v)
+            for dst, src in zip(self._g_init, initial):
+                dst.copy_(src)
         self._seed_dev.fill_(int(seed) & 0x7FFFFFFFFFFFFFFF)
         gP, gS1, gM1, gR, gM2a, gM2b, gS2, gM3 = self._graph
         main = torch.cuda.current_stream()
