@@ -179,6 +179,7 @@ int sd_conv2d_fwd_pool(const float* in, const float* w, const float* bias, const
                        int pad, float eps, int nchw_flat, sd_stream stream);
 int sd_pool_rms_fwd(const float* x, const float* w, float* pooled, uint8_t* amax, float* y, float* rstd, int Nb,
                     int H, int W, int C, float eps, int nchw_flat, sd_stream stream);
+/* dw_partial >= (sd_pool_rms_bwd_blocks + sd_colsum_chunks(sd_pool_rms_bwd_blocks)) * C floats */
 int sd_pool_rms_bwd_blocks(int Nb, int H, int W);
 int sd_pool_rms_bwd(const float* pooled, const uint8_t* amax, const float* w, const float* rstd, const float* dy,
                     float* dx, float* dw, float* dw_partial, int Nb, int H, int W, int C, int nchw_flat,

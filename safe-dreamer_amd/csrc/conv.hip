@@ -17,6 +17,8 @@
 #include "sdhip.h"
 
 extern "C" int sd_colsum(const float* in, float* out, int R, int N, long ld, int accumulate, sd_stream s);
+extern "C" int sd_colsum_ws(const float* in, float* out, int R, int N, long ld, int accumulate, float* workspace,
+                            sd_stream s);
 
 namespace {
 using namespace sdg;
@@ -1061,10 +1063,8 @@ int wgrad_direct(const float* in, const float* dout, float* dw_db, float* ws, lo
 #undef SD_WD
   if (!launched) return SD_ESHAPE;
   SD_LAUNCH_CHECK();
-  GemmArgs g{};
-  g.C = dw_db; g.ldc = J + 1; g.ws = ws; g.M = Co; g.N = J + 1; g.batch = 1; g.ksplit = pl.slabs; g.alpha = 1.f;
-  const long total = (long)Co * (J + 1);
-  gemm_reduce_kernel<<<(int)((total + 255) / 256), 256, 0, s>>>(g);
+  const long total = (long)Co * (J + 1);  // fixed-order sum of the row-block slabs (4 waves x unrolled loads)
+  slab_reduce<<<(int)((total + 63) / 64), 256, 0, s>>>(ws, pl.slabs, total, dw_db);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
@@ -1233,7 +1233,8 @@ extern "C" int sd_pool_rms_bwd(const float* pooled, const uint8_t* amax, const f
   const int grid = sd_pool_rms_bwd_blocks(Nb, H, W);
   SD_POOL_SWITCH(pool_rms_bwd, grid, pooled, amax, w, rstd, dy, dx, dw_partial, Nb, H, W, C, nchw_flat)
   SD_LAUNCH_CHECK();
-  return sd_colsum(dw_partial, dw, grid, C, C, accumulate_dw, stream_);
+  // two-pass column sum of the per-block dw partials; its chunk workspace follows them in dw_partial
+  return sd_colsum_ws(dw_partial, dw, grid, C, C, accumulate_dw, dw_partial + (long)grid * C, stream_);
 }
 
 // ---------------------------------------------------------------- split-bf16 backward entry points

@@ -436,7 +436,7 @@ def pool_rms_bwd(pooled, amax, w, rstd, dy, H, W, dw, nchw_flat=False):
     Nb, Ho, Wo, C = pooled.shape
     dx = torch.empty(Nb, H, W, C, dtype=torch.float32, device=pooled.device)
     nb = nat.fns["sd_pool_rms_bwd_blocks"](Nb, H, W)
-    part = torch.empty(nb * C, dtype=torch.float32, device=pooled.device)
+    part = torch.empty((nb + nat.fns["sd_colsum_chunks"](nb)) * C, dtype=torch.float32, device=pooled.device)
     nat.call("sd_pool_rms_bwd", p(pooled), p(amax), p(w), p(rstd), p(_c(dy)), p(dx), p(dw), p(part), Nb, H, W, C,
              int(nchw_flat), 1, stream())
     return dx
