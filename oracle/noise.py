@@ -21,6 +21,7 @@ STREAM_OBS = 1
 STREAM_IMG = 2
 STREAM_ACT = 3
 STREAM_POLICY = 4
+STREAM_POLICY_ACT = 5  # the action sample of Dreamer.act (the posterior sample there uses STREAM_POLICY)
 
 _M0 = np.uint64(0xD2511F53)
 _M1 = np.uint64(0xCD9E8D57)

@@ -455,17 +455,46 @@ class Oracle:
                            P[f"{pre}.mlp.layers.{name}_norm{i}.weight"]))
         return F.linear(x, P[f"{pre}.last.weight"], P[f"{pre}.last.bias"])
 
-    def actor_sample(self, logits, seed, step, row_offset):
+    def actor_sample(self, logits, seed, step, row_offset, stream=nz.STREAM_ACT):
         """frozen actor rsample (dreamer.py:684): bounded_normal or onehot."""
         s = self.s
         N = logits.shape[0]
         if s.discrete:
             nl = unimix_logits(logits, float(s.actor_dist.unimix_ratio))
-            g = torch.from_numpy(nz.gumbel_block(seed, nz.STREAM_ACT, step, N, row_offset, s.A))
+            g = torch.from_numpy(nz.gumbel_block(seed, stream, step, N, row_offset, s.A))
             return st_gumbel_sample(nl, g)
         loc, scale = bounded_normal_params(logits, float(s.actor_dist.min_std), float(s.actor_dist.max_std))
-        eps = torch.from_numpy(nz.normal_block(seed, nz.STREAM_ACT, step, N, row_offset, s.A))
+        eps = torch.from_numpy(nz.normal_block(seed, stream, step, N, row_offset, s.A))
         return loc + eps * scale
+
+    @torch.no_grad()
+    def act(self, obs, state, seed, step=0, eval=False):
+        """Dreamer.act (dreamer.py:330-357; the frozen modules share the trained weights): encoder on the (B, *)
+        observation, RSSM.obs_step (rssm.py:158-178: is_first resets the carried state), actor mode or rsample.
+        Noise: posterior sample STREAM_POLICY, action sample STREAM_POLICY_ACT."""
+        s = self.s
+        data = {k: v.unsqueeze(1) for k, v in obs.items() if k != "is_first"}
+        if "image" in data and data["image"].dtype == torch.uint8:
+            data["image"] = data["image"].float() / 255.0  # Dreamer.preprocess, dreamer.py:710-713
+        embed = self.encode(data)[:, 0]
+        B = embed.shape[0]
+        rs = obs["is_first"].reshape(B)
+        stoch = torch.where(rs.reshape(B, 1, 1), torch.zeros_like(state["stoch"]), state["stoch"])
+        deter = torch.where(rs.reshape(B, 1), torch.zeros_like(state["deter"]), state["deter"])
+        act = torch.where(rs.reshape(B, 1), torch.zeros_like(state["prev_action"]), state["prev_action"])
+        deter = self.deter_step(stoch, deter, act)
+        logit = self.obs_logit(deter, embed)
+        g = torch.from_numpy(nz.gumbel_block(seed, nz.STREAM_POLICY, step, B, 0, s.SK)).reshape(B, s.S, s.K)
+        stoch = self.sample_stoch(logit, g)
+        logits = self.head_logits("actor", self.get_feat(stoch, deter))
+        if eval:
+            if s.discrete:
+                action = F.one_hot(logits.argmax(-1), s.A).float()
+            else:
+                action = torch.tanh(logits[:, :s.A])
+        else:
+            action = self.actor_sample(logits, seed, step, 0, nz.STREAM_POLICY_ACT)
+        return action, {"stoch": stoch, "deter": deter, "prev_action": action}
 
     @torch.no_grad()
     def imagine(self, start, horizon, seed, row_offset=0):  # Dreamer._imagine, dreamer.py:673-692

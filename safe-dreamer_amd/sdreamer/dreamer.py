@@ -31,7 +31,7 @@ from . import ops
 from . import parallel
 from .networks import MLPHead, MultiDecoder, MultiEncoder, Projector, ReturnEMA, heads_nograd
 from .optim import LaProp, WarmupSchedule
-from .rssm import RSSM, STREAM_ACT, STREAM_IMG, STREAM_POLICY
+from .rssm import RSSM, STREAM_ACT, STREAM_IMG, STREAM_POLICY, STREAM_POLICY_ACT
 
 # SDREAMER_S2_AFTER_SCAN=1 (schedule knob): the actor/critic phase starts after the scan backward (beside the encoder
 # backward) instead of right after the replay-value backward (beside the scan backward)
@@ -209,8 +209,37 @@ class Dreamer(nn.Module):
             else:
                 action = torch.tanh(logits[:, : self.act_dim])  # Normal mean = tanh(mean) (dreamer act uses .mode)
         else:
-            action = self._sample_action(logits, seed, step, 0, STREAM_POLICY)
+            action = self._sample_action(logits, seed, step, 0, STREAM_POLICY_ACT)
         return action, {"stoch": stoch, "deter": deter, "prev_action": action}
+
+    def policy_graph(self, B, obs_example, eval=False):
+        """Dreamer.act for B environments as one replayed HIP graph (latency path).
+        Returns policy(obs, state) -> (action, state): copies obs/state into the graph's static inputs, replays, and
+        returns views of the graph's static outputs (valid until the next call). Call k samples exactly as
+        act(obs, state, eval, seed=seed_base + k, step=0) does (the per-step seed lives on the device)."""
+        dev = self.device
+        s_obs = {k: torch.zeros_like(v, device=dev) for k, v in obs_example.items()}
+        s_state = self.get_initial_state(B)
+        seed_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            act, st = self.act(s_obs, s_state, eval=eval, seed=seed_dev, step=0)
+        counter = [0]
+        base = self._seed_base + 7
+
+        def policy(obs, state):
+            for k, v in obs.items():
+                s_obs[k].copy_(v)
+            for k in ("stoch", "deter", "prev_action"):
+                s_state[k].copy_(state[k])
+            seed_dev.fill_(base + counter[0])
+            counter[0] += 1
+            g.replay()
+            return act, st
+
+        policy.graph, policy.counter = g, counter
+        return policy
 
     def _sample_action(self, logits, seed, step, row_offset, stream_id):
         d = self.config.actor.dist

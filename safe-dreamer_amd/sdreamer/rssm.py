@@ -26,7 +26,7 @@ from . import kernels as K
 from . import ops
 from .networks import Act, BlockLinear, Lambda, Linear, RMSNorm
 
-STREAM_OBS, STREAM_IMG, STREAM_ACT, STREAM_POLICY = 1, 2, 3, 4
+STREAM_OBS, STREAM_IMG, STREAM_ACT, STREAM_POLICY, STREAM_POLICY_ACT = 1, 2, 3, 4, 5  # oracle/noise.py
 # the fused scan (csrc/scan.hip) is the default; SDREAMER_FUSED_SCAN=0 selects the per-op HIP kernels (tests compare)
 FUSED_SCAN = os.environ.get("SDREAMER_FUSED_SCAN", "1") != "0"
 # debugging aid: fill the fused backward's scratch tensors with NaN so any element read before it is written shows
