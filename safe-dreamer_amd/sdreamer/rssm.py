@@ -159,8 +159,15 @@ class RSSM(nn.Module):
         B, T = action.shape[:2]
         r = reset.reshape(B, T).to(torch.uint8)
         stoch0, deter0 = initial
-        return ObserveScan.apply(embed, action, r, stoch0.reshape(B, -1).contiguous(), deter0.contiguous(), self,
-                                 seed, int(row_offset))
+        s0 = stoch0.reshape(B, -1)
+        if B > 16 and _fused_scan_ok(self, 16):
+            # rows are independent: batches above the fused scan's 16-row tile run as 16-row scans (each its own
+            # autograd node; noise indexed by global row, weight gradients accumulate)
+            outs = [ObserveScan.apply(embed[c:c + 16], action[c:c + 16], r[c:c + 16].contiguous(),
+                                      s0[c:c + 16].contiguous(), deter0[c:c + 16].contiguous(), self, seed,
+                                      int(row_offset) + c) for c in range(0, B, 16)]
+            return tuple(torch.cat([o[i] for o in outs], 0) for i in range(3))
+        return ObserveScan.apply(embed, action, r, s0.contiguous(), deter0.contiguous(), self, seed, int(row_offset))
 
     @torch.no_grad()
     def obs_step(self, stoch, deter, prev_action, embed, reset, seed=0, step=0, row_offset=0,
