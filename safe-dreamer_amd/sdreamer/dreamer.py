@@ -212,6 +212,30 @@ class Dreamer(nn.Module):
             action = self._sample_action(logits, seed, step, 0, STREAM_POLICY_ACT)
         return action, {"stoch": stoch, "deter": deter, "prev_action": action}
 
+    @torch.no_grad()
+    def video_pred(self, data, initial, seed=0):
+        """dreamer.py:366-400 (rep_loss == "dreamer" only): posterior over the first 5 steps, then open-loop
+        imagination on the logged actions (RSSM.imagine_with_action, rssm.py:197-209), both decoded; returns
+        cat([truth, model, (model - truth + 1) / 2], 2): (min(B, 6), T, 3H, W, C)."""
+        if self.rep_loss != "dreamer":
+            raise NotImplementedError("video_pred requires decoder and is only supported when rep_loss == 'dreamer'.")
+        p = self.preprocess(dict(data))
+        B = min(p["action"].shape[0], 6)
+        embed = self.encoder(p)
+        ps, pd, _ = self.rssm.observe(embed[:B, :5], p["action"][:B, :5].contiguous(),
+                                      tuple(v[:B].contiguous() for v in initial), p["is_first"][:B, :5].contiguous(),
+                                      seed=seed)
+        recon = self.decoder(ps, pd)["image"][:B]
+        if p["action"].shape[1] > 5:
+            st, de = self.rssm.imagine_with_action(ps[:, -1].contiguous(), pd[:, -1].contiguous(),
+                                                   p["action"][:B, 5:].contiguous(), seed=seed)
+            model = torch.cat([recon[:, :5], self.decoder(st, de)["image"]], 1)
+        else:  # sequences of <= 5 steps have no open-loop part (the reference's torch.stack would fail there)
+            model = recon
+        truth = p["image"][:B]
+        error = (model - truth + 1.0) / 2.0
+        return torch.cat([truth, model, error], 2)
+
     def policy_graph(self, B, obs_example, eval=False):
         """Dreamer.act for B environments as one replayed HIP graph (latency path).
         Returns policy(obs, state) -> (action, state): copies obs/state into the graph's static inputs, replays, and

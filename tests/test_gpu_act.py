@@ -59,3 +59,25 @@ def test_policy_graph_equals_eager_act():
         for n in st_e:
             assert torch.equal(st_g[n], st_e[n]), (k, n)
         obs["is_first"] = torch.zeros_like(obs["is_first"])
+
+
+def test_video_pred_decoder_agent():
+    """dreamer.py:366-400 on the decoder (rep_loss=dreamer) agent: layout cat([truth, model, error], 2), the first
+    5 model frames are the decoded posterior, the rest open-loop; deterministic for a fixed seed."""
+    ag, z, spec, obs = build_agent("walker_dreamer")
+    g = torch.Generator().manual_seed(4)
+    B0, T, A = 3, 9, int(z["meta_A"])
+    first = torch.zeros(B0, T, 1, dtype=torch.bool)
+    first[:, 0] = True
+    data = {"image": torch.randint(0, 256, (B0, T, 64, 64, 3), dtype=torch.uint8, generator=g).cuda(),
+            "action": (torch.rand(B0, T, A, generator=g) * 2 - 1).cuda(), "is_first": first.cuda()}
+    init = (torch.zeros(B0, spec.S, spec.K, device="cuda"), torch.zeros(B0, spec.D, device="cuda"))
+    v1 = ag.video_pred(dict(data), init, seed=3)
+    v2 = ag.video_pred(dict(data), init, seed=3)
+    B = min(data["action"].shape[0], 6)
+    assert tuple(v1.shape) == (B, T, 3 * 64, 64, 3) and torch.isfinite(v1).all()
+    assert torch.equal(v1, v2)
+    truth = data["image"][:B].float() / 255.0
+    assert torch.allclose(v1[:, :, :64], truth)
+    model = v1[:, :, 64:128]
+    assert torch.allclose(v1[:, :, 128:], (model - truth + 1.0) / 2.0)
