@@ -22,6 +22,7 @@ STREAM_IMG = 2
 STREAM_ACT = 3
 STREAM_POLICY = 4
 STREAM_POLICY_ACT = 5  # the action sample of Dreamer.act (the posterior sample there uses STREAM_POLICY)
+STREAM_AUG = 6  # r2dreamer random_translate shifts
 
 _M0 = np.uint64(0xD2511F53)
 _M1 = np.uint64(0xCD9E8D57)
@@ -92,3 +93,25 @@ def gumbel_block(seed, stream, step, rows, row_offset, width):
 def normal_block(seed, stream, step, rows, row_offset, width):
     idx = (np.arange(rows, dtype=np.int64)[:, None] + row_offset) * width + np.arange(width, dtype=np.int64)[None]
     return normal(seed, stream, step, idx)
+
+
+def uniform_int(seed, stream, step, idx, n):
+    """integer in [0, n) from the word gumbel() would use for idx (augmentation shifts)."""
+    idx = np.asarray(idx, dtype=np.int64)
+    q = (idx >> 2).astype(np.uint64)
+    w = (idx & 3).astype(np.int64)
+    k0, k1 = _key(seed)
+    out = philox4x32_10((q & _MASK).astype(np.uint32), (q >> np.uint64(32)).astype(np.uint32),
+                        np.uint32(step), np.uint32(stream), k0, k1)
+    v = np.floor(_uniform(np.choose(w, out)) * n).astype(np.int64)
+    return np.minimum(v, n - 1)
+
+
+def aug_shifts(seed, rows, row_offset, T, pad, same_across_time):
+    """random_translate shifts (dreamer.py:864-868) for slice rows row_offset..: (rows, T, 2) ints, (x, y)."""
+    n = 2 * pad + 1
+    b = np.arange(rows, dtype=np.int64)[:, None, None] + row_offset
+    t = np.arange(T, dtype=np.int64)[None, :, None]
+    ax = np.arange(2, dtype=np.int64)[None, None, :]
+    idx = b * 2 + ax + 0 * t if same_across_time else (b * T + t) * 2 + ax
+    return uniform_int(seed, STREAM_AUG, 0, idx, n)

@@ -333,6 +333,28 @@ class Spec:
 # --------------------------------------------------------------------------------------------------------
 
 
+def random_translate(img, shifts, pad, bilinear):
+    """Dreamer.random_translate (dreamer.py:845-880) on (B, T, H, W, C) images with given integer shifts (B, T, 2)
+    = (x, y) in [0, 2 pad]: out[y][x] = in[clamp(y + sy - pad)][clamp(x + sx - pad)]. The reference samples the
+    replicate-padded image with grid_sample at exactly those pixel centres; bilinear mode does so through float
+    grid arithmetic, whose last-bit weights (|d| ~ 6e-8) are reproduced here so the oracle tracks the reference's
+    gradients to the golden tolerance. The HIP kernel performs the exact integer gather."""
+    B, T, H, W, C = img.shape
+    x = F.pad(img.reshape(B * T, H, W, C).permute(0, 3, 1, 2), (pad, pad, pad, pad), mode="replicate")
+    Hp, Wp = H + 2 * pad, W + 2 * pad
+    if not bilinear:
+        ys = torch.arange(H)[None, :] + shifts.reshape(B * T, 2)[:, 1:2]
+        xs = torch.arange(W)[None, :] + shifts.reshape(B * T, 2)[:, 0:1]
+        out = x[torch.arange(B * T)[:, None, None], :, ys[:, :, None], xs[:, None, :]]  # (BT, H, W, C)
+        return out.reshape(B, T, H, W, C)
+    gy = torch.linspace(-1.0 + 1.0 / Hp, 1.0 - 1.0 / Hp, Hp)[:H]
+    gx = torch.linspace(-1.0 + 1.0 / Wp, 1.0 - 1.0 / Wp, Wp)[:W]
+    grid = torch.stack([gx[None, :].expand(H, W), gy[:, None].expand(H, W)], -1)[None]  # (1, H, W, 2): (x, y)
+    off = shifts.reshape(B * T, 1, 1, 2).float() * 2.0 / torch.tensor([Wp, Hp], dtype=torch.float32)
+    out = F.grid_sample(x, grid + off, mode="bilinear", padding_mode="zeros", align_corners=False)
+    return out.permute(0, 2, 3, 1).reshape(B, T, H, W, C)
+
+
 class Oracle:
     """Dreamer hot path on CPU. `P` maps reference state_dict names to fp32 tensors (leafs for trainables)."""
 
@@ -648,7 +670,15 @@ class OracleAgent:
             losses.update(self.decode_losses(data, post_stoch, post_deter))
         elif s.rep_loss == "r2dreamer":  # dreamer.py:497-532
             x1 = F.linear(feat.reshape(B * T, -1), P["prj.w.weight"])
-            x2 = embed.reshape(B * T, -1).detach()
+            aug = c.r2dreamer.aug
+            if bool(aug.enabled):  # _augment_images + random_translate (dreamer.py:716-729,845-880)
+                with torch.no_grad():
+                    pad, same = int(aug.max_delta), bool(aug.same_across_time)
+                    sh = torch.from_numpy(nz.aug_shifts(seed, B, row_offset, T, pad, same))  # (B, T, 2): (x, y)
+                    aug_img = random_translate(data["image"], sh, pad, bool(aug.bilinear))
+                    x2 = M.encode({**data, "image": aug_img}).reshape(B * T, -1)
+            else:
+                x2 = embed.reshape(B * T, -1).detach()
             x1n = (x1 - x1.mean(0)) / (x1.std(0) + 1e-8)
             x2n = (x2 - x2.mean(0)) / (x2.std(0) + 1e-8)
             cc = torch.mm(x1n.T, x2n) / (B * T)

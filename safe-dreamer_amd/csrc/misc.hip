@@ -359,6 +359,47 @@ extern "C" int sd_replay_slices(const sd_slice_keys* keys, const int64_t* starts
   return SD_OK;
 }
 
+// ---- r2dreamer image augmentation (Dreamer._augment_images / random_translate, dreamer.py:716-729,845-880):
+// replicate-pad by `pad`, shift by an integer (sx, sy) in [0, 2 pad] per slice (same_across_time) or per image, i.e.
+// out[y][x] = in[clamp(y + sy - pad)][clamp(x + sx - pad)] — the reference's grid_sample samples exactly those
+// pixel centres (its grid is built on them; bilinear weights are 1/0 up to float rounding). Shifts from Philox
+// (SD_STREAM_AUG, step 0): index (row * 2 + axis) or ((row * T + t) * 2 + axis), axis 0 = x, 1 = y; row = global
+// slice row (row_offset + b).
+namespace {
+__global__ void random_translate_kernel(const float* __restrict__ in, float* __restrict__ out, int N, int T, int H,
+                                        int W, int C, int pad, uint64_t seed, const uint64_t* seed_ptr,
+                                        long row_offset, int same_across_time) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)N * H * W * C;
+  if (i >= total) return;
+  const int c = (int)(i % C);
+  long r = i / C;
+  const int x = (int)(r % W);
+  r /= W;
+  const int y = (int)(r % H);
+  const int n = (int)(r / H);
+  const int b = n / T, t = n - b * T;
+  const uint64_t sd = seed + (seed_ptr ? *seed_ptr : 0ull);
+  const uint64_t base = same_across_time ? (uint64_t)(row_offset + b) * 2 : ((uint64_t)(row_offset + b) * T + t) * 2;
+  const int sx = sd_uniform_int(sd, SD_STREAM_AUG, 0, base, 2 * pad + 1);
+  const int sy = sd_uniform_int(sd, SD_STREAM_AUG, 0, base + 1, 2 * pad + 1);
+  const int yy = min(max(y + sy - pad, 0), H - 1), xx = min(max(x + sx - pad, 0), W - 1);
+  out[i] = in[(((long)n * H + yy) * W + xx) * C + c];
+}
+}  // namespace
+
+extern "C" int sd_random_translate(const float* in, float* out, int B, int T, int H, int W, int C, int pad,
+                                   uint64_t seed, const uint64_t* seed_ptr, long row_offset, int same_across_time,
+                                   sd_stream s) {
+  const long total = (long)B * T * H * W * C;
+  if (total <= 0) return SD_OK;
+  if (pad < 0) return SD_EARG;
+  random_translate_kernel<<<nb(total), 256, 0, (hipStream_t)s>>>(in, out, B * T, T, H, W, C, pad, seed, seed_ptr,
+                                                                 row_offset, same_across_time);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
 // ---- timeline marks (profiling aid): one thread stores the constant-rate wall clock into buf[idx]; enqueued on a
 // stream (and capturable into a HIP graph) it timestamps the point the stream has reached
 namespace {

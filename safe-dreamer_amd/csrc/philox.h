@@ -11,6 +11,8 @@
 #define SD_STREAM_IMG 2
 #define SD_STREAM_ACT 3
 #define SD_STREAM_POLICY 4
+#define SD_STREAM_POLICY_ACT 5
+#define SD_STREAM_AUG 6
 
 struct sd_u32x4 { uint32_t x, y, z, w; };
 
@@ -47,4 +49,15 @@ __device__ __forceinline__ float sd_normal(uint64_t seed, uint32_t stream, uint3
                                 (uint32_t)(seed >> 32));
   const double u1 = sd_u01(r.x), u2 = sd_u01(r.y);
   return (float)(sqrt(-2.0 * log(u1)) * cos(2.0 * 3.141592653589793 * u2));
+}
+
+// uniform integer in [0, n) from the same word as sd_gumbel(seed, stream, step, idx) (augmentation shifts)
+__device__ __forceinline__ int sd_uniform_int(uint64_t seed, uint32_t stream, uint32_t step, uint64_t idx, int n) {
+  const uint64_t q = idx >> 2;
+  sd_u32x4 r = sd_philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), step, stream, (uint32_t)seed,
+                                (uint32_t)(seed >> 32));
+  const uint32_t sel = (uint32_t)(idx & 3);
+  const uint32_t w = sel == 0 ? r.x : sel == 1 ? r.y : sel == 2 ? r.z : r.w;
+  const int v = (int)(sd_u01(w) * (double)n);
+  return v < n ? v : n - 1;
 }

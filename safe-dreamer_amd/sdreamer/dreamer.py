@@ -115,8 +115,10 @@ class Dreamer(nn.Module):
             self.prj = Projector(self.rssm.feat_size, self.embed_size)
             modules["projector"] = self.prj
             self.barlow_lambd = float(config.r2dreamer.lambd)
-            if self.rep_loss == "r2dreamer" and bool(config.r2dreamer.aug.enabled):
-                raise NotImplementedError("r2dreamer augmentation is an off-path variant (SURVEY.md §8(f) f4)")
+            aug = config.r2dreamer.aug
+            # Barlow target from a translated view (dreamer.py:506-520): (pad, same_across_time) or None
+            self.r2_aug = (int(aug.max_delta), bool(aug.same_across_time)) if \
+                (self.rep_loss == "r2dreamer" and bool(aug.enabled)) else None
         else:
             raise NotImplementedError(f"rep_loss={self.rep_loss} (off-path variant, SURVEY.md §8(f) f4)")
         self._named_params = OrderedDict()
@@ -517,7 +519,7 @@ class Dreamer(nn.Module):
         """main: world-model head losses and their backward down to the posterior leaves; the replay-value parts
         that do not need the imagined returns."""
         st["wm_total"], st["wm_losses"], st["wm_metrics"] = self._wm_heads(st["data"], st["embed"], st["leaves"],
-                                                                           st["feat_l"])
+                                                                           st["feat_l"], st["seed"], st["ro"])
         self._mark("wm_heads")
         st["rv"] = self._repval_pre(st["data"], st["feat_r"])
         self._mark("repval_fwd")
@@ -578,7 +580,7 @@ class Dreamer(nn.Module):
                           imag_feat_tm=st["ifeat"], imag_action_tm=st["iact"], ret=rr["ret"], rret=st["rret"])
         return (st["post_stoch"], st["post_deter"]), metrics
 
-    def _wm_heads(self, data, embed, leaves, feat):
+    def _wm_heads(self, data, embed, leaves, feat, seed=0, ro=0):
         """World-model losses (dreamer.py:453-576) on the posterior leaves, backward down to the leaves."""
         losses, metrics = {}, {}
         B, T = data["action"].shape[:2]
@@ -603,7 +605,14 @@ class Dreamer(nn.Module):
             losses["infonce"] = parallel.infonce(x1, embed.reshape(B * T, -1), self.world)
         else:
             x1 = self.prj(feat.reshape(B * T, -1))
-            x2 = embed.reshape(B * T, -1).detach()
+            if self.r2_aug is not None:  # encoder on a randomly translated view, no gradient (dreamer.py:506-520)
+                with torch.no_grad():
+                    pad, same = self.r2_aug
+                    aug = dict(data)
+                    aug["image"] = K.random_translate(data["image"], pad, seed, ro, same)
+                    x2 = self.encoder(aug).reshape(B * T, -1)
+            else:
+                x2 = embed.reshape(B * T, -1).detach()
             losses["barlow"] = parallel.barlow(x1, x2, self.barlow_lambd, self.world)
         rew_logits = self.reward(feat)
         losses["rew"] = -ops.TwoHotLogProbFn.apply(rew_logits, self.rbins, data["reward"].float()).mean()

@@ -394,6 +394,17 @@ def conv_flip_weight(w):
     return wf
 
 
+def random_translate(img, pad, seed, row_offset=0, same_across_time=True):
+    """Dreamer.random_translate (dreamer.py:845-880) on preprocessed (B, T, H, W, C) f32 images (NHWC, as the
+    reference permutes back): replicate pad + Philox integer shift per slice row (or per image)."""
+    B, T, H, W, C = img.shape
+    out = torch.empty_like(img)
+    sh, sp = seed_args(seed)
+    nat.call("sd_random_translate", p(_c(img)), p(out), B, T, H, W, C, int(pad), sh, sp, int(row_offset),
+             int(bool(same_across_time)), stream())
+    return out
+
+
 def sumpool2(du):
     Nb, H2, W2, C = du.shape
     din = torch.empty(Nb, H2 // 2, W2 // 2, C, dtype=torch.float32, device=du.device)

@@ -39,6 +39,7 @@ CASES = {
     "proprio_dreamer": ("dmc/proprio", [], {"position": (3,), "velocity": (2,)}, 1, False, 4, 16, 8),
     "walker_r2": ("dmc/cnn", [], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
     "walker_infonce": ("dmc/cnn", ["model.rep_loss=infonce"], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
+    "walker_r2aug": ("dmc/cnn", ["model.r2dreamer.aug.enabled=True"], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
     "walker_dreamer": ("dmc/walker_dreamer", [], {"image": (64, 64, 3)}, 6, False, 2, 4, 3),
     "atari_r2": ("dmc/atari_breakout", [], {"image": (64, 64, 3)}, 4, True, 2, 4, 3),
     "maze_r2": ("dmc/memory_maze", [], {"image": (64, 64, 3)}, 6, True, 2, 4, 3),
@@ -114,6 +115,20 @@ class NoiseSeq:
         return nz.normal_block(self.seed, nz.STREAM_ACT, t, N, 0, int(np.prod(shape[1:]))).reshape(shape)
 
 
+def aug_randint(aug, seed, B, T):
+    """torch.randint stand-in for random_translate's shifts (dreamer.py:864-868): oracle/noise.aug_shifts."""
+    orig = torch.randint
+
+    def randint(low, high=None, size=None, **kw):
+        if size is None or size[-1] != 2:
+            return orig(low, high, size, **kw)
+        sh = nz.aug_shifts(seed, B, 0, T, int(aug.max_delta), bool(aug.same_across_time))  # (B, T, 2): (x, y)
+        sh = sh[:, :1] if bool(aug.same_across_time) else sh
+        return torch.from_numpy(sh.astype(np.float32)).reshape(size).to(kw.get("dtype") or torch.float32)
+
+    return randint
+
+
 def run_case(name, mods, TD):
     cfg_name, ovr, obs, A, discrete, B, T, H = CASES[name]
     cfg = load_config(cfg_name, ["device=cpu", "model.compile=False", f"model.imag_horizon={H}"] + ovr)
@@ -174,7 +189,10 @@ def run_case(name, mods, TD):
     hook(ag.rssm, "prior", "prior")
     hook(ag, "_imagine", "imagine")
     hook(ag, "_lambda_return", "lret", many=True)
-    ag.encoder.register_forward_hook(lambda m, i, o: rec.__setitem__("embed", o))
+    def enc_hook(m, i, o):  # the first call only, not the aug view; returning None keeps the output
+        rec.setdefault("embed", o)
+
+    ag.encoder.register_forward_hook(enc_hook)
 
     for u in range(2):
         seed = 1000 + u
@@ -202,6 +220,9 @@ def run_case(name, mods, TD):
 
         torch.nn.functional.gumbel_softmax = gs
         torch.distributions.Normal.rsample = rs
+        orig_randint = torch.randint
+        if bool(cfg.model.r2dreamer.aug.enabled):
+            torch.randint = aug_randint(cfg.model.r2dreamer.aug, seed, B, T)
 
         class Buf:
             def sample(self_):
@@ -217,6 +238,7 @@ def run_case(name, mods, TD):
         finally:
             torch.nn.functional.gumbel_softmax = orig_gs
             torch.distributions.Normal.rsample = orig_rs
+            torch.randint = orig_randint
         assert seq.g == T + 1 + (H + 1) * (2 if discrete else 1), seq.g
         assert seq.n == (0 if discrete else H + 1), seq.n
         ps, pdet, plog = rec["observe"]
@@ -303,6 +325,9 @@ def grad_case(name, mods, TD):
 
     torch.nn.functional.gumbel_softmax = gs
     torch.distributions.Normal.rsample = rs
+    orig_randint = torch.randint
+    if bool(cfg.model.r2dreamer.aug.enabled):
+        torch.randint = aug_randint(cfg.model.r2dreamer.aug, 1000, B, T)
     try:
         d = TD({k: torch.from_numpy(v) for k, v in data_np.items()}, batch_size=(B, T))
         d = ag.preprocess(d)
@@ -311,6 +336,7 @@ def grad_case(name, mods, TD):
     finally:
         torch.nn.functional.gumbel_softmax = orig_gs
         torch.distributions.Normal.rsample = orig_rs
+        torch.randint = orig_randint
     out = {}
     named = dict(ag.named_parameters())
     for k in spec.shapes:

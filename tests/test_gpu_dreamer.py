@@ -105,9 +105,10 @@ def test_update_matches_reference(name):
             assert np.abs(got - ref).max() <= max(2e-3 * step, 1e-6 * np.abs(ref).max()), k
 
 
-def test_graph_replay_matches_eager():
-    """HIP-graph replays (update 3+) produce exactly the eager results: same kernels, device-resident seed."""
-    name = "walker_r2"
+@pytest.mark.parametrize("name", ["walker_r2", "walker_r2aug"])
+def test_graph_replay_matches_eager(name):
+    """HIP-graph replays (update 3+) produce exactly the eager results: same kernels, device-resident seed
+    (walker_r2aug: the augmentation shifts also follow the device seed)."""
     runs = []
     for graphs in (False, True):
         ag, z, spec, obs = build_agent(name)

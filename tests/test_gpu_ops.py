@@ -38,6 +38,20 @@ def test_noise_matches_oracle():
     assert np.abs(n - refn).max() <= 1e-6
 
 
+@pytest.mark.parametrize("same", [True, False])
+def test_random_translate_bit_exact(same):
+    """sd_random_translate vs oracle.ref_cpu.random_translate (nearest: the exact integer gather), with the shifts
+    drawn from oracle/noise.aug_shifts at a nonzero slice-row offset (data-parallel shard of rows 5..)."""
+    from sdreamer import kernels as K
+    B, T, H, W, C, pad, seed, ro = 3, 4, 16, 12, 3, 3, 4242, 5
+    img = torch.rand(B, T, H, W, C, generator=_g(3))
+    out = K.random_translate(img.to(DEV), pad, seed, ro, same).cpu()
+    sh = torch.from_numpy(nz.aug_shifts(seed, B, ro, T, pad, same))
+    assert torch.equal(out, R.random_translate(img, sh, pad, False))
+    if same:
+        assert (sh == sh[:, :1]).all()
+
+
 @pytest.mark.parametrize("M,N", [(7, 256), (1024, 256), (33, 2048), (5, 4096), (100, 48), (64, 32), (3, 512)])
 def test_rmsnorm_silu(M, N):
     from sdreamer import kernels as K

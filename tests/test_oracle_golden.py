@@ -70,3 +70,25 @@ def test_oracle_grads_match_reference(name):
         _close(np.linalg.norm(flat.astype(np.float64)), z[f"g_{k}__n"], rtol=1e-4, atol=1e-9, what=f"gnorm {k}")
         ref = z[f"g_{k}__s"]
         _close(flat[sample_idx(k, flat.size)], ref, rtol=1e-3, atol=1e-6 * max(1e-3, np.abs(ref).max()), what=f"grad {k}")
+
+
+def test_random_translate_restatement():
+    """oracle random_translate: nearest = exact integer gather with replicate edges; bilinear (the reference's
+    float grid arithmetic) within 1e-6 of it; shifts uniform over [0, 2 pad] and shared over T when asked."""
+    from oracle import noise as nz
+    from oracle.ref_cpu import random_translate
+    B, T, H, W, C, pad = 2, 3, 9, 7, 2, 3
+    img = torch.rand(B, T, H, W, C, generator=torch.Generator().manual_seed(0))
+    sh = torch.from_numpy(nz.aug_shifts(7, B, 0, T, pad, False))
+    near = random_translate(img, sh, pad, False)
+    for b in range(B):
+        for t in range(T):
+            sx, sy = int(sh[b, t, 0]), int(sh[b, t, 1])
+            for y in range(H):
+                for x in range(W):
+                    src = img[b, t, min(max(y + sy - pad, 0), H - 1), min(max(x + sx - pad, 0), W - 1)]
+                    assert torch.equal(near[b, t, y, x], src)
+    assert (random_translate(img, sh, pad, True) - near).abs().max() <= 1e-6
+    big = nz.aug_shifts(1, 4096, 0, 1, pad, True)
+    assert big.min() == 0 and big.max() == 2 * pad
+    assert np.abs(np.bincount(big.reshape(-1), minlength=2 * pad + 1) / big.size - 1 / (2 * pad + 1)).max() < 0.02
