@@ -22,7 +22,8 @@ STREAM_IMG = 2
 STREAM_ACT = 3
 STREAM_POLICY = 4
 STREAM_POLICY_ACT = 5  # the action sample of Dreamer.act (the posterior sample there uses STREAM_POLICY)
-STREAM_AUG = 6  # r2dreamer random_translate shifts
+STREAM_AUG = 6  # random_translate shifts (r2dreamer aug; DreamerPro's doubled batch)
+STREAM_OBS_AUG = 7  # DreamerPro's posterior scan over the augmented (2B) batch
 
 _M0 = np.uint64(0xD2511F53)
 _M1 = np.uint64(0xCD9E8D57)

@@ -267,8 +267,20 @@ class Spec:
         for k in list(p):
             if k.startswith("value."):
                 self.slow_names[k] = "_slow_value." + k[len("value."):]
+        self.ema_names = {}
         if self.rep_loss in ("r2dreamer", "infonce"):
             p["prj.w.weight"] = (E, Fd)
+        elif self.rep_loss == "dreamerpro":  # dreamer.py:131-162
+            dpc = mcfg.dreamer_pro
+            Kp, Pd = int(dpc.num_prototypes), int(dpc.proto_dim)
+            enc_names = [k for k in p if k.startswith("encoder.")]
+            p["_prototypes"] = (Kp, Pd)
+            p["obs_proj.weight"] = (Pd, E)
+            p["obs_proj.bias"] = (Pd,)
+            p["feat_proj.weight"] = (Pd, Fd)
+            p["feat_proj.bias"] = (Pd,)
+            self.ema_names = {k: "_ema_" + k for k in enc_names}
+            self.ema_names.update({"obs_proj.weight": "_ema_obs_proj.weight", "obs_proj.bias": "_ema_obs_proj.bias"})
         elif self.rep_loss == "dreamer":
             dec = mcfg.decoder
             dexcl = ("is_first", "is_last", "is_terminal")
@@ -366,8 +378,8 @@ class Oracle:
         self.rbins = twohot_bins(int(c.reward.dist.bin_num))
 
     # ---- encoder (networks.py:99-141, 192-234, 313-336)
-    def encode(self, data):
-        s, P = self.s, self.P
+    def encode(self, data, P=None):  # P: a parameter table with the encoder.* names (the EMA encoder's view)
+        s, P = self.s, (P or self.P)
         outs = []
         if s.cnn_keys:
             obs = torch.cat([data[k] for k in s.cnn_keys], -1)
@@ -442,7 +454,7 @@ class Oracle:
     def sample_stoch(self, logit, g):  # get_dist(logit).rsample(), rssm.py:219-220 + distributions.py:32-33
         return st_gumbel_sample(unimix_logits(logit, self.s.unimix), g)
 
-    def observe(self, embed, action, initial, reset, seed, row_offset=0):  # RSSM.observe, rssm.py:140-156
+    def observe(self, embed, action, initial, reset, seed, row_offset=0, stream=nz.STREAM_OBS):  # rssm.py:140-156
         s = self.s
         L = action.shape[1]
         B = action.shape[0]
@@ -456,7 +468,7 @@ class Oracle:
             act = torch.where(rs.reshape(B, 1), torch.zeros_like(action[:, i]), action[:, i])
             deter = self.deter_step(stoch, deter, act)
             logit = self.obs_logit(deter, embed[:, i])
-            g = torch.from_numpy(nz.gumbel_block(seed, nz.STREAM_OBS, i, B, row_offset, s.SK)).reshape(B, s.S, s.K)
+            g = torch.from_numpy(nz.gumbel_block(seed, stream, i, B, row_offset, s.SK)).reshape(B, s.S, s.K)
             stoch = self.sample_stoch(logit, g)
             stochs.append(stoch)
             deters.append(deter)
@@ -576,6 +588,9 @@ class OracleAgent:
         for k, sk in spec.slow_names.items():
             v = params.get(sk, params[k])
             self.P[sk] = torch.tensor(v, dtype=torch.float32)
+        for k, ek in spec.ema_names.items():  # DreamerPro's EMA encoder / projection (not trainable)
+            self.P[ek] = torch.tensor(params.get(ek, params[k]), dtype=torch.float32)
+        self.ema_updates = 0
         self.ema_vals = torch.zeros(2, dtype=torch.float32)
         self.model = Oracle(spec, self.P)
         c = spec.cfg
@@ -693,6 +708,22 @@ class OracleAgent:
             norm_logits = logits - torch.max(logits, 1)[0][:, None]
             labels = torch.arange(norm_logits.shape[0]).long()
             losses["infonce"] = F.cross_entropy(norm_logits, labels)
+        elif s.rep_loss == "dreamerpro":  # dreamer.py:543-566: doubled augmented batch, EMA targets, Sinkhorn
+            assert row_offset == 0, "DreamerPro's Sinkhorn normalises over the whole batch: whole batches only"
+            aug = c.dreamer_pro.aug
+            pad, same = int(aug.max_delta), bool(aug.same_across_time)
+            with torch.no_grad():  # augment_data (dreamer.py:731-743): rows [0, B) and [B, 2B) get their own shifts
+                data_aug = {k: torch.cat([v, v], 0) for k, v in data.items()}
+                sh = torch.from_numpy(nz.aug_shifts(seed, 2 * B, 0, T, pad, same))
+                data_aug["image"] = random_translate(data_aug["image"], sh, pad, bool(aug.bilinear))
+                init_aug = (torch.cat([initial[0], initial[0]], 0), torch.cat([initial[1], initial[1]], 0))
+                Pe = {k: P[ek] for k, ek in s.ema_names.items()}  # ema_proj (dreamer.py:745-750)
+                ema = F.linear(M.encode(data_aug, Pe), Pe["obs_proj.weight"], Pe["obs_proj.bias"])
+                ema = F.normalize(ema, p=2, dim=-1)
+            embed_aug = M.encode(data_aug)
+            ps_aug, pd_aug, _ = M.observe(embed_aug, data_aug["action"], init_aug, data_aug["is_first"], seed, 0,
+                                          nz.STREAM_OBS_AUG)
+            losses.update(self.proto_loss(ps_aug, pd_aug, embed_aug, ema))
         else:
             raise NotImplementedError(s.rep_loss)
         losses["rew"] = torch.mean(-twohot_log_prob(M.head_logits("reward", feat), M.rbins, data["reward"].float()))
@@ -805,10 +836,60 @@ class OracleAgent:
             st["exp_avg"].mul_(b1).add_(g / denom, alpha=(1 - b1) * lr)
             p.data.add_(st["exp_avg"], alpha=-step_size)
 
+    def ema_update(self):  # Dreamer.ema_update (dreamer.py:752-762)
+        dpc = self.s.cfg.dreamer_pro
+        with torch.no_grad():
+            self.P["_prototypes"].copy_(F.normalize(self.P["_prototypes"], p=2, dim=-1))
+            if self.ema_updates % int(dpc.ema_update_every) == 0:
+                mix = float(dpc.ema_update_fraction) if self.ema_updates > 0 else 1.0
+                for k, ek in self.s.ema_names.items():
+                    self.P[ek].copy_(mix * self.P[k].data + (1 - mix) * self.P[ek])
+        self.ema_updates += 1
+
+    def sinkhorn(self, scores):  # Dreamer.sinkhorn (dreamer.py:764-790): log-space Sinkhorn-Knopp over (K, N)
+        dpc = self.s.cfg.dreamer_pro
+        Kp = scores.shape[0]
+        log_q = F.log_softmax(scores.reshape(-1) / float(dpc.sinkhorn_eps), dim=0).reshape(Kp, -1)
+        N = log_q.shape[1]
+        for _ in range(int(dpc.sinkhorn_iters)):
+            log_q = log_q - torch.logsumexp(log_q, dim=1, keepdim=True) - math.log(Kp)
+            log_q = log_q - torch.logsumexp(log_q, dim=0, keepdim=True) - math.log(N)
+        return torch.exp(log_q + math.log(N)).reshape(scores.shape)
+
+    def proto_loss(self, post_stoch, post_deter, embed, ema_proj):  # Dreamer.proto_loss (dreamer.py:792-843)
+        P, dpc = self.P, self.s.cfg.dreamer_pro
+        w, tau = int(dpc.warm_up), float(dpc.temperature)
+        protos = F.normalize(P["_prototypes"], p=2, dim=-1)
+        B2, T = embed.shape[:2]
+
+        def scores(x):  # (B2, T, Pd) unit rows -> (K, B2, T - warm_up)
+            return (x.reshape(B2 * T, -1) @ protos.t()).reshape(B2, T, -1).permute(2, 0, 1)[:, :, w:]
+
+        obs = F.linear(embed, P["obs_proj.weight"], P["obs_proj.bias"])
+        obs_norm = obs.norm(dim=-1)
+        obs_logits = F.log_softmax(scores(F.normalize(obs, p=2, dim=-1)) / tau, dim=0)
+        o1, o2 = obs_logits.chunk(2, dim=1)
+        e1, e2 = scores(ema_proj).chunk(2, dim=1)
+        with torch.no_grad():
+            t1, t2 = self.sinkhorn(e1), self.sinkhorn(e2)
+        targets = torch.cat([t1, t2], 1)
+        feat = F.linear(torch.cat([post_stoch.reshape(B2, T, -1), post_deter], -1), P["feat_proj.weight"],
+                        P["feat_proj.bias"])
+        feat_norm = feat.norm(dim=-1)
+        feat_logits = F.log_softmax(scores(F.normalize(feat, p=2, dim=-1)) / tau, dim=0)
+        swav = -0.5 * (t2 * o1).sum(0).mean() - 0.5 * (t1 * o2).sum(0).mean()
+        temp = -(targets * feat_logits).sum(0).mean()
+        norm = ((obs_norm - 1) ** 2).mean() + ((feat_norm - 1) ** 2).mean()
+        return {"swav": swav, "temp": temp, "norm": norm}
+
     def update(self, data, initial, seed, row_offset=0, keep=None):
         """Dreamer.update (dreamer.py:402-451) minus sampling/autocast/GradScaler (no-op scale 1 on CPU)."""
         self.update_slow_target()
+        if self.s.rep_loss == "dreamerpro":
+            self.ema_update()
         post, losses, metrics = self.cal_grad(data, initial, seed, row_offset, keep)
+        if self.s.rep_loss == "dreamerpro" and self.ema_updates < int(self.s.cfg.dreamer_pro.freeze_prototypes_iters):
+            self.P["_prototypes"].grad.zero_()  # dreamer.py:424-425
         self.agc_()
         self.laprop_step()
         self.opt_step += 1  # scheduler.step()

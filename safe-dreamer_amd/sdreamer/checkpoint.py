@@ -28,7 +28,8 @@ def checkpoint_items(agent):
         "agent_state_dict": {k: v.detach().cpu() for k, v in agent.state_dict().items()},
         "optims_state_dict": {k: _to_cpu(v) for k, v in collect_optim_state_dict(agent).items()},
         "resume": {"updates": int(agent._updates), "slow_value_updates": int(agent._slow_value_updates),
-                   "optimizer_host_steps": int(agent._optimizer.host_steps), "seed_base": int(agent._seed_base)},
+                   "optimizer_host_steps": int(agent._optimizer.host_steps), "seed_base": int(agent._seed_base),
+                   "ema_updates": int(getattr(agent, "_ema_updates", 0))},
     }
 
 
@@ -53,6 +54,8 @@ def load_checkpoint(agent, path, map_location=None):
         agent._updates = int(res["updates"])
         agent._slow_value_updates = int(res["slow_value_updates"])
         agent._optimizer.host_steps = int(res["optimizer_host_steps"])
+        if hasattr(agent, "_ema_updates"):  # DreamerPro's EMA / prototype-freeze counter
+            agent._ema_updates = int(res.get("ema_updates", 0))
         agent._seed_base = int(res["seed_base"])
     return ckpt
 

@@ -23,15 +23,16 @@ from collections import OrderedDict
 
 import torch
 import torch.distributed as dist
+import torch.nn.functional as F
 from torch import nn
 
 from . import _native as nat
 from . import kernels as K
 from . import ops
 from . import parallel
-from .networks import MLPHead, MultiDecoder, MultiEncoder, Projector, ReturnEMA, heads_nograd
+from .networks import Linear, MLPHead, MultiDecoder, MultiEncoder, Projector, ReturnEMA, heads_nograd
 from .optim import LaProp, WarmupSchedule
-from .rssm import RSSM, STREAM_ACT, STREAM_IMG, STREAM_POLICY, STREAM_POLICY_ACT
+from .rssm import RSSM, STREAM_ACT, STREAM_IMG, STREAM_OBS_AUG, STREAM_POLICY, STREAM_POLICY_ACT
 
 # SDREAMER_S2_AFTER_SCAN=1 (schedule knob): the actor/critic phase starts after the scan backward (beside the encoder
 # backward) instead of right after the replay-value backward (beside the scan backward)
@@ -119,10 +120,28 @@ class Dreamer(nn.Module):
             # Barlow target from a translated view (dreamer.py:506-520): (pad, same_across_time) or None
             self.r2_aug = (int(aug.max_delta), bool(aug.same_across_time)) if \
                 (self.rep_loss == "r2dreamer" and bool(aug.enabled)) else None
+        elif self.rep_loss == "dreamerpro":  # dreamer.py:131-162
+            dpc = config.dreamer_pro
+            self._pro = dict(warm_up=int(dpc.warm_up), tau=float(dpc.temperature), eps=float(dpc.sinkhorn_eps),
+                             iters=int(dpc.sinkhorn_iters), every=int(dpc.ema_update_every),
+                             frac=float(dpc.ema_update_fraction), freeze=int(dpc.freeze_prototypes_iters),
+                             pad=int(dpc.aug.max_delta), same=bool(dpc.aug.same_across_time))
+            self._prototypes = nn.Parameter(torch.randn(int(dpc.num_prototypes), int(dpc.proto_dim)))
+            self.obs_proj = Linear(self.embed_size, int(dpc.proto_dim))
+            self.feat_proj = Linear(self.rssm.feat_size, int(dpc.proto_dim))
+            self._ema_encoder = copy.deepcopy(self.encoder)
+            self._ema_obs_proj = copy.deepcopy(self.obs_proj)
+            for prm in list(self._ema_encoder.parameters()) + list(self._ema_obs_proj.parameters()):
+                prm.requires_grad = False
+            self._ema_updates = 0
+            modules.update({"prototypes": self._prototypes, "obs_proj": self.obs_proj, "feat_proj": self.feat_proj})
         else:
-            raise NotImplementedError(f"rep_loss={self.rep_loss} (off-path variant, SURVEY.md §8(f) f4)")
+            raise NotImplementedError(f"rep_loss={self.rep_loss}")
         self._named_params = OrderedDict()
         for name, module in modules.items():
+            if isinstance(module, nn.Parameter):
+                self._named_params[name] = module
+                continue
             for pn, prm in module.named_parameters():
                 if prm.requires_grad:
                     self._named_params[f"{name}.{pn}"] = prm
@@ -142,6 +161,10 @@ class Dreamer(nn.Module):
             j = pos[id(p)]
             o = a.offsets[j] - self._v_lo
             sp.data = self._slow_arena[o:o + a.sizes[j]].view(sp.shape)
+        if self.rep_loss == "dreamerpro":  # EMA encoder / projection: arena-slice mirrors (one Polyak launch each)
+            self._ema_mirrors = [self._mirror("encoder.", self._ema_encoder),
+                                 self._mirror("obs_proj.", self._ema_obs_proj)]
+            self._proto_gate = torch.ones(1, device=self.device)  # graphs: 0 while the prototypes are frozen
         self.rbins = _symexp_bins(int(config.reward.dist.bin_num), self.device)
         self.vbins = _symexp_bins(int(config.critic.dist.bin_num), self.device)
         self._updates = 0
@@ -179,6 +202,43 @@ class Dreamer(nn.Module):
 
     def _polyak(self):
         K.polyak(self._optimizer.arena.data[self._v_lo:self._v_hi], self._slow_arena, self.slow_target_fraction)
+
+    def _mirror(self, prefix, module):
+        """A non-trainable copy of the contiguous arena slice holding `prefix`'s parameters; `module`'s parameters
+        become views of it (DreamerPro's EMA encoder / obs projection)."""
+        a = self._optimizer.arena
+        pos = {id(p): i for i, p in enumerate(a.params)}
+        idx = [pos[id(p)] for n, p in self._named_params.items() if n.startswith(prefix)]
+        if idx != list(range(idx[0], idx[0] + len(idx))):
+            raise RuntimeError(f"{prefix} parameters are not contiguous in the arena")
+        lo, hi = a.offsets[idx[0]], a.offsets[idx[-1]] + a.sizes[idx[-1]]
+        buf = a.data[lo:hi].clone()
+        mps = list(module.parameters())
+        if len(mps) != len(idx):
+            raise RuntimeError(f"{prefix} mirror has {len(mps)} parameters for {len(idx)} arena slots")
+        for j, mp in zip(idx, mps):
+            o = a.offsets[j] - lo
+            mp.data = buf[o:o + a.sizes[j]].view(mp.shape)
+        return lo, hi, buf
+
+    @torch.no_grad()
+    def _ema_apply(self, mix):
+        """dreamer.py:752-762 on device: unit prototypes, EMA encoder / projection <- mix * online + (1 - mix) * EMA."""
+        pr = self._prototypes
+        pr.copy_(pr / pr.norm(dim=-1, keepdim=True).clamp_min(1e-12))
+        if mix is not None:
+            a = self._optimizer.arena.data
+            for lo, hi, buf in self._ema_mirrors:
+                K.polyak(a[lo:hi], buf, mix)
+
+    def ema_update(self):  # Dreamer.ema_update, dreamer.py:752-762
+        c = self._pro
+        self._ema_apply((c["frac"] if self._ema_updates > 0 else 1.0) if self._ema_updates % c["every"] == 0
+                        else None)
+        self._ema_updates += 1
+
+    def _protos_frozen(self):  # dreamer.py:424-425 (checked after ema_update has counted this update)
+        return self.rep_loss == "dreamerpro" and self._ema_updates < self._pro["freeze"]
 
     @torch.no_grad()
     def preprocess(self, data):  # dreamer.py:709-713
@@ -300,7 +360,8 @@ class Dreamer(nn.Module):
         graphs (set `use_graphs = False` to stay eager); multi-GPU runs split the graphs at the RCCL exchange steps
         (parallel.collective) and issue those eagerly between graph replays."""
         ro = self.rank * data["action"].shape[0] if row_offset is None else row_offset
-        if self.use_graphs and self.slow_target_update == 1:
+        if self.use_graphs and self.slow_target_update == 1 and \
+                (self.rep_loss != "dreamerpro" or self._pro["every"] == 1):
             if self._graph is not None or self._eager_updates >= 2:
                 return self._update_graphed(data, initial, seed, ro)
         self._eager_updates += 1
@@ -308,8 +369,12 @@ class Dreamer(nn.Module):
             self.marks.reset()
         p_data = self.preprocess(dict(data))
         self._update_slow_target()
+        if self.rep_loss == "dreamerpro":
+            self.ema_update()
         self._optimizer.zero_grad()
         post, mets = self._cal_grad(p_data, initial, seed, ro)
+        if self._protos_frozen():
+            ops.grad_buf(self._prototypes).zero_()
         if self.world > 1:
             parallel.allreduce_mean_(self._optimizer.arena.grad)
         self._optimizer.step()
@@ -330,6 +395,8 @@ class Dreamer(nn.Module):
             self.marks.reset()
         p_data = self.preprocess(dict(data))
         self._polyak()
+        if self.rep_loss == "dreamerpro":  # replays run with ema_update_every == 1 and past update 0
+            self._ema_apply(self._pro["frac"])
         self._optimizer.zero_grad()
         return self._ph_forward(p_data, initial, seed, ro)
 
@@ -338,6 +405,8 @@ class Dreamer(nn.Module):
         post, mets = self._ph_finish(st)
         if self.world > 1:  # the arena was sum-all-reduced between the phase graphs (_update_graphed)
             self._optimizer.arena.grad.mul_(1.0 / self.world)
+        if self.rep_loss == "dreamerpro":
+            ops.grad_buf(self._prototypes).mul_(self._proto_gate)
         self._optimizer.launch_step()
         self._mark("optimizer")
         keys = [k for k, v in mets.items() if isinstance(v, torch.Tensor)]
@@ -395,6 +464,9 @@ class Dreamer(nn.Module):
             for dst, src in zip(self._g_init, initial):
                 dst.copy_(src)
         self._seed_dev.fill_(int(seed) & 0x7FFFFFFFFFFFFFFF)
+        if self.rep_loss == "dreamerpro":
+            self._ema_updates += 1
+            self._proto_gate.fill_(0.0 if self._protos_frozen() else 1.0)
         gP, gS1, gM1, gR, gM2a, gM2b, gS2, gM3 = self._graph
         main = torch.cuda.current_stream()
         side = self._side if self.use_side_stream else main
@@ -498,7 +570,7 @@ class Dreamer(nn.Module):
         leaves = [t.detach().requires_grad_(True) for t in (post_stoch, post_deter, post_logit)]
         feat_l = self.rssm.get_feat(leaves[0], leaves[1])
         feat_r = feat_l.detach().requires_grad_(True)  # replay-value leaf (side stream)
-        return dict(data=data, seed=seed, ro=ro, embed=embed, embed_l=embed_l, post_stoch=post_stoch,
+        return dict(data=data, initial=initial, seed=seed, ro=ro, embed=embed, embed_l=embed_l, post_stoch=post_stoch,
                     post_deter=post_deter, post_logit=post_logit, leaves=leaves, feat_l=feat_l, feat_r=feat_r)
 
     def _ph_side_returns(self, st):
@@ -519,7 +591,8 @@ class Dreamer(nn.Module):
         """main: world-model head losses and their backward down to the posterior leaves; the replay-value parts
         that do not need the imagined returns."""
         st["wm_total"], st["wm_losses"], st["wm_metrics"] = self._wm_heads(st["data"], st["embed"], st["leaves"],
-                                                                           st["feat_l"], st["seed"], st["ro"])
+                                                                           st["feat_l"], st["seed"], st["ro"],
+                                                                           st["initial"])
         self._mark("wm_heads")
         st["rv"] = self._repval_pre(st["data"], st["feat_r"])
         self._mark("repval_fwd")
@@ -580,7 +653,7 @@ class Dreamer(nn.Module):
                           imag_feat_tm=st["ifeat"], imag_action_tm=st["iact"], ret=rr["ret"], rret=st["rret"])
         return (st["post_stoch"], st["post_deter"]), metrics
 
-    def _wm_heads(self, data, embed, leaves, feat, seed=0, ro=0):
+    def _wm_heads(self, data, embed, leaves, feat, seed=0, ro=0, initial=None):
         """World-model losses (dreamer.py:453-576) on the posterior leaves, backward down to the leaves."""
         losses, metrics = {}, {}
         B, T = data["action"].shape[:2]
@@ -603,6 +676,8 @@ class Dreamer(nn.Module):
         elif self.rep_loss == "infonce":  # dreamer.py:533-542
             x1 = self.prj(feat.reshape(B * T, -1))
             losses["infonce"] = parallel.infonce(x1, embed.reshape(B * T, -1), self.world)
+        elif self.rep_loss == "dreamerpro":  # dreamer.py:543-566
+            losses.update(self._proto_losses(data, initial, seed, ro))
         else:
             x1 = self.prj(feat.reshape(B * T, -1))
             if self.r2_aug is not None:  # encoder on a randomly translated view, no gradient (dreamer.py:506-520)
@@ -623,6 +698,74 @@ class Dreamer(nn.Module):
         wm_total = sum(v * self._loss_scales[k] for k, v in losses.items())
         wm_total.backward()
         return wm_total, losses, metrics
+
+    def _proto_losses(self, data, initial, seed, ro):
+        """DreamerPro (dreamer.py:543-566, 731-750): the batch doubled under two random translations (shifts
+        indexed by the global augmented row: copy 1 rows ro.., copy 2 rows B_global + ro..), targets from the EMA
+        encoder, and a second posterior scan (noise stream OBS_AUG, same global-row indexing) whose backward joins
+        the world-model backward. Rows are independent in the scan, so the two copies run as two scans."""
+        c = self._pro
+        B, T = data["action"].shape[:2]
+        Bg = B * self.world
+        with torch.no_grad():
+            aug = {k: torch.cat([v, v], 0) for k, v in data.items()}
+            img = data["image"]
+            aug["image"] = torch.cat([K.random_translate(img, c["pad"], seed, ro, c["same"]),
+                                      K.random_translate(img, c["pad"], seed, Bg + ro, c["same"])], 0)
+            ema = self._ema_obs_proj(self._ema_encoder(aug))
+            ema = ema / ema.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+        embed = self.encoder(aug)
+        outs = [self.rssm.observe(embed[h], data["action"], initial, data["is_first"], seed=seed, row_offset=off,
+                                  stream_id=STREAM_OBS_AUG)
+                for h, off in ((slice(0, B), ro), (slice(B, 2 * B), Bg + ro))]
+        post_stoch = torch.cat([outs[0][0], outs[1][0]], 0)
+        post_deter = torch.cat([outs[0][1], outs[1][1]], 0)
+        return self._proto_loss(post_stoch, post_deter, embed, ema)
+
+    def _sinkhorn(self, scores):  # dreamer.py:764-790: log-space Sinkhorn-Knopp over (K, N)
+        c = self._pro
+        Kp = scores.shape[0]
+        lq = torch.log_softmax(scores.reshape(-1) / c["eps"], 0).view(Kp, -1)
+        N = lq.shape[1]
+        for _ in range(c["iters"]):
+            lq = lq - torch.logsumexp(lq, 1, keepdim=True) - math.log(Kp)
+            lq = lq - torch.logsumexp(lq, 0, keepdim=True) - math.log(N)
+        return torch.exp(lq + math.log(N)).view(scores.shape)
+
+    def _proto_loss(self, post_stoch, post_deter, embed, ema):
+        """Dreamer.proto_loss (dreamer.py:792-843). The Sinkhorn targets balance each augmented half over the
+        GLOBAL batch: under data parallelism each half's EMA projections are gathered (rank order = global row
+        order), every rank runs the same Sinkhorn and keeps its own columns."""
+        c = self._pro
+        w, tau = c["warm_up"], c["tau"]
+        B2, T = embed.shape[:2]
+        B = B2 // 2
+        protos = F.normalize(self._prototypes, p=2, dim=-1)
+
+        def scores(x, pr):  # unit rows (n, T, Pd) -> (K, n, T - warm_up)
+            n = x.shape[0]
+            return ops.MatmulNTFn.apply(x.reshape(n * T, -1), pr).view(n, T, -1).permute(2, 0, 1)[:, :, w:]
+
+        obs = self.obs_proj(embed)
+        obs_norm = obs.norm(dim=-1)
+        obs_logits = F.log_softmax(scores(F.normalize(obs, p=2, dim=-1), protos) / tau, dim=0)
+        o1, o2 = obs_logits.chunk(2, dim=1)
+        with torch.no_grad():
+            pr = protos.detach()
+            lo = self.rank * B if self.world > 1 else 0
+            t = []
+            for half in (ema[:B], ema[B:]):
+                q = self._sinkhorn(scores(parallel.gather_returns(half.contiguous(), self.world), pr))
+                t.append(q[:, lo:lo + B])
+            t1, t2 = t
+        targets = torch.cat([t1, t2], 1)
+        feat = self.feat_proj(self.rssm.get_feat(post_stoch, post_deter))
+        feat_norm = feat.norm(dim=-1)
+        feat_logits = F.log_softmax(scores(F.normalize(feat, p=2, dim=-1), protos) / tau, dim=0)
+        swav = -0.5 * (t2 * o1).sum(0).mean() - 0.5 * (t1 * o2).sum(0).mean()
+        temp = -(targets * feat_logits).sum(0).mean()
+        norm = ((obs_norm - 1) ** 2).mean() + ((feat_norm - 1) ** 2).mean()
+        return {"swav": swav, "temp": temp, "norm": norm}
 
     def _repval_pre(self, data, feat_r):
         """Replay-value parts that do not need the imagined returns (dreamer.py:638-652): value / slow-value modes on

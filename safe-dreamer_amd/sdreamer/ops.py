@@ -346,6 +346,26 @@ class BarlowFn(torch.autograd.Function):
         return dx1, None, None
 
 
+class MatmulNTFn(torch.autograd.Function):
+    """a (M, K) @ b (N, K)^T with gradients for both operands on the HIP GEMM (DreamerPro's prototype scores,
+    dreamer.py:801/811/832, where b is the normalised prototype table: a non-leaf, so its gradient is returned
+    through autograd rather than accumulated into a parameter buffer)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = a.contiguous(), b.contiguous()
+        ctx.save_for_backward(a, b)
+        return k.mm(a, b.t())
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.contiguous()
+        da = k.mm(g, b, fast=True) if ctx.needs_input_grad[0] else None
+        db = k.mm(g.t(), a, fast=True) if ctx.needs_input_grad[1] else None
+        return da, db
+
+
 class InfoNCEFn(torch.autograd.Function):
     """InfoNCE loss (dreamer.py:533-542): logits = x1 x2g^T (f32 GEMM), cross entropy against the diagonal; rows of x1
     (n, E) with grad, x2g (Nc, E) detached (all ranks' x2 under data parallel), row r labelled Nc-column r + off.

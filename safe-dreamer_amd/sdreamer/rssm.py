@@ -27,6 +27,7 @@ from . import ops
 from .networks import Act, BlockLinear, Lambda, Linear, RMSNorm
 
 STREAM_OBS, STREAM_IMG, STREAM_ACT, STREAM_POLICY, STREAM_POLICY_ACT = 1, 2, 3, 4, 5  # oracle/noise.py
+STREAM_OBS_AUG = 7  # DreamerPro's augmented-view posterior scan
 # the fused scan (csrc/scan.hip) is the default; SDREAMER_FUSED_SCAN=0 selects the per-op HIP kernels (tests compare)
 FUSED_SCAN = os.environ.get("SDREAMER_FUSED_SCAN", "1") != "0"
 # debugging aid: fill the fused backward's scratch tensors with NaN so any element read before it is written shows
@@ -42,14 +43,14 @@ def _fused_scan_ok(rssm, B):
         D % 64 == 0
 
 
-def _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, work):
+def _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, work, stream_id=STREAM_OBS):
     d = nat.ScanDesc()
     D, U, SK, Kd, G = rssm._deter, rssm._hidden, rssm.flat_stoch, rssm._discrete, rssm._blocks
     d.B, d.T, d.D, d.U, d.SK, d.Kd, d.G = B, T, D, U, SK, Kd, G
     d.ks_d, d.ks_s = 4, 2  # K splits of the D-wide / SK-wide step GEMMs (slabs summed by the consumer)
     d.eps, d.unimix = K.EPS, rssm._unimix_ratio
     sh, sp = K.seed_args(seed)
-    d.seed, d.seed_ptr, d.stream_id, d.group_offset = sh, sp, STREAM_OBS, int(row_offset) * rssm._stoch
+    d.seed, d.seed_ptr, d.stream_id, d.group_offset = sh, sp, int(stream_id), int(row_offset) * rssm._stoch
     for k in ("W0", "b0", "n0", "W1", "b1", "n1", "Wh", "bh", "nh", "Wg", "bg", "Wl", "bl"):
         setattr(d, k, P[k].data_ptr())
     d.no = P["no"].data_ptr()
@@ -153,9 +154,9 @@ class RSSM(nn.Module):
     def get_feat(self, stoch, deter):  # rssm.py:211-217
         return torch.cat([stoch.reshape(*stoch.shape[:-2], self.flat_stoch), deter], -1)
 
-    def observe(self, embed, action, initial, reset, seed=0, row_offset=0):
+    def observe(self, embed, action, initial, reset, seed=0, row_offset=0, stream_id=STREAM_OBS):
         """rssm.py:140-156. embed (B,T,E), action (B,T,A), initial ((B,S,K),(B,D)), reset (B,T[,1]) bool.
-        `seed`/`row_offset` select the counter-based posterior noise (oracle/noise.py STREAM_OBS)."""
+        `seed`/`row_offset`/`stream_id` select the counter-based posterior noise (oracle/noise.py)."""
         B, T = action.shape[:2]
         r = reset.reshape(B, T).to(torch.uint8)
         stoch0, deter0 = initial
@@ -165,9 +166,10 @@ class RSSM(nn.Module):
             # autograd node; noise indexed by global row, weight gradients accumulate)
             outs = [ObserveScan.apply(embed[c:c + 16], action[c:c + 16], r[c:c + 16].contiguous(),
                                       s0[c:c + 16].contiguous(), deter0[c:c + 16].contiguous(), self, seed,
-                                      int(row_offset) + c) for c in range(0, B, 16)]
+                                      int(row_offset) + c, stream_id) for c in range(0, B, 16)]
             return tuple(torch.cat([o[i] for o in outs], 0) for i in range(3))
-        return ObserveScan.apply(embed, action, r, s0.contiguous(), deter0.contiguous(), self, seed, int(row_offset))
+        return ObserveScan.apply(embed, action, r, s0.contiguous(), deter0.contiguous(), self, seed, int(row_offset),
+                                 stream_id)
 
     @torch.no_grad()
     def obs_step(self, stoch, deter, prev_action, embed, reset, seed=0, step=0, row_offset=0,
@@ -273,7 +275,7 @@ class ObserveScan(torch.autograd.Function):
     """RSSM.observe (rssm.py:140-156) forward + BPTT backward on HIP kernels. Saved activations are time-major."""
 
     @staticmethod
-    def forward(ctx, embed, action, reset, stoch0, deter0, rssm, seed, row_offset):
+    def forward(ctx, embed, action, reset, stoch0, deter0, rssm, seed, row_offset, stream_id=STREAM_OBS):
         P = rssm._p()
         B, T, A = action.shape
         E = embed.shape[-1]
@@ -311,7 +313,7 @@ class ObserveScan(torch.autograd.Function):
         fused = _fused_scan_ok(rssm, B)
         if fused:
             WoD = P["Wo"][:, :D].contiguous()
-            d = _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, None)
+            d = _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, None, stream_id)
             work = torch.empty(_scan_work(d), dtype=f32, device=dev)
             d.work, d.WoD = work.data_ptr(), WoD.data_ptr()
             d.stoch0, d.deter0 = stoch0.data_ptr(), deter0.data_ptr()
@@ -343,11 +345,11 @@ class ObserveScan(torch.autograd.Function):
             K.gemm(deter[t], P["Wo"][:, :D].t(), op[t], beta=1.0)
             K.rmsnorm_fwd(op[t], P["no"], y=oo[t], rstd=ro[t])
             K.linear(oo[t], P["Wl"], P["bl"], out=logit[t])
-            K.onehot_sample(logit[t], Kd, rssm._unimix_ratio, seed, STREAM_OBS, t, row_offset * S, out=stoch[t])
+            K.onehot_sample(logit[t], Kd, rssm._unimix_ratio, seed, stream_id, t, row_offset * S, out=stoch[t])
             prev_s, prev_h = stoch[t], deter[t]
         ctx.save_for_backward(rt, a_n, x2p, r2, emb_t, s_in, h_in, x0p, x1p, r0, r1, xcat, hp, hh, rh, gates, deter,
                               op, oo, ro, logit)
-        ctx.rssm, ctx.seed, ctx.row_offset = rssm, seed, row_offset
+        ctx.rssm, ctx.seed, ctx.row_offset, ctx.stream_id = rssm, seed, row_offset, stream_id
         ctx.dims = (B, T, A, E)
         ctx.fused = fused
         if fused:
@@ -394,7 +396,7 @@ class ObserveScan(torch.autograd.Function):
         carry_h = torch.zeros(B, D, dtype=f32, device=dev)
         for t in reversed(range(T)):
             ds = ds_out[t] + carry_s
-            K.onehot_sample_bwd(logit[t], ds, Kd, rssm._unimix_ratio, ctx.seed, STREAM_OBS, t, ctx.row_offset * S,
+            K.onehot_sample_bwd(logit[t], ds, Kd, rssm._unimix_ratio, ctx.seed, ctx.stream_id, t, ctx.row_offset * S,
                                 dlogits=dl_all[t], accumulate=True)
             d_o = K.mm(dl_all[t], P["Wl"])
             K.rmsnorm_bwd(op[t], P["no"], ro[t], d_o, dx=d_op[t], dw=gb(P["no"]))
@@ -444,7 +446,7 @@ class ObserveScan(torch.autograd.Function):
                   WbdT=P["Wbd"].transpose(1, 2).contiguous(), WgT=P["Wg"].transpose(1, 2).contiguous(),
                   WoDT=Wo_d.t().contiguous(), WlT=P["Wl"].t().contiguous())
         x2 = ctx.x2
-        d = _scan_desc(rssm, P, B, T, ctx.seed, ctx.row_offset, rt, x2, x2, None)
+        d = _scan_desc(rssm, P, B, T, ctx.seed, ctx.row_offset, rt, x2, x2, None, ctx.stream_id)
         work = e(_scan_work(d))
         d.work = work.data_ptr()
         for k, v in list(tr.items()) + [("s_in", s_in), ("h_in", h_in), ("x0p", x0p), ("x1p", x1p), ("r0", r0),
@@ -499,4 +501,4 @@ class ObserveScan(torch.autograd.Function):
         K.gemm(d_x2p.t(), a_n, gb(P["W2"]), beta=1.0, fast=True)
         K.colsum(d_x2p, gb(P["b2"]))
         d_embed = d_emb.view(T, B, E).transpose(0, 1).contiguous()
-        return d_embed, None, None, None, None, None, None, None
+        return d_embed, None, None, None, None, None, None, None, None

@@ -40,6 +40,7 @@ CASES = {
     "walker_r2": ("dmc/cnn", [], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
     "walker_infonce": ("dmc/cnn", ["model.rep_loss=infonce"], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
     "walker_r2aug": ("dmc/cnn", ["model.r2dreamer.aug.enabled=True"], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
+    "walker_pro": ("dmc/cnn", ["model.rep_loss=dreamerpro"], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
     "walker_dreamer": ("dmc/walker_dreamer", [], {"image": (64, 64, 3)}, 6, False, 2, 4, 3),
     "atari_r2": ("dmc/atari_breakout", [], {"image": (64, 64, 3)}, 4, True, 2, 4, 3),
     "maze_r2": ("dmc/memory_maze", [], {"image": (64, 64, 3)}, 6, True, 2, 4, 3),
@@ -85,8 +86,9 @@ def make_initial(rng, S, K, D, B):
 class NoiseSeq:
     """Injects oracle noise in _cal_grad call order (see module doc)."""
 
-    def __init__(self, T, H1, seed):
+    def __init__(self, T, H1, seed, pro=False):
         self.T, self.H1, self.seed = T, H1, seed
+        self.pro = pro  # DreamerPro: a second posterior scan over the augmented 2B batch follows the prior
         self.g = 0
         self.n = 0
 
@@ -99,7 +101,10 @@ class NoiseSeq:
             return nz.gumbel_block(self.seed, nz.STREAM_OBS, i, B, 0, int(np.prod(shape[1:]))).reshape(shape)
         if i == T:  # prior over (B, T, S, K): sample discarded
             return np.zeros(shape, np.float32)
-        j = i - T - 1
+        if self.pro and i <= 2 * T:  # augmented observe step i - T - 1, (2B, S, K)
+            return nz.gumbel_block(self.seed, nz.STREAM_OBS_AUG, i - T - 1, shape[0], 0,
+                                   int(np.prod(shape[1:]))).reshape(shape)
+        j = i - T - 1 - (T if self.pro else 0)
         N = shape[0]
         if self.discrete_act:
             t, which = divmod(j, 2)
@@ -129,6 +134,13 @@ def aug_randint(aug, seed, B, T):
     return randint
 
 
+def patch_randint(cfg, seed, B, T):
+    if cfg.model.rep_loss == "dreamerpro":  # augment_data's doubled batch (dreamer.py:731-743)
+        torch.randint = aug_randint(cfg.model.dreamer_pro.aug, seed, 2 * B, T)
+    elif bool(cfg.model.r2dreamer.aug.enabled):
+        torch.randint = aug_randint(cfg.model.r2dreamer.aug, seed, B, T)
+
+
 def run_case(name, mods, TD):
     cfg_name, ovr, obs, A, discrete, B, T, H = CASES[name]
     cfg = load_config(cfg_name, ["device=cpu", "model.compile=False", f"model.imag_horizon={H}"] + ovr)
@@ -150,7 +162,7 @@ def run_case(name, mods, TD):
     ag = D.Dreamer(copy.deepcopy(cfg.model), Spaces({k: Sp(v) for k, v in obs.items()}), act_space)
     spec = Spec(cfg.model, obs, A, discrete)
     sd = ag.state_dict()
-    ref_train = [k for k in sd if not k.startswith("_frozen") and not k.startswith("_slow_value")
+    ref_train = [k for k in sd if not k.startswith(("_frozen", "_slow_value", "_ema_"))
                  and k != "return_ema.ema_vals"]
     assert sorted(ref_train) == sorted(spec.shapes), (set(ref_train) ^ set(spec.shapes))
     for k, v in spec.shapes.items():
@@ -180,7 +192,7 @@ def run_case(name, mods, TD):
             if many:
                 rec.setdefault(key, []).append(r)
             else:
-                rec[key] = r
+                rec.setdefault(key, r)  # first call (DreamerPro's augmented observe comes second)
             return r
 
         setattr(obj, attr, w)
@@ -203,7 +215,7 @@ def run_case(name, mods, TD):
         out[f"u{u}_in_init_stoch"] = init_np[0].argmax(-1).astype(np.int16)
         out[f"u{u}_in_init_deter"] = init_np[1]
         out[f"u{u}_seed"] = seed
-        seq = NoiseSeq(T, H + 1, seed)
+        seq = NoiseSeq(T, H + 1, seed, cfg.model.rep_loss == "dreamerpro")
         seq.discrete_act = discrete
 
         def gs(logits, tau=1, hard=False, eps=1e-10, dim=-1):
@@ -221,8 +233,7 @@ def run_case(name, mods, TD):
         torch.nn.functional.gumbel_softmax = gs
         torch.distributions.Normal.rsample = rs
         orig_randint = torch.randint
-        if bool(cfg.model.r2dreamer.aug.enabled):
-            torch.randint = aug_randint(cfg.model.r2dreamer.aug, seed, B, T)
+        patch_randint(cfg, seed, B, T)
 
         class Buf:
             def sample(self_):
@@ -239,7 +250,7 @@ def run_case(name, mods, TD):
             torch.nn.functional.gumbel_softmax = orig_gs
             torch.distributions.Normal.rsample = orig_rs
             torch.randint = orig_randint
-        assert seq.g == T + 1 + (H + 1) * (2 if discrete else 1), seq.g
+        assert seq.g == T + 1 + (T if seq.pro else 0) + (H + 1) * (2 if discrete else 1), seq.g
         assert seq.n == (0 if discrete else H + 1), seq.n
         ps, pdet, plog = rec["observe"]
         out[f"u{u}_post_idx"] = ps.argmax(-1).numpy().astype(np.int16)
@@ -307,7 +318,7 @@ def grad_case(name, mods, TD):
     rng = np.random.default_rng(zlib.crc32(name.encode()))
     data_np = make_batch(rng, obs, A, discrete, B, T)
     init_np = make_initial(rng, spec.S, spec.K, spec.D, B)
-    seq = NoiseSeq(T, H + 1, 1000)
+    seq = NoiseSeq(T, H + 1, 1000, cfg.model.rep_loss == "dreamerpro")
     seq.discrete_act = discrete
     orig_gs = torch.nn.functional.gumbel_softmax
     orig_rs = torch.distributions.Normal.rsample
@@ -326,12 +337,13 @@ def grad_case(name, mods, TD):
     torch.nn.functional.gumbel_softmax = gs
     torch.distributions.Normal.rsample = rs
     orig_randint = torch.randint
-    if bool(cfg.model.r2dreamer.aug.enabled):
-        torch.randint = aug_randint(cfg.model.r2dreamer.aug, 1000, B, T)
+    patch_randint(cfg, 1000, B, T)
     try:
         d = TD({k: torch.from_numpy(v) for k, v in data_np.items()}, batch_size=(B, T))
         d = ag.preprocess(d)
         ag._update_slow_target()
+        if cfg.model.rep_loss == "dreamerpro":
+            ag.ema_update()  # EMA encoder := online encoder, unit prototypes (as update 0 does)
         ag._cal_grad(d, (torch.from_numpy(init_np[0]), torch.from_numpy(init_np[1])))
     finally:
         torch.nn.functional.gumbel_softmax = orig_gs

@@ -16,6 +16,7 @@ CASES = {
     "walker_r2": ("dmc/cnn", {"image": (64, 64, 3)}),
     "walker_infonce": ("dmc/cnn", {"image": (64, 64, 3)}, ["model.rep_loss=infonce"]),
     "walker_r2aug": ("dmc/cnn", {"image": (64, 64, 3)}, ["model.r2dreamer.aug.enabled=True"]),
+    "walker_pro": ("dmc/cnn", {"image": (64, 64, 3)}, ["model.rep_loss=dreamerpro"]),
     "walker_dreamer": ("dmc/walker_dreamer", {"image": (64, 64, 3)}),
     "atari_r2": ("dmc/atari_breakout", {"image": (64, 64, 3)}),
     "maze_r2": ("dmc/memory_maze", {"image": (64, 64, 3)}),

@@ -81,7 +81,7 @@ def _run(name, world):
     return res
 
 
-@pytest.mark.parametrize("name", ["walker_r2", "walker_dreamer", "walker_infonce", "walker_r2aug"])
+@pytest.mark.parametrize("name", ["walker_r2", "walker_dreamer", "walker_infonce", "walker_r2aug", "walker_pro"])
 def test_two_rank_update_equals_one_rank(name):
     one = _run(name, 1)[0]
     two = _run(name, 2)

@@ -21,7 +21,7 @@ from sdreamer.config import load_config
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-WM_KEYS = ("dyn", "rep", "rew", "con", "barlow", "infonce", "image", "position", "velocity")
+WM_KEYS = ("dyn", "rep", "rew", "con", "barlow", "infonce", "swav", "temp", "norm", "image", "position", "velocity")
 
 
 class _Sp:
@@ -46,7 +46,7 @@ def build_agent(name):
         act.discrete = True
     ag = Dreamer(copy.deepcopy(gcfg.model), _Spaces({k: _Sp(v) for k, v in obs.items()}), act)
     sd = {k: torch.from_numpy(v) for k, v in params.items()}
-    for k, sk in spec.slow_names.items():
+    for k, sk in list(spec.slow_names.items()) + list(spec.ema_names.items()):
         sd[sk] = torch.from_numpy(params[k])
     sd["return_ema.ema_vals"] = torch.zeros(2)
     missing, unexpected = ag.load_state_dict(sd, strict=False)
@@ -105,7 +105,7 @@ def test_update_matches_reference(name):
             assert np.abs(got - ref).max() <= max(2e-3 * step, 1e-6 * np.abs(ref).max()), k
 
 
-@pytest.mark.parametrize("name", ["walker_r2", "walker_r2aug"])
+@pytest.mark.parametrize("name", ["walker_r2", "walker_r2aug", "walker_pro"])
 def test_graph_replay_matches_eager(name):
     """HIP-graph replays (update 3+) produce exactly the eager results: same kernels, device-resident seed
     (walker_r2aug: the augmentation shifts also follow the device seed)."""
@@ -129,3 +129,29 @@ def test_graph_replay_matches_eager(name):
         assert e[u][:3] == g[u][:3], (u, e[u][:3], g[u][:3])
         assert torch.equal(e[u][3], g[u][3]) and torch.equal(e[u][4], g[u][4])
     assert torch.equal(e[5], g[5])
+
+
+@pytest.mark.parametrize("name", ["walker_pro", "walker_r2aug"])
+def test_cal_grad_matches_reference(name):
+    """Gradients of one _cal_grad at the initial weights vs the reference's (golden g_*): walker_pro checks the
+    prototype / projection gradients that the default prototype freeze zeroes before the optimizer step."""
+    ag, z, spec, obs = build_agent(name)
+    ag.use_graphs = False
+    data = ag.preprocess(batch(z, 0, obs, DEV))
+    init = initial(z, 0, spec, DEV)
+    ag._update_slow_target()
+    if spec.rep_loss == "dreamerpro":
+        ag.ema_update()
+    ag._optimizer.zero_grad()
+    ag._cal_grad(data, init, 1000, 0)
+    torch.cuda.synchronize()
+    named = dict(ag.named_parameters())
+    bad = []
+    for k in spec.shapes:
+        g = named[k].grad
+        flat = (torch.zeros_like(named[k]) if g is None else g).reshape(-1).double().cpu().numpy()
+        ref_n = float(z[f"g_{k}__n"])
+        n = float(np.linalg.norm(flat))
+        if abs(n - ref_n) > 2e-3 * max(ref_n, 1e-9) and abs(n - ref_n) > 1e-7:
+            bad.append((k, n, ref_n))
+    assert not bad, bad

@@ -63,6 +63,8 @@ def test_oracle_grads_match_reference(name):
     torch.set_num_threads(8)
     ag = OracleAgent(spec, params)
     ag.update_slow_target()
+    if spec.rep_loss == "dreamerpro":
+        ag.ema_update()
     ag.cal_grad(batch(z, 0, obs), initial(z, 0, spec), int(z["u0_seed"]))
     for k in spec.shapes:
         g = ag.P[k].grad
