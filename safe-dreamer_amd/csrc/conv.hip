@@ -319,31 +319,14 @@ __global__ __launch_bounds__(256) void conv_fwd16(GemmArgs g, Geom G, int lw, in
   }
 }
 
-// ConvEncoder stage fused: conv (fwd16 main loop) -> MaxPool2d(2) -> RMSNorm2D -> SiLU (networks.py:201-216).
-// A 128-pixel M tile holds whole 2x2 windows (128 % 2W == 0, image rows come in pairs), so the epilogue stages the
-// conv tile in the main loop's LDS area, pools it, normalises over the Co channels (8 threads per pooled pixel) and
-// writes only the pooled outputs (pooled pre-norm values, argmax, rstd for the backward; y NHWC or NCHW-flat).
-template <int BN, bool ES>
-__global__ __launch_bounds__(256) void conv_fwd16_pool(GemmArgs g, Geom G, int lw, int lhw, const float* nw,
-                                                       float* pooled, uint8_t* amax, float* y, float* rstd, float eps,
-                                                       int nchw_flat) {
-  __shared__ int tab[MAX_TAPQ];
-  build_taps(tab, G, g.K);
-  constexpr int BM = 128, WM = 32, LDC = BN + 1;
-  const int bm0 = blockIdx.x * BM;
-  f32x4 acc[WM / 16][BN / 16];
-  if constexpr (ES) {
-    Im2colRowsB<BM> la(G, tab, g.M, bm0, lw, lhw);
-    DenseKCB<BN> lb(g.B, g.ldb, g.N, 0);
-    gemm16_mainloop_es<BM, BN, WM, BN>(la, lb, 0, g.K, acc);
-  } else {
-    Im2colRowsT<BM> la(G, tab, g.M, bm0, lw, lhw);
-    DenseOperand<BN, true, true> lb(g.B, g.ldb, g.N, 0);
-    gemm16_mainloop<BM, BN, WM, BN>(la, lb, 0, g.K, acc);
-  }
-  __syncthreads();  // every wave is done reading the staging area
-  float* C = sd_smem<gemm16_smem_floats<BM, BN>()>();
-  static_assert(BM * LDC <= gemm16_smem_floats<BM, BN>(), "tile fits the staging area");
+// Stage epilogue shared by the fused forward kernels: the 128-pixel conv tile (+ bias) is staged in LDS at C, 2x2
+// max-pooled (argmax kept for the backward), RMS-normalised over the BN channels (8 threads per pooled pixel) and
+// SiLU'd; only the pooled outputs are written (pooled pre-norm values, argmax, rstd; y NHWC or NCHW-flat).
+template <int BN, int WM>
+SD_DEV void pool_epilogue(const f32x4 (&acc)[WM / 16][BN / 16], float* C, const GemmArgs& g, const Geom& G, int lw,
+                          int lhw, int bm0, const float* nw, float* pooled, uint8_t* amax, float* y, float* rstd,
+                          float eps, int nchw_flat) {
+  constexpr int LDC = BN + 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
 #pragma unroll
   for (int i = 0; i < WM / 16; ++i)
@@ -395,6 +378,143 @@ __global__ __launch_bounds__(256) void conv_fwd16_pool(GemmArgs g, Geom G, int l
     const long o = nchw_flat ? (long)n * BN * Ho * Wo + (long)c * Ho * Wo + prem : gpp * BN + c;
     if (valid) y[o] = siluf_(z);
   }
+}
+
+
+// ConvEncoder stage fused: conv (fwd16 main loop) -> MaxPool2d(2) -> RMSNorm2D -> SiLU (networks.py:201-216).
+// A 128-pixel M tile holds whole 2x2 windows (128 % 2W == 0, image rows come in pairs), so the epilogue stages the
+// conv tile in the main loop's LDS area, pools it, normalises over the Co channels (8 threads per pooled pixel) and
+// writes only the pooled outputs (pooled pre-norm values, argmax, rstd for the backward; y NHWC or NCHW-flat).
+template <int BN, bool ES>
+__global__ __launch_bounds__(256) void conv_fwd16_pool(GemmArgs g, Geom G, int lw, int lhw, const float* nw,
+                                                       float* pooled, uint8_t* amax, float* y, float* rstd, float eps,
+                                                       int nchw_flat) {
+  __shared__ int tab[MAX_TAPQ];
+  build_taps(tab, G, g.K);
+  constexpr int BM = 128, WM = 32;
+  const int bm0 = blockIdx.x * BM;
+  f32x4 acc[WM / 16][BN / 16];
+  if constexpr (ES) {
+    Im2colRowsB<BM> la(G, tab, g.M, bm0, lw, lhw);
+    DenseKCB<BN> lb(g.B, g.ldb, g.N, 0);
+    gemm16_mainloop_es<BM, BN, WM, BN>(la, lb, 0, g.K, acc);
+  } else {
+    Im2colRowsT<BM> la(G, tab, g.M, bm0, lw, lhw);
+    DenseOperand<BN, true, true> lb(g.B, g.ldb, g.N, 0);
+    gemm16_mainloop<BM, BN, WM, BN>(la, lb, 0, g.K, acc);
+  }
+  __syncthreads();  // every wave is done reading the staging area
+  float* C = sd_smem<gemm16_smem_floats<BM, BN>()>();
+  static_assert(BM * (BN + 1) <= gemm16_smem_floats<BM, BN>(), "tile fits the staging area");
+  pool_epilogue<BN, WM>(acc, C, g, G, lw, lhw, bm0, nw, pooled, amax, y, rstd, eps, nchw_flat);
+}
+
+// Direct ConvEncoder stage forward (stride 1, same padding, no upsample): the 128-pixel tile is R = 128 / W whole
+// output rows of one image, so its receptive field is one (R + KS - 1) x (W + KS - 1) x CI input patch. The patch
+// is staged in LDS once (pixel stride CI + 4 floats: conflict-free ds_read_b128 fragments) and every tap's A
+// fragments are read from it at the tap's offset — the 25x im2col expansion is never re-read from L2. The weights
+// stream through a double-buffered early-store B stage, one (tap, 32-channel) k tile per iteration; the epilogue
+// (pool + RMSNorm + SiLU) is conv_fwd16_pool's. Wave w owns tile pixels 32w..32w+31 (TM = 2) x all BN channels.
+template <int BN, int CI, int LW, int KS>
+__global__ __launch_bounds__(256) void conv_fwd_direct_pool(GemmArgs g, Geom G, int lhw, const float* nw,
+                                                            float* pooled, uint8_t* amax, float* y, float* rstd,
+                                                            float eps, int nchw_flat) {
+  constexpr int BM = 128, WM = 32, TM = WM / 16, TN = BN / 16, W = 1 << LW, R = BM / W;
+  constexpr int PH = R + KS - 1, PW = W + KS - 1, CSI = CI + 4, PAD = KS / 2;
+  constexpr int PATCH = PH * PW * CSI, SB = BN * LDS_ROW;
+  constexpr int NQ = PH * PW * (CI / 4), NQT = (NQ + 255) / 256;
+  static_assert(CI % 32 == 0 && (CSI / 4) % 2 == 1, "32-channel k tiles, odd float4 pixel stride");
+  static_assert(BM * (BN + 1) <= PATCH, "epilogue tile fits the patch area");
+  float* smem = sd_smem<PATCH + 2 * SB>();
+  float* patch = smem;
+  float* bst = smem + PATCH;
+  // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs, so XCD x gets the contiguous tile range
+  // x * (tiles / 8) ...; vertically adjacent tiles (which share KS - 1 halo rows) then meet in the same L2
+  const int nt = gridDim.x, tile = (nt & 7) ? blockIdx.x : (blockIdx.x & 7) * (nt >> 3) + (blockIdx.x >> 3);
+  const int bm0 = tile * BM;
+  const int n = bm0 >> lhw, y0 = (bm0 & ((1 << lhw) - 1)) >> LW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+  DenseKCB<BN> lb(g.B, g.ldb, g.N, 0);
+  lb.load(0, g.K);
+  {  // the input patch, zero outside the image (range-checked buffer loads), all loads issued before the stores
+    const sd_rsrc rs = sd_make_rsrc(G.in, (long)G.Nb * G.Hs * G.Ws * CI * 4);
+    f32x4 v[NQT];
+#pragma unroll
+    for (int u = 0; u < NQT; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int pix = i / (CI / 4), c4 = i % (CI / 4);
+      const int py = pix / PW, px = pix % PW;
+      const int yy = y0 + py - PAD, xx = px - PAD;
+      const bool ok = i < NQ && (unsigned)yy < (unsigned)G.Hs && (unsigned)xx < (unsigned)W;
+      v[u] = sd_bload4(rs, ok ? (uint32_t)((((n * G.Hs + yy) * W + xx) * CI + 4 * c4) * 4) : SD_OOB);
+    }
+#pragma unroll
+    for (int u = 0; u < NQT; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      if ((u + 1) * 256 <= NQ || i < NQ)
+        *reinterpret_cast<f32x4*>(patch + (i / (CI / 4)) * CSI + 4 * (i % (CI / 4))) = v[u];
+    }
+  }
+  lb.store(bst);
+  lb.load(BK, g.K);
+  __syncthreads();
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fragment base of tile pixel p = 32w + 16i + l16 (row p >> LW, column p & (W - 1)) at tap (0, 0)
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int p = wave * WM + 16 * i + l16;
+    abase[i] = ((p >> LW) * PW + (p & (W - 1))) * CSI + 8 * q;
+  }
+  constexpr int NK = KS * KS * (CI / BK);
+  for (int kt = 0; kt < NK; ++kt) {
+    const float* cur = bst + (kt & 1) * SB;
+    float* nxt = bst + ((kt & 1) ^ 1) * SB;
+    const int tap = kt / (CI / BK), ci0 = (kt % (CI / BK)) * BK;
+    const int toff = ((tap / KS) * PW + tap % KS) * CSI + ci0;
+    float af[TM][8], bf[TN][8];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* pa = patch + abase[i] + toff;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(pa), x1 = *reinterpret_cast<const f32x4*>(pa + 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) { af[i][s] = x0[s]; af[i][4 + s] = x1[s]; }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* pb = cur + (16 * j + l16) * LDS_ROW + 8 * q;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(pb), x1 = *reinterpret_cast<const f32x4*>(pb + 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) { bf[j][s] = x0[s]; bf[j][4 + s] = x1[s]; }
+    }
+    lb.store(nxt);
+    lb.load((kt + 2 < NK ? kt + 2 : NK - 1) * BK, g.K);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    __syncthreads();
+  }
+  pool_epilogue<BN, WM>(acc, patch, g, G, LW, lhw, bm0, nw, pooled, amax, y, rstd, eps, nchw_flat);
+}
+
+// SDHIP_CONV_DIRECT_FWD (benchmarking knob): 1 (default) = conv_fwd_direct_pool where it applies, 0 = implicit GEMM.
+// (A variant streaming each lane's weight fragments into registers — no LDS stage, no barriers, 3 workgroups per
+// CU — measured slower: 679 vs 660 us on encoder stage 2 at 1024 images.)
+bool conv_direct_fwd() {
+  static int a = -1;
+  if (a < 0) {
+    const char* e = getenv("SDHIP_CONV_DIRECT_FWD");
+    a = e ? atoi(e) : 1;
+  }
+  return a != 0;
 }
 
 // bwd-weight: M = Co (one tile), N = kh*kw*Ci + 1, K = pixels (split-K slabs), 4 waves along N
@@ -1120,6 +1240,12 @@ extern "C" int sd_conv2d_fwd_pool(const float* in, const float* w, const float* 
     return SD_ESHAPE;
   const dim3 grid(g.M / 128);
   const bool es = conv_es() && (long)Nb * Hs * Ws * Ci < (1L << 29);  // buffer offsets < 2 GiB
+  if (conv_direct_fwd() && es && Co == 48 && Ci == 32 && Ws == 32 && kh == 5 && kw == 5 && pad == 2 &&
+      Hs % 4 == 0 && al16(in)) {
+    conv_fwd_direct_pool<48, 32, 5, 5><<<grid, 256, 0, s>>>(g, G, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat);
+    SD_LAUNCH_CHECK();
+    return SD_OK;
+  }
 #define SD_FWDP(BN)                                                                                          \
   (es ? conv_fwd16_pool<BN, true><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat) \
       : conv_fwd16_pool<BN, false><<<grid, 256, 0, s>>>(g, G, lw, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat))

@@ -22,7 +22,7 @@ def from_csv(path):
     return sorted(rows, key=lambda r: -r[2])
 
 
-def probe_rows(path, name_like="conv_fwd16_poolILi48E", grid_wgs=8192):
+def probe_rows(path, name_like="conv_fwd_direct_poolILi48E", grid_wgs=8192):
     """Dispatches of the bench roofline probe kernel (encoder conv2 fwd: 8192 workgroups) — the per-launch average
     to compare with bench.py's roofline.avg_us."""
     con = sqlite3.connect(path)
@@ -39,7 +39,7 @@ def main(path, top=40, per=1):
     if path.endswith(".db"):
         pr = probe_rows(path)
         if pr:
-            print(f"roofline probe kernel conv_fwd16_pool<48> at 8192 workgroups (encoder conv2 fwd): {len(pr)} dispatches, "
+            print(f"roofline probe kernel conv_fwd_direct_pool<48> at 8192 workgroups (encoder conv2 fwd): {len(pr)} dispatches, "
                   f"avg {sum(pr) / len(pr) / 1e3:.1f} us, min {min(pr) / 1e3:.1f} us\n")
     tot = sum(r[2] for r in rows)
     print(f"total kernel time {tot / 1e6:.2f} ms over the profiled run ({tot / 1e6 / per:.2f} ms per step, {per} steps)")

@@ -23,10 +23,11 @@ ALGO = {
     "conv_fwd16<48>": 4.0 * 1024 * 32 * 32 * (32 + 48),  # NHWC input, full-resolution conv output
     # input + pooled (f32) + y (f32) + argmax (u8) + rstd (f32 per pooled pixel)
     "conv_fwd16_pool<48>": 4.0 * 1024 * 32 * 32 * 32 + 1024 * 16 * 16 * (48 * (4 + 4 + 1) + 4),
+    "conv_fwd_direct_pool<48>": 4.0 * 1024 * 32 * 32 * 32 + 1024 * 16 * 16 * (48 * (4 + 4 + 1) + 4),
 }
 
 
-def main(fetch_db, write_db, out, name="conv_fwd16_pool<48>"):
+def main(fetch_db, write_db, out, name="conv_fwd_direct_pool<48>"):
     wgs = 8192
     pat = name.rstrip(">")  # demangled names carry further template arguments (e.g. conv_fwd16_pool<48, true>)
     f, nf, fdesc = per_launch(fetch_db, "FETCH_SIZE", pat, wgs)
