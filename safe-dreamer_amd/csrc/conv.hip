@@ -414,8 +414,11 @@ __global__ __launch_bounds__(256) void conv_fwd16_pool(GemmArgs g, Geom G, int l
 // is staged in LDS once (pixel stride CI + 4 floats: conflict-free ds_read_b128 fragments) and every tap's A
 // fragments are read from it at the tap's offset — the 25x im2col expansion is never re-read from L2. The weights
 // stream through a double-buffered early-store B stage, one (tap, 32-channel) k tile per iteration; the epilogue
-// (pool + RMSNorm + SiLU) is conv_fwd16_pool's. Wave w owns tile pixels 32w..32w+31 (TM = 2) x all BN channels.
-template <int BN, int CI, int LW, int KS>
+// (pool + RMSNorm + SiLU) is conv_fwd16_pool's, staged in the patch area. Wave w owns tile pixels 32w..32w+31
+// (TM = 2) x all BN channels. A workgroup runs TPW vertically adjacent tiles (XCD-aware order: an XCD's workgroups
+// cover a contiguous tile range, so the KS - 1 halo rows adjacent tiles share are L2 hits), loading the next tile's
+// patch into registers under the current tile's MFMAs.
+template <int BN, int CI, int LW, int KS, int TPW>
 __global__ __launch_bounds__(256) void conv_fwd_direct_pool(GemmArgs g, Geom G, int lhw, const float* nw,
                                                             float* pooled, uint8_t* amax, float* y, float* rstd,
                                                             float eps, int nchw_flat) {
@@ -423,46 +426,29 @@ __global__ __launch_bounds__(256) void conv_fwd_direct_pool(GemmArgs g, Geom G, 
   constexpr int PH = R + KS - 1, PW = W + KS - 1, CSI = CI + 4, PAD = KS / 2;
   constexpr int PATCH = PH * PW * CSI, SB = BN * LDS_ROW;
   constexpr int NQ = PH * PW * (CI / 4), NQT = (NQ + 255) / 256;
+  constexpr int NK = KS * KS * (CI / BK);
   static_assert(CI % 32 == 0 && (CSI / 4) % 2 == 1, "32-channel k tiles, odd float4 pixel stride");
   static_assert(BM * (BN + 1) <= PATCH, "epilogue tile fits the patch area");
   float* smem = sd_smem<PATCH + 2 * SB>();
   float* patch = smem;
   float* bst = smem + PATCH;
-  // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs, so XCD x gets the contiguous tile range
-  // x * (tiles / 8) ...; vertically adjacent tiles (which share KS - 1 halo rows) then meet in the same L2
-  const int nt = gridDim.x, tile = (nt & 7) ? blockIdx.x : (blockIdx.x & 7) * (nt >> 3) + (blockIdx.x >> 3);
-  const int bm0 = tile * BM;
-  const int n = bm0 >> lhw, y0 = (bm0 & ((1 << lhw) - 1)) >> LW;
+  const int nwg = gridDim.x, ntiles = g.M / BM;
+  const int wg = (nwg & 7) ? blockIdx.x : (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
-  DenseKCB<BN> lb(g.B, g.ldb, g.N, 0);
-  lb.load(0, g.K);
-  {  // the input patch, zero outside the image (range-checked buffer loads), all loads issued before the stores
-    const sd_rsrc rs = sd_make_rsrc(G.in, (long)G.Nb * G.Hs * G.Ws * CI * 4);
-    f32x4 v[NQT];
+  const sd_rsrc rs = sd_make_rsrc(G.in, (long)G.Nb * G.Hs * G.Ws * CI * 4);
+  f32x4 v[NQT];
+  auto load_patch = [&](int tile) {  // zero outside the image (range-checked buffer loads)
+    const int bm0 = tile * BM, n = bm0 >> lhw, y0 = (bm0 & ((1 << lhw) - 1)) >> LW;
 #pragma unroll
     for (int u = 0; u < NQT; ++u) {
       const int i = threadIdx.x + 256 * u;
       const int pix = i / (CI / 4), c4 = i % (CI / 4);
       const int py = pix / PW, px = pix % PW;
       const int yy = y0 + py - PAD, xx = px - PAD;
-      const bool ok = i < NQ && (unsigned)yy < (unsigned)G.Hs && (unsigned)xx < (unsigned)W;
+      const bool ok = i < NQ && tile < ntiles && (unsigned)yy < (unsigned)G.Hs && (unsigned)xx < (unsigned)W;
       v[u] = sd_bload4(rs, ok ? (uint32_t)((((n * G.Hs + yy) * W + xx) * CI + 4 * c4) * 4) : SD_OOB);
     }
-#pragma unroll
-    for (int u = 0; u < NQT; ++u) {
-      const int i = threadIdx.x + 256 * u;
-      if ((u + 1) * 256 <= NQ || i < NQ)
-        *reinterpret_cast<f32x4*>(patch + (i / (CI / 4)) * CSI + 4 * (i % (CI / 4))) = v[u];
-    }
-  }
-  lb.store(bst);
-  lb.load(BK, g.K);
-  __syncthreads();
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
   // fragment base of tile pixel p = 32w + 16i + l16 (row p >> LW, column p & (W - 1)) at tap (0, 0)
   int abase[TM];
 #pragma unroll
@@ -470,39 +456,141 @@ __global__ __launch_bounds__(256) void conv_fwd_direct_pool(GemmArgs g, Geom G, 
     const int p = wave * WM + 16 * i + l16;
     abase[i] = ((p >> LW) * PW + (p & (W - 1))) * CSI + 8 * q;
   }
-  constexpr int NK = KS * KS * (CI / BK);
-  for (int kt = 0; kt < NK; ++kt) {
-    const float* cur = bst + (kt & 1) * SB;
-    float* nxt = bst + ((kt & 1) ^ 1) * SB;
-    const int tap = kt / (CI / BK), ci0 = (kt % (CI / BK)) * BK;
-    const int toff = ((tap / KS) * PW + tap % KS) * CSI + ci0;
-    float af[TM][8], bf[TN][8];
+  DenseKCB<BN> lb(g.B, g.ldb, g.N, 0);
+  load_patch(wg * TPW);
+  for (int it = 0; it < TPW; ++it) {
+    const int tile = wg * TPW + it;
+    if (tile >= ntiles) break;  // uniform over the workgroup
+    if (it > 0) __syncthreads();  // the previous tile's epilogue is done with the patch area
+    lb.load(0, g.K);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float* pa = patch + abase[i] + toff;
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(pa), x1 = *reinterpret_cast<const f32x4*>(pa + 4);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) { af[i][s] = x0[s]; af[i][4 + s] = x1[s]; }
+    for (int u = 0; u < NQT; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      if ((u + 1) * 256 <= NQ || i < NQ)
+        *reinterpret_cast<f32x4*>(patch + (i / (CI / 4)) * CSI + 4 * (i % (CI / 4))) = v[u];
     }
+    lb.store(bst);
+    lb.load(BK, g.K);
+    __syncthreads();
+    if (it + 1 < TPW) load_patch(tile + 1);
+    f32x4 acc[TM][TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float* pb = cur + (16 * j + l16) * LDS_ROW + 8 * q;
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(pb), x1 = *reinterpret_cast<const f32x4*>(pb + 4);
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) { bf[j][s] = x0[s]; bf[j][4 + s] = x1[s]; }
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < NK; ++kt) {
+      const float* cur = bst + (kt & 1) * SB;
+      float* nxt = bst + ((kt & 1) ^ 1) * SB;
+      const int tap = kt / (CI / BK), ci0 = (kt % (CI / BK)) * BK;
+      const int toff = ((tap / KS) * PW + tap % KS) * CSI + ci0;
+      float af[TM][8], bf[TN][8];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float* pa = patch + abase[i] + toff;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(pa), x1 = *reinterpret_cast<const f32x4*>(pa + 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) { af[i][s] = x0[s]; af[i][4 + s] = x1[s]; }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float* pb = cur + (16 * j + l16) * LDS_ROW + 8 * q;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(pb), x1 = *reinterpret_cast<const f32x4*>(pb + 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) { bf[j][s] = x0[s]; bf[j][4 + s] = x1[s]; }
+      }
+      lb.store(nxt);
+      lb.load((kt + 2 < NK ? kt + 2 : NK - 1) * BK, g.K);
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+      __syncthreads();
     }
-    lb.store(nxt);
-    lb.load((kt + 2 < NK ? kt + 2 : NK - 1) * BK, g.K);
+    pool_epilogue<BN, WM>(acc, patch, g, G, LW, lhw, tile * BM, nw, pooled, amax, y, rstd, eps, nchw_flat);
+  }
+}
+
+// Direct forward for the 4-channel (padded RGB) first stage: K = 25 taps x 4 channels, so one
+// v_mfma_f32_16x16x4_f32 step is exactly one tap (lane (l16, q) supplies channel q of pixel l16's tap sample) and
+// nothing is padded to a 32-wide k tile. The whole weight (BN x 100 floats) lives in registers (each lane keeps its
+// 25 x TN fragments, loaded once per workgroup), the (R + KS - 1) x (W + KS - 1) x 4 input patch in LDS (one
+// float4 per pixel: the b32 fragment reads of 64 lanes hit 64 distinct banks). A workgroup runs TPW vertically
+// adjacent tiles (XCD-aware: an XCD's workgroups cover a contiguous tile range), prefetching the next tile's patch
+// into registers under the current tile's MFMAs; the epilogue is conv_fwd16_pool's, in its own LDS area.
+template <int BN, int LW, int KS, int TPW>
+__global__ __launch_bounds__(256) void conv_fwd_direct_pool_c4(GemmArgs g, Geom G, int lhw, const float* nw,
+                                                               float* pooled, uint8_t* amax, float* y, float* rstd,
+                                                               float eps, int nchw_flat) {
+  constexpr int BM = 128, WM = 32, TM = WM / 16, TN = BN / 16, W = 1 << LW, R = BM / W;
+  constexpr int PH = R + KS - 1, PW = W + KS - 1, PAD = KS / 2, NT = KS * KS;
+  constexpr int NQ = PH * PW, NQT = (NQ + 255) / 256;
+  float* smem = sd_smem<NQ * 4 + BM * (BN + 1)>();
+  float* patch = smem;
+  float* C = smem + NQ * 4;
+  const int nwg = gridDim.x, ntiles = g.M / BM;
+  const int wg = (nwg & 7) ? blockIdx.x : (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+  float bw[NT][TN];
+  {
+    const sd_rsrc rb = sd_make_rsrc(g.B, (long)g.N * g.ldb * 4);
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bw[t][j] = sd_bload1(rb, (uint32_t)(((16 * j + l16) * g.ldb + 4 * t + q) * 4));
+  }
+  const sd_rsrc rs = sd_make_rsrc(G.in, (long)G.Nb * G.Hs * G.Ws * 16);
+  f32x4 v[NQT];
+  auto load_patch = [&](int tile) {
+    const int bm0 = tile * BM, n = bm0 >> lhw, y0 = (bm0 & ((1 << lhw) - 1)) >> LW;
+#pragma unroll
+    for (int u = 0; u < NQT; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      const int py = i / PW, px = i % PW;
+      const int yy = y0 + py - PAD, xx = px - PAD;
+      const bool ok = i < NQ && tile < ntiles && (unsigned)yy < (unsigned)G.Hs && (unsigned)xx < (unsigned)W;
+      v[u] = sd_bload4(rs, ok ? (uint32_t)(((n * G.Hs + yy) * W + xx) * 16) : SD_OOB);
+    }
+  };
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int p = wave * WM + 16 * i + l16;
+    abase[i] = ((p >> LW) * PW + (p & (W - 1))) * 4 + q;
+  }
+  load_patch(wg * TPW);
+  for (int it = 0; it < TPW; ++it) {
+    const int tile = wg * TPW + it;
+    if (tile >= ntiles) break;  // uniform over the workgroup
+#pragma unroll
+    for (int u = 0; u < NQT; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      if ((u + 1) * 256 <= NQ || i < NQ) *reinterpret_cast<f32x4*>(patch + 4 * i) = v[u];
+    }
+    __syncthreads();  // patch staged (and the previous tile's epilogue is past its C reads)
+    if (it + 1 < TPW) load_patch(tile + 1);
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int toff = ((t / KS) * PW + t % KS) * 4;
+      float a[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = patch[abase[i] + toff];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
-    __syncthreads();
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], bw[t][j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();  // every wave is done reading the patch before the next tile's is stored
+    pool_epilogue<BN, WM>(acc, C, g, G, LW, lhw, tile * BM, nw, pooled, amax, y, rstd, eps, nchw_flat);
   }
-  pool_epilogue<BN, WM>(acc, patch, g, G, LW, lhw, bm0, nw, pooled, amax, y, rstd, eps, nchw_flat);
 }
 
 // SDHIP_CONV_DIRECT_FWD (benchmarking knob): 1 (default) = conv_fwd_direct_pool where it applies, 0 = implicit GEMM.
@@ -1242,7 +1330,30 @@ extern "C" int sd_conv2d_fwd_pool(const float* in, const float* w, const float* 
   const bool es = conv_es() && (long)Nb * Hs * Ws * Ci < (1L << 29);  // buffer offsets < 2 GiB
   if (conv_direct_fwd() && es && Co == 48 && Ci == 32 && Ws == 32 && kh == 5 && kw == 5 && pad == 2 &&
       Hs % 4 == 0 && al16(in)) {
-    conv_fwd_direct_pool<48, 32, 5, 5><<<grid, 256, 0, s>>>(g, G, lhw, nw, pooled, amax, y, rstd, eps, nchw_flat);
+    const char* e = getenv("SDHIP_C32_TPW");
+    const int tpw = e ? atoi(e) : 1;
+#define SD_C32(TPW)                                                                                                \
+  conv_fwd_direct_pool<48, 32, 5, 5, TPW><<<sd_cdiv(g.M / 128, TPW), 256, 0, s>>>(g, G, lhw, nw, pooled, amax, y, \
+                                                                                 rstd, eps, nchw_flat)
+    if (tpw == 4) SD_C32(4);
+    else if (tpw == 1) SD_C32(1);
+    else SD_C32(2);
+#undef SD_C32
+    SD_LAUNCH_CHECK();
+    return SD_OK;
+  }
+  if (conv_direct_fwd() && es && Co == 32 && Ci == 4 && Ws == 64 && kh == 5 && kw == 5 && pad == 2 &&
+      Hs % 2 == 0 && al16(in)) {
+    const char* e = getenv("SDHIP_C4_TPW");
+    const int tpw = e ? atoi(e) : 16;
+#define SD_C4(TPW)                                                                                                \
+  conv_fwd_direct_pool_c4<32, 6, 5, TPW><<<sd_cdiv(g.M / 128, TPW), 256, 0, s>>>(g, G, lhw, nw, pooled, amax, y, \
+                                                                               rstd, eps, nchw_flat)
+    if (tpw == 16) SD_C4(16);
+    else if (tpw == 8) SD_C4(8);
+    else if (tpw == 2) SD_C4(2);
+    else SD_C4(4);
+#undef SD_C4
     SD_LAUNCH_CHECK();
     return SD_OK;
   }

@@ -230,8 +230,10 @@ def test_conv_pool_norm(ci, co, hw, nb):
 @pytest.mark.parametrize("ci,co,hw,nb,nchw", [(4, 32, 64, 2, False), (32, 48, 32, 4, True), (48, 64, 16, 8, False),
                                              (64, 16, 8, 16, True), (16, 64, 8, 2, True)])
 def test_conv_pool_fused_matches_two_launches(ci, co, hw, nb, nchw):
-    """sd_conv2d_fwd_pool vs sd_conv2d_fwd + sd_pool_rms_fwd: same conv main loop, so the pooled values and argmax are
-    bit-exact; rstd / y differ only in the channel-sum order (1e-6 relative)."""
+    """sd_conv2d_fwd_pool vs sd_conv2d_fwd + sd_pool_rms_fwd: same k order (the implicit-GEMM kernels and the stage-2
+    direct kernel), so the pooled values and argmax are bit-exact; rstd / y differ only in the channel-sum order
+    (1e-6 relative). The 4-channel direct kernel (stage 1) contracts one tap per MFMA step instead of the 32-wide
+    k tiles' interleave: pooled within 1e-6, argmax equal except on near-ties."""
     from sdreamer import kernels as K
     x = (torch.rand(nb, hw, hw, ci, generator=_g(ci)) - 0.5).to(DEV)
     w = (torch.randn(co, 5, 5, ci, generator=_g(co)) / (ci * 25) ** 0.5).to(DEV)
@@ -241,10 +243,11 @@ def test_conv_pool_fused_matches_two_launches(ci, co, hw, nb, nchw):
     fused = K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)
     assert fused is not None, "shape should take the fused kernel"
     ref = K.pool_rms_fwd(K.conv2d_fwd(x, w, b), nw, nchw_flat=nchw)
+    exact_order = ci != 4
     for a, r, what in zip(fused, ref, ("y", "pooled", "amax", "rstd")):
         if what == "amax":
-            assert torch.equal(a, r), what
-        elif what == "pooled":
+            assert torch.equal(a, r) if exact_order else (a == r).float().mean().item() > 0.999, what
+        elif what == "pooled" and exact_order:
             assert torch.equal(a.isnan(), r.isnan()) and torch.equal(a.nan_to_num(), r.nan_to_num()), what
         else:
             assert torch.equal(a.isnan(), r.isnan()), what
