@@ -418,17 +418,18 @@ class Dreamer(nn.Module):
 
             main: P (encoder, scan fwd) ─┬─ M1 (world-model heads, replay-value fwd) ─ wait(S1) ─ R (replay-value
                                          │   loss + bwd) ─┬─ M2 (posterior bwd) ─ wait(S2) ─ [grad all-reduce] ─ M3
-            side:                        └─ S1 (imagination, heads, returns) ─ wait(R) ─ S2 (actor / critic)
+            side:                        └─ S1 (imagination, heads, λ-returns) ─ wait(R) ─ S2 (ReturnEMA, actor /
+                                                                                                 critic)
 
         One graph per stream phase keeps every graph linear: the HIP runtime launches a linear graph as a batch
         (~0.5 ms of host time for the whole update) and the cross-stream edges become device-side event waits.
         A single two-stream graph instead costs ~12 ms of host time per launch, stalling on each cross-stream
         edge. Every graph has its own memory pool; tensors that cross phases are held by `self._gst`.
 
-        Data parallel: a phase that exchanges data (Barlow statistics in M1, the returns gather in S1) is a chain
-        graph → collective → graph (parallel.PhaseGraph); the collectives are issued eagerly on the phase's stream,
-        in the same order on every rank: M1's before S1's, so RCCL's single stream never queues the world-model
-        branch behind the imagination. The gradient arena is sum-all-reduced between the joins and M3 (which
+        Data parallel: a phase that exchanges data (Barlow statistics in M1, the returns gather for the global
+        ReturnEMA in S2) is a chain graph → collective → graph (parallel.PhaseGraph); the collectives are issued
+        eagerly on the phase's stream, in the same host order on every rank (M1's, then S2's after the R phase's
+        launch), so RCCL's single stream never queues the world-model branch behind the actor-critic branch. The gradient arena is sum-all-reduced between the joins and M3 (which
         scales it by 1/world before AGC + LaProp)."""
         if self._graph is None:
             self._g_in = {k: v.clone() for k, v in data.items()}
@@ -453,7 +454,7 @@ class Dreamer(nn.Module):
             gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
             gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st), main_cap)
             torch.cuda.synchronize()
-            for g in (gP, gR, gM2a, gM2b, gS2, gM3):
+            for g in (gP, gR, gM2a, gM2b, gM3):
                 if g.n_collectives:
                     raise RuntimeError("unexpected exchange step in a single-graph phase")
             self._graph = (gP, gS1, gM1, gR, gM2a, gM2b, gS2, gM3)
@@ -629,7 +630,8 @@ class Dreamer(nn.Module):
         self._mark("encoder_bwd")
 
     def _ph_side_ac(self, st):
-        """side: policy / value losses on the imagined trajectories and their backward."""
+        """side: ReturnEMA + advantage, policy / value losses on the imagined trajectories and their backward."""
+        self._returns_norm(st["rr"])
         st["ac_losses"], st["ac_metrics"] = self._ac_losses(st["ifeat"], st["iact"], st["rr"])
         with torch.no_grad():  # replay-value statistics (dreamer.py:649-651), off the main stream's critical path
             st["ac_metrics"].update(_tstats(st["rret"], "ret_replay"))
@@ -798,8 +800,9 @@ class Dreamer(nn.Module):
 
     @torch.no_grad()
     def _heads_returns(self, ifeat):
-        """Imagined reward / continue / value / slow-value heads (dreamer.py:598-622), lambda-returns, ReturnEMA and
-        the advantage (dreamer.py:623-636)."""
+        """Imagined reward / continue / value / slow-value heads (dreamer.py:598-622) and the lambda-returns. The
+        ReturnEMA quantiles and the advantage (dreamer.py:623-636) are only read by the policy / value losses, so they
+        run at the start of the side stream's actor-critic phase (_returns_norm), off the replay-value path."""
         H1, N = ifeat.shape[:2]
         dev = ifeat.device
         flat = ifeat.reshape(H1 * N, -1)
@@ -816,11 +819,14 @@ class Dreamer(nn.Module):
         weight = torch.empty(N, H1, device=dev)
         ret = K.lambda_return(rew_n, val_n, disc, self.lamb, cont_logit=contl_n, cont_out=i_cont,
                               weight_out=weight)  # (N, H)
-        ret_all = parallel.gather_returns(ret, self.world)
+        return dict(ret=ret, weight=weight, i_cont=i_cont, i_rew=i_rew, i_val=i_val, i_slow=i_slow, val_n=val_n)
+
+    @torch.no_grad()
+    def _returns_norm(self, rr):
+        """ReturnEMA over every rank's returns (global quantiles, dreamer.py:623-627) and the advantage (628-636)."""
+        ret_all = parallel.gather_returns(rr["ret"], self.world)
         ret_offset, ret_scale = self.return_ema(ret_all)
-        adv = (ret - val_n[:, :-1]) / ret_scale
-        return dict(ret=ret, weight=weight, adv=adv, i_cont=i_cont, i_rew=i_rew, i_val=i_val, i_slow=i_slow,
-                    ret_offset=ret_offset, ret_scale=ret_scale)
+        rr.update(adv=(rr["ret"] - rr["val_n"][:, :-1]) / ret_scale, ret_offset=ret_offset, ret_scale=ret_scale)
 
     def _ac_losses(self, ifeat, iact, rr):
         """Policy and value losses on the imagined trajectories (dreamer.py:653-671) and their backward."""
