@@ -153,6 +153,13 @@ int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db, float* wor
  * slabs > 1): stride-1 convs with Co % 16 == 0 take a direct kernel (dy rows + input patch staged in LDS, no im2col
  * re-reads) whose split is fixed by the library; others use `ksplit` over the im2col implicit GEMM. */
 int sd_conv2d_wgrad_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int ups, int ksplit);
+/* bwd-weight of a pooled ConvEncoder stage from (dpool, argmax) of sd_pool_rms_bwd_compact (the conv gradient is
+ * expanded inside the direct kernel while staging). _slabs: workspace slabs (each Co x (kh*kw*Ci+1) floats), 0 when
+ * the shape is outside the direct kernel (then sd_conv2d_wgrad_pool returns SD_ESHAPE). */
+int sd_conv2d_wgrad_pool_slabs(int Nb, int H, int W, int Ci, int Co, int kh, int kw);
+int sd_conv2d_wgrad_pool(const float* in, const float* dpool, const uint8_t* amax, float* dw_db, float* workspace,
+                         long ws_floats, int Nb, int H, int W, int Ci, int Co, int kh, int kw, int pad,
+                         sd_stream stream);
 /* Split-bf16 (bf16x3, ~1e-5 relative) backward convolutions (csrc/conv.hip, gemm3_core.h). SD_ESHAPE when the
  * shape is outside the kernels (the caller then takes the f32 path). dgrad: same arguments as sd_conv2d_fwd with
  * in = dOut (Ci channels), w = the flipped weight (sd_conv_flip_weight), out = dIn (Co channels), ups = 0.
@@ -184,6 +191,11 @@ int sd_pool_rms_bwd_blocks(int Nb, int H, int W);
 int sd_pool_rms_bwd(const float* pooled, const uint8_t* amax, const float* w, const float* rstd, const float* dy,
                     float* dx, float* dw, float* dw_partial, int Nb, int H, int W, int C, int nchw_flat,
                     int accumulate_dw, sd_stream stream);
+/* Same backward, writing the pooled-resolution gradient dpool (Nb, H/2, W/2, C) instead of scattering it into the
+ * full-resolution (3/4 zero) conv gradient; consumed by sd_conv2d_wgrad_pool together with the forward's argmax. */
+int sd_pool_rms_bwd_compact(const float* pooled, const uint8_t* amax, const float* w, const float* rstd,
+                            const float* dy, float* dpool, float* dw, float* dw_partial, int Nb, int H, int W, int C,
+                            int nchw_flat, int accumulate_dw, sd_stream stream);
 
 /* ---------------------------------------------------------------- optimiser (flat parameter arena)
  * clip_grad_agc_ (agc.py:15-53) + LaProp.step (laprop.py:46-118) + LambdaLR warm-up (dreamer.py:214-225), fused.

@@ -629,7 +629,8 @@ __global__ __launch_bounds__(256) void conv_wgrad16(GemmArgs g, Geom G, int J, i
 // LDS row strides are padded to 16 (mod 64) floats so the 4 lane groups hit distinct banks.
 struct DirectW {
   const float* x;
-  const float* dy;
+  const float* dy;      // (Nb, H, W, Co) conv-output gradient, or (PL) the pooled-resolution gradient (Nb, H/2, W/2, Co)
+  const uint8_t* amax;  // PL: the 2x2 max-pool argmax per pooled element (dy is routed to that window position)
   float* ws;
   int Nb, H, W, Ci, Co, kh, kw, pad, R, lw;  // lw = log2(W)
   int J, PW, PH, SA, CP, blocks;
@@ -640,7 +641,9 @@ SD_DEV int pad16(int c) { return c % 32 == 0 ? c + 16 : c; }
 constexpr int WD_VA = 4, WD_VP = 6;  // max float4 per thread of a staged dy block / input patch
 
 // WS (wave split): for narrow j ranges every wave covers all j blocks over every 8th k step and writes its own slab
-template <int TM, int NBW, bool WS>
+// PL: dy is the max-pool backward's input (pooled resolution + argmax), expanded while it is fetched — the
+// full-resolution conv gradient (3/4 zeros) is never written to or read from HBM.
+template <int TM, int NBW, bool WS, bool PL = false>
 __global__ __launch_bounds__(512) void conv_wgrad_direct(DirectW d) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -667,6 +670,7 @@ __global__ __launch_bounds__(512) void conv_wgrad_direct(DirectW d) {
     for (int b = 0; b < NBW; ++b) acc[i][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int rows_per_img = d.H / d.R, cq = d.Ci / 4, nA = P * d.Co / 4, nP = d.PH * d.PW * cq;
   f32x4 ra[WD_VA], rp[WD_VP];
+  uint32_t aa[PL ? WD_VA : 1];
   // global -> registers for row block rb (all loads issued together)
   auto fetch = [&](int rb) {
     const int n = rb / rows_per_img, y0 = (rb - n * rows_per_img) * d.R;
@@ -674,7 +678,17 @@ __global__ __launch_bounds__(512) void conv_wgrad_direct(DirectW d) {
 #pragma unroll
     for (int v = 0; v < WD_VA; ++v) {
       const int i = tid + 512 * v;
-      ra[v] = i < nA ? *reinterpret_cast<const f32x4*>(dsrc + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (PL) {  // item i = (pooled pixel of the block, 4-channel group): raw gradient + argmax bytes
+        ra[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+        aa[v] = 0xffffffffu;
+        if (i < nA / 4) {
+          const long pp = (((long)n * (d.H >> 1) + (y0 >> 1)) * (d.W >> 1)) * d.Co + 4 * i;
+          ra[v] = *reinterpret_cast<const f32x4*>(d.dy + pp);
+          aa[v] = *reinterpret_cast<const uint32_t*>(d.amax + pp);
+        }
+      } else {
+        ra[v] = i < nA ? *reinterpret_cast<const f32x4*>(dsrc + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
 #pragma unroll
     for (int v = 0; v < WD_VP; ++v) {
@@ -694,7 +708,20 @@ __global__ __launch_bounds__(512) void conv_wgrad_direct(DirectW d) {
 #pragma unroll
     for (int v = 0; v < WD_VA; ++v) {
       const int i = tid + 512 * v;
-      if (i < nA) {
+      if constexpr (PL) {  // route the pooled gradient to its argmax position of the 2x2 window, zeros elsewhere
+        if (i < nA / 4) {
+          const int e = 4 * i, pl = e / d.Co, c = e - pl * d.Co;
+          const int hw = d.W >> 1, pr = pl / hw, pc = pl - pr * hw;
+#pragma unroll
+          for (int qd = 0; qd < 4; ++qd) {
+            const int p = (2 * pr + (qd >> 1)) * d.W + 2 * pc + (qd & 1);
+            f32x4 val;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) val[k] = ((aa[v] >> (8 * k)) & 0xffu) == (uint32_t)qd ? ra[v][k] : 0.f;
+            *reinterpret_cast<f32x4*>(dyl + p * d.SA + c) = val;
+          }
+        }
+      } else if (i < nA) {
         const int e = 4 * i, p = e / d.Co, c = e - p * d.Co;
         *reinterpret_cast<f32x4*>(dyl + p * d.SA + c) = ra[v];
       }
@@ -1082,7 +1109,8 @@ __global__ void pool_rms_fwd(const float* __restrict__ x, const float* __restric
   }
 }
 
-template <int T, int VPT>
+// COMPACT: dx is the pooled-resolution gradient (Nb, H/2, W/2, C) for sd_conv2d_wgrad_pool (no window scatter)
+template <int T, int VPT, bool COMPACT = false>
 __global__ void pool_rms_bwd(const float* __restrict__ pooled, const uint8_t* __restrict__ amax,
                              const float* __restrict__ w, const float* __restrict__ rstd, const float* __restrict__ dy,
                              float* __restrict__ dx, float* __restrict__ dw_part, int Nb, int H, int W, int C,
@@ -1125,11 +1153,15 @@ __global__ void pool_rms_bwd(const float* __restrict__ pooled, const uint8_t* __
       const int c = t + j * T;
       if (c < C) {
         const float dp = r * (g[j] - xh[j] * dot);
-        const int bi = amax[pix * C + c];
+        if constexpr (COMPACT) {
+          dx[pix * C + c] = dp;
+        } else {
+          const int bi = amax[pix * C + c];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int yy = 2 * yo + (q >> 1), xx = 2 * xo + (q & 1);
-          dx[(((long)n * H + yy) * W + xx) * C + c] = q == bi ? dp : 0.f;
+          for (int q = 0; q < 4; ++q) {
+            const int yy = 2 * yo + (q >> 1), xx = 2 * xo + (q & 1);
+            dx[(((long)n * H + yy) * W + xx) * C + c] = q == bi ? dp : 0.f;
+          }
         }
       }
     }
@@ -1236,9 +1268,10 @@ bool direct_plan(int Nb, int H, int W, int Ci, int Co, int kh, int kw, int ups, 
 }
 
 int wgrad_direct(const float* in, const float* dout, float* dw_db, float* ws, long ws_floats, int Nb, int H, int W,
-                 int Ci, int Co, int kh, int kw, int pad, int J, int lw, const DirectPlan& pl, hipStream_t s) {
+                 int Ci, int Co, int kh, int kw, int pad, int J, int lw, const DirectPlan& pl, hipStream_t s,
+                 const uint8_t* amax = nullptr) {
   DirectW d;
-  d.x = in; d.dy = dout; d.Nb = Nb; d.H = H; d.W = W; d.Ci = Ci; d.Co = Co; d.kh = kh; d.kw = kw; d.pad = pad;
+  d.x = in; d.dy = dout; d.amax = amax; d.Nb = Nb; d.H = H; d.W = W; d.Ci = Ci; d.Co = Co; d.kh = kh; d.kw = kw; d.pad = pad;
   d.lw = lw; d.J = J; d.R = pl.R;
   d.PW = W + kw - 1; d.PH = d.R + kh - 1;
   d.SA = Co % 32 == 0 ? Co + 16 : Co;
@@ -1250,25 +1283,28 @@ int wgrad_direct(const float* in, const float* dout, float* dw_db, float* ws, lo
   d.ws = ws;
   const dim3 grid(gx, gy);
   const int TM = Co / 16;
-#define SD_WD(TM_, NB_, WS_)                                                                               \
-  if (TM == TM_ && nbw == NB_ && pl.ws == WS_) {                                                           \
+#define SD_WD_PL(TM_, NB_, WS_, PL_)                                                                       \
+  if (TM == TM_ && nbw == NB_ && pl.ws == WS_ && (amax != nullptr) == PL_) {                               \
     static bool raised = false;                                                                            \
     if (!raised && lds > 65536) {                                                                          \
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad_direct<TM_, NB_, WS_>),             \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad_direct<TM_, NB_, WS_, PL_>),        \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)       \
         return SD_EARG;                                                                                    \
       raised = true;                                                                                       \
     }                                                                                                      \
-    conv_wgrad_direct<TM_, NB_, WS_><<<grid, 512, lds, s>>>(d);                                            \
+    conv_wgrad_direct<TM_, NB_, WS_, PL_><<<grid, 512, lds, s>>>(d);                                       \
     launched = true;                                                                                       \
   }
+#define SD_WD(TM_, NB_, WS_) SD_WD_PL(TM_, NB_, WS_, false)
   bool launched = false;
   SD_WD(1, 7, true) SD_WD(2, 7, true) SD_WD(3, 7, true) SD_WD(4, 7, true)
+  SD_WD_PL(1, 7, true, true) SD_WD_PL(2, 7, true, true) SD_WD_PL(3, 7, true, true) SD_WD_PL(4, 7, true, true)
   SD_WD(1, 2, false) SD_WD(1, 4, false) SD_WD(1, 7, false) SD_WD(1, 10, false)
   SD_WD(2, 2, false) SD_WD(2, 4, false) SD_WD(2, 7, false) SD_WD(2, 10, false)
   SD_WD(3, 2, false) SD_WD(3, 4, false) SD_WD(3, 7, false) SD_WD(3, 10, false)
   SD_WD(4, 2, false) SD_WD(4, 4, false) SD_WD(4, 7, false)
 #undef SD_WD
+#undef SD_WD_PL
   if (!launched) return SD_ESHAPE;
   SD_LAUNCH_CHECK();
   const long total = (long)Co * (J + 1);  // fixed-order sum of the row-block slabs (4 waves x unrolled loads)
@@ -1421,6 +1457,25 @@ extern "C" int sd_conv2d_wgrad_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int
   return ksplit < 1 ? 1 : ksplit;
 }
 
+// bwd-weight of a pooled stage straight from the max-pool backward's pooled-resolution gradient + argmax
+// (sd_pool_rms_bwd_compact): the direct f32 kernel expands it while staging. SD_ESHAPE outside the direct plan.
+extern "C" int sd_conv2d_wgrad_pool_slabs(int Nb, int H, int W, int Ci, int Co, int kh, int kw) {
+  DirectPlan pl;
+  if (H % 2 || W % 2 || !direct_plan(Nb, H, W, Ci, Co, kh, kw, 0, pl) || !pl.ws || pl.nbw != 7 || pl.R % 2) return 0;
+  return pl.slabs;
+}
+extern "C" int sd_conv2d_wgrad_pool(const float* in, const float* dpool, const uint8_t* amax, float* dw_db,
+                                    float* workspace, long ws_floats, int Nb, int H, int W, int Ci, int Co, int kh,
+                                    int kw, int pad, sd_stream stream_) {
+  if (Nb <= 0) return SD_OK;
+  DirectPlan pl;
+  if (!sd_conv2d_wgrad_pool_slabs(Nb, H, W, Ci, Co, kh, kw) || !direct_plan(Nb, H, W, Ci, Co, kh, kw, 0, pl))
+    return SD_ESHAPE;
+  if (!al16(dpool) || !al16(in) || Co % 4 || Ci % 4 || !amax) return SD_EARG;
+  return wgrad_direct(in, dpool, dw_db, workspace, ws_floats, Nb, H, W, Ci, Co, kh, kw, pad, kh * kw * Ci,
+                      ilog2_exact(W), pl, (hipStream_t)stream_, amax);
+}
+
 extern "C" int sd_conv_flip_weight(const float* w, float* wf, int Co, int kh, int kw, int Ci, sd_stream s) {
   const long total = (long)Co * kh * kw * Ci;
   flip_weight<<<(int)((total + 255) / 256), 256, 0, (hipStream_t)s>>>(w, wf, Co, kh, kw, Ci);
@@ -1471,6 +1526,22 @@ extern "C" int sd_pool_rms_bwd(const float* pooled, const uint8_t* amax, const f
   SD_POOL_SWITCH(pool_rms_bwd, grid, pooled, amax, w, rstd, dy, dx, dw_partial, Nb, H, W, C, nchw_flat)
   SD_LAUNCH_CHECK();
   // two-pass column sum of the per-block dw partials; its chunk workspace follows them in dw_partial
+  return sd_colsum_ws(dw_partial, dw, grid, C, C, accumulate_dw, dw_partial + (long)grid * C, stream_);
+}
+
+extern "C" int sd_pool_rms_bwd_compact(const float* pooled, const uint8_t* amax, const float* w, const float* rstd,
+                                       const float* dy, float* dpool, float* dw, float* dw_partial, int Nb, int H,
+                                       int W, int C, int nchw_flat, int accumulate_dw, sd_stream stream_) {
+  hipStream_t s = (hipStream_t)stream_;
+  if (C > 128) return SD_ESHAPE;
+  const int grid = sd_pool_rms_bwd_blocks(Nb, H, W);
+  switch (vpt_for(C, 16)) {
+    case 1: pool_rms_bwd<16, 1, true><<<grid, 256, 0, s>>>(pooled, amax, w, rstd, dy, dpool, dw_partial, Nb, H, W, C, nchw_flat); break;
+    case 2: pool_rms_bwd<16, 2, true><<<grid, 256, 0, s>>>(pooled, amax, w, rstd, dy, dpool, dw_partial, Nb, H, W, C, nchw_flat); break;
+    case 4: pool_rms_bwd<16, 4, true><<<grid, 256, 0, s>>>(pooled, amax, w, rstd, dy, dpool, dw_partial, Nb, H, W, C, nchw_flat); break;
+    default: pool_rms_bwd<16, 8, true><<<grid, 256, 0, s>>>(pooled, amax, w, rstd, dy, dpool, dw_partial, Nb, H, W, C, nchw_flat); break;
+  }
+  SD_LAUNCH_CHECK();
   return sd_colsum_ws(dw_partial, dw, grid, C, C, accumulate_dw, dw_partial + (long)grid * C, stream_);
 }
 

@@ -387,6 +387,30 @@ def conv2d_wgrad(x, dout, kh, kw, ups=0, pad=None, fast=True):
     return out
 
 
+def conv2d_wgrad_pool_slabs(x, Co, kh, kw):
+    """> 0 when the pooled-gradient bwd-weight (sd_conv2d_wgrad_pool) handles this stage's shape."""
+    Nb, H, W, Ci = x.shape
+    return nat.fns["sd_conv2d_wgrad_pool_slabs"](Nb, H, W, Ci, Co, kh, kw)
+
+
+def conv2d_wgrad_pool(x, dpool, amax, kh, kw, pad=None):
+    """[dW | db] (Co, kh*kw*Ci + 1) of a pooled stage from the max-pool backward's pooled-resolution gradient and the
+    forward's argmax (the f32 direct kernel expands them while staging; bit-identical to conv2d_wgrad on the
+    expanded gradient)."""
+    Nb, H, W, Ci = x.shape
+    Co = dpool.shape[-1]
+    pad = (kh - 1) // 2 if pad is None else pad
+    J = kh * kw * Ci
+    ks = conv2d_wgrad_pool_slabs(x, Co, kh, kw)
+    if ks <= 0:
+        raise nat.NativeError("sd_conv2d_wgrad_pool: shape outside the direct kernel")
+    out = torch.empty(Co, J + 1, dtype=torch.float32, device=x.device)
+    ws = torch.empty(ks * Co * (J + 1), dtype=torch.float32, device=x.device)
+    nat.call("sd_conv2d_wgrad_pool", p(_c(x)), p(_c(dpool)), p(_c(amax)), p(out), p(ws), ws.numel(), Nb, H, W, Ci, Co,
+             kh, kw, pad, stream())
+    return out
+
+
 def conv_flip_weight(w):
     Co, kh, kw, Ci = w.shape
     wf = torch.empty(Ci, kh, kw, Co, dtype=torch.float32, device=w.device)
@@ -441,6 +465,18 @@ def conv2d_fwd_pool(x, w, b, nw, nchw_flat=False):
     ok = nat.call_shaped("sd_conv2d_fwd_pool", p(_c(x)), p(_c(w)), p(b), p(nw), p(pooled), p(amax), p(y), p(rstd),
                          Nb, H, W, Ci, Co, kh, kw, (kh - 1) // 2, EPS, int(nchw_flat), stream())
     return (y, pooled, amax, rstd) if ok else None
+
+
+def pool_rms_bwd_compact(pooled, amax, w, rstd, dy, dw, nchw_flat=False):
+    """pool_rms_bwd writing the pooled-resolution gradient (Nb, H/2, W/2, C) instead of the scattered conv gradient."""
+    Nb, Ho, Wo, C = pooled.shape
+    H, W = 2 * Ho, 2 * Wo
+    dp = torch.empty_like(pooled)
+    nb = nat.fns["sd_pool_rms_bwd_blocks"](Nb, H, W)
+    part = torch.empty((nb + nat.fns["sd_colsum_chunks"](nb)) * C, dtype=torch.float32, device=pooled.device)
+    nat.call("sd_pool_rms_bwd_compact", p(pooled), p(amax), p(w), p(rstd), p(_c(dy)), p(dp), p(dw), p(part), Nb, H, W,
+             C, int(nchw_flat), 1, stream())
+    return dp
 
 
 def pool_rms_bwd(pooled, amax, w, rstd, dy, H, W, dw, nchw_flat=False):

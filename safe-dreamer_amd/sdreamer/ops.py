@@ -120,6 +120,10 @@ def block_linear(x, wp, b):
 
 
 # ------------------------------------------------------------------------------------------------- conv
+# SDREAMER_POOL_COMPACT=0: first-stage backward through the full-resolution conv gradient (benchmark / test knob)
+POOL_COMPACT = os.environ.get("SDREAMER_POOL_COMPACT", "1") != "0"
+
+
 class ConvPoolNormFn(torch.autograd.Function):
     """One ConvEncoder stage: Conv2dSamePad -> MaxPool2d(2) -> RMSNorm2D -> SiLU (networks.py:201-216), NHWC.
     Forward on the exact f32 MFMA kernels (the posterior samples depend on it); both backward contractions on the
@@ -146,8 +150,15 @@ class ConvPoolNormFn(torch.autograd.Function):
         x, w, b, nw, pooled, amax, rstd = ctx.saved_tensors
         Nb, H, W, _ = x.shape
         Co, kh, kw, Ci = w.shape
-        dconv = k.pool_rms_bwd(pooled, amax, nw, rstd, dy.contiguous(), H, W, grad_buf(nw), nchw_flat=ctx.nchw_flat)
-        dwdb = k.conv2d_wgrad(x, dconv, kh, kw)
+        if not ctx.needs_input_grad[0] and POOL_COMPACT and k.conv2d_wgrad_pool_slabs(x, Co, kh, kw) > 0:
+            # first stage (no input gradient): the bwd-weight kernel expands the pooled gradient + argmax itself, so
+            # the full-resolution conv gradient (3/4 zeros) is never written or read
+            dpool = k.pool_rms_bwd_compact(pooled, amax, nw, rstd, dy.contiguous(), grad_buf(nw), nchw_flat=ctx.nchw_flat)
+            dwdb = k.conv2d_wgrad_pool(x, dpool, amax, kh, kw)
+            dconv = None
+        else:
+            dconv = k.pool_rms_bwd(pooled, amax, nw, rstd, dy.contiguous(), H, W, grad_buf(nw), nchw_flat=ctx.nchw_flat)
+            dwdb = k.conv2d_wgrad(x, dconv, kh, kw)
         Cx = x.shape[-1]
         grad_buf(w).add_(dwdb[:, :-1].reshape(Co, kh, kw, Cx)[..., :Ci])
         grad_buf(b).add_(dwdb[:, -1])

@@ -374,3 +374,32 @@ def test_conv_backward_bf16x3(ci, co, hw, nb):
     assert ((dw - dw_ref).abs() - bound).max().item() <= 0, "wgrad"
     if K.nat.fns["sd_conv2d_wgrad_bf16x3_slabs"](nb, hw, hw, ci, co, 5, 5, 0) > 0:  # the split kernel's range
         assert (dw - dw_ref).abs().max().item() > 0, "wgrad took the f32 path"
+
+
+@pytest.mark.parametrize("ci,co,hw,nb", [(4, 32, 64, 3), (32, 48, 32, 2)])
+def test_first_stage_pooled_wgrad_bit_exact(ci, co, hw, nb):
+    """A stage without input gradient (the encoder's first) takes the compact backward — sd_pool_rms_bwd_compact +
+    sd_conv2d_wgrad_pool, the conv gradient expanded from (pooled gradient, argmax) inside the direct kernel — and
+    must give exactly the weight / bias / norm gradients of the dense path (same values staged, same order)."""
+    from sdreamer import kernels as K
+    from sdreamer import ops
+    x = torch.rand(nb, hw, hw, ci, generator=_g(5)).to(DEV)
+    grads = []
+    for compact in (True, False):
+        w = (torch.randn(co, 5, 5, ci, generator=_g(6)) / (ci * 25) ** 0.5).to(DEV).requires_grad_()
+        b = (0.1 * torch.randn(co, generator=_g(7))).to(DEV).requires_grad_()
+        nw = (1 + 0.1 * torch.randn(co, generator=_g(8))).to(DEV).requires_grad_()
+        ops.POOL_COMPACT = compact
+        try:
+            y = ops.ConvPoolNormFn.apply(x, w, b, nw, False)
+            gy = torch.randn(y.shape, generator=_g(9)).to(DEV)
+            y.backward(gy)
+        finally:
+            ops.POOL_COMPACT = True
+        grads.append((w.grad.clone(), b.grad.clone(), nw.grad.clone()))
+    if K.conv2d_wgrad_pool_slabs(x, co, 5, 5) > 0 and ci == 4:
+        for a, r, what in zip(grads[0], grads[1], ("w", "b", "nw")):
+            assert torch.equal(a, r), what
+    else:
+        for a, r, what in zip(grads[0], grads[1], ("w", "b", "nw")):
+            close(a, r, 2e-5, what)
