@@ -602,7 +602,11 @@ class Dreamer(nn.Module):
         """main (after the returns): replay-value loss (dreamer.py:638-652, attached to the world model through
         feat_r) and its backward."""
         loss, rv_metrics, rret = self._repval_post(st["data"], st["rv"], st["rr"]["ret"])
-        (loss * self._loss_scales["repval"]).backward()
+        # the posterior backward needs only the feat gradient: the value head's weight / bias gradients are queued
+        # and run at the start of the side stream's actor-critic phase (which accumulates into the same head next)
+        st["rv_wgrads"] = []
+        with ops.defer_wgrads(st["rv_wgrads"]):
+            (loss * self._loss_scales["repval"]).backward()
         self._mark("repval_bwd")
         st.update(repval=loss, rv_metrics=rv_metrics, rret=rret)
 
@@ -630,7 +634,9 @@ class Dreamer(nn.Module):
         self._mark("encoder_bwd")
 
     def _ph_side_ac(self, st):
-        """side: ReturnEMA + advantage, policy / value losses on the imagined trajectories and their backward."""
+        """side: the replay-value loss's deferred value-head weight gradients, ReturnEMA + advantage, policy / value
+        losses on the imagined trajectories and their backward."""
+        ops.flush_wgrads(st["rv_wgrads"])
         self._returns_norm(st["rr"])
         st["ac_losses"], st["ac_metrics"] = self._ac_losses(st["ifeat"], st["iact"], st["rr"])
         with torch.no_grad():  # replay-value statistics (dreamer.py:649-651), off the main stream's critical path

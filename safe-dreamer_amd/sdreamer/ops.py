@@ -28,6 +28,39 @@ def _flat(x):
 
 
 # ------------------------------------------------------------------------------------------------- dense layers
+_DEFER = None  # a list while defer_wgrads is active
+
+
+class defer_wgrads:
+    """Within this context LinearFn's backward computes the input gradient immediately and queues its weight / bias
+    gradient contractions in `bucket`; flush_wgrads runs them later, possibly on another stream (the replay-value
+    loss's value-head weight gradients run on the side stream, off the path to the posterior backward)."""
+
+    def __init__(self, bucket):
+        self.bucket = bucket
+
+    def __enter__(self):
+        global _DEFER
+        self.prev, _DEFER = _DEFER, self.bucket
+        return self.bucket
+
+    def __exit__(self, *exc):
+        global _DEFER
+        _DEFER = self.prev
+
+
+def flush_wgrads(bucket):
+    """Run the queued weight-gradient work on the current stream (inputs marked as used by it)."""
+    st = torch.cuda.current_stream()
+    eager = not torch.cuda.is_current_stream_capturing()  # captured phases keep their tensors in the graph pools
+    for fn, tensors in bucket:
+        if eager:
+            for t in tensors:
+                t.record_stream(st)
+        fn()
+    bucket.clear()
+
+
 class LinearFn(torch.autograd.Function):
     """nn.Linear (y = x W^T + b). Gradients on the split-bf16 GEMM (k.gemm fast=True, ~1e-5 relative); the forward
     too when `fast` (imagined-trajectory heads: no sampled index depends on them)."""
@@ -47,10 +80,17 @@ class LinearFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = k.mm(dy2, w, fast=True).view(ctx.in_shape)
-        if w.requires_grad:
-            k.gemm(dy2.t(), x2, grad_buf(w), beta=1.0, fast=True)
-        if b is not None and b.requires_grad:
-            k.colsum(dy2, grad_buf(b), accumulate=True)
+
+        def wgrad():
+            if w.requires_grad:
+                k.gemm(dy2.t(), x2, grad_buf(w), beta=1.0, fast=True)
+            if b is not None and b.requires_grad:
+                k.colsum(dy2, grad_buf(b), accumulate=True)
+
+        if _DEFER is not None:
+            _DEFER.append((wgrad, (dy2, x2)))
+        else:
+            wgrad()
         return dx, None, None, None
 
 
