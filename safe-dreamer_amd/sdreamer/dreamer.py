@@ -414,12 +414,13 @@ class Dreamer(nn.Module):
         return post, keys, mvec
 
     def _update_graphed(self, data, initial, seed, ro):
-        """Replay of the update as seven single-stream phases (captured once) joined by stream events:
+        """Replay of the update as nine single-stream phases (captured once) joined by stream events:
 
             main: P (encoder, scan fwd) ─┬─ M1 (world-model heads, replay-value fwd) ─ wait(S1) ─ R (replay-value
-                                         │   loss + bwd) ─┬─ M2 (posterior bwd) ─ wait(S2) ─ [grad all-reduce] ─ M3
-            side:                        └─ S1 (imagination, heads, λ-returns) ─ wait(R) ─ S2 (ReturnEMA, actor /
-                                                                                                 critic)
+                                         │   loss + bwd) ─┬─ M2a (scan bwd) ─┬─ M2b (encoder bwd) ─ wait(S3)
+                                         │                │                  │    ─ [grad all-reduce] ─ M3
+            side:                        └─ S1 (imagination, heads, λ-returns) ─ wait(R) ─ S2 (value-head weight
+                                                grads, ReturnEMA, actor / critic) ─ wait(M2a) ─ S3 (scan weight grads)
 
         One graph per stream phase keeps every graph linear: the HIP runtime launches a linear graph as a batch
         (~0.5 ms of host time for the whole update) and the cross-stream edges become device-side event waits.
@@ -449,15 +450,16 @@ class Dreamer(nn.Module):
             gS1, _ = cap(lambda: self._ph_side_returns(st), side_cap)
             gM1, _ = cap(lambda: self._ph_wm(st), main_cap)
             gR, _ = cap(lambda: self._ph_repval(st), main_cap)
-            gM2a, _ = cap(lambda: self._ph_scan_bwd(st), main_cap)
+            gM2a, _ = cap(lambda: self._ph_scan_bwd(st, defer=True), main_cap)
+            gS3, _ = cap(lambda: ops.flush_wgrads(st["scan_wgrads"]), side_cap)
             gM2b, _ = cap(lambda: self._ph_encoder_bwd(st), main_cap)
             gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
             gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st), main_cap)
             torch.cuda.synchronize()
-            for g in (gP, gR, gM2a, gM2b, gM3):
+            for g in (gP, gR, gM2a, gS3, gM2b, gM3):
                 if g.n_collectives:
                     raise RuntimeError("unexpected exchange step in a single-graph phase")
-            self._graph = (gP, gS1, gM1, gR, gM2a, gM2b, gS2, gM3)
+            self._graph = (gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS2, gM3)
             self._gst, self._g_post, self._g_keys, self._g_mvec = st, post, keys, mvec
         if data is not None:
             for k, v in data.items():
@@ -468,7 +470,7 @@ class Dreamer(nn.Module):
         if self.rep_loss == "dreamerpro":
             self._ema_updates += 1
             self._proto_gate.fill_(0.0 if self._protos_frozen() else 1.0)
-        gP, gS1, gM1, gR, gM2a, gM2b, gS2, gM3 = self._graph
+        gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS2, gM3 = self._graph
         main = torch.cuda.current_stream()
         side = self._side if self.use_side_stream else main
         gP.replay()
@@ -487,13 +489,16 @@ class Dreamer(nn.Module):
         ev_rep = torch.cuda.Event()
         ev_rep.record()
         gM2a.replay()
+        ev_scan = torch.cuda.Event()
+        ev_scan.record()
         if S2_AFTER_SCAN:
-            ev_rep = torch.cuda.Event()
-            ev_rep.record()
+            ev_rep = ev_scan
         gM2b.replay()
         with torch.cuda.stream(side):
             side.wait_event(ev_rep)
             gS2.replay()
+            side.wait_event(ev_scan)  # S3: the scan's weight gradients, beside the encoder backward
+            gS3.replay()
         if side is not main:
             main.wait_stream(side)
         if self.world > 1:
@@ -614,8 +619,10 @@ class Dreamer(nn.Module):
         self._ph_scan_bwd(st)
         self._ph_encoder_bwd(st)
 
-    def _ph_scan_bwd(self, st):
-        """main: posterior gradient = head-loss leaf grads + replay-value feat grad -> scan backward (to embed)."""
+    def _ph_scan_bwd(self, st, defer=False):
+        """main: posterior gradient = head-loss leaf grads + replay-value feat grad -> scan backward (to embed).
+        defer: the scan's weight-gradient GEMMs are queued in st["scan_wgrads"] (graphed update: they run on the
+        side stream beside the encoder backward, phase S3)."""
         SK = self.rssm.flat_stoch
         leaves = st["leaves"]
         self._mark("repval_wait")
@@ -623,7 +630,13 @@ class Dreamer(nn.Module):
         lg = [l.grad if l.grad is not None else torch.zeros_like(l) for l in leaves]
         g_stoch = lg[0] + g_feat[..., :SK].reshape(leaves[0].shape)
         g_deter = lg[1] + g_feat[..., SK:]
-        torch.autograd.backward([st["post_stoch"], st["post_deter"], st["post_logit"]], [g_stoch, g_deter, lg[2]])
+        st["scan_wgrads"] = []
+        if defer:
+            with ops.defer_wgrads(st["scan_wgrads"]):
+                torch.autograd.backward([st["post_stoch"], st["post_deter"], st["post_logit"]],
+                                        [g_stoch, g_deter, lg[2]])
+        else:
+            torch.autograd.backward([st["post_stoch"], st["post_deter"], st["post_logit"]], [g_stoch, g_deter, lg[2]])
         self._mark("scan_bwd")
 
     def _ph_encoder_bwd(self, st):

@@ -477,28 +477,36 @@ class ObserveScan(torch.autograd.Function):
         M = T * B
         gb = ops.grad_buf
         f = lambda x: x.reshape(M, -1)  # noqa: E731
-        K.gemm(f(dl_all).t(), f(oo), gb(P["Wl"]), beta=1.0, fast=True)
-        K.colsum(f(dl_all), gb(P["bl"]))
-        gWo = gb(P["Wo"])
-        K.gemm(f(d_op).t(), f(deter), gWo[:, :D], beta=1.0, fast=True)
-        K.gemm(f(d_op).t(), emb_t, gWo[:, D:], beta=1.0, fast=True)
-        K.colsum(f(d_op), gb(P["bo"]))
-        d_emb = K.mm(f(d_op), P["Wo"][:, D:], fast=True)  # (M, E) time-major
-        K.gemm(f(d_gates).view(M, G, 3 * Dg).permute(1, 2, 0), f(hh).view(M, G, Dg).permute(1, 0, 2), gb(P["Wg"]),
-               beta=1.0, fast=True)
-        K.colsum(f(d_gates), gb(P["bg"]))
-        gWh = gb(P["Wh"])
-        Ig = gWh.shape[2]
-        K.gemm(f(d_hp).t(), f(xcat), gWh.view(D, Ig)[:, Dg:], beta=1.0, fast=True)
-        K.gemm(f(d_hp).view(M, G, Dg).permute(1, 2, 0), f(h_in).view(M, G, Dg).permute(1, 0, 2), gWh[:, :, :Dg],
-               beta=1.0, fast=True)
-        K.colsum(f(d_hp), gb(P["bh"]))
-        K.gemm(f(d_x0p).t(), f(h_in), gb(P["W0"]), beta=1.0, fast=True)
-        K.colsum(f(d_x0p), gb(P["b0"]))
-        K.gemm(f(d_x1p).t(), f(s_in), gb(P["W1"]), beta=1.0, fast=True)
-        K.colsum(f(d_x1p), gb(P["b1"]))
-        d_x2p = K.rmsnorm_bwd(x2p, P["n2"], r2, f(d_x2), dw=gb(P["n2"]))
-        K.gemm(d_x2p.t(), a_n, gb(P["W2"]), beta=1.0, fast=True)
-        K.colsum(d_x2p, gb(P["b2"]))
+        d_emb = K.mm(f(d_op), P["Wo"][:, D:], fast=True)  # (M, E) time-major: the only output the encoder waits for
+
+        def wgrads():
+            K.gemm(f(dl_all).t(), f(oo), gb(P["Wl"]), beta=1.0, fast=True)
+            K.colsum(f(dl_all), gb(P["bl"]))
+            gWo = gb(P["Wo"])
+            K.gemm(f(d_op).t(), f(deter), gWo[:, :D], beta=1.0, fast=True)
+            K.gemm(f(d_op).t(), emb_t, gWo[:, D:], beta=1.0, fast=True)
+            K.colsum(f(d_op), gb(P["bo"]))
+            K.gemm(f(d_gates).view(M, G, 3 * Dg).permute(1, 2, 0), f(hh).view(M, G, Dg).permute(1, 0, 2),
+                   gb(P["Wg"]), beta=1.0, fast=True)
+            K.colsum(f(d_gates), gb(P["bg"]))
+            gWh = gb(P["Wh"])
+            Ig = gWh.shape[2]
+            K.gemm(f(d_hp).t(), f(xcat), gWh.view(D, Ig)[:, Dg:], beta=1.0, fast=True)
+            K.gemm(f(d_hp).view(M, G, Dg).permute(1, 2, 0), f(h_in).view(M, G, Dg).permute(1, 0, 2), gWh[:, :, :Dg],
+                   beta=1.0, fast=True)
+            K.colsum(f(d_hp), gb(P["bh"]))
+            K.gemm(f(d_x0p).t(), f(h_in), gb(P["W0"]), beta=1.0, fast=True)
+            K.colsum(f(d_x0p), gb(P["b0"]))
+            K.gemm(f(d_x1p).t(), f(s_in), gb(P["W1"]), beta=1.0, fast=True)
+            K.colsum(f(d_x1p), gb(P["b1"]))
+            d_x2p = K.rmsnorm_bwd(x2p, P["n2"], r2, f(d_x2), dw=gb(P["n2"]))
+            K.gemm(d_x2p.t(), a_n, gb(P["W2"]), beta=1.0, fast=True)
+            K.colsum(d_x2p, gb(P["b2"]))
+
+        if ops._DEFER is not None:  # queued (ops.defer_wgrads): the caller runs them on another stream
+            ops._DEFER.append((wgrads, (a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all, d_op, d_gates,
+                                        d_hp, d_x0p, d_x1p, d_x2)))
+        else:
+            wgrads()
         d_embed = d_emb.view(T, B, E).transpose(0, 1).contiguous()
         return d_embed, None, None, None, None, None, None, None, None
