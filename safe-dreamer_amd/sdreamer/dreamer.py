@@ -452,14 +452,16 @@ class Dreamer(nn.Module):
             gR, _ = cap(lambda: self._ph_repval(st), main_cap)
             gM2a, _ = cap(lambda: self._ph_scan_bwd(st, defer=True), main_cap)
             gS3, _ = cap(lambda: ops.flush_wgrads(st["scan_wgrads"]), side_cap)
-            gM2b, _ = cap(lambda: self._ph_encoder_bwd(st), main_cap)
+            gM2b, _ = cap(lambda: self._ph_encoder_bwd_hi(st, defer=True), main_cap)
+            gS4, _ = cap(lambda: ops.flush_wgrads(st["enc_wgrads"]), side_cap)
+            gM2c, _ = cap(lambda: self._ph_encoder_bwd_lo(st), main_cap)
             gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
             gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st), main_cap)
             torch.cuda.synchronize()
-            for g in (gP, gR, gM2a, gS3, gM2b, gM3):
+            for g in (gP, gR, gM2a, gS3, gM2b, gS4, gM2c, gM3):
                 if g.n_collectives:
                     raise RuntimeError("unexpected exchange step in a single-graph phase")
-            self._graph = (gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS2, gM3)
+            self._graph = (gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gS2, gM3)
             self._gst, self._g_post, self._g_keys, self._g_mvec = st, post, keys, mvec
         if data is not None:
             for k, v in data.items():
@@ -470,7 +472,7 @@ class Dreamer(nn.Module):
         if self.rep_loss == "dreamerpro":
             self._ema_updates += 1
             self._proto_gate.fill_(0.0 if self._protos_frozen() else 1.0)
-        gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS2, gM3 = self._graph
+        gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gS2, gM3 = self._graph
         main = torch.cuda.current_stream()
         side = self._side if self.use_side_stream else main
         gP.replay()
@@ -494,11 +496,16 @@ class Dreamer(nn.Module):
         if S2_AFTER_SCAN:
             ev_rep = ev_scan
         gM2b.replay()
+        ev_enc = torch.cuda.Event()
+        ev_enc.record()
+        gM2c.replay()
         with torch.cuda.stream(side):
             side.wait_event(ev_rep)
             gS2.replay()
             side.wait_event(ev_scan)  # S3: the scan's weight gradients, beside the encoder backward
             gS3.replay()
+            side.wait_event(ev_enc)  # S4: encoder stages 2..'s weight gradients, beside the first stage's backward
+            gS4.replay()
         if side is not main:
             main.wait_stream(side)
         if self.world > 1:
@@ -565,7 +572,8 @@ class Dreamer(nn.Module):
         """main: encoder + posterior scan (dreamer.py:453-470); detached leaves for the two branches."""
         mk = self._mark
         mk("start")
-        embed = self.encoder(data)
+        split = []  # the first encoder stage is backpropagated separately (_ph_encoder_bwd_lo)
+        embed = self.encoder(data, split=split)
         mk("encoder_fwd")
         # the scan sees a leaf copy of embed: its backward stops there, so scan and encoder backward are separate
         # phases (_ph_scan_bwd / _ph_encoder_bwd)
@@ -576,7 +584,8 @@ class Dreamer(nn.Module):
         leaves = [t.detach().requires_grad_(True) for t in (post_stoch, post_deter, post_logit)]
         feat_l = self.rssm.get_feat(leaves[0], leaves[1])
         feat_r = feat_l.detach().requires_grad_(True)  # replay-value leaf (side stream)
-        return dict(data=data, initial=initial, seed=seed, ro=ro, embed=embed, embed_l=embed_l, post_stoch=post_stoch,
+        return dict(data=data, initial=initial, seed=seed, ro=ro, embed=embed, embed_l=embed_l,
+                    enc_split=split[0] if split else None, post_stoch=post_stoch,
                     post_deter=post_deter, post_logit=post_logit, leaves=leaves, feat_l=feat_l, feat_r=feat_r)
 
     def _ph_side_returns(self, st):
@@ -641,9 +650,27 @@ class Dreamer(nn.Module):
 
     def _ph_encoder_bwd(self, st):
         """main: encoder backward from the scan's embed gradient."""
+        self._ph_encoder_bwd_hi(st)
+        self._ph_encoder_bwd_lo(st)
+
+    def _ph_encoder_bwd_hi(self, st, defer=False):
+        """main: encoder stages 2.. backward (the data-gradient chain) down to the first stage's output leaf.
+        defer: their bwd-weight contractions are queued in st["enc_wgrads"] (graphed update: side phase S4, beside
+        the first stage's backward)."""
         g = st["embed_l"].grad
+        st["enc_wgrads"] = []
         if g is not None:
-            st["embed"].backward(g)
+            if defer:
+                with ops.defer_wgrads(st["enc_wgrads"]):
+                    st["embed"].backward(g)
+            else:
+                st["embed"].backward(g)
+
+    def _ph_encoder_bwd_lo(self, st):
+        """main: the first encoder stage's backward (weight gradients only)."""
+        sp = st["enc_split"]
+        if sp is not None and sp[1].grad is not None:
+            sp[0].backward(sp[1].grad)
         self._mark("encoder_bwd")
 
     def _ph_side_ac(self, st):

@@ -211,12 +211,18 @@ class ConvEncoder(nn.Module):
         self.layers = nn.Sequential(*layers)
         self.out_dim = self.depths[-1] * h * w
 
-    def forward(self, obs):
+    def forward(self, obs, split=None):
+        """split (a list): the first stage's output is continued as a detached leaf and (output, leaf) appended, so
+        the backward runs as two calls (stages 2.. down to the leaf, then the first stage)."""
         x = obs
         n = len(self.depths)
         for i in range(n):
             conv, norm = self.layers[4 * i], self.layers[4 * i + 2]
             x = ops.ConvPoolNormFn.apply(x, conv.weight, conv.bias, norm.weight, i == n - 1)
+            if i == 0 and n > 1 and split is not None and x.requires_grad:
+                leaf = x.detach().requires_grad_(True)
+                split.append((x, leaf))
+                x = leaf
         return x
 
 
@@ -246,8 +252,9 @@ class MultiEncoder(nn.Module):
             raise NotImplementedError
         self.encoders = nn.ModuleList(encs)
 
-    def forward(self, obs):
-        """obs: dict of (B, T, *); images already float in [0, 1] (after preprocess). Returns (B, T, E)."""
+    def forward(self, obs, split=None):
+        """obs: dict of (B, T, *); images already float in [0, 1] (after preprocess). Returns (B, T, E).
+        split: see ConvEncoder.forward."""
         outs = []
         for kind, enc in zip(self.kinds, self.encoders):
             if kind == "cnn":
@@ -258,7 +265,7 @@ class MultiEncoder(nn.Module):
                     x = K.pad_channels(x.contiguous(), (x.shape[-1] + 3) // 4 * 4, 0.5)
                 else:
                     x = x - 0.5  # ConvEncoder.forward, networks.py:224
-                outs.append(enc(x.contiguous()).reshape(*BT, -1))
+                outs.append(enc(x.contiguous(), split).reshape(*BT, -1))
             else:
                 x = torch.cat([obs[k] for k in self.mlp_shapes], -1)
                 outs.append(enc(x))

@@ -198,10 +198,19 @@ class ConvPoolNormFn(torch.autograd.Function):
             dconv = None
         else:
             dconv = k.pool_rms_bwd(pooled, amax, nw, rstd, dy.contiguous(), H, W, grad_buf(nw), nchw_flat=ctx.nchw_flat)
-            dwdb = k.conv2d_wgrad(x, dconv, kh, kw)
+            dwdb = None
         Cx = x.shape[-1]
-        grad_buf(w).add_(dwdb[:, :-1].reshape(Co, kh, kw, Cx)[..., :Ci])
-        grad_buf(b).add_(dwdb[:, -1])
+
+        def wgrad(dwdb=dwdb):
+            if dwdb is None:
+                dwdb = k.conv2d_wgrad(x, dconv, kh, kw)
+            grad_buf(w).add_(dwdb[:, :-1].reshape(Co, kh, kw, Cx)[..., :Ci])
+            grad_buf(b).add_(dwdb[:, -1])
+
+        if _DEFER is not None and dwdb is None:  # queued: only the data gradient continues the backward chain
+            _DEFER.append((wgrad, (x, dconv)))
+        else:
+            wgrad()
         dx = None
         if ctx.needs_input_grad[0]:
             if Cx != Ci:
