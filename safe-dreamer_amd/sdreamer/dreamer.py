@@ -414,13 +414,15 @@ class Dreamer(nn.Module):
         return post, keys, mvec
 
     def _update_graphed(self, data, initial, seed, ro):
-        """Replay of the update as nine single-stream phases (captured once) joined by stream events:
+        """Replay of the update as eleven single-stream phases (captured once) joined by stream events:
 
             main: P (encoder, scan fwd) ─┬─ M1 (world-model heads, replay-value fwd) ─ wait(S1) ─ R (replay-value
-                                         │   loss + bwd) ─┬─ M2a (scan bwd) ─┬─ M2b (encoder bwd) ─ wait(S3)
-                                         │                │                  │    ─ [grad all-reduce] ─ M3
+                                         │   loss + bwd) ─┬─ M2a (scan bwd) ─┬─ M2b (encoder stages 2.. bwd) ─┬─ M2c
+                                         │                │                  │                                │  (first
+                                         │                │                  │   stage) ─ wait(side) ─ [grad all-reduce] ─ M3
             side:                        └─ S1 (imagination, heads, λ-returns) ─ wait(R) ─ S2 (value-head weight
                                                 grads, ReturnEMA, actor / critic) ─ wait(M2a) ─ S3 (scan weight grads)
+                                                ─ wait(M2b) ─ S4 (encoder stages 2.. weight grads)
 
         One graph per stream phase keeps every graph linear: the HIP runtime launches a linear graph as a batch
         (~0.5 ms of host time for the whole update) and the cross-stream edges become device-side event waits.
