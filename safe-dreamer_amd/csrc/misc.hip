@@ -59,20 +59,25 @@ __global__ void fill_normal(float* out, long n, uint64_t seed, uint32_t stream, 
   if (i < n) out[i] = sd_normal(seed, stream, step, (uint64_t)(i + offset));
 }
 
-// column mean and unbiased std of x (R x C): two passes over rows, 4 row-partials per column, fixed order
-__global__ void colstats_kernel(const float* __restrict__ x, int R, int C, float* __restrict__ mean,
-                                float* __restrict__ stdv) {
+// column mean and unbiased std of x (R x C): two passes over rows, NP row-partials per column (64 x NP threads per
+// workgroup, so a 1024-row batch is 64 dependent loads per thread, not 256), fixed summation order
+constexpr int CS_NP = 16;
+__global__ __launch_bounds__(64 * CS_NP) void colstats_kernel(const float* __restrict__ x, int R, int C,
+                                                             float* __restrict__ mean, float* __restrict__ stdv) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int part = threadIdx.x >> 6;
-  __shared__ float red[4][64];
+  __shared__ float red[CS_NP][64];
   __shared__ float mu_s[64];
   float s = 0.f;
   if (c < C)
-    for (int r = part; r < R; r += 4) s += x[(long)r * C + c];
+    for (int r = part; r < R; r += CS_NP) s += x[(long)r * C + c];
   red[part][threadIdx.x & 63] = s;
   __syncthreads();
   if (part == 0) {
-    const float mu = (red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]) / (float)R;
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < CS_NP; ++k) t += red[k][threadIdx.x];
+    const float mu = t / (float)R;
     mu_s[threadIdx.x] = mu;
     if (c < C) mean[c] = mu;
   }
@@ -80,14 +85,19 @@ __global__ void colstats_kernel(const float* __restrict__ x, int R, int C, float
   const float mu = mu_s[threadIdx.x & 63];
   float q = 0.f;
   if (c < C)
-    for (int r = part; r < R; r += 4) {
+    for (int r = part; r < R; r += CS_NP) {
       const float d = x[(long)r * C + c] - mu;
       q += d * d;
     }
+  __syncthreads();  // every thread has read mu_s / red from the first pass
   red[part][threadIdx.x & 63] = q;
   __syncthreads();
-  if (part == 0 && c < C)
-    stdv[c] = sqrtf((red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]) / (float)(R - 1));
+  if (part == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < CS_NP; ++k) t += red[k][threadIdx.x];
+    stdv[c] = sqrtf(t / (float)(R - 1));
+  }
 }
 
 __global__ void standardize_kernel(const float* __restrict__ x, const float* __restrict__ mean,
@@ -99,17 +109,19 @@ __global__ void standardize_kernel(const float* __restrict__ x, const float* __r
 }
 
 // dx = (dn - mean_r dn)/s - (x - mu) * A / (s^2 (R-1) sigma),  A = sum_r dn (x - mu),  s = sigma + eps
-__global__ void standardize_bwd_kernel(const float* __restrict__ x, const float* __restrict__ mean,
-                                       const float* __restrict__ stdv, const float* __restrict__ dn,
-                                       float* __restrict__ dx, int R, int C, float eps) {
+__global__ __launch_bounds__(64 * CS_NP) void standardize_bwd_kernel(const float* __restrict__ x,
+                                                                    const float* __restrict__ mean,
+                                                                    const float* __restrict__ stdv,
+                                                                    const float* __restrict__ dn,
+                                                                    float* __restrict__ dx, int R, int C, float eps) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int part = threadIdx.x >> 6;
-  __shared__ float red0[4][64], red1[4][64];
+  __shared__ float red0[CS_NP][64], red1[CS_NP][64];
   __shared__ float mdn[64], aa[64];
   const float mu = c < C ? mean[c] : 0.f;
   float s0 = 0.f, s1 = 0.f;
   if (c < C)
-    for (int r = part; r < R; r += 4) {
+    for (int r = part; r < R; r += CS_NP) {
       const float d = dn[(long)r * C + c];
       s0 += d;
       s1 += d * (x[(long)r * C + c] - mu);
@@ -119,8 +131,11 @@ __global__ void standardize_bwd_kernel(const float* __restrict__ x, const float*
   __syncthreads();
   if (part == 0) {
     const int l = threadIdx.x;
-    mdn[l] = (red0[0][l] + red0[1][l] + red0[2][l] + red0[3][l]) / (float)R;
-    aa[l] = red1[0][l] + red1[1][l] + red1[2][l] + red1[3][l];
+    float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < CS_NP; ++k) { t0 += red0[k][l]; t1 += red1[k][l]; }
+    mdn[l] = t0 / (float)R;
+    aa[l] = t1;
   }
   __syncthreads();
   if (c >= C) return;
@@ -128,7 +143,7 @@ __global__ void standardize_bwd_kernel(const float* __restrict__ x, const float*
   const float sc = sg + eps;
   const float m = mdn[threadIdx.x & 63], A = aa[threadIdx.x & 63];
   const float k2 = A / (sc * sc * (float)(R - 1) * sg);
-  for (int r = part; r < R; r += 4) {
+  for (int r = part; r < R; r += CS_NP) {
     const long o = (long)r * C + c;
     dx[o] = (dn[o] - m) / sc - (x[o] - mu) * k2;
   }
@@ -219,7 +234,7 @@ extern "C" int sd_fill_normal(float* out, long n, uint64_t seed, int stream_id, 
 }
 extern "C" int sd_colstats(const float* x, int R, int C, float* mean, float* stdv, sd_stream s) {
   if (R <= 1 || C <= 0) return SD_EARG;
-  colstats_kernel<<<(C + 63) / 64, 256, 0, (hipStream_t)s>>>(x, R, C, mean, stdv);
+  colstats_kernel<<<(C + 63) / 64, 64 * CS_NP, 0, (hipStream_t)s>>>(x, R, C, mean, stdv);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
@@ -233,7 +248,7 @@ extern "C" int sd_standardize(const float* x, const float* mean, const float* st
 extern "C" int sd_standardize_bwd(const float* x, const float* mean, const float* stdv, const float* dn, float* dx,
                                   int R, int C, float eps, sd_stream s) {
   if (R <= 1) return SD_EARG;
-  standardize_bwd_kernel<<<(C + 63) / 64, 256, 0, (hipStream_t)s>>>(x, mean, stdv, dn, dx, R, C, eps);
+  standardize_bwd_kernel<<<(C + 63) / 64, 64 * CS_NP, 0, (hipStream_t)s>>>(x, mean, stdv, dn, dx, R, C, eps);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
