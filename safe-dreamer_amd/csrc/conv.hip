@@ -1246,15 +1246,30 @@ int patch_stride(int Ci) {  // >= Ci + 2 (ones / zero channels), % 4 == 0, 16 or
   return c;
 }
 
-bool direct_plan(int Nb, int H, int W, int Ci, int Co, int kh, int kw, int ups, DirectPlan& pl) {
+// pixels per staged row block of the max-pool-fused f32 direct bwd-weight (encoder first stage): more pixels per
+// block = more MFMA steps per barrier (128 -> 256 px: 397 -> 337 us at 1024 images); SDHIP_WGRAD_PIX overrides
+int wgrad_pool_pix() {
+  static int a = -1;
+  if (a < 0) {
+    const char* e = getenv("SDHIP_WGRAD_PIX");
+    a = e ? atoi(e) : 512;
+    if (a < 1) a = 512;
+  }
+  return a;
+}
+
+// pool_pix > 0: dy arrives at pooled resolution (a quarter of the block's pixels are fetched), blocks of pool_pix px
+bool direct_plan(int Nb, int H, int W, int Ci, int Co, int kh, int kw, int ups, DirectPlan& pl, int pool_pix = 0) {
+  const bool pool = pool_pix > 0;
   if (conv_algo() != 0 || ups != 0 || Co % 16 || Co > 64 || Ci % 4 || ilog2_exact(W) < 0) return false;
-  pl.R = W >= 128 ? 1 : (128 / W < H ? 128 / W : H);
+  const int pix = pool ? pool_pix : 128;
+  pl.R = W >= pix ? 1 : (pix / W < H ? pix / W : H);
   if (H % pl.R || (pl.R * W) % 4) return false;
   const int SA = Co % 32 == 0 ? Co + 16 : Co, CP = patch_stride(Ci);
   const int PH = pl.R + kh - 1, PW = W + kw - 1;
   pl.lds = ((size_t)pl.R * W * SA + (size_t)PH * PW * CP) * 4;
   if (pl.lds > 160 * 1024) return false;
-  if (pl.R * W * Co / 4 > WD_VA * 512 || PH * PW * (Ci / 4) > WD_VP * 512) return false;
+  if (pl.R * W * Co / (pool ? 16 : 4) > WD_VA * 512 || PH * PW * (Ci / 4) > WD_VP * 512) return false;
   const int J = kh * kw * Ci, JB = (J + 1 + 15) / 16;
   pl.ws = JB <= 7;  // few column blocks: split the pixels over the waves instead
   pl.nbw = pl.ws ? 7 : JB <= 16 ? 2 : JB <= 32 ? 4 : JB <= 56 ? 7 : (Co <= 48 ? 10 : 7);
@@ -1457,11 +1472,18 @@ extern "C" int sd_conv2d_wgrad_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int
   return ksplit < 1 ? 1 : ksplit;
 }
 
+// the pooled plan at the largest block (<= wgrad_pool_pix()) whose staging fits
+static bool pool_plan(int Nb, int H, int W, int Ci, int Co, int kh, int kw, DirectPlan& pl) {
+  if (H % 2 || W % 2) return false;
+  for (int pix = wgrad_pool_pix(); pix >= 128; pix /= 2)
+    if (direct_plan(Nb, H, W, Ci, Co, kh, kw, 0, pl, pix) && pl.ws && pl.nbw == 7 && pl.R % 2 == 0) return true;
+  return false;
+}
 // bwd-weight of a pooled stage straight from the max-pool backward's pooled-resolution gradient + argmax
 // (sd_pool_rms_bwd_compact): the direct f32 kernel expands it while staging. SD_ESHAPE outside the direct plan.
 extern "C" int sd_conv2d_wgrad_pool_slabs(int Nb, int H, int W, int Ci, int Co, int kh, int kw) {
   DirectPlan pl;
-  if (H % 2 || W % 2 || !direct_plan(Nb, H, W, Ci, Co, kh, kw, 0, pl) || !pl.ws || pl.nbw != 7 || pl.R % 2) return 0;
+  if (!pool_plan(Nb, H, W, Ci, Co, kh, kw, pl)) return 0;
   return pl.slabs;
 }
 extern "C" int sd_conv2d_wgrad_pool(const float* in, const float* dpool, const uint8_t* amax, float* dw_db,
@@ -1469,7 +1491,7 @@ extern "C" int sd_conv2d_wgrad_pool(const float* in, const float* dpool, const u
                                     int kw, int pad, sd_stream stream_) {
   if (Nb <= 0) return SD_OK;
   DirectPlan pl;
-  if (!sd_conv2d_wgrad_pool_slabs(Nb, H, W, Ci, Co, kh, kw) || !direct_plan(Nb, H, W, Ci, Co, kh, kw, 0, pl))
+  if (!pool_plan(Nb, H, W, Ci, Co, kh, kw, pl))
     return SD_ESHAPE;
   if (!al16(dpool) || !al16(in) || Co % 4 || Ci % 4 || !amax) return SD_EARG;
   return wgrad_direct(in, dpool, dw_db, workspace, ws_floats, Nb, H, W, Ci, Co, kh, kw, pad, kh * kw * Ci,

@@ -380,7 +380,8 @@ def test_conv_backward_bf16x3(ci, co, hw, nb):
 def test_first_stage_pooled_wgrad_bit_exact(ci, co, hw, nb):
     """A stage without input gradient (the encoder's first) takes the compact backward — sd_pool_rms_bwd_compact +
     sd_conv2d_wgrad_pool, the conv gradient expanded from (pooled gradient, argmax) inside the direct kernel — and
-    must give exactly the weight / bias / norm gradients of the dense path (same values staged, same order)."""
+    must give the dense path's weight / bias / norm gradients: the same values staged, in 512-pixel row blocks (the
+    dense direct kernel stages 128) — so the f32 sums are reordered (close at 2e-5) and the norm gradient is exact."""
     from sdreamer import kernels as K
     from sdreamer import ops
     x = torch.rand(nb, hw, hw, ci, generator=_g(5)).to(DEV)
@@ -398,8 +399,9 @@ def test_first_stage_pooled_wgrad_bit_exact(ci, co, hw, nb):
             ops.POOL_COMPACT = True
         grads.append((w.grad.clone(), b.grad.clone(), nw.grad.clone()))
     if K.conv2d_wgrad_pool_slabs(x, co, 5, 5) > 0 and ci == 4:
-        for a, r, what in zip(grads[0], grads[1], ("w", "b", "nw")):
-            assert torch.equal(a, r), what
+        assert torch.equal(grads[0][2], grads[1][2]), "nw"
+        for a, r, what in zip(grads[0][:2], grads[1][:2], ("w", "b")):
+            close(a, r, 2e-5, what)
     else:
         for a, r, what in zip(grads[0], grads[1], ("w", "b", "nw")):
             close(a, r, 2e-5, what)
