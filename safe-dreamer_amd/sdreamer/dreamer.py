@@ -389,6 +389,11 @@ class Dreamer(nn.Module):
         if self.marks is not None:
             self.marks(tag)
 
+    def _flush(self, wgrads, tag):
+        """side phases S3 / S4: the deferred weight-gradient contractions, then a timeline mark."""
+        ops.flush_wgrads(wgrads)
+        self._mark(tag)
+
     def _core_forward(self, data, initial, seed, ro):
         """Graph phase P (main): preprocess, Polyak, zero_grad, encoder + posterior scan."""
         if self.marks is not None:
@@ -453,9 +458,9 @@ class Dreamer(nn.Module):
             gM1, _ = cap(lambda: self._ph_wm(st), main_cap)
             gR, _ = cap(lambda: self._ph_repval(st), main_cap)
             gM2a, _ = cap(lambda: self._ph_scan_bwd(st, defer=True), main_cap)
-            gS3, _ = cap(lambda: ops.flush_wgrads(st["scan_wgrads"]), side_cap)
+            gS3, _ = cap(lambda: self._flush(st["scan_wgrads"], "side:scan_wgrads"), side_cap)
             gM2b, _ = cap(lambda: self._ph_encoder_bwd_hi(st, defer=True), main_cap)
-            gS4, _ = cap(lambda: ops.flush_wgrads(st["enc_wgrads"]), side_cap)
+            gS4, _ = cap(lambda: self._flush(st["enc_wgrads"], "side:enc_wgrads"), side_cap)
             gM2c, _ = cap(lambda: self._ph_encoder_bwd_lo(st), main_cap)
             gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
             gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st), main_cap)
