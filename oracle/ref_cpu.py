@@ -531,21 +531,28 @@ class Oracle:
         return action, {"stoch": stoch, "deter": deter, "prev_action": action}
 
     @torch.no_grad()
-    def imagine(self, start, horizon, seed, row_offset=0):  # Dreamer._imagine, dreamer.py:673-692
+    def imagine(self, start, horizon, seed, row_offset=0, rec=None):  # Dreamer._imagine, dreamer.py:673-692
+        """rec (tests only): if a dict, collects the per-step actor logits and prior logits (near-tie margins)."""
         P = {k: v.detach() for k, v in self.P.items()}
         stoch, deter = start
         N = deter.shape[0]
         feats, actions = [], []
         for t in range(horizon):
             feat = self.get_feat(stoch, deter)
-            action = self.actor_sample(self.head_logits("actor", feat, P), seed, t, row_offset)
+            alogit = self.head_logits("actor", feat, P)
+            action = self.actor_sample(alogit, seed, t, row_offset)
             feats.append(feat)
             actions.append(action)
+            if rec is not None:
+                rec.setdefault("imag_actor_logit", []).append(alogit)
             if t == horizon - 1:
                 break  # the last img_step's output is discarded by the reference (dreamer.py:688)
             deter = self.deter_step(stoch, deter, action, P)
             g = torch.from_numpy(nz.gumbel_block(seed, nz.STREAM_IMG, t, N, row_offset, self.s.SK))
-            stoch = self.sample_stoch(self.img_logit(deter, P), g.reshape(N, self.s.S, self.s.K))
+            ilogit = self.img_logit(deter, P)
+            stoch = self.sample_stoch(ilogit, g.reshape(N, self.s.S, self.s.K))
+            if rec is not None:
+                rec.setdefault("imag_prior_logit", []).append(ilogit)
         return torch.stack(feats, 1), torch.stack(actions, 1)
 
 
@@ -735,7 +742,8 @@ class OracleAgent:
         # imagination (dreamer.py:578-636)
         start = (post_stoch.reshape(-1, s.S, s.K).detach(), post_deter.reshape(-1, s.D).detach())
         H1 = int(c.imag_horizon) + 1
-        imag_feat, imag_action = M.imagine(start, H1, seed, row_offset * T)
+        rec = {} if keep is not None else None
+        imag_feat, imag_action = M.imagine(start, H1, seed, row_offset * T, rec)
         imag_feat, imag_action = imag_feat.detach(), imag_action.detach()
         imag_reward = twohot_mode(M.head_logits("reward", imag_feat, Pd), M.rbins)
         imag_cont = torch.sigmoid(M.head_logits("cont", imag_feat, Pd).float())  # Bernoulli.mean
@@ -800,7 +808,9 @@ class OracleAgent:
         if keep is not None:
             keep.update(dict(embed=embed, post_logit=post_logit, prior_logit=prior_logit, imag_feat=imag_feat,
                              imag_action=imag_action, ret=ret, imag_value=imag_value, imag_reward=imag_reward,
-                             imag_cont=imag_cont, rret=rret))
+                             imag_cont=imag_cont, rret=rret,
+                             imag_actor_logit=torch.stack(rec["imag_actor_logit"], 1),
+                             imag_prior_logit=torch.stack(rec["imag_prior_logit"], 1)))
         return (post_stoch, post_deter), losses, metrics
 
     @torch.no_grad()

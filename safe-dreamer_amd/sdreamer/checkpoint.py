@@ -4,8 +4,10 @@ File = torch.save of a dict with
   * "agent_state_dict": Dreamer.state_dict() — the reference's keys and shapes, including the `_frozen_*` aliases
     (BlockLinear (O/G, I/G, G), conv (Co, Ci, k, k)); eval.py's `agent.load_state_dict(ckpt["agent_state_dict"])`
     works on either implementation's file;
-  * "optims_state_dict": {"_optimizer": LaProp state} — the path tools.recursively_collect_optim_state_dict
-    (utils/tools.py:298-318) finds for the reference agent, in torch.optim.Optimizer.state_dict() form;
+  * "optims_state_dict": {"_optimizer": LaProp state, "_scheduler.optimizer": the same} — the two paths
+    tools.recursively_collect_optim_state_dict (utils/tools.py:298-318) finds for the reference agent (the optimizer,
+    and again through the LambdaLR's `.optimizer`), in torch.optim.Optimizer.state_dict() form: state index i is
+    Dreamer._named_params[i] (the reference's parameter order, dreamer.py:196-206);
   * "resume" (this implementation only; the reference saves once at the end and cannot resume): update counters
     that drive the LR warm-up, the slow-critic schedule and the per-update noise seed, so a resumed run continues
     the same sequence of updates. Everything in the file is tensors / plain Python values: it loads with
@@ -19,14 +21,22 @@ import torch
 
 
 def collect_optim_state_dict(agent):
-    """tools.recursively_collect_optim_state_dict(agent) for this agent: its one optimizer."""
-    return {"_optimizer": agent._optimizer.state_dict()}
+    """tools.recursively_collect_optim_state_dict(agent) for this agent: its one optimizer, reached twice as in the
+    reference (agent._optimizer and agent._scheduler.optimizer; one state_dict object, so torch.save stores the
+    moments once)."""
+    sd = agent._optimizer.state_dict()
+    return {"_optimizer": sd, "_scheduler.optimizer": sd}
 
 
 def checkpoint_items(agent):
+    seen, osd = {}, {}  # the same optimizer state under two keys: converted once, stored once
+    for k, v in collect_optim_state_dict(agent).items():
+        if id(v) not in seen:
+            seen[id(v)] = _to_cpu(v)
+        osd[k] = seen[id(v)]
     return {
         "agent_state_dict": {k: v.detach().cpu() for k, v in agent.state_dict().items()},
-        "optims_state_dict": {k: _to_cpu(v) for k, v in collect_optim_state_dict(agent).items()},
+        "optims_state_dict": osd,
         "resume": {"updates": int(agent._updates), "slow_value_updates": int(agent._slow_value_updates),
                    "optimizer_host_steps": int(agent._optimizer.host_steps), "seed_base": int(agent._seed_base),
                    "ema_updates": int(getattr(agent, "_ema_updates", 0))},

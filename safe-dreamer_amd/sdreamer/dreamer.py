@@ -146,9 +146,20 @@ class Dreamer(nn.Module):
                 if prm.requires_grad:
                     self._named_params[f"{name}.{pn}"] = prm
         super().to(self.device)
+        # parameters whose internal layout differs from the reference's (BlockLinear, Conv2d weights): how to view a
+        # tensor of that parameter's shape (its gradient, its LaProp moments) in the reference layout and back
+        packed = {}
+        for name, module in modules.items():
+            if isinstance(module, nn.Parameter):
+                continue
+            for mn, m in module.named_modules():
+                if hasattr(m, "weight_to_ref"):
+                    packed[f"{name}.{mn}.weight" if mn else f"{name}.weight"] = (m.weight_to_ref, m.weight_from_ref)
+        self._ref_layouts = [packed.get(n) for n in self._named_params]
         self._optimizer = LaProp(self._named_params.values(), lr=float(config.lr),
                                  betas=(float(config.beta1), float(config.beta2)), eps=float(config.eps),
-                                 agc=float(config.agc), pmin=float(config.pmin), warmup=int(config.warmup or 0))
+                                 agc=float(config.agc), pmin=float(config.pmin), warmup=int(config.warmup or 0),
+                                 ref_layouts=self._ref_layouts)
         self._scheduler = WarmupSchedule(self._optimizer)
         # slow critic arena mirrors the value head's slice of the parameter arena (one Polyak kernel)
         a = self._optimizer.arena
@@ -1029,6 +1040,12 @@ class Dreamer(nn.Module):
     _FROZEN = (("encoder", "_frozen_encoder"), ("rssm", "_frozen_rssm"), ("reward", "_frozen_reward"),
                ("cont", "_frozen_cont"), ("actor", "_frozen_actor"), ("value", "_frozen_value"),
                ("_slow_value", "_frozen_slow_value"))
+
+    def to_ref_layout(self, param, t):
+        """A tensor shaped like trainable parameter `param` (e.g. its .grad), viewed in the reference's layout."""
+        i = [id(p) for p in self._named_params.values()].index(id(param))
+        lay = self._ref_layouts[i]
+        return t if lay is None else lay[0](t)
 
     def state_dict(self, *args, **kwargs):
         sd = super().state_dict(*args, **kwargs)

@@ -73,6 +73,14 @@ class BlockLinear(nn.Module):
     def forward(self, x):
         return ops.block_linear(x, self.weight, self.bias)
 
+    @staticmethod
+    def weight_to_ref(t):  # internal (G, O/G, I/G) -> reference (O/G, I/G, G)
+        return t.permute(1, 2, 0)
+
+    @staticmethod
+    def weight_from_ref(t):
+        return t.permute(2, 0, 1)
+
     def _save_to_state_dict(self, destination, prefix, keep_vars):
         w = self.weight if keep_vars else self.weight.detach()
         destination[prefix + "weight"] = w.permute(1, 2, 0).contiguous()
@@ -96,6 +104,14 @@ class Conv2d(nn.Module):
         _trunc_normal_(w, self.ci * self.k * self.k)
         self.weight = nn.Parameter(w.permute(0, 2, 3, 1).contiguous())
         self.bias = nn.Parameter(torch.zeros(self.co))
+
+    @staticmethod
+    def weight_to_ref(t):  # internal (Co, kh, kw, Ci) -> reference (Co, Ci, kh, kw)
+        return t.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def weight_from_ref(t):
+        return t.permute(0, 2, 3, 1)
 
     def _save_to_state_dict(self, destination, prefix, keep_vars):
         w = self.weight if keep_vars else self.weight.detach()

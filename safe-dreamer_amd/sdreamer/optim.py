@@ -66,8 +66,12 @@ class LaProp(torch.optim.Optimizer):
     """Drop-in for utils/optim/laprop.py's LaProp (amsgrad/centered/weight_decay unsupported, as unused there),
     fused with clip_grad_agc_ and the LambdaLR warm-up of Dreamer (dreamer.py:209-225)."""
 
-    def __init__(self, params, lr=4e-4, betas=(0.9, 0.999), eps=1e-15, agc=0.3, pmin=1e-3, warmup=0, arena=None):
+    def __init__(self, params, lr=4e-4, betas=(0.9, 0.999), eps=1e-15, agc=0.3, pmin=1e-3, warmup=0, arena=None,
+                 ref_layouts=None):
         params = list(params)
+        # per parameter: None, or (to_ref, from_ref) views between the internal and the reference layout, so that
+        # state_dict() holds moments shaped like the reference's parameters (checkpoint interop)
+        self.ref_layouts = list(ref_layouts) if ref_layouts is not None else [None] * len(params)
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False, centered=False))
         self.arena = arena if arena is not None else FlatArena(params, params[0].device)
         dev = self.arena.data.device
@@ -116,9 +120,11 @@ class LaProp(torch.optim.Optimizer):
         for i, (o, n, p) in enumerate(zip(a.offsets, a.sizes, a.params)):
             if steps == 0:
                 continue
-            st[i] = {"step": steps, "exp_avg": self.exp_avg[o:o + n].view(p.shape).clone(),
+            lay = self.ref_layouts[i]
+            view = (lambda t: t) if lay is None else lay[0]
+            st[i] = {"step": steps, "exp_avg": view(self.exp_avg[o:o + n].view(p.shape)).contiguous().clone(),
                      "exp_avg_lr_1": float(sc[1]), "exp_avg_lr_2": float(sc[2]),
-                     "exp_avg_sq": self.exp_avg_sq[o:o + n].view(p.shape).clone()}
+                     "exp_avg_sq": view(self.exp_avg_sq[o:o + n].view(p.shape)).contiguous().clone()}
         lr = self.current_lr()
         groups = [{"lr": lr, "betas": self.betas, "eps": self.eps, "weight_decay": 0, "amsgrad": False,
                    "centered": False, "initial_lr": self.base_lr, "params": list(range(len(a.params)))}]
@@ -132,8 +138,11 @@ class LaProp(torch.optim.Optimizer):
             s = st.get(i, st.get(str(i)))
             if not s:
                 continue
-            self.exp_avg[o:o + n].copy_(s["exp_avg"].reshape(-1))
-            self.exp_avg_sq[o:o + n].copy_(s["exp_avg_sq"].reshape(-1))
+            lay, shape = self.ref_layouts[i], a.params[i].shape
+            for dst, src in ((self.exp_avg, s["exp_avg"]), (self.exp_avg_sq, s["exp_avg_sq"])):
+                if lay is not None:  # state_dict moments are in the reference layout (see state_dict)
+                    src = lay[1](src)
+                dst[o:o + n].view(shape).copy_(src)
             steps, e1, e2 = int(s["step"]), float(s["exp_avg_lr_1"]), float(s["exp_avg_lr_2"])
         self.scalars.copy_(torch.tensor([steps, e1, e2, 0.0][: self.scalars.numel()], dtype=torch.float64))
         self.host_steps = steps

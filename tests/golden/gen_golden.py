@@ -14,6 +14,7 @@ L2 norms + 32 sampled elements; parameters after the LaProp step the same way. T
 so LaProp's lr-EMA state and ReturnEMA carry over.
 """
 import contextlib
+import json
 import os
 import sys
 import zlib
@@ -38,6 +39,8 @@ CASES = {
     # name: (config, overrides, obs shapes, act_dim, discrete, B, T, H)
     "proprio_dreamer": ("dmc/proprio", [], {"position": (3,), "velocity": (2,)}, 1, False, 4, 16, 8),
     "walker_r2": ("dmc/cnn", [], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
+    # no LR warm-up: the first LaProp step is lr = 4e-5 per element (not 4e-8), so parameter deltas are resolvable
+    "walker_r2_nowarm": ("dmc/cnn", ["model.warmup=0"], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
     "walker_infonce": ("dmc/cnn", ["model.rep_loss=infonce"], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
     "walker_r2aug": ("dmc/cnn", ["model.r2dreamer.aug.enabled=True"], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
     "walker_pro": ("dmc/cnn", ["model.rep_loss=dreamerpro"], {"image": (64, 64, 3)}, 6, False, 2, 6, 4),
@@ -167,6 +170,11 @@ def run_case(name, mods, TD):
     assert sorted(ref_train) == sorted(spec.shapes), (set(ref_train) ^ set(spec.shapes))
     for k, v in spec.shapes.items():
         assert tuple(sd[k].shape) == tuple(v), (k, sd[k].shape, v)
+    init_stats = {}
+    for k in spec.shapes:  # the reference's own initialiser (tools.weight_init_ + outscale) under manual_seed(0)
+        w = sd[k].detach().double().reshape(-1)
+        init_stats[f"init_{k}__stat"] = np.array([w.mean().item(), w.std().item() if w.numel() > 1 else 0.0,
+                                                  w.abs().max().item(), float(w.numel())])
     vals = params_for(spec.shapes, PARAM_SEED)
     with torch.no_grad():
         named = dict(ag.named_parameters())
@@ -177,6 +185,7 @@ def run_case(name, mods, TD):
                 v.data.copy_(torch.from_numpy(vals["value." + k[len("_slow_value."):]]))
     out = {"meta_B": B, "meta_T": T, "meta_H": H, "meta_A": A, "meta_discrete": int(discrete),
            "meta_param_seed": PARAM_SEED}
+    out.update(init_stats)
 
     rng = np.random.default_rng(zlib.crc32(name.encode()))
     D.autocast = lambda **k: contextlib.nullcontext()
@@ -278,12 +287,95 @@ def run_case(name, mods, TD):
         st = ag._optimizer.state[named["rssm._img_net.img_net_logit.bias"]]
         out[f"u{u}_laprop_lr1"] = np.asarray(st["exp_avg_lr_1"])
         out[f"u{u}_laprop_lr2"] = np.asarray(st["exp_avg_lr_2"])
+        for k in spec.shapes:  # LaProp moments per parameter (laprop.py:62-70), same sampled elements
+            stk = ag._optimizer.state[named[k]]
+            idx = sample_idx(k, named[k].numel())
+            out[f"u{u}_st_{k}__m"] = stk["exp_avg"].reshape(-1).numpy()[idx]
+            out[f"u{u}_st_{k}__v"] = stk["exp_avg_sq"].reshape(-1).numpy()[idx]
         for k in spec.slow_names.values():
             flat = named[k].detach().reshape(-1).numpy()
             idx = sample_idx(k, flat.size)
             out[f"u{u}_p_{k}__s"] = flat[idx]
     # grads of the FIRST update are not observable after update(); re-run _cal_grad on update-0 inputs with
     # the initial weights for a gradient fixture.
+    layout = optim_layout(ag, mods)
+    return out, layout
+
+
+def optim_layout(ag, mods):
+    """What train.py:126-130 would write as optims_state_dict (tools.recursively_collect_optim_state_dict,
+    tools.py:298-318): its keys, each optimizer state_dict's structure, and the parameter name behind state index i
+    (LaProp's param_groups[0]['params'] follow Dreamer._named_params, dreamer.py:196-227)."""
+    osd = mods["utils.tools"].recursively_collect_optim_state_dict(ag)
+    names = list(ag._named_params.keys())
+    lay = {"optims_keys": list(osd.keys()), "named_params": names, "optimizers": {}}
+    for key, sd in osd.items():
+        g = sd["param_groups"][0]
+        lay["optimizers"][key] = {
+            "top_keys": sorted(sd.keys()),
+            "n_groups": len(sd["param_groups"]),
+            "group": {k: (list(v) if isinstance(v, tuple) else v) for k, v in g.items() if k != "params"},
+            "params": list(g["params"]),
+            "state_keys": sorted(next(iter(sd["state"].values())).keys()) if sd["state"] else [],
+            "n_state": len(sd["state"]),
+        }
+    return lay
+
+
+def video_case(name, mods, TD):
+    """Dreamer.video_pred (dreamer.py:366-400) at the initial weights on a T=8 batch: posterior over 5 steps (noise
+    STREAM_OBS step i), then imagine_with_action over the last 3 logged actions (rssm.py:197-209; noise STREAM_IMG
+    step i). Output (B, T, 3*64, 64, 3), stored subsampled [..., ::4, ::4, :]."""
+    cfg_name, ovr, obs, A, discrete, _, _, H = CASES[name]
+    B, T, seed = 2, 8, 3000
+    cfg = load_config(cfg_name, ["device=cpu", "model.compile=False", f"model.imag_horizon={H}"] + ovr)
+    D = mods["world_model.dreamer"]
+    import copy
+
+    class Sp:
+        def __init__(s, shape):
+            s.shape = shape
+
+    class Spaces:
+        def __init__(s, d):
+            s.spaces = d
+
+    ag = D.Dreamer(copy.deepcopy(cfg.model), Spaces({k: Sp(v) for k, v in obs.items()}), Sp((A,)))
+    spec = Spec(cfg.model, obs, A, discrete)
+    vals = params_for(spec.shapes, PARAM_SEED)
+    with torch.no_grad():
+        named = dict(ag.named_parameters())
+        for k, v in vals.items():
+            named[k].data.copy_(torch.from_numpy(v))
+    rng = np.random.default_rng(zlib.crc32((name + "/video").encode()))
+    data_np = make_batch(rng, obs, A, discrete, B, T)
+    init_np = make_initial(rng, spec.S, spec.K, spec.D, B)
+    calls = [0]
+
+    def gs(logits, tau=1, hard=False, eps=1e-10, dim=-1):
+        i = calls[0]
+        calls[0] += 1
+        stream, step = (nz.STREAM_OBS, i) if i < 5 else (nz.STREAM_IMG, i - 5)
+        g = torch.from_numpy(nz.gumbel_block(seed, stream, step, logits.shape[0], 0,
+                                             int(np.prod(logits.shape[1:]))).reshape(logits.shape))
+        y_soft = ((logits + g) / tau).softmax(dim)
+        index = y_soft.max(dim, keepdim=True)[1]
+        return torch.zeros_like(logits).scatter_(dim, index, 1.0) - y_soft.detach() + y_soft
+
+    orig_gs = torch.nn.functional.gumbel_softmax
+    torch.nn.functional.gumbel_softmax = gs
+    try:
+        d = TD({k: torch.from_numpy(v) for k, v in data_np.items()}, batch_size=(B, T))
+        vid = ag.video_pred(d, (torch.from_numpy(init_np[0]), torch.from_numpy(init_np[1])))
+    finally:
+        torch.nn.functional.gumbel_softmax = orig_gs
+    assert calls[0] == T, calls[0]
+    out = {f"vp_in_{k}": v for k, v in data_np.items()}
+    out["vp_in_init_stoch"] = init_np[0].argmax(-1).astype(np.int16)
+    out["vp_in_init_deter"] = init_np[1]
+    out["vp_seed"] = seed
+    out["vp_out"] = vid.numpy()[:, :, ::4, ::4, :].copy()
+    out["vp_shape"] = np.asarray(vid.shape)
     return out
 
 
@@ -364,12 +456,18 @@ def main():
     mods, TD = import_reference()
     torch.set_num_threads(8)
     only = sys.argv[1:] or list(CASES)
+    lay_path = os.path.join(HERE, "optim_layout.json")
+    layouts = json.load(open(lay_path)) if os.path.exists(lay_path) else {}
     for name in only:
-        out = run_case(name, mods, TD)
+        out, layouts[name] = run_case(name, mods, TD)
         out.update(grad_case(name, mods, TD))
+        if CASES[name][0] == "dmc/walker_dreamer":
+            out.update(video_case(name, mods, TD))
         path = os.path.join(HERE, f"{name}.npz")
         np.savez_compressed(path, **out)
         print(name, "->", path, os.path.getsize(path) // 1024, "KB")
+    with open(lay_path, "w") as f:
+        json.dump({k: layouts[k] for k in sorted(layouts)}, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -14,6 +14,7 @@ HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = {
     "proprio_dreamer": ("dmc/proprio", {"position": (3,), "velocity": (2,)}),
     "walker_r2": ("dmc/cnn", {"image": (64, 64, 3)}),
+    "walker_r2_nowarm": ("dmc/cnn", {"image": (64, 64, 3)}, ["model.warmup=0"]),
     "walker_infonce": ("dmc/cnn", {"image": (64, 64, 3)}, ["model.rep_loss=infonce"]),
     "walker_r2aug": ("dmc/cnn", {"image": (64, 64, 3)}, ["model.r2dreamer.aug.enabled=True"]),
     "walker_pro": ("dmc/cnn", {"image": (64, 64, 3)}, ["model.rep_loss=dreamerpro"]),

@@ -81,3 +81,18 @@ def test_video_pred_decoder_agent():
     assert torch.allclose(v1[:, :, :64], truth)
     model = v1[:, :, 64:128]
     assert torch.allclose(v1[:, :, 128:], (model - truth + 1.0) / 2.0)
+
+
+def test_video_pred_matches_reference():
+    """Dreamer.video_pred vs the reference's own (golden vp_*, tests/golden/gen_golden.py video_case): walker decoder
+    agent at the initial weights, B2 T8 — posterior over 5 steps (noise STREAM_OBS step i), open-loop
+    imagine_with_action over the last 3 logged actions (STREAM_IMG step i), decoded; subsampled output within 1e-4."""
+    ag, z, spec, obs = build_agent("walker_dreamer")
+    data = {k: torch.from_numpy(z[f"vp_in_{k}"]).cuda()
+            for k in ("image", "action", "reward", "is_first", "is_terminal", "is_last")}
+    idx = torch.from_numpy(z["vp_in_init_stoch"].astype(np.int64))
+    init = (torch.nn.functional.one_hot(idx, spec.K).float().cuda(), torch.from_numpy(z["vp_in_init_deter"]).cuda())
+    vid = ag.video_pred(data, init, seed=int(z["vp_seed"]))
+    assert tuple(vid.shape) == tuple(z["vp_shape"])
+    got = vid[:, :, ::4, ::4, :].cpu().numpy()
+    np.testing.assert_allclose(got, z["vp_out"], rtol=1e-4, atol=1e-4)

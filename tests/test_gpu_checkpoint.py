@@ -52,3 +52,47 @@ def test_save_resume_bit_exact(tmp_path):
         assert s["step"] == opt["state"][i]["step"]
         assert torch.equal(s["exp_avg"], opt["state"][i]["exp_avg"])
         assert torch.equal(s["exp_avg_sq"], opt["state"][i]["exp_avg_sq"])
+
+
+@pytest.mark.parametrize("name", ["walker_r2", "walker_dreamer", "proprio_dreamer", "atari_r2", "maze_r2", "walker_pro"])
+def test_optim_state_layout_matches_reference(name, tmp_path):
+    """optims_state_dict as the reference's train.py:126-130 writes it (tools.recursively_collect_optim_state_dict,
+    tools.py:298-318; golden tests/golden/optim_layout.json recorded from the reference after its two updates): the
+    same keys ("_optimizer", "_scheduler.optimizer"), state_dict structure and param_group values, and LaProp state
+    index i <-> Dreamer._named_params[i] in the reference's order (dreamer.py:196-206; the moments of index i are
+    checked element-wise against the reference's by test_update_matches_reference). Round-trips through the file."""
+    import json
+    from golden_io import HERE
+    from sdreamer.checkpoint import load_checkpoint, save_checkpoint
+    lay = json.load(open(os.path.join(HERE, "optim_layout.json")))[name]
+    ag, z, spec, obs = build_agent(name)
+    assert list(ag._named_params) == lay["named_params"]
+    sd_name = {id(p): n for n, p in ag.named_parameters()}  # state_dict key of each _named_params entry
+    shape_of = {n: spec.shapes[sd_name[id(p)]] for n, p in ag._named_params.items()}
+    for u in range(2):
+        ag.update_batch(batch(z, u, obs, "cuda"), initial(z, u, spec, "cuda"), int(z[f"u{u}_seed"]))
+    path = save_checkpoint(ag, os.path.join(tmp_path, "latest.pt"))
+    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    osd = ckpt["optims_state_dict"]
+    assert list(osd) == lay["optims_keys"]
+    for key, ref in lay["optimizers"].items():
+        sd = osd[key]
+        assert sorted(sd) == ref["top_keys"]
+        assert len(sd["param_groups"]) == ref["n_groups"]
+        g = sd["param_groups"][0]
+        assert list(g["params"]) == ref["params"]
+        for k, v in ref["group"].items():
+            got = list(g[k]) if isinstance(g[k], tuple) else g[k]
+            if isinstance(v, float):
+                assert abs(got - v) <= 1e-12 * abs(v), (k, got, v)
+            else:
+                assert got == v, (k, got, v)
+        assert len(sd["state"]) == ref["n_state"]
+        for i, st in sd["state"].items():
+            assert sorted(st) == ref["state_keys"], i
+            assert tuple(st["exp_avg"].shape) == tuple(shape_of[lay["named_params"][i]])
+    b, _, _, _ = build_agent(name)
+    load_checkpoint(b, path)
+    o1, o2 = ag._optimizer.state_dict(), b._optimizer.state_dict()
+    for i, st in o1["state"].items():
+        assert torch.equal(st["exp_avg"], o2["state"][i]["exp_avg"]) and st["step"] == o2["state"][i]["step"]

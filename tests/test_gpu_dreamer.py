@@ -17,6 +17,7 @@ import pytest
 import torch
 
 from golden_io import CASES, batch, case_overrides, initial, load_case, sample_idx
+from parity import assert_close, compare_indices, imag_margins, post_margins, ulp
 from sdreamer.config import load_config
 
 pytestmark = pytest.mark.gpu
@@ -59,27 +60,96 @@ def _rel(a, b):
     return abs(float(a) - float(b)) / max(abs(float(b)), 1e-6)
 
 
+class _OracleRun:
+    """Lazily runs the CPU oracle over the same two updates (only when a near-tie margin is needed)."""
+
+    def __init__(self, name, z, spec, obs):
+        self.name, self.z, self.spec, self.obs = name, z, spec, obs
+        self.keeps = None
+
+    def keep(self, u):
+        if self.keeps is None:
+            from oracle.ref_cpu import OracleAgent
+            _, _, _, params, _ = load_case(self.name)
+            orc = OracleAgent(self.spec, params)
+            self.keeps = []
+            for v in range(2):
+                k = {}
+                orc.update(batch(self.z, v, self.obs), initial(self.z, v, self.spec), int(self.z[f"u{v}_seed"]), keep=k)
+                self.keeps.append(k)
+        return self.keeps[u]
+
+
+def _opt_samples(ag, spec):
+    """name -> (exp_avg, exp_avg_sq) sampled like the golden u*_st_* (LaProp state index i = _named_params[i])."""
+    sd = ag._optimizer.state_dict()["state"]
+    sd_name = {id(p): n for n, p in ag.named_parameters()}  # _named_params keys can differ (prj vs projector)
+    out = {}
+    for i, prm in enumerate(ag._named_params.values()):
+        k = sd_name[id(prm)]
+        if k not in spec.shapes or i not in sd:
+            continue
+        m = sd[i]["exp_avg"].reshape(-1).cpu().numpy()
+        v = sd[i]["exp_avg_sq"].reshape(-1).cpu().numpy()
+        idx = sample_idx(k, m.size)
+        out[k] = (m[idx], v[idx])
+    return out
+
+
 @pytest.mark.parametrize("name", list(CASES))
 def test_update_matches_reference(name):
     ag, z, spec, obs = build_agent(name)
+    orc = _OracleRun(name, z, spec, obs)
+    SK, S, Kd = spec.SK, spec.S, spec.K
+    unimix = float(spec.unimix)
+    _, _, _, params0, _ = load_case(name)
+    prev = {k: params0[k].reshape(-1)[sample_idx(k, params0[k].size)] for k in spec.shapes}
+    report = {}
     for u in range(2):
+        seed = int(z[f"u{u}_seed"])
         data = batch(z, u, obs, DEV)
         if "image" in obs:
             data["image"] = torch.from_numpy(z[f"u{u}_in_image"]).to(DEV)  # uint8: exercise preprocess
         init = initial(z, u, spec, DEV)
-        (ps, pd), mets = ag.update_batch(data, init, int(z[f"u{u}_seed"]))
+        (ps, pd), mets = ag.update_batch(data, init, seed)
         torch.cuda.synchronize()
-        # latents
-        idx = ps.argmax(-1).cpu().numpy()
-        ref_idx = z[f"u{u}_post_idx"]
-        mism = (idx != ref_idx).mean()
-        assert mism <= 0.002, f"posterior index mismatch fraction {mism}"
-        if u == 0:
-            assert mism == 0.0, "posterior indices must be bit-exact on the first update"
-            pdv = pd.detach().cpu().numpy()[..., ::4]
-            np.testing.assert_allclose(pdv, z["u0_post_deter"], rtol=1e-3, atol=1e-4)
-            pl = ag._last["post_logit"].detach().cpu().numpy()
-            np.testing.assert_allclose(pl, z["u0_post_logit"], rtol=1e-3, atol=2e-4)
+        # posterior latents (rssm.py:140-178): bit-exact except near-ties; deter / logits on the rows that did not flip
+        ref_logit = z[f"u{u}_post_logit"]
+        dv = compare_indices(ps.argmax(-1).cpu().numpy(), z[f"u{u}_post_idx"],
+                             lambda: post_margins(ref_logit, seed, unimix), f"u{u} posterior indices")
+        keep_rows = ~dv
+        pdv = pd.detach().cpu().numpy()[..., ::4]
+        assert_close(pdv, z[f"u{u}_post_deter"], 1e-4, 1e-5, f"u{u} post_deter", mask=~keep_rows[..., None])
+        pl = ag._last["post_logit"].detach().cpu().numpy()
+        assert_close(pl, ref_logit, 1e-4, 1e-4, f"u{u} post_logit", mask=~keep_rows[..., None, None])
+        prl = ag._last["prior_logit"].detach().cpu().numpy().reshape(ref_logit.shape)
+        assert_close(prl, z[f"u{u}_prior_logit"], 1e-4, 1e-4, f"u{u} prior_logit", mask=~keep_rows[..., None, None])
+        report[f"u{u}_post_deter"] = float(np.abs(pdv - z[f"u{u}_post_deter"]).max())
+        # imagination (dreamer.py:673-692): time-major (H+1, N, F) -> batch-major
+        ifeat = ag._last["imag_feat_tm"].detach().transpose(0, 1).cpu().numpy()
+        N, H1 = ifeat.shape[:2]
+        iidx = ifeat[..., :SK].reshape(N, H1, S, Kd).argmax(-1)
+
+        def imargin():
+            k = orc.keep(u)
+            m = imag_margins(k["imag_prior_logit"].numpy(), seed, unimix)
+            return np.concatenate([np.full((N, 1, S), np.inf, np.float32), m], 1)  # feat 0 = posterior start
+
+        start_bad = dv.reshape(-1)  # imagination starts from the posterior rows (b, t): a flipped start diverges
+        idv = compare_indices(iidx, z[f"u{u}_imag_idx"], imargin, f"u{u} imagined indices")
+        idv = idv | start_bad[:, None]
+        assert_close(ifeat[..., SK::16], z[f"u{u}_imag_deter"], 1e-4, 1e-5, f"u{u} imag_deter", mask=idv[..., None])
+        iact = ag._last["imag_action_tm"].detach().transpose(0, 1).cpu().numpy()
+        assert_close(iact, z[f"u{u}_imag_action"], 1e-4, 1e-5, f"u{u} imag_action", mask=idv[..., None])
+        ret = ag._last["ret"].detach().cpu().numpy()[..., None]
+        rows_ok = ~idv.any(1)
+        assert_close(ret, z[f"u{u}_imag_ret"], 1e-3, 1e-4, f"u{u} imag_ret", mask=~rows_ok[:, None, None])
+        rret = ag._last["rret"].detach().cpu().numpy()[..., None]
+        if rows_ok.all():
+            assert_close(rret, z[f"u{u}_replay_ret"], 1e-3, 1e-4, f"u{u} replay_ret")
+            assert_close(ag.return_ema.ema_vals.cpu().numpy(), z[f"u{u}_ema_vals"], 1e-4, 1e-6, f"u{u} ema_vals")
+        report[f"u{u}_imag_deter"] = float(np.where(idv[..., None], 0, np.abs(ifeat[..., SK::16] - z[f"u{u}_imag_deter"])).max())
+        report[f"u{u}_ret"] = float(np.abs(ret - z[f"u{u}_imag_ret"]).max())
         # losses and metrics
         bad = []
         for k, v in mets.items():
@@ -95,14 +165,40 @@ def test_update_matches_reference(name):
             if r > tol and abs(float(v) - float(z[key])) > 1e-5:
                 bad.append((k, float(v), float(z[key]), r))
         assert not bad, bad
-        # parameters after the LaProp step
+        # LaProp moments and the parameter step (laprop.py:85-116 after agc.py:15-53), per sampled element.
+        # v = EMA of (AGC-scaled g)^2 pins every gradient element's magnitude; m and dp carry its sign. Elements whose
+        # gradient is ~0 relative to the tensor (|g| < 1e-3 of the sample max) may take either sign: excluded there.
+        # Gradient elements carry the split-bf16 contraction error, amplified by cancellation in long sums (e.g. the
+        # first conv layer's weight gradient sums dy*x over B*T*64*64 pixels: up to ~0.5 % of an element measured),
+        # so v is held to 2e-2 rel + 2e-4 of max v, m and dp to 2e-2 rel + 1e-2 of their sample max (+ 4 ulp of p):
+        # a flipped step sign (2x), a skipped AGC clip (1/scale^2 in v) or a skipped Polyak still fail
+        # (tools/sabotage_optim.sh).
+        opt = _opt_samples(ag, spec)
         sd = ag.state_dict()
+        worst = 0.0
         for k in spec.shapes:
+            m, v = opt[k]
+            m_ref, v_ref = z[f"u{u}_st_{k}__m"], z[f"u{u}_st_{k}__v"]
+            assert_close(v, v_ref, 2e-2, 2e-4 * np.abs(v_ref).max() + 1e-30, f"u{u} exp_avg_sq {k}")
+            tiny = np.sqrt(v_ref) < 1e-3 * np.sqrt(v_ref).max()
+            assert_close(m, m_ref, 2e-2, 1e-2 * np.abs(m_ref).max() + 1e-30, f"u{u} exp_avg {k}", mask=tiny)
             flat = sd[k].detach().reshape(-1).cpu().numpy()
             got = flat[sample_idx(k, flat.size)]
             ref = z[f"u{u}_p_{k}__s"]
-            step = 4e-5 * (u + 1) / 1000 * 5  # |dp| <= lr * O(1) for LaProp; compare to the step scale
-            assert np.abs(got - ref).max() <= max(2e-3 * step, 1e-6 * np.abs(ref).max()), k
+            d_got, d_ref = got.astype(np.float64) - prev[k], ref.astype(np.float64) - prev[k]
+            assert_close(d_got, d_ref, 2e-2, 1e-2 * np.abs(d_ref).max() + 4 * ulp(ref), f"u{u} parameter step {k}",
+                         mask=tiny)
+            nz_ = (~tiny) & (np.abs(d_ref) > 0)
+            if nz_.any():
+                worst = max(worst, float((np.abs(d_got - d_ref)[nz_] / np.abs(d_ref)[nz_]).max()))
+            prev[k] = ref.astype(np.float64)
+        report[f"u{u}_max_rel_dp"] = worst
+        # slow critic after this update's Polyak (dreamer.py:242-249): s = 0.02 v + 0.98 s, before the step
+        for k, sk in spec.slow_names.items():
+            flat = sd[sk].detach().reshape(-1).cpu().numpy()
+            ref = z[f"u{u}_p_{sk}__s"]
+            assert_close(flat[sample_idx(sk, flat.size)], ref, 0.0, 4 * ulp(ref) + 1e-12, f"u{u} slow critic {sk}")
+    print(name, report)
 
 
 @pytest.mark.parametrize("name", ["walker_r2", "walker_r2aug", "walker_pro"])
@@ -131,10 +227,12 @@ def test_graph_replay_matches_eager(name):
     assert torch.equal(e[5], g[5])
 
 
-@pytest.mark.parametrize("name", ["walker_pro", "walker_r2aug"])
+@pytest.mark.parametrize("name", list(CASES))
 def test_cal_grad_matches_reference(name):
-    """Gradients of one _cal_grad at the initial weights vs the reference's (golden g_*): walker_pro checks the
-    prototype / projection gradients that the default prototype freeze zeroes before the optimizer step."""
+    """Gradients of one _cal_grad at the initial weights vs the reference's (golden g_*: per-tensor L2 norm and 32
+    sampled elements of every trainable tensor). walker_pro checks the prototype / projection gradients that the
+    default prototype freeze zeroes before the optimizer step. Gradient contractions run split-bf16:
+    elements within 2e-3 relative + 1e-4 of the tensor's largest sampled |g|; norms within 2e-4."""
     ag, z, spec, obs = build_agent(name)
     ag.use_graphs = False
     data = ag.preprocess(batch(z, 0, obs, DEV))
@@ -146,12 +244,61 @@ def test_cal_grad_matches_reference(name):
     ag._cal_grad(data, init, 1000, 0)
     torch.cuda.synchronize()
     named = dict(ag.named_parameters())
-    bad = []
+    bad, worst = [], (0.0, None)
     for k in spec.shapes:
         g = named[k].grad
-        flat = (torch.zeros_like(named[k]) if g is None else g).reshape(-1).double().cpu().numpy()
+        g = torch.zeros_like(named[k]) if g is None else g
+        flat = ag.to_ref_layout(named[k], g).reshape(-1).double().cpu().numpy()
         ref_n = float(z[f"g_{k}__n"])
         n = float(np.linalg.norm(flat))
-        if abs(n - ref_n) > 2e-3 * max(ref_n, 1e-9) and abs(n - ref_n) > 1e-7:
-            bad.append((k, n, ref_n))
+        if abs(n - ref_n) > 2e-4 * max(ref_n, 1e-9) and abs(n - ref_n) > 1e-9:
+            bad.append((k, "norm", n, ref_n))
+        ref = z[f"g_{k}__s"].astype(np.float64)
+        got = flat[sample_idx(k, flat.size)]
+        scale = np.abs(ref).max()
+        err = np.abs(got - ref) - (2e-3 * np.abs(ref) + 1e-4 * scale + 1e-12)
+        if err.max() > 0:
+            i = int(np.argmax(err))
+            bad.append((k, "element", float(got[i]), float(ref[i])))
+        r = float((np.abs(got - ref) / (np.abs(ref) + 1e-3 * scale + 1e-30)).max())
+        if r > worst[0]:
+            worst = (r, k)
+    print(name, "worst element rel err", worst)
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("name", ["walker_r2", "walker_dreamer", "proprio_dreamer", "atari_r2", "maze_r2"])
+def test_weight_init_matches_reference(name):
+    """Dreamer's own initialisation (networks._trunc_normal_ = tools.weight_init_, tools.py:76-100, plus the
+    outscale of the last head layers, networks.py:370-372) vs the reference's initialiser run under
+    torch.manual_seed(0) (golden init_*__stat: mean, std, max|w|, numel per tensor). The draws differ (different
+    RNG call order), so the test is distributional: constants (zero biases, unit norm scales, outscale 0) exact;
+    std within 4/sqrt(n) + 1 %, mean within 6 std/sqrt(n), max|w| <= 2 sigma (the truncation) and >= 0.5x the
+    reference's (the 2 sigma bound is taken from the reference's sample std, widened by its sampling error)."""
+    from sdreamer.dreamer import Dreamer
+    z, cfg, spec, params, obs = load_case(name)
+    gcfg = load_config(CASES[name][0], ["device=cuda:0", "model.compile=False"] + case_overrides(name))
+    act = _Sp((int(z["meta_A"]),))
+    if bool(z["meta_discrete"]):
+        act.discrete = True
+    torch.manual_seed(0)
+    ag = Dreamer(copy.deepcopy(gcfg.model), _Spaces({k: _Sp(v) for k, v in obs.items()}), act)
+    sd = ag.state_dict()
+    bad = []
+    for k in spec.shapes:
+        mean_r, std_r, amax_r, n = (float(x) for x in z[f"init_{k}__stat"])
+        w = sd[k].detach().double().reshape(-1).cpu()
+        assert w.numel() == int(n), k
+        mean, std, amax = w.mean().item(), (w.std().item() if w.numel() > 1 else 0.0), w.abs().max().item()
+        if std_r == 0.0:
+            if not (mean == mean_r and amax == amax_r):
+                bad.append((k, "constant", mean, mean_r))
+            continue
+        sigma = std_r / 0.8796  # std of N(0, s^2) truncated at +-2s is 0.8796 s
+        if abs(std / std_r - 1) > 4 / np.sqrt(n) + 0.01:
+            bad.append((k, "std", std, std_r))
+        if abs(mean - mean_r) > 6 * std_r / np.sqrt(n):
+            bad.append((k, "mean", mean, mean_r))
+        if amax > max(2 * sigma * (1 + 4 / np.sqrt(n)), amax_r) * 1.001 or amax < 0.5 * amax_r:
+            bad.append((k, "max", amax, amax_r))
     assert not bad, bad

@@ -323,14 +323,20 @@ def test_barlow():
     close(xd.grad, xr.grad, 1e-5, "grad")
 
 
-def test_laprop_agc_step():
+@pytest.mark.parametrize("warmup", [1000, 0])
+def test_laprop_agc_step(warmup):
+    """sd_agc_laprop_step (AGC agc.py:15-53 + LaProp laprop.py:85-116 + LambdaLR warm-up dreamer.py:214-225) vs the
+    oracle restatement, compared as per-element parameter DELTAS (|dp_gpu - dp_ref| <= 1e-4 |dp_ref| + 4 ulp(p))
+    and moments (1e-5): a step of lr * O(1) = 4e-8 (warm-up) or 4e-5 is resolved, so a flipped sign, a skipped AGC
+    clip (step 2 clips: 1000x larger gradients) or a wrong bias correction fails. Steps 1-3 mix unclipped and clipped
+    tensors; the clip is active in step 2 only."""
     from sdreamer.optim import LaProp
     from oracle.ref_cpu import OracleAgent
     torch.manual_seed(0)
     shapes = [(256, 2560), (256,), (7, 5), (1000,)]
     ps_cpu = [torch.randn(s) for s in shapes]
     params = [torch.nn.Parameter(p.clone().to(DEV)) for p in ps_cpu]
-    opt = LaProp(params, lr=4e-5, betas=(0.9, 0.999), eps=1e-20, agc=0.3, pmin=1e-3, warmup=1000)
+    opt = LaProp(params, lr=4e-5, betas=(0.9, 0.999), eps=1e-20, agc=0.3, pmin=1e-3, warmup=warmup)
 
     class _S:
         pass
@@ -338,10 +344,12 @@ def test_laprop_agc_step():
     ag.P = {str(i): p.clone().requires_grad_() for i, p in enumerate(ps_cpu)}
     ag.s = _S()
     ag.s.shapes = {str(i): s for i, s in enumerate(shapes)}
-    ag.lr0, ag.warmup, ag.betas, ag.eps, ag.agc, ag.pmin = 4e-5, 1000, (0.9, 0.999), 1e-20, 0.3, 1e-3
+    ag.lr0, ag.warmup, ag.betas, ag.eps, ag.agc, ag.pmin = 4e-5, warmup, (0.9, 0.999), 1e-20, 0.3, 1e-3
     ag.opt_step, ag.state = 0, {}
     for it in range(3):
         grads = [torch.randn(s) * (10.0 if it == 1 else 0.01) for s in shapes]
+        prev_g = [p.data.detach().cpu().double() for p in params]
+        prev_r = [ag.P[str(i)].data.clone().double() for i in range(len(shapes))]
         for i, g in enumerate(grads):
             params[i].grad.copy_(g.to(DEV))
             ag.P[str(i)].grad = g.clone()
@@ -349,8 +357,31 @@ def test_laprop_agc_step():
         ag.agc_()
         ag.laprop_step()
         ag.opt_step += 1
+        sd = opt.state_dict()["state"]
         for i in range(len(shapes)):
-            close(params[i].data, ag.P[str(i)].data, 1e-6, f"param {i} step {it}")
+            pr = ag.P[str(i)].data
+            d_got = params[i].data.detach().cpu().double() - prev_g[i]
+            d_ref = pr.double() - prev_r[i]
+            tol = 1e-4 * d_ref.abs() + 4 * torch.from_numpy(np.spacing(np.abs(pr.numpy()))).double()
+            assert ((d_got - d_ref).abs() <= tol).all(), (i, it, float((d_got - d_ref).abs().max()))
+            st = ag.state[id(ag.P[str(i)])]
+            for nm in ("exp_avg", "exp_avg_sq"):
+                a, b = sd[i][nm].cpu().double(), st[nm].double()
+                assert ((a - b).abs() <= 1e-5 * b.abs() + 1e-5 * b.abs().max()).all(), (nm, i, it, float((a - b).abs().max()))
+            assert abs(sd[i]["exp_avg_lr_1"] - st["exp_avg_lr_1"]) <= 1e-12 * abs(st["exp_avg_lr_1"])
+
+
+def test_polyak():
+    """sd_polyak = the slow-critic update s = 0.02 v + 0.98 s (dreamer.py:242-249), within 1 ulp of the torch f32
+    expression (fma contraction)."""
+    from sdreamer import _native as nat, kernels as K
+    g = torch.Generator().manual_seed(3)
+    v = torch.randn(100003, generator=g)
+    s0 = torch.randn(100003, generator=g)
+    dst = s0.clone().to(DEV)
+    nat.call("sd_polyak", K.p(v.to(DEV)), K.p(dst), v.numel(), 0.02, K.stream())
+    ref = (0.02 * v + (1 - 0.02) * s0)
+    assert ((dst.cpu() - ref).abs() <= torch.from_numpy(np.spacing(np.abs(ref.numpy())))).all()
 
 
 @pytest.mark.parametrize("ci,co,hw,nb", [(4, 32, 64, 3), (32, 48, 32, 8), (48, 64, 16, 16), (64, 64, 8, 40),

@@ -55,6 +55,14 @@ def test_oracle_update_matches_reference(name):
         for k in spec.slow_names.values():
             flat = ag.P[k].detach().reshape(-1).numpy()
             _close(flat[sample_idx(k, flat.size)], z[f"u{u}_p_{k}__s"], rtol=1e-5, atol=1e-7, what=k)
+        for k in spec.shapes:  # LaProp moments (laprop.py:62-116)
+            st = ag.state[id(ag.P[k])]
+            idx = sample_idx(k, ag.P[k].numel())
+            v_ref, m_ref = z[f"u{u}_st_{k}__v"], z[f"u{u}_st_{k}__m"]
+            _close(st["exp_avg_sq"].reshape(-1).numpy()[idx], v_ref, rtol=1e-3, atol=1e-9 * np.abs(v_ref).max(),
+                   what=f"exp_avg_sq {k}")
+            _close(st["exp_avg"].reshape(-1).numpy()[idx], m_ref, rtol=1e-3, atol=1e-5 * np.abs(m_ref).max(),
+                   what=f"exp_avg {k}")
 
 
 @pytest.mark.parametrize("name", list(CASES))
