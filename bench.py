@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Headline benchmark: imagined latent steps / s of the full Dreamer update (BASELINE.json `metric`).
 
-Workload (BASELINE.json configs[1]): DMC-vision walker_walk 64x64x3, rep_loss=r2dreamer, B16 L64 H15 per GPU,
+Workload (default, BASELINE.json configs[1]): DMC-vision walker_walk 64x64x3, rep_loss=r2dreamer, B16 L64 H15 per
+GPU; --config selects another BASELINE workload (WORKLOADS), --global-batch splits its batch over the ranks;
 synthetic data (uniform uint8 images, U(-1,1) actions, U(0,1) rewards), reference-initialised
 random weights. One step = one `Dreamer.update(replay_buffer)` (dreamer.py:402-451): on-device replay sampling,
 encoder + RSSM observe scan fwd/bwd, prior/KL, Barlow, heads, H+1-step imagination, λ-returns, ReturnEMA,
@@ -42,8 +43,23 @@ class _Spaces:
         self.spaces = d
 
 
-def synth_buffer(cfg, device, rank, T=160, A=6):
-    """Fill an HBM replay buffer with synthetic walker-like transitions (16 envs x T steps, one episode each)."""
+# --config -> the BASELINE.json workload it is (act dim, one-hot actions, label). Weak scaling keeps the config's
+# batch per GPU; --global-batch divides it over the ranks instead (configs[2]: B64 over 8 GPUs = 8 rows per GPU).
+WORKLOADS = {
+    "dmc/cnn": (6, False, "dmc walker_walk vision 64x64x3, rep_loss=r2dreamer (BASELINE configs[1])"),
+    "dmc/walker_dreamer": (6, False, "dmc walker_walk vision 64x64x3, rep_loss=dreamer conv decoder (BASELINE configs[2])"),
+    "dmc/atari_breakout": (4, True, "Atari100k-like breakout 64x64x3, 4 one-hot actions, 32x32 stoch, r2dreamer "
+                                    "(BASELINE configs[3], synthetic)"),
+    "dmc/memory_maze": (6, True, "Memory-Maze-like 9x9 64x64x3, 6 one-hot actions, deter 4096, r2dreamer "
+                                 "(BASELINE configs[4], synthetic)"),
+}
+# fwd+bwd matmul/conv FLOP of one update at the headline workload (FlopCounterMode on the reference)
+UPDATE_FLOP = {("dmc/cnn", 16, 64, 15): 927.7e9}
+
+
+def synth_buffer(cfg, device, rank, T=160, A=6, discrete=False):
+    """Fill an HBM replay buffer with synthetic transitions (16 envs x T steps, one episode each): uniform uint8
+    images, U(-1,1) actions (one-hot of a uniform index for discrete action spaces), U(0,1) rewards."""
     from sdreamer.buffer import Buffer
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     E = 16
@@ -52,9 +68,13 @@ def synth_buffer(cfg, device, rank, T=160, A=6):
     first = torch.zeros(T, E, 1, dtype=torch.bool)
     first[0] = True
     idx = torch.randint(0, Kd, (T, E, S), generator=g)
+    if discrete:
+        act = torch.nn.functional.one_hot(torch.randint(0, A, (T, E), generator=g), A).float()
+    else:
+        act = torch.rand(T, E, A, generator=g) * 2 - 1
     data = {
         "image": torch.randint(0, 256, (T, E, 64, 64, 3), dtype=torch.uint8, generator=g),
-        "action": torch.rand(T, E, A, generator=g) * 2 - 1,
+        "action": act,
         "reward": torch.rand(T, E, 1, generator=g),
         "is_first": first,
         "is_last": torch.zeros(T, E, 1, dtype=torch.bool),
@@ -67,19 +87,31 @@ def synth_buffer(cfg, device, rank, T=160, A=6):
     return buf
 
 
-def cpu_baseline(cfg, n_updates, threads):
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline(cfg, n_updates, threads, A=6, discrete=False):
     """The CPU oracle (oracle/ref_cpu.py: fp32 restatement of the reference update) on the host cores."""
     from oracle.init import params_for
     from oracle.ref_cpu import OracleAgent, Spec
     torch.set_num_threads(threads)
     B, L = int(cfg.batch_size), int(cfg.batch_length)
-    spec = Spec(cfg.model, {"image": (64, 64, 3)}, 6, False)
+    spec = Spec(cfg.model, {"image": (64, 64, 3)}, A, discrete)
     ag = OracleAgent(spec, params_for(spec.shapes, 0))
     g = torch.Generator().manual_seed(0)
     first = torch.zeros(B, L, 1, dtype=torch.bool)
     first[:, 0] = True
+    act = torch.nn.functional.one_hot(torch.randint(0, A, (B, L), generator=g), A).float() if discrete else \
+        torch.rand(B, L, A, generator=g) * 2 - 1
     data = {"image": torch.randint(0, 256, (B, L, 64, 64, 3), generator=g, dtype=torch.uint8).float() / 255.0,
-            "action": torch.rand(B, L, 6, generator=g) * 2 - 1, "reward": torch.rand(B, L, 1, generator=g),
+            "action": act, "reward": torch.rand(B, L, 1, generator=g),
             "is_first": first, "is_last": torch.zeros(B, L, 1, dtype=torch.bool),
             "is_terminal": torch.zeros(B, L, 1, dtype=torch.bool)}
     init = (torch.zeros(B, spec.S, spec.K), torch.zeros(B, spec.D))
@@ -146,12 +178,13 @@ def dominant_probe(K):
                                "N tile = 48)")
 
 
-def phase_rooflines(agent, cfg, ms_update, reps=10):
+def phase_rooflines(agent, cfg, cfg_name, ms_update, reps=10):
     """SURVEY §8(d) 'report separately': (i) the imagination rollout alone (secondary metric N*H / t_rollout; FLOP =
     2 * weights per img_step (Deter + img_net) per imagined latent + 2 * actor weights per actor sample, H img_steps
     and H+1 actor samples per start row), (ii) the observe scan forward (RSSM.observe: bytes = the Deter + obs_net
     weights streamed once per step, the 'HBM GB/s on the recurrent scan' figure), (iv) the whole update (927.7
-    GFLOP fwd+bwd at this config, SURVEY §8(d), FlopCounterMode on the reference). Each phase runs eagerly after the
+    GFLOP fwd+bwd at the headline config, SURVEY §8(d), FlopCounterMode on the reference; omitted for other
+    workloads, whose update FLOP were not counted). Each phase runs eagerly after the
     timed steps on synthetic inputs of the update's shapes, bracketed by HIP events on the stream it launches on."""
     r = agent.rssm
     B, L, H = int(cfg.batch_size), int(cfg.batch_length), int(cfg.model.imag_horizon)
@@ -187,8 +220,8 @@ def phase_rooflines(agent, cfg, ms_update, reps=10):
     with torch.no_grad():
         ms_obs = timed(lambda: r.observe(embed, action, r.initial(B), reset, seed=5))
     b_obs = 4.0 * L * (numel(r._deter_net) + numel(r._obs_net))
-    f_upd = 927.7e9
-    return {
+    f_upd = UPDATE_FLOP.get((cfg_name, B, L, H))
+    out = {
         "imagination": {"bound": "mfma", "latents_per_s": N * H / (ms_img * 1e-3), "ms": ms_img,
                         "achieved": f_img / (ms_img * 1e-3) / 1e12, "peak": 157.3, "unit": "TFLOP/s",
                         "frac": f_img / (ms_img * 1e-3) / 1e12 / 157.3, "work": f_img,
@@ -196,10 +229,12 @@ def phase_rooflines(agent, cfg, ms_update, reps=10):
         "observe_scan": {"bound": "hbm", "ms": ms_obs, "achieved": b_obs / (ms_obs * 1e-3) / 1e9, "peak": 8000.0,
                          "unit": "GB/s", "frac": b_obs / (ms_obs * 1e-3) / 1e9 / 8000.0, "work": b_obs,
                          "what": f"RSSM.observe forward, B={B} L={L}: Deter + obs_net weights once per step"},
-        "update": {"bound": "mfma", "achieved": f_upd / (ms_update * 1e-3) / 1e12, "peak": 157.3, "unit": "TFLOP/s",
-                   "frac": f_upd / (ms_update * 1e-3) / 1e12 / 157.3, "work": f_upd,
-                   "what": "whole Dreamer.update, 927.7 GFLOP fwd+bwd (SURVEY §8(d)) / ms_per_step"},
     }
+    if f_upd:  # only where the update's FLOP were counted on the reference
+        out["update"] = {"bound": "mfma", "achieved": f_upd / (ms_update * 1e-3) / 1e12, "peak": 157.3,
+                         "unit": "TFLOP/s", "frac": f_upd / (ms_update * 1e-3) / 1e12 / 157.3, "work": f_upd,
+                         "what": f"whole Dreamer.update, {f_upd / 1e9:.1f} GFLOP fwd+bwd (SURVEY §8(d)) / ms_per_step"}
+    return out
 
 
 def main():
@@ -207,7 +242,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="dmc/cnn")
+    ap.add_argument("--config", default="dmc/cnn", choices=sorted(WORKLOADS))
+    ap.add_argument("--global-batch", action="store_true",
+                    help="divide the config's batch_size over the ranks (strong scaling of the batch) instead of "
+                         "keeping it per GPU (weak scaling, the default)")
     ap.add_argument("--cpu-updates", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -230,11 +268,21 @@ def main():
     from sdreamer.config import load_config
     from sdreamer.dreamer import Dreamer
 
-    cfg = load_config(args.config, [f"device=cuda:{local}", "model.compile=False"])
+    A, discrete, workload = WORKLOADS[args.config]
+    ovr = [f"device=cuda:{local}", "model.compile=False"]
+    B0 = int(load_config(args.config, ovr).batch_size)
+    if args.global_batch:
+        if B0 % world:
+            raise SystemExit(f"--global-batch: batch_size {B0} does not split over {world} ranks")
+        ovr.append(f"batch_size={B0 // world}")
+    cfg = load_config(args.config, ovr)
     B, L, H = int(cfg.batch_size), int(cfg.batch_length), int(cfg.model.imag_horizon)
     torch.manual_seed(0)  # identical initial weights on every rank
-    agent = Dreamer(cfg.model, _Spaces({"image": _Sp((64, 64, 3))}), _Sp((6,)), rank=rank, world=world)
-    buf = synth_buffer(cfg, device, rank)
+    act_space = _Sp((A,))
+    if discrete:
+        act_space.discrete = True
+    agent = Dreamer(cfg.model, _Spaces({"image": _Sp((64, 64, 3))}), act_space, rank=rank, world=world)
+    buf = synth_buffer(cfg, device, rank, T=max(160, 2 * (L + 1)), A=A, discrete=discrete)
 
     # roofline probe on the dominant kernel: sees its launch (eager warm-up or graph capture), then re-times that
     # exact launch with HIP events on its stream after the timed steps
@@ -265,10 +313,16 @@ def main():
     out = {
         "metric": METRIC,
         "value": value, "unit": "imagined_latents/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic (uniform uint8 64x64x3 images, U(-1,1) actions, U(0,1) rewards; random-init weights)",
-        "config": {"workload": "dmc walker_walk vision, rep_loss=r2dreamer, per-GPU B16 L64 H15 (BASELINE configs[1])",
-                   "global_batch": B * world, "seq_len": L, "imag_horizon": H, "parallelism": f"dp{world}"},
+        "ms_per_step": ms, "higher_is_better": True, "scaling": "strong" if args.global_batch else "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "precision": "fp32 everywhere a sampled index or a WM loss depends on (fp32 MFMA, and the fp32-accurate "
+                     "3-way split-bf16 'bf16x6' MFMA in the imagination); gradient contractions and the frozen "
+                     "imagined heads on 2-way split-bf16 (~1e-5 rel); DESIGN.md §2",
+        "data": "synthetic (uniform uint8 64x64x3 images, " + ("one-hot uniform" if discrete else "U(-1,1)") +
+                " actions, U(0,1) rewards; random-init weights)",
+        "config": {"workload": f"{workload}, per-GPU B{B} L{L} H{H}", "config": args.config,
+                   "global_batch": B * world, "per_gpu_batch": B, "seq_len": L, "imag_horizon": H,
+                   "parallelism": f"dp{world}"},
     }
     if probe is not None:
         out["roofline"] = probe.report()
@@ -286,14 +340,18 @@ def main():
                 out["roofline"]["traffic_source"] = f"profiles/{os.path.basename(tf)} (rocprofv3 --pmc)"
                 out["roofline"]["algorithmic_bytes"] = t.get("algorithmic_bytes")
     if not args.no_roofline:
-        out["phases"] = phase_rooflines(agent, cfg, ms)
+        out["phases"] = phase_rooflines(agent, cfg, args.config, ms)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["parity"] = wm_loss_parity()
-        threads = min(len(os.sched_getaffinity(0)), 16)
-        cfg_cpu = load_config(args.config, ["device=cpu", "model.compile=False"])
-        t_cpu = cpu_baseline(cfg_cpu, args.cpu_updates, threads)
+        if args.config == "dmc/cnn":
+            out["parity"] = wm_loss_parity()
+        # every core of this process's affinity, capped by the box's CPU share (OMP_NUM_THREADS, 16 per GPU there)
+        share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+        aff = len(os.sched_getaffinity(0))
+        threads = min(aff, share) if share > 0 else aff
+        cfg_cpu = load_config(args.config, ["device=cpu", "model.compile=False", f"batch_size={B}"])
+        t_cpu = cpu_baseline(cfg_cpu, args.cpu_updates, threads, A, discrete)
         out["cpu_baseline"] = {"value": B * L * H / t_cpu, "unit": "imagined_latents/s", "cores": threads,
-                               "kind": "port", "cpu": platform.processor() or platform.machine(),
+                               "kind": "port", "cpu": cpu_model(), "affinity_cores": aff,
                                "sample": f"oracle/ref_cpu.py OracleAgent.update() at walker B{B} L{L} H{H} fp32, "
                                          f"median of {args.cpu_updates} after 1 warm-up ({t_cpu:.2f} s/update)"}
     if rank == 0:

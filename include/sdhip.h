@@ -155,7 +155,8 @@ int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db, float* wor
 int sd_conv2d_wgrad_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int ups, int ksplit);
 /* bwd-weight of a pooled ConvEncoder stage from (dpool, argmax) of sd_pool_rms_bwd_compact (the conv gradient is
  * expanded inside the direct kernel while staging). _slabs: workspace slabs (each Co x (kh*kw*Ci+1) floats), 0 when
- * the shape is outside the direct kernel (then sd_conv2d_wgrad_pool returns SD_ESHAPE). */
+ * the shape is outside the direct kernel (then sd_conv2d_wgrad_pool returns SD_ESHAPE). Alignment: in and dpool
+ * 16 B, amax 4 B (read as uint32 words), else SD_EARG. */
 int sd_conv2d_wgrad_pool_slabs(int Nb, int H, int W, int Ci, int Co, int kh, int kw);
 int sd_conv2d_wgrad_pool(const float* in, const float* dpool, const uint8_t* amax, float* dw_db, float* workspace,
                          long ws_floats, int Nb, int H, int W, int Ci, int Co, int kh, int kw, int pad,

@@ -74,9 +74,11 @@ SD_DEV float sd_bload1(sd_rsrc r, uint32_t byte_off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
 }
 
-// hardware exp2 + reciprocal forms (v_exp_f32, v_rcp_f32): ~1e-7 relative error, a handful of VALU instead of the
-// ~25-instruction IEEE expf/division expansions — these sit on the A-operand path of the fused GEMM loaders
-SD_DEV float sigmoidf_(float x) { return __fdividef(1.f, 1.f + __expf(-x)); }
-SD_DEV float siluf_(float x) { return __fdividef(x, 1.f + __expf(-x)); }
+// hardware exp2 + reciprocal forms (v_exp_f32, v_rcp_f32): ~1e-7 relative error, 4 VALU instead of the
+// ~25-instruction IEEE expf/division expansions — these sit on the A-operand path of the fused GEMM loaders.
+// (__fdividef is NOT the fast form on ROCm 7.2 / gfx950: it lowers to the 13-instruction v_div_scale/fmas/fixup
+// IEEE sequence; __builtin_amdgcn_rcpf is one v_rcp_f32.) exp(-x) = inf for x << 0 gives rcp = 0: silu -> -0.
+SD_DEV float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+SD_DEV float siluf_(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 static inline int sd_cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1247,7 +1247,8 @@ int patch_stride(int Ci) {  // >= Ci + 2 (ones / zero channels), % 4 == 0, 16 or
 }
 
 // pixels per staged row block of the max-pool-fused f32 direct bwd-weight (encoder first stage): more pixels per
-// block = more MFMA steps per barrier (128 -> 256 px: 397 -> 337 us at 1024 images); SDHIP_WGRAD_PIX overrides
+// block = more MFMA steps per barrier (128 / 256 / 512 px: 397 / 337 / 305 us at 1024 images; default 512, falling
+// back to smaller blocks where the staging does not fit, pool_plan); SDHIP_WGRAD_PIX overrides
 int wgrad_pool_pix() {
   static int a = -1;
   if (a < 0) {
@@ -1493,7 +1494,8 @@ extern "C" int sd_conv2d_wgrad_pool(const float* in, const float* dpool, const u
   DirectPlan pl;
   if (!pool_plan(Nb, H, W, Ci, Co, kh, kw, pl))
     return SD_ESHAPE;
-  if (!al16(dpool) || !al16(in) || Co % 4 || Ci % 4 || !amax) return SD_EARG;
+  // amax is read as uint32 words (4 pooled pixels' argmax bytes per load)
+  if (!al16(dpool) || !al16(in) || Co % 4 || Ci % 4 || !amax || reinterpret_cast<uintptr_t>(amax) % 4) return SD_EARG;
   return wgrad_direct(in, dpool, dw_db, workspace, ws_floats, Nb, H, W, Ci, Co, kh, kw, pad, kh * kw * Ci,
                       ilog2_exact(W), pl, (hipStream_t)stream_, amax);
 }

@@ -14,6 +14,7 @@
 // Results land directly in the reference's (H1, N, F) feat and (H1, N, A) action layouts.
 #include "common.h"
 #include "dist_core.h"
+#include "gemm6_core.h"
 #include "gemm_core.h"
 #include "philox.h"
 #include "sdhip.h"
@@ -39,6 +40,11 @@ struct AStage {
 #pragma unroll
     for (int v = 0; v < NV; ++v)
       if (live(v)) *reinterpret_cast<f32x4*>(lds + row(v) * LDS_ROW + 4 * kq(v)) = r[v];
+  }
+  SD_DEV void store6(__bf16* lds) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      if (live(v)) split3_store(lds + row(v) * LROW6 + 4 * kq(v), r[v]);
   }
 };
 
@@ -115,15 +121,21 @@ struct ARms : AStage<BM> {
       wr[v] = ld4(w + gk);
     }
   }
+  SD_DEV f32x4 val(int v) const {
+    f32x4 y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = siluf_(r[v][j] * rr[v] * wr[v][j]);
+    return y;
+  }
   SD_DEV void store(float* lds) const {
 #pragma unroll
     for (int v = 0; v < NV; ++v)
-      if (this->live(v)) {
-        f32x4 y;
+      if (this->live(v)) *reinterpret_cast<f32x4*>(lds + this->row(v) * LDS_ROW + 4 * this->kq(v)) = val(v);
+  }
+  SD_DEV void store6(__bf16* lds) const {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) y[j] = siluf_(r[v][j] * rr[v] * wr[v][j]);
-        *reinterpret_cast<f32x4*>(lds + this->row(v) * LDS_ROW + 4 * this->kq(v)) = y;
-      }
+    for (int v = 0; v < NV; ++v)
+      if (this->live(v)) split3_store(lds + this->row(v) * LROW6 + 4 * this->kq(v), val(v));
   }
 };
 
@@ -154,8 +166,37 @@ struct BRows {
       if (256 * (v + 1) <= BN * BK / 4 || i < BN * BK / 4)
         *reinterpret_cast<f32x4*>(lds + (i / (BK / 4)) * LDS_ROW + 4 * (i % (BK / 4))) = r[v];
     }
+  }  SD_DEV void store6(__bf16* lds) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + 256 * v;
+      if (256 * (v + 1) <= BN * BK / 4 || i < BN * BK / 4)
+        split3_store(lds + (i / (BK / 4)) * LROW6 + 4 * (i % (BK / 4)), r[v]);
+    }
   }
 };
+
+// ------------------------------------------------------------------------------------------- contraction
+// F6: the bf16x6 main loop (gemm6_core.h: fp32-accurate, 2.67x the fp32 MFMA rate) instead of v_mfma_f32_16x16x4_f32.
+// ES (early store) applies to the fp32 loop only.
+template <bool F6, int BM, int BN, int WM, int WN, int PF, bool ES = false, class OpA, class OpB>
+SD_DEV void mainloop(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16],
+                     bool accumulate = false) {
+  static_assert(BK == BK6, "tile depth");
+  if constexpr (F6)
+    gemm6_mainloop_pf<BM, BN, WM, WN, PF>(la, lb, kbeg, kend, acc, accumulate);
+  else
+    gemm16_mainloop_pf<BM, BN, WM, WN, PF, ES>(la, lb, kbeg, kend, acc, accumulate);
+}
+// per-kernel choice (measured, imagination alone, N = 1024): k_hid 54.0 -> 50.7 us and k_gate 41.9 -> 38.7 us on
+// bf16x6; k_lin (28.6 vs 30.0) and the short-K latency-bound launches stay on fp32. These launches are bound by
+// operand traffic and per-launch latency, not by the MFMA pipe (tools/pmc_table.py: k_hid MFMA busy ~0.45).
+// (SD_IMG_F6 = bitmask over LIN, RMSLIN, HID, GATE, PRIOR, ACTION: a build-time A/B knob, tools/ab_variants.sh)
+#ifndef SD_IMG_F6
+#define SD_IMG_F6 0b001100
+#endif
+constexpr bool F6_LIN = SD_IMG_F6 & 1, F6_RMSLIN = SD_IMG_F6 & 2, F6_HID = SD_IMG_F6 & 4, F6_GATE = SD_IMG_F6 & 8,
+               F6_PRIOR = SD_IMG_F6 & 16, F6_ACTION = SD_IMG_F6 & 32;
 
 // ------------------------------------------------------------------------------------------- epilogue helpers
 // Wave (wr, wc) of a BM x BN tile owns rows wr*16 + 4q + r and columns wc*WN + 16j + l16 (gemm16_mainloop layout).
@@ -221,7 +262,7 @@ __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2,
   APlain<BM> la[3] = {a0, a0, a0};
   BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][WN / 16];
-  gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, p.K, acc);
+  mainloop<F6_LIN, BM, BN, 16, WN, 3>(la, lb, 0, p.K, acc);
   ep_bias_part<BM, BN, WN>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
 }
 
@@ -240,7 +281,7 @@ __global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw,
   ARms<BM> la[3] = {a0, a0, a0};
   BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][WN / 16];
-  gemm16_mainloop_pf<BM, BN, 16, WN, 3, true>(la, lb, 0, K, acc);
+  mainloop<F6_RMSLIN, BM, BN, 16, WN, 3, true>(la, lb, 0, K, acc);
   ep_bias_part<BM, BN, WN>(acc, bias, out, gridDim.x * BN, part, M, m0, n0);
 }
 
@@ -263,28 +304,28 @@ __global__ __launch_bounds__(256) void k_hid(sd_imagine d, const float* h, long 
     const BRows<BN> b0(Wseg, Ig, 0, BN, 0);
     APlain<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, Dg, acc);
+    mainloop<F6_HID, BM, BN, 16, WN, 3>(la, lb, 0, Dg, acc);
   }
   {
     const ARms<BM> a0(x0p, U, d.n0, rs0, m0, M, U);
     const BRows<BN> b0(Wseg + Dg, Ig, 0, BN, 0);
     ARms<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, U, acc, true);
+    mainloop<F6_HID, BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
   }
   {
     const ARms<BM> a0(x1p, U, d.n1, rs1, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + U, Ig, 0, BN, 0);
     ARms<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, U, acc, true);
+    mainloop<F6_HID, BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
   }
   {
     const APlain<BM> a0(x2, U, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + 2 * U, Ig, 0, BN, 0);
     APlain<BM> la[3] = {a0, a0, a0};
     BRows<BN> lb[3] = {b0, b0, b0};
-    gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, U, acc, true);
+    mainloop<F6_HID, BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
   }
   ep_bias_part<BM, BN, WN>(acc, d.bh, hp, d.D, ph, M, m0, n0);
 }
@@ -303,7 +344,7 @@ __global__ __launch_bounds__(256) void k_gate(sd_imagine d, const float* hp, con
   ARms<BM> la[2] = {a0, a0};
   BRows<BN> lb[2] = {b0, b0};
   f32x4 acc[1][6];
-  gemm16_mainloop_pf<BM, BN, 16, BN, 2, false>(la, lb, 0, Dg, acc);
+  mainloop<F6_GATE, BM, BN, 16, BN, 2>(la, lb, 0, Dg, acc);
   const Lane L = lane_ids<BN, BN>();
   const float* bg = d.bg + (long)g * 3 * Dg;
 #pragma unroll
@@ -340,7 +381,7 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
   ARms<BM> la[3] = {a0, a0, a0};
   BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][1];
-  gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, U, acc);
+  mainloop<F6_PRIOR, BM, BN, 16, WN, 3>(la, lb, 0, U, acc);
   const Lane L = lane_ids<BN, WN>();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -386,7 +427,7 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
   ARms<BM> la[3] = {a0, a0, a0};
   BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][1];
-  gemm16_mainloop_pf<BM, BN, 16, WN, 3, false>(la, lb, 0, U, acc);
+  mainloop<F6_ACTION, BM, BN, 16, WN, 3>(la, lb, 0, U, acc);
   const Lane L = lane_ids<BN, WN>();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {

@@ -186,6 +186,8 @@ class Dreamer(nn.Module):
         # SDREAMER_MARKS=1: device timestamps at the phase boundaries of every update (kernels.Marks)
         self.marks = K.Marks(self.device) if os.environ.get("SDREAMER_MARKS", "0") != "0" else None
         self._side = torch.cuda.Stream(device=self.device)
+        self._comm = None  # data parallel: the gradient all-reduce stream (created on first use)
+        self._buckets = self._grad_buckets()
         self._graph = None
         self._eager_updates = 0
         self._seed_base = int(getattr(config, "seed", 0) or 0) * 1_000_003 + 12345
@@ -396,6 +398,37 @@ class Dreamer(nn.Module):
         self._updates += 1
         return post, mets
 
+    def _grad_buckets(self):
+        """Data parallel: the gradient arena split into all-reduce buckets by the phase after which each parameter's
+        gradient is final (_update_graphed), as merged contiguous arena ranges:
+          heads — world-model heads, projector / decoder / prototypes: M1 (main);
+          ac    — actor and value heads: S2 (side; the replay-value part of the value head is deferred into S2);
+          rssm  — the RSSM: S3 (side: the scan's deferred weight gradients; the prior's come from M1 before it);
+          rest  — the encoder and anything unlisted: after M2c (main) and S4 (side)."""
+        a = self._optimizer.arena
+        pos = {id(p): i for i, p in enumerate(a.params)}
+        group = {"actor": "ac", "value": "ac", "rssm": "rssm", "encoder": "rest"}
+        out = {"heads": [], "ac": [], "rssm": [], "rest": []}
+        for name, prm in self._named_params.items():
+            i = pos[id(prm)]
+            b = group.get(name.split(".")[0], "heads")
+            lo, hi = a.offsets[i], (a.offsets[i + 1] if i + 1 < len(a.offsets) else a.total)
+            rng = out[b]
+            if rng and rng[-1][1] == lo:
+                rng[-1] = (rng[-1][0], hi)
+            else:
+                rng.append((lo, hi))
+        return out
+
+    def _allreduce_bucket(self, name, *events):
+        """Sum all-reduce of one gradient bucket on the communication stream once `events` have fired (overlaps the
+        phases still running on main / side; RCCL runs collectives in issue order, the same on every rank)."""
+        with torch.cuda.stream(self._comm):
+            for e in events:
+                self._comm.wait_event(e)
+            for lo, hi in self._buckets[name]:
+                dist.all_reduce(self._optimizer.arena.grad[lo:hi])
+
     def _mark(self, tag):
         if self.marks is not None:
             self.marks(tag)
@@ -448,8 +481,11 @@ class Dreamer(nn.Module):
         Data parallel: a phase that exchanges data (Barlow statistics in M1, the returns gather for the global
         ReturnEMA in S2) is a chain graph → collective → graph (parallel.PhaseGraph); the collectives are issued
         eagerly on the phase's stream, in the same host order on every rank (M1's, then S2's after the R phase's
-        launch), so RCCL's single stream never queues the world-model branch behind the actor-critic branch. The gradient arena is sum-all-reduced between the joins and M3 (which
-        scales it by 1/world before AGC + LaProp)."""
+        launch), so RCCL's single stream never queues the world-model branch behind the actor-critic branch. The
+        gradient arena is sum-all-reduced in four buckets (_grad_buckets) on a communication stream as soon as each
+        bucket's last writer phase is done — WM heads after M1, actor / value after S2, RSSM after S3, encoder at the
+        end — so only the encoder bucket's all-reduce sits between the joins and M3 (which scales the arena by
+        1/world before AGC + LaProp)."""
         if self._graph is None:
             self._g_in = {k: v.clone() for k, v in data.items()}
             self._g_ro = ro
@@ -500,6 +536,13 @@ class Dreamer(nn.Module):
         with torch.cuda.stream(side):
             gS1.replay(0, k1)
         gM1.replay()
+        dp = self.world > 1
+        if dp and self._comm is None:
+            self._comm = torch.cuda.Stream(device=self.device)
+        if dp:  # heads bucket final after M1
+            ev_m1 = torch.cuda.Event()
+            ev_m1.record()
+            self._allreduce_bucket("heads", ev_m1)
         with torch.cuda.stream(side):
             gS1.replay(k1)
             ev_s1 = torch.cuda.Event()
@@ -517,17 +560,31 @@ class Dreamer(nn.Module):
         ev_enc = torch.cuda.Event()
         ev_enc.record()
         gM2c.replay()
+        ev_side = [None, None]
         with torch.cuda.stream(side):
             side.wait_event(ev_rep)
             gS2.replay()
+            if dp:
+                ev_side[0] = torch.cuda.Event()
+                ev_side[0].record()
             side.wait_event(ev_scan)  # S3: the scan's weight gradients, beside the encoder backward
             gS3.replay()
+            if dp:
+                ev_side[1] = torch.cuda.Event()
+                ev_side[1].record()
             side.wait_event(ev_enc)  # S4: encoder stages 2..'s weight gradients, beside the first stage's backward
             gS4.replay()
+        if dp:  # bucketed sum all-reduce of the gradient arena, overlapping the backward phases still running
+            self._allreduce_bucket("ac", ev_side[0])
+            self._allreduce_bucket("rssm", ev_side[1])
+            ev_main, ev_s4 = torch.cuda.Event(), torch.cuda.Event()
+            ev_main.record(main)
+            ev_s4.record(side)
+            self._allreduce_bucket("rest", ev_main, ev_s4)
         if side is not main:
             main.wait_stream(side)
-        if self.world > 1:
-            parallel.collective(lambda: dist.all_reduce(self._optimizer.arena.grad))
+        if dp:
+            main.wait_stream(self._comm)
         gM3.replay()
         self._slow_value_updates += 1
         self._optimizer.host_steps += 1

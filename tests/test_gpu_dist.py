@@ -4,7 +4,8 @@ Each rank runs the product update on its half of the golden batch rows (row offs
 single-GPU noise of those rows) through the same code the 8-GPU bench runs: the two-stream schedule, eager warm-up
 updates, then the captured phase graphs split at the exchange steps (Barlow statistics, the returns gather, the
 gradient all-reduce — sdreamer/parallel.py). gloo stands in for RCCL (one GPU on the test box; RCCL refuses two
-ranks on one device); the collectives are issued by the same `parallel.collective` calls. Stated tolerances:
+ranks on one device); the collectives are issued by the same calls (`parallel.collective`, and the bucketed gradient
+all-reduce on the communication stream, Dreamer._allreduce_bucket). Stated tolerances:
 world-model losses <= 1e-4 relative, other scalar losses <= 1e-3 (sums of differently ordered partial sums), the
 parameters after 4 updates: L2 distance <= 2% of the L2 norm of the 4-update change, and <= 0.1% of the elements off
 by more than 5% of the largest step (LaProp normalises per element, so summation-order noise on near-zero gradients
@@ -81,7 +82,8 @@ def _run(name, world):
     return res
 
 
-@pytest.mark.parametrize("name", ["walker_r2", "walker_dreamer", "walker_infonce", "walker_r2aug", "walker_pro"])
+@pytest.mark.parametrize("name", ["walker_r2", "walker_dreamer", "walker_infonce", "walker_r2aug", "walker_pro",
+                                  "atari_r2", "maze_r2"])
 def test_two_rank_update_equals_one_rank(name):
     one = _run(name, 1)[0]
     two = _run(name, 2)

@@ -408,7 +408,7 @@ def test_conv_backward_bf16x3(ci, co, hw, nb):
 
 
 @pytest.mark.parametrize("ci,co,hw,nb", [(4, 32, 64, 3), (32, 48, 32, 2)])
-def test_first_stage_pooled_wgrad_bit_exact(ci, co, hw, nb):
+def test_first_stage_pooled_wgrad_reordered_sums(ci, co, hw, nb):
     """A stage without input gradient (the encoder's first) takes the compact backward — sd_pool_rms_bwd_compact +
     sd_conv2d_wgrad_pool, the conv gradient expanded from (pooled gradient, argmax) inside the direct kernel — and
     must give the dense path's weight / bias / norm gradients: the same values staged, in 512-pixel row blocks (the
