@@ -157,10 +157,62 @@ def wm_loss_parity():
                                     f"B{int(z['meta_B'])} L{int(z['meta_T'])} H{int(z['meta_H'])})"}
 
 
+IMAG_KERNELS = {  # sd_imagine_step_kernel `which` -> (label, FLOP per launch as f(N, D, U, Dg))
+    0: ("k_lin<32, 64> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
+        "GEMMs in one launch, RMSNorm row partials in the epilogue; v_mfma_f32_16x16x4_f32)",
+        lambda N, D, U, Dg: 3 * 2.0 * N * D * U),
+    1: ("k_hid (imagination step: _dyn_hid BlockLinear, K = Dg + 3U per block, RMSNorm + SiLU of x0 / x1 in the A "
+        "loader; bf16x6)", lambda N, D, U, Dg: 2.0 * N * D * (Dg + 3 * U)),
+    2: ("k_gate (imagination step: _dyn_gru BlockLinear + GRU epilogue, RMSNorm + SiLU of hp in the A loader; bf16x6)",
+        lambda N, D, U, Dg: 2.0 * N * 3 * D * Dg),
+}
+
+
+def imag_kernel_probe(agent, cfg, which=0, reps=30):
+    """Roofline probe on the update's dominant kernel symbol, k_lin<32, 64> (imagination; largest total time per
+    update, profiles/r02_kernel_summary.md): the imagination runs once at the update's shape (N = B*L start rows),
+    then its step-t launch is re-issued alone (sd_imagine_step_kernel: same descriptor, workspace and grid) `reps`
+    times over t = 0 .. H-1, each bracketed by HIP events on the stream it is launched on."""
+    import ctypes
+    from sdreamer import _native as nat
+    from sdreamer import kernels as K
+    r = agent.rssm
+    B, L, H = int(cfg.batch_size), int(cfg.batch_length), int(cfg.model.imag_horizon)
+    N, H1, dev = B * L, H + 1, agent.device
+    SK, D, U, G = r.flat_stoch, r._deter, r._hidden, r._blocks
+    g = torch.Generator(device=dev).manual_seed(11)
+    idx = torch.randint(0, r._discrete, (N, r._stoch), device=dev, generator=g)
+    feats = torch.empty(H1, N, SK + D, device=dev)
+    actions = torch.empty(H1, N, agent.act_dim, device=dev)
+    feats[0, :, :SK] = torch.nn.functional.one_hot(idx, r._discrete).float().reshape(N, SK)
+    feats[0, :, SK:] = torch.randn(N, D, device=dev, generator=g)
+    keep = {}
+    with torch.no_grad():
+        agent._imagine_fused(feats, actions, H1, 5, 0, keep=keep)
+    torch.cuda.synchronize()
+    desc = keep["desc"]
+    label, flop = IMAG_KERNELS[which]
+    work = flop(N, D, U, D // G)
+    ms = []
+    for i in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        nat.call("sd_imagine_step_kernel", ctypes.addressof(desc), which, i % H, K.stream())
+        e.record()
+        ms.append((s, e))
+    torch.cuda.synchronize()
+    avg_ms = sum(s.elapsed_time(e) for s, e in ms) / reps
+    achieved = work / (avg_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA, "unit": "TFLOP/s",
+            "frac": achieved / PEAK_FP32_MFMA, "key": ("k_lin", "k_hid", "k_gate")[which], "kernel": label,
+            "launches": reps, "avg_us": avg_ms * 1e3,
+            "work_per_launch": work, "shape": f"N={N} D={D} U={U}"}
+
+
 def dominant_probe(K):
-    """Roofline probe on the dominant kernel of the step: the encoder's second stage forward, conv + MaxPool2d(2) +
-    RMSNorm2D + SiLU in one launch (direct conv, M = B*L*32*32 pixels, N = 48, K = 5*5*32), the largest MFMA launch
-    of the update. Algorithmic work = 2*M*N*K FLOP per launch."""
+    """Secondary roofline probe: the encoder's second stage forward, conv + MaxPool2d(2) + RMSNorm2D + SiLU in one
+    launch (direct conv, M = B*L*32*32 pixels, N = 48, K = 5*5*32), the largest single MFMA launch of the update
+    (DESIGN.md §5). Algorithmic work = 2*M*N*K FLOP per launch."""
     if not K.ops_fused_pool():
         def flops(a):  # sd_conv2d_fwd(in, w, b, out, Nb, Hs, Ws, Ci, Co, kh, kw, pad, ups, stream)
             Nb, Hs, Ws, Ci, Co, kh, kw, ups = a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[12]
@@ -325,20 +377,25 @@ def main():
                    "parallelism": f"dp{world}"},
     }
     if probe is not None:
-        out["roofline"] = probe.report()
-        # HBM bytes per launch of the same kernel from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
-        # (tools/roofline_traffic.py: gfx950 FETCH_SIZE x2 correction), committed under profiles/
+        # the dominant kernel (k_lin, imagination) and, as secondary entries, the other two imagination contractions
+        # and the largest single MFMA launch (encoder stage 2); HBM bytes per launch from separate rocprofv3 --pmc
+        # FETCH_SIZE / WRITE_SIZE passes (tools/roofline_traffic.py: gfx950 FETCH_SIZE x2), committed under profiles/
         import glob
+        out["roofline"] = imag_kernel_probe(agent, cfg, 0)
+        out["roofline_secondary"] = {"k_hid": imag_kernel_probe(agent, cfg, 1),
+                                     "k_gate": imag_kernel_probe(agent, cfg, 2), "conv_stage2": probe.report()}
         tfs = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                                             "r*_roofline_traffic.json")))
         tf = tfs[-1] if tfs else ""
         if tf:
-            t = json.load(open(tf))
-            if out["roofline"] and out["roofline"]["kernel"].startswith(t.get("kernel", "?") + " ") \
-                    and t.get("traffic_bytes"):
-                out["roofline"]["traffic"] = t["traffic_bytes"]
-                out["roofline"]["traffic_source"] = f"profiles/{os.path.basename(tf)} (rocprofv3 --pmc)"
-                out["roofline"]["algorithmic_bytes"] = t.get("algorithmic_bytes")
+            tj = json.load(open(tf))
+            for ent in [out["roofline"]] + list(out["roofline_secondary"].values()):
+                t = tj.get(ent.get("key", "conv_fwd_direct_pool")) if ent else None
+                if t and t.get("traffic_bytes"):
+                    ent["traffic"] = t["traffic_bytes"]
+                    ent["traffic_source"] = f"profiles/{os.path.basename(tf)} (rocprofv3 --pmc)"
+                    ent["algorithmic_bytes"] = t.get("algorithmic_bytes")
+            out["roofline"].setdefault("traffic", None)
     if not args.no_roofline:
         out["phases"] = phase_rooflines(agent, cfg, args.config, ms)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -300,6 +300,10 @@ typedef struct sd_imagine {
 } sd_imagine;
 int sd_imagine_work_floats(const sd_imagine* d);
 int sd_imagine_run(const sd_imagine* d, sd_stream stream);
+/* Measurement aid (bench.py roofline): one launch of step t's largest contractions exactly as sd_imagine_run issues
+ * them, after a run on the same descriptor/workspace (idempotent): which = 0: img_net_0 + _dyn_in0 + actor layer 0's
+ * deter part (three (N, D) x (D, U) GEMMs, k_lin), 1: _dyn_hid (k_hid), 2: _dyn_gru + GRU (k_gate). 0 <= t < H1 - 1. */
+int sd_imagine_step_kernel(const sd_imagine* d, int which, int t, sd_stream stream);
 
 /* InfoNCE representation loss (dreamer.py:533-542): cross_entropy(logits - rowmax(logits), arange) on an (n, ncol)
  * row-major logits block (ld floats between rows), row r labelled with column r + label_off (data parallel: local

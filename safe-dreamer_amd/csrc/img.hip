@@ -547,6 +547,36 @@ extern "C" int sd_imagine_work_floats(const sd_imagine* d) {
   return (int)iwork(*d, nullptr).total;
 }
 
+// One launch of step t's k_lin (img_net_0 + _dyn_in0 + actor layer 0's deter part: which = 0), k_hid (1) or
+// k_gate (2), exactly as sd_imagine_run issues it (same descriptor and workspace; the launch recomputes the values that
+// run already wrote, so it can be repeated): bench.py times the dominant kernel of the update this way.
+extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd_stream stream_) {
+  int rc = icheck(dp);
+  if (rc) return rc;
+  const sd_imagine& d = *dp;
+  if (t < 0 || t >= d.H1 - 1 || which < 0 || which > 2) return SD_EARG;
+  hipStream_t st = (hipStream_t)stream_;
+  const IWork w = iwork(d, d.work);
+  const int N = d.N, U = d.U, SK = d.SK, D = d.D, F = SK + D;
+  const long NF = (long)N * F;
+  const int npU = U / 32;
+  auto feats = [&](int s) { return d.feats + s * NF; };
+  if (which == 0) {
+    LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};
+    LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
+    LinProb pd{feats(t + 1) + SK, F, D, d.Wa[0] + SK, F, nullptr, w.ad, U, nullptr, nullptr};
+    k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), 3), 256, 0, st>>>(pi, px, pd, N);
+  } else if (which == 1) {
+    k_hid<<<dim3(D / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, npU, w.x2, w.hp,
+                                                       w.ph);
+  } else {
+    // k_gate reads hold = feats(t) deter and writes feats(t + 1) deter: the same values again
+    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / 64, feats(t) + SK, feats(t + 1) + SK, F);
+  }
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
 // BRows reads BN = 32 rows of the actor output weight: the caller passes Wao padded to 32 rows (zero rows)
 extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   int rc = icheck(dp);

@@ -1000,7 +1000,7 @@ class Dreamer(nn.Module):
             (A <= 16 if self.act_discrete else 2 * A <= 32) and 1 <= a.mlp.n <= 4 and 1 <= r._img_layers <= 4 and \
             a.last.weight.shape[0] <= 32
 
-    def _imagine_fused(self, feats, actions, H1, seed, row_offset, chunks=None):
+    def _imagine_fused(self, feats, actions, H1, seed, row_offset, chunks=None, keep=None):
         """sd_imagine_run (csrc/img.hip): feats[0] holds the start state. chunks: step boundaries [t0, t1, ..., H1];
         the steps run as one launch sequence per chunk with an event recorded after each (returned), so consumers on
         other streams can start on a chunk's feats while the next chunk is imagined."""
@@ -1038,6 +1038,8 @@ class Dreamer(nn.Module):
         work = torch.empty(nwork, dtype=torch.float32, device=feats.device)
         d.work = work.data_ptr()
         bounds = list(chunks) if chunks else [0, H1]
+        if keep is not None:  # measurement aid (bench.py): the descriptor and every buffer it points to
+            keep.update(desc=d, work=work, wpad=wpad, feats=feats, actions=actions, P=P)
         events = []
         for t0, t1 in zip(bounds[:-1], bounds[1:]):
             d.t_begin, d.t_end = int(t0), int(t1)

@@ -22,14 +22,15 @@ def from_csv(path):
     return sorted(rows, key=lambda r: -r[2])
 
 
-def probe_rows(path, name_like="conv_fwd_direct_poolILi48E", grid_wgs=8192):
-    """Dispatches of the bench roofline probe kernel (encoder conv2 fwd: 8192 workgroups) — the per-launch average
-    to compare with bench.py's roofline.avg_us."""
+def probe_rows(path, name_like="conv_fwd_direct_poolILi48E", grid=(8192, 1, 1)):
+    """Dispatches of a bench roofline probe kernel by name and grid (workgroups x, y, z) — the per-launch average to
+    compare with bench.py's roofline avg_us. Probe replays after the timed steps are included."""
     con = sqlite3.connect(path)
     q = """select d.end - d.start from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id = s.id
-           where s.kernel_name like ? and d.grid_size_x / d.workgroup_size_x = ?"""
+           where s.kernel_name like ? and d.grid_size_x / d.workgroup_size_x = ? and d.grid_size_y = ?
+           and d.grid_size_z = ?"""
     try:
-        return [r[0] for r in con.execute(q, (f"%{name_like}%", grid_wgs))]
+        return [r[0] for r in con.execute(q, (f"%{name_like}%",) + tuple(grid))]
     except sqlite3.OperationalError:
         return []
 
@@ -37,10 +38,14 @@ def probe_rows(path, name_like="conv_fwd_direct_poolILi48E", grid_wgs=8192):
 def main(path, top=40, per=1):
     rows = from_db(path) if path.endswith(".db") else from_csv(path)
     if path.endswith(".db"):
-        pr = probe_rows(path)
-        if pr:
-            print(f"roofline probe kernel conv_fwd_direct_pool<48> at 8192 workgroups (encoder conv2 fwd): {len(pr)} dispatches, "
-                  f"avg {sum(pr) / len(pr) / 1e3:.1f} us, min {min(pr) / 1e3:.1f} us\n")
+        for label, pat, grid in (("roofline kernel k_lin<32, 64> x3 (imagination, grid 4x32x3)", "k_linILi32ELi64E",
+                                  (4, 32, 3)),
+                                 ("secondary conv_fwd_direct_pool<48> (encoder stage 2, 8192 workgroups)",
+                                  "conv_fwd_direct_poolILi48E", (8192, 1, 1))):
+            pr = probe_rows(path, pat, grid)
+            if pr:
+                print(f"{label}: {len(pr)} dispatches, avg {sum(pr) / len(pr) / 1e3:.1f} us, "
+                      f"min {min(pr) / 1e3:.1f} us\n")
     tot = sum(r[2] for r in rows)
     print(f"total kernel time {tot / 1e6:.2f} ms over the profiled run ({tot / 1e6 / per:.2f} ms per step, {per} steps)")
     print("| share | total ms | calls | avg us | kernel |")
