@@ -172,7 +172,8 @@ def imag_kernel_probe(agent, cfg, which=0, reps=30):
     """Roofline probe on the update's dominant kernel symbol, k_lin<32, 64> (imagination; largest total time per
     update, profiles/r02_kernel_summary.md): the imagination runs once at the update's shape (N = B*L start rows),
     then its step-t launch is re-issued alone (sd_imagine_step_kernel: same descriptor, workspace and grid) `reps`
-    times over t = 0 .. H-1, each bracketed by HIP events on the stream it is launched on."""
+    times over t = 0 .. H-1, back to back between two HIP events on the stream it is launched on (per-launch event
+    pairs would add the event records' own cost to every launch; back to back only the ~1 us dispatch gap remains)."""
     import ctypes
     from sdreamer import _native as nat
     from sdreamer import kernels as K
@@ -193,15 +194,14 @@ def imag_kernel_probe(agent, cfg, which=0, reps=30):
     desc = keep["desc"]
     label, flop = IMAG_KERNELS[which]
     work = flop(N, D, U, D // G)
-    ms = []
+    nat.call("sd_imagine_step_kernel", ctypes.addressof(desc), which, 0, K.stream())  # warm
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
     for i in range(reps):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
         nat.call("sd_imagine_step_kernel", ctypes.addressof(desc), which, i % H, K.stream())
-        e.record()
-        ms.append((s, e))
+    e.record()
     torch.cuda.synchronize()
-    avg_ms = sum(s.elapsed_time(e) for s, e in ms) / reps
+    avg_ms = s.elapsed_time(e) / reps
     achieved = work / (avg_ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA, "unit": "TFLOP/s",
             "frac": achieved / PEAK_FP32_MFMA, "key": ("k_lin", "k_hid", "k_gate")[which], "kernel": label,

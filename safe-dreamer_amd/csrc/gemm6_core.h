@@ -126,5 +126,99 @@ SD_DEV void gemm6_mainloop_pf(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend, 
     if (kt + u < nk) step(kt + u, u);
 }
 
+// Fragment-prefetch form (gemm_core.h gemm16_mainloop_fp): iteration kt reads tile kt+1's three planes from LDS
+// before running tile kt's MFMAs on fragments read one iteration earlier, then stores tile kt+2 into stage kt&1.
+template <int BM, int BN, int WM, int WN, int PF, class OpA, class OpB>
+SD_DEV void gemm6_mainloop_fp(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16],
+                              bool accumulate = false) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+  constexpr int SA = BM * LROW6, STAGE = (BM + BN) * LROW6;
+  __bf16* smem = sd_smem6<2 * STAGE>();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  const int l16 = lane & 15, q = lane >> 4;
+  if (!accumulate) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int nk = (kend - kbeg + BK6 - 1) / BK6;
+  if (nk <= 0) return;
+  auto ktile = [&](int t) { return kbeg + (t < nk ? t : nk - 1) * BK6; };
+  bf16x8 fa[TM][3], fb[TN][3], na[TM][3], nb[TN][3];
+  auto frags = [&](int stage, bf16x8 (&a)[TM][3], bf16x8 (&b)[TN][3]) {
+    const __bf16* cur = smem + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const __bf16* p = cur + (wr * WM + 16 * i + l16) * LROW6 + 8 * q;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) a[i][s] = *reinterpret_cast<const bf16x8*>(p + s * BK6);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const __bf16* p = cur + SA + (wc * WN + 16 * j + l16) * LROW6 + 8 * q;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) b[j][s] = *reinterpret_cast<const bf16x8*>(p + s * BK6);
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    la[u].load(ktile(u), kend);
+    lb[u].load(ktile(u), kend);
+  }
+  la[0].store6(smem);
+  lb[0].store6(smem + SA);
+  la[0].load(ktile(PF), kend);
+  lb[0].load(ktile(PF), kend);
+  __syncthreads();
+  frags(0, fa, fb);
+  la[1 % PF].store6(smem + STAGE);
+  lb[1 % PF].store6(smem + STAGE + SA);
+  la[1 % PF].load(ktile(1 + PF), kend);
+  lb[1 % PF].load(ktile(1 + PF), kend);
+  __syncthreads();
+  auto step = [&](int kt, int u) {
+    frags((kt + 1) & 1, na, nb);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x4 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+      }
+    const int nx = (u + 2) % PF;
+    __builtin_amdgcn_sched_barrier(0);
+    la[nx].store6(smem + (kt & 1) * STAGE);
+    lb[nx].store6(smem + (kt & 1) * STAGE + SA);
+    la[nx].load(ktile(kt + 2 + PF), kend);
+    lb[nx].load(ktile(kt + 2 + PF), kend);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) fa[i][s] = na[i][s];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) fb[j][s] = nb[j][s];
+  };
+  int kt = 0;
+  for (; kt + PF <= nk; kt += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) step(kt + u, u);
+  }
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (kt + u < nk) step(kt + u, u);
+}
+
 }  // namespace
 }  // namespace sdg

@@ -415,6 +415,109 @@ SD_DEV void gemm16_mainloop_pf(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend,
   }
 }
 
+// Fragment-prefetch variant of gemm16_mainloop_pf (row-major LDS operands): iteration kt issues the LDS fragment
+// reads of tile kt+1 BEFORE its own MFMAs, which run on fragments read one iteration earlier, so the LDS latency sits
+// under the MFMAs instead of in front of them; the MFMA pipe only idles over the next tile's store and the barrier.
+// Two LDS stages suffice: iteration kt stores tile kt+2 into stage kt&1, whose tile-kt fragments every wave read
+// before iteration kt-1's barrier. Register tile t lives in set t % PF as in gemm16_mainloop_pf.
+template <int BM, int BN, int WM, int WN, int PF = 1, class OpA, class OpB>
+SD_DEV void gemm16_mainloop_fp(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16],
+                               bool accumulate = false) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+  static_assert(!is_kmajor<OpA>::value && !is_kmajor<OpB>::value, "row-major LDS operands");
+  constexpr int SA = BM * LDS_ROW, STAGE = SA + BN * LDS_ROW;
+  float* smem = sd_smem<2 * STAGE>();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  const int l16 = lane & 15, q = lane >> 4;
+  constexpr int XC = TM * TN < 4 ? 2 : 1;
+  f32x4 acc2[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!accumulate) acc[i][j] = acc2[i][j];
+    }
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk <= 0) return;
+  auto ktile = [&](int t) { return kbeg + (t < nk ? t : nk - 1) * BK; };
+  f32x4 fa[TM][2], fb[TN][2], na[TM][2], nb[TN][2];
+  auto frags = [&](int stage, f32x4 (&a)[TM][2], f32x4 (&b)[TN][2]) {
+    const float* s = smem + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* p = s + (wr * WM + 16 * i + l16) * LDS_ROW + 8 * q;
+      a[i][0] = *reinterpret_cast<const f32x4*>(p);
+      a[i][1] = *reinterpret_cast<const f32x4*>(p + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* p = s + SA + (wc * WN + 16 * j + l16) * LDS_ROW + 8 * q;
+      b[j][0] = *reinterpret_cast<const f32x4*>(p);
+      b[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    la[u].load(ktile(u), kend);
+    lb[u].load(ktile(u), kend);
+  }
+  la[0].store(smem);
+  lb[0].store(smem + SA);
+  la[0].load(ktile(PF), kend);
+  lb[0].load(ktile(PF), kend);
+  __syncthreads();
+  frags(0, fa, fb);
+  la[1 % PF].store(smem + STAGE);
+  lb[1 % PF].store(smem + STAGE + SA);
+  la[1 % PF].load(ktile(1 + PF), kend);
+  lb[1 % PF].load(ktile(1 + PF), kend);
+  __syncthreads();
+  auto step = [&](int kt, int u) {
+    frags((kt + 1) & 1, na, nb);  // tile kt+1 (a clamped, unused copy past the end)
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const float av = fa[i][s >> 2][s & 3], bv = fb[j][s >> 2][s & 3];
+          if (XC == 2 && (s & 1))
+            acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc2[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i][j], 0, 0, 0);
+        }
+    const int nx = (u + 2) % PF;  // static after unrolling: register set of tile kt+2
+    __builtin_amdgcn_sched_barrier(0);
+    la[nx].store(smem + (kt & 1) * STAGE);
+    lb[nx].store(smem + (kt & 1) * STAGE + SA);
+    la[nx].load(ktile(kt + 2 + PF), kend);
+    lb[nx].load(ktile(kt + 2 + PF), kend);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TM; ++i) { fa[i][0] = na[i][0]; fa[i][1] = na[i][1]; }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) { fb[j][0] = nb[j][0]; fb[j][1] = nb[j][1]; }
+  };
+  int kt = 0;
+  for (; kt + PF <= nk; kt += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) step(kt + u, u);
+  }
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (kt + u < nk) step(kt + u, u);
+  if (XC == 2) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += acc2[i][j];
+  }
+}
+
 // Early-store variant for row-major LDS operands (one register set): iteration kt reads its fragments from
 // LDS[kt&1], stages tile kt+1 (loaded during iteration kt-1, so its loads had a whole MFMA phase to land) into the
 // other buffer, issues the loads of tile kt+2, and only then runs its MFMAs — the loads are in flight under the

@@ -82,6 +82,7 @@ struct APlain : AStage<BM> {
   sd_rsrc rx;
   long ld;
   int m0, M;
+  SD_DEV APlain() = default;
   SD_DEV APlain(const float* X, long ld_, int m0_, int M_, int K) : ld(ld_), m0(m0_), M(M_) {
     rx = sd_make_rsrc(X, ((long)(M - 1) * ld + K) * 4);
   }
@@ -107,6 +108,7 @@ struct ARms : AStage<BM> {
   int m0, M;
   float rr[NV];
   f32x4 wr[NV];
+  SD_DEV ARms() = default;
   SD_DEV ARms(const float* X, long ld_, const float* w_, const float* rs, int m0_, int M_, int K)
       : w(w_), ld(ld_), m0(m0_), M(M_) {
     rx = sd_make_rsrc(X, ((long)(M - 1) * ld + K) * 4);
@@ -147,6 +149,7 @@ struct BRows {
   const float* W;
   long ld;
   int base, seg, stride;
+  SD_DEV BRows() = default;
   SD_DEV BRows(const float* W_, long ld_, int base_, int seg_, int stride_) : W(W_), ld(ld_), base(base_), seg(seg_), stride(stride_) {}
   SD_DEV void load(int k0, int) {
 #pragma unroll
@@ -166,7 +169,8 @@ struct BRows {
       if (256 * (v + 1) <= BN * BK / 4 || i < BN * BK / 4)
         *reinterpret_cast<f32x4*>(lds + (i / (BK / 4)) * LDS_ROW + 4 * (i % (BK / 4))) = r[v];
     }
-  }  SD_DEV void store6(__bf16* lds) const {
+  }
+  SD_DEV void store6(__bf16* lds) const {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int i = threadIdx.x + 256 * v;
@@ -179,12 +183,25 @@ struct BRows {
 // ------------------------------------------------------------------------------------------- contraction
 // F6: the bf16x6 main loop (gemm6_core.h: fp32-accurate, 2.67x the fp32 MFMA rate) instead of v_mfma_f32_16x16x4_f32.
 // ES (early store) applies to the fp32 loop only.
-template <bool F6, int BM, int BN, int WM, int WN, int PF, bool ES = false, class OpA, class OpB>
-SD_DEV void mainloop(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16],
+// FP: the fragment-prefetch loop order (LDS reads of tile k+1 issued ahead of tile k's MFMAs, gemm_core.h
+// gemm16_mainloop_fp). The loaders are built from one prototype into PF register sets.
+template <bool F6, bool FP, int BM, int BN, int WM, int WN, int PF, bool ES = false, class OpA, class OpB>
+SD_DEV void mainloop(const OpA& a0, const OpB& b0, int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16],
                      bool accumulate = false) {
   static_assert(BK == BK6, "tile depth");
-  if constexpr (F6)
+  OpA la[PF];
+  OpB lb[PF];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    la[u] = a0;
+    lb[u] = b0;
+  }
+  if constexpr (F6 && FP)
+    gemm6_mainloop_fp<BM, BN, WM, WN, PF>(la, lb, kbeg, kend, acc, accumulate);
+  else if constexpr (F6)
     gemm6_mainloop_pf<BM, BN, WM, WN, PF>(la, lb, kbeg, kend, acc, accumulate);
+  else if constexpr (FP)
+    gemm16_mainloop_fp<BM, BN, WM, WN, PF>(la, lb, kbeg, kend, acc, accumulate);
   else
     gemm16_mainloop_pf<BM, BN, WM, WN, PF, ES>(la, lb, kbeg, kend, acc, accumulate);
 }
@@ -197,6 +214,16 @@ SD_DEV void mainloop(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend, f32x4 (&a
 #endif
 constexpr bool F6_LIN = SD_IMG_F6 & 1, F6_RMSLIN = SD_IMG_F6 & 2, F6_HID = SD_IMG_F6 & 4, F6_GATE = SD_IMG_F6 & 8,
                F6_PRIOR = SD_IMG_F6 & 16, F6_ACTION = SD_IMG_F6 & 32;
+// fragment-prefetch loop order per kernel (same bit order) and a global prefetch-depth override (0: per-kernel)
+#ifndef SD_IMG_FP
+#define SD_IMG_FP 0b110011
+#endif
+#ifndef SD_IMG_PF
+#define SD_IMG_PF 0
+#endif
+constexpr bool FP_LIN = SD_IMG_FP & 1, FP_RMSLIN = SD_IMG_FP & 2, FP_HID = SD_IMG_FP & 4, FP_GATE = SD_IMG_FP & 8,
+               FP_PRIOR = SD_IMG_FP & 16, FP_ACTION = SD_IMG_FP & 32;
+constexpr int pf_of(int d) { return SD_IMG_PF ? SD_IMG_PF : d; }
 
 // ------------------------------------------------------------------------------------------- epilogue helpers
 // Wave (wr, wc) of a BM x BN tile owns rows wr*16 + 4q + r and columns wc*WN + 16j + l16 (gemm16_mainloop layout).
@@ -209,13 +236,16 @@ SD_DEV Lane lane_ids() {
   return Lane{lane & 15, lane >> 4, wave / (BN / WN), wave % (BN / WN)};
 }
 
-// out[m][n] = acc + bias[n] (+ add[m][n]); part[(n0 + wc*WN)/WN * M + m] = sum over the wave's WN columns of out^2
-template <int BM, int BN, int WN>
+// out[m][n] = acc + bias[n] (+ add[m][n]); part[(n / PW) * M + m] = sum over each PW-column group of out^2 (the
+// consumers' wg_rstd reads width / PW partials per row whatever the producer's tile shape: PW = 32 for the U-wide
+// MLP layers, 64 for dyn_hid). WN % PW == 0.
+template <int BM, int BN, int WN, int PW = 32>
 SD_DEV void ep_bias_part(const f32x4 (&acc)[1][WN / 16], const float* bias, float* out, long ldo, float* part, int M,
                          int m0, int n0, const float* add = nullptr) {
-  constexpr int TN = WN / 16;
+  constexpr int TN = WN / 16, TP = PW / 16;
+  static_assert(WN % PW == 0, "whole row-partial groups per wave");
   const Lane L = lane_ids<BN, WN>();
-  float ss[4] = {0.f, 0.f, 0.f, 0.f};
+  float ss[WN / PW][4] = {};
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + L.wc * WN + 16 * j + L.l16;
@@ -226,15 +256,17 @@ SD_DEV void ep_bias_part(const f32x4 (&acc)[1][WN / 16], const float* bias, floa
       float v = acc[0][j][r] + bv;
       if (add && m < M) v += add[(long)m * ldo + n];
       if (m < M) out[(long)m * ldo + n] = v;
-      ss[r] += v * v;
+      ss[j / TP][r] += v * v;
     }
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float s = group_sum<16>(ss[r]);
-    const int m = m0 + L.wr * 16 + 4 * L.q + r;
-    if (L.l16 == 0 && part && m < M) part[(long)((n0 + L.wc * WN) / WN) * M + m] = s;
-  }
+  for (int p = 0; p < WN / PW; ++p)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float s = group_sum<16>(ss[p][r]);
+      const int m = m0 + L.wr * 16 + 4 * L.q + r;
+      if (L.l16 == 0 && part && m < M) part[(long)((n0 + L.wc * WN) / PW + p) * M + m] = s;
+    }
 }
 
 // ------------------------------------------------------------------------------------------- kernels
@@ -251,6 +283,14 @@ struct LinProb {
   const float* add;  // optional (M, ldo) term added before the row partials (a K-split layer's first part)
 };
 
+// tile of the step's three (N, D) x (D, U) contractions (img_net_0 + _dyn_in0 + actor layer 0's deter part); build-time
+// A/B knobs (tools/ab_variants.sh)
+#ifndef KL3_BM
+#define KL3_BM 32
+#endif
+#ifndef KL3_BN
+#define KL3_BN 64
+#endif
 // grouped plain-A linear layers (N = 256 each): out = A . W^T + b (+ add), with row partials. grid (N/BN, M/BM, nprob)
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2, int M) {
@@ -259,10 +299,8 @@ __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2,
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const APlain<BM> a0(p.A, p.lda, m0, M, p.K);
   const BRows<BN> b0(p.W, p.ldw, n0, BN, 0);
-  APlain<BM> la[3] = {a0, a0, a0};
-  BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][WN / 16];
-  mainloop<F6_LIN, BM, BN, 16, WN, 3>(la, lb, 0, p.K, acc);
+  mainloop<F6_LIN, FP_LIN, BM, BN, 16, WN, pf_of(2)>(a0, b0, 0, p.K, acc);
   ep_bias_part<BM, BN, WN>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
 }
 
@@ -278,10 +316,8 @@ __global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw,
   wg_rstd<BM, 8>(part_in, np, M, m0, K, eps, rs, red);
   const ARms<BM> a0(X, K, nw, rs, m0, M, K);
   const BRows<BN> b0(W, K, n0, BN, 0);
-  ARms<BM> la[3] = {a0, a0, a0};
-  BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][WN / 16];
-  mainloop<F6_RMSLIN, BM, BN, 16, WN, 3, true>(la, lb, 0, K, acc);
+  mainloop<F6_RMSLIN, FP_RMSLIN, BM, BN, 16, WN, pf_of(FP_RMSLIN ? 2 : 3), true>(a0, b0, 0, K, acc);
   ep_bias_part<BM, BN, WN>(acc, bias, out, gridDim.x * BN, part, M, m0, n0);
 }
 
@@ -302,32 +338,24 @@ __global__ __launch_bounds__(256) void k_hid(sd_imagine d, const float* h, long 
   {
     const APlain<BM> a0(h + (long)g * Dg, ldh, m0, M, Dg);
     const BRows<BN> b0(Wseg, Ig, 0, BN, 0);
-    APlain<BM> la[3] = {a0, a0, a0};
-    BRows<BN> lb[3] = {b0, b0, b0};
-    mainloop<F6_HID, BM, BN, 16, WN, 3>(la, lb, 0, Dg, acc);
+    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(3)>(a0, b0, 0, Dg, acc);
   }
   {
     const ARms<BM> a0(x0p, U, d.n0, rs0, m0, M, U);
     const BRows<BN> b0(Wseg + Dg, Ig, 0, BN, 0);
-    ARms<BM> la[3] = {a0, a0, a0};
-    BRows<BN> lb[3] = {b0, b0, b0};
-    mainloop<F6_HID, BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
+    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(3)>(a0, b0, 0, U, acc, true);
   }
   {
     const ARms<BM> a0(x1p, U, d.n1, rs1, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + U, Ig, 0, BN, 0);
-    ARms<BM> la[3] = {a0, a0, a0};
-    BRows<BN> lb[3] = {b0, b0, b0};
-    mainloop<F6_HID, BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
+    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(3)>(a0, b0, 0, U, acc, true);
   }
   {
     const APlain<BM> a0(x2, U, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + 2 * U, Ig, 0, BN, 0);
-    APlain<BM> la[3] = {a0, a0, a0};
-    BRows<BN> lb[3] = {b0, b0, b0};
-    mainloop<F6_HID, BM, BN, 16, WN, 3>(la, lb, 0, U, acc, true);
+    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(3)>(a0, b0, 0, U, acc, true);
   }
-  ep_bias_part<BM, BN, WN>(acc, d.bh, hp, d.D, ph, M, m0, n0);
+  ep_bias_part<BM, BN, WN, 64>(acc, d.bh, hp, d.D, ph, M, m0, n0);
 }
 
 // gates = BlockLinear(dyn_gru)(silu(rms(hp))) + bg; deter' = GRU (rssm.py:65-75) -> feats[t+1][:, SK:].
@@ -341,10 +369,8 @@ __global__ __launch_bounds__(256) void k_gate(sd_imagine d, const float* hp, con
   wg_rstd<BM, 16>(ph, nph, d.N, m0, d.D, d.eps, rs, red);
   const ARms<BM> a0(hp + (long)g * Dg, d.D, d.nh + (long)g * Dg, rs, m0, d.N, Dg);
   const BRows<BN> b0(d.Wg + (long)g * 3 * Dg * Dg, Dg, j0, 32, Dg);
-  ARms<BM> la[2] = {a0, a0};
-  BRows<BN> lb[2] = {b0, b0};
   f32x4 acc[1][6];
-  mainloop<F6_GATE, BM, BN, 16, BN, 2>(la, lb, 0, Dg, acc);
+  mainloop<F6_GATE, FP_GATE, BM, BN, 16, BN, pf_of(2)>(a0, b0, 0, Dg, acc);
   const Lane L = lane_ids<BN, BN>();
   const float* bg = d.bg + (long)g * 3 * Dg;
 #pragma unroll
@@ -378,10 +404,8 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
   wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
   const ARms<BM> a0(X, U, nw, rs, m0, d.N, U);
   const BRows<BN> b0(d.Wl, U, n0, BN, 0);
-  ARms<BM> la[3] = {a0, a0, a0};
-  BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][1];
-  mainloop<F6_PRIOR, BM, BN, 16, WN, 3>(la, lb, 0, U, acc);
+  mainloop<F6_PRIOR, FP_PRIOR, BM, BN, 16, WN, pf_of(FP_PRIOR ? 2 : 3)>(a0, b0, 0, U, acc);
   const Lane L = lane_ids<BN, WN>();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -424,10 +448,8 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
   wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
   const ARms<BM> a0(X, U, nw, rs, m0, d.N, U);
   const BRows<BN> b0(d.Wao, U, 0, BN, 0);  // 32 rows: the caller passes the output weight zero-padded to 32 rows
-  ARms<BM> la[3] = {a0, a0, a0};
-  BRows<BN> lb[3] = {b0, b0, b0};
   f32x4 acc[1][1];
-  mainloop<F6_ACTION, BM, BN, 16, WN, 3>(la, lb, 0, U, acc);
+  mainloop<F6_ACTION, FP_ACTION, BM, BN, 16, WN, pf_of(FP_ACTION ? 2 : 3)>(a0, b0, 0, U, acc);
   const Lane L = lane_ids<BN, WN>();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -565,7 +587,7 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
     LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};
     LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
     LinProb pd{feats(t + 1) + SK, F, D, d.Wa[0] + SK, F, nullptr, w.ad, U, nullptr, nullptr};
-    k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), 3), 256, 0, st>>>(pi, px, pd, N);
+    k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N);
   } else if (which == 1) {
     k_hid<<<dim3(D / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, npU, w.x2, w.hp,
                                                        w.ph);
@@ -626,7 +648,7 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};
       LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
       LinProb pd{feats(t + 1) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
-      k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), 3), 256, 0, st>>>(pi, px, pd, N);
+      k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N);
       SD_LAUNCH_CHECK();
     }
     int ci = 0;

@@ -66,10 +66,11 @@ def main():
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so")
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    for keep_every in (8, 4, 2):
+    for keep_every in (8, 2, -8):
         bits = [0] * ((ncu + 31) // 32)
         for cu in range(ncu):
-            if cu % keep_every != 0:
+            use = (cu % 8 == 0) if keep_every < 0 else (cu % keep_every != 0)  # -8: encoder on 1/8 of the CUs
+            if use:
                 bits[cu // 32] |= 1 << (cu % 32)
         arr = (ctypes.c_uint32 * len(bits))(*bits)
         h = ctypes.c_void_p()
@@ -82,7 +83,8 @@ def main():
         so, eo = timed(enc_work, other)
         s, e = timed(scan, scan_s)
         torch.cuda.synchronize()
-        print(f"cu mask rc={rc}: encoder on {ncu - ncu // keep_every} CUs: x3 alone {alone:.3f} ms; scan beside "
+        used = sum(bin(b).count("1") for b in bits)
+        print(f"cu mask rc={rc}: encoder on {used} CUs: x3 alone {alone:.3f} ms; scan beside "
               f"{s.elapsed_time(e):.3f} ms, encoder x3 beside {so.elapsed_time(eo):.3f} ms", flush=True)
 
 
