@@ -158,7 +158,7 @@ def wm_loss_parity():
 
 
 IMAG_KERNELS = {  # sd_imagine_step_kernel `which` -> (label, FLOP per launch as f(N, D, U, Dg))
-    0: ("k_lin<32, 64> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
+    0: ("k_lin<32, 32> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
         "GEMMs in one launch, RMSNorm row partials in the epilogue; v_mfma_f32_16x16x4_f32)",
         lambda N, D, U, Dg: 3 * 2.0 * N * D * U),
     1: ("k_hid (imagination step: _dyn_hid BlockLinear, K = Dg + 3U per block, RMSNorm + SiLU of x0 / x1 in the A "
@@ -169,7 +169,7 @@ IMAG_KERNELS = {  # sd_imagine_step_kernel `which` -> (label, FLOP per launch as
 
 
 def imag_kernel_probe(agent, cfg, which=0, reps=30):
-    """Roofline probe on the update's dominant kernel symbol, k_lin<32, 64> (imagination; largest total time per
+    """Roofline probe on the update's dominant kernel symbol, k_lin<32, 32> (imagination; largest total time per
     update, profiles/r02_kernel_summary.md): the imagination runs once at the update's shape (N = B*L start rows),
     then its step-t launch is re-issued alone (sd_imagine_step_kernel: same descriptor, workspace and grid) `reps`
     times over t = 0 .. H-1, back to back between two HIP events on the stream it is launched on (per-launch event

@@ -288,7 +288,7 @@ typedef struct sd_imagine {
   int stream_img, stream_act;
   long row_offset;
   const float* Wa[4]; const float* ba[4]; const float* na[4];  /* actor layer i: (U, in_i) (U) (U) */
-  const float *Wao, *bao;                                        /* actor output: (2A or A, U) */
+  const float *Wao, *bao;                  /* actor output: (2A or A, U) rows, zero-padded to 64 rows (the tile reads 64) */
   const float *W0, *b0, *n0, *W1, *b1, *n1, *W2, *b2, *n2;       /* _dyn_in0/1/2 */
   const float *Wh, *bh, *nh, *Wg, *bg;                           /* _dyn_hid (G,Dg,Dg+3U), _dyn_gru (G,3Dg,Dg) */
   const float* Wi[4]; const float* bi[4]; const float* ni[4];    /* img_net layer i */

@@ -224,6 +224,12 @@ constexpr bool F6_LIN = SD_IMG_F6 & 1, F6_RMSLIN = SD_IMG_F6 & 2, F6_HID = SD_IM
 constexpr bool FP_LIN = SD_IMG_FP & 1, FP_RMSLIN = SD_IMG_FP & 2, FP_HID = SD_IMG_FP & 4, FP_GATE = SD_IMG_FP & 8,
                FP_PRIOR = SD_IMG_FP & 16, FP_ACTION = SD_IMG_FP & 32;
 constexpr int pf_of(int d) { return SD_IMG_PF ? SD_IMG_PF : d; }
+#ifndef KH_PF
+#define KH_PF 3
+#endif
+#ifndef KG_PF
+#define KG_PF 2
+#endif
 
 // ------------------------------------------------------------------------------------------- epilogue helpers
 // Wave (wr, wc) of a BM x BN tile owns rows wr*16 + 4q + r and columns wc*WN + 16j + l16 (gemm16_mainloop layout).
@@ -270,6 +276,15 @@ SD_DEV void ep_bias_part(const f32x4 (&acc)[1][WN / 16], const float* bias, floa
 }
 
 // ------------------------------------------------------------------------------------------- kernels
+// XCD-aware column-tile order for the block-diagonal (G blocks) layers: workgroups are dealt to the 8 XCDs round
+// robin by linear id, and gridDim.x is a multiple of 8, so an XCD runs the x = xcd (mod 8) column tiles of every row
+// tile. Mapping x -> tile (x % G) * tpb + x / G puts all tiles of block g = x % G on one XCD (G = 8): that XCD's L2
+// then serves the block's input columns and weights to all of them, instead of every XCD streaming every block.
+SD_DEV int xcd_col(int x, int nx, int tpb) {
+  const int G = nx / tpb;
+  return (x % G) * tpb + x / G;
+}
+
 struct LinProb {
   const float* A;
   long lda;
@@ -289,8 +304,12 @@ struct LinProb {
 #define KL3_BM 32
 #endif
 #ifndef KL3_BN
-#define KL3_BN 64
+#define KL3_BN 32
 #endif
+#ifndef KL_PF
+#define KL_PF 2
+#endif
+constexpr int KL3_WN = KL3_BN / (4 / (KL3_BM / 16)), KL3_PW = KL3_WN < 32 ? KL3_WN : 32;  // its row-partial width
 // grouped plain-A linear layers (N = 256 each): out = A . W^T + b (+ add), with row partials. grid (N/BN, M/BM, nprob)
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2, int M) {
@@ -300,12 +319,17 @@ __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2,
   const APlain<BM> a0(p.A, p.lda, m0, M, p.K);
   const BRows<BN> b0(p.W, p.ldw, n0, BN, 0);
   f32x4 acc[1][WN / 16];
-  mainloop<F6_LIN, FP_LIN, BM, BN, 16, WN, pf_of(2)>(a0, b0, 0, p.K, acc);
-  ep_bias_part<BM, BN, WN>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
+  mainloop<F6_LIN, FP_LIN, BM, BN, 16, WN, pf_of(KL_PF)>(a0, b0, 0, p.K, acc);
+  ep_bias_part<BM, BN, WN, (WN < 32 ? WN : 32)>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
 }
 
 // out = silu(rms(X)) . W^T + b (MLP hidden layer after the first), with row partials
-// early-store main loop order (gemm16_mainloop_pf ES): measured faster here, slower in the other imagination kernels
+// early-store main loop order (gemm16_mainloop_pf ES): measured faster here, slower in the other imagination kernels.
+// Row partials per min(WN, 32) columns (16-row tiles: one wave per 16 columns -> 16-column partials).
+#ifndef KR_BM
+#define KR_BM 16
+#endif
+constexpr int KR_WN = 64 / (4 / (KR_BM / 16)), KR_PW = KR_WN < 32 ? KR_WN : 32;
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw, const float* part_in, int np, int K,
                                                 const float* W, const float* bias, float* out, float* part, int M,
@@ -318,42 +342,42 @@ __global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw,
   const BRows<BN> b0(W, K, n0, BN, 0);
   f32x4 acc[1][WN / 16];
   mainloop<F6_RMSLIN, FP_RMSLIN, BM, BN, 16, WN, pf_of(FP_RMSLIN ? 2 : 3), true>(a0, b0, 0, K, acc);
-  ep_bias_part<BM, BN, WN>(acc, bias, out, gridDim.x * BN, part, M, m0, n0);
+  ep_bias_part<BM, BN, WN, (WN < 32 ? WN : 32)>(acc, bias, out, gridDim.x * BN, part, M, m0, n0);
 }
 
 // hp = BlockLinear(dyn_hid_0)([h_g | x0 | x1 | x2]) + bh with x0 = silu(rms(x0p)), x1 = silu(rms(x1p)) applied by the
 // A loaders (rssm.py:52-63): four main loops over the input segments accumulate into one tile. BM = BN = 64,
 // grid (D/64, M/64); row partials per 64 columns (D/64 of them) for the gate norm.
 __global__ __launch_bounds__(256) void k_hid(sd_imagine d, const float* h, long ldh, const float* x0p, const float* x1p,
-                                             const float* px0, const float* px1, int npx, const float* x2, float* hp,
+                                             const float* px0, const float* px1, int npx0, int npx1, const float* x2, float* hp,
                                              float* ph) {
   constexpr int BM = 64, BN = 64, WN = 64;
   __shared__ float rs0[BM], rs1[BM], red[256];
   const int Dg = d.D / d.G, U = d.U, Ig = Dg + 3 * U, M = d.N;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, g = n0 / Dg;
-  wg_rstd<BM, 8>(px0, npx, M, m0, U, d.eps, rs0, red);
-  wg_rstd<BM, 8>(px1, npx, M, m0, U, d.eps, rs1, red);
+  const int n0 = xcd_col(blockIdx.x, gridDim.x, Dg / BN) * BN, m0 = blockIdx.y * BM, g = n0 / Dg;
+  wg_rstd<BM, 8>(px0, npx0, M, m0, U, d.eps, rs0, red);
+  wg_rstd<BM, 8>(px1, npx1, M, m0, U, d.eps, rs1, red);
   const float* Wseg = d.Wh + (long)n0 * Ig;  // rows n0.. of Wh viewed as (D, Ig)
   f32x4 acc[1][WN / 16];
   {
     const APlain<BM> a0(h + (long)g * Dg, ldh, m0, M, Dg);
     const BRows<BN> b0(Wseg, Ig, 0, BN, 0);
-    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(3)>(a0, b0, 0, Dg, acc);
+    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(KH_PF)>(a0, b0, 0, Dg, acc);
   }
   {
     const ARms<BM> a0(x0p, U, d.n0, rs0, m0, M, U);
     const BRows<BN> b0(Wseg + Dg, Ig, 0, BN, 0);
-    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(3)>(a0, b0, 0, U, acc, true);
+    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(KH_PF)>(a0, b0, 0, U, acc, true);
   }
   {
     const ARms<BM> a0(x1p, U, d.n1, rs1, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + U, Ig, 0, BN, 0);
-    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(3)>(a0, b0, 0, U, acc, true);
+    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(KH_PF)>(a0, b0, 0, U, acc, true);
   }
   {
     const APlain<BM> a0(x2, U, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + 2 * U, Ig, 0, BN, 0);
-    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(3)>(a0, b0, 0, U, acc, true);
+    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(KH_PF)>(a0, b0, 0, U, acc, true);
   }
   ep_bias_part<BM, BN, WN, 64>(acc, d.bh, hp, d.D, ph, M, m0, n0);
 }
@@ -364,13 +388,13 @@ __global__ __launch_bounds__(256) void k_gate(sd_imagine d, const float* hp, con
                                               const float* hold, float* hnew, long ldf) {
   constexpr int BM = 64, BN = 96;
   const int Dg = d.D / d.G;
-  const int c0 = blockIdx.x * 32, m0 = blockIdx.y * BM, g = c0 / Dg, j0 = c0 % Dg;
+  const int c0 = xcd_col(blockIdx.x, gridDim.x, Dg / 32) * 32, m0 = blockIdx.y * BM, g = c0 / Dg, j0 = c0 % Dg;
   __shared__ float rs[BM], red[256];
   wg_rstd<BM, 16>(ph, nph, d.N, m0, d.D, d.eps, rs, red);
   const ARms<BM> a0(hp + (long)g * Dg, d.D, d.nh + (long)g * Dg, rs, m0, d.N, Dg);
   const BRows<BN> b0(d.Wg + (long)g * 3 * Dg * Dg, Dg, j0, 32, Dg);
   f32x4 acc[1][6];
-  mainloop<F6_GATE, FP_GATE, BM, BN, 16, BN, pf_of(2)>(a0, b0, 0, Dg, acc);
+  mainloop<F6_GATE, FP_GATE, BM, BN, 16, BN, pf_of(KG_PF)>(a0, b0, 0, Dg, acc);
   const Lane L = lane_ids<BN, BN>();
   const float* bg = d.bg + (long)g * 3 * Dg;
 #pragma unroll
@@ -434,20 +458,25 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
 
 // actor output layer + action sample (bounded normal: loc = tanh, scale in [min_std, max_std]; or unimix one-hot),
 // action_norm, and the action branch of the next Deter step: x2 = silu(rms(_dyn_in2(a_n))) (rssm.py:40-46).
-// BM = 32, BN = 32 (2A or A <= 32 columns), grid (1, M/32).
+// BM = KA_BM rows (16: 64 workgroups at N = 1,024 — the sampler and the x2 epilogue loop over the tile's rows, so
+// the per-workgroup chain halves against 32-row tiles), BN = 64 / 32 columns (2A or A <= 32 used), grid (1, M/BM).
+#ifndef KA_BM
+#define KA_BM 16
+#endif
+constexpr int KA_BN = KA_BM == 16 ? 64 : 32;  // 4 waves of 16 columns x 16 rows or 2 x 2 waves
 __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, const float* nw, const float* part_in,
                                                 int np, float* act, float* x2, int t, int want_x2) {
-  constexpr int BM = 32, BN = 32, WN = 16;
+  constexpr int BM = KA_BM, BN = KA_BN, WN = 16, RT = 256 / BM;  // RT threads per row in the row-sum pass
   __shared__ float tile[BM][BN + 1];
   __shared__ float an[BM][17];
   __shared__ float xs[BM][257];
-  __shared__ float rsum[BM][9];
+  __shared__ float rsum[BM][RT + 1];
   const int m0 = blockIdx.y * BM, U = d.U, A = d.A;
   const int NO = d.act_discrete ? A : 2 * A;
   __shared__ float rs[BM], red[256];
   wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
   const ARms<BM> a0(X, U, nw, rs, m0, d.N, U);
-  const BRows<BN> b0(d.Wao, U, 0, BN, 0);  // 32 rows: the caller passes the output weight zero-padded to 32 rows
+  const BRows<BN> b0(d.Wao, U, 0, BN, 0);  // BN rows: the caller passes the output weight zero-padded to 64 rows
   f32x4 acc[1][1];
   mainloop<F6_ACTION, FP_ACTION, BM, BN, 16, WN, pf_of(FP_ACTION ? 2 : 3)>(a0, b0, 0, U, acc);
   const Lane L = lane_ids<BN, WN>();
@@ -507,10 +536,10 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
     }
   }
   __syncthreads();
-  {  // row sums of squares: 8 threads per row
-    const int rl = tid / 8, part = tid % 8;
+  {  // row sums of squares: RT threads per row
+    const int rl = tid / RT, part = tid % RT;
     float s = 0.f;
-    for (int c = part; c < U; c += 8) s += xs[rl][c] * xs[rl][c];
+    for (int c = part; c < U; c += RT) s += xs[rl][c] * xs[rl][c];
     rsum[rl][part] = s;
   }
   __syncthreads();
@@ -520,7 +549,7 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
     for (int rl = 0; rl < BM; ++rl) {
       float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s += rsum[rl][k];
+      for (int k = 0; k < RT; ++k) s += rsum[rl][k];
       const float rs = rsqrtf(s / (float)U + d.eps);
       if (m0 + rl < d.N) x2[(long)(m0 + rl) * U + c] = siluf_(xs[rl][c] * rs * wn);
     }
@@ -537,7 +566,7 @@ IWork iwork(const sd_imagine& d, float* base) {
   IWork w;
   long o = 0;
   auto take = [&](long n) { float* p = base ? base + o : nullptr; o += al64(n); return p; };
-  const long NU = (long)d.N * d.U, NP = (long)d.N * (d.U / 32);
+  const long NU = (long)d.N * d.U, NP = (long)d.N * (d.U / 16);  // up to 16-column row partials
   for (int k = 0; k < 2; ++k) { w.a[k] = take(NU); w.pa[k] = take(NP); }
   w.ad = take(NU);
   w.x0p = take(NU); w.px0 = take(NP);
@@ -589,7 +618,7 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
     LinProb pd{feats(t + 1) + SK, F, D, d.Wa[0] + SK, F, nullptr, w.ad, U, nullptr, nullptr};
     k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N);
   } else if (which == 1) {
-    k_hid<<<dim3(D / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, npU, w.x2, w.hp,
+    k_hid<<<dim3(D / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU, w.x2, w.hp,
                                                        w.ph);
   } else {
     // k_gate reads hold = feats(t) deter and writes feats(t + 1) deter: the same values again
@@ -599,7 +628,7 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
   return SD_OK;
 }
 
-// BRows reads BN = 32 rows of the actor output weight: the caller passes Wao padded to 32 rows (zero rows)
+// BRows reads KA_BN <= 64 rows of the actor output weight: the caller passes Wao zero-padded to 64 rows
 extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   int rc = icheck(dp);
   if (rc) return rc;
@@ -608,8 +637,9 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   const IWork w = iwork(d, d.work);
   const int N = d.N, U = d.U, SK = d.SK, D = d.D, F = SK + D;
   const long NF = (long)N * F;
-  const int npU = U / 32;  // row partials per hidden row (k_lin / k_rmslin with BM = 32, BN = 64 -> WN = 32)
-  const dim3 g32(U / 64, sd_cdiv(N, 32));
+  const int npU = U / 32;  // row partials per hidden row written by k_lin<32, 64> (WN = 32)
+  const dim3 gr(U / 64, sd_cdiv(N, KR_BM));
+  const int npR = U / KR_PW;  // row partials written by k_rmslin
   auto feats = [&](int t) { return d.feats + t * NF; };
   // actor layer 0 on feat = [stoch, deter] is K-split: the deter part (no bias) runs in the launch that already
   // reads deter' (img_net_0 / _dyn_in0), the stoch part (+ bias + deter part, row partials) after the prior sample
@@ -618,7 +648,8 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   if (d.t_begin == 0) {  // x0p(0) = h0 . W0^T + b0 and the deter part of actor layer 0 at t = 0
     LinProb p{feats(0) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
     LinProb pd{feats(0) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
-    k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), 2), 256, 0, st>>>(p, pd, pd, N);
+    // the 3-problem launch's tile, so x0p's row partials have one width for every step
+    k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 2), 256, 0, st>>>(p, pd, pd, N);
     SD_LAUNCH_CHECK();
   }
   for (int t = d.t_begin; t < t_end; ++t) {
@@ -629,18 +660,20 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, px, N);
       SD_LAUNCH_CHECK();
     }
-    int cur = 0;
+    int cur = 0, npa = npU;
     for (int l = 1; l < d.actor_layers; ++l) {
-      k_rmslin<32, 64><<<g32, 256, 0, st>>>(w.a[cur], d.na[l - 1], w.pa[cur], npU, U, d.Wa[l], d.ba[l], w.a[cur ^ 1],
-                                            w.pa[cur ^ 1], N, d.eps);
+      k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(w.a[cur], d.na[l - 1], w.pa[cur], npa, U, d.Wa[l], d.ba[l], w.a[cur ^ 1],
+                                              w.pa[cur ^ 1], N, d.eps);
       SD_LAUNCH_CHECK();
       cur ^= 1;
+      npa = npR;
     }
-    k_action<<<dim3(1, sd_cdiv(N, 32)), 256, 0, st>>>(d, w.a[cur], d.na[d.actor_layers - 1], w.pa[cur], npU,
+    k_action<<<dim3(1, sd_cdiv(N, KA_BM)), 256, 0, st>>>(d, w.a[cur], d.na[d.actor_layers - 1], w.pa[cur], npa,
                                               d.actions + (long)t * N * d.A, w.x2, t, last ? 0 : 1);
     SD_LAUNCH_CHECK();
     if (last) break;
-    k_hid<<<dim3(D / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, npU, w.x2, w.hp, w.ph);
+    k_hid<<<dim3(D / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU,
+                                                         w.x2, w.hp, w.ph);
     SD_LAUNCH_CHECK();
     k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / 64, feats(t) + SK, feats(t + 1) + SK, F);
     SD_LAUNCH_CHECK();
@@ -651,18 +684,19 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N);
       SD_LAUNCH_CHECK();
     }
-    int ci = 0;
+    int ci = 0, npi = U / KL3_PW;
     for (int l = 1; l < d.img_layers; ++l) {
-      k_rmslin<32, 64><<<g32, 256, 0, st>>>(w.i[ci], d.ni[l - 1], w.pi[ci], npU, U, d.Wi[l], d.bi[l], w.i[ci ^ 1],
-                                            w.pi[ci ^ 1], N, d.eps);
+      k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(w.i[ci], d.ni[l - 1], w.pi[ci], npi, U, d.Wi[l], d.bi[l], w.i[ci ^ 1],
+                                              w.pi[ci ^ 1], N, d.eps);
       SD_LAUNCH_CHECK();
       ci ^= 1;
+      npi = npR;
     }
     if (d.Kd == 16)
-      k_prior<16><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npU,
+      k_prior<16><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi,
                                                           feats(t + 1), F, t);
     else
-      k_prior<32><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npU,
+      k_prior<32><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi,
                                                           feats(t + 1), F, t);
     SD_LAUNCH_CHECK();
   }

@@ -1022,7 +1022,7 @@ class Dreamer(nn.Module):
         for i, (lin, norm) in enumerate(a.mlp._mods):
             d.Wa[i], d.ba[i], d.na[i] = lin.weight.data_ptr(), lin.bias.data_ptr(), norm.weight.data_ptr()
         wo = a.last.weight
-        wpad = torch.zeros(32, wo.shape[1], dtype=torch.float32, device=wo.device)  # the action tile reads 32 rows
+        wpad = torch.zeros(64, wo.shape[1], dtype=torch.float32, device=wo.device)  # the action tile reads 64 rows
         wpad[:wo.shape[0]] = wo
         d.Wao, d.bao = wpad.data_ptr(), a.last.bias.data_ptr()
         for k in ("W0", "b0", "n0", "W1", "b1", "n1", "W2", "b2", "n2", "Wh", "bh", "nh", "Wg", "bg"):

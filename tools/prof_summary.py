@@ -38,8 +38,8 @@ def probe_rows(path, name_like="conv_fwd_direct_poolILi48E", grid=(8192, 1, 1)):
 def main(path, top=40, per=1):
     rows = from_db(path) if path.endswith(".db") else from_csv(path)
     if path.endswith(".db"):
-        for label, pat, grid in (("roofline kernel k_lin<32, 64> x3 (imagination, grid 4x32x3)", "k_linILi32ELi64E",
-                                  (4, 32, 3)),
+        for label, pat, grid in (("roofline kernel k_lin<32, 32> x3 (imagination, grid 8x32x3)", "k_linILi32ELi32E",
+                                  (8, 32, 3)),
                                  ("secondary conv_fwd_direct_pool<48> (encoder stage 2, 8192 workgroups)",
                                   "conv_fwd_direct_poolILi48E", (8192, 1, 1))):
             pr = probe_rows(path, pat, grid)

@@ -12,8 +12,8 @@ import sys
 
 N, D, U, DG = 1024, 2048, 256, 256
 KERNELS = {  # key: (name substring of the demangled symbol, grid filter (wg_x, wg_y, wg_z) or None, algorithmic bytes)
-    "k_lin": ("k_lin<32, 64>", (U // 64, N // 32, 3),
-              4.0 * (N * D + 3 * U * D + 3 * N * U + 2 * (U // 32) * N)),  # deter' + 3 W + 3 outputs + row partials
+    "k_lin": ("k_lin<32, 32>", (U // 32, N // 32, 3),
+              4.0 * (N * D + 3 * U * D + 3 * N * U + 2 * (U // 16) * N)),  # deter' + 3 W + 3 outputs + row partials
     "k_hid": ("k_hid(sd_imagine", None,
               4.0 * (N * D + 3 * N * U + D * (DG + 3 * U) + N * D + N * D // 64)),  # h, x0/x1/x2, W, hp, partials
     "k_gate": ("k_gate(sd_imagine", None, 4.0 * (N * D + 3 * D * DG + 2 * N * D)),  # hp, W, hold, deter'
