@@ -37,6 +37,10 @@ from .rssm import RSSM, STREAM_ACT, STREAM_IMG, STREAM_OBS_AUG, STREAM_POLICY, S
 # SDREAMER_S2_AFTER_SCAN=1 (schedule knob): the actor/critic phase starts after the scan backward (beside the encoder
 # backward) instead of right after the replay-value backward (beside the scan backward)
 S2_AFTER_SCAN = os.environ.get("SDREAMER_S2_AFTER_SCAN", "0") == "1"
+# graphed update, opt-in: the world-model heads' weight-gradient contractions leave phase M1 (which runs beside the
+# imagination and slows it) for phase M2d on main after the encoder backward. Measured: the imagination got 0.27 ms
+# faster but M2d (0.68 ms) outgrew the join slack it fills: 13.59 vs 13.34 ms per update, so off by default.
+DEFER_WM = os.environ.get("SDREAMER_DEFER_WM", "0") == "1"
 # SDREAMER_FUSED_SAMPLE=0: replayed updates sample through Buffer.sample() + copies instead of sample_into (A/B knob)
 FUSED_SAMPLE = os.environ.get("SDREAMER_FUSED_SAMPLE", "1") != "0"
 
@@ -502,20 +506,21 @@ class Dreamer(nn.Module):
 
             gP, st = cap(lambda: self._core_forward(self._g_in, self._g_init, self._seed_dev, ro), main_cap)
             gS1, _ = cap(lambda: self._ph_side_returns(st), side_cap)
-            gM1, _ = cap(lambda: self._ph_wm(st), main_cap)
+            gM1, _ = cap(lambda: self._ph_wm(st, defer=DEFER_WM), main_cap)
             gR, _ = cap(lambda: self._ph_repval(st), main_cap)
             gM2a, _ = cap(lambda: self._ph_scan_bwd(st, defer=True), main_cap)
             gS3, _ = cap(lambda: self._flush(st["scan_wgrads"], "side:scan_wgrads"), side_cap)
             gM2b, _ = cap(lambda: self._ph_encoder_bwd_hi(st, defer=True), main_cap)
             gS4, _ = cap(lambda: self._flush(st["enc_wgrads"], "side:enc_wgrads"), side_cap)
             gM2c, _ = cap(lambda: self._ph_encoder_bwd_lo(st), main_cap)
+            gM2d, _ = cap(lambda: self._flush(st.get("wm_wgrads", []), "wm_wgrads"), main_cap)
             gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
             gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st), main_cap)
             torch.cuda.synchronize()
-            for g in (gP, gR, gM2a, gS3, gM2b, gS4, gM2c, gM3):
+            for g in (gP, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gM3):
                 if g.n_collectives:
                     raise RuntimeError("unexpected exchange step in a single-graph phase")
-            self._graph = (gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gS2, gM3)
+            self._graph = (gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gS2, gM3)
             self._gst, self._g_post, self._g_keys, self._g_mvec = st, post, keys, mvec
         if data is not None:
             for k, v in data.items():
@@ -526,7 +531,7 @@ class Dreamer(nn.Module):
         if self.rep_loss == "dreamerpro":
             self._ema_updates += 1
             self._proto_gate.fill_(0.0 if self._protos_frozen() else 1.0)
-        gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gS2, gM3 = self._graph
+        gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gS2, gM3 = self._graph
         main = torch.cuda.current_stream()
         side = self._side if self.use_side_stream else main
         gP.replay()
@@ -539,7 +544,7 @@ class Dreamer(nn.Module):
         dp = self.world > 1
         if dp and self._comm is None:
             self._comm = torch.cuda.Stream(device=self.device)
-        if dp:  # heads bucket final after M1
+        if dp and not DEFER_WM:  # heads bucket final after M1 (else after M2d)
             ev_m1 = torch.cuda.Event()
             ev_m1.record()
             self._allreduce_bucket("heads", ev_m1)
@@ -560,6 +565,7 @@ class Dreamer(nn.Module):
         ev_enc = torch.cuda.Event()
         ev_enc.record()
         gM2c.replay()
+        gM2d.replay()
         ev_side = [None, None]
         with torch.cuda.stream(side):
             side.wait_event(ev_rep)
@@ -575,11 +581,16 @@ class Dreamer(nn.Module):
             side.wait_event(ev_enc)  # S4: encoder stages 2..'s weight gradients, beside the first stage's backward
             gS4.replay()
         if dp:  # bucketed sum all-reduce of the gradient arena, overlapping the backward phases still running
-            self._allreduce_bucket("ac", ev_side[0])
-            self._allreduce_bucket("rssm", ev_side[1])
             ev_main, ev_s4 = torch.cuda.Event(), torch.cuda.Event()
             ev_main.record(main)
+            self._allreduce_bucket("ac", ev_side[0])
+            if DEFER_WM:  # the prior's img_net weight gradients are in M2d: the RSSM bucket also waits for main
+                self._allreduce_bucket("rssm", ev_side[1], ev_main)
+            else:
+                self._allreduce_bucket("rssm", ev_side[1])
             ev_s4.record(side)
+            if DEFER_WM:
+                self._allreduce_bucket("heads", ev_main)
             self._allreduce_bucket("rest", ev_main, ev_s4)
         if side is not main:
             main.wait_stream(side)
@@ -677,12 +688,15 @@ class Dreamer(nn.Module):
         self._mark("side:heads_returns")
         st.update(ifeat=ifeat, iact=iact, rr=rr)
 
-    def _ph_wm(self, st):
+    def _ph_wm(self, st, defer=False):
         """main: world-model head losses and their backward down to the posterior leaves; the replay-value parts
-        that do not need the imagined returns."""
-        st["wm_total"], st["wm_losses"], st["wm_metrics"] = self._wm_heads(st["data"], st["embed"], st["leaves"],
-                                                                           st["feat_l"], st["seed"], st["ro"],
-                                                                           st["initial"])
+        that do not need the imagined returns. defer: the heads' weight-gradient contractions are queued in
+        st["wm_wgrads"] (graphed update: phase M2d)."""
+        st["wm_wgrads"] = []
+        with ops.defer_wgrads(st["wm_wgrads"] if defer else None):
+            st["wm_total"], st["wm_losses"], st["wm_metrics"] = self._wm_heads(st["data"], st["embed"], st["leaves"],
+                                                                               st["feat_l"], st["seed"], st["ro"],
+                                                                               st["initial"])
         self._mark("wm_heads")
         st["rv"] = self._repval_pre(st["data"], st["feat_r"])
         self._mark("repval_fwd")
