@@ -278,9 +278,15 @@ def phase_rooflines(agent, cfg, cfg_name, ms_update, reps=10):
                         "achieved": f_img / (ms_img * 1e-3) / 1e12, "peak": 157.3, "unit": "TFLOP/s",
                         "frac": f_img / (ms_img * 1e-3) / 1e12 / 157.3, "work": f_img,
                         "what": f"_imagine_tm: N={N} start rows, H={H} img_steps + {H + 1} actor samples, alone"},
-        "observe_scan": {"bound": "hbm", "ms": ms_obs, "achieved": b_obs / (ms_obs * 1e-3) / 1e9, "peak": 8000.0,
-                         "unit": "GB/s", "frac": b_obs / (ms_obs * 1e-3) / 1e9 / 8000.0, "work": b_obs,
-                         "what": f"RSSM.observe forward, B={B} L={L}: Deter + obs_net weights once per step"},
+        # the weights stream from L2/MALL, so the HBM fraction is no bound; the real bound is the dependent launch
+        # chain: 5 fused launches per step, each >= one kernel boundary (1.45 us between trivial kernels,
+        # MI355X_MICROARCH.md price list row 'boundary') plus its dependent prologue load (~1 us, an L2 round trip)
+        "observe_scan": {"bound": "launch latency", "ms": ms_obs, "launches": 5 * L,
+                         "latency_floor_ms": 5 * L * (1.45 + 1.0) * 1e-3,
+                         "frac": 5 * L * (1.45 + 1.0) * 1e-3 / ms_obs,
+                         "weight_stream_GBps": b_obs / (ms_obs * 1e-3) / 1e9, "work": b_obs,
+                         "what": f"RSSM.observe forward, B={B} L={L}: 5 dependent launches per step; weight bytes "
+                                 "(Deter + obs_net once per step) over the phase time as weight_stream_GBps"},
     }
     if f_upd:  # only where the update's FLOP were counted on the reference
         out["update"] = {"bound": "mfma", "achieved": f_upd / (ms_update * 1e-3) / 1e12, "peak": 157.3,

@@ -284,6 +284,23 @@ SD_DEV int xcd_col(int x, int nx, int tpb) {
   const int G = nx / tpb;
   return (x % G) * tpb + x / G;
 }
+// XCD-aware tile order for the grouped plain GEMMs (k_lin, grid (col tiles, row tiles, problems)): the 8 XCDs form a
+// 4 (row groups) x 2 (column groups over all problems) grid, so an XCD's L2 serves a quarter of A and half of the
+// weights instead of all of A (dispatch order deals linear ids round robin to the XCDs). Identity when the grid does
+// not split that way.
+#ifndef KL_XCD
+#define KL_XCD 1
+#endif
+SD_DEV void xcd_tile(int& tx, int& ty, int& tz) {
+  const int nx = gridDim.x, ny = gridDim.y, cols = nx * gridDim.z;
+  if (ny % 4 || cols % 2) return;
+  const int id = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), xcd = id % 8, slot = id / 8;
+  const int R4 = ny / 4, C2 = cols / 2;
+  const int row = (xcd >> 1) * R4 + slot % R4, col = (xcd & 1) * C2 + slot / R4;
+  tx = col % nx;
+  ty = row;
+  tz = col / nx;
+}
 
 struct LinProb {
   const float* A;
@@ -314,8 +331,10 @@ constexpr int KL3_WN = KL3_BN / (4 / (KL3_BM / 16)), KL3_PW = KL3_WN < 32 ? KL3_
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2, int M) {
   constexpr int WN = BN / (4 / (BM / 16));
-  const LinProb p = blockIdx.z == 0 ? p0 : (blockIdx.z == 1 ? p1 : p2);
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
+  if (KL_XCD) xcd_tile(tx, ty, tz);
+  const LinProb p = tz == 0 ? p0 : (tz == 1 ? p1 : p2);
+  const int n0 = tx * BN, m0 = ty * BM;
   const APlain<BM> a0(p.A, p.lda, m0, M, p.K);
   const BRows<BN> b0(p.W, p.ldw, n0, BN, 0);
   f32x4 acc[1][WN / 16];
