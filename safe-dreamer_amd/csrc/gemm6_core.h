@@ -126,6 +126,78 @@ SD_DEV void gemm6_mainloop_pf(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend, 
     if (kt + u < nk) step(kt + u, u);
 }
 
+// Single-stage form: half the LDS of gemm6_mainloop_pf (one staging buffer), two barriers per k tile (stage ->
+// barrier -> fragment reads -> barrier -> MFMAs, which run from registers while the next tile is staged). For
+// launches whose double-buffered LDS footprint would cap residency below the grid (k_gate: 2 -> 4 workgroups per CU,
+// its 1,024 workgroups in one round instead of two).
+template <int BM, int BN, int WM, int WN, int PF, class OpA, class OpB>
+SD_DEV void gemm6_mainloop_1s(OpA (&la)[PF], OpB (&lb)[PF], int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16],
+                              bool accumulate = false) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+  constexpr int SA = BM * LROW6, STAGE = (BM + BN) * LROW6;
+  __bf16* smem = sd_smem6<STAGE>();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  const int l16 = lane & 15, q = lane >> 4;
+  if (!accumulate) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int nk = (kend - kbeg + BK6 - 1) / BK6;
+  if (nk <= 0) return;
+  auto ktile = [&](int t) { return kbeg + (t < nk ? t : nk - 1) * BK6; };
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    la[u].load(ktile(u), kend);
+    lb[u].load(ktile(u), kend);
+  }
+  auto step = [&](int kt, int u) {
+    la[u].store6(smem);
+    lb[u].store6(smem + SA);
+    la[u].load(ktile(kt + PF), kend);
+    lb[u].load(ktile(kt + PF), kend);
+    __syncthreads();
+    bf16x8 a[TM][3], b[TN][3];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const __bf16* p = smem + (wr * WM + 16 * i + l16) * LROW6 + 8 * q;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) a[i][s] = *reinterpret_cast<const bf16x8*>(p + s * BK6);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const __bf16* p = smem + SA + (wc * WN + 16 * j + l16) * LROW6 + 8 * q;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) b[j][s] = *reinterpret_cast<const bf16x8*>(p + s * BK6);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x4 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], c, 0, 0, 0);
+      }
+  };
+  int kt = 0;
+  for (; kt + PF <= nk; kt += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) step(kt + u, u);
+  }
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (kt + u < nk) step(kt + u, u);
+}
+
 // Fragment-prefetch form (gemm_core.h gemm16_mainloop_fp): iteration kt reads tile kt+1's three planes from LDS
 // before running tile kt's MFMAs on fragments read one iteration earlier, then stores tile kt+2 into stage kt&1.
 template <int BM, int BN, int WM, int WN, int PF, class OpA, class OpB>

@@ -225,10 +225,13 @@ constexpr bool FP_LIN = SD_IMG_FP & 1, FP_RMSLIN = SD_IMG_FP & 2, FP_HID = SD_IM
                FP_PRIOR = SD_IMG_FP & 16, FP_ACTION = SD_IMG_FP & 32;
 constexpr int pf_of(int d) { return SD_IMG_PF ? SD_IMG_PF : d; }
 #ifndef KH_PF
-#define KH_PF 3
+#define KH_PF 1
 #endif
 #ifndef KG_PF
-#define KG_PF 2
+#define KG_PF 1
+#endif
+#ifndef KG_1S  // k_gate on the single-stage bf16x6 loop (gemm6_core.h gemm6_mainloop_1s)
+#define KG_1S 1
 #endif
 
 // ------------------------------------------------------------------------------------------- epilogue helpers
@@ -364,13 +367,40 @@ __global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw,
   ep_bias_part<BM, BN, WN, (WN < 32 ? WN : 32)>(acc, bias, out, gridDim.x * BN, part, M, m0, n0);
 }
 
+// k_hid tiling knobs: 64 or 32 rows per workgroup, single-stage LDS loop, register budget (waves per SIMD)
+#ifndef KH_BM
+#define KH_BM 64
+#endif
+#ifndef KH_1S
+#define KH_1S 1
+#endif
+#ifndef KH_WAVES
+#define KH_WAVES 2
+#endif
+constexpr int KH_WN = 64 / (4 / (KH_BM / 16)), KH_PW = KH_WN < 64 ? KH_WN : 64;  // hp row-partial width
+template <int BM, int BN, int WN, class OpA, class OpB>
+SD_DEV void hid_seg(const OpA& a0, const OpB& b0, int K, f32x4 (&acc)[1][WN / 16], bool accumulate) {
+  if constexpr (KH_1S && F6_HID) {
+    OpA la[KH_PF];
+    OpB lb[KH_PF];
+#pragma unroll
+    for (int u = 0; u < KH_PF; ++u) {
+      la[u] = a0;
+      lb[u] = b0;
+    }
+    gemm6_mainloop_1s<BM, BN, 16, WN, KH_PF>(la, lb, 0, K, acc, accumulate);
+  } else {
+    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(KH_PF)>(a0, b0, 0, K, acc, accumulate);
+  }
+}
+
 // hp = BlockLinear(dyn_hid_0)([h_g | x0 | x1 | x2]) + bh with x0 = silu(rms(x0p)), x1 = silu(rms(x1p)) applied by the
 // A loaders (rssm.py:52-63): four main loops over the input segments accumulate into one tile. BM = BN = 64,
 // grid (D/64, M/64); row partials per 64 columns (D/64 of them) for the gate norm.
-__global__ __launch_bounds__(256) void k_hid(sd_imagine d, const float* h, long ldh, const float* x0p, const float* x1p,
+__global__ __launch_bounds__(256, KH_WAVES) void k_hid(sd_imagine d, const float* h, long ldh, const float* x0p, const float* x1p,
                                              const float* px0, const float* px1, int npx0, int npx1, const float* x2, float* hp,
                                              float* ph) {
-  constexpr int BM = 64, BN = 64, WN = 64;
+  constexpr int BM = KH_BM, BN = 64, WN = BN / (4 / (BM / 16));
   __shared__ float rs0[BM], rs1[BM], red[256];
   const int Dg = d.D / d.G, U = d.U, Ig = Dg + 3 * U, M = d.N;
   const int n0 = xcd_col(blockIdx.x, gridDim.x, Dg / BN) * BN, m0 = blockIdx.y * BM, g = n0 / Dg;
@@ -381,29 +411,32 @@ __global__ __launch_bounds__(256) void k_hid(sd_imagine d, const float* h, long 
   {
     const APlain<BM> a0(h + (long)g * Dg, ldh, m0, M, Dg);
     const BRows<BN> b0(Wseg, Ig, 0, BN, 0);
-    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(KH_PF)>(a0, b0, 0, Dg, acc);
+    hid_seg<BM, BN, WN>(a0, b0, Dg, acc, false);
   }
   {
     const ARms<BM> a0(x0p, U, d.n0, rs0, m0, M, U);
     const BRows<BN> b0(Wseg + Dg, Ig, 0, BN, 0);
-    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(KH_PF)>(a0, b0, 0, U, acc, true);
+    hid_seg<BM, BN, WN>(a0, b0, U, acc, true);
   }
   {
     const ARms<BM> a0(x1p, U, d.n1, rs1, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + U, Ig, 0, BN, 0);
-    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(KH_PF)>(a0, b0, 0, U, acc, true);
+    hid_seg<BM, BN, WN>(a0, b0, U, acc, true);
   }
   {
     const APlain<BM> a0(x2, U, m0, M, U);
     const BRows<BN> b0(Wseg + Dg + 2 * U, Ig, 0, BN, 0);
-    mainloop<F6_HID, FP_HID, BM, BN, 16, WN, pf_of(KH_PF)>(a0, b0, 0, U, acc, true);
+    hid_seg<BM, BN, WN>(a0, b0, U, acc, true);
   }
-  ep_bias_part<BM, BN, WN, 64>(acc, d.bh, hp, d.D, ph, M, m0, n0);
+  ep_bias_part<BM, BN, WN, KH_PW>(acc, d.bh, hp, d.D, ph, M, m0, n0);
 }
 
 // gates = BlockLinear(dyn_gru)(silu(rms(hp))) + bg; deter' = GRU (rssm.py:65-75) -> feats[t+1][:, SK:].
 // Tile: 64 rows x (r | c | u) for 32 deter columns of block g (BN = 96). grid (D/32, M/64)
-__global__ __launch_bounds__(256) void k_gate(sd_imagine d, const float* hp, const float* ph, int nph,
+#ifndef KG_WAVES  // minimum waves per SIMD for k_gate's register allocation (occupancy; its LDS admits 4 per CU)
+#define KG_WAVES 4
+#endif
+__global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const float* hp, const float* ph, int nph,
                                               const float* hold, float* hnew, long ldf) {
   constexpr int BM = 64, BN = 96;
   const int Dg = d.D / d.G;
@@ -413,7 +446,18 @@ __global__ __launch_bounds__(256) void k_gate(sd_imagine d, const float* hp, con
   const ARms<BM> a0(hp + (long)g * Dg, d.D, d.nh + (long)g * Dg, rs, m0, d.N, Dg);
   const BRows<BN> b0(d.Wg + (long)g * 3 * Dg * Dg, Dg, j0, 32, Dg);
   f32x4 acc[1][6];
-  mainloop<F6_GATE, FP_GATE, BM, BN, 16, BN, pf_of(KG_PF)>(a0, b0, 0, Dg, acc);
+  if constexpr (KG_1S && F6_GATE) {
+    ARms<BM> la[KG_PF];
+    BRows<BN> lb[KG_PF];
+#pragma unroll
+    for (int u = 0; u < KG_PF; ++u) {
+      la[u] = a0;
+      lb[u] = b0;
+    }
+    gemm6_mainloop_1s<BM, BN, 16, BN, KG_PF>(la, lb, 0, Dg, acc);
+  } else {
+    mainloop<F6_GATE, FP_GATE, BM, BN, 16, BN, pf_of(KG_PF)>(a0, b0, 0, Dg, acc);
+  }
   const Lane L = lane_ids<BN, BN>();
   const float* bg = d.bg + (long)g * 3 * Dg;
 #pragma unroll
@@ -592,7 +636,7 @@ IWork iwork(const sd_imagine& d, float* base) {
   w.x1p = take(NU); w.px1 = take(NP);
   w.x2 = take(NU);
   w.hp = take((long)d.N * d.D);
-  w.ph = take((long)d.N * (d.D / 64));
+  w.ph = take((long)d.N * (d.D / 32));
   for (int k = 0; k < 2; ++k) { w.i[k] = take(NU); w.pi[k] = take(NP); }
   w.total = o;
   return w;
@@ -637,11 +681,11 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
     LinProb pd{feats(t + 1) + SK, F, D, d.Wa[0] + SK, F, nullptr, w.ad, U, nullptr, nullptr};
     k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N);
   } else if (which == 1) {
-    k_hid<<<dim3(D / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU, w.x2, w.hp,
+    k_hid<<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU, w.x2, w.hp,
                                                        w.ph);
   } else {
     // k_gate reads hold = feats(t) deter and writes feats(t + 1) deter: the same values again
-    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / 64, feats(t) + SK, feats(t + 1) + SK, F);
+    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F);
   }
   SD_LAUNCH_CHECK();
   return SD_OK;
@@ -691,10 +735,10 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
                                               d.actions + (long)t * N * d.A, w.x2, t, last ? 0 : 1);
     SD_LAUNCH_CHECK();
     if (last) break;
-    k_hid<<<dim3(D / 64, sd_cdiv(N, 64)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU,
+    k_hid<<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU,
                                                          w.x2, w.hp, w.ph);
     SD_LAUNCH_CHECK();
-    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / 64, feats(t) + SK, feats(t + 1) + SK, F);
+    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F);
     SD_LAUNCH_CHECK();
     {  // img_net_0, the next step's _dyn_in0 and the deter part of its actor layer 0 share A = deter'
       LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};

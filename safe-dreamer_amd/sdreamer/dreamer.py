@@ -513,12 +513,12 @@ class Dreamer(nn.Module):
             gM2b, _ = cap(lambda: self._ph_encoder_bwd_hi(st, defer=True), main_cap)
             gS4, _ = cap(lambda: self._flush(st["enc_wgrads"], "side:enc_wgrads"), side_cap)
             gM2c, _ = cap(lambda: self._ph_encoder_bwd_lo(st), main_cap)
-            gM2d, _ = cap(lambda: self._flush(st.get("wm_wgrads", []), "wm_wgrads"), main_cap)
+            gM2d = cap(lambda: self._flush(st["wm_wgrads"], "wm_wgrads"), main_cap)[0] if DEFER_WM else None
             gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
             gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st), main_cap)
             torch.cuda.synchronize()
             for g in (gP, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gM3):
-                if g.n_collectives:
+                if g is not None and g.n_collectives:
                     raise RuntimeError("unexpected exchange step in a single-graph phase")
             self._graph = (gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gS2, gM3)
             self._gst, self._g_post, self._g_keys, self._g_mvec = st, post, keys, mvec
@@ -565,7 +565,8 @@ class Dreamer(nn.Module):
         ev_enc = torch.cuda.Event()
         ev_enc.record()
         gM2c.replay()
-        gM2d.replay()
+        if gM2d is not None:
+            gM2d.replay()
         ev_side = [None, None]
         with torch.cuda.stream(side):
             side.wait_event(ev_rep)
