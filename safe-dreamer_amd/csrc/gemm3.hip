@@ -10,6 +10,10 @@
 namespace {
 using namespace sdb;
 
+#ifndef SD_G3_FP  // fragment-prefetch main loop (gemm3_core.h gemm3_mainloop_fp): measured no faster (4096^3 536 vs 540 us, update 13.85 vs 13.76 ms), off
+#define SD_G3_FP 0
+#endif
+
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool VA, bool VB>
 __global__ __launch_bounds__(256, 2) void gemm3_kernel(GemmArgs g) {
   const int bn0 = blockIdx.x * BN, bm0 = blockIdx.y * BM;
@@ -23,7 +27,10 @@ __global__ __launch_bounds__(256, 2) void gemm3_kernel(GemmArgs g) {
   OA la(A, g.lda, g.M, bm0);
   OB lb(Bp, g.ldb, g.N, bn0);
   f32x4 acc[WM / 16][WN / 16];
-  gemm3_mainloop<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
+  if (SD_G3_FP)
+    gemm3_mainloop_fp<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
+  else
+    gemm3_mainloop<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
   gemm3_epilogue<BM, BN, WM, WN>(g, acc, bm0, bn0, b, split);
 }
 

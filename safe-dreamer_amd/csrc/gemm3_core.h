@@ -184,6 +184,84 @@ SD_DEV void gemm3_mainloop(OpA& la, OpB& lb, int kbeg, int kend, f32x4 (&acc)[WM
   }
 }
 
+// Fragment-prefetch form (gemm_core.h gemm16_mainloop_fp): iteration kt reads tile kt+1's fragments from LDS before
+// its MFMAs on tile kt (read one iteration earlier), then stages tile kt+2 into the stage tile kt came from and
+// issues tile kt+3's loads. Branch-free (clamped tile indices); unrolled by two so the fragment sets swap roles
+// instead of being copied.
+template <int BM, int BN, int WM, int WN, class OpA, class OpB>
+SD_DEV void gemm3_mainloop_fp(OpA& la, OpB& lb, int kbeg, int kend, f32x4 (&acc)[WM / 16][WN / 16]) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+  constexpr int SA = BM * LROW, STAGE = (BM + BN) * LROW;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  const int l16 = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk <= 0) return;
+  auto ktile = [&](int t) { return kbeg + (t < nk ? t : nk - 1) * BK; };
+  struct Frags {
+    bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+  };
+  auto frags = [&](int stage, Frags& f) {
+    const __bf16* cur = smem + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const __bf16* p = cur + (wr * WM + 16 * i + l16) * LROW + 8 * q;
+      f.ah[i] = *reinterpret_cast<const bf16x8*>(p);
+      f.al[i] = *reinterpret_cast<const bf16x8*>(p + BK);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const __bf16* p = cur + SA + (wc * WN + 16 * j + l16) * LROW + 8 * q;
+      f.bh[j] = *reinterpret_cast<const bf16x8*>(p);
+      f.bl[j] = *reinterpret_cast<const bf16x8*>(p + BK);
+    }
+  };
+  Frags f0, f1;
+  la.load(ktile(0), kend);
+  lb.load(ktile(0), kend);
+  la.store(smem);
+  lb.store(smem + SA);
+  la.load(ktile(1), kend);
+  lb.load(ktile(1), kend);
+  __syncthreads();
+  frags(0, f0);
+  la.store(smem + STAGE);
+  lb.store(smem + STAGE + SA);
+  la.load(ktile(2), kend);
+  lb.load(ktile(2), kend);
+  __syncthreads();
+  auto step = [&](int kt, const Frags& f, Frags& nf) {
+    frags((kt + 1) & 1, nf);  // tile kt+1 (a clamped, unused copy past the end)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.al[i], f.bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.ah[i], f.bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.ah[i], f.bh[j], acc[i][j], 0, 0, 0);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    la.store(smem + (kt & 1) * STAGE);  // tile kt+2
+    lb.store(smem + (kt & 1) * STAGE + SA);
+    la.load(ktile(kt + 3), kend);
+    lb.load(ktile(kt + 3), kend);
+    __syncthreads();
+  };
+  int kt = 0;
+  for (; kt + 2 <= nk; kt += 2) {
+    step(kt, f0, f1);
+    step(kt + 1, f1, f0);
+  }
+  if (kt < nk) step(kt, f0, f1);
+}
+
 // C tile epilogue (alpha, bias, beta; or a split-K partial slab)
 template <int BM, int BN, int WM, int WN>
 SD_DEV void gemm3_epilogue(const GemmArgs& g, const f32x4 (&acc)[WM / 16][WN / 16], int bm0, int bn0, int b,
