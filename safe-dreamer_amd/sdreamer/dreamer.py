@@ -694,6 +694,8 @@ class Dreamer(nn.Module):
         that do not need the imagined returns. defer: the heads' weight-gradient contractions are queued in
         st["wm_wgrads"] (graphed update: phase M2d)."""
         st["wm_wgrads"] = []
+        # the scan backward's transposed weights, while main has slack (it waits for the imagined returns next)
+        st["scan_tr"] = self.rssm._bwd_tr = self.rssm.scan_bwd_weights()
         with ops.defer_wgrads(st["wm_wgrads"] if defer else None):
             st["wm_total"], st["wm_losses"], st["wm_metrics"] = self._wm_heads(st["data"], st["embed"], st["leaves"],
                                                                                st["feat_l"], st["seed"], st["ro"],
@@ -736,6 +738,7 @@ class Dreamer(nn.Module):
                                         [g_stoch, g_deter, lg[2]])
         else:
             torch.autograd.backward([st["post_stoch"], st["post_deter"], st["post_logit"]], [g_stoch, g_deter, lg[2]])
+        self.rssm._bwd_tr = None
         self._mark("scan_bwd")
 
     def _ph_encoder_bwd(self, st):

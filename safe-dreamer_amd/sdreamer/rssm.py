@@ -96,6 +96,7 @@ class RSSM(nn.Module):
         self._hidden = int(config.hidden)
         self._discrete = int(config.discrete)
         self._unimix_ratio = float(config.unimix_ratio)
+        self._bwd_tr = None  # scan_bwd_weights() computed ahead of the scan backward (Dreamer._ph_wm), or None
         self._initial = str(config.initial)
         self._device = torch.device(config.device)
         self._act_dim = int(act_dim)
@@ -141,6 +142,16 @@ class RSSM(nn.Module):
             Wo=self._obs_net.obs_net_0.weight, bo=self._obs_net.obs_net_0.bias, no=self._obs_net.obs_net_n_0.weight,
             Wl=self._obs_net.obs_net_logit.weight, bl=self._obs_net.obs_net_logit.bias,
         )
+
+    def scan_bwd_weights(self):
+        """The transposed weight layouts sd_rssm_scan_bwd reads (W^T of the scan's contractions). Dreamer computes
+        them on the main stream while it waits for the imagined returns, so the seven transposes are off the way
+        from the head losses to the encoder gradient; the weights do not change until the optimizer step."""
+        P = self._p()
+        D = self._deter
+        return dict(W0T=P["W0"].t().contiguous(), W1T=P["W1"].t().contiguous(), WshT=P["Wsh"].t().contiguous(),
+                    WbdT=P["Wbd"].transpose(1, 2).contiguous(), WgT=P["Wg"].transpose(1, 2).contiguous(),
+                    WoDT=P["Wo"][:, :D].t().contiguous(), WlT=P["Wl"].t().contiguous())
 
     def _img_mods(self):
         return [(self._img_net[3 * i], self._img_net[3 * i + 1]) for i in range(self._img_layers)], self._img_net.img_net_logit
@@ -379,10 +390,10 @@ class ObserveScan(torch.autograd.Function):
 
         gb = ops.grad_buf
         if ctx.fused:
-            dl_all, d_op, d_gates, d_hp, d_x0p, d_x1p, d_x2 = ObserveScan._bwd_fused(
+            dl_all, d_op, d_gates, d_hp, d_x0p, d_x1p, norm_w = ObserveScan._bwd_fused(
                 ctx, d_stoch, d_deter, d_logit, rt, s_in, h_in, x0p, x1p, r0, r1, hp, rh, gates, op, ro, logit)
             return ObserveScan._wgrads(ctx, P, rt, a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all,
-                                       d_op, d_gates, d_hp, d_x0p, d_x1p, d_x2)
+                                       d_op, d_gates, d_hp, d_x0p, d_x1p, None, norm_w)
         ds_out = tm(d_stoch, SK)
         dd_out = tm(d_deter, D)
         dl_all = tm(d_logit, SK)  # becomes d logit (incl. the straight-through sample gradient) in place
@@ -441,10 +452,7 @@ class ObserveScan(torch.autograd.Function):
                             else torch.empty(*shape, dtype=f32, device=dev))
         dl, d_o, d_op, d_x0p, d_x1p = e(T, B, SK), e(T, B, U), e(T, B, U), e(T, B, U), e(T, B, U)
         d_gates, d_hh, d_hp, d_xcat = e(T, B, 3 * D), e(T, B, D), e(T, B, D), e(T, B, 3 * U)
-        Wo_d = P["Wo"][:, :D]
-        tr = dict(W0T=P["W0"].t().contiguous(), W1T=P["W1"].t().contiguous(), WshT=P["Wsh"].t().contiguous(),
-                  WbdT=P["Wbd"].transpose(1, 2).contiguous(), WgT=P["Wg"].transpose(1, 2).contiguous(),
-                  WoDT=Wo_d.t().contiguous(), WlT=P["Wl"].t().contiguous())
+        tr = rssm._bwd_tr if rssm._bwd_tr is not None else rssm.scan_bwd_weights()
         x2 = ctx.x2
         d = _scan_desc(rssm, P, B, T, ctx.seed, ctx.row_offset, rt, x2, x2, None, ctx.stream_id)
         work = e(_scan_work(d))
@@ -459,17 +467,24 @@ class ObserveScan(torch.autograd.Function):
         nat.call("sd_rssm_scan_bwd", ctypes.addressof(d), K.stream())
         gb = ops.grad_buf
         f = lambda x: x.reshape(M, -1)  # noqa: E731
-        K.rmsnorm_bwd(f(op), P["no"], ro.reshape(M), f(d_o), dw=gb(P["no"]))
-        K.rmsnorm_bwd(f(hp), P["nh"], rh.reshape(M), f(d_hh), dw=gb(P["nh"]))
-        K.rmsnorm_bwd(f(x0p), P["n0"], r0.reshape(M), f(d_xcat)[:, :U].contiguous(), dw=gb(P["n0"]))
-        K.rmsnorm_bwd(f(x1p), P["n1"], r1.reshape(M), f(d_xcat)[:, U:2 * U].contiguous(), dw=gb(P["n1"]))
-        d_x2 = d_xcat[:, :, 2 * U:].contiguous()
-        return dl, d_op, d_gates, d_hp, d_x0p, d_x1p, d_x2
+
+        def norm_w():
+            """the four in-loop norms' weight gradients and d_x2 (deferred with the weight-gradient GEMMs: nothing on
+            the way to the encoder's gradient reads them)"""
+            K.rmsnorm_bwd(f(op), P["no"], ro.reshape(M), f(d_o), dw=gb(P["no"]))
+            K.rmsnorm_bwd(f(hp), P["nh"], rh.reshape(M), f(d_hh), dw=gb(P["nh"]))
+            K.rmsnorm_bwd(f(x0p), P["n0"], r0.reshape(M), f(d_xcat)[:, :U].contiguous(), dw=gb(P["n0"]))
+            K.rmsnorm_bwd(f(x1p), P["n1"], r1.reshape(M), f(d_xcat)[:, U:2 * U].contiguous(), dw=gb(P["n1"]))
+            return d_xcat[:, :, 2 * U:].contiguous()
+
+        norm_w.tensors = (op, hp, x0p, x1p, ro, rh, r0, r1, d_o, d_hh, d_xcat)
+        return dl, d_op, d_gates, d_hp, d_x0p, d_x1p, norm_w
 
     @staticmethod
     def _wgrads(ctx, P, rt, a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all, d_op, d_gates, d_hp,
-                d_x0p, d_x1p, d_x2):
-        """Deferred weight gradients: one GEMM (or column sum) over all T*B time-major rows each (split-bf16 GEMMs)."""
+                d_x0p, d_x1p, d_x2, norm_w=None):
+        """Deferred weight gradients: one GEMM (or column sum) over all T*B time-major rows each (split-bf16 GEMMs).
+        norm_w (fused path): the in-loop norms' weight gradients, run first; returns d_x2."""
         rssm = ctx.rssm
         B, T, A, E = ctx.dims
         D, G = rssm._deter, rssm._blocks
@@ -479,7 +494,9 @@ class ObserveScan(torch.autograd.Function):
         f = lambda x: x.reshape(M, -1)  # noqa: E731
         d_emb = K.mm(f(d_op), P["Wo"][:, D:], fast=True)  # (M, E) time-major: the only output the encoder waits for
 
-        def wgrads():
+        def wgrads(d_x2=d_x2):
+            if norm_w is not None:
+                d_x2 = norm_w()
             K.gemm(f(dl_all).t(), f(oo), gb(P["Wl"]), beta=1.0, fast=True)
             K.colsum(f(dl_all), gb(P["bl"]))
             gWo = gb(P["Wo"])
@@ -504,8 +521,9 @@ class ObserveScan(torch.autograd.Function):
             K.colsum(d_x2p, gb(P["b2"]))
 
         if ops._DEFER is not None:  # queued (ops.defer_wgrads): the caller runs them on another stream
-            ops._DEFER.append((wgrads, (a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all, d_op, d_gates,
-                                        d_hp, d_x0p, d_x1p, d_x2)))
+            keep = (a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all, d_op, d_gates, d_hp, d_x0p, d_x1p)
+            keep += (d_x2,) if d_x2 is not None else norm_w.tensors
+            ops._DEFER.append((wgrads, keep))
         else:
             wgrads()
         d_embed = d_emb.view(T, B, E).transpose(0, 1).contiguous()
