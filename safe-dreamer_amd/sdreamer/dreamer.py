@@ -694,8 +694,10 @@ class Dreamer(nn.Module):
         that do not need the imagined returns. defer: the heads' weight-gradient contractions are queued in
         st["wm_wgrads"] (graphed update: phase M2d)."""
         st["wm_wgrads"] = []
-        # the scan backward's transposed weights, while main has slack (it waits for the imagined returns next)
+        # the scan backward's transposed weights and the encoder's flipped conv weights, while main has slack (it
+        # waits for the imagined returns next): off the chain from the head losses to the encoder gradient
         st["scan_tr"] = self.rssm._bwd_tr = self.rssm.scan_bwd_weights()
+        st["enc_flip"] = K.set_flip_cache(self.encoder.dgrad_weights())
         with ops.defer_wgrads(st["wm_wgrads"] if defer else None):
             st["wm_total"], st["wm_losses"], st["wm_metrics"] = self._wm_heads(st["data"], st["embed"], st["leaves"],
                                                                                st["feat_l"], st["seed"], st["ro"],
@@ -729,8 +731,15 @@ class Dreamer(nn.Module):
         self._mark("repval_wait")
         g_feat = st["feat_r"].grad
         lg = [l.grad if l.grad is not None else torch.zeros_like(l) for l in leaves]
-        g_stoch = lg[0] + g_feat[..., :SK].reshape(leaves[0].shape)
-        g_deter = lg[1] + g_feat[..., SK:]
+        # summed straight into the scan's time-major layout (one kernel each; the scan backward's own transposes of
+        # these two gradients become no-ops): (B, T, .) views of (T, B, .) storage
+        B, T = g_feat.shape[:2]
+        gs = torch.empty(T, B, SK, dtype=g_feat.dtype, device=g_feat.device)
+        torch.add(lg[0].reshape(B, T, SK).transpose(0, 1), g_feat[..., :SK].transpose(0, 1), out=gs)
+        gd = torch.empty(T, B, g_feat.shape[-1] - SK, dtype=g_feat.dtype, device=g_feat.device)
+        torch.add(lg[1].transpose(0, 1), g_feat[..., SK:].transpose(0, 1), out=gd)
+        g_stoch = gs.transpose(0, 1).reshape(leaves[0].shape)
+        g_deter = gd.transpose(0, 1)
         st["scan_wgrads"] = []
         if defer:
             with ops.defer_wgrads(st["scan_wgrads"]):
@@ -758,6 +767,7 @@ class Dreamer(nn.Module):
                     st["embed"].backward(g)
             else:
                 st["embed"].backward(g)
+        K.clear_flip_cache()
 
     def _ph_encoder_bwd_lo(self, st):
         """main: the first encoder stage's backward (weight gradients only)."""

@@ -350,7 +350,9 @@ def conv2d_dgrad(dout, w, pad=None, fast=True):
     (Nb, H, W, Ci). fast: split-bf16 MFMA kernel (sd_conv2d_dgrad_bf16x3) where its shape constraints hold."""
     Co, kh, kw, Ci = w.shape
     pad = kh - 1 - (kh - 1) // 2 if pad is None else pad
-    wf = conv_flip_weight(w)
+    wf = _FLIP.get(w.data_ptr())
+    if wf is None:
+        wf = conv_flip_weight(w)
     if fast and FAST_GEMM:
         Nb, H, W, _ = dout.shape
         din = torch.empty(Nb, H, W, Ci, dtype=torch.float32, device=dout.device)
@@ -409,6 +411,23 @@ def conv2d_wgrad_pool(x, dpool, amax, kh, kw, pad=None):
     nat.call("sd_conv2d_wgrad_pool", p(_c(x)), p(_c(dpool)), p(_c(amax)), p(out), p(ws), ws.numel(), Nb, H, W, Ci, Co,
              kh, kw, pad, stream())
     return out
+
+
+_FLIP = {}  # weight data_ptr -> flipped weight, built ahead of the backward (set_flip_cache)
+
+
+def set_flip_cache(weights):
+    """Flip conv weights for conv2d_dgrad ahead of time (Dreamer builds them on the main stream while it waits for
+    the imagined returns, off the encoder backward's chain); valid until clear_flip_cache (the optimizer step changes
+    the weights). Returns the flipped tensors (the caller keeps them alive)."""
+    _FLIP.clear()
+    for w in weights:
+        _FLIP[w.data_ptr()] = conv_flip_weight(w)
+    return list(_FLIP.values())
+
+
+def clear_flip_cache():
+    _FLIP.clear()
 
 
 def conv_flip_weight(w):

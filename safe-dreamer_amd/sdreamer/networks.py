@@ -227,6 +227,10 @@ class ConvEncoder(nn.Module):
         self.layers = nn.Sequential(*layers)
         self.out_dim = self.depths[-1] * h * w
 
+    def dgrad_weights(self):
+        """conv weights whose input gradient the backward computes (every stage but the first)"""
+        return [self.layers[4 * i].weight for i in range(1, len(self.depths))]
+
     def forward(self, obs, split=None):
         """split (a list): the first stage's output is continued as a detached leaf and (output, leaf) appended, so
         the backward runs as two calls (stages 2.. down to the leaf, then the first stage)."""
@@ -267,6 +271,9 @@ class MultiEncoder(nn.Module):
         if not encs:
             raise NotImplementedError
         self.encoders = nn.ModuleList(encs)
+
+    def dgrad_weights(self):
+        return [w for kind, enc in zip(self.kinds, self.encoders) if kind == "cnn" for w in enc.dgrad_weights()]
 
     def forward(self, obs, split=None):
         """obs: dict of (B, T, *); images already float in [0, 1] (after preprocess). Returns (B, T, E).

@@ -301,8 +301,10 @@ class ObserveScan(torch.autograd.Function):
         a_n = K.action_norm(K.mask_rows(act_t, rt.reshape(M)))
         x2p = K.linear(a_n, P["W2"], P["b2"])
         x2, r2 = K.rmsnorm_fwd(x2p, P["n2"])
-        emb_t = embed.detach().transpose(0, 1).reshape(M, E).contiguous()
-        eproj = K.linear(emb_t, P["Wo"][:, D:], P["bo"])  # (M, U): embed half of obs_net_0 + bias
+        # embed half of obs_net_0 + bias on the batch-major rows, then the (M, U) result is made time-major: the
+        # (M, E) embedding itself is never transposed (emb_t: batch-major rows b*T + t, see _wgrads)
+        emb_t = embed.detach().reshape(M, E)
+        eproj = K.linear(emb_t, P["Wo"][:, D:], P["bo"]).view(B, T, U).transpose(0, 1).reshape(M, U).contiguous()
         # ---- per-step buffers (time-major)
         s_in = torch.empty(T, B, SK, dtype=f32, device=dev)
         h_in = torch.empty(T, B, D, dtype=f32, device=dev)
@@ -492,7 +494,9 @@ class ObserveScan(torch.autograd.Function):
         M = T * B
         gb = ops.grad_buf
         f = lambda x: x.reshape(M, -1)  # noqa: E731
-        d_emb = K.mm(f(d_op), P["Wo"][:, D:], fast=True)  # (M, E) time-major: the only output the encoder waits for
+        # batch-major d_op (a (M, U) copy), so the embed gradient comes out in the encoder's (B, T, E) order directly
+        d_op_b = d_op.transpose(0, 1).reshape(M, -1).contiguous()
+        d_emb = K.mm(d_op_b, P["Wo"][:, D:], fast=True)  # (M, E): the only output the encoder waits for
 
         def wgrads(d_x2=d_x2):
             if norm_w is not None:
@@ -501,7 +505,7 @@ class ObserveScan(torch.autograd.Function):
             K.colsum(f(dl_all), gb(P["bl"]))
             gWo = gb(P["Wo"])
             K.gemm(f(d_op).t(), f(deter), gWo[:, :D], beta=1.0, fast=True)
-            K.gemm(f(d_op).t(), emb_t, gWo[:, D:], beta=1.0, fast=True)
+            K.gemm(d_op_b.t(), emb_t, gWo[:, D:], beta=1.0, fast=True)  # both batch-major
             K.colsum(f(d_op), gb(P["bo"]))
             K.gemm(f(d_gates).view(M, G, 3 * Dg).permute(1, 2, 0), f(hh).view(M, G, Dg).permute(1, 0, 2),
                    gb(P["Wg"]), beta=1.0, fast=True)
@@ -521,10 +525,10 @@ class ObserveScan(torch.autograd.Function):
             K.colsum(d_x2p, gb(P["b2"]))
 
         if ops._DEFER is not None:  # queued (ops.defer_wgrads): the caller runs them on another stream
-            keep = (a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all, d_op, d_gates, d_hp, d_x0p, d_x1p)
+            keep = (a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all, d_op, d_op_b, d_gates, d_hp, d_x0p,
+                    d_x1p)
             keep += (d_x2,) if d_x2 is not None else norm_w.tensors
             ops._DEFER.append((wgrads, keep))
         else:
             wgrads()
-        d_embed = d_emb.view(T, B, E).transpose(0, 1).contiguous()
-        return d_embed, None, None, None, None, None, None, None, None
+        return d_emb.view(B, T, E), None, None, None, None, None, None, None, None

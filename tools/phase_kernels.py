@@ -1,7 +1,7 @@
 """Per-phase kernel list of one graph-replayed update from a rocprofv3 kernel-trace database of tools/timeline.py
 (SDREAMER_MARKS=1): the device marks (mark_kernel dispatches) split each queue's dispatches into phases; prints, per
 phase of the LAST update, the kernels in order with their durations, and a per-phase summary.
-Usage: python tools/phase_kernels.py run.db [marks_per_update]"""
+Usage: python tools/phase_kernels.py run.db [kernels listed per phase]"""
 import sqlite3
 import sys
 from collections import defaultdict
@@ -54,4 +54,4 @@ def main(path, top=12):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 12)
