@@ -41,6 +41,9 @@ S2_AFTER_SCAN = os.environ.get("SDREAMER_S2_AFTER_SCAN", "0") == "1"
 # imagination and slows it) for phase M2d on main after the encoder backward. Measured: the imagination got 0.27 ms
 # faster but M2d (0.68 ms) outgrew the join slack it fills: 13.59 vs 13.34 ms per update, so off by default.
 DEFER_WM = os.environ.get("SDREAMER_DEFER_WM", "0") == "1"
+# graphed update: the first N queued encoder weight-gradient contractions (the last stages', queued first) run on main
+# after the first stage's backward (phase M2d) instead of on the side stream (S4), which ends the update
+S4_MAIN = int(os.environ.get("SDREAMER_S4_MAIN", "1"))  # measured: 0 -> 13.01, 1 -> 12.93, 2 -> 12.98 ms
 # SDREAMER_FUSED_SAMPLE=0: replayed updates sample through Buffer.sample() + copies instead of sample_into (A/B knob)
 FUSED_SAMPLE = os.environ.get("SDREAMER_FUSED_SAMPLE", "1") != "0"
 
@@ -437,6 +440,13 @@ class Dreamer(nn.Module):
         if self.marks is not None:
             self.marks(tag)
 
+    def _main_tail(self, st):
+        """phase M2d (main, after the first encoder stage's backward): deferred weight gradients moved off the side
+        stream's tail (SDREAMER_DEFER_WM / SDREAMER_S4_MAIN)."""
+        ops.flush_wgrads(st.get("wm_wgrads", []))
+        ops.flush_wgrads(st.get("enc_wgrads_main", []))
+        self._mark("main_tail")
+
     def _flush(self, wgrads, tag):
         """side phases S3 / S4: the deferred weight-gradient contractions, then a timeline mark."""
         ops.flush_wgrads(wgrads)
@@ -511,9 +521,12 @@ class Dreamer(nn.Module):
             gM2a, _ = cap(lambda: self._ph_scan_bwd(st, defer=True), main_cap)
             gS3, _ = cap(lambda: self._flush(st["scan_wgrads"], "side:scan_wgrads"), side_cap)
             gM2b, _ = cap(lambda: self._ph_encoder_bwd_hi(st, defer=True), main_cap)
+            if S4_MAIN:
+                st["enc_wgrads_main"] = st["enc_wgrads"][:S4_MAIN]
+                del st["enc_wgrads"][:S4_MAIN]
             gS4, _ = cap(lambda: self._flush(st["enc_wgrads"], "side:enc_wgrads"), side_cap)
             gM2c, _ = cap(lambda: self._ph_encoder_bwd_lo(st), main_cap)
-            gM2d = cap(lambda: self._flush(st["wm_wgrads"], "wm_wgrads"), main_cap)[0] if DEFER_WM else None
+            gM2d = cap(lambda: self._main_tail(st), main_cap)[0] if (DEFER_WM or S4_MAIN) else None
             gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
             gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st), main_cap)
             torch.cuda.synchronize()
