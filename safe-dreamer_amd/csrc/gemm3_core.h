@@ -22,7 +22,10 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 32;
-constexpr int LROW = 2 * BK + 8;  // bf16 per LDS row
+#ifndef SD_G3_PAD  // bf16 of padding per LDS row (A/B knob)
+#define SD_G3_PAD 8
+#endif
+constexpr int LROW = 2 * BK + SD_G3_PAD;  // bf16 per LDS row
 
 SD_DEV void split_store(__bf16* dst, f32x4 v) {
   const bf16x4 hi = __builtin_convertvector(v, bf16x4);
