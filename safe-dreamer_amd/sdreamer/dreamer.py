@@ -463,18 +463,23 @@ class Dreamer(nn.Module):
         self._optimizer.zero_grad()
         return self._ph_forward(p_data, initial, seed, ro)
 
-    def _core_finish(self, st):
-        """Graph phase M3 (main): merged metrics, optimizer step, metric vector."""
+    def _side_ac_metrics(self, st):
+        """Graph phase S2 (side): the actor-critic phase, then the merged loss / metric vector. The metrics are built
+        here, where the side stream has slack, instead of in front of the optimizer step (M3)."""
+        self._ph_side_ac(st)
         post, mets = self._ph_finish(st)
+        keys = [k for k, v in mets.items() if isinstance(v, torch.Tensor)]
+        mvec = torch.stack([mets[k].float().reshape(()) for k in keys])
+        return post, keys, mvec
+
+    def _core_step(self, st):
+        """Graph phase M3 (main): the optimizer step."""
         if self.world > 1:  # the arena was sum-all-reduced between the phase graphs (_update_graphed)
             self._optimizer.arena.grad.mul_(1.0 / self.world)
         if self.rep_loss == "dreamerpro":
             ops.grad_buf(self._prototypes).mul_(self._proto_gate)
         self._optimizer.launch_step()
         self._mark("optimizer")
-        keys = [k for k, v in mets.items() if isinstance(v, torch.Tensor)]
-        mvec = torch.stack([mets[k].float().reshape(()) for k in keys])
-        return post, keys, mvec
 
     def _update_graphed(self, data, initial, seed, ro):
         """Replay of the update as eleven single-stream phases (captured once) joined by stream events:
@@ -527,8 +532,8 @@ class Dreamer(nn.Module):
             gS4, _ = cap(lambda: self._flush(st["enc_wgrads"], "side:enc_wgrads"), side_cap)
             gM2c, _ = cap(lambda: self._ph_encoder_bwd_lo(st), main_cap)
             gM2d = cap(lambda: self._main_tail(st), main_cap)[0] if (DEFER_WM or S4_MAIN) else None
-            gS2, _ = cap(lambda: self._ph_side_ac(st), side_cap)
-            gM3, (post, keys, mvec) = cap(lambda: self._core_finish(st), main_cap)
+            gS2, (post, keys, mvec) = cap(lambda: self._side_ac_metrics(st), side_cap)
+            gM3, _ = cap(lambda: self._core_step(st), main_cap)
             torch.cuda.synchronize()
             for g in (gP, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gM3):
                 if g is not None and g.n_collectives:
