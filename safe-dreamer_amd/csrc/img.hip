@@ -329,6 +329,11 @@ struct LinProb {
 #ifndef KL_PF
 #define KL_PF 2
 #endif
+// tile of the step's K = S*Kd launch (actor layer 0's stoch part + _dyn_in1)
+#ifndef KL2_BN
+#define KL2_BN 32
+#endif
+constexpr int KL2_WN = KL2_BN / 2, KL2_PW = KL2_WN < 32 ? KL2_WN : 32;
 constexpr int KL3_WN = KL3_BN / (4 / (KL3_BM / 16)), KL3_PW = KL3_WN < 32 ? KL3_WN : 32;  // its row-partial width
 // grouped plain-A linear layers (N = 256 each): out = A . W^T + b (+ add), with row partials. grid (N/BN, M/BM, nprob)
 template <int BM, int BN>
@@ -673,7 +678,7 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
   const IWork w = iwork(d, d.work);
   const int N = d.N, U = d.U, SK = d.SK, D = d.D, F = SK + D;
   const long NF = (long)N * F;
-  const int npU = U / 32;
+  const int npU = U / KL2_PW;
   auto feats = [&](int s) { return d.feats + s * NF; };
   if (which == 0) {
     LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};
@@ -700,7 +705,7 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   const IWork w = iwork(d, d.work);
   const int N = d.N, U = d.U, SK = d.SK, D = d.D, F = SK + D;
   const long NF = (long)N * F;
-  const int npU = U / 32;  // row partials per hidden row written by k_lin<32, 64> (WN = 32)
+  const int npU = U / KL2_PW;  // row partials per hidden row written by the K = S*Kd k_lin
   const dim3 gr(U / 64, sd_cdiv(N, KR_BM));
   const int npR = U / KR_PW;  // row partials written by k_rmslin
   auto feats = [&](int t) { return d.feats + t * NF; };
@@ -720,7 +725,7 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     {  // actor layer 0, stoch part (+ deter part); _dyn_in1 on stoch
       LinProb pa{feats(t), F, SK, d.Wa[0], F, d.ba[0], w.a[0], U, w.pa[0], w.ad};
       LinProb px{feats(t), F, SK, d.W1, SK, d.b1, w.x1p, U, w.px1, nullptr};
-      k_lin<32, 64><<<dim3(U / 64, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, px, N);
+      k_lin<32, KL2_BN><<<dim3(U / KL2_BN, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, px, N);
       SD_LAUNCH_CHECK();
     }
     int cur = 0, npa = npU;
