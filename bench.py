@@ -372,7 +372,7 @@ def main():
         "metric": METRIC,
         "value": value, "unit": "imagined_latents/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms, "higher_is_better": True, "scaling": "strong" if args.global_batch else "weak",
-        "vs_baseline": None, "dtype": "f32",
+        "vs_baseline": None, "dtype": "f32 (split-bf16 gradient GEMMs)",
         "precision": "fp32 everywhere a sampled index or a WM loss depends on (fp32 MFMA, and the fp32-accurate "
                      "3-way split-bf16 'bf16x6' MFMA in the imagination); gradient contractions and the frozen "
                      "imagined heads on 2-way split-bf16 (~1e-5 rel); DESIGN.md §2",

@@ -6,6 +6,7 @@ Per (kernel, grid) group: dispatches, average duration (trace pass), and per-dis
 found in the PMC passes, with derived columns:
   clock GHz   = GRBM_GUI_ACTIVE / 8 XCDs / duration (MI355X_MICROARCH.md 'DVFS give-back': reads high below ~0.3 ms)
   mfma util   = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x clock x duration)
+  waves/CU    = 4 x SQ_WAVE_CYCLES (quad-cycles summed over waves) / (256 CUs x clock x duration): mean resident waves
   wait/stall/active % of SQ_WAVE_CYCLES (SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY)
   HBM bytes   = 2 x FETCH_SIZE (gfx950: FETCH_SIZE reports half of wide coalesced reads) + WRITE_SIZE, KB -> B
   L2 hit %    = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
@@ -76,15 +77,16 @@ def main(tdir, *pdirs):
     rows = sorted(tr.items(), key=lambda kv: -sum(kv[1]))
     tot = sum(sum(v) for v in tr.values())
     print(f"kernel trace: {sum(len(v) for v in tr.values())} dispatches, {tot / 1e6:.2f} ms of kernel time\n")
-    print("| share | kernel | grid (wg x, y, z) | n | avg us | clock GHz | mfma util | wait % | stall % | active % "
-          "| HBM MB/disp | L2 hit % |")
-    print("|---:|---|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
+    print("| share | kernel | grid (wg x, y, z) | n | avg us | clock GHz | mfma util | waves/CU | wait % | stall % | "
+          "active % | HBM MB/disp | L2 hit % |")
+    print("|---:|---|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     for k, ts in rows[:45]:
         avg = sum(ts) / len(ts)
         c = cs.get(k, {})
         gui, mf, wc = c.get("GRBM_GUI_ACTIVE"), c.get("SQ_VALU_MFMA_BUSY_CYCLES"), c.get("SQ_WAVE_CYCLES")
         clk = gui / 8 / (avg * 1e-9) / 1e9 if gui else None
         util = mf / (1024 * clk * 1e9 * avg * 1e-9) if (mf is not None and clk) else None
+        wpc = 4 * wc / (256 * clk * 1e9 * avg * 1e-9) if (wc and clk) else None
         f, w = c.get("FETCH_SIZE"), c.get("WRITE_SIZE")
         hbm = (2 * f + w) * 1024 / 1e6 if (f is not None and w is not None) else None
         h, m = c.get("TCC_HIT_sum"), c.get("TCC_MISS_sum")
@@ -94,7 +96,7 @@ def main(tdir, *pdirs):
             return s.format(x) if x is not None else "-"
         pct = (lambda n: fmt(100 * c[n] / wc, "{:.0f}") if (wc and n in c) else "-")
         print(f"| {100 * sum(ts) / tot:.1f}% | `{k[0]}` | {k[1]}x{k[2]}x{k[3]} | {len(ts)} | {avg / 1e3:.1f} | "
-              f"{fmt(clk)} | {fmt(util)} | {pct('SQ_WAIT_ANY')} | {pct('SQ_WAIT_INST_ANY')} | "
+              f"{fmt(clk)} | {fmt(util)} | {fmt(wpc, '{:.1f}')} | {pct('SQ_WAIT_ANY')} | {pct('SQ_WAIT_INST_ANY')} | "
               f"{pct('SQ_ACTIVE_INST_ANY')} | {fmt(hbm, '{:.1f}')} | {fmt(hit, '{:.0f}')} |")
 
 
