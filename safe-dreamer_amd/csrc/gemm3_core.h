@@ -28,10 +28,16 @@ constexpr int BK = 32;
 constexpr int LROW = 2 * BK + SD_G3_PAD;  // bf16 per LDS row
 
 SD_DEV void split_store(__bf16* dst, f32x4 v) {
-  const bf16x4 hi = __builtin_convertvector(v, bf16x4);
-  const f32x4 r = v - __builtin_convertvector(hi, f32x4);
-  *reinterpret_cast<bf16x4*>(dst) = hi;
-  *reinterpret_cast<bf16x4*>(dst + BK) = __builtin_convertvector(r, bf16x4);
+  // hi as packed RNE pairs, read back by shift / mask (hipcc re-converts each element otherwise)
+  typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+  typedef float f32x2_ __attribute__((ext_vector_type(2)));
+  typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
+  const uint32_t p0 = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{v[0], v[1]}, bf16x2_));
+  const uint32_t p1 = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{v[2], v[3]}, bf16x2_));
+  const f32x4 h{__builtin_bit_cast(float, p0 << 16), __builtin_bit_cast(float, p0 & 0xffff0000u),
+                __builtin_bit_cast(float, p1 << 16), __builtin_bit_cast(float, p1 & 0xffff0000u)};
+  *reinterpret_cast<u32x2_*>(dst) = u32x2_{p0, p1};
+  *reinterpret_cast<bf16x4*>(dst + BK) = __builtin_convertvector(v - h, bf16x4);
 }
 
 // Operand with k contiguous (row r, k at p[r * ld + k]): thread loads float4 runs along k.

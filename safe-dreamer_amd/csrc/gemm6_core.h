@@ -29,14 +29,28 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int BK6 = 32;            // fp32-equivalent k per tile (one 16x16x32 step per plane pair)
 constexpr int LROW6 = 3 * BK6 + 16;  // bf16 per LDS row
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// RNE bf16 pair of (a, b) in one v_cvt_pk_bf16_f32, and the two floats it represents read back from the packed bits
+// (a shift and a mask: hipcc otherwise re-converts each element separately to get them back)
+SD_DEV uint32_t bf16_pair(float a, float b, float& ra, float& rb) {
+  const uint32_t p = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+  ra = __builtin_bit_cast(float, p << 16);
+  rb = __builtin_bit_cast(float, p & 0xffff0000u);
+  return p;
+}
+
 SD_DEV void split3_store(__bf16* dst, f32x4 v) {
-  const bf16x4 h = __builtin_convertvector(v, bf16x4);
-  const f32x4 r1 = v - __builtin_convertvector(h, f32x4);
-  const bf16x4 m = __builtin_convertvector(r1, bf16x4);
-  const f32x4 r2 = r1 - __builtin_convertvector(m, f32x4);
-  *reinterpret_cast<bf16x4*>(dst) = h;
-  *reinterpret_cast<bf16x4*>(dst + BK6) = m;
-  *reinterpret_cast<bf16x4*>(dst + 2 * BK6) = __builtin_convertvector(r2, bf16x4);
+  float h0, h1, h2, h3, m0, m1, m2, m3;
+  const u32x2 h{bf16_pair(v[0], v[1], h0, h1), bf16_pair(v[2], v[3], h2, h3)};
+  const float r0 = v[0] - h0, r1 = v[1] - h1, r2 = v[2] - h2, r3 = v[3] - h3;
+  const u32x2 m{bf16_pair(r0, r1, m0, m1), bf16_pair(r2, r3, m2, m3)};
+  const f32x4 l{r0 - m0, r1 - m1, r2 - m2, r3 - m3};
+  *reinterpret_cast<u32x2*>(dst) = h;
+  *reinterpret_cast<u32x2*>(dst + BK6) = m;
+  *reinterpret_cast<bf16x4*>(dst + 2 * BK6) = __builtin_convertvector(l, bf16x4);
 }
 
 template <int N>
