@@ -938,11 +938,11 @@ __global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const f32x4 t = {rd[0][jj], rd[1][jj], rd[2][jj], rd[3][jj]};
-        const sdb::bf16x4 hi = __builtin_convertvector(t, sdb::bf16x4);
-        const f32x4 r = t - __builtin_convertvector(hi, f32x4);
+        sdb::bf16x4 hi, lo;
+        sdb::split2(t, hi, lo);
         const int o = (4 * dq4 + jj) * d.PS + pos;
         *reinterpret_cast<sdb::bf16x4*>(dyh + o) = hi;
-        *reinterpret_cast<sdb::bf16x4*>(dyl + o) = __builtin_convertvector(r, sdb::bf16x4);
+        *reinterpret_cast<sdb::bf16x4*>(dyl + o) = lo;
       }
     }
 #pragma unroll
@@ -983,9 +983,9 @@ __global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
       for (int b = 0; b < NBW; ++b) {
         const f32x4 v0 = {xp[pb[0] + off[b]], xp[pb[1] + off[b]], xp[pb[2] + off[b]], xp[pb[3] + off[b]]};
         const f32x4 v1 = {xp[pb[4] + off[b]], xp[pb[5] + off[b]], xp[pb[6] + off[b]], xp[pb[7] + off[b]]};
-        const sdb::bf16x4 h0 = __builtin_convertvector(v0, sdb::bf16x4), h1 = __builtin_convertvector(v1, sdb::bf16x4);
-        const sdb::bf16x4 e0 = __builtin_convertvector(v0 - __builtin_convertvector(h0, f32x4), sdb::bf16x4);
-        const sdb::bf16x4 e1 = __builtin_convertvector(v1 - __builtin_convertvector(h1, f32x4), sdb::bf16x4);
+        sdb::bf16x4 h0, h1, e0, e1;
+        sdb::split2(v0, h0, e0);
+        sdb::split2(v1, h1, e1);
         const sdb::bf16x8 bh = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
         const sdb::bf16x8 bl = __builtin_shufflevector(e0, e1, 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll

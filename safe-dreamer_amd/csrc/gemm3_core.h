@@ -27,17 +27,25 @@ constexpr int BK = 32;
 #endif
 constexpr int LROW = 2 * BK + SD_G3_PAD;  // bf16 per LDS row
 
-SD_DEV void split_store(__bf16* dst, f32x4 v) {
-  // hi as packed RNE pairs, read back by shift / mask (hipcc re-converts each element otherwise)
-  typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
-  typedef float f32x2_ __attribute__((ext_vector_type(2)));
-  typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
-  const uint32_t p0 = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{v[0], v[1]}, bf16x2_));
-  const uint32_t p1 = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{v[2], v[3]}, bf16x2_));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// v = hi + lo (+ <= 2^-17 |v|): hi as packed RNE pairs read back by shift / mask (hipcc otherwise converts each element
+// back separately: 16 -> 10 VALU per float4), lo = bf16(v - hi)
+SD_DEV void split2(f32x4 v, bf16x4& hi, bf16x4& lo) {
+  const uint32_t p0 = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2));
+  const uint32_t p1 = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2));
   const f32x4 h{__builtin_bit_cast(float, p0 << 16), __builtin_bit_cast(float, p0 & 0xffff0000u),
                 __builtin_bit_cast(float, p1 << 16), __builtin_bit_cast(float, p1 & 0xffff0000u)};
-  *reinterpret_cast<u32x2_*>(dst) = u32x2_{p0, p1};
-  *reinterpret_cast<bf16x4*>(dst + BK) = __builtin_convertvector(v - h, bf16x4);
+  hi = __builtin_bit_cast(bf16x4, (uint64_t)p0 | ((uint64_t)p1 << 32));
+  lo = __builtin_convertvector(v - h, bf16x4);
+}
+
+SD_DEV void split_store(__bf16* dst, f32x4 v) {
+  bf16x4 hi, lo;
+  split2(v, hi, lo);
+  *reinterpret_cast<bf16x4*>(dst) = hi;
+  *reinterpret_cast<bf16x4*>(dst + BK) = lo;
 }
 
 // Operand with k contiguous (row r, k at p[r * ld + k]): thread loads float4 runs along k.
