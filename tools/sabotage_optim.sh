@@ -9,8 +9,8 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 CSRC=$ROOT/safe-dreamer_amd/csrc
 SAB=$ROOT/_sab
 declare -A EDIT=(
-  [laprop_sign]='s/p\[i\] = p\[i\] + neg_step \* mv;/p[i] = p[i] - neg_step * mv;/'
-  [agc_skip]='s/const float gv = g\[i\] \* sc;/const float gv = g[i];/'
+  [laprop_sign]='s/pq\[j\] = pq\[j\] + neg_step \* mv;/pq[j] = pq[j] - neg_step * mv;/'
+  [agc_skip]='s/const float gv = gq\[j\] \* sc;/const float gv = gq[j];/'
   [polyak_skip]='s/dst\[i\] = mix \* src\[i\] + keep \* dst\[i\];/dst[i] = dst[i] + 0.f * src[i] * mix * keep;/'
 )
 if [ "${1:-}" = build ]; then
