@@ -12,6 +12,8 @@
 //   * independent contractions that share an A operand grouped into one launch (actor layer 0 with _dyn_in1,
 //     img_net_0 with the next step's _dyn_in0).
 // Results land directly in the reference's (H1, N, F) feat and (H1, N, A) action layouts.
+#include <type_traits>
+
 #include "common.h"
 #include "dist_core.h"
 #include "gemm6_core.h"
@@ -179,6 +181,56 @@ struct BRows {
     }
   }
 };
+
+// B operand from a pre-split weight image (k_presplit6): the BN x 32 tile (ct, kt) is stored as its three bf16
+// planes, [row][a0 32 | a1 32 | a2 32] (192 B a row), contiguous per tile, so a k tile is one coalesced read of
+// 12 KB and store6 copies it into the LDS image in 16-B pieces with no VALU. The planes are split3_store's, so the
+// contraction is bit-identical to BRows + store6 on the fp32 weight.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int PRE_ROW = 3 * BK6;  // bf16 per row of a pre-split tile
+template <int BN>
+struct BPre6 {
+  static constexpr int PCS = BN * PRE_ROW / 8, NV = (PCS + 255) / 256;  // 16-B pieces per tile
+  u32x4 r[NV];
+  const __bf16* tile0;
+  SD_DEV BPre6() = default;
+  SD_DEV BPre6(const __bf16* pre, int ct, int nkt, int kt0) : tile0(pre + ((long)ct * nkt + kt0) * BN * PRE_ROW) {}
+  SD_DEV static bool live(int v) { return 256 * (v + 1) <= PCS || threadIdx.x + 256 * v < PCS; }
+  SD_DEV void load(int k0, int) {
+    const __bf16* t = tile0 + (long)(k0 / BK6) * BN * PRE_ROW;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      if (live(v)) r[v] = *reinterpret_cast<const u32x4*>(t + (threadIdx.x + 256 * v) * 8);
+  }
+  SD_DEV void store6(__bf16* lds) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + 256 * v;
+      if (live(v)) *reinterpret_cast<u32x4*>(lds + (i / (PRE_ROW / 8)) * LROW6 + (i % (PRE_ROW / 8)) * 8) = r[v];
+    }
+  }
+};
+// W (rows, K) fp32, k contiguous -> the BPre6 image of BN-row column tiles: tile (n / BN, k / 32), row n % BN.
+// One thread per (row, k quad). rows % BN == 0, K % 32 == 0 (the caller checks).
+// _dyn_gru's weight for k_gate: tile ct = 32 deter columns c0 = 32 ct of block g = c0 / Dg, its 96 rows the r / c / u
+// gate rows g*3Dg + {0, Dg, 2Dg} + c0 % Dg + (0..31) of Wg viewed as (3D, Dg); K = Dg.
+__global__ __launch_bounds__(256) void k_presplit6_gate(const float* Wg, int D, int Dg, __bf16* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int nq = Dg / 4;
+  if (i >= (long)3 * D * nq) return;
+  const int rr = (int)(i / nq), k = 4 * (int)(i % nq), nkt = Dg / BK6;  // rr: row of the (3D) tile-ordered image
+  const int ct = rr / 96, lr = rr % 96, c0 = ct * 32, g = c0 / Dg;
+  const long wrow = (long)g * 3 * Dg + (lr / 32) * Dg + c0 % Dg + lr % 32;
+  split3_store(out + (((long)ct * nkt + k / BK6) * 96 + lr) * PRE_ROW + k % BK6, ld4(Wg + wrow * Dg + k));
+}
+template <int BN>
+__global__ __launch_bounds__(256) void k_presplit6(const float* W, int rows, int K, __bf16* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int nq = K / 4;
+  if (i >= (long)rows * nq) return;
+  const int n = (int)(i / nq), k = 4 * (int)(i % nq), nkt = K / BK6;
+  split3_store(out + (((long)(n / BN) * nkt + k / BK6) * BN + n % BN) * PRE_ROW + k % BK6, ld4(W + (long)n * K + k));
+}
 
 // ------------------------------------------------------------------------------------------- contraction
 // F6: the bf16x6 main loop (gemm6_core.h: fp32-accurate, 2.67x the fp32 MFMA rate) instead of v_mfma_f32_16x16x4_f32.
@@ -379,6 +431,9 @@ __global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw,
 #ifndef KH_1S
 #define KH_1S 1
 #endif
+#ifndef KH_PRE  // k_hid reads _dyn_hid's weight from the once-per-imagination pre-split image (BPre6)
+#define KH_PRE 1
+#endif
 #ifndef KH_WAVES
 #define KH_WAVES 2
 #endif
@@ -404,7 +459,7 @@ SD_DEV void hid_seg(const OpA& a0, const OpB& b0, int K, f32x4 (&acc)[1][WN / 16
 // grid (D/64, M/64); row partials per 64 columns (D/64 of them) for the gate norm.
 __global__ __launch_bounds__(256, KH_WAVES) void k_hid(sd_imagine d, const float* h, long ldh, const float* x0p, const float* x1p,
                                              const float* px0, const float* px1, int npx0, int npx1, const float* x2, float* hp,
-                                             float* ph) {
+                                             float* ph, const __bf16* wh6) {
   constexpr int BM = KH_BM, BN = 64, WN = BN / (4 / (BM / 16));
   __shared__ float rs0[BM], rs1[BM], red[256];
   const int Dg = d.D / d.G, U = d.U, Ig = Dg + 3 * U, M = d.N;
@@ -412,48 +467,65 @@ __global__ __launch_bounds__(256, KH_WAVES) void k_hid(sd_imagine d, const float
   wg_rstd<BM, 8>(px0, npx0, M, m0, U, d.eps, rs0, red);
   wg_rstd<BM, 8>(px1, npx1, M, m0, U, d.eps, rs1, red);
   const float* Wseg = d.Wh + (long)n0 * Ig;  // rows n0.. of Wh viewed as (D, Ig)
+  const int ct = n0 / BN, nkt = Ig / BK6;
+  // the four K segments of [h_g | x0 | x1 | x2]: B from the pre-split image (KH_PRE) or split while staged
+  auto bseg = [&](int k0) {
+    if constexpr (KH_PRE && F6_HID)
+      return BPre6<BN>(wh6, ct, nkt, k0 / BK6);
+    else
+      return BRows<BN>(Wseg + k0, Ig, 0, BN, 0);
+  };
   f32x4 acc[1][WN / 16];
   {
     const APlain<BM> a0(h + (long)g * Dg, ldh, m0, M, Dg);
-    const BRows<BN> b0(Wseg, Ig, 0, BN, 0);
-    hid_seg<BM, BN, WN>(a0, b0, Dg, acc, false);
+    hid_seg<BM, BN, WN>(a0, bseg(0), Dg, acc, false);
   }
   {
     const ARms<BM> a0(x0p, U, d.n0, rs0, m0, M, U);
-    const BRows<BN> b0(Wseg + Dg, Ig, 0, BN, 0);
-    hid_seg<BM, BN, WN>(a0, b0, U, acc, true);
+    hid_seg<BM, BN, WN>(a0, bseg(Dg), U, acc, true);
   }
   {
     const ARms<BM> a0(x1p, U, d.n1, rs1, m0, M, U);
-    const BRows<BN> b0(Wseg + Dg + U, Ig, 0, BN, 0);
-    hid_seg<BM, BN, WN>(a0, b0, U, acc, true);
+    hid_seg<BM, BN, WN>(a0, bseg(Dg + U), U, acc, true);
   }
   {
     const APlain<BM> a0(x2, U, m0, M, U);
-    const BRows<BN> b0(Wseg + Dg + 2 * U, Ig, 0, BN, 0);
-    hid_seg<BM, BN, WN>(a0, b0, U, acc, true);
+    hid_seg<BM, BN, WN>(a0, bseg(Dg + 2 * U), U, acc, true);
   }
   ep_bias_part<BM, BN, WN, KH_PW>(acc, d.bh, hp, d.D, ph, M, m0, n0);
 }
 
 // gates = BlockLinear(dyn_gru)(silu(rms(hp))) + bg; deter' = GRU (rssm.py:65-75) -> feats[t+1][:, SK:].
 // Tile: 64 rows x (r | c | u) for 32 deter columns of block g (BN = 96). grid (D/32, M/64)
+// k_gate's B operand: the pre-split image of tile c0 / 32, or the r / c / u gate rows of Wg split while staged
+template <bool PRE, int BN>
+SD_DEV auto gate_b(const __bf16* wg6, int ct, int nkt, const float* Wblk, int Dg, int j0) {
+  if constexpr (PRE)
+    return BPre6<BN>(wg6, ct, nkt, 0);
+  else
+    return BRows<BN>(Wblk, Dg, j0, 32, Dg);
+}
+#ifndef KG_PRE  // k_gate reads _dyn_gru's weight from the once-per-imagination pre-split image (BPre6)
+#define KG_PRE 1
+#endif
 #ifndef KG_WAVES  // minimum waves per SIMD for k_gate's register allocation (occupancy; its LDS admits 4 per CU)
 #define KG_WAVES 4
 #endif
 __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const float* hp, const float* ph, int nph,
-                                              const float* hold, float* hnew, long ldf) {
+                                              const float* hold, float* hnew, long ldf, const __bf16* wg6) {
   constexpr int BM = 64, BN = 96;
   const int Dg = d.D / d.G;
   const int c0 = xcd_col(blockIdx.x, gridDim.x, Dg / 32) * 32, m0 = blockIdx.y * BM, g = c0 / Dg, j0 = c0 % Dg;
   __shared__ float rs[BM], red[256];
   wg_rstd<BM, 16>(ph, nph, d.N, m0, d.D, d.eps, rs, red);
   const ARms<BM> a0(hp + (long)g * Dg, d.D, d.nh + (long)g * Dg, rs, m0, d.N, Dg);
-  const BRows<BN> b0(d.Wg + (long)g * 3 * Dg * Dg, Dg, j0, 32, Dg);
+  constexpr bool PRE = KG_PRE && KG_1S && F6_GATE;
+  using OpB = std::conditional_t<PRE, BPre6<BN>, BRows<BN>>;
+  const OpB b0 = gate_b<PRE, BN>(wg6, c0 / 32, Dg / BK6, d.Wg + (long)g * 3 * Dg * Dg, Dg, j0);
   f32x4 acc[1][6];
   if constexpr (KG_1S && F6_GATE) {
     ARms<BM> la[KG_PF];
-    BRows<BN> lb[KG_PF];
+    OpB lb[KG_PF];
 #pragma unroll
     for (int u = 0; u < KG_PF; ++u) {
       la[u] = a0;
@@ -627,6 +699,7 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
 // ------------------------------------------------------------------------------------------- host side
 struct IWork {
   float *a[2], *pa[2], *ad, *x0p, *px0, *x1p, *px1, *x2, *hp, *ph, *i[2], *pi[2];
+  __bf16 *wh6, *wg6;  // pre-split _dyn_hid / _dyn_gru weights (BPre6 images, 3 bf16 per element)
   long total;
 };
 long al64(long n) { return (n + 63) / 64 * 64; }
@@ -643,6 +716,9 @@ IWork iwork(const sd_imagine& d, float* base) {
   w.hp = take((long)d.N * d.D);
   w.ph = take((long)d.N * (d.D / 32));
   for (int k = 0; k < 2; ++k) { w.i[k] = take(NU); w.pi[k] = take(NP); }
+  const long Ig = d.D / d.G + 3L * d.U;
+  w.wh6 = reinterpret_cast<__bf16*>(take((long)d.D * Ig * 3 / 2));
+  w.wg6 = reinterpret_cast<__bf16*>(take((long)3 * d.D * (d.D / d.G) * 3 / 2));
   w.total = o;
   return w;
 }
@@ -687,10 +763,10 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
     k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N);
   } else if (which == 1) {
     k_hid<<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU, w.x2, w.hp,
-                                                       w.ph);
+                                                       w.ph, w.wh6);
   } else {
     // k_gate reads hold = feats(t) deter and writes feats(t + 1) deter: the same values again
-    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F);
+    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F, w.wg6);
   }
   SD_LAUNCH_CHECK();
   return SD_OK;
@@ -713,6 +789,15 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   // reads deter' (img_net_0 / _dyn_in0), the stoch part (+ bias + deter part, row partials) after the prior sample
   const float* Wa0d = d.Wa[0] + SK;  // (U, F) columns SK.. of the actor's first weight
   const int t_end = d.t_end > 0 ? d.t_end : d.H1;
+  if (d.t_begin == 0 && KH_PRE && F6_HID) {  // _dyn_hid's weight split into its bf16 planes once per imagination
+    const long Ig = D / d.G + 3L * U;
+    k_presplit6<64><<<(int)sd_cdiv((long)D * Ig / 4, 256), 256, 0, st>>>(d.Wh, D, (int)Ig, w.wh6);
+    SD_LAUNCH_CHECK();
+  }
+  if (d.t_begin == 0 && KG_PRE && KG_1S && F6_GATE) {  // and _dyn_gru's
+    k_presplit6_gate<<<(int)sd_cdiv((long)3 * D * (D / d.G) / 4, 256), 256, 0, st>>>(d.Wg, D, D / d.G, w.wg6);
+    SD_LAUNCH_CHECK();
+  }
   if (d.t_begin == 0) {  // x0p(0) = h0 . W0^T + b0 and the deter part of actor layer 0 at t = 0
     LinProb p{feats(0) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
     LinProb pd{feats(0) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
@@ -741,9 +826,9 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     SD_LAUNCH_CHECK();
     if (last) break;
     k_hid<<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU,
-                                                         w.x2, w.hp, w.ph);
+                                                         w.x2, w.hp, w.ph, w.wh6);
     SD_LAUNCH_CHECK();
-    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F);
+    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F, w.wg6);
     SD_LAUNCH_CHECK();
     {  // img_net_0, the next step's _dyn_in0 and the deter part of its actor layer 0 share A = deter'
       LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};
