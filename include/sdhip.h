@@ -296,7 +296,8 @@ typedef struct sd_imagine {
   float* feats;
   float* actions;                                                /* (H1, N, A) */
   float* work;
-  int t_begin, t_end; /* run steps [t_begin, t_end) (t_end <= 0: H1); chunks share `work` and run in order */
+  int t_begin, t_end; /* run steps [t_begin, t_end) (t_end <= 0: H1); chunks share `work` and run in order (the
+                         t_begin == 0 chunk also writes the pre-split images of _dyn_hid / _dyn_gru into `work`) */
 } sd_imagine;
 int sd_imagine_work_floats(const sd_imagine* d);
 int sd_imagine_run(const sd_imagine* d, sd_stream stream);
