@@ -106,6 +106,13 @@ int sd_twohot_logp_fwd(const float* logits, const float* bins, const float* targ
                        sd_stream stream);
 int sd_twohot_logp_bwd(const float* logits, const float* bins, const float* target, const float* glogp,
                        float* dlogits, long rows, int NB, int accumulate, sd_stream stream);
+/* Replay-value loss (dreamer.py:652-658; replaces the two TwoHot.log_prob calls, distributions.py:100-129, and the
+ * weighted mean's elementwise ops): row_loss[r] = w[r] * (-logp(ret[r]) - logp(slow[r])); the backward writes the
+ * logits gradient of mean(row_loss) * gscale[0] (device scalar), inv_n = 1 / rows. NB <= 256. */
+int sd_repval_loss_fwd(const float* logits, const float* bins, const float* ret, const float* slow, const float* w,
+                       float* row_loss, long rows, int NB, sd_stream s);
+int sd_repval_loss_bwd(const float* logits, const float* bins, const float* ret, const float* slow, const float* w,
+                       const float* gscale, float inv_n, float* dlogits, long rows, int NB, sd_stream s);
 /* bounded normal actor (bounded_normal, distributions.py:217-222): x (rows, 2A) = [mean | std-logit] */
 int sd_bnormal_sample(const float* x, float* action, long rows, int A, float min_std, float max_std, uint64_t seed,
                       int stream_id, int step, long row_offset, const uint64_t* seed_ptr, sd_stream stream);

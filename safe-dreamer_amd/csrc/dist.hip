@@ -294,6 +294,59 @@ __global__ void twohot_logp_bwd(const float* __restrict__ logits, const float* _
   }
 }
 
+// Replay-value loss (dreamer.py:652-658): row r's term w[r] * (-logp(ret[r]) - logp(slow[r])) under the TwoHot head
+// logits (distributions.py:100-129), and its logits gradient for a given d loss / d term (one wave per row). The
+// backward is the sum of the two twohot_logp_bwd terms in one pass: g (td_ret + td_slow - p (tsum_ret + tsum_slow)),
+// g = -w[r] * gscale[0] * inv_n (gscale: device scalar, d total / d mean).
+__global__ void repval_fwd_kernel(const float* __restrict__ logits, const float* __restrict__ bins,
+                                  const float* __restrict__ ret, const float* __restrict__ slow,
+                                  const float* __restrict__ w, float* __restrict__ row_loss, long rows, int NB) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long r = (long)blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const float* l = logits + r * NB;
+  float p[4], lse;
+  row_softmax64(l, NB, p, lse, lane);
+  int b1, a1, b2, a2;
+  float wb1, wa1, wb2, wa2;
+  twohot_target(bins, NB, ret[r], b1, a1, wb1, wa1, lane);
+  twohot_target(bins, NB, slow[r], b2, a2, wb2, wa2, lane);
+  if (lane == 0) {
+    float lr = wb1 * (l[b1] - lse);
+    lr += wa1 * (l[a1] - lse);
+    float ls = wb2 * (l[b2] - lse);
+    ls += wa2 * (l[a2] - lse);
+    row_loss[r] = w[r] * (-lr - ls);
+  }
+}
+
+__global__ void repval_bwd_kernel(const float* __restrict__ logits, const float* __restrict__ bins,
+                                  const float* __restrict__ ret, const float* __restrict__ slow,
+                                  const float* __restrict__ w, const float* __restrict__ gscale, float inv_n,
+                                  float* __restrict__ dlogits, long rows, int NB) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long r = (long)blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const float* l = logits + r * NB;
+  float p[4], lse;
+  row_softmax64(l, NB, p, lse, lane);
+  int b1, a1, b2, a2;
+  float wb1, wa1, wb2, wa2;
+  twohot_target(bins, NB, ret[r], b1, a1, wb1, wa1, lane);
+  twohot_target(bins, NB, slow[r], b2, a2, wb2, wa2, lane);
+  const float g = -w[r] * (gscale[0] * inv_n);
+  const float t1 = wb1 + wa1, t2 = wb2 + wa2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = lane + 64 * j;
+    if (c < NB) {
+      const float td1 = (c == b1 ? wb1 : 0.f) + (c == a1 ? wa1 : 0.f);
+      const float td2 = (c == b2 ? wb2 : 0.f) + (c == a2 ? wa2 : 0.f);
+      dlogits[r * NB + c] = g * (td1 - p[j] * t1) + g * (td2 - p[j] * t2);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- bounded normal actor
 __global__ void bnormal_sample(const float* __restrict__ x, float* __restrict__ action, long rows, int A, float min_std,
                                float max_std, uint64_t seed, uint32_t stream, uint32_t step, long row_offset,
@@ -518,6 +571,26 @@ extern "C" int sd_twohot_logp_bwd(const float* logits, const float* bins, const 
   if (NB > 256) return SD_ESHAPE;
   twohot_logp_bwd<<<blocks_for(rows, 4), 256, 0, (hipStream_t)s>>>(logits, bins, target, glogp, dlogits, rows, NB,
                                                                     accumulate);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_repval_loss_fwd(const float* logits, const float* bins, const float* ret, const float* slow,
+                                  const float* w, float* row_loss, long rows, int NB, sd_stream s) {
+  if (rows <= 0) return SD_OK;
+  if (NB > 256) return SD_ESHAPE;
+  repval_fwd_kernel<<<blocks_for(rows, 4), 256, 0, (hipStream_t)s>>>(logits, bins, ret, slow, w, row_loss, rows, NB);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_repval_loss_bwd(const float* logits, const float* bins, const float* ret, const float* slow,
+                                  const float* w, const float* gscale, float inv_n, float* dlogits, long rows, int NB,
+                                  sd_stream s) {
+  if (rows <= 0) return SD_OK;
+  if (NB > 256 || !gscale) return SD_ESHAPE;
+  repval_bwd_kernel<<<blocks_for(rows, 4), 256, 0, (hipStream_t)s>>>(logits, bins, ret, slow, w, gscale, inv_n,
+                                                                      dlogits, rows, NB);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

@@ -111,6 +111,8 @@ class Dreamer(nn.Module):
             p.requires_grad = False
         self._slow_value_updates = 0
         self._loss_scales = dict(config.loss_scales)
+        # d total / d repval as a device scalar: the replay-value backward starts from it (no scaling kernels)
+        self._repval_scale = torch.full((), float(self._loss_scales["repval"]), device=self.device)
         self._log_grads = bool(config.log_grads)
         modules = {"rssm": self.rssm, "actor": self.actor, "value": self.value, "reward": self.reward,
                    "cont": self.cont, "encoder": self.encoder}
@@ -732,7 +734,7 @@ class Dreamer(nn.Module):
         # and run at the start of the side stream's actor-critic phase (which accumulates into the same head next)
         st["rv_wgrads"] = []
         with ops.defer_wgrads(st["rv_wgrads"]):
-            (loss * self._loss_scales["repval"]).backward()
+            torch.autograd.backward(loss, self._repval_scale)
         self._mark("repval_bwd")
         st.update(repval=loss, rv_metrics=rv_metrics, rret=rret)
 
@@ -946,8 +948,12 @@ class Dreamer(nn.Module):
             value = K.twohot_mode(self.value.logits_nograd(fd), self.vbins).view(B, T)
             slow_value = K.twohot_mode(self._slow_value.logits_nograd(fd), self.vbins).view(B, T)
         vd = self.value(feat_r[:, :-1])
-        lp_s = ops.TwoHotLogProbFn.apply(vd, self.vbins, slow_value[:, :-1].contiguous().reshape(-1))
-        return dict(value=value, slow_value=slow_value, vd=vd, lp_s=lp_s)
+        with torch.no_grad():  # the loss operands that do not wait for the returns
+            last = data["is_last"].float().reshape(B, T)
+            rp = dict(slow_t=slow_value[:, :-1].contiguous(), w=(1.0 - last[:, :-1]).contiguous(),
+                      last=last.contiguous(), term=data["is_terminal"].float().reshape(B, T).contiguous(),
+                      reward=data["reward"].float().reshape(B, T).contiguous())
+        return dict(value=value, slow_value=slow_value, vd=vd, **rp)
 
     def _repval_post(self, data, rv, ret):
         """Replay lambda-return bootstrapped from the imagined return (dreamer.py:645) and the replay-value loss."""
@@ -955,14 +961,10 @@ class Dreamer(nn.Module):
         H = self.imag_horizon
         disc = 1 - 1 / self.horizon
         with torch.no_grad():
-            last = data["is_last"].float().reshape(B, T)
-            term = data["is_terminal"].float().reshape(B, T)
-            reward = data["reward"].float().reshape(B, T)
             # boot = imag ret[:, 0]: ret is (N, H) with N = (b, t)
-            rret = K.lambda_return(reward.contiguous(), ret, disc, self.lamb, term=term.contiguous(),
-                                   last=last.contiguous(), boot_row_stride=T * H, boot_t_stride=H)  # (B, T-1)
-        lp_r = ops.TwoHotLogProbFn.apply(rv["vd"], self.vbins, rret.reshape(-1))
-        loss = torch.mean((1.0 - last[:, :-1]) * (-lp_r - rv["lp_s"]))
+            rret = K.lambda_return(rv["reward"], ret, disc, self.lamb, term=rv["term"], last=rv["last"],
+                                   boot_row_stride=T * H, boot_t_stride=H)  # (B, T-1)
+        loss = ops.RepvalLossFn.apply(rv["vd"], self.vbins, rret, rv["slow_t"], rv["w"])
         return loss, {}, rret  # the replay statistics are logged from the side stream (_ph_side_ac)
 
     @torch.no_grad()

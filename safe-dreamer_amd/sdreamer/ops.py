@@ -292,6 +292,33 @@ class TwoHotLogProbFn(torch.autograd.Function):
         return dl.view(ctx.shape), None, None
 
 
+class RepvalLossFn(torch.autograd.Function):
+    """Replay-value loss mean(w * (-logp(ret) - logp(slow))) under the TwoHot value head (dreamer.py:652-658;
+    TwoHot.log_prob distributions.py:100-129): one launch forward (row terms; the mean is a torch reduce), one
+    backward launch for the logits gradient (both log-prob terms at once). Targets and weights are detached."""
+
+    @staticmethod
+    def forward(ctx, logits, bins, ret, slow, w):
+        NB = logits.shape[-1]
+        l2 = _flat(logits).contiguous()
+        r, sl, ww = (t.reshape(-1).contiguous() for t in (ret, slow, w))
+        rows = torch.empty(l2.shape[0], dtype=torch.float32, device=logits.device)
+        k.nat.call("sd_repval_loss_fwd", k.p(l2), k.p(bins), k.p(r), k.p(sl), k.p(ww), k.p(rows), l2.shape[0], NB,
+                   k.stream())
+        ctx.save_for_backward(l2, bins, r, sl, ww)
+        ctx.shape = logits.shape
+        return rows.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        l2, bins, r, sl, ww = ctx.saved_tensors
+        dl = torch.empty_like(l2)
+        gs = g.reshape(1).to(torch.float32).contiguous()
+        k.nat.call("sd_repval_loss_bwd", k.p(l2), k.p(bins), k.p(r), k.p(sl), k.p(ww), k.p(gs), 1.0 / l2.shape[0],
+                   k.p(dl), l2.shape[0], l2.shape[1], k.stream())
+        return dl.view(ctx.shape), None, None, None, None
+
+
 class BernoulliLogProbFn(torch.autograd.Function):
     """Independent(Bernoulli(logits), 1).log_prob with a single logit (binary head, distributions.py:238)."""
 
