@@ -43,6 +43,71 @@ __global__ void lambda_return_kernel(const float* __restrict__ reward, const flo
   }
 }
 
+// The same recursion with the inputs staged first: a workgroup stages LR_RB rows x T of reward, term (or continue
+// logit), last and boot into LDS with all its threads (independent loads, one round trip), then one thread per row
+// runs the serial T-step recursion from LDS. The per-thread version above issues its loads inside the serial loop,
+// one dependent memory round trip per step (the replay return at B = 16, T = 64 took 17 us). Same arithmetic, same
+// order: bit-identical.
+constexpr int LR_RB = 16;
+__global__ __launch_bounds__(256) void lambda_return_staged(const float* __restrict__ reward,
+                                                            const float* __restrict__ term_in,
+                                                            const float* __restrict__ cont_logit,
+                                                            const float* __restrict__ last_in,
+                                                            const float* __restrict__ boot, long boot_row_stride,
+                                                            long boot_t_stride, float* __restrict__ ret,
+                                                            float* __restrict__ cont_out, float* __restrict__ weight,
+                                                            int N, int T, float disc, float lamb) {
+  extern __shared__ float sm[];
+  float* s_rew = sm;
+  float* s_tc = sm + LR_RB * T;
+  float* s_last = sm + 2 * LR_RB * T;
+  float* s_boot = sm + 3 * LR_RB * T;
+  const int r0 = blockIdx.x * LR_RB;
+  for (int i = threadIdx.x; i < LR_RB * T; i += blockDim.x) {
+    const int row = i / T, t = i % T, r = r0 + row;
+    float rw = 0.f, tc = 0.f, ls = 0.f, bt = 0.f;
+    if (r < N) {
+      const long gi = (long)r * T + t;
+      rw = reward[gi];
+      tc = term_in ? term_in[gi] : cont_logit[gi];
+      ls = last_in ? last_in[gi] : 0.f;
+      bt = boot[(long)r * boot_row_stride + (long)t * boot_t_stride];
+    }
+    s_rew[i] = rw;
+    s_tc[i] = tc;
+    s_last[i] = ls;
+    s_boot[i] = bt;
+  }
+  __syncthreads();
+  const int row = threadIdx.x, r = r0 + row;
+  if (row >= LR_RB || r >= N) return;
+  const long base = (long)r * T;
+  const float* rw = s_rew + row * T;
+  const float* tc = s_tc + row * T;
+  const float* ls = s_last + row * T;
+  const float* bt = s_boot + row * T;
+  if (!term_in && (cont_out || weight)) {
+    float w = 1.f;
+    for (int t = 0; t < T; ++t) {
+      const float c = sigmoidf_(tc[t]);
+      if (cont_out) cont_out[base + t] = c;
+      w = w * (c * disc);  // torch.cumprod(imag_cont * disc)
+      if (weight) weight[base + t] = w;
+    }
+  }
+  float out = bt[T - 1];
+  for (int t = T - 2; t >= 0; --t) {
+    const int i = t + 1;
+    const float term = term_in ? tc[i] : 1.f - sigmoidf_(tc[i]);  // term = 1 - imag_cont (dreamer.py:599)
+    const float last = ls[i];
+    const float live = (1.f - term) * disc;
+    const float cnt = (1.f - last) * lamb;
+    const float interm = rw[i] + (1.f - cnt) * live * bt[i];
+    out = interm + live * cnt * out;
+    ret[(long)r * (T - 1) + t] = out;
+  }
+}
+
 SD_DEV uint32_t fkey(float f) {
   const uint32_t b = __float_as_uint(f);
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
@@ -123,9 +188,13 @@ extern "C" int sd_lambda_return(const float* reward, const float* term, const fl
                                 float* weight, int N, int T, float disc, float lamb, sd_stream s) {
   if (N <= 0 || T <= 0) return SD_OK;
   if (!term && !cont_logit) return SD_EARG;
-  lambda_return_kernel<<<(N + 255) / 256, 256, 0, (hipStream_t)s>>>(reward, term, cont_logit, last, boot,
-                                                                   boot_row_stride, boot_t_stride, ret, cont, weight, N,
-                                                                   T, disc, lamb);
+  if (T <= 255 && !(term && cont_logit))  // 4 staged (LR_RB, T) planes fit the default 64 KB of dynamic LDS
+    lambda_return_staged<<<(N + LR_RB - 1) / LR_RB, 256, 4 * LR_RB * T * sizeof(float), (hipStream_t)s>>>(
+        reward, term, cont_logit, last, boot, boot_row_stride, boot_t_stride, ret, cont, weight, N, T, disc, lamb);
+  else
+    lambda_return_kernel<<<(N + 255) / 256, 256, 0, (hipStream_t)s>>>(reward, term, cont_logit, last, boot,
+                                                                     boot_row_stride, boot_t_stride, ret, cont, weight,
+                                                                     N, T, disc, lamb);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
