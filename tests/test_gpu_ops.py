@@ -131,6 +131,28 @@ def test_twohot_mode_logp():
     close(l.grad, lr.grad, 1e-5, "dlogits")
 
 
+def test_repval_loss_fused():
+    """sd_repval_loss_fwd/bwd (ops.RepvalLossFn) vs the reference expression mean(w * (-logp(ret) - logp(slow)))
+    (dreamer.py:652-658) on the oracle's TwoHot log-prob, with the backward seeded by a loss scale."""
+    from sdreamer import ops
+    M = 1008
+    bins = R.twohot_bins(255)
+    logits = -0.5 * (torch.arange(255) - 127).abs().float() + torch.randn(M, 255, generator=_g(11))
+    ret = torch.randn(M, generator=_g(12)) * 30
+    slow = torch.randn(M, generator=_g(13)) * 30
+    ret[:4] = torch.tensor([0.0, bins[3].item(), 1e9, -1e9])
+    w = (torch.rand(M, generator=_g(14)) > 0.1).float()
+    scale = 0.3
+    lr = logits.clone().requires_grad_()
+    ref = torch.mean(w * (-R.twohot_log_prob(lr, bins, ret.unsqueeze(-1)) - R.twohot_log_prob(lr, bins, slow.unsqueeze(-1))))
+    (ref * scale).backward()
+    l = logits.to(DEV).requires_grad_()
+    out = ops.RepvalLossFn.apply(l, bins.to(DEV), ret.to(DEV), slow.to(DEV), w.to(DEV))
+    close(out, ref, 1e-5, "loss")
+    torch.autograd.backward(out, torch.full((), scale, device=DEV))
+    close(l.grad, lr.grad, 1e-5, "dlogits")
+
+
 def test_bnormal_and_bernoulli():
     from sdreamer import ops
     M, A = 300, 6
