@@ -402,6 +402,101 @@ __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2,
   ep_bias_part<BM, BN, WN, (WN < 32 ? WN : 32)>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
 }
 
+// The step's K = S*Kd contractions (actor layer 0's stoch part + _dyn_in1) read a straight-through one-hot sample:
+// every categorical holds one nonzero (the sampler writes ((k == idx) - ys) + ys: exactly 0 off the index). So
+// out[m] = b + add[m] + sum_s v_s WT[s*Kd + idx_s] — a gather of S rows of the pre-transposed weight WT (SK, U) per
+// row, not a dense (N, SK) x (SK, U) GEMM. One wave per row, 4 columns per lane (U = 256); lane s finds categorical
+// s's nonzero; the S row loads are issued in batches of OH_BATCH before their FMAs. A row with a categorical holding more
+// than one nonzero takes the exact dense loop over all SK entries instead. Row partials per 16 columns, as k_lin's.
+#ifndef KL_ONEHOT
+#define KL_ONEHOT 1
+#endif
+#ifndef OH_BATCH  // weight-row loads issued before their FMAs
+#define OH_BATCH 32
+#endif
+struct OneHotProb {
+  const float* WT;  // (SK, U) transposed weight
+  const float* bias;
+  const float* add;  // optional (M, U)
+  float* out;        // (M, U)
+  float* part;       // (U / 16, M)
+};
+__global__ __launch_bounds__(256) void k_onehot_lin(const float* X, long ldx, int SK, int Kd, OneHotProb p0,
+                                                    OneHotProb p1, int nprob, int M) {
+  constexpr int U = 256;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long m = (long)blockIdx.x * 4 + wave;
+  if (m >= M) return;
+  const int S = SK / Kd;
+  const float* x = X + m * ldx;
+  // lane s < S: categorical s's first nonzero (index, value) and whether it holds another
+  int idx = 0, many = 0;
+  float val = 0.f;
+  if (lane < S) {
+    int cnt = 0;
+    for (int j = 0; j < Kd; j += 4) {
+      const f32x4 q = ld4(x + lane * Kd + j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (q[e] != 0.f) {
+          if (cnt == 0) { idx = j + e; val = q[e]; }
+          ++cnt;
+        }
+    }
+    many = cnt > 1;
+  }
+  const bool dense = __any(many);
+  const int c = 4 * lane;
+#pragma unroll 1
+  for (int pr = 0; pr < nprob; ++pr) {
+    const OneHotProb& p = pr == 0 ? p0 : p1;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (!dense) {
+      for (int s0 = 0; s0 < S; s0 += OH_BATCH) {
+        f32x4 w[OH_BATCH];
+        float v[OH_BATCH];
+#pragma unroll
+        for (int u = 0; u < OH_BATCH; ++u) {
+          const int s = s0 + u < S ? s0 + u : S - 1;
+          const int k = s * Kd + __shfl(idx, s, 64);
+          v[u] = s0 + u < S ? __shfl(val, s, 64) : 0.f;
+          w[u] = ld4(p.WT + (long)k * U + c);
+        }
+#pragma unroll
+        for (int u = 0; u < OH_BATCH; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] += v[u] * w[u][e];
+      }
+    } else {
+      for (int k = 0; k < SK; ++k) {
+        const float xv = x[k];
+        if (xv != 0.f) {
+          const f32x4 w = ld4(p.WT + (long)k * U + c);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] += xv * w[e];
+        }
+      }
+    }
+    const f32x4 b = p.bias ? ld4(p.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 a = p.add ? ld4(p.add + m * U + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = acc[e] + b[e] + a[e];
+    *reinterpret_cast<f32x4*>(p.out + m * U + c) = o;
+    float ss = o[0] * o[0] + o[1] * o[1] + o[2] * o[2] + o[3] * o[3];
+    ss += __shfl_xor(ss, 1, 64);
+    ss += __shfl_xor(ss, 2, 64);
+    if ((lane & 3) == 0 && p.part) p.part[(long)(lane >> 2) * M + m] = ss;
+  }
+}
+// WT (K, U) = W[:, 0:K]^T for a (U, ldw) weight
+__global__ __launch_bounds__(256) void k_transpose_w(const float* W, long ldw, int U, int K, float* WT) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)U * K) return;
+  const int k = (int)(i / U), c = (int)(i % U);
+  WT[i] = W[(long)c * ldw + k];
+}
+
 // out = silu(rms(X)) . W^T + b (MLP hidden layer after the first), with row partials
 // early-store main loop order (gemm16_mainloop_pf ES): measured faster here, slower in the other imagination kernels.
 // Row partials per min(WN, 32) columns (16-row tiles: one wave per 16 columns -> 16-column partials).
@@ -700,6 +795,7 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
 struct IWork {
   float *a[2], *pa[2], *ad, *x0p, *px0, *x1p, *px1, *x2, *hp, *ph, *i[2], *pi[2];
   __bf16 *wh6, *wg6;  // pre-split _dyn_hid / _dyn_gru weights (BPre6 images, 3 bf16 per element)
+  float *waT, *w1T;   // actor layer 0's stoch columns and _dyn_in1, transposed (SK, U) for k_onehot_lin
   long total;
 };
 long al64(long n) { return (n + 63) / 64 * 64; }
@@ -719,6 +815,8 @@ IWork iwork(const sd_imagine& d, float* base) {
   const long Ig = d.D / d.G + 3L * d.U;
   w.wh6 = reinterpret_cast<__bf16*>(take((long)d.D * Ig * 3 / 2));
   w.wg6 = reinterpret_cast<__bf16*>(take((long)3 * d.D * (d.D / d.G) * 3 / 2));
+  w.waT = take((long)d.SK * d.U);
+  w.w1T = take((long)d.SK * d.U);
   w.total = o;
   return w;
 }
@@ -794,6 +892,11 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     k_presplit6<64><<<(int)sd_cdiv((long)D * Ig / 4, 256), 256, 0, st>>>(d.Wh, D, (int)Ig, w.wh6);
     SD_LAUNCH_CHECK();
   }
+  if (d.t_begin == 0 && KL_ONEHOT) {  // the one-hot contractions' weights, transposed
+    k_transpose_w<<<sd_cdiv((long)SK * U, 256), 256, 0, st>>>(d.Wa[0], F, U, SK, w.waT);
+    k_transpose_w<<<sd_cdiv((long)SK * U, 256), 256, 0, st>>>(d.W1, SK, U, SK, w.w1T);
+    SD_LAUNCH_CHECK();
+  }
   if (d.t_begin == 0 && KG_PRE && KG_1S && F6_GATE) {  // and _dyn_gru's
     k_presplit6_gate<<<(int)sd_cdiv((long)3 * D * (D / d.G) / 4, 256), 256, 0, st>>>(d.Wg, D, D / d.G, w.wg6);
     SD_LAUNCH_CHECK();
@@ -810,7 +913,12 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     {  // actor layer 0, stoch part (+ deter part); _dyn_in1 on stoch
       LinProb pa{feats(t), F, SK, d.Wa[0], F, d.ba[0], w.a[0], U, w.pa[0], w.ad};
       LinProb px{feats(t), F, SK, d.W1, SK, d.b1, w.x1p, U, w.px1, nullptr};
-      k_lin<32, KL2_BN><<<dim3(U / KL2_BN, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, px, N);
+      if (KL_ONEHOT && d.SK / d.Kd <= 64) {
+        const OneHotProb oa{w.waT, d.ba[0], w.ad, w.a[0], w.pa[0]}, ox{w.w1T, d.b1, nullptr, w.x1p, w.px1};
+        k_onehot_lin<<<sd_cdiv(N, 4), 256, 0, st>>>(feats(t), F, SK, d.Kd, oa, ox, last ? 1 : 2, N);
+      } else {
+        k_lin<32, KL2_BN><<<dim3(U / KL2_BN, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, px, N);
+      }
       SD_LAUNCH_CHECK();
     }
     int cur = 0, npa = npU;
