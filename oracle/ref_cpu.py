@@ -38,10 +38,18 @@ def unimix_logits(logits, unimix):
     return lg - lg.logsumexp(dim=-1, keepdim=True)
 
 
-def st_gumbel_sample(norm_logits, g):
-    """OneHotDist.rsample (distributions.py:32-33) = F.gumbel_softmax(hard=True) with injected gumbel g."""
+def st_gumbel_sample(norm_logits, g, force=None):
+    """OneHotDist.rsample (distributions.py:32-33) = F.gumbel_softmax(hard=True) with injected gumbel g.
+
+    force (tests only, teacher forcing at near-ties): (site, index) integer arrays; the hard sample at `site` (a
+    tuple of leading indices, e.g. (rows, latents)) takes `index` instead of the argmax. The soft part, and so the
+    straight-through gradient, is untouched."""
     y_soft = ((norm_logits + g) / 1.0).softmax(-1)
     index = y_soft.max(-1, keepdim=True)[1]
+    if force is not None:
+        site, k = force
+        index[tuple(torch.as_tensor(np.asarray(a), dtype=torch.long) for a in site) + (0,)] = \
+            torch.as_tensor(np.asarray(k), dtype=torch.long)
     y_hard = torch.zeros_like(norm_logits).scatter_(-1, index, 1.0)
     return y_hard - y_soft.detach() + y_soft
 
@@ -373,6 +381,10 @@ class Oracle:
     def __init__(self, spec: Spec, P: dict):
         self.s = spec
         self.P = P
+        # teacher forcing (tests only): {(kind, stream, step): (site arrays, indices)} for kind "obs" (posterior
+        # sample of observe step `step` on noise stream `stream`), "img" (prior sample of img_step `step`) and "act"
+        # (actor sample at imagined step `step`); see tests/test_gpu_fullsize.py
+        self.force = {}
         c = spec.cfg
         self.bins = twohot_bins(int(c.critic.dist.bin_num))
         self.rbins = twohot_bins(int(c.reward.dist.bin_num))
@@ -451,8 +463,8 @@ class Oracle:
         x = F.linear(x, P["rssm._img_net.img_net_logit.weight"], P["rssm._img_net.img_net_logit.bias"])
         return x.reshape(*x.shape[:-1], s.S, s.K)
 
-    def sample_stoch(self, logit, g):  # get_dist(logit).rsample(), rssm.py:219-220 + distributions.py:32-33
-        return st_gumbel_sample(unimix_logits(logit, self.s.unimix), g)
+    def sample_stoch(self, logit, g, force=None):  # get_dist(logit).rsample(), rssm.py:219-220 + distributions.py:32-33
+        return st_gumbel_sample(unimix_logits(logit, self.s.unimix), g, force)
 
     def observe(self, embed, action, initial, reset, seed, row_offset=0, stream=nz.STREAM_OBS):  # rssm.py:140-156
         s = self.s
@@ -469,7 +481,7 @@ class Oracle:
             deter = self.deter_step(stoch, deter, act)
             logit = self.obs_logit(deter, embed[:, i])
             g = torch.from_numpy(nz.gumbel_block(seed, stream, i, B, row_offset, s.SK)).reshape(B, s.S, s.K)
-            stoch = self.sample_stoch(logit, g)
+            stoch = self.sample_stoch(logit, g, self.force.get(("obs", stream, i)))
             stochs.append(stoch)
             deters.append(deter)
             logits.append(logit)
@@ -496,7 +508,7 @@ class Oracle:
         if s.discrete:
             nl = unimix_logits(logits, float(s.actor_dist.unimix_ratio))
             g = torch.from_numpy(nz.gumbel_block(seed, stream, step, N, row_offset, s.A))
-            return st_gumbel_sample(nl, g)
+            return st_gumbel_sample(nl, g, self.force.get(("act", stream, step)))
         loc, scale = bounded_normal_params(logits, float(s.actor_dist.min_std), float(s.actor_dist.max_std))
         eps = torch.from_numpy(nz.normal_block(seed, stream, step, N, row_offset, s.A))
         return loc + eps * scale
@@ -550,7 +562,7 @@ class Oracle:
             deter = self.deter_step(stoch, deter, action, P)
             g = torch.from_numpy(nz.gumbel_block(seed, nz.STREAM_IMG, t, N, row_offset, self.s.SK))
             ilogit = self.img_logit(deter, P)
-            stoch = self.sample_stoch(ilogit, g.reshape(N, self.s.S, self.s.K))
+            stoch = self.sample_stoch(ilogit, g.reshape(N, self.s.S, self.s.K), self.force.get(("img", nz.STREAM_IMG, t)))
             if rec is not None:
                 rec.setdefault("imag_prior_logit", []).append(ilogit)
         return torch.stack(feats, 1), torch.stack(actions, 1)

@@ -414,6 +414,8 @@ __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2,
 #ifndef OH_BATCH  // weight-row loads issued before their FMAs
 #define OH_BATCH 32
 #endif
+// k_onehot_lin writes one row partial per 16 columns (4 lanes x 4 columns); its consumers read U / KL2_PW partials
+static_assert(!KL_ONEHOT || KL2_PW == 16, "k_onehot_lin's 16-column row partials need KL2_PW == 16 (KL2_BN = 32)");
 struct OneHotProb {
   const float* WT;  // (SK, U) transposed weight
   const float* bias;

@@ -39,7 +39,8 @@ def checkpoint_items(agent):
         "optims_state_dict": osd,
         "resume": {"updates": int(agent._updates), "slow_value_updates": int(agent._slow_value_updates),
                    "optimizer_host_steps": int(agent._optimizer.host_steps), "seed_base": int(agent._seed_base),
-                   "ema_updates": int(getattr(agent, "_ema_updates", 0))},
+                   "ema_updates": int(getattr(agent, "_ema_updates", 0)),
+                   "moment_layout": "reference"},
     }
 
 
@@ -57,9 +58,11 @@ def load_checkpoint(agent, path, map_location=None):
     ckpt = torch.load(path, map_location=map_location or "cpu", weights_only=True)
     agent.load_state_dict(ckpt["agent_state_dict"])
     opt = ckpt.get("optims_state_dict", {})
-    if "_optimizer" in opt:
-        agent._optimizer.load_state_dict(_to_device(opt["_optimizer"], agent.device))
     res = ckpt.get("resume")
+    if "_optimizer" in opt:  # the reference's train.py and this module both write reference-layout moments
+        ref = not res or res.get("moment_layout") == "reference"
+        agent._optimizer.load_state_dict(_to_device(opt["_optimizer"], agent.device),
+                                         internal_layout=False if ref else None)
     if res:
         agent._updates = int(res["updates"])
         agent._slow_value_updates = int(res["slow_value_updates"])

@@ -564,14 +564,16 @@ class Dreamer(nn.Module):
         dp = self.world > 1
         if dp and self._comm is None:
             self._comm = torch.cuda.Stream(device=self.device)
-        if dp and not DEFER_WM:  # heads bucket final after M1 (else after M2d)
+        if dp and not DEFER_WM:
             ev_m1 = torch.cuda.Event()
             ev_m1.record()
-            self._allreduce_bucket("heads", ev_m1)
         with torch.cuda.stream(side):
             gS1.replay(k1)
             ev_s1 = torch.cuda.Event()
             ev_s1.record()
+        if dp and not DEFER_WM:  # heads bucket final after M1 (else after M2d); issued after S1's returns gather so
+            # RCCL's one communicator stream does not queue that gather (R waits on it) behind this all-reduce
+            self._allreduce_bucket("heads", ev_m1)
         main.wait_event(ev_s1)
         gR.replay()
         ev_rep = torch.cuda.Event()

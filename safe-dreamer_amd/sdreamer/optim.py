@@ -130,7 +130,10 @@ class LaProp(torch.optim.Optimizer):
                    "centered": False, "initial_lr": self.base_lr, "params": list(range(len(a.params)))}]
         return {"state": st, "param_groups": groups}
 
-    def load_state_dict(self, sd):
+    def load_state_dict(self, sd, internal_layout=None):
+        """internal_layout: None = infer each moment's layout from its shape (reference layout wins where both
+        match, i.e. for square permutations), False = the file declares reference-layout moments (checkpoint.py
+        writes `resume.moment_layout = "reference"`)."""
         a = self.arena
         st = sd.get("state", {})
         steps, e1, e2 = 0, 0.0, 0.0
@@ -138,10 +141,17 @@ class LaProp(torch.optim.Optimizer):
             s = st.get(i, st.get(str(i)))
             if not s:
                 continue
-            lay, shape = self.ref_layouts[i], a.params[i].shape
+            lay, shape = self.ref_layouts[i], tuple(a.params[i].shape)
+            ref_shape = shape if lay is None else tuple(lay[0](torch.empty(shape, device="meta")).shape)
             for dst, src in ((self.exp_avg, s["exp_avg"]), (self.exp_avg_sq, s["exp_avg_sq"])):
-                if lay is not None:  # state_dict moments are in the reference layout (see state_dict)
-                    src = lay[1](src)
+                # state_dict moments are in the reference layout (see state_dict); a tensor in the internal layout
+                # (a file written before the moments were stored that way) is taken as it is only when its shape
+                # cannot be mistaken for the reference one, anything else is an error rather than a silent broadcast
+                if tuple(src.shape) == ref_shape:
+                    src = src if lay is None else lay[1](src)
+                elif tuple(src.shape) != shape or (internal_layout is False and lay is not None):
+                    raise ValueError(f"LaProp state {i}: moment shape {tuple(src.shape)} matches neither the "
+                                     f"reference layout {ref_shape} nor the internal layout {shape}")
                 dst[o:o + n].view(shape).copy_(src)
             steps, e1, e2 = int(s["step"]), float(s["exp_avg_lr_1"]), float(s["exp_avg_lr_2"])
         self.scalars.copy_(torch.tensor([steps, e1, e2, 0.0][: self.scalars.numel()], dtype=torch.float64))

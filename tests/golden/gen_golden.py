@@ -1,6 +1,7 @@
 """Generate golden vectors by running the REAL reference (/root/reference) on CPU in the survey container.
 
 Run:  python tests/golden/gen_golden.py     (writes tests/golden/<case>.npz; needs /root/reference)
+      python tests/golden/gen_golden.py full [C2_walker_r2 ...]   (full-size fixtures, see full_case)
 
 For each case the reference `Dreamer` (world_model/dreamer.py:22) is built from our config surface
 (which mirrors configs/base.yaml key for key), given deterministic weights (oracle/init.py), fed a seeded
@@ -28,6 +29,10 @@ sys.path.insert(0, HERE)
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "safe-dreamer_amd"))
 
+sys.path.insert(0, os.path.dirname(HERE))
+from fullsize_io import FULL, full_inputs, fixture_path  # noqa: E402
+from fullsize_io import OVERRIDES as FULL_OVR, PARAM_SEED as FULL_PARAM_SEED, ROW_STRIDE as FULL_STRIDE  # noqa: E402
+from fullsize_io import SEED as FULL_SEED, sample_idx as full_sample_idx  # noqa: E402
 from refimport import import_reference  # noqa: E402
 
 from oracle import noise as nz  # noqa: E402
@@ -452,10 +457,135 @@ def grad_case(name, mods, TD):
     return out
 
 
+def full_case(name, mods, TD):
+    """One reference update() at a BASELINE size (tests/fullsize_io.py FULL: C2 walker B16 L64 H15, the C3 shard,
+    C4 atari B32, C5 maze B16 L256 H25 deter 4096) on the inputs full_inputs() regenerates from the case name, with
+    params_for() weights, model.warmup=0 and noise seed fullsize_io.SEED. Only outputs are stored, compactly: every
+    metric, the posterior indices, deter columns, replay returns, ReturnEMA, imagined indices / deter columns /
+    actions / returns of every ROW_STRIDE-th start row, and per parameter the norms of the step and of the second
+    moment plus 32 sampled elements of the updated parameter and both LaProp moments."""
+    cfg_name, ovr, obs, A, discrete, B, L, H = FULL[name]
+    cfg = load_config(cfg_name, ["device=cpu"] + ovr + FULL_OVR)
+    D = mods["world_model.dreamer"]
+
+    class Sp:
+        def __init__(s, shape):
+            s.shape = shape
+
+    class Spaces:
+        def __init__(s, d):
+            s.spaces = d
+
+    act_space = Sp((A,))
+    if discrete:
+        act_space.discrete = True
+    import copy
+    ag = D.Dreamer(copy.deepcopy(cfg.model), Spaces({k: Sp(v) for k, v in obs.items()}), act_space)
+    spec = Spec(cfg.model, obs, A, discrete)
+    vals = params_for(spec.shapes, FULL_PARAM_SEED)
+    with torch.no_grad():
+        named = dict(ag.named_parameters())
+        for k, v in vals.items():
+            named[k].data.copy_(torch.from_numpy(v))
+        for k, v in named.items():
+            if k.startswith("_slow_value."):
+                v.data.copy_(torch.from_numpy(vals["value." + k[len("_slow_value."):]]))
+    data_np, init_np = full_inputs(name, spec.K, spec.S, spec.D)
+    seq = NoiseSeq(L, H + 1, FULL_SEED, cfg.model.rep_loss == "dreamerpro")
+    seq.discrete_act = discrete
+    D.autocast = lambda **k: contextlib.nullcontext()
+    orig_gs = torch.nn.functional.gumbel_softmax
+    orig_rs = torch.distributions.Normal.rsample
+    rec = {}
+
+    def gs(logits, tau=1, hard=False, eps=1e-10, dim=-1):
+        g = torch.from_numpy(seq.gumbel(tuple(logits.shape)))
+        y_soft = ((logits + g) / tau).softmax(dim)
+        index = y_soft.max(dim, keepdim=True)[1]
+        return torch.zeros_like(logits).scatter_(dim, index, 1.0) - y_soft.detach() + y_soft
+
+    def rs(self, sample_shape=torch.Size()):
+        shape = self._extended_shape(sample_shape)
+        return self.loc + torch.from_numpy(seq.normal(tuple(shape))) * self.scale
+
+    def hook(obj, attr, key, many=False):
+        orig = getattr(obj, attr)
+
+        def w(*a, **k):
+            r = orig(*a, **k)
+            if many:
+                rec.setdefault(key, []).append(r)
+            else:
+                rec.setdefault(key, r)
+            return r
+
+        setattr(obj, attr, w)
+
+    hook(ag.rssm, "observe", "observe")
+    hook(ag, "_imagine", "imagine")
+    hook(ag, "_lambda_return", "lret", many=True)
+
+    class Buf:
+        def sample(self_):
+            d = TD({k: torch.from_numpy(v) for k, v in data_np.items()}, batch_size=(B, L))
+            return d, None, (torch.from_numpy(init_np[0]), torch.from_numpy(init_np[1]))
+
+        def update(self_, index, stoch, deter):
+            pass
+
+    torch.nn.functional.gumbel_softmax = gs
+    torch.distributions.Normal.rsample = rs
+    try:
+        mets = ag.update(Buf())
+    finally:
+        torch.nn.functional.gumbel_softmax = orig_gs
+        torch.distributions.Normal.rsample = orig_rs
+    assert seq.g == L + 1 + (H + 1) * (2 if discrete else 1), seq.g
+    rs_ = FULL_STRIDE[name]
+    out = {"meta_B": B, "meta_L": L, "meta_H": H, "meta_seed": FULL_SEED, "meta_param_seed": FULL_PARAM_SEED,
+           "meta_row_stride": rs_}
+    ps, pdet, _ = rec["observe"]
+    dcol = max(1, spec.D // 8)
+    out["post_idx"] = ps.argmax(-1).numpy().astype(np.uint8)
+    out["post_deter"] = pdet.detach().numpy()[..., ::dcol].copy()
+    ifeat, iact = rec["imagine"]  # (N, H1, F), (N, H1, A)
+    SK = spec.SK
+    out["imag_idx"] = ifeat[::rs_, :, :SK].reshape(-1, H + 1, spec.S, spec.K).argmax(-1).numpy().astype(np.uint8)
+    out["imag_deter"] = ifeat[::rs_, :, SK::max(1, spec.D // 4)].numpy().copy()
+    out["imag_action"] = (iact[::rs_].argmax(-1).numpy().astype(np.uint8) if discrete else iact[::rs_].numpy().copy())
+    out["imag_ret"] = rec["lret"][0][::rs_, :, 0].numpy().copy()
+    out["replay_ret"] = rec["lret"][1][..., 0].numpy().copy()
+    for k, v in mets.items():
+        out[f"m_{k}"] = np.asarray(float(v), np.float64)
+    out["ema_vals"] = ag.return_ema.ema_vals.numpy().copy()
+    named = dict(ag.named_parameters())
+    for k in spec.shapes:
+        p1 = named[k].detach().reshape(-1).numpy()
+        p0 = vals[k].reshape(-1)
+        st = ag._optimizer.state[named[k]]
+        v = st["exp_avg_sq"].reshape(-1).numpy()
+        idx = full_sample_idx(k, p1.size)
+        out[f"dp_{k}__n"] = np.asarray(np.linalg.norm(p1.astype(np.float64) - p0.astype(np.float64)))
+        out[f"v_{k}__n"] = np.asarray(np.linalg.norm(v.astype(np.float64)))
+        out[f"v_{k}__max"] = np.asarray(float(np.abs(v).max()))
+        out[f"p_{k}__s"] = p1[idx]
+        out[f"m_{k}__s"] = st["exp_avg"].reshape(-1).numpy()[idx]
+        out[f"v_{k}__s"] = v[idx]
+    return out
+
+
 def main():
     mods, TD = import_reference()
     torch.set_num_threads(8)
-    only = sys.argv[1:] or list(CASES)
+    args = sys.argv[1:]
+    if args and args[0] == "full":  # python tests/golden/gen_golden.py full [case ...]
+        for name in args[1:] or list(FULL):
+            out = full_case(name, mods, TD)
+            path = fixture_path(name)
+            np.savez_compressed(path, **out)
+            print(name, "->", path, os.path.getsize(path) // 1024, "KB")
+        return
+    only = args or list(CASES)
     lay_path = os.path.join(HERE, "optim_layout.json")
     layouts = json.load(open(lay_path)) if os.path.exists(lay_path) else {}
     for name in only:

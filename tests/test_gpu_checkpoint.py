@@ -96,3 +96,36 @@ def test_optim_state_layout_matches_reference(name, tmp_path):
     o1, o2 = ag._optimizer.state_dict(), b._optimizer.state_dict()
     for i, st in o1["state"].items():
         assert torch.equal(st["exp_avg"], o2["state"][i]["exp_avg"]) and st["step"] == o2["state"][i]["step"]
+
+
+def test_optim_load_layouts():
+    """LaProp.load_state_dict: reference-layout moments (train.py's files and save_checkpoint's) load; internal-layout
+    moments of an older file (no `moment_layout` marker) are recognised by shape; a moment whose shape matches
+    neither layout raises instead of broadcasting."""
+    a, z, spec, obs = build_agent("walker_r2")
+    _step(a, z, spec, obs, 0)
+    sd = a._optimizer.state_dict()
+    arena = a._optimizer.arena
+    internal = {"param_groups": sd["param_groups"], "state": {}}
+    packed = 0
+    for i, st in sd["state"].items():
+        lay = a._optimizer.ref_layouts[i]
+        conv = (lambda t: t) if lay is None else lay[1]
+        packed += lay is not None
+        internal["state"][i] = dict(st, exp_avg=conv(st["exp_avg"]).contiguous(),
+                                    exp_avg_sq=conv(st["exp_avg_sq"]).contiguous())
+    assert packed > 0
+    for src in (sd, internal):
+        b, _, _, _ = build_agent("walker_r2")
+        b._optimizer.load_state_dict(src)
+        o = b._optimizer.state_dict()
+        for i, st in sd["state"].items():
+            assert torch.equal(st["exp_avg"], o["state"][i]["exp_avg"]), i
+            assert torch.equal(st["exp_avg_sq"], o["state"][i]["exp_avg_sq"]), i
+    b, _, _, _ = build_agent("walker_r2")
+    with pytest.raises(ValueError):  # a file that declares reference-layout moments but holds internal ones
+        b._optimizer.load_state_dict(internal, internal_layout=False)
+    bad = {"param_groups": sd["param_groups"],
+           "state": {0: dict(sd["state"][0], exp_avg=torch.zeros(3), exp_avg_sq=torch.zeros(3))}}
+    with pytest.raises(ValueError):
+        b._optimizer.load_state_dict(bad)
