@@ -218,7 +218,14 @@ int sd_agc_laprop_step(float* params, float* grads, float* exp_avg, float* exp_a
 int sd_polyak(const float* src, float* dst, long n, float mix, sd_stream stream);
 
 /* ---------------------------------------------------------------- misc
- * Dreamer.preprocess + ConvEncoder's "-0.5": out = in/255 - shift (dreamer.py:710-713, networks.py:224) */
+ * Measurement aid: one empty dispatch (kernel k_trace_mark, `tag` workgroups, 1 <= tag <= 64) that a rocprofv3 kernel
+ * trace can find; bench.py brackets its timed steps with tags 1 and 2 (tools/kernel_table.py). */
+int sd_trace_mark(int tag, sd_stream stream);
+/* Measurement aid: shader clock under an f32-MFMA load. nwg workgroups run `iters` MFMA chains each; stamps
+ * (2 * nwg int64) receive per workgroup (shader cycles, 100 MHz ticks) around the loop: clock = cycles / ticks * 0.1 GHz.
+ * sink (nwg floats) is never written in practice. */
+int sd_clock_probe(long long* stamps, float* sink, int nwg, int iters, sd_stream stream);
+/* Dreamer.preprocess + ConvEncoder's "-0.5": out = in/255 - shift (dreamer.py:710-713, networks.py:224) */
 int sd_u8_to_f32(const uint8_t* in, float* out, long n, float shift, sd_stream stream);
 /* NHWC channel pad + shift: out[p][c] = in[p][c] - shift (c < C), 0 (C <= c < Cp). The ConvEncoder input
  * (obs - 0.5, networks.py:224) padded 3 -> 4 channels so the first conv takes the float4 / direct-wgrad paths. */
@@ -236,6 +243,21 @@ int sd_standardize_bwd(const float* x, const float* mean, const float* stdv, con
                        int C, float eps, sd_stream stream);
 int sd_barlow_loss(const float* c, int E, float lambd, float* partial, int nblocks, float* loss, sd_stream stream);
 int sd_barlow_dc(const float* c, const float* g, float* dc, int E, float lambd, sd_stream stream);
+/* Data-parallel Barlow (sdreamer/parallel.py barlow_dist; dreamer.py:525-532 over the global batch of Nt rows, R of
+ * them on this rank, E = embed width). sums (2, E): the all-reduced column sums of x1 and x2.
+ * center: d1 = x1 - sums[0] / Nt, d2 = x2 - sums[1] / Nt (R, E), q (2, E) = this rank's column sums of d^2.
+ * finish: from stats = [q (2, E) | d1^T d2 (E, E)] all-reduced: stdv (2, E) = sqrt(q / (Nt - 1)), sc = stdv + 1e-8,
+ *   c (E, E) = (d1^T d2)_ij / (sc1_i sc2_j) / Nt, n2 (R, E) = d2 / sc2, z2 (E) = (sums[1] - Nt (sums[1] / Nt)) / sc2.
+ * rowstats: s0_j = (dc z2)_j / Nt, A_j = (stdv1_j + 1e-8) sum_k dc_jk c_jk.
+ * dist_dx: dx1 = world ((dn1 - s0 / Nt) / sc1 - (x1 - sums[0] / Nt) A / (sc1^2 (Nt - 1) stdv1)), dn1 = n2 dc^T / Nt. */
+int sd_barlow_center(const float* x1, const float* x2, const float* sums, float Nt, int R, int E, float* d1, float* d2,
+                     float* q, sd_stream stream);
+int sd_barlow_finish(const float* stats, const float* sums, float Nt, int E, const float* d2, int R, float* c,
+                     float* stdv, float* n2, float* z2, sd_stream stream);
+int sd_barlow_rowstats(const float* dc, const float* c, const float* z2, const float* stdv1, float Nt, int E, float* s0,
+                       float* A, sd_stream stream);
+int sd_barlow_dist_dx(const float* x1, const float* dn1, const float* sums, const float* stdv1, const float* s0,
+                      const float* A, float Nt, float world, long R, int E, float* dx1, sd_stream stream);
 
 /* ---------------------------------------------------------------- fused RSSM posterior scan (ObserveScan)
  * RSSM.observe's recurrence (rssm.py:140-178 + Deter.forward rssm.py:36-75) for B <= 16 rows per step, as
@@ -277,6 +299,11 @@ typedef struct sd_rssm_scan {
 int sd_rssm_scan_work_floats(const sd_rssm_scan* d);
 int sd_rssm_scan_fwd(const sd_rssm_scan* d, sd_stream stream);
 int sd_rssm_scan_bwd(const sd_rssm_scan* d, sd_stream stream);
+/* Measurement aid (bench.py): one launch of forward step t's phase `which` as sd_rssm_scan_fwd issues it, after a run
+ * on the same descriptor: 0 = x1p slab (k_slab), 1 = _dyn_hid (k_hid), 2 = _dyn_gru + GRU (k_gate), 3 = obs_net_0 deter
+ * half + next _dyn_in0 (k_slab), 4 = obs_net logits + sampler (k_logit). Only t = T - 1 rewrites the values the run
+ * wrote. */
+int sd_rssm_scan_step_kernel(const sd_rssm_scan* d, int which, int t, sd_stream stream);
 
 /* ---------------------------------------------------------------- fused imagination (Dreamer._imagine)
  * Dreamer._imagine (dreamer.py:673-692) over N start states for H1 actor steps: per step the actor MLP
@@ -305,6 +332,8 @@ typedef struct sd_imagine {
   float* work;
   int t_begin, t_end; /* run steps [t_begin, t_end) (t_end <= 0: H1); chunks share `work` and run in order (the
                          t_begin == 0 chunk also writes the pre-split images of _dyn_hid / _dyn_gru into `work`) */
+  float* actor_h0;    /* optional (H1, N, U): actor layer 0's pre-norm output of every step, feat . Wa0^T + ba0 in
+                         fp32 (null: kept in `work` only); the policy loss's actor forward starts from it */
 } sd_imagine;
 int sd_imagine_work_floats(const sd_imagine* d);
 int sd_imagine_run(const sd_imagine* d, sd_stream stream);

@@ -14,10 +14,40 @@ using namespace sdb;
 #define SD_G3_FP 0
 #endif
 
+#ifndef SD_G3_XCD  // XCD-contiguous tile order (below)
+#define SD_G3_XCD 1
+#endif
+// Tile order. The dispatcher deals workgroups to the 8 XCDs round robin by linear id, and each XCD has its own L2:
+// in the plain (x fastest) order the column tiles that share an A row panel run on different XCDs at the same time,
+// so every XCD streams that panel from HBM. Remapped, XCD x runs a contiguous run of the logical order (x fastest,
+// then the row tile, then batch x split), so the tiles sharing an A row panel (and, across the short row loop of a
+// weight-gradient GEMM, a B column panel) are resident together on one XCD and read it once into its L2. When A is
+// broadcast over the batch (strideA == 0, e.g. the imagined heads' first layers: one input, four weights), the batch
+// loop moves inside the row loop, so one A panel feeds every batch entry's tiles from the same L2.
+SD_DEV void g3_tile(const GemmArgs& g, int& tx, int& ty, int& tz) {
+  const int nx = gridDim.x, ny = gridDim.y, nz = gridDim.z;
+  int L = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  if (SD_G3_XCD) {
+    const int T = nx * ny * nz, per = T / 8, rem = T % 8, xcd = L % 8, slot = L / 8;
+    L = xcd * per + (xcd < rem ? xcd : rem) + slot;  // XCD xcd holds per (+1 for the first rem XCDs) tiles
+  }
+  if (g.sA == 0 && g.batch > 1 && g.ksplit == 1) {  // A broadcast over the batch: x, then batch, then row tile
+    tx = L % nx;
+    tz = (L / nx) % nz;
+    ty = L / (nx * nz);
+  } else {
+    tx = L % nx;
+    ty = (L / nx) % ny;
+    tz = L / (nx * ny);
+  }
+}
+
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool VA, bool VB>
 __global__ __launch_bounds__(256, 2) void gemm3_kernel(GemmArgs g) {
-  const int bn0 = blockIdx.x * BN, bm0 = blockIdx.y * BM;
-  const int b = blockIdx.z / g.ksplit, split = blockIdx.z % g.ksplit;
+  int tx, ty, tz;
+  g3_tile(g, tx, ty, tz);
+  const int bn0 = tx * BN, bm0 = ty * BM;
+  const int b = tz / g.ksplit, split = tz % g.ksplit;
   const int kbeg = split * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
   const float* A = g.A + (long)b * g.sA;

@@ -912,11 +912,13 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   }
   for (int t = d.t_begin; t < t_end; ++t) {
     const bool last = t == d.H1 - 1;
+    // actor layer 0's output: the caller's per-step buffer when given (read again by the policy loss), else scratch
+    float* a0 = d.actor_h0 ? d.actor_h0 + (long)t * N * U : w.a[0];
     {  // actor layer 0, stoch part (+ deter part); _dyn_in1 on stoch
-      LinProb pa{feats(t), F, SK, d.Wa[0], F, d.ba[0], w.a[0], U, w.pa[0], w.ad};
+      LinProb pa{feats(t), F, SK, d.Wa[0], F, d.ba[0], a0, U, w.pa[0], w.ad};
       LinProb px{feats(t), F, SK, d.W1, SK, d.b1, w.x1p, U, w.px1, nullptr};
       if (KL_ONEHOT && d.SK / d.Kd <= 64) {
-        const OneHotProb oa{w.waT, d.ba[0], w.ad, w.a[0], w.pa[0]}, ox{w.w1T, d.b1, nullptr, w.x1p, w.px1};
+        const OneHotProb oa{w.waT, d.ba[0], w.ad, a0, w.pa[0]}, ox{w.w1T, d.b1, nullptr, w.x1p, w.px1};
         k_onehot_lin<<<sd_cdiv(N, 4), 256, 0, st>>>(feats(t), F, SK, d.Kd, oa, ox, last ? 1 : 2, N);
       } else {
         k_lin<32, KL2_BN><<<dim3(U / KL2_BN, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, px, N);
@@ -925,13 +927,14 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     }
     int cur = 0, npa = npU;
     for (int l = 1; l < d.actor_layers; ++l) {
-      k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(w.a[cur], d.na[l - 1], w.pa[cur], npa, U, d.Wa[l], d.ba[l], w.a[cur ^ 1],
-                                              w.pa[cur ^ 1], N, d.eps);
+      k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(l == 1 ? a0 : w.a[cur], d.na[l - 1], w.pa[cur], npa, U, d.Wa[l], d.ba[l],
+                                              w.a[cur ^ 1], w.pa[cur ^ 1], N, d.eps);
       SD_LAUNCH_CHECK();
       cur ^= 1;
       npa = npR;
     }
-    k_action<<<dim3(1, sd_cdiv(N, KA_BM)), 256, 0, st>>>(d, w.a[cur], d.na[d.actor_layers - 1], w.pa[cur], npa,
+    k_action<<<dim3(1, sd_cdiv(N, KA_BM)), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur],
+                                              d.na[d.actor_layers - 1], w.pa[cur], npa,
                                               d.actions + (long)t * N * d.A, w.x2, t, last ? 0 : 1);
     SD_LAUNCH_CHECK();
     if (last) break;

@@ -186,7 +186,136 @@ __global__ void barlow_dc(const float* __restrict__ c, const float* __restrict__
 
 int nb(long n) { return (int)((n + 255) / 256); }
 
+// ---- data-parallel Barlow (parallel.barlow_dist; dreamer.py:525-532 over the GLOBAL batch of Nt rows, this rank
+// holding R of them). Forward: local column sums -> all-reduce -> barlow_center (centred rows, local column sums of
+// squares) -> d1^T d2 (GEMM) -> all-reduce -> barlow_finish. Backward: barlow_dc, dn1 = n2 dc^T / Nt (GEMM),
+// barlow_rowstats, barlow_dist_dx.
+// d_k = x_k - sums_k / Nt, q_k = sum over this rank's rows of d_k^2 (k = 0: x1, 1: x2); grid (E / 64, 2)
+__global__ __launch_bounds__(64 * CS_NP) void barlow_center_kernel(const float* __restrict__ x1,
+                                                                   const float* __restrict__ x2,
+                                                                   const float* __restrict__ sums, float Nt, int R, int E,
+                                                                   float* __restrict__ d1, float* __restrict__ d2,
+                                                                   float* __restrict__ q) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), part = threadIdx.x >> 6, k = blockIdx.y;
+  const float* x = k ? x2 : x1;
+  float* d = k ? d2 : d1;
+  __shared__ float red[CS_NP][64];
+  const float m = c < E ? sums[(long)k * E + c] / Nt : 0.f;
+  float s = 0.f;
+  if (c < E)
+    for (int r = part; r < R; r += CS_NP) {
+      const float v = x[(long)r * E + c] - m;
+      d[(long)r * E + c] = v;
+      s += v * v;
+    }
+  red[part][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (part == 0 && c < E) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < CS_NP; ++j) t += red[j][threadIdx.x];
+    q[(long)k * E + c] = t;
+  }
+}
+// stats = [q (2, E) | craw (E, E)] summed over ranks -> s = sqrt(q / (Nt - 1)) (2, E), c = craw / (sc1_i sc2_j) / Nt,
+// n2 = d2 / sc2 (this rank's rows), z2 = (sums2 - Nt * (sums2 / Nt)) / sc2; sc = s + 1e-8. One flat index space.
+__global__ void barlow_finish_kernel(const float* __restrict__ stats, const float* __restrict__ sums, float Nt, int E,
+                                     const float* __restrict__ d2, int R, float* __restrict__ c,
+                                     float* __restrict__ s, float* __restrict__ n2, float* __restrict__ z2) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long EE = (long)E * E, RE = (long)R * E;
+  const float* q = stats;
+  auto sc_of = [&](int k, int j) { return sqrtf(q[(long)k * E + j] / (Nt - 1.f)) + 1e-8f; };
+  if (i < EE) {
+    const int r = (int)(i / E), col = (int)(i % E);
+    c[i] = stats[2L * E + i] / (sc_of(0, r) * sc_of(1, col)) / Nt;
+  } else if (i < EE + RE) {
+    const long o = i - EE;
+    n2[o] = d2[o] / sc_of(1, (int)(o % E));
+  } else if (i < EE + RE + 2L * E) {
+    const long o = i - EE - RE;
+    s[o] = sqrtf(q[o] / (Nt - 1.f));
+  } else if (i < EE + RE + 3L * E) {
+    const int j = (int)(i - EE - RE - 2L * E);
+    const float t = sums[(long)E + j];
+    z2[j] = (t - Nt * (t / Nt)) / sc_of(1, j);
+  }
+}
+// s0_j = (sum_k dc[j, k] z2[k]) / Nt, A_j = (s1_j + 1e-8) sum_k dc[j, k] c[j, k]; one wave per row j
+__global__ __launch_bounds__(256) void barlow_rowstats_kernel(const float* __restrict__ dc, const float* __restrict__ c,
+                                                              const float* __restrict__ z2,
+                                                              const float* __restrict__ s1, float Nt, int E,
+                                                              float* __restrict__ s0, float* __restrict__ A) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (j >= E) return;
+  float a = 0.f, b = 0.f;
+  for (int k = lane; k < E; k += 64) {
+    const float g = dc[(long)j * E + k];
+    a += g * z2[k];
+    b += g * c[(long)j * E + k];
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if (lane == 0) {
+    s0[j] = a / Nt;
+    A[j] = (s1[j] + 1e-8f) * b;
+  }
+}
+// dx1 = world * ((dn1 - s0 / Nt) / sc - (x1 - m1) * A / (sc^2 (Nt - 1) s1)), m1 = sums1 / Nt, sc = s1 + 1e-8
+__global__ void barlow_dist_dx_kernel(const float* __restrict__ x1, const float* __restrict__ dn1,
+                                      const float* __restrict__ sums, const float* __restrict__ s1,
+                                      const float* __restrict__ s0, const float* __restrict__ A, float Nt, float world,
+                                      long R, int E, float* __restrict__ dx1) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * E) return;
+  const int j = (int)(i % E);
+  const float sg = s1[j], sc = sg + 1e-8f, m = sums[j] / Nt;
+  dx1[i] = ((dn1[i] - s0[j] / Nt) / sc - (x1[i] - m) * (A[j] / (sc * sc * (Nt - 1.f) * sg))) * world;
+}
+
+// an empty dispatch whose name and grid (tag workgroups) a kernel trace can find: bench.py brackets its timed steps
+// with tags 1 and 2 so tools/kernel_table.py counts only the dispatches of those steps
+__global__ void k_trace_mark(int tag) {}
+
+// Shader clock under an f32 MFMA load (MI355X_MICROARCH.md 'DVFS give-back' item 6): every wave runs `iters` dependent
+// v_mfma_f32_16x16x4_f32 chains on non-trivial operands; lane 0 of wave 0 stamps s_memtime (shader cycles) and
+// s_memrealtime (100 MHz) around the loop and writes (cycles, ticks) for its workgroup to stamps[2 * wg]. The stamps go
+// to their own buffer; the accumulators feed one guarded store that never fires (keeps the loop).
+__global__ __launch_bounds__(256) void k_clock_probe(long long* stamps, float* sink, int iters) {
+  const int lane = threadIdx.x & 63;
+  float a = 1.f + 1e-3f * lane, b = 0.5f - 1e-4f * threadIdx.x;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+  const long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < iters; ++i) {
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, b, acc3, 0, 0, 0);
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    stamps[2 * blockIdx.x] = t1 - t0;
+    stamps[2 * blockIdx.x + 1] = r1 - r0;
+  }
+  const float s = acc0[0] + acc1[1] + acc2[2] + acc3[3];
+  if (s == -1.2345e30f) sink[blockIdx.x] = s;
+}
+
 }  // namespace
+
+extern "C" int sd_clock_probe(long long* stamps, float* sink, int nwg, int iters, sd_stream s) {
+  if (nwg < 1 || nwg > 4096 || iters < 1) return SD_EARG;
+  k_clock_probe<<<nwg, 256, 0, (hipStream_t)s>>>(stamps, sink, iters);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_trace_mark(int tag, sd_stream s) {
+  if (tag < 1 || tag > 64) return SD_EARG;
+  k_trace_mark<<<tag, 64, 0, (hipStream_t)s>>>(tag);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
 
 extern "C" int sd_u8_to_f32(const uint8_t* in, float* out, long n, float shift, sd_stream s) {
   if (n <= 0) return SD_OK;
@@ -257,6 +386,36 @@ extern "C" int sd_barlow_loss(const float* c, int E, float lambd, float* partial
   barlow_partial<<<nblocks, 256, 0, (hipStream_t)s>>>(c, E, lambd, partial);
   SD_LAUNCH_CHECK();
   barlow_final<<<1, 256, 0, (hipStream_t)s>>>(partial, nblocks, lambd, loss);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_barlow_center(const float* x1, const float* x2, const float* sums, float Nt, int R, int E, float* d1,
+                                float* d2, float* q, sd_stream s) {
+  if (R < 0 || E <= 0) return SD_ESHAPE;
+  barlow_center_kernel<<<dim3((E + 63) / 64, 2), 64 * CS_NP, 0, (hipStream_t)s>>>(x1, x2, sums, Nt, R, E, d1, d2, q);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_barlow_finish(const float* stats, const float* sums, float Nt, int E, const float* d2, int R, float* c,
+                                float* stdv, float* n2, float* z2, sd_stream s) {
+  if (R < 0 || E <= 0) return SD_ESHAPE;
+  const long n = (long)E * E + (long)R * E + 3L * E;
+  barlow_finish_kernel<<<nb(n), 256, 0, (hipStream_t)s>>>(stats, sums, Nt, E, d2, R, c, stdv, n2, z2);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_barlow_rowstats(const float* dc, const float* c, const float* z2, const float* s1, float Nt, int E,
+                                  float* s0, float* A, sd_stream s) {
+  if (E <= 0) return SD_ESHAPE;
+  barlow_rowstats_kernel<<<(E + 3) / 4, 256, 0, (hipStream_t)s>>>(dc, c, z2, s1, Nt, E, s0, A);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_barlow_dist_dx(const float* x1, const float* dn1, const float* sums, const float* s1, const float* s0,
+                                 const float* A, float Nt, float world, long R, int E, float* dx1, sd_stream s) {
+  if (R < 0 || E <= 0) return SD_ESHAPE;
+  if (R == 0) return SD_OK;
+  barlow_dist_dx_kernel<<<nb(R * E), 256, 0, (hipStream_t)s>>>(x1, dn1, sums, s1, s0, A, Nt, world, R, E, dx1);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

@@ -879,6 +879,50 @@ extern "C" int sd_rssm_scan_fwd(const sd_rssm_scan* dp, sd_stream stream_) {
   return SD_OK;
 }
 
+// One launch of forward step t's phase `which` exactly as sd_rssm_scan_fwd issues it (same descriptor, workspace and
+// grid): 0 = k_slab (x1p), 1 = k_hid, 2 = k_gate, 3 = k_slab (obs_net_0 deter half + next x0p), 4 = k_logit. A
+// measurement aid (bench.py times the scan's phases with it, after a full sd_rssm_scan_fwd on the same descriptor);
+// only t = T - 1 rewrites exactly the values the run wrote (the workspace slabs hold the last step's partials).
+extern "C" int sd_rssm_scan_step_kernel(const sd_rssm_scan* dp, int which, int t, sd_stream stream_) {
+  int rc = check(dp);
+  if (rc) return rc;
+  const sd_rssm_scan& d = *dp;
+  if (t < 0 || t >= d.T || which < 0 || which > 4) return SD_EARG;
+  hipStream_t st = (hipStream_t)stream_;
+  const Work w = work_layout(d, d.work);
+  const int B = d.B, D = d.D, SK = d.SK, Dg = D / d.G, Ig = Dg + 3 * UH;
+  const int span_d = D / d.ks_d, span_s = SK / d.ks_s;
+  const int cp_d = cpw_for(span_d), cp_s = cpw_for(span_s), cp_h = cpw_for(Ig);
+  if (cp_d < 0 || cp_s < 0 || cp_h < 0) return SD_ESHAPE;
+  const size_t core1 = core_lds_floats<1>() * 4;
+  const size_t lds_hid = core1 + (size_t)MR * (Ig + 4) * 4;
+  const size_t lds_gate = core_lds_floats<3>() * 4 + (size_t)MR * (Dg + 4) * 4;
+  const long BD = (long)B * D, BS = (long)B * SK;
+  if (which == 0) {
+    SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr};
+    SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(UH / 16, d.ks_s, 1), NTHR, core1, st>>>(p, p, B, UH, span_s));
+  } else if (which == 1) {
+    SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG>>(lds_hid))) return SD_EARG;
+                                   k_hid<CP, NG><<<D / 16, NTHR, lds_hid, st>>>(d, w, t)));
+  } else if (which == 2) {
+    SD_NG_SWITCH(Dg, if (!(raise_lds<k_gate<NG, NG>>(lds_gate))) return SD_EARG;
+                 k_gate<NG, NG><<<D / 16, NTHR, lds_gate, st>>>(d, w, t));
+  } else if (which == 3) {
+    SlabProb po{d.deter + t * BD, D, d.WoD, D, w.ops, nullptr};
+    SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset + (t + 1) * B};
+    const int np = t + 1 < d.T ? 2 : 1;
+    SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, np), NTHR, core1, st>>>(po, px, B, UH, span_d));
+  } else {
+    SD_KD_SWITCH(d.Kd, {
+      const size_t lds = core_lds_floats<KD / 16>() * 4 + (size_t)MR * (UH + 4) * 4;
+      if (!(raise_lds<k_logit<KD>>(lds))) return SD_EARG;
+      k_logit<KD><<<SK / KD, NTHR, lds, st>>>(d, w, t);
+    });
+  }
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
 extern "C" int sd_rssm_scan_bwd(const sd_rssm_scan* dp, sd_stream stream_) {
   int rc = check(dp);
   if (rc) return rc;

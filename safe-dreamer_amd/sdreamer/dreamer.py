@@ -50,6 +50,10 @@ FUSED_SAMPLE = os.environ.get("SDREAMER_FUSED_SAMPLE", "1") != "0"
 # csrc/img.hip runs the whole imagination as 9 fused launches per step; SDREAMER_FUSED_IMAG=0 selects the per-op
 # HIP kernels (tests compare the two)
 FUSED_IMAG = os.environ.get("SDREAMER_FUSED_IMAG", "1") != "0"
+# the policy / value losses start from first-layer outputs computed earlier in the update (the imagination's fp32
+# actor layer 0, the imagined heads' batched value layer 0) instead of re-contracting the imagined feats;
+# SDREAMER_REUSE_H0=0 recomputes them (A/B knob)
+REUSE_H0 = os.environ.get("SDREAMER_REUSE_H0", "1") != "0"
 
 
 def _symexp_bins(n, device):  # symexp_twohot bins, distributions.py:242-251
@@ -705,9 +709,13 @@ class Dreamer(nn.Module):
         self._mark("side:fork")
         start = (st["post_stoch"].detach().reshape(N, self.rssm._stoch, self.rssm._discrete),
                  st["post_deter"].detach().reshape(N, self.rssm._deter))
-        ifeat, iact = self._imagine_tm(start, H1, st["seed"], st["ro"] * T)
+        # actor layer 0's fp32 output of every imagined step, kept for the policy loss's actor forward (REUSE_H0)
+        ah0 = torch.empty(H1, N, self.actor.mlp.out_dim, device=start[1].device) \
+            if REUSE_H0 and self._fused_imag_ok() and not self.actor.mlp._symlog_inputs else None
+        ifeat, iact = self._imagine_tm(start, H1, st["seed"], st["ro"] * T, actor_h0=ah0)
         self._mark("side:imagine")
         rr = self._heads_returns(ifeat)
+        rr["act_h0"] = ah0
         self._mark("side:heads_returns")
         st.update(ifeat=ifeat, iact=iact, rr=rr)
 
@@ -979,7 +987,9 @@ class Dreamer(nn.Module):
         flat = ifeat.reshape(H1 * N, -1)
         # frozen heads on the imagined trajectories: split-bf16 contractions (no sampled index depends on them), the
         # four first layers as one batched launch
-        l_rew, l_cont, l_val, l_slow = heads_nograd((self.reward, self.cont, self.value, self._slow_value), flat, True)
+        firsts = []
+        l_rew, l_cont, l_val, l_slow = heads_nograd((self.reward, self.cont, self.value, self._slow_value), flat, True,
+                                                    firsts_out=firsts)
         i_rew = K.twohot_mode(l_rew, self.rbins).view(H1, N)
         i_contl = l_cont.view(H1, N)
         i_val = K.twohot_mode(l_val, self.vbins).view(H1, N)
@@ -990,7 +1000,11 @@ class Dreamer(nn.Module):
         weight = torch.empty(N, H1, device=dev)
         ret = K.lambda_return(rew_n, val_n, disc, self.lamb, cont_logit=contl_n, cont_out=i_cont,
                               weight_out=weight)  # (N, H)
-        return dict(ret=ret, weight=weight, i_cont=i_cont, i_rew=i_rew, i_val=i_val, i_slow=i_slow, val_n=val_n)
+        # the value head's first layer on the imagined feats, the same contraction the value loss's forward needs
+        # (_frozen_value aliases value; the weights change only at the optimizer step)
+        val_h0 = firsts[0][2] if (firsts and REUSE_H0) else None
+        return dict(ret=ret, weight=weight, i_cont=i_cont, i_rew=i_rew, i_val=i_val, i_slow=i_slow, val_n=val_n,
+                    val_h0=val_h0)
 
     @torch.no_grad()
     def _returns_norm(self, rr):
@@ -1005,7 +1019,12 @@ class Dreamer(nn.Module):
         H1, N = ifeat.shape[:2]
         H = H1 - 1
         ret, weight, adv, i_slow = rr["ret"], rr["weight"], rr["adv"], rr["i_slow"]
-        pl = self.actor(ifeat[:H].reshape(H * N, -1), fast=True)
+        xh = ifeat[:H].reshape(H * N, -1)
+        a_h0 = rr.get("act_h0")
+        if a_h0 is not None:  # layer 0 from the imagination (fp32), layers 1.. and the output on split-bf16
+            pl = self.actor.forward_from_first(xh, a_h0[:H].reshape(H * N, -1), fast=True)
+        else:
+            pl = self.actor(xh, fast=True)
         if self.act_discrete:
             logpi, ent = ops.OneHotLogProbEntFn.apply(pl, iact[:H].reshape(H * N, -1),
                                                        float(self.config.actor.dist.unimix_ratio))
@@ -1016,7 +1035,11 @@ class Dreamer(nn.Module):
         logpi, ent = logpi.view(H, N).t(), ent.view(H, N).t()
         w = weight[:, :H]
         losses["policy"] = torch.mean(w * -(logpi * adv + self.act_entropy * ent))
-        vl = self.value(ifeat[:H].reshape(H * N, -1), fast=True)
+        v_h0 = rr.get("val_h0")
+        if v_h0 is not None:  # layer 0 from the imagined heads' batched launch (its first H * N rows)
+            vl = self.value.forward_from_first(xh, v_h0[:H * N], fast=True)
+        else:
+            vl = self.value(xh, fast=True)
         lp_tar = ops.TwoHotLogProbFn.apply(vl, self.vbins, ret.t().contiguous().reshape(-1))
         lp_slow = ops.TwoHotLogProbFn.apply(vl, self.vbins, i_slow[:H].reshape(-1))
         losses["value"] = torch.mean(w * (-lp_tar - lp_slow).view(H, N).t())
@@ -1050,7 +1073,7 @@ class Dreamer(nn.Module):
             (A <= 16 if self.act_discrete else 2 * A <= 32) and 1 <= a.mlp.n <= 4 and 1 <= r._img_layers <= 4 and \
             a.last.weight.shape[0] <= 32
 
-    def _imagine_fused(self, feats, actions, H1, seed, row_offset, chunks=None, keep=None):
+    def _imagine_fused(self, feats, actions, H1, seed, row_offset, chunks=None, keep=None, actor_h0=None):
         """sd_imagine_run (csrc/img.hip): feats[0] holds the start state. chunks: step boundaries [t0, t1, ..., H1];
         the steps run as one launch sequence per chunk with an event recorded after each (returned), so consumers on
         other streams can start on a chunk's feats while the next chunk is imagined."""
@@ -1082,6 +1105,9 @@ class Dreamer(nn.Module):
             d.Wi[i], d.bi[i], d.ni[i] = lin.weight.data_ptr(), lin.bias.data_ptr(), norm.weight.data_ptr()
         d.Wl, d.bl = last.weight.data_ptr(), last.bias.data_ptr()
         d.feats, d.actions = feats.data_ptr(), actions.data_ptr()
+        if actor_h0 is not None:
+            assert actor_h0.is_contiguous() and tuple(actor_h0.shape) == (H1, N, r._hidden), actor_h0.shape
+            d.actor_h0 = actor_h0.data_ptr()
         nwork = nat.fns["sd_imagine_work_floats"](ctypes.addressof(d))
         if nwork < 0:
             raise nat.NativeError(f"sd_imagine_work_floats failed with status {nwork}")
@@ -1100,7 +1126,7 @@ class Dreamer(nn.Module):
                 events.append(ev)
         return events
 
-    def _imagine_tm(self, start, H1, seed, row_offset=0, chunks=None):
+    def _imagine_tm(self, start, H1, seed, row_offset=0, chunks=None, actor_h0=None):
         """Dreamer._imagine (dreamer.py:673-692), time-major: feats (H1, N, F), actions (H1, N, A).
         The reference's last img_step (whose output is discarded) is skipped. With `chunks` (step boundaries) returns
         (feats, actions, events) with one event per chunk (see _imagine_fused)."""
@@ -1114,7 +1140,7 @@ class Dreamer(nn.Module):
         if self._fused_imag_ok():
             feats[0, :, :SK] = s
             feats[0, :, SK:] = h
-            events = self._imagine_fused(feats, actions, H1, seed, row_offset, chunks)
+            events = self._imagine_fused(feats, actions, H1, seed, row_offset, chunks, actor_h0=actor_h0)
             return (feats, actions, events) if chunks else (feats, actions)
         for t in range(H1):
             feats[t, :, :SK] = s

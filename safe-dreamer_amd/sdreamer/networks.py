@@ -148,6 +148,15 @@ class MLP(nn.Module):
             x = ops.rms_silu(ops.linear(x, lin.weight, lin.bias, fast), norm.weight)
         return x
 
+    def forward_from_first(self, x, h0, fast=False):
+        """forward whose first linear output h0 = x . W0^T + b0 is given (ops.LinearPreFn: the backward still
+        produces W0 / b0's gradients from x)."""
+        (lin, norm), rest = self._mods[0], self._mods[1:]
+        h = ops.rms_silu(ops.linear_pre(h0, x, lin.weight, lin.bias), norm.weight)
+        for lin, norm in rest:
+            h = ops.rms_silu(ops.linear(h, lin.weight, lin.bias, fast), norm.weight)
+        return h
+
     @torch.no_grad()
     def forward_nograd(self, x, fast=False):
         if self._symlog_inputs:
@@ -175,6 +184,12 @@ class MLPHead(nn.Module):
         """fast: split-bf16 contractions (imagined trajectories; see ops.LinearFn)."""
         return ops.linear(self.mlp(x, fast), self.last.weight, self.last.bias, fast)
 
+    def forward_from_first(self, x, h0, fast=False):
+        """logits given the first layer's pre-norm output h0 (same rows as x), with gradients for every layer."""
+        if self.mlp._symlog_inputs:
+            return self.forward(x, fast)
+        return ops.linear(self.mlp.forward_from_first(x, h0, fast), self.last.weight, self.last.bias, fast)
+
     @torch.no_grad()
     def logits_nograd(self, x, fast=False):
         h = self.mlp.forward_nograd(x.reshape(-1, x.shape[-1]), fast)
@@ -191,10 +206,11 @@ class MLPHead(nn.Module):
 
 
 @torch.no_grad()
-def heads_nograd(heads, x, fast=False):
+def heads_nograd(heads, x, fast=False, firsts_out=None):
     """Frozen logits of several MLPHeads on the same input rows x (M, F) with ONE batched launch for their first
     layers (the contraction over F dominates: A is read once per column tile for all heads, 4x the workgroups of
-    one head's launch). Falls back to per-head forwards when the first layers differ in shape or use symlog."""
+    one head's launch). Falls back to per-head forwards when the first layers differ in shape or use symlog.
+    firsts_out (a list): receives the (n, M, U) first-layer outputs of the batched launch (kept for reuse)."""
     firsts = [h.mlp._mods[0][0] for h in heads]
     shape = tuple(firsts[0].weight.shape)
     if any(h.mlp._symlog_inputs or h.mlp.n < 1 for h in heads) or any(tuple(f.weight.shape) != shape for f in firsts):
@@ -205,6 +221,8 @@ def heads_nograd(heads, x, fast=False):
     b = torch.stack([f.bias for f in firsts])  # (n, U)
     h0 = torch.empty(n, M, shape[0], dtype=torch.float32, device=x.device)
     K.gemm(x.expand(n, M, x.shape[1]), w.transpose(1, 2), h0, bias=b, fast=fast)
+    if firsts_out is not None:
+        firsts_out.append(h0)
     return [h.logits_from_first(h0[i], fast) for i, h in enumerate(heads)]
 
 

@@ -94,6 +94,35 @@ class LinearFn(torch.autograd.Function):
         return dx, None, None, None
 
 
+class LinearPreFn(torch.autograd.Function):
+    """A linear layer whose forward output h = x W^T + b was already computed elsewhere (the imagination's fp32 actor
+    layer 0, the imagined heads' batched first layers): forward returns h0 as the layer's output, backward accumulates
+    the weight / bias gradients exactly as LinearFn does (split-bf16 dW = dh^T x, column sums for db). x is a detached
+    input (imagined features): no input gradient."""
+
+    @staticmethod
+    def forward(ctx, h0, x, w, b):
+        ctx.save_for_backward(_flat(x).contiguous(), w, b)
+        return h0.view_as(h0)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, b = ctx.saved_tensors
+        dy2 = _flat(dy).contiguous()
+
+        def wgrad():
+            if w.requires_grad:
+                k.gemm(dy2.t(), x2, grad_buf(w), beta=1.0, fast=True)
+            if b is not None and b.requires_grad:
+                k.colsum(dy2, grad_buf(b), accumulate=True)
+
+        if _DEFER is not None:
+            _DEFER.append((wgrad, (dy2, x2)))
+        else:
+            wgrad()
+        return None, None, None, None
+
+
 class RmsSiluFn(torch.autograd.Function):
     """nn.RMSNorm(eps=1e-4) followed by SiLU (act=1) or nothing (act=0)."""
 
@@ -149,6 +178,10 @@ class BlockLinearFn(torch.autograd.Function):
 
 def linear(x, w, b=None, fast=False):
     return LinearFn.apply(x, w, b, fast)
+
+
+def linear_pre(h0, x, w, b=None):
+    return LinearPreFn.apply(h0, x, w, b)
 
 
 def rms_silu(x, w, act=1):

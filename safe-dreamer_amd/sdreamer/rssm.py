@@ -282,6 +282,9 @@ class RSSM(nn.Module):
         return st, logit
 
 
+SCAN_KEEP = None  # bench.py sets a dict: the next fused observe scan's descriptor and buffers are kept in it
+
+
 class ObserveScan(torch.autograd.Function):
     """RSSM.observe (rssm.py:140-156) forward + BPTT backward on HIP kernels. Saved activations are time-major."""
 
@@ -337,6 +340,10 @@ class ObserveScan(torch.autograd.Function):
             op = torch.empty(T, B, U, dtype=f32, device=dev)  # eproj stays the (embed half + bias) input
             d.op = op.data_ptr()
             nat.call("sd_rssm_scan_fwd", ctypes.addressof(d), K.stream())
+            if SCAN_KEEP is not None:  # measurement aid (bench.py): the descriptor and every buffer it points to
+                SCAN_KEEP.update(desc=d, work=work, WoD=WoD, bufs=(s_in, h_in, x0p, x1p, r0, r1, xcat, hp, hh, rh,
+                                                                   gates, deter, op, oo, ro, logit, stoch, x2, eproj,
+                                                                   rt, stoch0, deter0), T=T, B=B)
         else:
             xcat[:, :, 2 * U:] = x2.view(T, B, U)
         prev_s, prev_h = stoch0, deter0

@@ -345,6 +345,45 @@ def test_barlow():
     close(xd.grad, xr.grad, 1e-5, "grad")
 
 
+@pytest.mark.parametrize("Nr,E", [(512, 1024), (96, 64)])
+def test_barlow_dist_steps(Nr, E):
+    """parallel.BarlowSteps (the data-parallel Barlow's HIP launches, csrc/misc.hip sd_barlow_*) at world 1 against the
+    single-GPU definition in torch fp32 (dreamer.py:525-532): loss and dx1 (x world = 1), and every intermediate the
+    exchange steps pass on (sums, centred rows, q, c, stds, n2, z2) against its torch formula."""
+    from sdreamer import parallel
+    BS = parallel.BarlowSteps
+    x1 = torch.randn(Nr, E, generator=_g(3)) * 2 + 0.5
+    x2 = torch.randn(Nr, E, generator=_g(4)) - 0.25
+    xr = x1.clone().requires_grad_()
+    x1n = (xr - xr.mean(0)) / (xr.std(0) + 1e-8)
+    x2n = (x2 - x2.mean(0)) / (x2.std(0) + 1e-8)
+    c_ref = torch.mm(x1n.T, x2n) / Nr
+    off = ~torch.eye(E, dtype=torch.bool)
+    loss = (torch.diagonal(c_ref) - 1).pow(2).sum() + 5e-4 * c_ref[off].pow(2).sum()
+    loss.backward()
+    xd, x2d = x1.to(DEV), x2.to(DEV)
+    Nt = float(Nr)
+    sums = BS.colsums(xd, x2d)
+    close(sums, torch.stack([x1.sum(0), x2.sum(0)]), 1e-5, "sums")
+    d1, d2, stats = BS.center(xd, x2d, sums, Nt)
+    m = sums.cpu() / Nt
+    close(d1, x1 - m[0], 1e-6, "d1")
+    close(d2, x2 - m[1], 1e-6, "d2")
+    e1, e2 = x1 - m[0], x2 - m[1]
+    close(stats[:2 * E], torch.cat([(e1 * e1).sum(0), (e2 * e2).sum(0)]), 1e-5, "q")
+    close(stats[2 * E:].view(E, E), e1.t() @ e2, 1e-5, "d1^T d2")
+    c, st, n2, z2 = BS.finish(stats, sums, Nt, d2)
+    close(c, c_ref, 1e-5, "c")
+    close(st, torch.stack([x1.std(0), x2.std(0)]), 1e-5, "stds")
+    close(n2, x2n, 1e-5, "n2")
+    close(z2, torch.zeros(E), 1e-4, "z2")
+    xg = xd.clone().requires_grad_()
+    ld = parallel._DistBarlowLoss.apply(xg, c, sums, st, n2, z2, 5e-4, Nt, 1)
+    close(ld, loss, 1e-5, "loss")
+    ld.backward()
+    close(xg.grad, xr.grad, 1e-5, "dx1")
+
+
 @pytest.mark.parametrize("warmup", [1000, 0])
 def test_laprop_agc_step(warmup):
     """sd_agc_laprop_step (AGC agc.py:15-53 + LaProp laprop.py:85-116 + LambdaLR warm-up dreamer.py:214-225) vs the

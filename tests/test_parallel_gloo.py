@@ -19,13 +19,55 @@ def _free_port():
     return p
 
 
+class _TorchBarlowSteps:
+    """torch restatement of parallel.BarlowSteps' HIP launches (csrc/misc.hip sd_barlow_*), same formulas, so the
+    exchange decomposition runs on gloo CPU ranks; the HIP launches themselves are checked on the GPU
+    (tests/test_gpu_ops.py test_barlow_dist_steps)."""
+
+    @staticmethod
+    def colsums(xd, x2):
+        return torch.stack([xd.sum(0), x2.sum(0)])
+
+    @staticmethod
+    def center(xd, x2, sums, Nt):
+        m = sums / Nt
+        d1, d2 = xd - m[0], x2 - m[1]
+        E = xd.shape[1]
+        stats = torch.cat([(d1 * d1).sum(0), (d2 * d2).sum(0), (d1.t() @ d2).reshape(-1)])
+        return d1, d2, stats
+
+    @staticmethod
+    def finish(stats, sums, Nt, d2):
+        E = d2.shape[1]
+        q, craw = stats[:2 * E].view(2, E), stats[2 * E:].view(E, E)
+        s = torch.sqrt(q / (Nt - 1.0))
+        sc = s + 1e-8
+        c = craw / (sc[0][:, None] * sc[1][None, :]) / Nt
+        return c, s, d2 / sc[1], (sums[1] - Nt * (sums[1] / Nt)) / sc[1]
+
+    @staticmethod
+    def loss(c, lambd):
+        d = torch.diagonal(c)
+        return (d - 1.0).pow(2).sum() + lambd * (c.pow(2).sum() - d.pow(2).sum())
+
+    @staticmethod
+    def grad_x1(x1, c, sums, st, n2, z2, g, lambd, Nt, world):
+        eye = torch.eye(c.shape[0], dtype=torch.bool)
+        dc = torch.where(eye, 2.0 * (c - 1.0), 2.0 * lambd * c) * g
+        dn1 = n2 @ dc.t() / Nt
+        sc = st[0] + 1e-8
+        s0 = (dc @ z2) / Nt
+        A = sc * (dc * c).sum(1)
+        m1 = sums[0] / Nt
+        return ((dn1 - s0 / Nt) / sc - (x1 - m1) * (A / (sc * sc * (Nt - 1) * st[0]))) * world
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        import sdreamer.kernels as K
         from sdreamer import parallel
-        K.mm = lambda a, b, alpha=1.0, **kw: alpha * (a @ b)  # CPU stand-in for the HIP GEMM (test only)
+        parallel.BarlowSteps = _TorchBarlowSteps  # CPU ranks: torch stand-ins for the HIP launches (test only)
         torch.manual_seed(0)
         g = torch.randn(10)
         t = g * (rank + 1)
