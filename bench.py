@@ -208,62 +208,228 @@ def wm_loss_parity_full(name="C2_walker_r2"):
                     f"B{B} L{L} H{H}, same weights / batch / noise seed)"}
 
 
-IMAG_KERNELS = {  # sd_imagine_step_kernel `which` -> (label, FLOP per launch as f(N, D, U, Dg))
-    0: ("k_lin<32, 32> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
-        "GEMMs in one launch, RMSNorm row partials in the epilogue; v_mfma_f32_16x16x4_f32)",
-        lambda N, D, U, Dg: 3 * 2.0 * N * D * U),
-    1: ("k_hid (imagination step: _dyn_hid BlockLinear, K = Dg + 3U per block, RMSNorm + SiLU of x0 / x1 in the A "
-        "loader; bf16x6)", lambda N, D, U, Dg: 2.0 * N * D * (Dg + 3 * U)),
-    2: ("k_gate (imagination step: _dyn_gru BlockLinear + GRU epilogue, RMSNorm + SiLU of hp in the A loader; bf16x6)",
-        lambda N, D, U, Dg: 2.0 * N * 3 * D * Dg),
+# The committed kernel table of this build (tools/profile_round.sh -> tools/kernel_table.py: the rocprofv3 kernel trace
+# of a bench run, windowed to its timed steps, joined with the separate --pmc passes). Named explicitly, never "the
+# newest file": its rows rank the update's launch shapes by time per update and carry their counter traffic.
+KERNEL_TABLE = "profiles/r03b_kernel_table.json"
+
+
+def clock_probe(nwg=256, iters=20000, reps=3):
+    """Shader clock under an f32-MFMA load (sd_clock_probe: per workgroup s_memtime cycles / s_memrealtime ticks around
+    an MFMA loop, MI355X_MICROARCH.md 'DVFS give-back' item 6): median over workgroups of the last of `reps` launches."""
+    from sdreamer import _native as nat
+    from sdreamer import kernels as K
+    stamps = torch.zeros(2 * nwg, dtype=torch.int64, device="cuda")
+    sink = torch.empty(nwg, device="cuda")
+    for _ in range(reps):
+        nat.call("sd_clock_probe", stamps.data_ptr(), sink.data_ptr(), nwg, iters, K.stream())
+    torch.cuda.synchronize()
+    st = stamps.view(nwg, 2).cpu().double()
+    ghz = (st[:, 0] / st[:, 1].clamp_min(1) * 0.1).median().item()
+    return round(ghz, 3)
+
+
+class _ImagStep:
+    """sd_imagine_step_kernel: one launch of an imagination step's kernel (0 k_lin, 1 k_hid, 2 k_gate) re-issued after a
+    run at the update's shape (same descriptor, workspace and grid), back to back between two HIP events on the stream
+    it is launched on (per-launch event pairs would add the events' own cost to every launch)."""
+
+    def __init__(self, agent, cfg):
+        r = agent.rssm
+        B, L, H = int(cfg.batch_size), int(cfg.batch_length), int(cfg.model.imag_horizon)
+        self.N, self.H1, dev = B * L, H + 1, agent.device
+        g = torch.Generator(device=dev).manual_seed(11)
+        idx = torch.randint(0, r._discrete, (self.N, r._stoch), device=dev, generator=g)
+        SK, D = r.flat_stoch, r._deter
+        feats = torch.empty(self.H1, self.N, SK + D, device=dev)
+        actions = torch.empty(self.H1, self.N, agent.act_dim, device=dev)
+        feats[0, :, :SK] = torch.nn.functional.one_hot(idx, r._discrete).float().reshape(self.N, SK)
+        feats[0, :, SK:] = torch.randn(self.N, D, device=dev, generator=g)
+        self.keep = {}
+        with torch.no_grad():
+            agent._imagine_fused(feats, actions, self.H1, 5, 0, keep=self.keep)
+        torch.cuda.synchronize()
+
+    def time(self, which, reps=30):
+        import ctypes
+        from sdreamer import _native as nat
+        from sdreamer import kernels as K
+        desc = self.keep["desc"]
+        H = self.H1 - 1
+        # k_gate rewrites feats(t + 1): only t = H - 1 reproduces the run's values (the probe times, it keeps no output)
+        ts = [H - 1] * reps if which == 2 else [i % H for i in range(reps)]
+        nat.call("sd_imagine_step_kernel", ctypes.addressof(desc), which, ts[0], K.stream())  # warm
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for t in ts:
+            nat.call("sd_imagine_step_kernel", ctypes.addressof(desc), which, t, K.stream())
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps * 1e3
+
+
+class _ScanStep:
+    """sd_rssm_scan_step_kernel: one launch of an observe-scan forward phase (0 x1p slab, 1 k_hid, 2 k_gate, 3 obs_net_0 +
+    next x0p slab, 4 k_logit) at step T - 1, re-issued after an eager RSSM.observe at the update's shape."""
+
+    def __init__(self, agent, cfg):
+        from sdreamer import rssm as R
+        r = agent.rssm
+        B, L = int(cfg.batch_size), int(cfg.batch_length)
+        dev = agent.device
+        g = torch.Generator(device=dev).manual_seed(13)
+        embed = torch.randn(B, L, r.embed_size, device=dev, generator=g)
+        action = torch.rand(B, L, r._act_dim, device=dev, generator=g) * 2 - 1
+        reset = torch.zeros(B, L, 1, dtype=torch.bool, device=dev)
+        reset[:, 0] = True
+        R.SCAN_KEEP = {}
+        try:
+            with torch.no_grad():
+                self.out = r.observe(embed, action, r.initial(B), reset, seed=5)
+            torch.cuda.synchronize()
+            self.keep = R.SCAN_KEEP
+        finally:
+            R.SCAN_KEEP = None
+        self.ok = "desc" in self.keep
+
+    def time(self, which, reps=40):
+        import ctypes
+        from sdreamer import _native as nat
+        from sdreamer import kernels as K
+        desc = self.keep["desc"]
+        t = self.keep["T"] - 1
+        nat.call("sd_rssm_scan_step_kernel", ctypes.addressof(desc), which, t, K.stream())
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            nat.call("sd_rssm_scan_step_kernel", ctypes.addressof(desc), which, t, K.stream())
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps * 1e3
+
+
+def probe_specs(agent, cfg, K):
+    """The update's largest launch shapes that bench.py can re-time live, keyed by the kernel-table row they match
+    (demangled name, launch grid in workgroups). Each entry: bound, work per launch (FLOP or bytes), algorithmic bytes
+    per launch (every operand read once, every output written once), and how to time it. LaunchProbes must exist
+    before the warm-up updates (they record the launch while the update's graphs are captured)."""
+    r = agent.rssm
+    B, L, H = int(cfg.batch_size), int(cfg.batch_length), int(cfg.model.imag_horizon)
+    N, D, U, SK, G, A = B * L, r._deter, r._hidden, r.flat_stoch, r._blocks, agent.act_dim
+    Dg, Ig, F = D // G, D // G + 3 * U, SK + D
+    ksd, kss = 4, 2
+    out = []
+
+    def add(key, name, grid, bound, work, algo, label, how, launches):
+        out.append(dict(key=key, name=name, grid=list(grid), bound=bound, work=work, algo=algo, label=label, how=how,
+                        launches=launches))
+
+    # encoder stage 2 forward (conv + pool + RMSNorm + SiLU, direct conv from an LDS patch)
+    cp = dominant_probe(K)
+    if K.ops_fused_pool():
+        pix = N * 32 * 32
+        add("conv_stage2", "conv_fwd_direct_pool<48, 32, 5, 5, 1>", (N * 32 * 32 // 128, 1, 1), "mfma",
+            2.0 * pix * 48 * 25 * 32, 4.0 * pix * 32 + N * 16 * 16 * (48 * 9 + 4), cp.label, ("launch", cp), 1)
+    # imagined heads' first layers: one split-bf16 GEMM, A = the imagined feats broadcast over 4 weights
+    M = N * (H + 1)
+    hp = K.LaunchProbe("sd_gemm_bf16x3", lambda a: a[0]._obj.batch == 4 and a[0]._obj.strideA == 0,
+                       lambda a: 2.0 * a[0]._obj.M * a[0]._obj.N * a[0]._obj.K * a[0]._obj.batch,
+                       label="gemm3_kernel<128, 128> (imagined reward / continue / value / slow-value first layers: "
+                             "(M, F) x 4 (F, U) split-bf16, 3 bf16 MFMAs per f32-equivalent product)")
+    add("heads_l0", "gemm3_kernel<128, 128", (U // 128, M // 128, 4), "mfma",
+        2.0 * M * F * U * 4, 4.0 * (M * F + 4 * F * U + 4 * M * U), hp.label, ("launch", hp), 1)
+    # imagination step kernels
+    imag = [("imag_k_lin", "k_lin<32, 32>", (U // 32, N // 32, 3), 3 * 2.0 * N * D * U,
+             4.0 * (N * D + 3 * U * D + 3 * N * U + 2 * (U // 16) * N), IMAG_LABELS[0], 0),
+            ("imag_k_hid", "k_hid", (D // 64, N // 64, 1), 2.0 * N * D * Ig,
+             4.0 * (N * D + 3 * N * U + D * Ig + N * D + N * D // 64), IMAG_LABELS[1], 1),
+            ("imag_k_gate", "k_gate", (D // 32, N // 64, 1), 2.0 * N * 3 * D * Dg,
+             4.0 * (N * D + 3 * D * Dg + 2 * N * D), IMAG_LABELS[2], 2)]
+    for key, name, grid, work, algo, label, which in imag:
+        add(key, name, grid, "mfma", work, algo, label, ("imag", which), H)
+    # observe-scan forward phases (M = B rows: weight-streaming, bytes-bound)
+    scan = [("scan_k_hid", "k_hid<8, 2>", (D // 16, 1, 1), 4.0 * (D * Ig + 2 * B * D + (ksd + kss + 1) * B * U),
+             "scan k_hid (RSSM.observe step: _dyn_hid BlockLinear, M = B rows, 16-column tiles; x0 / x1 RMSNorm + SiLU "
+             "prologue)", 1),
+            ("scan_k_gate", "k_gate<2, 2>", (D // 16, 1, 1), 4.0 * (3 * D * Dg + 8 * B * D),
+             "scan k_gate (_dyn_gru BlockLinear + GRU epilogue, M = B rows)", 2),
+            ("scan_k_logit", "k_logit<%d>" % r._discrete, (SK // r._discrete, 1, 1),
+             4.0 * (SK * U + (ksd + 1) * B * U + 3 * B * SK + 2 * B * U),
+             "scan k_logit (obs_net RMSNorm + logits + unimix one-hot sampler)", 4),
+            ("scan_k_slab_obs", "k_slab<4>", (U // 16, ksd, 2), 4.0 * (2 * U * D + B * D + 2 * ksd * B * U),
+             "scan k_slab (obs_net_0 deter half + next _dyn_in0, split-K slabs)", 3),
+            ("scan_k_slab_x1", "k_slab<2>", (U // 16, kss, 1), 4.0 * (U * SK + B * SK + kss * B * U),
+             "scan k_slab (_dyn_in1 on the sampled stoch, split-K slabs)", 0)]
+    for key, name, grid, algo, label, which in scan:
+        add(key, name, grid, "hbm", algo, algo, label, ("scan", which), L)
+    return out
+
+
+IMAG_LABELS = {
+    0: "k_lin<32, 32> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
+       "GEMMs in one launch, RMSNorm row partials in the epilogue; v_mfma_f32_16x16x4_f32)",
+    1: "k_hid (imagination step: _dyn_hid BlockLinear, K = Dg + 3U per block, RMSNorm + SiLU of x0 / x1 in the A "
+       "loader; bf16x6)",
+    2: "k_gate (imagination step: _dyn_gru BlockLinear + GRU epilogue, RMSNorm + SiLU of hp in the A loader; bf16x6)",
 }
 
 
-def imag_kernel_probe(agent, cfg, which=0, reps=30):
-    """Roofline probe on the update's dominant kernel symbol, k_lin<32, 32> (imagination; largest total time per
-    update, profiles/r02_kernel_summary.md): the imagination runs once at the update's shape (N = B*L start rows),
-    then its step-t launch is re-issued alone (sd_imagine_step_kernel: same descriptor, workspace and grid) `reps`
-    times over t = 0 .. H-1, back to back between two HIP events on the stream it is launched on (per-launch event
-    pairs would add the event records' own cost to every launch; back to back only the ~1 us dispatch gap remains)."""
-    import ctypes
-    from sdreamer import _native as nat
-    from sdreamer import kernels as K
-    r = agent.rssm
-    B, L, H = int(cfg.batch_size), int(cfg.batch_length), int(cfg.model.imag_horizon)
-    N, H1, dev = B * L, H + 1, agent.device
-    SK, D, U, G = r.flat_stoch, r._deter, r._hidden, r._blocks
-    g = torch.Generator(device=dev).manual_seed(11)
-    idx = torch.randint(0, r._discrete, (N, r._stoch), device=dev, generator=g)
-    feats = torch.empty(H1, N, SK + D, device=dev)
-    actions = torch.empty(H1, N, agent.act_dim, device=dev)
-    feats[0, :, :SK] = torch.nn.functional.one_hot(idx, r._discrete).float().reshape(N, SK)
-    feats[0, :, SK:] = torch.randn(N, D, device=dev, generator=g)
-    keep = {}
-    with torch.no_grad():
-        agent._imagine_fused(feats, actions, H1, 5, 0, keep=keep)
-    torch.cuda.synchronize()
-    desc = keep["desc"]
-    label, flop = IMAG_KERNELS[which]
-    work = flop(N, D, U, D // G)
-    nat.call("sd_imagine_step_kernel", ctypes.addressof(desc), which, 0, K.stream())  # warm
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for i in range(reps):
-        nat.call("sd_imagine_step_kernel", ctypes.addressof(desc), which, i % H, K.stream())
-    e.record()
-    torch.cuda.synchronize()
-    avg_ms = s.elapsed_time(e) / reps
-    achieved = work / (avg_ms * 1e-3) / 1e12
-    return {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA, "unit": "TFLOP/s",
-            "frac": achieved / PEAK_FP32_MFMA, "key": ("k_lin", "k_hid", "k_gate")[which], "kernel": label,
-            "launches": reps, "avg_us": avg_ms * 1e3,
-            "work_per_launch": work, "shape": f"N={N} D={D} U={U}"}
+def roofline_entries(specs, agent, cfg, table):
+    """Time every probe spec live and join it with its kernel-table row. Returns the entries ordered by the table's
+    per-update rank (live per-update time when there is no table)."""
+    imag = scan = None
+    rows = table["rows"] if table else []
+    res = []
+    for sp in specs:
+        kind = sp["how"][0]
+        if kind == "launch":
+            pr = sp["how"][1]
+            pr.stop()
+            pr.replay(20)
+            rep = pr.report()
+            if rep is None:
+                continue
+            avg_us = rep["avg_us"]
+        elif kind == "imag":
+            imag = imag or _ImagStep(agent, cfg)
+            avg_us = imag.time(sp["how"][1])
+        else:
+            scan = scan or _ScanStep(agent, cfg)
+            if not scan.ok:
+                continue
+            avg_us = scan.time(sp["how"][1])
+        peak = PEAK_FP32_MFMA if sp["bound"] == "mfma" else PEAK_HBM
+        unit = "TFLOP/s" if sp["bound"] == "mfma" else "GB/s"
+        achieved = sp["work"] / (avg_us * 1e-6) / (1e12 if unit == "TFLOP/s" else 1e9)
+        e = {"key": sp["key"], "kernel": sp["label"], "symbol": sp["name"], "grid": sp["grid"], "bound": sp["bound"],
+             "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak, "avg_us": avg_us,
+             "work_per_launch": sp["work"], "algorithmic_bytes": sp["algo"], "traffic": None}
+        row = next(((i, rw) for i, rw in enumerate(rows)
+                    if rw["kernel"].startswith(sp["name"]) and rw["grid"] == sp["grid"]), None)
+        if row:
+            i, rw = row
+            e.update(rank=i + 1, launches_per_update=rw["launches_per_update"],
+                     trace_avg_us=rw["avg_us"], trace_ms_per_update=rw["ms_per_update"],
+                     traffic=rw.get("hbm_bytes"), trace_clock_ghz=rw.get("clock_ghz"), mfma_util=rw.get("mfma_util"),
+                     l2_hit=rw.get("l2_hit"), traffic_source=f"{KERNEL_TABLE} (rocprofv3 --pmc FETCH_SIZE x2 + "
+                                                             "WRITE_SIZE, per dispatch)")
+            if e["traffic"]:
+                e["traffic_over_algorithmic"] = e["traffic"] / sp["algo"]
+        else:
+            e["launches_per_update"] = sp["launches"]
+        e["ms_per_update"] = e["avg_us"] * e["launches_per_update"] / 1e3
+        res.append(e)
+    if rows:
+        res.sort(key=lambda e: e.get("rank", 10 ** 6))
+    else:
+        res.sort(key=lambda e: -e["ms_per_update"])
+    return res
 
 
 def dominant_probe(K):
-    """Secondary roofline probe: the encoder's second stage forward, conv + MaxPool2d(2) + RMSNorm2D + SiLU in one
-    launch (direct conv, M = B*L*32*32 pixels, N = 48, K = 5*5*32), the largest single MFMA launch of the update
-    (DESIGN.md §5). Algorithmic work = 2*M*N*K FLOP per launch."""
+    """Roofline probe of the encoder's second stage forward, conv + MaxPool2d(2) + RMSNorm2D + SiLU in one launch
+    (direct conv, M = B*L*32*32 pixels, N = 48, K = 5*5*32), the update's largest single MFMA launch.
+    Algorithmic work = 2*M*N*K FLOP per launch."""
     if not K.ops_fused_pool():
         def flops(a):  # sd_conv2d_fwd(in, w, b, out, Nb, Hs, Ws, Ci, Co, kh, kw, pad, ups, stream)
             Nb, Hs, Ws, Ci, Co, kh, kw, ups = a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[12]
@@ -281,7 +447,7 @@ def dominant_probe(K):
                                "N tile = 48)")
 
 
-def phase_rooflines(agent, cfg, cfg_name, ms_update, reps=10):
+def phase_rooflines(agent, cfg, cfg_name, ms_update, table=None, reps=10):
     """SURVEY §8(d) 'report separately': (i) the imagination rollout alone (secondary metric N*H / t_rollout; FLOP =
     2 * weights per img_step (Deter + img_net) per imagined latent + 2 * actor weights per actor sample, H img_steps
     and H+1 actor samples per start row), (ii) the observe scan forward (RSSM.observe: bytes = the Deter + obs_net
@@ -339,6 +505,25 @@ def phase_rooflines(agent, cfg, cfg_name, ms_update, reps=10):
                          "what": f"RSSM.observe forward, B={B} L={L}: 5 dependent launches per step; weight bytes "
                                  "(Deter + obs_net once per step) over the phase time as weight_stream_GBps"},
     }
+    if table:  # counter bytes of the scan forward's kernels (k_slab / k_hid / k_gate / k_logit of the fused scan) from the
+        # committed PMC passes, per update, over the live phase time: the 'achieved HBM GB/s on the recurrent scan'
+        scan_rows = [rw for rw in table["rows"] if rw["kernel"].split("<")[0] in ("k_slab", "k_logit", "k_init") or
+                     rw["kernel"] in ("k_hid<8, 2>", "k_gate<2, 2>")]
+        cb = sum(rw.get("hbm_bytes", 0.0) * rw["launches_per_update"] for rw in scan_rows)
+        tm = sum(rw["ms_per_update"] for rw in scan_rows)
+        hit = [(rw.get("l2_hit"), rw["ms_per_update"]) for rw in scan_rows if rw.get("l2_hit") is not None]
+        out["observe_scan"].update(
+            counter_bytes_per_update=cb, counter_GBps=cb / (ms_obs * 1e-3) / 1e9,
+            counter_frac_of_hbm=cb / (ms_obs * 1e-3) / 1e9 / PEAK_HBM,
+            trace_kernel_ms_per_update=tm,
+            l2_hit_time_weighted=(sum(h * t for h, t in hit) / sum(t for _, t in hit)) if hit else None,
+            counter_source=f"{KERNEL_TABLE}: scan forward kernels' HBM bytes per dispatch x dispatches per update")
+        heads = [rw for rw in table["rows"] if rw["kernel"].startswith("gemm3_kernel")]
+        if heads:  # MFMA utilisation of the split-bf16 GEMMs (heads + gradient contractions), time-weighted
+            t = sum(rw["ms_per_update"] for rw in heads)
+            out["gemm3_mfma_util"] = {"time_weighted": sum(rw.get("mfma_util", 0.0) * rw["ms_per_update"]
+                                                           for rw in heads) / t, "ms_per_update": t,
+                                      "source": KERNEL_TABLE}
     if f_upd:  # only where the update's FLOP were counted on the reference
         out["update"] = {"bound": "mfma", "achieved": f_upd / (ms_update * 1e-3) / 1e12, "peak": 157.3,
                          "unit": "TFLOP/s", "frac": f_upd / (ms_update * 1e-3) / 1e12 / 157.3, "work": f_upd,
@@ -393,9 +578,10 @@ def main():
     agent = Dreamer(cfg.model, _Spaces({"image": _Sp((64, 64, 3))}), act_space, rank=rank, world=world)
     buf = synth_buffer(cfg, device, rank, T=max(160, 2 * (L + 1)), A=A, discrete=discrete)
 
-    # roofline probe on the dominant kernel: sees its launch (eager warm-up or graph capture), then re-times that
-    # exact launch with HIP events on its stream after the timed steps
-    probe = None if args.no_roofline else dominant_probe(K)
+    # roofline probes on the update's largest launch shapes: LaunchProbes see their launch during the warm-up (eager
+    # update or graph capture) and re-time that exact launch with HIP events on its stream after the timed steps;
+    # the imagination / scan kernels are re-issued through their step entry points
+    specs = None if args.no_roofline else probe_specs(agent, cfg, K)
     for _ in range(args.warmup):
         agent.update(buf)
     trace_mark(1)  # kernel-trace window of the timed steps (tools/kernel_table.py); outside the timed region
@@ -411,9 +597,6 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     trace_mark(2)
-    if probe is not None:
-        probe.stop()
-        probe.replay(20)
     if world > 1:
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -435,28 +618,27 @@ def main():
                    "global_batch": B * world, "per_gpu_batch": B, "seq_len": L, "imag_horizon": H,
                    "parallelism": f"dp{world}"},
     }
-    if probe is not None:
-        # the dominant kernel (k_lin, imagination) and, as secondary entries, the other two imagination contractions
-        # and the largest single MFMA launch (encoder stage 2); HBM bytes per launch from separate rocprofv3 --pmc
-        # FETCH_SIZE / WRITE_SIZE passes (tools/roofline_traffic.py: gfx950 FETCH_SIZE x2), committed under profiles/
-        import glob
-        out["roofline"] = imag_kernel_probe(agent, cfg, 0)
-        out["roofline_secondary"] = {"k_hid": imag_kernel_probe(agent, cfg, 1),
-                                     "k_gate": imag_kernel_probe(agent, cfg, 2), "conv_stage2": probe.report()}
-        tfs = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                            "r*_roofline_traffic.json")))
-        tf = tfs[-1] if tfs else ""
-        if tf:
-            tj = json.load(open(tf))
-            for ent in [out["roofline"]] + list(out["roofline_secondary"].values()):
-                t = tj.get(ent.get("key", "conv_fwd_direct_pool")) if ent else None
-                if t and t.get("traffic_bytes"):
-                    ent["traffic"] = t["traffic_bytes"]
-                    ent["traffic_source"] = f"profiles/{os.path.basename(tf)} (rocprofv3 --pmc)"
-                    ent["algorithmic_bytes"] = t.get("algorithmic_bytes")
-            out["roofline"].setdefault("traffic", None)
+    table = None
+    if specs is not None:
+        tpath = os.path.join(ROOT, KERNEL_TABLE)
+        if args.config == "dmc/cnn" and not args.global_batch and os.path.exists(tpath):
+            table = json.load(open(tpath))  # profiled at this workload (tools/profile_round.sh runs bench.py defaults)
+        clk0 = clock_probe()
+        ents = roofline_entries(specs, agent, cfg, table)
+        clk1 = clock_probe()
+        # `roofline`: the update's dominant launch shape (rank 1 of the kernel table by time per update among the
+        # shapes bench can re-time); `roofline_top`: the first three; every other probe in `roofline_more`
+        out["roofline"] = ents[0] if ents else None
+        out["roofline_top"] = ents[:3]
+        out["roofline_more"] = ents[3:]
+        out["kernel_table"] = {"file": KERNEL_TABLE if table else None,
+                               "note": "ranks / trace_avg_us / traffic / mfma_util / clock from the committed rocprofv3 "
+                                       "trace + PMC of this build at this workload; avg_us, achieved and frac are live"}
+        # shader clock under an f32-MFMA load before / after the probes (sd_clock_probe, in-kernel s_memtime over
+        # s_memrealtime): DVFS state of this box while the probes ran
+        out["clock_ghz_mfma_load"] = [clk0, clk1]
     if not args.no_roofline:
-        out["phases"] = phase_rooflines(agent, cfg, args.config, ms)
+        out["phases"] = phase_rooflines(agent, cfg, args.config, ms, table)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if args.config == "dmc/cnn":  # checker legs beside the CPU baseline
             out["parity"] = wm_loss_parity_full()

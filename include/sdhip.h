@@ -113,6 +113,18 @@ int sd_repval_loss_fwd(const float* logits, const float* bins, const float* ret,
                        float* row_loss, long rows, int NB, sd_stream s);
 int sd_repval_loss_bwd(const float* logits, const float* bins, const float* ret, const float* slow, const float* w,
                        const float* gscale, float inv_n, float* dlogits, long rows, int NB, sd_stream s);
+/* Imagined actor-critic losses (dreamer.py:623-636, 653-671) over H * N time-major rows r = t * N + n: value logits
+ * vl (H * N, NB), logpi / ent (H * N) of the imagined actions, slow (H * N) slow-value targets; batch-major
+ * ret (N, H), w = weight (N, H1), val = imagined value (N, H1); scale: device scalar (ReturnEMA scale).
+ * fwd writes adv (N, H) = (ret - val[:, :H]) / scale and the row terms rows_v = w (-logp(ret) - logp(slow)),
+ * rows_p = w -(logpi adv + coef ent) (H * N each; the losses are their means). bwd: d vl, d logpi, d ent from the
+ * upstream gradients of the two means (device scalars gpolicy / gvalue, null = 0). */
+int sd_imag_ac_loss_fwd(const float* vl, const float* bins, const float* ret, const float* slow, const float* w,
+                        const float* val, const float* scale, const float* logpi, const float* ent, float coef, long N,
+                        int H, int H1, int NB, float* rows_v, float* rows_p, float* adv, sd_stream s);
+int sd_imag_ac_loss_bwd(const float* vl, const float* bins, const float* ret, const float* slow, const float* w,
+                        const float* adv, const float* gpolicy, const float* gvalue, float coef, long N, int H, int H1,
+                        int NB, float* dvl, float* dlogpi, float* dent, sd_stream s);
 /* bounded normal actor (bounded_normal, distributions.py:217-222): x (rows, 2A) = [mean | std-logit] */
 int sd_bnormal_sample(const float* x, float* action, long rows, int A, float min_std, float max_std, uint64_t seed,
                       int stream_id, int step, long row_offset, const uint64_t* seed_ptr, sd_stream stream);
@@ -208,12 +220,15 @@ int sd_pool_rms_bwd_compact(const float* pooled, const uint8_t* amax, const floa
 /* ---------------------------------------------------------------- optimiser (flat parameter arena)
  * clip_grad_agc_ (agc.py:15-53) + LaProp.step (laprop.py:46-118) + LambdaLR warm-up (dreamer.py:214-225), fused.
  * chunk tables are device arrays built once by the caller; scalars = sd_opt_scalars_bytes() zeroed bytes of device
- * memory (float64 step / lr EMAs); workspace >= 3*nchunks floats; grad_norms (ntensors) optional. */
+ * memory (float64 step / lr EMAs); workspace >= 3*nchunks floats; grad_norms (ntensors) optional. Every gradient is
+ * read as grad_scale * g (data parallel: 1 / world after the sum all-reduce), tensor gate_tensor's (>= 0) also times
+ * the device scalar *gate (DreamerPro's prototype freeze, dreamer.py:424-425); -1 = no gated tensor. */
 int sd_opt_scalars_bytes(void);
 int sd_agc_laprop_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, const long* chunk_beg,
                        const long* chunk_end, const int* chunk_tensor, const int* tensor_chunk0, int nchunks,
                        int ntensors, float* workspace, void* scalars, float* grad_norms, float clip, float pmin,
-                       double lr0, double warmup, double beta1, double beta2, double eps, sd_stream stream);
+                       double lr0, double warmup, double beta1, double beta2, double eps, float grad_scale,
+                       int gate_tensor, const float* gate, sd_stream stream);
 /* slow critic: dst = mix*src + (1-mix)*dst (Dreamer._update_slow_target, dreamer.py:242-249) */
 int sd_polyak(const float* src, float* dst, long n, float mix, sd_stream stream);
 

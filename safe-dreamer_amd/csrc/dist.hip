@@ -347,6 +347,79 @@ __global__ void repval_bwd_kernel(const float* __restrict__ logits, const float*
   }
 }
 
+// imagined actor-critic losses (dreamer.py:623-636, 653-671) on H * N time-major rows r = t * N + n, the returns /
+// weights / values batch-major (n, t): adv = (ret[n, t] - val[n, t]) / scale[0] (written for the metrics),
+// value row  = w[n, t] * (-logp(vl[r], ret[n, t]) - logp(vl[r], slow[r]))   (TwoHot, distributions.py:100-129),
+// policy row = w[n, t] * -(logpi[r] * adv + coef * ent[r]).  One wave per row.
+__global__ void imag_ac_fwd_kernel(const float* __restrict__ vl, const float* __restrict__ bins,
+                                   const float* __restrict__ ret, const float* __restrict__ slow,
+                                   const float* __restrict__ w, const float* __restrict__ val,
+                                   const float* __restrict__ scale, const float* __restrict__ logpi,
+                                   const float* __restrict__ ent, float coef, long N, int H, int H1, int NB,
+                                   float* __restrict__ rows_v, float* __restrict__ rows_p, float* __restrict__ adv) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long r = (long)blockIdx.x * 4 + wave;
+  if (r >= N * H) return;
+  const long n = r % N;
+  const int t = (int)(r / N);
+  const float* l = vl + r * NB;
+  const float rt = ret[n * H + t];
+  float p[4], lse;
+  row_softmax64(l, NB, p, lse, lane);
+  int b1, a1, b2, a2;
+  float wb1, wa1, wb2, wa2;
+  twohot_target(bins, NB, rt, b1, a1, wb1, wa1, lane);
+  twohot_target(bins, NB, slow[r], b2, a2, wb2, wa2, lane);
+  if (lane == 0) {
+    float lr = wb1 * (l[b1] - lse);
+    lr += wa1 * (l[a1] - lse);
+    float ls = wb2 * (l[b2] - lse);
+    ls += wa2 * (l[a2] - lse);
+    const float wt = w[n * H1 + t];
+    const float a = (rt - val[n * H1 + t]) / scale[0];
+    rows_v[r] = wt * (-lr - ls);
+    rows_p[r] = wt * -(logpi[r] * a + coef * ent[r]);
+    adv[n * H + t] = a;
+  }
+}
+// d vl (value loss, both log-prob terms), d logpi and d ent (policy loss); g = (policy, value) upstream gradients
+__global__ void imag_ac_bwd_kernel(const float* __restrict__ vl, const float* __restrict__ bins,
+                                   const float* __restrict__ ret, const float* __restrict__ slow,
+                                   const float* __restrict__ w, const float* __restrict__ adv,
+                                   const float* __restrict__ gp, const float* __restrict__ gv, float coef, float inv_n,
+                                   long N, int H, int H1, int NB, float* __restrict__ dvl, float* __restrict__ dlogpi,
+                                   float* __restrict__ dent) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long r = (long)blockIdx.x * 4 + wave;
+  if (r >= N * H) return;
+  const long n = r % N;
+  const int t = (int)(r / N);
+  const float* l = vl + r * NB;
+  float p[4], lse;
+  row_softmax64(l, NB, p, lse, lane);
+  int b1, a1, b2, a2;
+  float wb1, wa1, wb2, wa2;
+  twohot_target(bins, NB, ret[n * H + t], b1, a1, wb1, wa1, lane);
+  twohot_target(bins, NB, slow[r], b2, a2, wb2, wa2, lane);
+  const float wt = w[n * H1 + t];
+  const float g = -wt * ((gv ? gv[0] : 0.f) * inv_n);
+  const float t1 = wb1 + wa1, t2 = wb2 + wa2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = lane + 64 * j;
+    if (c < NB) {
+      const float td1 = (c == b1 ? wb1 : 0.f) + (c == a1 ? wa1 : 0.f);
+      const float td2 = (c == b2 ? wb2 : 0.f) + (c == a2 ? wa2 : 0.f);
+      dvl[r * NB + c] = g * (td1 - p[j] * t1) + g * (td2 - p[j] * t2);
+    }
+  }
+  if (lane == 0) {
+    const float gg = -wt * ((gp ? gp[0] : 0.f) * inv_n);
+    dlogpi[r] = gg * adv[n * H + t];
+    dent[r] = gg * coef;
+  }
+}
+
 // ---------------------------------------------------------------- bounded normal actor
 __global__ void bnormal_sample(const float* __restrict__ x, float* __restrict__ action, long rows, int A, float min_std,
                                float max_std, uint64_t seed, uint32_t stream, uint32_t step, long row_offset,
@@ -591,6 +664,31 @@ extern "C" int sd_repval_loss_bwd(const float* logits, const float* bins, const 
   if (NB > 256 || !gscale) return SD_ESHAPE;
   repval_bwd_kernel<<<blocks_for(rows, 4), 256, 0, (hipStream_t)s>>>(logits, bins, ret, slow, w, gscale, inv_n,
                                                                       dlogits, rows, NB);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_imag_ac_loss_fwd(const float* vl, const float* bins, const float* ret, const float* slow,
+                                   const float* w, const float* val, const float* scale, const float* logpi,
+                                   const float* ent, float coef, long N, int H, int H1, int NB, float* rows_v,
+                                   float* rows_p, float* adv, sd_stream s) {
+  if (N <= 0 || H <= 0) return SD_OK;
+  if (NB > 256 || H1 <= H) return SD_ESHAPE;
+  imag_ac_fwd_kernel<<<blocks_for(N * H, 4), 256, 0, (hipStream_t)s>>>(vl, bins, ret, slow, w, val, scale, logpi, ent,
+                                                                       coef, N, H, H1, NB, rows_v, rows_p, adv);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_imag_ac_loss_bwd(const float* vl, const float* bins, const float* ret, const float* slow,
+                                   const float* w, const float* adv, const float* gpolicy, const float* gvalue,
+                                   float coef, long N, int H, int H1, int NB, float* dvl, float* dlogpi, float* dent,
+                                   sd_stream s) {
+  if (N <= 0 || H <= 0) return SD_OK;
+  if (NB > 256 || H1 <= H) return SD_ESHAPE;
+  imag_ac_bwd_kernel<<<blocks_for(N * H, 4), 256, 0, (hipStream_t)s>>>(vl, bins, ret, slow, w, adv, gpolicy, gvalue,
+                                                                       coef, 1.f / (float)(N * H), N, H, H1, NB, dvl,
+                                                                       dlogpi, dent);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

@@ -24,7 +24,8 @@ struct OptScalars {  // device-resident, float64 like the reference's Python flo
 // after this launch, and nothing else in this launch does.
 __global__ void norms_kernel(const float* __restrict__ p, const float* __restrict__ g, const long* __restrict__ chunk_beg,
                              const long* __restrict__ chunk_end, float* __restrict__ pn2, float* __restrict__ gn2,
-                             OptScalars* st, double lr0, double warmup, double beta1, double beta2) {
+                             OptScalars* st, double lr0, double warmup, double beta1, double beta2, float gscale,
+                             const int* __restrict__ chunk_tensor, int gate_tensor, const float* __restrict__ gate) {
   __shared__ float red[4];
   const int c = blockIdx.x;
   if (c == 0 && threadIdx.x == 0) {
@@ -35,9 +36,10 @@ __global__ void norms_kernel(const float* __restrict__ p, const float* __restric
     st->step += 1.0;
   }
   const long b = chunk_beg[c], e4 = (chunk_end[c] + 3) & ~3L;
+  const float gs = chunk_tensor[c] == gate_tensor ? gscale * gate[0] : gscale;
   float sp = 0.f, sg = 0.f;
   for (long i = b + 4 * threadIdx.x; i < e4; i += 1024) {
-    const f32x4 pv = *reinterpret_cast<const f32x4*>(p + i), gv = *reinterpret_cast<const f32x4*>(g + i);
+    const f32x4 pv = *reinterpret_cast<const f32x4*>(p + i), gv = gs * *reinterpret_cast<const f32x4*>(g + i);
     sp += pv[0] * pv[0] + pv[1] * pv[1] + pv[2] * pv[2] + pv[3] * pv[3];
     sg += gv[0] * gv[0] + gv[1] * gv[1] + gv[2] * gv[2] + gv[3] * gv[3];
   }
@@ -54,7 +56,8 @@ __global__ void laprop_kernel(float* __restrict__ p, const float* __restrict__ g
                               const int* __restrict__ chunk_tensor, const int* __restrict__ tensor_chunk0,
                               const float* __restrict__ pn2, const float* __restrict__ gn2, float* __restrict__ gnorm_out,
                               const OptScalars* __restrict__ st, float clip, float pmin, float beta1, float beta2,
-                              float one_m_beta2, float eps) {
+                              float one_m_beta2, float eps, float gscale, int gate_tensor,
+                              const float* __restrict__ gate) {
   __shared__ float red[4];
   const int c = blockIdx.x, t = chunk_tensor[c], c0 = tensor_chunk0[t], c1 = tensor_chunk0[t + 1];
   float sp = 0.f, sg = 0.f;
@@ -63,6 +66,7 @@ __global__ void laprop_kernel(float* __restrict__ p, const float* __restrict__ g
   sg = block_sum<256>(sg, red);
   const float pn = sqrtf(sp), gn = sqrtf(sg);
   const float sc = 1.f / fmaxf(gn / (fmaxf(pn, pmin) * clip), 1.f);  // agc.py:40-56
+  const float gs = t == gate_tensor ? gscale * gate[0] : gscale;
   if (gnorm_out && c == c0 && threadIdx.x == 0) gnorm_out[t] = gn;
   const double lr = st->lr;
   const float bc2 = (float)st->lr_ema2;
@@ -76,7 +80,7 @@ __global__ void laprop_kernel(float* __restrict__ p, const float* __restrict__ g
           pq = *reinterpret_cast<const f32x4*>(p + i);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float gv = gq[j] * sc;                  // AGC (agc.py:52-56)
+      const float gv = (gs * gq[j]) * sc;           // (data-parallel mean, gate) then AGC (agc.py:52-56)
       float vv = vq[j] * beta2;                     // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
       vv = vv + one_m_beta2 * gv * gv;
       vq[j] = vv;
@@ -105,18 +109,20 @@ extern "C" int sd_agc_laprop_step(float* params, float* grads, float* exp_avg, f
                                   const long* chunk_end, const int* chunk_tensor, const int* tensor_chunk0, int nchunks,
                                   int ntensors, float* workspace, void* scalars, float* grad_norms, float clip,
                                   float pmin, double lr0, double warmup, double beta1, double beta2, double eps,
-                                  sd_stream stream_) {
+                                  float grad_scale, int gate_tensor, const float* gate, sd_stream stream_) {
   hipStream_t s = (hipStream_t)stream_;
   if (nchunks <= 0) return SD_OK;
+  if (gate_tensor >= ntensors || (gate_tensor >= 0 && !gate)) return SD_EARG;
   float* pn2 = workspace;
   float* gn2 = workspace + nchunks;
   OptScalars* st = (OptScalars*)scalars;
   // two launches: per-chunk norms (+ the scalar state), then per-tensor AGC scale + LaProp per chunk
-  norms_kernel<<<nchunks, 256, 0, s>>>(params, grads, chunk_beg, chunk_end, pn2, gn2, st, lr0, warmup, beta1, beta2);
+  norms_kernel<<<nchunks, 256, 0, s>>>(params, grads, chunk_beg, chunk_end, pn2, gn2, st, lr0, warmup, beta1, beta2,
+                                       grad_scale, chunk_tensor, gate_tensor, gate);
   SD_LAUNCH_CHECK();
   laprop_kernel<<<nchunks, 256, 0, s>>>(params, grads, exp_avg, exp_avg_sq, chunk_beg, chunk_end, chunk_tensor,
                                          tensor_chunk0, pn2, gn2, grad_norms, st, clip, pmin, (float)beta1, (float)beta2,
-                                         (float)(1.0 - beta2), (float)eps);
+                                         (float)(1.0 - beta2), (float)eps, grad_scale, gate_tensor, gate);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

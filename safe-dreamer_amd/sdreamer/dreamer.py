@@ -188,7 +188,9 @@ class Dreamer(nn.Module):
         if self.rep_loss == "dreamerpro":  # EMA encoder / projection: arena-slice mirrors (one Polyak launch each)
             self._ema_mirrors = [self._mirror("encoder.", self._ema_encoder),
                                  self._mirror("obs_proj.", self._ema_obs_proj)]
-            self._proto_gate = torch.ones(1, device=self.device)  # graphs: 0 while the prototypes are frozen
+            self._proto_gate = torch.ones(1, device=self.device)  # 0 while the prototypes are frozen
+            # the fused optimizer step reads the prototype gradient times this gate (dreamer.py:424-425)
+            self._optimizer.gate = (pos[id(self._prototypes)], self._proto_gate)
         self.rbins = _symexp_bins(int(config.reward.dist.bin_num), self.device)
         self.vbins = _symexp_bins(int(config.critic.dist.bin_num), self.device)
         self._updates = 0
@@ -399,10 +401,11 @@ class Dreamer(nn.Module):
             self.ema_update()
         self._optimizer.zero_grad()
         post, mets = self._cal_grad(p_data, initial, seed, ro)
-        if self._protos_frozen():
-            ops.grad_buf(self._prototypes).zero_()
+        if self.rep_loss == "dreamerpro":
+            self._proto_gate.fill_(0.0 if self._protos_frozen() else 1.0)
         if self.world > 1:
             parallel.allreduce_mean_(self._optimizer.arena.grad)
+        self._optimizer.grad_scale = 1.0  # the eager all-reduce above already took the mean
         self._optimizer.step()
         self._mark("optimizer")
         self._scheduler.step()
@@ -480,10 +483,9 @@ class Dreamer(nn.Module):
 
     def _core_step(self, st):
         """Graph phase M3 (main): the optimizer step."""
-        if self.world > 1:  # the arena was sum-all-reduced between the phase graphs (_update_graphed)
-            self._optimizer.arena.grad.mul_(1.0 / self.world)
-        if self.rep_loss == "dreamerpro":
-            ops.grad_buf(self._prototypes).mul_(self._proto_gate)
+        # the arena was sum-all-reduced between the phase graphs (_update_graphed): the fused step reads the gradients
+        # times 1 / world; DreamerPro's prototype gradient is also gated there (LaProp.gate)
+        self._optimizer.grad_scale = 1.0 / self.world
         self._optimizer.launch_step()
         self._mark("optimizer")
 
@@ -1011,14 +1013,14 @@ class Dreamer(nn.Module):
         """ReturnEMA over every rank's returns (global quantiles, dreamer.py:623-627) and the advantage (628-636)."""
         ret_all = parallel.gather_returns(rr["ret"], self.world)
         ret_offset, ret_scale = self.return_ema(ret_all)
-        rr.update(adv=(rr["ret"] - rr["val_n"][:, :-1]) / ret_scale, ret_offset=ret_offset, ret_scale=ret_scale)
+        rr.update(ret_offset=ret_offset, ret_scale=ret_scale)  # the advantage is formed inside the AC loss launch
 
     def _ac_losses(self, ifeat, iact, rr):
         """Policy and value losses on the imagined trajectories (dreamer.py:653-671) and their backward."""
         losses, metrics = {}, {}
         H1, N = ifeat.shape[:2]
         H = H1 - 1
-        ret, weight, adv, i_slow = rr["ret"], rr["weight"], rr["adv"], rr["i_slow"]
+        ret, weight, i_slow = rr["ret"], rr["weight"], rr["i_slow"]
         xh = ifeat[:H].reshape(H * N, -1)
         a_h0 = rr.get("act_h0")
         if a_h0 is not None:  # layer 0 from the imagination (fp32), layers 1.. and the output on split-bf16
@@ -1032,17 +1034,15 @@ class Dreamer(nn.Module):
             d = self.config.actor.dist
             logpi, ent = ops.BNormalLogProbEntFn.apply(pl, iact[:H].reshape(H * N, -1), float(d.min_std),
                                                         float(d.max_std))
-        logpi, ent = logpi.view(H, N).t(), ent.view(H, N).t()
-        w = weight[:, :H]
-        losses["policy"] = torch.mean(w * -(logpi * adv + self.act_entropy * ent))
         v_h0 = rr.get("val_h0")
         if v_h0 is not None:  # layer 0 from the imagined heads' batched launch (its first H * N rows)
             vl = self.value.forward_from_first(xh, v_h0[:H * N], fast=True)
         else:
             vl = self.value(xh, fast=True)
-        lp_tar = ops.TwoHotLogProbFn.apply(vl, self.vbins, ret.t().contiguous().reshape(-1))
-        lp_slow = ops.TwoHotLogProbFn.apply(vl, self.vbins, i_slow[:H].reshape(-1))
-        losses["value"] = torch.mean(w * (-lp_tar - lp_slow).view(H, N).t())
+        # policy (dreamer.py:653-660) and value (661-671) losses and the advantage (628-636): one launch each way
+        losses["policy"], losses["value"], adv = ops.ImagACLossFn.apply(
+            vl, logpi, ent, self.vbins, ret, i_slow[:H], weight, rr["val_n"], rr["ret_scale"], self.act_entropy)
+        rr["adv"] = adv
         (losses["policy"] * self._loss_scales["policy"] + losses["value"] * self._loss_scales["value"]).backward()
         with torch.no_grad():
             ret_normed = (ret - rr["ret_offset"]) / rr["ret_scale"]

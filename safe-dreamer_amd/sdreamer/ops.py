@@ -352,6 +352,47 @@ class RepvalLossFn(torch.autograd.Function):
         return dl.view(ctx.shape), None, None, None, None
 
 
+class ImagACLossFn(torch.autograd.Function):
+    """Imagined policy and value losses (dreamer.py:623-636, 653-671) in one launch each way (sd_imag_ac_loss_fwd /
+    _bwd): rows are the H * N time-major imagined steps; value logits vl (H*N, NB), logpi / ent (H*N) with gradients;
+    ret (N, H), weight (N, H1), val (N, H1), slow (H, N), scale (device scalar) detached. Returns (policy, value, adv):
+    the two losses (means of the kernel's row terms) and adv (N, H) = (ret - val[:, :H]) / scale (no gradient)."""
+
+    @staticmethod
+    def forward(ctx, vl, logpi, ent, bins, ret, slow, weight, val, scale, coef):
+        N, H = ret.shape
+        H1 = weight.shape[1]
+        NB = vl.shape[-1]
+        l2 = _flat(vl).contiguous()
+        lp, en = logpi.reshape(-1).contiguous(), ent.reshape(-1).contiguous()
+        r, sl, w, v = ret.contiguous(), slow.reshape(-1).contiguous(), weight.contiguous(), val.contiguous()
+        sc = scale.reshape(1).contiguous()
+        rows = torch.empty(2, N * H, dtype=torch.float32, device=vl.device)
+        adv = torch.empty(N, H, dtype=torch.float32, device=vl.device)
+        k.nat.call("sd_imag_ac_loss_fwd", k.p(l2), k.p(bins), k.p(r), k.p(sl), k.p(w), k.p(v), k.p(sc), k.p(lp),
+                   k.p(en), float(coef), N, H, H1, NB, k.p(rows[1]), k.p(rows[0]), k.p(adv), k.stream())
+        ctx.save_for_backward(l2, bins, r, sl, w, adv)
+        ctx.coef, ctx.shapes = float(coef), (vl.shape, logpi.shape, ent.shape)
+        ctx.mark_non_differentiable(adv)
+        m = rows.mean(1)
+        return m[0], m[1], adv
+
+    @staticmethod
+    def backward(ctx, gp, gv, _gadv):
+        l2, bins, r, sl, w, adv = ctx.saved_tensors
+        N, H = r.shape
+        H1 = w.shape[1]
+        dvl = torch.empty_like(l2)
+        dlp = torch.empty(N * H, dtype=torch.float32, device=l2.device)
+        den = torch.empty(N * H, dtype=torch.float32, device=l2.device)
+        gp = gp.reshape(1).to(torch.float32).contiguous() if gp is not None else None
+        gv = gv.reshape(1).to(torch.float32).contiguous() if gv is not None else None
+        k.nat.call("sd_imag_ac_loss_bwd", k.p(l2), k.p(bins), k.p(r), k.p(sl), k.p(w), k.p(adv), k.p(gp), k.p(gv),
+                   ctx.coef, N, H, H1, l2.shape[1], k.p(dvl), k.p(dlp), k.p(den), k.stream())
+        vs, ls, es = ctx.shapes
+        return dvl.view(vs), dlp.view(ls), den.view(es), None, None, None, None, None, None, None
+
+
 class BernoulliLogProbFn(torch.autograd.Function):
     """Independent(Bernoulli(logits), 1).log_prob with a single logit (binary head, distributions.py:238)."""
 

@@ -72,6 +72,10 @@ class LaProp(torch.optim.Optimizer):
         # per parameter: None, or (to_ref, from_ref) views between the internal and the reference layout, so that
         # state_dict() holds moments shaped like the reference's parameters (checkpoint interop)
         self.ref_layouts = list(ref_layouts) if ref_layouts is not None else [None] * len(params)
+        # read into every gradient by the fused step: 1 / world after the data-parallel sum all-reduce, and
+        # (tensor index, device scalar) gating one tensor (DreamerPro's prototype freeze); -1 = none
+        self.grad_scale = 1.0
+        self.gate = (-1, None)
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False, centered=False))
         self.arena = arena if arena is not None else FlatArena(params, params[0].device)
         dev = self.arena.data.device
@@ -100,7 +104,8 @@ class LaProp(torch.optim.Optimizer):
         nat.call("sd_agc_laprop_step", K.p(a.data), K.p(a.grad), K.p(self.exp_avg), K.p(self.exp_avg_sq),
                  K.p(a.chunk_beg), K.p(a.chunk_end), K.p(a.chunk_tensor), K.p(a.tensor_chunk0), a.nchunks,
                  a.ntensors, K.p(self.workspace), K.p(self.scalars), K.p(self.grad_norms), self.agc, self.pmin,
-                 self.base_lr, self.warmup, self.betas[0], self.betas[1], self.eps, K.stream())
+                 self.base_lr, self.warmup, self.betas[0], self.betas[1], self.eps, float(self.grad_scale),
+                 int(self.gate[0]), K.p(self.gate[1]), K.stream())
 
     def current_lr(self):
         """lr the NEXT step will use (LambdaLR semantics; host-side bookkeeping, no device sync)."""

@@ -345,6 +345,45 @@ def test_barlow():
     close(xd.grad, xr.grad, 1e-5, "grad")
 
 
+def test_imag_ac_loss_fused():
+    """ops.ImagACLossFn (sd_imag_ac_loss_fwd / _bwd) against the reference's torch formulation (dreamer.py:623-671 with
+    TwoHot.log_prob, distributions.py:100-129): policy / value losses, the advantage, and the gradients of logits,
+    log-probs and entropies."""
+    from sdreamer import ops
+    from sdreamer.dreamer import _symexp_bins
+    N, H, NB = 96, 5, 255
+    H1 = H + 1
+    g = _g(21)
+    vl = torch.randn(H * N, NB, generator=g) * 0.5
+    logpi = torch.randn(H * N, generator=g)
+    ent = torch.rand(H * N, generator=g) + 0.5
+    ret = torch.randn(N, H, generator=g) * 30
+    slow = torch.randn(H, N, generator=g) * 30
+    weight = torch.rand(N, H1, generator=g)
+    val = torch.randn(N, H1, generator=g) * 30
+    scale = torch.tensor(7.5)
+    coef = 3e-4
+    bins = _symexp_bins(NB, "cpu")
+    vr, lr_, er = (t.clone().requires_grad_() for t in (vl, logpi, ent))
+    adv = (ret - val[:, :H]) / scale
+    w = weight[:, :H]
+    pol = torch.mean(w * -(lr_.view(H, N).t() * adv + coef * er.view(H, N).t()))
+    lt = R.twohot_log_prob(vr, bins, ret.t().reshape(-1))
+    ls = R.twohot_log_prob(vr, bins, slow.reshape(-1))
+    vlos = torch.mean(w * (-lt - ls).view(H, N).t())
+    (2.0 * pol + 0.5 * vlos).backward()
+    vd, ld, ed = (t.to(DEV).requires_grad_() for t in (vl, logpi, ent))
+    p_, v_, a_ = ops.ImagACLossFn.apply(vd, ld, ed, bins.to(DEV), ret.to(DEV), slow.to(DEV), weight.to(DEV),
+                                        val.to(DEV), scale.to(DEV), coef)
+    close(p_, pol, 1e-5, "policy")
+    close(v_, vlos, 1e-5, "value")
+    close(a_, adv, 1e-6, "adv")
+    (2.0 * p_ + 0.5 * v_).backward()
+    close(vd.grad, vr.grad, 1e-6, "d value logits")
+    close(ld.grad, lr_.grad, 1e-6, "d logpi")
+    close(ed.grad, er.grad, 1e-6, "d ent")
+
+
 @pytest.mark.parametrize("Nr,E", [(512, 1024), (96, 64)])
 def test_barlow_dist_steps(Nr, E):
     """parallel.BarlowSteps (the data-parallel Barlow's HIP launches, csrc/misc.hip sd_barlow_*) at world 1 against the
@@ -430,6 +469,37 @@ def test_laprop_agc_step(warmup):
                 a, b = sd[i][nm].cpu().double(), st[nm].double()
                 assert ((a - b).abs() <= 1e-5 * b.abs() + 1e-5 * b.abs().max()).all(), (nm, i, it, float((a - b).abs().max()))
             assert abs(sd[i]["exp_avg_lr_1"] - st["exp_avg_lr_1"]) <= 1e-12 * abs(st["exp_avg_lr_1"])
+
+
+def test_laprop_grad_scale_and_gate():
+    """The fused step's data-parallel mean (grad_scale = 1 / world after a sum all-reduce) and tensor gate (DreamerPro's
+    prototype freeze) equal the ATen forms they replace, bit for bit: grads g * world with grad_scale 1 / world (world a
+    power of two) == g; gate 0 == a zeroed gradient, gate 1 == the gradient."""
+    from sdreamer.optim import LaProp
+    shapes = [(64, 96), (96,), (33, 7)]
+    g0 = [torch.randn(s, generator=_g(31 + i)) for i, s in enumerate(shapes)]
+    p0 = [torch.randn(s, generator=_g(41 + i)) for i, s in enumerate(shapes)]
+
+    def run(scale, gate_val, gmul, zero_gated):
+        params = [torch.nn.Parameter(p.clone().to(DEV)) for p in p0]
+        opt = LaProp(params, lr=4e-5, warmup=0)
+        opt.grad_scale = scale
+        gate = torch.full((1,), 1.0 if gate_val is None else gate_val, device=DEV)
+        if gate_val is not None:
+            opt.gate = (1, gate)
+        for it in range(2):
+            for i, g in enumerate(g0):
+                gg = g * gmul * (it + 1)
+                params[i].grad.copy_(torch.zeros_like(gg) if (zero_gated and i == 1) else gg.to(DEV))
+            opt.step()
+        return [p.detach().cpu() for p in params]
+
+    ref = run(1.0, None, 1.0, False)
+    for got in (run(0.125, None, 8.0, False), run(1.0, 1.0, 1.0, False)):
+        assert all(torch.equal(a, b) for a, b in zip(got, ref))
+    gated = run(1.0, 0.0, 1.0, False)
+    zeroed = run(1.0, None, 1.0, True)
+    assert all(torch.equal(a, b) for a, b in zip(gated, zeroed))
 
 
 def test_polyak():
