@@ -232,6 +232,28 @@ int sd_agc_laprop_step(float* params, float* grads, float* exp_avg, float* exp_a
 /* slow critic: dst = mix*src + (1-mix)*dst (Dreamer._update_slow_target, dreamer.py:242-249) */
 int sd_polyak(const float* src, float* dst, long n, float mix, sd_stream stream);
 
+/* ---------------------------------------------------------------- metrics
+ * The update's metric vector in one launch (tools.tensorstats, tools.py:275-281, and the scalar losses / means of
+ * dreamer.py:566-671): out[b] = sum over requests r with r.out == b (in order) of r.scale * stat(r.x[0:r.n]),
+ * stat = mean (SD_STAT_MEAN, a scalar is its own mean), unbiased std, min or max. */
+#define SD_STAT_MEAN 0
+#define SD_STAT_STD 1
+#define SD_STAT_MIN 2
+#define SD_STAT_MAX 3
+#define SD_MAX_STATS 96
+typedef struct sd_stat_req {
+  const float* x;
+  long n;
+  int kind, out;
+  float scale;
+  int pad_;
+} sd_stat_req;
+typedef struct sd_stats {
+  sd_stat_req r[SD_MAX_STATS];
+  int nreq;
+} sd_stats;
+int sd_multi_stats(const sd_stats* s, float* out, int nout, sd_stream stream);
+
 /* ---------------------------------------------------------------- misc
  * Measurement aid: one empty dispatch (kernel k_trace_mark, `tag` workgroups, 1 <= tag <= 64) that a rocprofv3 kernel
  * trace can find; bench.py brackets its timed steps with tags 1 and 2 (tools/kernel_table.py). */

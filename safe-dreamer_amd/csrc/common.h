@@ -55,6 +55,19 @@ SD_DEV float block_sum(float v, float* red) {
   return s;
 }
 
+template <int NT>
+SD_DEV float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float s = red[0];
+#pragma unroll
+  for (int i = 1; i < NT / 64; ++i) s = fmaxf(s, red[i]);
+  return s;
+}
+
 // Branch-free bounded loads: a buffer descriptor (range-checked by the hardware) plus a per-lane byte offset; an
 // invalid element gets an offset >= the range (SD_OOB) and reads 0. A "cond ? load : 0" on a runtime condition
 // instead makes hipcc branch around the load and drain vmcnt(0) there, serialising every prefetch behind it.

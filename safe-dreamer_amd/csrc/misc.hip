@@ -273,6 +273,41 @@ __global__ void barlow_dist_dx_kernel(const float* __restrict__ x1, const float*
   dx1[i] = ((dn1[i] - s0[j] / Nt) / sc - (x1[i] - m) * (A[j] / (sc * sc * (Nt - 1.f) * sg))) * world;
 }
 
+// Metric vector in one launch: output slot b = sum over the requests r with r.out == b, in request order, of
+// r.scale * stat_r(x_r[0:n_r]) (stat: mean, unbiased std, min, max). One workgroup per output slot.
+__global__ __launch_bounds__(256) void multi_stats_kernel(sd_stats s, float* __restrict__ out) {
+  __shared__ float red[8];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  float acc = 0.f;
+  for (int q = 0; q < s.nreq; ++q) {
+    const sd_stat_req r = s.r[q];
+    if (r.out != b) continue;
+    float v;
+    if (r.kind == SD_STAT_MIN || r.kind == SD_STAT_MAX) {
+      const bool mx = r.kind == SD_STAT_MAX;
+      float m = mx ? -INFINITY : INFINITY;
+      for (long i = tid; i < r.n; i += 256) m = mx ? fmaxf(m, r.x[i]) : fminf(m, r.x[i]);
+      v = mx ? block_max<256>(m, red) : -block_max<256>(-m, red);
+    } else {
+      float t = 0.f;
+      for (long i = tid; i < r.n; i += 256) t += r.x[i];
+      const float mean = block_sum<256>(t, red) / (float)r.n;
+      if (r.kind == SD_STAT_STD) {
+        float q2 = 0.f;
+        for (long i = tid; i < r.n; i += 256) {
+          const float d = r.x[i] - mean;
+          q2 += d * d;
+        }
+        v = sqrtf(block_sum<256>(q2, red) / (float)(r.n - 1));
+      } else {
+        v = mean;
+      }
+    }
+    acc += r.scale * v;
+  }
+  if (tid == 0) out[b] = acc;
+}
+
 // an empty dispatch whose name and grid (tag workgroups) a kernel trace can find: bench.py brackets its timed steps
 // with tags 1 and 2 so tools/kernel_table.py counts only the dispatches of those steps
 __global__ void k_trace_mark(int tag) {}
@@ -306,6 +341,15 @@ __global__ __launch_bounds__(256) void k_clock_probe(long long* stamps, float* s
 extern "C" int sd_clock_probe(long long* stamps, float* sink, int nwg, int iters, sd_stream s) {
   if (nwg < 1 || nwg > 4096 || iters < 1) return SD_EARG;
   k_clock_probe<<<nwg, 256, 0, (hipStream_t)s>>>(stamps, sink, iters);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_multi_stats(const sd_stats* s, float* out, int nout, sd_stream st) {
+  if (!s || s->nreq < 0 || s->nreq > SD_MAX_STATS || nout <= 0) return SD_EARG;
+  for (int q = 0; q < s->nreq; ++q)
+    if (s->r[q].out < 0 || s->r[q].out >= nout || s->r[q].n <= 0 || !s->r[q].x) return SD_EARG;
+  multi_stats_kernel<<<nout, 256, 0, (hipStream_t)st>>>(*s, out);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

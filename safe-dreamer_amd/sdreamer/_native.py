@@ -78,6 +78,13 @@ def _define(path, name):
 class SliceKeys(ctypes.Structure):
     _fields_ = [("k", SliceKey * _define(HEADER, "SD_MAX_SLICE_KEYS")), ("n", c_int)]
 
+
+StatReq = _parse_struct(HEADER, "sd_stat_req")
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("r", StatReq * _define(HEADER, "SD_MAX_STATS")), ("nreq", c_int)]
+
 _CTYPES = {
     "int": c_int, "long": c_long, "float": c_float, "double": ctypes.c_double, "uint64_t": ctypes.c_uint64,
     "sd_stream": c_ptr, "void": None,

@@ -68,8 +68,8 @@ def _symexp_bins(n, device):  # symexp_twohot bins, distributions.py:242-251
     return bins.to(device)
 
 
-def _tstats(t, prefix):  # tools.tensorstats (tools.py:275-281)
-    return {f"{prefix}_mean": t.mean(), f"{prefix}_std": t.std(), f"{prefix}_min": t.min(), f"{prefix}_max": t.max()}
+def _tstats(t, prefix):  # tools.tensorstats (tools.py:275-281), resolved with the other metrics in one launch
+    return K.tensorstats(t, prefix)
 
 
 class Dreamer(nn.Module):
@@ -401,6 +401,7 @@ class Dreamer(nn.Module):
             self.ema_update()
         self._optimizer.zero_grad()
         post, mets = self._cal_grad(p_data, initial, seed, ro)
+        mets = K.resolve_metrics(mets)
         if self.rep_loss == "dreamerpro":
             self._proto_gate.fill_(0.0 if self._protos_frozen() else 1.0)
         if self.world > 1:
@@ -477,8 +478,8 @@ class Dreamer(nn.Module):
         here, where the side stream has slack, instead of in front of the optimizer step (M3)."""
         self._ph_side_ac(st)
         post, mets = self._ph_finish(st)
-        keys = [k for k, v in mets.items() if isinstance(v, torch.Tensor)]
-        mvec = torch.stack([mets[k].float().reshape(()) for k in keys])
+        keys = [k for k, v in mets.items() if isinstance(v, (torch.Tensor, K.Stat))]
+        mvec = K.metric_vector([mets[k] for k in keys])  # every metric of the update in one launch
         return post, keys, mvec
 
     def _core_step(self, st):
@@ -827,10 +828,12 @@ class Dreamer(nn.Module):
         losses.update(st["ac_losses"])
         metrics.update(st["rv_metrics"])
         metrics.update(st["ac_metrics"])
-        total = st["wm_total"] + sum(v.detach() * self._loss_scales[k] for k, v in losses.items()
-                                     if k in ("repval", "policy", "value"))
+        total = K.Stat(st["wm_total"].detach())
+        for k, v in losses.items():
+            if k in ("repval", "policy", "value"):
+                total = total + K.Stat(v.detach(), scale=self._loss_scales[k])
         metrics.update({f"loss/{k}": v.detach() for k, v in losses.items()})
-        metrics["opt/loss"] = total.detach()
+        metrics["opt/loss"] = total
         rr = st["rr"]
         self._last = dict(embed=st["embed"], post_logit=st["post_logit"], prior_logit=self._prior_logit,
                           imag_feat_tm=st["ifeat"], imag_action_tm=st["iact"], ret=rr["ret"], rret=st["rret"])
@@ -876,8 +879,8 @@ class Dreamer(nn.Module):
         losses["rew"] = -ops.TwoHotLogProbFn.apply(rew_logits, self.rbins, data["reward"].float()).mean()
         cont = 1.0 - data["is_terminal"].float()
         losses["con"] = -ops.BernoulliLogProbFn.apply(self.cont(feat), cont).mean()
-        metrics["dyn_entropy"] = self.rssm.entropy(prior_logit).mean()
-        metrics["rep_entropy"] = self.rssm.entropy(post_logit).mean()
+        metrics["dyn_entropy"] = K.Stat(self.rssm.entropy(prior_logit))
+        metrics["rep_entropy"] = K.Stat(self.rssm.entropy(post_logit))
         wm_total = sum(v * self._loss_scales[k] for k, v in losses.items())
         wm_total.backward()
         return wm_total, losses, metrics
@@ -1047,17 +1050,17 @@ class Dreamer(nn.Module):
         with torch.no_grad():
             ret_normed = (ret - rr["ret_offset"]) / rr["ret_scale"]
             metrics["ret"] = ret_normed.mean()
-            metrics["ret_005"] = self.return_ema.ema_vals[0].clone()
-            metrics["ret_095"] = self.return_ema.ema_vals[1].clone()
-            metrics["adv"] = adv.mean()
-            metrics["adv_std"] = adv.std()
-            metrics["con"] = rr["i_cont"].mean()
-            metrics["rew"] = rr["i_rew"].mean()
-            metrics["val"] = rr["i_val"].mean()
-            metrics["tar"] = ret.mean()
-            metrics["slowval"] = i_slow.mean()
-            metrics["weight"] = weight.mean()
-            metrics["action_entropy"] = ent.detach().mean()
+            metrics["ret_005"] = K.Stat(self.return_ema.ema_vals[0:1])
+            metrics["ret_095"] = K.Stat(self.return_ema.ema_vals[1:2])
+            metrics["adv"] = K.Stat(adv)
+            metrics["adv_std"] = K.Stat(adv, K.STAT_STD)
+            metrics["con"] = K.Stat(rr["i_cont"])
+            metrics["rew"] = K.Stat(rr["i_rew"])
+            metrics["val"] = K.Stat(rr["i_val"])
+            metrics["tar"] = K.Stat(ret)
+            metrics["slowval"] = K.Stat(i_slow)
+            metrics["weight"] = K.Stat(weight)
+            metrics["action_entropy"] = K.Stat(ent.detach())
             metrics.update(_tstats(iact, "action"))
         return losses, metrics
 

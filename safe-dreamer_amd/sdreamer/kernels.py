@@ -597,3 +597,82 @@ class LaunchProbe:
         return {"bound": self.bound, "achieved": achieved, "peak": self.peak, "unit": self.unit,
                 "frac": achieved / self.peak, "traffic": None, "kernel": self.label, "launches": len(ms),
                 "avg_us": avg_ms * 1e3, "work_per_launch": per_launch}
+
+
+# ------------------------------------------------------------------------------------------------- metrics
+STAT_MEAN, STAT_STD, STAT_MIN, STAT_MAX = 0, 1, 2, 3
+
+
+class Stat:
+    """A metric resolved later, with every other metric of the update, by ONE sd_multi_stats launch: a sum of
+    scale * stat(tensor) terms (stat: mean, unbiased std, min, max of the whole tensor; a scalar is its own mean)."""
+
+    __slots__ = ("terms",)
+
+    def __init__(self, t, kind=STAT_MEAN, scale=1.0):
+        self.terms = [(t, int(kind), float(scale))]
+
+    def __add__(self, other):
+        r = Stat.__new__(Stat)
+        r.terms = self.terms + (other.terms if isinstance(other, Stat) else Stat(other).terms)
+        return r
+
+    __radd__ = __add__
+
+    def __mul__(self, k):
+        r = Stat.__new__(Stat)
+        r.terms = [(t, kind, sc * float(k)) for t, kind, sc in self.terms]
+        return r
+
+    __rmul__ = __mul__
+
+    def record_stream(self, s):
+        for t, _, _ in self.terms:
+            t.record_stream(s)
+
+
+def tensorstats(t, prefix):
+    """tools.tensorstats (tools.py:275-281) as lazy metrics"""
+    t = t.detach()
+    return {f"{prefix}_mean": Stat(t, STAT_MEAN), f"{prefix}_std": Stat(t, STAT_STD),
+            f"{prefix}_min": Stat(t, STAT_MIN), f"{prefix}_max": Stat(t, STAT_MAX)}
+
+
+def metric_vector(values):
+    """(len(values),) float32 device tensor: values are Stat or tensors (a tensor = its mean); one launch per
+    SD_MAX_STATS terms (normally one)."""
+    reqs = []
+    for i, v in enumerate(values):
+        for t, kind, sc in (v.terms if isinstance(v, Stat) else [(v, STAT_MEAN, 1.0)]):
+            t = t.detach()
+            if t.dtype != torch.float32:
+                t = t.float()
+            reqs.append((_c(t), kind, sc, i))
+    out = torch.empty(len(values), dtype=torch.float32, device=reqs[0][0].device if reqs else "cuda")
+    cap = len(nat.Stats().r)
+    first = True
+    for lo in range(0, len(reqs), cap):
+        st = nat.Stats()
+        chunk = reqs[lo:lo + cap]
+        for j, (t, kind, sc, i) in enumerate(chunk):
+            r = st.r[j]
+            r.x, r.n, r.kind, r.out, r.scale = p(t), t.numel(), kind, i, sc
+        st.nreq = len(chunk)
+        if first:
+            nat.call("sd_multi_stats", ctypes.addressof(st), p(out), len(values), stream())
+            first = False
+        else:  # a second chunk adds to the first's slots
+            extra = torch.empty_like(out)
+            nat.call("sd_multi_stats", ctypes.addressof(st), p(extra), len(values), stream())
+            out.add_(extra)
+    return out
+
+
+def resolve_metrics(mets):
+    """dict with Stat values -> dict of 0-dim device tensors (one launch for all of them)"""
+    keys = [k for k, v in mets.items() if isinstance(v, (Stat, torch.Tensor))]
+    vec = metric_vector([mets[k] for k in keys])
+    out = dict(mets)
+    for i, k in enumerate(keys):
+        out[k] = vec[i]
+    return out

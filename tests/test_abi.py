@@ -42,12 +42,19 @@ def test_gemm_desc_layout_matches_c():
     assert [int(x) for x in out] == [ctypes.sizeof(G), G.M.offset, G.ksplit.offset, G.beta.offset]
 
 
-def test_scan_desc_layout_matches_c():
+@pytest.mark.parametrize("cname,pyname,probe", [
+    ("sd_rssm_scan", "ScanDesc", ["B", "eps", "seed", "seed_ptr", "group_offset", "W0", "WlT", "reset", "stoch", "dl",
+                                  "work"]),
+    ("sd_imagine", "ImagineDesc", ["eps", "seed", "seed_ptr", "row_offset", "Wa", "Wao", "Wl", "feats", "work",
+                                   "t_end", "actor_h0"]),
+    ("sd_stat_req", "StatReq", ["x", "n", "kind", "out", "scale"]),
+    ("sd_stats", "Stats", ["r", "nreq"]),
+])
+def test_struct_layout_matches_c(cname, pyname, probe):
     from sdreamer import _native as nat
-    S = nat.ScanDesc
-    probe = ["B", "eps", "seed", "seed_ptr", "group_offset", "W0", "WlT", "reset", "stoch", "dl", "work"]
+    S = getattr(nat, pyname)
     fmt = " ".join(["%zu"] * (len(probe) + 1))
-    args = ", ".join(["sizeof(sd_rssm_scan)"] + [f"offsetof(sd_rssm_scan, {f})" for f in probe])
+    args = ", ".join([f"sizeof({cname})"] + [f"offsetof({cname}, {f})" for f in probe])
     src = f'#include <stdio.h>\n#include <stddef.h>\n#include "sdhip.h"\nint main(void){{printf("{fmt}", {args}); return 0;}}\n'
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "t.c")
