@@ -53,6 +53,23 @@ int sd_gemm_f32(const sd_gemm_desc* d, float* workspace, long workspace_floats, 
  * v_mfma_f32_16x16x32_bf16 with f32 accumulation, ~1e-5 relative to the typical |term| * sqrt(K), 5.3x the f32 MFMA
  * rate. For gradient contractions and frozen heads (no sampled index depends on them). M, N or K < 64 -> f32 path. */
 int sd_gemm_bf16x3(const sd_gemm_desc* d, float* workspace, long workspace_floats, sd_stream stream);
+/* One MLP layer (networks.py:313-336 Linear -> RMSNorm -> SiLU chains) on the split-bf16 core, batched like the GEMM:
+ * C[b] = act(rms(A[b]) * norm_w[b]) . B[b] + bias[b] with k-contiguous A (M, K) and B = W^T (W (N, K) row-major),
+ * K a multiple of 32, beta 0, no split-K. norm_w null: A used as is. Otherwise rstd(row m) = 1 / sqrt(sum_q
+ * part_in[b][q][m] / K + eps) from the producer's npart_in partial sums of squares per row, act 1 = SiLU (0: none).
+ * part_out (N % 64 == 0) receives this layer's partials, (N / 64, M) per batch entry: part_out[b][n / 64][m] =
+ * sum of C[b][m][n'] ^ 2 over the 64 columns n' of block n / 64. Returns SD_ESHAPE outside these shapes. */
+typedef struct sd_mlp_ext {
+  const float* norm_w;
+  long stride_norm_w;
+  const float* part_in;
+  long stride_part_in;
+  int npart_in, act;
+  float eps;
+  float* part_out;
+  long stride_part_out;
+} sd_mlp_ext;
+int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd_stream stream);
 
 /* ---------------------------------------------------------------- row norms
  * y = act(x * rsqrt(mean(x^2) + eps) * w) per row; act 0 = none, 1 = SiLU. rstd (M) saved for backward.
@@ -233,9 +250,11 @@ int sd_agc_laprop_step(float* params, float* grads, float* exp_avg, float* exp_a
 int sd_polyak(const float* src, float* dst, long n, float mix, sd_stream stream);
 
 /* ---------------------------------------------------------------- metrics
- * The update's metric vector in one launch (tools.tensorstats, tools.py:275-281, and the scalar losses / means of
+ * The update's metric vector in two launches (tools.tensorstats, tools.py:275-281, and the scalar losses / means of
  * dreamer.py:566-671): out[b] = sum over requests r with r.out == b (in order) of r.scale * stat(r.x[0:r.n]),
- * stat = mean (SD_STAT_MEAN, a scalar is its own mean), unbiased std, min or max. */
+ * stat = mean (SD_STAT_MEAN, a scalar is its own mean), unbiased std, min or max. Request q covers chunks
+ * [chunk0, chunk0 + ceil(n / SD_STAT_CHUNK)) (consecutive from 0); workspace >= 5 floats per chunk. */
+#define SD_STAT_CHUNK 4096
 #define SD_STAT_MEAN 0
 #define SD_STAT_STD 1
 #define SD_STAT_MIN 2
@@ -246,13 +265,13 @@ typedef struct sd_stat_req {
   long n;
   int kind, out;
   float scale;
-  int pad_;
+  int chunk0;
 } sd_stat_req;
 typedef struct sd_stats {
   sd_stat_req r[SD_MAX_STATS];
   int nreq;
 } sd_stats;
-int sd_multi_stats(const sd_stats* s, float* out, int nout, sd_stream stream);
+int sd_multi_stats(const sd_stats* s, float* workspace, float* out, int nout, sd_stream stream);
 
 /* ---------------------------------------------------------------- misc
  * Measurement aid: one empty dispatch (kernel k_trace_mark, `tag` workgroups, 1 <= tag <= 64) that a rocprofv3 kernel

@@ -81,7 +81,160 @@ void launch3_layout(const GemmArgs& g, int tile, bool va, bool vb, hipStream_t s
 
 bool al16_3(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// ---- MLP layer on the split-bf16 core (sd_gemm_bf16x3_mlp): C[b] = act(rms(A[b]) * nw[b]) . B[b] + bias[b], the
+// RMSNorm (nn.RMSNorm, eps) + SiLU of the previous layer applied to A rows while they are staged into LDS (rstd from
+// the producer's per-row partial sums of squares), and optionally this layer's own per-row partials written by the
+// epilogue (one per 64 output columns) for the next layer. No normalised tensor is ever materialised.
+struct MlpExt {
+  const float* nw;
+  long sNw;
+  const float* pin;
+  long sPin;
+  int npin, act;
+  float eps;
+  float* pout;
+  long sPout;
+};
+
+// A operand, k contiguous, rows normalised (x * rs[row] * nw[k], then SiLU if act) when stored into LDS
+template <int ROWS>
+struct KC3Rms {
+  static constexpr int NV = (ROWS * BK / 4 + 255) / 256;
+  f32x4 r[NV], w[NV];
+  const float* p;
+  const float* nw;
+  const float* rs;  // LDS, ROWS entries (this tile's rows)
+  long ld;
+  int nrows, row0, act;
+  SD_DEV KC3Rms(const float* base, long ld_, int nrows_, int row0_, const float* nw_, const float* rs_, int act_)
+      : p(base), nw(nw_), rs(rs_), ld(ld_), nrows(nrows_), row0(row0_), act(act_) {}
+  SD_DEV void load(int k0, int kend) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      const int row = i / (BK / 4), gk = k0 + 4 * (i % (BK / 4)), gr = row0 + row;
+      const bool ok = i < ROWS * BK / 4 && gr < nrows;
+      r[v] = ok ? *reinterpret_cast<const f32x4*>(p + (long)gr * ld + gk) : f32x4{0.f, 0.f, 0.f, 0.f};
+      w[v] = *reinterpret_cast<const f32x4*>(nw + gk);
+    }
+  }
+  SD_DEV void store(__bf16* lds) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = threadIdx.x + v * 256;
+      if ((v + 1) * 256 <= ROWS * BK / 4 || i < ROWS * BK / 4) {
+        const int row = i / (BK / 4);
+        const float s = rs[row];
+        f32x4 x;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float y = r[v][j] * s * w[v][j];
+          x[j] = act ? y * sigmoidf_(y) : y;
+        }
+        split_store(lds + row * LROW + 4 * (i % (BK / 4)), x);
+      }
+    }
+  }
+};
+
+template <bool RMS, bool POUT>
+__global__ __launch_bounds__(256, 2) void gemm3_mlp_kernel(GemmArgs g, MlpExt e) {
+  constexpr int BM = 128, BN = 128, WM = 64, WN = 64, TM = WM / 16, TN = WN / 16;
+  int tx, ty, tz;
+  g3_tile(g, tx, ty, tz);
+  const int bn0 = tx * BN, bm0 = ty * BM, b = tz;
+  __shared__ float rs[BM];
+  const float* A = g.A + (long)b * g.sA;
+  const float* Bp = g.B + (long)b * g.sB;
+  if (RMS) {  // this tile's rows: rstd from the producer's partial sums of squares
+    const float* pin = e.pin + (long)b * e.sPin;
+    for (int r = threadIdx.x; r < BM; r += 256) {
+      const int m = bm0 + r;
+      float s = 0.f;
+      if (m < g.M)
+        for (int q = 0; q < e.npin; ++q) s += pin[(long)q * g.M + m];
+      rs[r] = rsqrtf(s / (float)g.K + e.eps);
+    }
+    __syncthreads();
+  }
+  f32x4 acc[TM][TN];
+  KC3<BN, true> lb(Bp, g.ldb, g.N, bn0);
+  if constexpr (RMS) {
+    KC3Rms<BM> la(A, g.lda, g.M, bm0, e.nw + (long)b * e.sNw, rs, e.act);
+    gemm3_mainloop<BM, BN, WM, WN>(la, lb, 0, g.K, acc);
+  } else {
+    KC3<BM, true> la(A, g.lda, g.M, bm0);
+    gemm3_mainloop<BM, BN, WM, WN>(la, lb, 0, g.K, acc);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / (BN / WN), wc = wave % (BN / WN), l16 = lane & 15, q = lane >> 4;
+  float* C = g.C + (long)b * g.sC;
+  const float* bias = g.bias ? g.bias + (long)b * g.sBias : nullptr;
+  float ss[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ss[i][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = bn0 + wc * WN + 16 * j + l16;
+    const float bv = (bias && n < g.N) ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm0 + wr * WM + 16 * i + 4 * q + r;
+        const float v = g.alpha * acc[i][j][r] + bv;
+        if (m < g.M && n < g.N) C[(long)m * g.ldc + n] = v;
+        ss[i][r] += n < g.N ? v * v : 0.f;
+      }
+  }
+  if (POUT) {  // partial (64 columns of this wave) of every row's sum of squares
+    float* pout = e.pout + (long)b * e.sPout + (long)((bn0 + wc * WN) / 64) * g.M;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = ss[i][r];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        const int m = bm0 + wr * WM + 16 * i + 4 * q + r;
+        if (l16 == 0 && m < g.M) pout[m] = v;
+      }
+  }
+}
+
 }  // namespace
+
+extern "C" int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd_stream stream_) {
+  if (!d || !x || !d->A || !d->B || !d->C) return SD_EARG;
+  if (d->M <= 0 || d->N <= 0 || d->batch <= 0) return SD_OK;
+  // the fused path's shapes: k-contiguous A and B (C = A . W^T), 16-B aligned, whole 32-deep k tiles, no split-K
+  if (!d->a_kcontig || !d->b_kcontig || d->K % BK || d->K < BK || d->N < 64 || d->beta != 0.f) return SD_ESHAPE;
+  if (!al16_3(d->A) || !al16_3(d->B) || d->lda % 4 || d->ldb % 4 || (d->batch > 1 && (d->strideA % 4 || d->strideB % 4)))
+    return SD_ESHAPE;
+  const bool rms = x->norm_w != nullptr, pout = x->part_out != nullptr;
+  if (rms && (!x->part_in || x->npart_in <= 0 || !al16_3(x->norm_w) || x->stride_norm_w % 4)) return SD_EARG;
+  if (pout && d->N % 64) return SD_ESHAPE;
+  GemmArgs g;
+  g.A = d->A; g.B = d->B; g.C = d->C; g.bias = d->bias; g.ws = nullptr;
+  g.lda = d->lda; g.ldb = d->ldb; g.ldc = d->ldc;
+  g.sA = d->strideA; g.sB = d->strideB; g.sC = d->strideC; g.sBias = d->strideBias;
+  g.M = d->M; g.N = d->N; g.K = d->K; g.batch = d->batch;
+  g.alpha = d->alpha; g.beta = 0.f; g.ksplit = 1; g.kchunk = d->K;
+  MlpExt e{x->norm_w, x->stride_norm_w, x->part_in, x->stride_part_in, x->npart_in, x->act, x->eps, x->part_out,
+           x->stride_part_out};
+  dim3 grid(sd_cdiv(g.N, 128), sd_cdiv(g.M, 128), g.batch);
+  hipStream_t st = (hipStream_t)stream_;
+  if (rms && pout) gemm3_mlp_kernel<true, true><<<grid, 256, 0, st>>>(g, e);
+  else if (rms) gemm3_mlp_kernel<true, false><<<grid, 256, 0, st>>>(g, e);
+  else if (pout) gemm3_mlp_kernel<false, true><<<grid, 256, 0, st>>>(g, e);
+  else gemm3_mlp_kernel<false, false><<<grid, 256, 0, st>>>(g, e);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
 
 extern "C" int sd_gemm_bf16x3(const sd_gemm_desc* d, float* workspace, long workspace_floats, sd_stream stream_) {
   hipStream_t stream = (hipStream_t)stream_;

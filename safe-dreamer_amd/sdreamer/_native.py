@@ -80,6 +80,7 @@ class SliceKeys(ctypes.Structure):
 
 
 StatReq = _parse_struct(HEADER, "sd_stat_req")
+MlpExt = _parse_struct(HEADER, "sd_mlp_ext")
 
 
 class Stats(ctypes.Structure):

@@ -996,7 +996,7 @@ class Dreamer(nn.Module):
         l_rew, l_cont, l_val, l_slow = heads_nograd((self.reward, self.cont, self.value, self._slow_value), flat, True,
                                                     firsts_out=firsts)
         i_rew = K.twohot_mode(l_rew, self.rbins).view(H1, N)
-        i_contl = l_cont.view(H1, N)
+        i_contl = l_cont.reshape(H1, N)  # a column of the fused output layer's padded logits
         i_val = K.twohot_mode(l_val, self.vbins).view(H1, N)
         i_slow = K.twohot_mode(l_slow, self.vbins).view(H1, N)
         disc = 1 - 1 / self.horizon

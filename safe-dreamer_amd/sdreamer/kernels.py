@@ -147,6 +147,41 @@ def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1, fast=F
     return out
 
 
+def mlp_layer(x, w, out, bias=None, norm_w=None, part_in=None, part_out=None, act=1, alpha=1.0):
+    """One Linear of an MLP on the split-bf16 core with the previous layer's RMSNorm + SiLU fused into the A loader
+    (sd_gemm_bf16x3_mlp): out[b] = act(rms(x[b]) * norm_w[b]) @ w[b]^T + bias[b]. Batched over dim 0 of 3-D operands
+    (x may be an expanded (stride-0) view); norm_w None = x taken as is; part_in (n, q, M): the producer's row
+    partial sums of squares; part_out (n, N / 64, M) receives this layer's. Returns False when the shape is outside the
+    fused kernel (the caller then takes the unfused path)."""
+    if x.dim() == 2:
+        x, w, out = x[None], w[None], out[None]
+        bias = bias[None] if bias is not None else None
+        norm_w = norm_w[None] if norm_w is not None else None
+        part_in = part_in[None] if part_in is not None else None
+        part_out = part_out[None] if part_out is not None else None
+    n, M, Kk = x.shape
+    Nn = w.shape[1]
+    _chk(x, w, out, bias)
+    if x.stride(2) != 1 or w.stride(2) != 1 or not out.is_contiguous() or (bias is not None and bias.stride(1) != 1):
+        return False
+    d = nat.GemmDesc()
+    d.A, d.B, d.C, d.bias = p(x), p(w), p(out), (p(bias) if bias is not None else None)
+    d.lda, d.ldb, d.ldc = x.stride(1), w.stride(1), Nn
+    d.strideA, d.strideB, d.strideC = x.stride(0), w.stride(0), M * Nn
+    d.strideBias = bias.stride(0) if bias is not None else 0
+    d.M, d.N, d.K, d.batch = M, Nn, Kk, n
+    d.a_kcontig, d.b_kcontig, d.ksplit, d.tile = 1, 1, 1, 0
+    d.alpha, d.beta = float(alpha), 0.0
+    e = nat.MlpExt()
+    if norm_w is not None:
+        e.norm_w, e.stride_norm_w = p(norm_w), norm_w.stride(0)
+        e.part_in, e.stride_part_in, e.npart_in = p(part_in), part_in.stride(0), part_in.shape[1]
+        e.act, e.eps = int(act), EPS
+    if part_out is not None:
+        e.part_out, e.stride_part_out = p(part_out), part_out.stride(0)
+    return nat.call_shaped("sd_gemm_bf16x3_mlp", ctypes.byref(d), ctypes.addressof(e), stream())
+
+
 def mm(a, b, bias=None, out=None, **kw):
     M, Nn = a.shape[-2], b.shape[-1]
     if out is None:
@@ -601,6 +636,7 @@ class LaunchProbe:
 
 # ------------------------------------------------------------------------------------------------- metrics
 STAT_MEAN, STAT_STD, STAT_MIN, STAT_MAX = 0, 1, 2, 3
+_STAT_CHUNK = nat._define(nat.HEADER, "SD_STAT_CHUNK")
 
 
 class Stat:
@@ -639,8 +675,8 @@ def tensorstats(t, prefix):
 
 
 def metric_vector(values):
-    """(len(values),) float32 device tensor: values are Stat or tensors (a tensor = its mean); one launch per
-    SD_MAX_STATS terms (normally one)."""
+    """(len(values),) float32 device tensor: values are Stat or tensors (a tensor = its mean); one sd_multi_stats call
+    (two launches) per SD_MAX_STATS terms (normally one)."""
     reqs = []
     for i, v in enumerate(values):
         for t, kind, sc in (v.terms if isinstance(v, Stat) else [(v, STAT_MEAN, 1.0)]):
@@ -650,21 +686,21 @@ def metric_vector(values):
             reqs.append((_c(t), kind, sc, i))
     out = torch.empty(len(values), dtype=torch.float32, device=reqs[0][0].device if reqs else "cuda")
     cap = len(nat.Stats().r)
-    first = True
+    chunk = _STAT_CHUNK
     for lo in range(0, len(reqs), cap):
         st = nat.Stats()
-        chunk = reqs[lo:lo + cap]
-        for j, (t, kind, sc, i) in enumerate(chunk):
+        part = reqs[lo:lo + cap]
+        c0 = 0
+        for j, (t, kind, sc, i) in enumerate(part):
             r = st.r[j]
-            r.x, r.n, r.kind, r.out, r.scale = p(t), t.numel(), kind, i, sc
-        st.nreq = len(chunk)
-        if first:
-            nat.call("sd_multi_stats", ctypes.addressof(st), p(out), len(values), stream())
-            first = False
-        else:  # a second chunk adds to the first's slots
-            extra = torch.empty_like(out)
-            nat.call("sd_multi_stats", ctypes.addressof(st), p(extra), len(values), stream())
-            out.add_(extra)
+            r.x, r.n, r.kind, r.out, r.scale, r.chunk0 = p(t), t.numel(), kind, i, sc, c0
+            c0 += (t.numel() + chunk - 1) // chunk
+        st.nreq = len(part)
+        ws = torch.empty(5 * c0, dtype=torch.float32, device=out.device)
+        dst = out if lo == 0 else torch.empty_like(out)
+        nat.call("sd_multi_stats", ctypes.addressof(st), p(ws), p(dst), len(values), stream())
+        if lo:  # a second table's slots add to the first's
+            out.add_(dst)
     return out
 
 

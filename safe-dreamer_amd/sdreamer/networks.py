@@ -10,6 +10,7 @@ All forward/backward compute goes through sdreamer.ops (HIP kernels).
 from __future__ import annotations
 
 import math
+import os
 import re
 
 import torch
@@ -205,25 +206,89 @@ class MLPHead(nn.Module):
         return K.linear(h, self.last.weight, self.last.bias, fast=fast)
 
 
+FUSED_HEADS = os.environ.get("SDREAMER_FUSED_HEADS", "1") != "0"
+
+
 @torch.no_grad()
 def heads_nograd(heads, x, fast=False, firsts_out=None):
-    """Frozen logits of several MLPHeads on the same input rows x (M, F) with ONE batched launch for their first
-    layers (the contraction over F dominates: A is read once per column tile for all heads, 4x the workgroups of
-    one head's launch). Falls back to per-head forwards when the first layers differ in shape or use symlog.
-    firsts_out (a list): receives the (n, M, U) first-layer outputs of the batched launch (kept for reuse)."""
+    """Frozen logits of several MLPHeads on the same input rows x (M, F). The four first layers run as ONE batched
+    launch (A = x broadcast over the heads: read once per row tile on one XCD, gemm3's tile order); with `fast` the
+    rest of every head is fused too (_heads_rest_fused: each later layer applies the previous layer's RMSNorm + SiLU
+    while staging its input, so no normalised tensor is written). Falls back to per-head forwards when the first
+    layers differ in shape or use symlog. firsts_out (a list): receives the (n, M, U) first-layer outputs."""
     firsts = [h.mlp._mods[0][0] for h in heads]
     shape = tuple(firsts[0].weight.shape)
     if any(h.mlp._symlog_inputs or h.mlp.n < 1 for h in heads) or any(tuple(f.weight.shape) != shape for f in firsts):
         return [h.logits_nograd(x, fast) for h in heads]
     x = x.reshape(-1, x.shape[-1])
-    M, n = x.shape[0], len(heads)
+    M, n, U = x.shape[0], len(heads), shape[0]
     w = torch.stack([f.weight for f in firsts])  # (n, U, F)
     b = torch.stack([f.bias for f in firsts])  # (n, U)
-    h0 = torch.empty(n, M, shape[0], dtype=torch.float32, device=x.device)
+    h0 = torch.empty(n, M, U, dtype=torch.float32, device=x.device)
+    if fast and FUSED_HEADS and U % 64 == 0:
+        p0 = torch.empty(n, U // 64, M, dtype=torch.float32, device=x.device)
+        if K.mlp_layer(x.expand(n, M, x.shape[1]), w, h0, bias=b, part_out=p0):
+            if firsts_out is not None:
+                firsts_out.append(h0)
+            out = _heads_rest_fused(heads, h0, p0)
+            if out is not None:
+                return out
     K.gemm(x.expand(n, M, x.shape[1]), w.transpose(1, 2), h0, bias=b, fast=fast)
     if firsts_out is not None:
         firsts_out.append(h0)
     return [h.logits_from_first(h0[i], fast) for i, h in enumerate(heads)]
+
+
+@torch.no_grad()
+def _heads_rest_fused(heads, h0, p0):
+    """Layers 1.. and the output layer of every head after the batched first layer, each a sd_gemm_bf16x3_mlp launch
+    batched over the heads that share it: heads with the same depth run their hidden layers together (their
+    activations are consecutive slices of one buffer), and the output layer of a depth group is one launch with the
+    output weights zero-padded to the group's widest head (the continue head's single logit rides with the reward
+    head's 255). Returns None when a shape falls outside the fused kernel."""
+    n, M, U = h0.shape
+    dev = h0.device
+    depth = [h.mlp.n for h in heads]
+    bufs, parts = {0: (list(range(n)), h0, p0)}, {}
+    for layer in range(1, max(depth)):
+        idx = [i for i in range(n) if depth[i] > layer]
+        prev_idx, prev_h, prev_p = bufs[layer - 1]
+        pos = [prev_idx.index(i) for i in idx]
+        if pos != list(range(pos[0], pos[0] + len(pos))):
+            return None
+        sl = slice(pos[0], pos[0] + len(pos))
+        w = torch.stack([heads[i].mlp._mods[layer][0].weight for i in idx])
+        b = torch.stack([heads[i].mlp._mods[layer][0].bias for i in idx])
+        nw = torch.stack([heads[i].mlp._mods[layer - 1][1].weight for i in idx])
+        h = torch.empty(len(idx), M, U, dtype=torch.float32, device=dev)
+        pt = torch.empty(len(idx), U // 64, M, dtype=torch.float32, device=dev)
+        if not K.mlp_layer(prev_h[sl], w, h, bias=b, norm_w=nw, part_in=prev_p[sl], part_out=pt):
+            return None
+        bufs[layer] = (idx, h, pt)
+    out = [None] * n
+    for dep in sorted(set(depth)):
+        idx = [i for i in range(n) if depth[i] == dep]
+        src_idx, src_h, src_p = bufs[dep - 1]
+        pos = [src_idx.index(i) for i in idx]
+        if pos != list(range(pos[0], pos[0] + len(pos))):
+            return None
+        sl = slice(pos[0], pos[0] + len(pos))
+        no = max(heads[i].last.weight.shape[0] for i in idx)
+        no_p = max(no, 64)
+        w = torch.zeros(len(idx), no_p, U, dtype=torch.float32, device=dev)
+        b = torch.zeros(len(idx), no_p, dtype=torch.float32, device=dev)
+        for j, i in enumerate(idx):
+            r = heads[i].last.weight.shape[0]
+            w[j, :r] = heads[i].last.weight
+            b[j, :r] = heads[i].last.bias
+        nw = torch.stack([heads[i].mlp._mods[dep - 1][1].weight for i in idx])
+        lg = torch.empty(len(idx), M, no_p, dtype=torch.float32, device=dev)
+        if not K.mlp_layer(src_h[sl], w, lg, bias=b, norm_w=nw, part_in=src_p[sl]):
+            return None
+        for j, i in enumerate(idx):
+            r = heads[i].last.weight.shape[0]
+            out[i] = lg[j] if r == no_p else lg[j, :, :r]
+    return out
 
 
 class ConvEncoder(nn.Module):

@@ -115,3 +115,55 @@ def test_gemm_bf16x3_batched_split():
     ref = a.double() @ b.double()
     bound = 4e-5 * (a.double().abs() @ b.double().abs()) + 1e-6
     assert ((out.double() - ref).abs() - bound).max().item() <= 0
+
+
+@pytest.mark.parametrize("M,N,K,n,rms", [(1000, 256, 2560, 4, False), (4096, 256, 256, 2, True),
+                                          (2048, 255, 256, 2, True), (300, 128, 96, 1, True)])
+def test_gemm_bf16x3_mlp(M, N, K, n, rms):
+    """sd_gemm_bf16x3_mlp: out[b] = silu(rms(x[b]) * nw[b]) @ w[b]^T + bias[b] (RMSNorm from the producer's row
+    partials, nn.RMSNorm eps 1e-4) and this layer's row partial sums of squares per 64 columns, against torch fp32
+    (split-bf16 tolerance 4e-5 * sum |a||b| per output, as test_gemm_bf16x3_*); x broadcast over the batch when not
+    normalised (the imagined heads' first layers)."""
+    from sdreamer import kernels as kern
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(n if rms else 1, M, K, generator=g) * 2
+    w = torch.randn(n, N, K, generator=g) / K ** 0.5
+    b = torch.randn(n, N, generator=g) * 0.1
+    nw = 1 + 0.1 * torch.randn(n, K, generator=g)
+    if rms:
+        a = x / torch.sqrt((x * x).mean(-1, keepdim=True) + 1e-4) * nw[:, None]
+        a = a * torch.sigmoid(a)
+        pin = torch.stack([(x[:, :, c:c + 64] ** 2).sum(-1) for c in range(0, K, 64)], 1)  # (n, K/64, M)
+    else:
+        a = x.expand(n, M, K)
+    ref = torch.einsum("bmk,bnk->bmn", a.double(), w.double()) + b.double()[:, None]
+    bound = torch.einsum("bmk,bnk->bmn", a.abs().double(), w.abs().double()) * 4e-5 + 1e-6
+    xd = x.to("cuda") if rms else x.to("cuda").expand(n, M, K)
+    out = torch.empty(n, M, N, device="cuda")
+    pout = torch.empty(n, N // 64, M, device="cuda") if N % 64 == 0 else None
+    ok = kern.mlp_layer(xd, w.to("cuda"), out, bias=b.to("cuda"), norm_w=nw.to("cuda") if rms else None,
+                     part_in=pin.to("cuda") if rms else None, part_out=pout)
+    assert ok
+    err = (out.double().cpu() - ref).abs()
+    assert (err <= bound).all(), float((err - bound).max())
+    if pout is not None:
+        o = out.double().cpu()
+        pref = torch.stack([(o[:, :, c:c + 64] ** 2).sum(-1) for c in range(0, N, 64)], 1)
+        assert torch.allclose(pout.double().cpu(), pref, rtol=1e-5, atol=1e-6)
+
+
+def test_heads_fused_match_unfused():
+    """networks.heads_nograd's fused path (every layer one batched sd_gemm_bf16x3_mlp launch) against the per-head
+    fp32 forwards on the same rows: the four imagined heads of the walker agent (reward / continue 1 hidden layer,
+    value / slow value 3)."""
+    from sdreamer.networks import heads_nograd
+    from test_gpu_dreamer import build_agent
+    ag, _, _, _ = build_agent("walker_r2")
+    heads = (ag.reward, ag.cont, ag.value, ag._slow_value)
+    F = heads[0].mlp._mods[0][0].weight.shape[1]
+    x = torch.randn(2048, F, generator=torch.Generator().manual_seed(3)).to("cuda")
+    got = heads_nograd(heads, x, True)
+    for h, gl in zip(heads, got):
+        ref = h.logits_nograd(x, False)
+        scale = float(ref.abs().max()) + 1e-6
+        assert float((gl - ref).abs().max()) <= 2e-4 * scale, (float((gl - ref).abs().max()), scale)

@@ -345,6 +345,24 @@ def test_barlow():
     close(xd.grad, xr.grad, 1e-5, "grad")
 
 
+def test_metric_vector():
+    """kernels.metric_vector (sd_multi_stats): mean / unbiased std / min / max of tensors above and below one chunk
+    (SD_STAT_CHUNK), scalar tensors, and scaled sums of several terms into one slot, against torch."""
+    from sdreamer import kernels as K
+    g = _g(5)
+    a = torch.randn(98304, generator=g) * 3 + 1
+    b = torch.rand(15, 1024, generator=g)
+    c = torch.tensor(2.5)
+    d = torch.randn(7, generator=g)
+    A, Bt, C, D = (t.to(DEV) for t in (a, b, c, d))
+    vals = list(K.tensorstats(A, "a").values()) + list(K.tensorstats(Bt, "b").values()) + [
+        C, K.Stat(D, K.STAT_STD), K.Stat(C) + K.Stat(A, scale=0.5) + K.Stat(D, K.STAT_MAX, scale=-2.0)]
+    got = K.metric_vector(vals).cpu().double()
+    ref = torch.tensor([a.mean(), a.std(), a.min(), a.max(), b.mean(), b.std(), b.min(), b.max(), c, d.std(),
+                        c + 0.5 * a.mean() - 2.0 * d.max()]).double()
+    assert torch.allclose(got, ref, rtol=2e-6, atol=1e-6), (got, ref)
+
+
 def test_imag_ac_loss_fused():
     """ops.ImagACLossFn (sd_imag_ac_loss_fwd / _bwd) against the reference's torch formulation (dreamer.py:623-671 with
     TwoHot.log_prob, distributions.py:100-129): policy / value losses, the advantage, and the gradients of logits,

@@ -21,6 +21,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_table import _db, counters, short  # noqa: E402
 
+MARK_US = []
+
 
 def window(tdir):
     con = _db(tdir)
@@ -33,6 +35,8 @@ def window(tdir):
     if not b or not e:
         raise SystemExit("no k_trace_mark window in the trace (bench.py too old?)")
     t0, t1 = b[-1][2], e[-1][1]
+    global MARK_US
+    MARK_US = [(m[2] - m[1]) / 1e3 for m in (b[-1], e[-1])]  # durations of the two empty dispatches
     out = collections.defaultdict(list)
     for k, gx, gy, gz, st, en in rows:
         if t0 <= st and en <= t1 and not k.startswith("k_trace_mark"):
@@ -69,11 +73,12 @@ def main(tdir, steps, out_json, *pdirs):
             h, m = c["TCC_HIT_sum"], c.get("TCC_MISS_sum", 0.0)
             r["l2_hit"] = h / (h + m) if h + m else None
         rows.append(r)
-    res = {"steps": steps, "window_ms_per_update": span / steps / 1e6, "kernel_ms_per_update": total / steps / 1e6,
+    res = {"empty_dispatch_us": MARK_US, "steps": steps, "window_ms_per_update": span / steps / 1e6, "kernel_ms_per_update": total / steps / 1e6,
            "trace_dir": os.path.basename(os.path.normpath(tdir)), "rows": rows}
     json.dump(res, open(out_json, "w"), indent=1)
     print(f"timed window: {span / steps / 1e6:.3f} ms per update ({steps} updates); kernel time "
-          f"{total / steps / 1e6:.3f} ms per update (two streams overlap)\n")
+          f"{total / steps / 1e6:.3f} ms per update (two streams overlap); an empty dispatch (k_trace_mark) lasts "
+          f"{MARK_US[0]:.2f} / {MARK_US[1]:.2f} us in this trace\n")
     print("| rank | ms/update | share | launches/update | avg us | kernel | grid | HBM MB/launch | clock GHz | "
           "mfma util | L2 hit |")
     print("|---:|---:|---:|---:|---:|---|---|---:|---:|---:|---:|")

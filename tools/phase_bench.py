@@ -1,0 +1,70 @@
+"""Stand-alone timing of update phases at the bench shape (walker B16 L64 H15), HIP events on the current stream:
+  * every captured phase graph of a graph-replayed update, replayed alone (its inputs persist between replays);
+  * the imagined heads + lambda-returns (_heads_returns) with the fused heads path on and off, and its first-layer
+    batched GEMM alone.
+Usage: python tools/phase_bench.py [reps]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "safe-dreamer_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def timed(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    from sdreamer import networks
+    from sdreamer.config import load_config
+    from sdreamer.dreamer import Dreamer
+    cfg = load_config("dmc/cnn", ["device=cuda:0", "model.compile=False"])
+    torch.manual_seed(0)
+    agent = Dreamer(cfg.model, bench._Spaces({"image": bench._Sp((64, 64, 3))}), bench._Sp((6,)))
+    buf = bench.synth_buffer(cfg, torch.device("cuda", 0), 0)
+    for _ in range(4):
+        agent.update(buf)
+    torch.cuda.synchronize()
+    names = ("P", "S1", "M1", "R", "M2a", "S3", "M2b", "S4", "M2c", "M2d", "S2", "M3")
+    for nm, g in zip(names, agent._graph):
+        if g is not None:
+            print(f"phase {nm:4s} alone: {timed(g.replay, reps):8.3f} ms")
+    r = agent.rssm
+    N, H1 = 1024, 16
+    g = torch.Generator(device="cuda").manual_seed(1)
+    feats = torch.randn(H1, N, r.feat_size, device="cuda", generator=g)
+    with torch.no_grad():
+        for fused in (True, False):
+            networks.FUSED_HEADS = fused
+            print(f"heads + returns (fused heads {fused}): {timed(lambda: agent._heads_returns(feats), reps):8.3f} ms")
+            heads = (agent.reward, agent.cont, agent.value, agent._slow_value)
+            flat = feats.reshape(H1 * N, -1)
+            print(f"  heads_nograd only: {timed(lambda: networks.heads_nograd(heads, flat, True), reps):8.3f} ms")
+        networks.FUSED_HEADS = True
+        from sdreamer import kernels as K
+        w = torch.stack([h.mlp._mods[0][0].weight for h in heads])
+        b = torch.stack([h.mlp._mods[0][0].bias for h in heads])
+        M, F = flat.shape
+        h0 = torch.empty(4, M, 256, device="cuda")
+        p0 = torch.empty(4, 4, M, device="cuda")
+        print(f"  layer-0 batched GEMM (mlp kernel, partials): "
+              f"{timed(lambda: K.mlp_layer(flat.expand(4, M, F), w, h0, bias=b, part_out=p0), reps) * 1e3:8.1f} us")
+        print(f"  layer-0 batched GEMM (gemm3): "
+              f"{timed(lambda: K.gemm(flat.expand(4, M, F), w.transpose(1, 2), h0, bias=b, fast=True), reps) * 1e3:8.1f} us")
+
+
+if __name__ == "__main__":
+    main()
