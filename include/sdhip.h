@@ -53,6 +53,12 @@ int sd_gemm_f32(const sd_gemm_desc* d, float* workspace, long workspace_floats, 
  * v_mfma_f32_16x16x32_bf16 with f32 accumulation, ~1e-5 relative to the typical |term| * sqrt(K), 5.3x the f32 MFMA
  * rate. For gradient contractions and frozen heads (no sampled index depends on them). M, N or K < 64 -> f32 path. */
 int sd_gemm_bf16x3(const sd_gemm_desc* d, float* workspace, long workspace_floats, sd_stream stream);
+/* Weight gradient with its bias gradient (nn.Linear backward): the sd_gemm_bf16x3 contraction C = A . B for
+ * rows-contiguous A (A = dy^T, a_kcontig 0, batch 1) that also forms rowsum[m] = alpha * sum_k A[m, k] (the bias
+ * gradient, dy's column sums), added to rowsum when accumulate. With split-K the workspace needs ksplit * M floats
+ * after the ksplit * M * N partial slabs. SD_ESHAPE for shapes the split-bf16 kernel does not take (M, N or K < 64). */
+int sd_gemm_bf16x3_wgrad(const sd_gemm_desc* d, float* workspace, long workspace_floats, float* rowsum, int accumulate,
+                         sd_stream stream);
 /* One MLP layer (networks.py:313-336 Linear -> RMSNorm -> SiLU chains) on the split-bf16 core, batched like the GEMM:
  * C[b] = act(rms(A[b]) * norm_w[b]) . B[b] + bias[b] with k-contiguous A (M, K) and B = W^T (W (N, K) row-major),
  * K a multiple of 32, beta 0, no split-K. norm_w null: A used as is. Otherwise rstd(row m) = 1 / sqrt(sum_q

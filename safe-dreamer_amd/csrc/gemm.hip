@@ -232,7 +232,7 @@ extern "C" int sd_gemm_f32(const sd_gemm_desc* d, float* workspace, long workspa
   hipStream_t stream = (hipStream_t)stream_;
   if (!d || !d->A || !d->B || !d->C) return SD_EARG;
   if (d->M <= 0 || d->N <= 0 || d->batch <= 0) return SD_OK;
-  GemmArgs g;
+  GemmArgs g{};
   g.A = d->A; g.B = d->B; g.C = d->C; g.bias = d->bias; g.ws = workspace;
   g.lda = d->lda; g.ldb = d->ldb; g.ldc = d->ldc;
   g.sA = d->strideA; g.sB = d->strideB; g.sC = d->strideC; g.sBias = d->strideBias;

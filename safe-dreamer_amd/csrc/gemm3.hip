@@ -42,7 +42,7 @@ SD_DEV void g3_tile(const GemmArgs& g, int& tx, int& ty, int& tz) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool VA, bool VB>
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool VA, bool VB, bool RS = false>
 __global__ __launch_bounds__(256, 2) void gemm3_kernel(GemmArgs g) {
   int tx, ty, tz;
   g3_tile(g, tx, ty, tz);
@@ -57,16 +57,42 @@ __global__ __launch_bounds__(256, 2) void gemm3_kernel(GemmArgs g) {
   OA la(A, g.lda, g.M, bm0);
   OB lb(Bp, g.ldb, g.N, bn0);
   f32x4 acc[WM / 16][WN / 16];
-  if (SD_G3_FP)
+  if constexpr (RS) {  // weight gradient: also the row sums of A (the bias gradient), written by column tile 0
+    static_assert(!AK, "row sums need the rows-contiguous A loader");
+    RowSumOp<OA> ra(la);
+    gemm3_mainloop<BM, BN, WM, WN>(ra, lb, kbeg, kend, acc);
+    if (tx == 0) {
+      __shared__ float part[(BK / 4) * BM], rows[BM];
+      row_sums_km3<BM>(ra, part, rows);
+      for (int r = threadIdx.x; r < BM; r += 256) {
+        const int m = bm0 + r;
+        if (m >= g.M) continue;
+        if (g.ksplit > 1)
+          g.rs_ws[(long)split * g.M + m] = rows[r];
+        else
+          g.rowsum[m] = (g.rs_acc ? g.rowsum[m] : 0.f) + g.alpha * rows[r];
+      }
+    }
+  } else if (SD_G3_FP) {
     gemm3_mainloop_fp<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
-  else
+  } else {
     gemm3_mainloop<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
+  }
   gemm3_epilogue<BM, BN, WM, WN>(g, acc, bm0, bn0, b, split);
 }
 
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC>
 void launch3_tile(const GemmArgs& g, bool va, bool vb, hipStream_t st) {
   dim3 grid(sd_cdiv(g.N, BN), sd_cdiv(g.M, BM), g.batch * g.ksplit);
+  if constexpr (!AK) {
+    if (g.rowsum) {
+      if (va && vb) gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, true, true><<<grid, 256, 0, st>>>(g);
+      else if (va) gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, false, true><<<grid, 256, 0, st>>>(g);
+      else if (vb) gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, true, true><<<grid, 256, 0, st>>>(g);
+      else gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, false, true><<<grid, 256, 0, st>>>(g);
+      return;
+    }
+  }
   if (va && vb) gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, true><<<grid, 256, 0, st>>>(g);
   else if (va) gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, false><<<grid, 256, 0, st>>>(g);
   else if (vb) gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, true><<<grid, 256, 0, st>>>(g);
@@ -218,7 +244,7 @@ extern "C" int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd
   const bool rms = x->norm_w != nullptr, pout = x->part_out != nullptr;
   if (rms && (!x->part_in || x->npart_in <= 0 || !al16_3(x->norm_w) || x->stride_norm_w % 4)) return SD_EARG;
   if (pout && d->N % 64) return SD_ESHAPE;
-  GemmArgs g;
+  GemmArgs g{};
   g.A = d->A; g.B = d->B; g.C = d->C; g.bias = d->bias; g.ws = nullptr;
   g.lda = d->lda; g.ldb = d->ldb; g.ldc = d->ldc;
   g.sA = d->strideA; g.sB = d->strideB; g.sC = d->strideC; g.sBias = d->strideBias;
@@ -236,19 +262,43 @@ extern "C" int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd
   return SD_OK;
 }
 
+namespace {
+int gemm3_run(const sd_gemm_desc* d, float* workspace, long workspace_floats, float* rowsum, int rs_acc,
+              sd_stream stream_);
+}
+
 extern "C" int sd_gemm_bf16x3(const sd_gemm_desc* d, float* workspace, long workspace_floats, sd_stream stream_) {
-  hipStream_t stream = (hipStream_t)stream_;
   if (!d || !d->A || !d->B || !d->C) return SD_EARG;
   if (d->M <= 0 || d->N <= 0 || d->batch <= 0) return SD_OK;
   if (d->M < 64 || d->N < 64 || d->K < 64) return sd_gemm_f32(d, workspace, workspace_floats, stream_);
-  GemmArgs g;
+  return gemm3_run(d, workspace, workspace_floats, nullptr, 0, stream_);
+}
+
+extern "C" int sd_gemm_bf16x3_wgrad(const sd_gemm_desc* d, float* workspace, long workspace_floats, float* rowsum,
+                                    int accumulate, sd_stream stream_) {
+  if (!d || !d->A || !d->B || !d->C || !rowsum) return SD_EARG;
+  if (d->M <= 0 || d->N <= 0) return SD_OK;
+  if (d->M < 64 || d->N < 64 || d->K < 64 || d->batch != 1 || d->a_kcontig) return SD_ESHAPE;
+  return gemm3_run(d, workspace, workspace_floats, rowsum, accumulate, stream_);
+}
+
+namespace {
+int gemm3_run(const sd_gemm_desc* d, float* workspace, long workspace_floats, float* rowsum, int rs_acc,
+              sd_stream stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  GemmArgs g{};
+  g.rowsum = rowsum;
+  g.rs_acc = rs_acc;
+  g.rs_ws = nullptr;
   g.A = d->A; g.B = d->B; g.C = d->C; g.bias = d->bias; g.ws = workspace;
   g.lda = d->lda; g.ldb = d->ldb; g.ldc = d->ldc;
   g.sA = d->strideA; g.sB = d->strideB; g.sC = d->strideC; g.sBias = d->strideBias;
   g.M = d->M; g.N = d->N; g.K = d->K; g.batch = d->batch;
   g.alpha = d->alpha; g.beta = d->beta;
   int ks = d->ksplit < 1 ? 1 : d->ksplit;
-  if (ks > 1 && (!workspace || workspace_floats < (long)ks * d->batch * d->M * d->N)) return SD_EARG;
+  const long slabs = (long)ks * d->batch * d->M * d->N;
+  if (ks > 1 && (!workspace || workspace_floats < slabs + (rowsum ? (long)ks * d->M : 0))) return SD_EARG;
+  if (ks > 1 && rowsum) g.rs_ws = workspace + slabs;
   g.ksplit = ks;
   long kc = ((long)d->K + ks - 1) / ks;
   g.kchunk = (int)((kc + BK - 1) / BK * BK);
@@ -274,3 +324,4 @@ extern "C" int sd_gemm_bf16x3(const sd_gemm_desc* d, float* workspace, long work
   }
   return SD_OK;
 }
+}  // namespace

@@ -93,6 +93,11 @@ struct KM3 {
   static constexpr int NBLK = ROWS * BK / 16;
   static constexpr int NV = (NBLK + 255) / 256;
   f32x4 r[NV][4];
+  // sums over k of the thread's 4 rows per block (rowsum(): the bias gradient of a weight-gradient GEMM)
+  SD_DEV void rowsum_add(f32x4 (&acc)[NV]) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] += (r[v][0] + r[v][1]) + (r[v][2] + r[v][3]);
+  }
   const float* p;
   long ld;
   int nrows, row0;
@@ -136,6 +141,45 @@ struct KM3 {
     }
   }
 };
+
+// Row sums of an A loader's tiles over the K loop, in a fixed order: per thread in rowsum_add, then over the BK / 4
+// k-quads of a row in row_sums. Wraps the loader: load() also accumulates.
+template <class Op>
+struct RowSumOp {
+  Op& op;
+  f32x4 acc[Op::NV];
+  static constexpr int NVv = Op::NV;
+  SD_DEV explicit RowSumOp(Op& o) : op(o) {
+#pragma unroll
+    for (int v = 0; v < Op::NV; ++v) acc[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  SD_DEV void load(int k0, int kend) {
+    op.load(k0, kend);
+    op.rowsum_add(acc);
+  }
+  SD_DEV void store(__bf16* lds) const { op.store(lds); }
+};
+// KM3<ROWS> block i = (rq = i % (ROWS / 4), kq = i / (ROWS / 4)) holds rows 4rq..4rq+3; part: LDS (BK / 4) x ROWS
+template <int ROWS, class R>
+SD_DEV void row_sums_km3(const R& rs, float* part, float* out_rows) {
+#pragma unroll
+  for (int v = 0; v < R::NVv; ++v) {
+    const int i = threadIdx.x + v * 256;
+    if (i < ROWS * BK / 16) {
+      const int rq = i % (ROWS / 4), kq = i / (ROWS / 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) part[kq * ROWS + 4 * rq + j] = rs.acc[v][j];
+    }
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < ROWS; r += 256) {
+    float s = 0.f;
+#pragma unroll
+    for (int kq = 0; kq < BK / 4; ++kq) s += part[kq * ROWS + r];
+    out_rows[r] = s;
+  }
+  __syncthreads();
+}
 
 template <int BM, int BN>
 constexpr int gemm3_smem_bf16() {

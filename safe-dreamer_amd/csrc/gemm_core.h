@@ -20,6 +20,11 @@ struct GemmArgs {
   long sA, sB, sC, sBias;
   int M, N, K, batch, ksplit, kchunk;
   float alpha, beta;
+  // split-bf16 weight-gradient GEMMs (sd_gemm_bf16x3_wgrad): rowsum[m] (+)= alpha * sum_k A[m, k] (the bias gradient
+  // of C = dy^T x); with split-K each split writes its partial to rs_ws[split * M + m], summed by gemm_reduce_kernel
+  float* rowsum;
+  float* rs_ws;
+  int rs_acc;
 };
 
 // Load a ROWS x BK tile of an operand into registers (rows = m for A / n for B).
@@ -664,6 +669,13 @@ __global__ void gemm_reduce_kernel(GemmArgs g) {
     float* c = g.C + (long)b * g.sC + (long)m * g.ldc + n;
     if (g.beta != 0.f) v += g.beta * *c;
     *c = v;
+  }
+  if (g.rowsum) {  // the bias gradient's split partials, fixed order (batch 1)
+    for (long m = blockIdx.x * (long)blockDim.x + threadIdx.x; m < g.M; m += (long)gridDim.x * blockDim.x) {
+      float v = 0.f;
+      for (int s = 0; s < g.ksplit; ++s) v += g.rs_ws[(long)s * g.M + m];
+      g.rowsum[m] = (g.rs_acc ? g.rowsum[m] : 0.f) + g.alpha * v;
+    }
   }
 }
 

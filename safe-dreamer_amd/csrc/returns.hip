@@ -118,13 +118,14 @@ SD_DEV float funkey(uint32_t k) {
 }
 
 // x: n floats. ema[2] updated in place; os[0] = offset, os[1] = scale, qout[2] = raw quantiles (optional)
+constexpr int RE_KPT = 16;  // keys kept in registers per thread (n <= 16,384: one global read of x in all 4 passes)
 __global__ __launch_bounds__(1024) void return_ema_kernel(const float* __restrict__ x, int n, float* ema, float* os,
                                                           float* qout, float alpha, float q0, float q1) {
   __shared__ unsigned hist[4][256];
   __shared__ uint32_t prefix[4];
   __shared__ int rank[4];
   __shared__ float val[4];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // ranks = q * (n - 1) in float32 (torch.quantile), below = floor, above = ceil
   const float nm1 = (float)(n - 1);
   const float r0 = q0 * nm1, r1 = q1 * nm1;
@@ -135,30 +136,58 @@ __global__ __launch_bounds__(1024) void return_ema_kernel(const float* __restric
     rank[tid] = (tid & 1) ? hi : lo;
     prefix[tid] = 0;
   }
+  const bool in_regs = n <= 1024 * RE_KPT;
+  uint32_t kr[RE_KPT];
+#pragma unroll
+  for (int j = 0; j < RE_KPT; ++j) {
+    const int i = tid + 1024 * j;
+    kr[j] = (in_regs && i < n) ? fkey(x[i]) : 0u;
+  }
   __syncthreads();
   for (int pass = 0; pass < 4; ++pass) {
     const int shift = 24 - 8 * pass;
-    for (int i = tid; i < 4 * 256; i += 1024) (&hist[0][0])[i] = 0;
+    (&hist[0][0])[tid] = 0;
     __syncthreads();
     const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (32 - 8 * pass));
-    for (int i = tid; i < n; i += 1024) {
-      const uint32_t k = fkey(x[i]);
-      const uint32_t d = (k >> shift) & 0xFFu;
+    const uint32_t p0 = prefix[0], p1 = prefix[1], p2 = prefix[2], p3 = prefix[3];
+    auto add = [&](uint32_t k) {
+      const uint32_t d = (k >> shift) & 0xFFu, h = k & hmask;
+      if (h == p0) atomicAdd(&hist[0][d], 1u);
+      if (h == p1) atomicAdd(&hist[1][d], 1u);
+      if (h == p2) atomicAdd(&hist[2][d], 1u);
+      if (h == p3) atomicAdd(&hist[3][d], 1u);
+    };
+    if (in_regs) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if ((k & hmask) == prefix[q]) atomicAdd(&hist[q][d], 1u);
+      for (int j = 0; j < RE_KPT; ++j)
+        if (tid + 1024 * j < n) add(kr[j]);
+    } else {
+      for (int i = tid; i < n; i += 1024) add(fkey(x[i]));
     }
     __syncthreads();
-    if (tid < 4) {
-      int rem = rank[tid];
-      int b = 0;
-      for (; b < 255; ++b) {
-        const int c = (int)hist[tid][b];
-        if (rem < c) break;
-        rem -= c;
+    if (wave < 4) {  // wave q finds quantile q's digit: lane l holds bins 4l..4l+3, wave-wide inclusive prefix sum
+      const int rem = rank[wave];
+      const unsigned c0 = hist[wave][4 * lane], c1 = hist[wave][4 * lane + 1], c2 = hist[wave][4 * lane + 2],
+                     c3 = hist[wave][4 * lane + 3];
+      const unsigned own = c0 + c1 + c2 + c3;
+      unsigned inc = own;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
       }
-      prefix[tid] |= ((uint32_t)b << shift);
-      rank[tid] = rem;
+      const unsigned exc = inc - own;
+      // the lane whose [exc, inc) holds rem: its first bin with rem < running count
+      const bool mine = (unsigned)rem >= exc && (unsigned)rem < inc;
+      if (mine) {
+        unsigned r = (unsigned)rem - exc;
+        int b = 4 * lane;
+        if (r >= c0) { r -= c0; ++b;
+          if (r >= c1) { r -= c1; ++b;
+            if (r >= c2) { r -= c2; ++b; } } }
+        prefix[wave] |= ((uint32_t)b << shift);
+        rank[wave] = (int)r;
+      }
     }
     __syncthreads();
   }

@@ -54,6 +54,9 @@ FUSED_IMAG = os.environ.get("SDREAMER_FUSED_IMAG", "1") != "0"
 # actor layer 0, the imagined heads' batched value layer 0) instead of re-contracting the imagined feats;
 # SDREAMER_REUSE_H0=0 recomputes them (A/B knob)
 REUSE_H0 = os.environ.get("SDREAMER_REUSE_H0", "1") != "0"
+# SDREAMER_PRIO=1 (schedule knob): graph-replayed updates run the critical chain on high-priority streams and the filler
+# phases (M1, S2-S4) on normal-priority ones
+STREAM_PRIO = os.environ.get("SDREAMER_PRIO", "0") == "1"
 
 
 def _symexp_bins(n, device):  # symexp_twohot bins, distributions.py:242-251
@@ -201,6 +204,7 @@ class Dreamer(nn.Module):
         # SDREAMER_MARKS=1: device timestamps at the phase boundaries of every update (kernels.Marks)
         self.marks = K.Marks(self.device) if os.environ.get("SDREAMER_MARKS", "0") != "0" else None
         self._side = torch.cuda.Stream(device=self.device)
+        self._prio_streams = None  # (main, side, fill, side fill) of STREAM_PRIO, created at the first replay
         self._comm = None  # data parallel: the gradient all-reduce stream (created on first use)
         self._buckets = self._grad_buckets()
         self._graph = None
@@ -559,21 +563,36 @@ class Dreamer(nn.Module):
             self._ema_updates += 1
             self._proto_gate.fill_(0.0 if self._protos_frozen() else 1.0)
         gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gS2, gM3 = self._graph
-        main = torch.cuda.current_stream()
-        side = self._side if self.use_side_stream else main
-        gP.replay()
+        caller = torch.cuda.current_stream()
+        if STREAM_PRIO and self.use_side_stream:
+            # the critical chain (P, S1, R, M2a..M2d, M3) on high-priority streams, the phases that fill its idle CUs
+            # (M1 beside the imagination, S2-S4 beside the backward) on normal-priority ones: the dispatcher then
+            # serves a waiting critical-chain workgroup before a filler one
+            if self._prio_streams is None:
+                mk = lambda pr: torch.cuda.Stream(device=self.device, priority=pr)  # noqa: E731
+                self._prio_streams = (mk(-1), mk(-1), mk(0), mk(0))
+            main, side, fill, side_fill = self._prio_streams
+            main.wait_stream(caller)
+        else:
+            main = caller
+            side = self._side if self.use_side_stream else main
+            fill, side_fill = main, side
+        with torch.cuda.stream(main):
+            gP.replay()
         if side is not main:
             side.wait_stream(main)
+        if fill is not main:
+            fill.wait_stream(main)
         k1 = gS1.first_collective()
         with torch.cuda.stream(side):
             gS1.replay(0, k1)
-        gM1.replay()
+        with torch.cuda.stream(fill):
+            gM1.replay()
+            ev_m1 = torch.cuda.Event()
+            ev_m1.record()
         dp = self.world > 1
         if dp and self._comm is None:
             self._comm = torch.cuda.Stream(device=self.device)
-        if dp and not DEFER_WM:
-            ev_m1 = torch.cuda.Event()
-            ev_m1.record()
         with torch.cuda.stream(side):
             gS1.replay(k1)
             ev_s1 = torch.cuda.Event()
@@ -581,34 +600,38 @@ class Dreamer(nn.Module):
         if dp and not DEFER_WM:  # heads bucket final after M1 (else after M2d); issued after S1's returns gather so
             # RCCL's one communicator stream does not queue that gather (R waits on it) behind this all-reduce
             self._allreduce_bucket("heads", ev_m1)
+        main.wait_event(ev_m1)
         main.wait_event(ev_s1)
-        gR.replay()
-        ev_rep = torch.cuda.Event()
-        ev_rep.record()
-        gM2a.replay()
-        ev_scan = torch.cuda.Event()
-        ev_scan.record()
-        if S2_AFTER_SCAN:
-            ev_rep = ev_scan
-        gM2b.replay()
-        ev_enc = torch.cuda.Event()
-        ev_enc.record()
-        gM2c.replay()
-        if gM2d is not None:
-            gM2d.replay()
+        with torch.cuda.stream(main):
+            gR.replay()
+            ev_rep = torch.cuda.Event()
+            ev_rep.record()
+            gM2a.replay()
+            ev_scan = torch.cuda.Event()
+            ev_scan.record()
+            if S2_AFTER_SCAN:
+                ev_rep = ev_scan
+            gM2b.replay()
+            ev_enc = torch.cuda.Event()
+            ev_enc.record()
+            gM2c.replay()
+            if gM2d is not None:
+                gM2d.replay()
         ev_side = [None, None]
-        with torch.cuda.stream(side):
-            side.wait_event(ev_rep)
+        if side_fill is not side:
+            side_fill.wait_stream(side)
+        with torch.cuda.stream(side_fill):
+            side_fill.wait_event(ev_rep)
             gS2.replay()
             if dp:
                 ev_side[0] = torch.cuda.Event()
                 ev_side[0].record()
-            side.wait_event(ev_scan)  # S3: the scan's weight gradients, beside the encoder backward
+            side_fill.wait_event(ev_scan)  # S3: the scan's weight gradients, beside the encoder backward
             gS3.replay()
             if dp:
                 ev_side[1] = torch.cuda.Event()
                 ev_side[1].record()
-            side.wait_event(ev_enc)  # S4: encoder stages 2..'s weight gradients, beside the first stage's backward
+            side_fill.wait_event(ev_enc)  # S4: encoder stages 2..'s weight gradients, beside the first stage's backward
             gS4.replay()
         if dp:  # bucketed sum all-reduce of the gradient arena, overlapping the backward phases still running
             ev_main, ev_s4 = torch.cuda.Event(), torch.cuda.Event()
@@ -618,15 +641,18 @@ class Dreamer(nn.Module):
                 self._allreduce_bucket("rssm", ev_side[1], ev_main)
             else:
                 self._allreduce_bucket("rssm", ev_side[1])
-            ev_s4.record(side)
+            ev_s4.record(side_fill)
             if DEFER_WM:
                 self._allreduce_bucket("heads", ev_main)
             self._allreduce_bucket("rest", ev_main, ev_s4)
-        if side is not main:
-            main.wait_stream(side)
+        if side_fill is not main:
+            main.wait_stream(side_fill)
         if dp:
             main.wait_stream(self._comm)
-        gM3.replay()
+        with torch.cuda.stream(main):
+            gM3.replay()
+        if main is not caller:
+            caller.wait_stream(main)
         self._slow_value_updates += 1
         self._optimizer.host_steps += 1
         self._updates += 1

@@ -92,10 +92,12 @@ def _fast_split(M, N, K, batch):
     return max(1, min(K // 128, -(-256 // t64), 16))
 
 
-def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1, fast=False):
+def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1, fast=False, rowsum=None):
     """out[M,N] = alpha * a[M,K] @ b[K,N] (+ bias[N]) (+ beta*out). Strided views allowed (one unit stride each);
     3-D operands are a strided batch over dim 0. fast=True: split-bf16 MFMA path (sd_gemm_bf16x3, ~1e-5 relative)
-    for contractions no sampled index depends on (gradients, frozen heads)."""
+    for contractions no sampled index depends on (gradients, frozen heads). rowsum (M,): also accumulate
+    alpha * a's row sums into it in the same launch (sd_gemm_bf16x3_wgrad: a weight gradient's bias gradient);
+    returns False without launching when that fused form does not apply (the caller reduces separately)."""
     _chk(a, b, out, bias)
     if a.dtype != torch.float32 or b.dtype != torch.float32 or out.dtype != torch.float32:
         raise TypeError("fp32 GEMM")
@@ -126,6 +128,8 @@ def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1, fast=F
     if M == 0 or Nn == 0:
         return out
     fast = fast and FAST_GEMM and M >= 64 and Nn >= 64 and K >= 64
+    if rowsum is not None and not (fast and Bt == 1 and not ak and rowsum.is_contiguous()):
+        return False
     if ksplit is None:
         if fast:
             ksplit = _fast_split(M, Nn, K, Bt)
@@ -141,10 +145,24 @@ def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1, fast=F
     d.alpha, d.beta = float(alpha), float(beta)
     ws = None
     if ksplit > 1:
-        ws = torch.empty(ksplit * Bt * M * Nn, dtype=torch.float32, device=out.device)
+        extra = ksplit * M if rowsum is not None else 0
+        ws = torch.empty(ksplit * Bt * M * Nn + extra, dtype=torch.float32, device=out.device)
+    if rowsum is not None:
+        return nat.call_shaped("sd_gemm_bf16x3_wgrad", ctypes.byref(d), p(ws), ws.numel() if ws is not None else 0,
+                               p(rowsum), 1, stream())
     nat.call("sd_gemm_bf16x3" if fast else "sd_gemm_f32", ctypes.byref(d), p(ws), ws.numel() if ws is not None else 0,
              stream())
     return out
+
+
+def wgrad(dy, x, dw, db=None):
+    """nn.Linear backward's parameter gradients on the split-bf16 path: dw += dy^T x, db += column sums of dy (in the
+    same launch when the shape allows, else a separate column-sum launch). dy (R, O), x (R, I), dw (O, I)."""
+    if db is not None and gemm(dy.t(), x, dw, beta=1.0, fast=True, rowsum=db) is not False:
+        return
+    gemm(dy.t(), x, dw, beta=1.0, fast=True)
+    if db is not None:
+        colsum(dy, db, accumulate=True)
 
 
 def mlp_layer(x, w, out, bias=None, norm_w=None, part_in=None, part_out=None, act=1, alpha=1.0):

@@ -82,9 +82,9 @@ class LinearFn(torch.autograd.Function):
             dx = k.mm(dy2, w, fast=True).view(ctx.in_shape)
 
         def wgrad():
-            if w.requires_grad:
-                k.gemm(dy2.t(), x2, grad_buf(w), beta=1.0, fast=True)
-            if b is not None and b.requires_grad:
+            if w.requires_grad:  # dW (+ db in the same launch)
+                k.wgrad(dy2, x2, grad_buf(w), grad_buf(b) if (b is not None and b.requires_grad) else None)
+            elif b is not None and b.requires_grad:
                 k.colsum(dy2, grad_buf(b), accumulate=True)
 
         if _DEFER is not None:
@@ -111,9 +111,9 @@ class LinearPreFn(torch.autograd.Function):
         dy2 = _flat(dy).contiguous()
 
         def wgrad():
-            if w.requires_grad:
-                k.gemm(dy2.t(), x2, grad_buf(w), beta=1.0, fast=True)
-            if b is not None and b.requires_grad:
+            if w.requires_grad:  # dW (+ db in the same launch)
+                k.wgrad(dy2, x2, grad_buf(w), grad_buf(b) if (b is not None and b.requires_grad) else None)
+            elif b is not None and b.requires_grad:
                 k.colsum(dy2, grad_buf(b), accumulate=True)
 
         if _DEFER is not None:

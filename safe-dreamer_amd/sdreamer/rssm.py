@@ -508,28 +508,22 @@ class ObserveScan(torch.autograd.Function):
         def wgrads(d_x2=d_x2):
             if norm_w is not None:
                 d_x2 = norm_w()
-            K.gemm(f(dl_all).t(), f(oo), gb(P["Wl"]), beta=1.0, fast=True)
-            K.colsum(f(dl_all), gb(P["bl"]))
+            K.wgrad(f(dl_all), f(oo), gb(P["Wl"]), gb(P["bl"]))  # weight + bias gradient, one launch
             gWo = gb(P["Wo"])
-            K.gemm(f(d_op).t(), f(deter), gWo[:, :D], beta=1.0, fast=True)
+            K.wgrad(f(d_op), f(deter), gWo[:, :D], gb(P["bo"]))
             K.gemm(d_op_b.t(), emb_t, gWo[:, D:], beta=1.0, fast=True)  # both batch-major
-            K.colsum(f(d_op), gb(P["bo"]))
             K.gemm(f(d_gates).view(M, G, 3 * Dg).permute(1, 2, 0), f(hh).view(M, G, Dg).permute(1, 0, 2),
                    gb(P["Wg"]), beta=1.0, fast=True)
             K.colsum(f(d_gates), gb(P["bg"]))
             gWh = gb(P["Wh"])
             Ig = gWh.shape[2]
-            K.gemm(f(d_hp).t(), f(xcat), gWh.view(D, Ig)[:, Dg:], beta=1.0, fast=True)
+            K.wgrad(f(d_hp), f(xcat), gWh.view(D, Ig)[:, Dg:], gb(P["bh"]))
             K.gemm(f(d_hp).view(M, G, Dg).permute(1, 2, 0), f(h_in).view(M, G, Dg).permute(1, 0, 2), gWh[:, :, :Dg],
                    beta=1.0, fast=True)
-            K.colsum(f(d_hp), gb(P["bh"]))
-            K.gemm(f(d_x0p).t(), f(h_in), gb(P["W0"]), beta=1.0, fast=True)
-            K.colsum(f(d_x0p), gb(P["b0"]))
-            K.gemm(f(d_x1p).t(), f(s_in), gb(P["W1"]), beta=1.0, fast=True)
-            K.colsum(f(d_x1p), gb(P["b1"]))
+            K.wgrad(f(d_x0p), f(h_in), gb(P["W0"]), gb(P["b0"]))
+            K.wgrad(f(d_x1p), f(s_in), gb(P["W1"]), gb(P["b1"]))
             d_x2p = K.rmsnorm_bwd(x2p, P["n2"], r2, f(d_x2), dw=gb(P["n2"]))
-            K.gemm(d_x2p.t(), a_n, gb(P["W2"]), beta=1.0, fast=True)
-            K.colsum(d_x2p, gb(P["b2"]))
+            K.wgrad(d_x2p, a_n, gb(P["W2"]), gb(P["b2"]))
 
         if ops._DEFER is not None:  # queued (ops.defer_wgrads): the caller runs them on another stream
             keep = (a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all, d_op, d_op_b, d_gates, d_hp, d_x0p,

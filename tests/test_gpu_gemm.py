@@ -167,3 +167,23 @@ def test_heads_fused_match_unfused():
         ref = h.logits_nograd(x, False)
         scale = float(ref.abs().max()) + 1e-6
         assert float((gl - ref).abs().max()) <= 2e-4 * scale, (float((gl - ref).abs().max()), scale)
+
+
+@pytest.mark.parametrize("R,O,I", [(15360, 256, 2560), (1024, 255, 256), (4096, 512, 256), (100, 64, 64)])
+def test_wgrad_fused_bias(R, O, I):
+    """kernels.wgrad: dw += dy^T x on the split-bf16 path with db += column sums of dy fused into the same launch
+    (sd_gemm_bf16x3_wgrad, split-K partials summed by the reduce launch) against torch fp32; the column sums to
+    1e-5 relative (fp32 sums in a fixed order), dw to the split-bf16 bound."""
+    from sdreamer import kernels as kern
+    g = torch.Generator().manual_seed(R + O)
+    dy = torch.randn(R, O, generator=g)
+    x = torch.randn(R, I, generator=g)
+    dw0 = torch.randn(O, I, generator=g)
+    db0 = torch.randn(O, generator=g)
+    dw, db = dw0.clone().to("cuda"), db0.clone().to("cuda")
+    kern.wgrad(dy.to("cuda"), x.to("cuda"), dw, db)
+    ref = dw0.double() + dy.double().t() @ x.double()
+    bound = (dy.abs().double().t() @ x.abs().double()) * 4e-5 + 1e-5
+    assert ((dw.double().cpu() - ref).abs() <= bound).all()
+    dref = db0.double() + dy.double().sum(0)
+    assert torch.allclose(db.double().cpu(), dref, rtol=1e-5, atol=1e-4 * float(dy.abs().sum(0).max()) * 1e-2)

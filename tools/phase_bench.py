@@ -2,7 +2,7 @@
   * every captured phase graph of a graph-replayed update, replayed alone (its inputs persist between replays);
   * the imagined heads + lambda-returns (_heads_returns) with the fused heads path on and off, and its first-layer
     batched GEMM alone.
-Usage: python tools/phase_bench.py [reps]"""
+Usage: python tools/phase_bench.py [reps] [phases, e.g. S2,M2a: only those, no heads timing]"""
 import os
 import sys
 
@@ -28,6 +28,7 @@ def timed(fn, reps):
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     from sdreamer import networks
     from sdreamer.config import load_config
     from sdreamer.dreamer import Dreamer
@@ -40,8 +41,15 @@ def main():
     torch.cuda.synchronize()
     names = ("P", "S1", "M1", "R", "M2a", "S3", "M2b", "S4", "M2c", "M2d", "S2", "M3")
     for nm, g in zip(names, agent._graph):
-        if g is not None:
+        if g is not None and (only is None or nm in only):
+            if only is not None:  # kernel-trace window around this phase's timed replays (tools/phase_trace.sh)
+                g.replay()
+                bench.trace_mark(1)
             print(f"phase {nm:4s} alone: {timed(g.replay, reps):8.3f} ms")
+            if only is not None:
+                bench.trace_mark(2)
+    if only is not None:
+        return
     r = agent.rssm
     N, H1 = 1024, 16
     g = torch.Generator(device="cuda").manual_seed(1)
