@@ -2,7 +2,8 @@
   * every captured phase graph of a graph-replayed update, replayed alone (its inputs persist between replays);
   * the imagined heads + lambda-returns (_heads_returns) with the fused heads path on and off, and its first-layer
     batched GEMM alone.
-Usage: python tools/phase_bench.py [reps] [phases, e.g. S2,M2a: only those, no heads timing]"""
+  * `contention`: the latency-bound critical phases beside their fillers and beside synthetic fillers.
+Usage: python tools/phase_bench.py [reps] [phases, e.g. S2,M2a: only those, no heads timing | contention]"""
 import os
 import sys
 
@@ -26,6 +27,54 @@ def timed(fn, reps):
     return s.elapsed_time(e) / reps
 
 
+def contended(crit, filler, reps):
+    """crit() on stream a with filler() (or nothing) on stream b started together: mean ms of crit's own span"""
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    tot = 0.0
+    for i in range(reps + 1):
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(a):
+            s.record()
+            if filler is not None:
+                b.wait_event(s)
+                with torch.cuda.stream(b):
+                    filler()
+            crit()
+            e.record()
+        torch.cuda.synchronize()
+        if i:
+            tot += s.elapsed_time(e)
+    return tot / reps
+
+
+def contention(agent, reps):
+    """Which property of a filler phase slows a latency-bound phase beside it: the critical S1 / M2a graphs replayed
+    alone, beside their real filler (M1 / S2), beside a filler of empty dispatches (launch count only) and beside a few
+    long memory-bound launches (occupancy and bandwidth only)."""
+    G = dict(zip(("P", "S1", "M1", "R", "M2a", "S3", "M2b", "S4", "M2c", "M2d", "S2", "M3"), agent._graph))
+    empty = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(empty, stream=s):
+            for _ in range(160):
+                bench.trace_mark(4)
+    x = torch.empty(64 << 20, device="cuda")
+    y = torch.empty_like(x)
+
+    def bw():  # 12 launches of 512 MB traffic each (~0.1 ms apiece at 5-6 TB/s)
+        for _ in range(12):
+            y.copy_(x)
+
+    for crit, fill in (("S1", "M1"), ("M2a", "S2")):
+        print(f"{crit}: alone {contended(G[crit].replay, None, reps):7.3f} ms | beside {fill} "
+              f"{contended(G[crit].replay, G[fill].replay, reps):7.3f} | beside 160 empty dispatches "
+              f"{contended(G[crit].replay, empty.replay, reps):7.3f} | beside 12 copy launches (6 GB) "
+              f"{contended(G[crit].replay, bw, reps):7.3f}")
+    print(f"filler alone: M1 {contended(G['M1'].replay, None, reps):.3f} S2 {contended(G['S2'].replay, None, reps):.3f} "
+          f"empty x160 {contended(empty.replay, None, reps):.3f} copies {contended(bw, None, reps):.3f} ms")
+
+
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
@@ -39,6 +88,9 @@ def main():
     for _ in range(4):
         agent.update(buf)
     torch.cuda.synchronize()
+    if only == ["contention"]:
+        contention(agent, reps)
+        return
     names = ("P", "S1", "M1", "R", "M2a", "S3", "M2b", "S4", "M2c", "M2d", "S2", "M3")
     for nm, g in zip(names, agent._graph):
         if g is not None and (only is None or nm in only):
