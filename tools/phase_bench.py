@@ -66,13 +66,31 @@ def contention(agent, reps):
         for _ in range(12):
             y.copy_(x)
 
+    xs, ys = x[:16 << 20], y[:16 << 20]
+
+    def bw4():  # the same launches at a quarter of the bytes
+        for _ in range(12):
+            ys.copy_(xs)
+
+    from sdreamer import _native as nat
+    from sdreamer import kernels as K
+    stamps = torch.zeros(2 * 512, dtype=torch.int64, device="cuda")
+    sink = torch.empty(512, device="cuda")
+
+    def mfma():  # 512 workgroups of dependent f32 MFMA chains, no memory traffic
+        nat.call("sd_clock_probe", stamps.data_ptr(), sink.data_ptr(), 512, 60000, K.stream())
+
+    fillers = (("empty x160", empty.replay), ("copies 6 GB", bw), ("copies 1.5 GB", bw4), ("MFMA-only", mfma))
     for crit, fill in (("S1", "M1"), ("M2a", "S2")):
-        print(f"{crit}: alone {contended(G[crit].replay, None, reps):7.3f} ms | beside {fill} "
-              f"{contended(G[crit].replay, G[fill].replay, reps):7.3f} | beside 160 empty dispatches "
-              f"{contended(G[crit].replay, empty.replay, reps):7.3f} | beside 12 copy launches (6 GB) "
-              f"{contended(G[crit].replay, bw, reps):7.3f}")
-    print(f"filler alone: M1 {contended(G['M1'].replay, None, reps):.3f} S2 {contended(G['S2'].replay, None, reps):.3f} "
-          f"empty x160 {contended(empty.replay, None, reps):.3f} copies {contended(bw, None, reps):.3f} ms")
+        line = f"{crit}: alone {contended(G[crit].replay, None, reps):7.3f} ms | beside {fill} " \
+               f"{contended(G[crit].replay, G[fill].replay, reps):7.3f}"
+        for nm, f in fillers:
+            line += f" | beside {nm} {contended(G[crit].replay, f, reps):7.3f}"
+        print(line)
+    line = f"filler alone: M1 {contended(G['M1'].replay, None, reps):.3f} S2 {contended(G['S2'].replay, None, reps):.3f}"
+    for nm, f in fillers:
+        line += f" | {nm} {contended(f, None, reps):.3f}"
+    print(line + " ms")
 
 
 def main():
