@@ -64,7 +64,12 @@ int sd_gemm_bf16x3_wgrad(const sd_gemm_desc* d, float* workspace, long workspace
  * K a multiple of 32, beta 0, no split-K. norm_w null: A used as is. Otherwise rstd(row m) = 1 / sqrt(sum_q
  * part_in[b][q][m] / K + eps) from the producer's npart_in partial sums of squares per row, act 1 = SiLU (0: none).
  * part_out (N % 64 == 0) receives this layer's partials, (N / 64, M) per batch entry: part_out[b][n / 64][m] =
- * sum of C[b][m][n'] ^ 2 over the 64 columns n' of block n / 64. Returns SD_ESHAPE outside these shapes. */
+ * sum of C[b][m][n'] ^ 2 over the 64 columns n' of block n / 64. Returns SD_ESHAPE outside these shapes.
+ * Per-entry operands (batch <= SD_MLP_MAXB): a non-null w_ptr[b] / bias_ptr[b] / norm_w_ptr[b] replaces
+ * B + b * strideB / bias + b * strideBias / norm_w + b * stride_norm_w (each weight (w_rows[b], K) row-major with row
+ * stride ldb), and w_rows[b] > 0 limits entry b's weight to that many rows: its columns n >= w_rows[b] of C get 0
+ * (+ no bias). So several heads' layers run as one launch without stacking (or zero-padding) their weights. */
+#define SD_MLP_MAXB 4
 typedef struct sd_mlp_ext {
   const float* norm_w;
   long stride_norm_w;
@@ -74,6 +79,10 @@ typedef struct sd_mlp_ext {
   float eps;
   float* part_out;
   long stride_part_out;
+  const float* w_ptr[SD_MLP_MAXB];
+  const float* bias_ptr[SD_MLP_MAXB];
+  const float* norm_w_ptr[SD_MLP_MAXB];
+  int w_rows[SD_MLP_MAXB];
 } sd_mlp_ext;
 int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd_stream stream);
 
@@ -138,7 +147,7 @@ int sd_repval_loss_bwd(const float* logits, const float* bins, const float* ret,
                        const float* gscale, float inv_n, float* dlogits, long rows, int NB, sd_stream s);
 /* Imagined actor-critic losses (dreamer.py:623-636, 653-671) over H * N time-major rows r = t * N + n: value logits
  * vl (H * N, NB), logpi / ent (H * N) of the imagined actions, slow (H * N) slow-value targets; batch-major
- * ret (N, H), w = weight (N, H1), val = imagined value (N, H1); scale: device scalar (ReturnEMA scale).
+ * ret (N, H), w = weight (N, H1), val = imagined value (H1, N) time-major; scale: device scalar (ReturnEMA scale).
  * fwd writes adv (N, H) = (ret - val[:, :H]) / scale and the row terms rows_v = w (-logp(ret) - logp(slow)),
  * rows_p = w -(logpi adv + coef ent) (H * N each; the losses are their means). bwd: d vl, d logpi, d ent from the
  * upstream gradients of the two means (device scalars gpolicy / gvalue, null = 0). */
@@ -178,6 +187,13 @@ int sd_mask_rows(const float* x, const uint8_t* mask, long mask_stride, float* y
 int sd_lambda_return(const float* reward, const float* term, const float* cont_logit, const float* last,
                      const float* boot, long boot_row_stride, long boot_t_stride, float* ret, float* cont,
                      float* weight, int N, int T, float disc, float lamb, sd_stream stream);
+/* The same with reward(r, t) = reward[r*rew_row_stride + t*rew_t_stride] and the continue logit likewise (the
+ * imagined heads' time-major outputs read in place, dreamer.py:598-602); term / last / ret / cont / weight stay
+ * (N, T) row-major. sd_lambda_return is this with strides (T, 1). */
+int sd_lambda_return_strided(const float* reward, long rew_row_stride, long rew_t_stride, const float* term,
+                             const float* cont_logit, long cont_row_stride, long cont_t_stride, const float* last,
+                             const float* boot, long boot_row_stride, long boot_t_stride, float* ret, float* cont,
+                             float* weight, int N, int T, float disc, float lamb, sd_stream stream);
 /* ReturnEMA (networks.py:406-422): torch.quantile(x, [q0, q1]) (exact radix select + lerp), ema <- alpha q +
  * (1-alpha) ema, offset_scale = (ema[0], max(ema[1]-ema[0], 1)). quantiles (2) optional. */
 int sd_return_ema(const float* x, int n, float* ema, float* offset_scale, float* quantiles, float alpha, float q0,
@@ -245,13 +261,15 @@ int sd_pool_rms_bwd_compact(const float* pooled, const uint8_t* amax, const floa
  * chunk tables are device arrays built once by the caller; scalars = sd_opt_scalars_bytes() zeroed bytes of device
  * memory (float64 step / lr EMAs); workspace >= 3*nchunks floats; grad_norms (ntensors) optional. Every gradient is
  * read as grad_scale * g (data parallel: 1 / world after the sum all-reduce), tensor gate_tensor's (>= 0) also times
- * the device scalar *gate (DreamerPro's prototype freeze, dreamer.py:424-425); -1 = no gated tensor. */
+ * the device scalar *gate (DreamerPro's prototype freeze, dreamer.py:424-425); -1 = no gated tensor. zero_grads: every
+ * gradient element the step reads is set to 0 after the read (the next update's optimizer.zero_grad(), dreamer.py:423,
+ * folded into this pass; the arena padding between tensors stays 0 anyway). */
 int sd_opt_scalars_bytes(void);
 int sd_agc_laprop_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, const long* chunk_beg,
                        const long* chunk_end, const int* chunk_tensor, const int* tensor_chunk0, int nchunks,
                        int ntensors, float* workspace, void* scalars, float* grad_norms, float clip, float pmin,
                        double lr0, double warmup, double beta1, double beta2, double eps, float grad_scale,
-                       int gate_tensor, const float* gate, sd_stream stream);
+                       int gate_tensor, const float* gate, int zero_grads, sd_stream stream);
 /* slow critic: dst = mix*src + (1-mix)*dst (Dreamer._update_slow_target, dreamer.py:242-249) */
 int sd_polyak(const float* src, float* dst, long n, float mix, sd_stream stream);
 
@@ -384,7 +402,7 @@ typedef struct sd_imagine {
   int stream_img, stream_act;
   long row_offset;
   const float* Wa[4]; const float* ba[4]; const float* na[4];  /* actor layer i: (U, in_i) (U) (U) */
-  const float *Wao, *bao;                  /* actor output: (2A or A, U) rows, zero-padded to 64 rows (the tile reads 64) */
+  const float *Wao, *bao;                  /* actor output: (2A or A, U) rows */
   const float *W0, *b0, *n0, *W1, *b1, *n1, *W2, *b2, *n2;       /* _dyn_in0/1/2 */
   const float *Wh, *bh, *nh, *Wg, *bg;                           /* _dyn_hid (G,Dg,Dg+3U), _dyn_gru (G,3Dg,Dg) */
   const float* Wi[4]; const float* bi[4]; const float* ni[4];    /* img_net layer i */

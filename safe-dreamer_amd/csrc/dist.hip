@@ -348,7 +348,7 @@ __global__ void repval_bwd_kernel(const float* __restrict__ logits, const float*
 }
 
 // imagined actor-critic losses (dreamer.py:623-636, 653-671) on H * N time-major rows r = t * N + n, the returns /
-// weights / values batch-major (n, t): adv = (ret[n, t] - val[n, t]) / scale[0] (written for the metrics),
+// weights batch-major (n, t), the values time-major (t, n): adv = (ret[n, t] - val[t, n]) / scale[0] (metrics),
 // value row  = w[n, t] * (-logp(vl[r], ret[n, t]) - logp(vl[r], slow[r]))   (TwoHot, distributions.py:100-129),
 // policy row = w[n, t] * -(logpi[r] * adv + coef * ent[r]).  One wave per row.
 __global__ void imag_ac_fwd_kernel(const float* __restrict__ vl, const float* __restrict__ bins,
@@ -376,7 +376,7 @@ __global__ void imag_ac_fwd_kernel(const float* __restrict__ vl, const float* __
     float ls = wb2 * (l[b2] - lse);
     ls += wa2 * (l[a2] - lse);
     const float wt = w[n * H1 + t];
-    const float a = (rt - val[n * H1 + t]) / scale[0];
+    const float a = (rt - val[(long)t * N + n]) / scale[0];
     rows_v[r] = wt * (-lr - ls);
     rows_p[r] = wt * -(logpi[r] * a + coef * ent[r]);
     adv[n * H + t] = a;

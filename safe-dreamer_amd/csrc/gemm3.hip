@@ -120,7 +120,19 @@ struct MlpExt {
   float eps;
   float* pout;
   long sPout;
+  const float* wp[SD_MLP_MAXB];  // per-entry operands (sd_mlp_ext): null = the strided batch
+  const float* bp[SD_MLP_MAXB];
+  const float* nwp[SD_MLP_MAXB];
+  int wrows[SD_MLP_MAXB];
 };
+
+// entry b of a per-entry array as a chain of selects (a dynamic index into a kernel-argument array would copy it to
+// scratch)
+template <class T>
+SD_DEV T pick_b(const T (&a)[SD_MLP_MAXB], int b) {
+  static_assert(SD_MLP_MAXB == 4, "pick_b");
+  return b == 0 ? a[0] : b == 1 ? a[1] : b == 2 ? a[2] : b == 3 ? a[3] : T{};
+}
 
 // A operand, k contiguous, rows normalised (x * rs[row] * nw[k], then SiLU if act) when stored into LDS
 template <int ROWS>
@@ -171,7 +183,9 @@ __global__ __launch_bounds__(256, 2) void gemm3_mlp_kernel(GemmArgs g, MlpExt e)
   const int bn0 = tx * BN, bm0 = ty * BM, b = tz;
   __shared__ float rs[BM];
   const float* A = g.A + (long)b * g.sA;
-  const float* Bp = g.B + (long)b * g.sB;
+  const float* wpb = pick_b(e.wp, b);
+  const float* Bp = wpb ? wpb : g.B + (long)b * g.sB;
+  const int wr_b = pick_b(e.wrows, b), nb = wr_b > 0 ? wr_b : g.N;  // entry b's weight rows (columns >= nb: 0)
   if (RMS) {  // this tile's rows: rstd from the producer's partial sums of squares
     const float* pin = e.pin + (long)b * e.sPin;
     for (int r = threadIdx.x; r < BM; r += 256) {
@@ -184,9 +198,10 @@ __global__ __launch_bounds__(256, 2) void gemm3_mlp_kernel(GemmArgs g, MlpExt e)
     __syncthreads();
   }
   f32x4 acc[TM][TN];
-  KC3<BN, true> lb(Bp, g.ldb, g.N, bn0);
+  KC3<BN, true> lb(Bp, g.ldb, nb, bn0);
   if constexpr (RMS) {
-    KC3Rms<BM> la(A, g.lda, g.M, bm0, e.nw + (long)b * e.sNw, rs, e.act);
+    const float* nwb = pick_b(e.nwp, b);
+    KC3Rms<BM> la(A, g.lda, g.M, bm0, nwb ? nwb : e.nw + (long)b * e.sNw, rs, e.act);
     gemm3_mainloop<BM, BN, WM, WN>(la, lb, 0, g.K, acc);
   } else {
     KC3<BM, true> la(A, g.lda, g.M, bm0);
@@ -195,7 +210,8 @@ __global__ __launch_bounds__(256, 2) void gemm3_mlp_kernel(GemmArgs g, MlpExt e)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave / (BN / WN), wc = wave % (BN / WN), l16 = lane & 15, q = lane >> 4;
   float* C = g.C + (long)b * g.sC;
-  const float* bias = g.bias ? g.bias + (long)b * g.sBias : nullptr;
+  const float* bpb = pick_b(e.bp, b);
+  const float* bias = bpb ? bpb : g.bias ? g.bias + (long)b * g.sBias : nullptr;
   float ss[TM][4];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -204,7 +220,7 @@ __global__ __launch_bounds__(256, 2) void gemm3_mlp_kernel(GemmArgs g, MlpExt e)
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = bn0 + wc * WN + 16 * j + l16;
-    const float bv = (bias && n < g.N) ? bias[n] : 0.f;
+    const float bv = (bias && n < nb) ? bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -241,9 +257,22 @@ extern "C" int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd
   if (!d->a_kcontig || !d->b_kcontig || d->K % BK || d->K < BK || d->N < 64 || d->beta != 0.f) return SD_ESHAPE;
   if (!al16_3(d->A) || !al16_3(d->B) || d->lda % 4 || d->ldb % 4 || (d->batch > 1 && (d->strideA % 4 || d->strideB % 4)))
     return SD_ESHAPE;
-  const bool rms = x->norm_w != nullptr, pout = x->part_out != nullptr;
-  if (rms && (!x->part_in || x->npart_in <= 0 || !al16_3(x->norm_w) || x->stride_norm_w % 4)) return SD_EARG;
+  bool any_nw = false;
+  for (int b = 0; b < SD_MLP_MAXB && b < d->batch; ++b) any_nw = any_nw || x->norm_w_ptr[b];
+  const bool rms = x->norm_w != nullptr || any_nw, pout = x->part_out != nullptr;
+  if (rms && (!x->part_in || x->npart_in <= 0 || (x->norm_w && (!al16_3(x->norm_w) || x->stride_norm_w % 4))))
+    return SD_EARG;
+  if (rms && !x->norm_w)  // every entry needs its own norm weight then
+    for (int b = 0; b < d->batch; ++b)
+      if (b >= SD_MLP_MAXB || !x->norm_w_ptr[b]) return SD_EARG;
   if (pout && d->N % 64) return SD_ESHAPE;
+  bool per_entry = false;
+  for (int b = 0; b < SD_MLP_MAXB; ++b) {
+    if (x->w_rows[b] < 0 || x->w_rows[b] > d->N) return SD_EARG;
+    if ((x->w_ptr[b] && !al16_3(x->w_ptr[b])) || (x->norm_w_ptr[b] && !al16_3(x->norm_w_ptr[b]))) return SD_ESHAPE;
+    per_entry = per_entry || x->w_ptr[b] || x->bias_ptr[b] || x->norm_w_ptr[b] || x->w_rows[b];
+  }
+  if (per_entry && d->batch > SD_MLP_MAXB) return SD_EARG;
   GemmArgs g{};
   g.A = d->A; g.B = d->B; g.C = d->C; g.bias = d->bias; g.ws = nullptr;
   g.lda = d->lda; g.ldb = d->ldb; g.ldc = d->ldc;
@@ -251,7 +280,13 @@ extern "C" int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd
   g.M = d->M; g.N = d->N; g.K = d->K; g.batch = d->batch;
   g.alpha = d->alpha; g.beta = 0.f; g.ksplit = 1; g.kchunk = d->K;
   MlpExt e{x->norm_w, x->stride_norm_w, x->part_in, x->stride_part_in, x->npart_in, x->act, x->eps, x->part_out,
-           x->stride_part_out};
+           x->stride_part_out, {}, {}, {}, {}};
+  for (int b = 0; b < SD_MLP_MAXB; ++b) {
+    e.wp[b] = x->w_ptr[b];
+    e.bp[b] = x->bias_ptr[b];
+    e.nwp[b] = x->norm_w_ptr[b];
+    e.wrows[b] = x->w_rows[b];
+  }
   dim3 grid(sd_cdiv(g.N, 128), sd_cdiv(g.M, 128), g.batch);
   hipStream_t st = (hipStream_t)stream_;
   if (rms && pout) gemm3_mlp_kernel<true, true><<<grid, 256, 0, st>>>(g, e);

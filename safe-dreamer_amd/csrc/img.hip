@@ -150,9 +150,10 @@ struct BRows {
   f32x4 r[NV];
   const float* W;
   long ld;
-  int base, seg, stride;
+  int base, seg, stride, nrows;  // rows >= nrows read as 0 (the actor's output weight has only 2A or A rows)
   SD_DEV BRows() = default;
-  SD_DEV BRows(const float* W_, long ld_, int base_, int seg_, int stride_) : W(W_), ld(ld_), base(base_), seg(seg_), stride(stride_) {}
+  SD_DEV BRows(const float* W_, long ld_, int base_, int seg_, int stride_, int nrows_ = 1 << 30)
+      : W(W_), ld(ld_), base(base_), seg(seg_), stride(stride_), nrows(nrows_) {}
   SD_DEV void load(int k0, int) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -160,7 +161,7 @@ struct BRows {
       if (256 * (v + 1) <= BN * BK / 4 || i < BN * BK / 4) {
         const int lr = i / (BK / 4), kq = i % (BK / 4);
         const long gr = base + (lr / seg) * stride + lr % seg;
-        r[v] = ld4(W + gr * ld + k0 + 4 * kq);
+        r[v] = gr < nrows ? ld4(W + gr * ld + k0 + 4 * kq) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
   }
@@ -713,7 +714,7 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
   __shared__ float rs[BM], red[256];
   wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
   const ARms<BM> a0(X, U, nw, rs, m0, d.N, U);
-  const BRows<BN> b0(d.Wao, U, 0, BN, 0);  // BN rows: the caller passes the output weight zero-padded to 64 rows
+  const BRows<BN> b0(d.Wao, U, 0, BN, 0, NO);  // the output weight's NO rows, zeros past them
   f32x4 acc[1][1];
   mainloop<F6_ACTION, FP_ACTION, BM, BN, 16, WN, pf_of(FP_ACTION ? 2 : 3)>(a0, b0, 0, U, acc);
   const Lane L = lane_ids<BN, WN>();
@@ -872,7 +873,6 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
   return SD_OK;
 }
 
-// BRows reads KA_BN <= 64 rows of the actor output weight: the caller passes Wao zero-padded to 64 rows
 extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   int rc = icheck(dp);
   if (rc) return rc;

@@ -51,13 +51,13 @@ __global__ void norms_kernel(const float* __restrict__ p, const float* __restric
 // AGC scale of the block's tensor from its chunks' sums (every block of a tensor sums them in the same order), then
 // the LaProp update of the chunk, float4-wide (elementwise: the same per-element arithmetic as the scalar form; the
 // arena padding stays 0 through it). The block of a tensor's first chunk writes the tensor's gradient norm.
-__global__ void laprop_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+__global__ void laprop_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                               float* __restrict__ v, const long* __restrict__ chunk_beg, const long* __restrict__ chunk_end,
                               const int* __restrict__ chunk_tensor, const int* __restrict__ tensor_chunk0,
                               const float* __restrict__ pn2, const float* __restrict__ gn2, float* __restrict__ gnorm_out,
                               const OptScalars* __restrict__ st, float clip, float pmin, float beta1, float beta2,
                               float one_m_beta2, float eps, float gscale, int gate_tensor,
-                              const float* __restrict__ gate) {
+                              const float* __restrict__ gate, int zero_grads) {
   __shared__ float red[4];
   const int c = blockIdx.x, t = chunk_tensor[c], c0 = tensor_chunk0[t], c1 = tensor_chunk0[t + 1];
   float sp = 0.f, sg = 0.f;
@@ -76,6 +76,7 @@ __global__ void laprop_kernel(float* __restrict__ p, const float* __restrict__ g
   const long b = chunk_beg[c], e4 = (chunk_end[c] + 3) & ~3L;
   for (long i = b + 4 * threadIdx.x; i < e4; i += 1024) {
     const f32x4 gq = *reinterpret_cast<const f32x4*>(g + i);
+    if (zero_grads) *reinterpret_cast<f32x4*>(g + i) = f32x4{0.f, 0.f, 0.f, 0.f};  // the next update's zero_grad
     f32x4 vq = *reinterpret_cast<const f32x4*>(v + i), mq = *reinterpret_cast<const f32x4*>(m + i),
           pq = *reinterpret_cast<const f32x4*>(p + i);
 #pragma unroll
@@ -109,7 +110,8 @@ extern "C" int sd_agc_laprop_step(float* params, float* grads, float* exp_avg, f
                                   const long* chunk_end, const int* chunk_tensor, const int* tensor_chunk0, int nchunks,
                                   int ntensors, float* workspace, void* scalars, float* grad_norms, float clip,
                                   float pmin, double lr0, double warmup, double beta1, double beta2, double eps,
-                                  float grad_scale, int gate_tensor, const float* gate, sd_stream stream_) {
+                                  float grad_scale, int gate_tensor, const float* gate, int zero_grads,
+                                  sd_stream stream_) {
   hipStream_t s = (hipStream_t)stream_;
   if (nchunks <= 0) return SD_OK;
   if (gate_tensor >= ntensors || (gate_tensor >= 0 && !gate)) return SD_EARG;
@@ -122,7 +124,8 @@ extern "C" int sd_agc_laprop_step(float* params, float* grads, float* exp_avg, f
   SD_LAUNCH_CHECK();
   laprop_kernel<<<nchunks, 256, 0, s>>>(params, grads, exp_avg, exp_avg_sq, chunk_beg, chunk_end, chunk_tensor,
                                          tensor_chunk0, pn2, gn2, grad_norms, st, clip, pmin, (float)beta1, (float)beta2,
-                                         (float)(1.0 - beta2), (float)eps, grad_scale, gate_tensor, gate);
+                                         (float)(1.0 - beta2), (float)eps, grad_scale, gate_tensor, gate,
+                                         zero_grads);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

@@ -11,18 +11,25 @@
 
 namespace {
 
+// reward (row r, step t) at reward[r * rs.rew_r + t * rs.rew_t], the continue logit likewise (the imagined heads'
+// outputs are time-major); term / last / the outputs are (N, T) row-major
+struct LrStrides {
+  long rew_r, rew_t, cont_r, cont_t, boot_r, boot_t;
+};
+
 __global__ void lambda_return_kernel(const float* __restrict__ reward, const float* __restrict__ term_in,
                                      const float* __restrict__ cont_logit, const float* __restrict__ last_in,
-                                     const float* __restrict__ boot, long boot_row_stride, long boot_t_stride,
+                                     const float* __restrict__ boot, LrStrides rs,
                                      float* __restrict__ ret, float* __restrict__ cont_out, float* __restrict__ weight,
                                      int N, int T, float disc, float lamb) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= N) return;
   const long base = (long)r * T;
+  const long boot_row_stride = rs.boot_r, boot_t_stride = rs.boot_t;
   if (cont_logit && (cont_out || weight)) {
     float w = 1.f;
     for (int t = 0; t < T; ++t) {
-      const float c = sigmoidf_(cont_logit[base + t]);
+      const float c = sigmoidf_(cont_logit[r * rs.cont_r + t * rs.cont_t]);
       if (cont_out) cont_out[base + t] = c;
       w = w * (c * disc);  // torch.cumprod(imag_cont * disc)
       if (weight) weight[base + t] = w;
@@ -33,11 +40,12 @@ __global__ void lambda_return_kernel(const float* __restrict__ reward, const flo
     const int i = t + 1;
     float term;
     if (term_in) term = term_in[base + i];
-    else term = 1.f - sigmoidf_(cont_logit[base + i]);  // term = 1 - imag_cont (dreamer.py:599)
+    else term = 1.f - sigmoidf_(cont_logit[r * rs.cont_r + i * rs.cont_t]);  // term = 1 - imag_cont (dreamer.py:599)
     const float last = last_in ? last_in[base + i] : 0.f;
     const float live = (1.f - term) * disc;
     const float cnt = (1.f - last) * lamb;
-    const float interm = reward[base + i] + (1.f - cnt) * live * boot[(long)r * boot_row_stride + (long)i * boot_t_stride];
+    const float interm = reward[r * rs.rew_r + i * rs.rew_t] +
+                         (1.f - cnt) * live * boot[(long)r * boot_row_stride + (long)i * boot_t_stride];
     out = interm + live * cnt * out;
     ret[(long)r * (T - 1) + t] = out;
   }
@@ -53,8 +61,8 @@ __global__ __launch_bounds__(256) void lambda_return_staged(const float* __restr
                                                             const float* __restrict__ term_in,
                                                             const float* __restrict__ cont_logit,
                                                             const float* __restrict__ last_in,
-                                                            const float* __restrict__ boot, long boot_row_stride,
-                                                            long boot_t_stride, float* __restrict__ ret,
+                                                            const float* __restrict__ boot, LrStrides rs,
+                                                            float* __restrict__ ret,
                                                             float* __restrict__ cont_out, float* __restrict__ weight,
                                                             int N, int T, float disc, float lamb) {
   extern __shared__ float sm[];
@@ -68,10 +76,10 @@ __global__ __launch_bounds__(256) void lambda_return_staged(const float* __restr
     float rw = 0.f, tc = 0.f, ls = 0.f, bt = 0.f;
     if (r < N) {
       const long gi = (long)r * T + t;
-      rw = reward[gi];
-      tc = term_in ? term_in[gi] : cont_logit[gi];
+      rw = reward[r * rs.rew_r + t * rs.rew_t];
+      tc = term_in ? term_in[gi] : cont_logit[r * rs.cont_r + t * rs.cont_t];
       ls = last_in ? last_in[gi] : 0.f;
-      bt = boot[(long)r * boot_row_stride + (long)t * boot_t_stride];
+      bt = boot[(long)r * rs.boot_r + (long)t * rs.boot_t];
     }
     s_rew[i] = rw;
     s_tc[i] = tc;
@@ -212,20 +220,29 @@ __global__ __launch_bounds__(1024) void return_ema_kernel(const float* __restric
 
 }  // namespace
 
+extern "C" int sd_lambda_return_strided(const float* reward, long rew_row_stride, long rew_t_stride, const float* term,
+                                        const float* cont_logit, long cont_row_stride, long cont_t_stride,
+                                        const float* last, const float* boot, long boot_row_stride, long boot_t_stride,
+                                        float* ret, float* cont, float* weight, int N, int T, float disc, float lamb,
+                                        sd_stream s) {
+  if (N <= 0 || T <= 0) return SD_OK;
+  if (!term && !cont_logit) return SD_EARG;
+  const LrStrides rs{rew_row_stride, rew_t_stride, cont_row_stride, cont_t_stride, boot_row_stride, boot_t_stride};
+  if (T <= 255 && !(term && cont_logit))  // 4 staged (LR_RB, T) planes fit the default 64 KB of dynamic LDS
+    lambda_return_staged<<<(N + LR_RB - 1) / LR_RB, 256, 4 * LR_RB * T * sizeof(float), (hipStream_t)s>>>(
+        reward, term, cont_logit, last, boot, rs, ret, cont, weight, N, T, disc, lamb);
+  else
+    lambda_return_kernel<<<(N + 255) / 256, 256, 0, (hipStream_t)s>>>(reward, term, cont_logit, last, boot, rs, ret,
+                                                                     cont, weight, N, T, disc, lamb);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
 extern "C" int sd_lambda_return(const float* reward, const float* term, const float* cont_logit, const float* last,
                                 const float* boot, long boot_row_stride, long boot_t_stride, float* ret, float* cont,
                                 float* weight, int N, int T, float disc, float lamb, sd_stream s) {
-  if (N <= 0 || T <= 0) return SD_OK;
-  if (!term && !cont_logit) return SD_EARG;
-  if (T <= 255 && !(term && cont_logit))  // 4 staged (LR_RB, T) planes fit the default 64 KB of dynamic LDS
-    lambda_return_staged<<<(N + LR_RB - 1) / LR_RB, 256, 4 * LR_RB * T * sizeof(float), (hipStream_t)s>>>(
-        reward, term, cont_logit, last, boot, boot_row_stride, boot_t_stride, ret, cont, weight, N, T, disc, lamb);
-  else
-    lambda_return_kernel<<<(N + 255) / 256, 256, 0, (hipStream_t)s>>>(reward, term, cont_logit, last, boot,
-                                                                     boot_row_stride, boot_t_stride, ret, cont, weight,
-                                                                     N, T, disc, lamb);
-  SD_LAUNCH_CHECK();
-  return SD_OK;
+  return sd_lambda_return_strided(reward, T, 1, term, cont_logit, T, 1, last, boot, boot_row_stride, boot_t_stride, ret,
+                                  cont, weight, N, T, disc, lamb, s);
 }
 
 extern "C" int sd_return_ema(const float* x, int n, float* ema, float* offset_scale, float* quantiles, float alpha,

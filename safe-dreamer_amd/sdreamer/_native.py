@@ -58,9 +58,11 @@ def _parse_struct(path, name):
         base, names = toks[0], [t for t in toks[1:] if t != ","]
         for n in names:
             typ = c_ptr if is_ptr else scalars[base]
-            m = re.match(r"(\w+)\[(\d+)\]$", n)
-            if m:
-                n, typ = m.group(1), typ * int(m.group(2))
+            m = re.match(r"(\w+)\[(\w+)\]$", n)
+            if m:  # array length: a literal or a #define of the header
+                ln = m.group(2)
+                ln = int(ln) if ln.isdigit() else int(re.search(r"#define " + ln + r"\s+(\d+)", text).group(1))
+                n, typ = m.group(1), typ * ln
             fields.append((n, typ))
     return type(name, (ctypes.Structure,), {"_fields_": fields})
 

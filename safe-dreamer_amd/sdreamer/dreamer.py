@@ -209,6 +209,8 @@ class Dreamer(nn.Module):
         self._buckets = self._grad_buckets()
         self._graph = None
         self._eager_updates = 0
+        self._step_zeroes = False  # graph replays: the optimizer step zeroes the gradients (_update_graphed)
+        self._grads_clean = False
         self._seed_base = int(getattr(config, "seed", 0) or 0) * 1_000_003 + 12345
         self.train()
 
@@ -474,7 +476,8 @@ class Dreamer(nn.Module):
         self._polyak()
         if self.rep_loss == "dreamerpro":  # replays run with ema_update_every == 1 and past update 0
             self._ema_apply(self._pro["frac"])
-        self._optimizer.zero_grad()
+        if not self._step_zeroes:  # else the previous replay's optimizer step left the gradients zeroed
+            self._optimizer.zero_grad()
         return self._ph_forward(p_data, initial, seed, ro)
 
     def _side_ac_metrics(self, st):
@@ -532,6 +535,9 @@ class Dreamer(nn.Module):
             def cap(fn, stream):
                 return parallel.capture_phase(fn, stream, mode)
 
+            # zero_grad folded into the optimizer step (M3 zeroes what it reads); the gradients are zeroed eagerly
+            # before a replay whenever something else wrote them (_grads_clean)
+            self._step_zeroes = True
             gP, st = cap(lambda: self._core_forward(self._g_in, self._g_init, self._seed_dev, ro), main_cap)
             gS1, _ = cap(lambda: self._ph_side_returns(st), side_cap)
             gM1, _ = cap(lambda: self._ph_wm(st, defer=DEFER_WM), main_cap)
@@ -546,7 +552,10 @@ class Dreamer(nn.Module):
             gM2c, _ = cap(lambda: self._ph_encoder_bwd_lo(st), main_cap)
             gM2d = cap(lambda: self._main_tail(st), main_cap)[0] if (DEFER_WM or S4_MAIN) else None
             gS2, (post, keys, mvec) = cap(lambda: self._side_ac_metrics(st), side_cap)
+            self._optimizer.zero_grads_after = True
             gM3, _ = cap(lambda: self._core_step(st), main_cap)
+            self._optimizer.zero_grads_after = False  # eager steps (step()) keep the PyTorch semantics
+            self._grads_clean = False
             torch.cuda.synchronize()
             for g in (gP, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gM3):
                 if g is not None and g.n_collectives:
@@ -578,6 +587,8 @@ class Dreamer(nn.Module):
             side = self._side if self.use_side_stream else main
             fill, side_fill = main, side
         with torch.cuda.stream(main):
+            if not self._grads_clean:
+                self._optimizer.zero_grad()
             gP.replay()
         if side is not main:
             side.wait_stream(main)
@@ -651,6 +662,7 @@ class Dreamer(nn.Module):
             main.wait_stream(self._comm)
         with torch.cuda.stream(main):
             gM3.replay()
+        self._grads_clean = True
         if main is not caller:
             caller.wait_stream(main)
         self._slow_value_updates += 1
@@ -677,6 +689,7 @@ class Dreamer(nn.Module):
         are ordered by an event (replay value on main first, then the imagined value loss on side). Graph mode
         captures each phase separately (_update_graphed). Data parallel runs the same two streams; the exchange steps
         (parallel.collective) are issued on the stream of the phase that needs them."""
+        self._grads_clean = False  # an eager backward writes the gradient arena
         st = self._ph_forward(data, initial, seed, row_offset)
         main = torch.cuda.current_stream()
         side = self._side if self.use_side_stream else main
@@ -724,11 +737,23 @@ class Dreamer(nn.Module):
                                                                seed=seed, row_offset=ro)
         mk("scan_fwd")
         leaves = [t.detach().requires_grad_(True) for t in (post_stoch, post_deter, post_logit)]
-        feat_l = self.rssm.get_feat(leaves[0], leaves[1])
+        ifeats = None
+        if self._fused_imag_ok():
+            # the posterior feat is written straight into the imagination's start slot (feats[0] of its time-major
+            # (H1, N, F) buffer): the side stream's imagination starts from it without a copy
+            B, T = post_deter.shape[:2]
+            r = self.rssm
+            ifeats = torch.empty(self.imag_horizon + 1, B * T, r.feat_size, dtype=torch.float32,
+                                 device=post_deter.device)
+            feat_l = ops.CatIntoFn.apply(leaves[0].reshape(B, T, r.flat_stoch), leaves[1],
+                                         [ifeats[0].view(B, T, r.feat_size)])
+        else:
+            feat_l = self.rssm.get_feat(leaves[0], leaves[1])
         feat_r = feat_l.detach().requires_grad_(True)  # replay-value leaf (side stream)
         return dict(data=data, initial=initial, seed=seed, ro=ro, embed=embed, embed_l=embed_l,
                     enc_split=split[0] if split else None, post_stoch=post_stoch,
-                    post_deter=post_deter, post_logit=post_logit, leaves=leaves, feat_l=feat_l, feat_r=feat_r)
+                    post_deter=post_deter, post_logit=post_logit, leaves=leaves, feat_l=feat_l, feat_r=feat_r,
+                    ifeats=ifeats)
 
     def _ph_side_returns(self, st):
         """side: imagination (dreamer.py:578-597), imagined heads, lambda-returns + ReturnEMA (598-636)."""
@@ -741,7 +766,7 @@ class Dreamer(nn.Module):
         # actor layer 0's fp32 output of every imagined step, kept for the policy loss's actor forward (REUSE_H0)
         ah0 = torch.empty(H1, N, self.actor.mlp.out_dim, device=start[1].device) \
             if REUSE_H0 and self._fused_imag_ok() and not self.actor.mlp._symlog_inputs else None
-        ifeat, iact = self._imagine_tm(start, H1, st["seed"], st["ro"] * T, actor_h0=ah0)
+        ifeat, iact = self._imagine_tm(start, H1, st["seed"], st["ro"] * T, actor_h0=ah0, feats=st.get("ifeats"))
         self._mark("side:imagine")
         rr = self._heads_returns(ifeat)
         rr["act_h0"] = ah0
@@ -1026,16 +1051,15 @@ class Dreamer(nn.Module):
         i_val = K.twohot_mode(l_val, self.vbins).view(H1, N)
         i_slow = K.twohot_mode(l_slow, self.vbins).view(H1, N)
         disc = 1 - 1 / self.horizon
-        rew_n, contl_n, val_n = i_rew.t().contiguous(), i_contl.t().contiguous(), i_val.t().contiguous()
         i_cont = torch.empty(N, H1, device=dev)
         weight = torch.empty(N, H1, device=dev)
-        ret = K.lambda_return(rew_n, val_n, disc, self.lamb, cont_logit=contl_n, cont_out=i_cont,
-                              weight_out=weight)  # (N, H)
+        # the time-major head outputs read in place through (N, H1) transposed views
+        ret = K.lambda_return(i_rew.t(), i_val, disc, self.lamb, cont_logit=i_contl.t(), cont_out=i_cont,
+                              weight_out=weight, boot_row_stride=1, boot_t_stride=N)  # (N, H)
         # the value head's first layer on the imagined feats, the same contraction the value loss's forward needs
         # (_frozen_value aliases value; the weights change only at the optimizer step)
         val_h0 = firsts[0][2] if (firsts and REUSE_H0) else None
-        return dict(ret=ret, weight=weight, i_cont=i_cont, i_rew=i_rew, i_val=i_val, i_slow=i_slow, val_n=val_n,
-                    val_h0=val_h0)
+        return dict(ret=ret, weight=weight, i_cont=i_cont, i_rew=i_rew, i_val=i_val, i_slow=i_slow, val_h0=val_h0)
 
     @torch.no_grad()
     def _returns_norm(self, rr):
@@ -1070,7 +1094,7 @@ class Dreamer(nn.Module):
             vl = self.value(xh, fast=True)
         # policy (dreamer.py:653-660) and value (661-671) losses and the advantage (628-636): one launch each way
         losses["policy"], losses["value"], adv = ops.ImagACLossFn.apply(
-            vl, logpi, ent, self.vbins, ret, i_slow[:H], weight, rr["val_n"], rr["ret_scale"], self.act_entropy)
+            vl, logpi, ent, self.vbins, ret, i_slow[:H], weight, rr["i_val"], rr["ret_scale"], self.act_entropy)
         rr["adv"] = adv
         (losses["policy"] * self._loss_scales["policy"] + losses["value"] * self._loss_scales["value"]).backward()
         with torch.no_grad():
@@ -1123,10 +1147,8 @@ class Dreamer(nn.Module):
         d.stream_img, d.stream_act, d.row_offset = STREAM_IMG, STREAM_ACT, int(row_offset)
         for i, (lin, norm) in enumerate(a.mlp._mods):
             d.Wa[i], d.ba[i], d.na[i] = lin.weight.data_ptr(), lin.bias.data_ptr(), norm.weight.data_ptr()
-        wo = a.last.weight
-        wpad = torch.zeros(64, wo.shape[1], dtype=torch.float32, device=wo.device)  # the action tile reads 64 rows
-        wpad[:wo.shape[0]] = wo
-        d.Wao, d.bao = wpad.data_ptr(), a.last.bias.data_ptr()
+        wo = a.last.weight.contiguous()  # (2A or A, U): the action tile zero-fills its rows past them
+        d.Wao, d.bao = wo.data_ptr(), a.last.bias.data_ptr()
         for k in ("W0", "b0", "n0", "W1", "b1", "n1", "W2", "b2", "n2", "Wh", "bh", "nh", "Wg", "bg"):
             setattr(d, k, P[k].data_ptr())
         mods, last = r._img_mods()
@@ -1144,7 +1166,7 @@ class Dreamer(nn.Module):
         d.work = work.data_ptr()
         bounds = list(chunks) if chunks else [0, H1]
         if keep is not None:  # measurement aid (bench.py): the descriptor and every buffer it points to
-            keep.update(desc=d, work=work, wpad=wpad, feats=feats, actions=actions, P=P)
+            keep.update(desc=d, work=work, wo=wo, feats=feats, actions=actions, P=P)
         events = []
         for t0, t1 in zip(bounds[:-1], bounds[1:]):
             d.t_begin, d.t_end = int(t0), int(t1)
@@ -1155,22 +1177,27 @@ class Dreamer(nn.Module):
                 events.append(ev)
         return events
 
-    def _imagine_tm(self, start, H1, seed, row_offset=0, chunks=None, actor_h0=None):
+    def _imagine_tm(self, start, H1, seed, row_offset=0, chunks=None, actor_h0=None, feats=None):
         """Dreamer._imagine (dreamer.py:673-692), time-major: feats (H1, N, F), actions (H1, N, A).
         The reference's last img_step (whose output is discarded) is skipped. With `chunks` (step boundaries) returns
-        (feats, actions, events) with one event per chunk (see _imagine_fused)."""
+        (feats, actions, events) with one event per chunk (see _imagine_fused). feats (fused path): a buffer whose
+        feats[0] already holds the start state [stoch | deter] (_ph_forward writes it there)."""
         stoch, deter = start
         N = deter.shape[0]
         SK = self.rssm.flat_stoch
-        feats = torch.empty(H1, N, self.rssm.feat_size, dtype=torch.float32, device=deter.device)
+        preset = feats is not None and self._fused_imag_ok()
+        if not preset:
+            feats = torch.empty(H1, N, self.rssm.feat_size, dtype=torch.float32, device=deter.device)
         actions = torch.empty(H1, N, self.act_dim, dtype=torch.float32, device=deter.device)
-        s = stoch.reshape(N, SK).contiguous()
-        h = deter.contiguous()
+        s = stoch.reshape(N, SK)
+        h = deter
         if self._fused_imag_ok():
-            feats[0, :, :SK] = s
-            feats[0, :, SK:] = h
+            if not preset:
+                feats[0, :, :SK] = s
+                feats[0, :, SK:] = h
             events = self._imagine_fused(feats, actions, H1, seed, row_offset, chunks, actor_h0=actor_h0)
             return (feats, actions, events) if chunks else (feats, actions)
+        s, h = s.contiguous(), h.contiguous()
         for t in range(H1):
             feats[t, :, :SK] = s
             feats[t, :, SK:] = h

@@ -170,7 +170,12 @@ def mlp_layer(x, w, out, bias=None, norm_w=None, part_in=None, part_out=None, ac
     (sd_gemm_bf16x3_mlp): out[b] = act(rms(x[b]) * norm_w[b]) @ w[b]^T + bias[b]. Batched over dim 0 of 3-D operands
     (x may be an expanded (stride-0) view); norm_w None = x taken as is; part_in (n, q, M): the producer's row
     partial sums of squares; part_out (n, N / 64, M) receives this layer's. Returns False when the shape is outside the
-    fused kernel (the caller then takes the unfused path)."""
+    fused kernel (the caller then takes the unfused path).
+    Per-entry form: w (and bias / norm_w) a list of n tensors, entry b's weight (N_b <= out.shape[2], K) row-major
+    and contiguous: several heads' layers in one launch without stacking or zero-padding their weights (columns
+    >= N_b of out[b] get 0)."""
+    if isinstance(w, (list, tuple)):
+        return _mlp_layer_entries(x, list(w), out, bias, norm_w, part_in, part_out, act, alpha)
     if x.dim() == 2:
         x, w, out = x[None], w[None], out[None]
         bias = bias[None] if bias is not None else None
@@ -193,6 +198,45 @@ def mlp_layer(x, w, out, bias=None, norm_w=None, part_in=None, part_out=None, ac
     e = nat.MlpExt()
     if norm_w is not None:
         e.norm_w, e.stride_norm_w = p(norm_w), norm_w.stride(0)
+        e.part_in, e.stride_part_in, e.npart_in = p(part_in), part_in.stride(0), part_in.shape[1]
+        e.act, e.eps = int(act), EPS
+    if part_out is not None:
+        e.part_out, e.stride_part_out = p(part_out), part_out.stride(0)
+    return nat.call_shaped("sd_gemm_bf16x3_mlp", ctypes.byref(d), ctypes.addressof(e), stream())
+
+
+_MLP_MAXB = nat._define(nat.HEADER, "SD_MLP_MAXB")
+
+
+def _mlp_layer_entries(x, ws, out, biases, norm_ws, part_in, part_out, act, alpha):
+    n, M, Kk = x.shape
+    Nn = out.shape[2]
+    if n != len(ws) or n > _MLP_MAXB or tuple(out.shape[:2]) != (n, M):
+        return False
+    _chk(x, out, *ws)
+    if x.stride(2) != 1 or not out.is_contiguous():
+        return False
+    for t in ws + list(biases or []) + list(norm_ws or []):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            return False
+    if any(w.shape[1] != Kk or w.shape[0] > Nn for w in ws):
+        raise ValueError(f"per-entry weights {[tuple(w.shape) for w in ws]} for K {Kk}, N {Nn}")
+    d = nat.GemmDesc()
+    d.A, d.B, d.C, d.bias = p(x), p(ws[0]), p(out), None
+    d.lda, d.ldb, d.ldc = x.stride(1), Kk, Nn
+    d.strideA, d.strideB, d.strideC, d.strideBias = x.stride(0), 0, M * Nn, 0
+    d.M, d.N, d.K, d.batch = M, Nn, Kk, n
+    d.a_kcontig, d.b_kcontig, d.ksplit, d.tile = 1, 1, 1, 0
+    d.alpha, d.beta = float(alpha), 0.0
+    e = nat.MlpExt()
+    for b, w in enumerate(ws):
+        e.w_ptr[b] = p(w)
+        e.w_rows[b] = w.shape[0] if w.shape[0] < Nn else 0
+        if biases is not None:
+            e.bias_ptr[b] = p(biases[b])
+        if norm_ws is not None:
+            e.norm_w_ptr[b] = p(norm_ws[b])
+    if norm_ws is not None:
         e.part_in, e.stride_part_in, e.npart_in = p(part_in), part_in.stride(0), part_in.shape[1]
         e.act, e.eps = int(act), EPS
     if part_out is not None:
@@ -336,11 +380,18 @@ def kl_rows(post, prior, S, K):
 
 def lambda_return(reward, boot, disc, lamb, term=None, cont_logit=None, last=None, boot_row_stride=None,
                   boot_t_stride=1, cont_out=None, weight_out=None):
+    """reward / cont_logit: (N, T) views of any strides (e.g. the transposed view of a time-major (T, N) tensor,
+    read in place); boot: (row, t) strides given explicitly (default (T, 1)); term / last / outputs (N, T) row-major."""
     N, T = reward.shape
     ret = torch.empty(N, T - 1, dtype=torch.float32, device=reward.device)
     brs = T if boot_row_stride is None else boot_row_stride
-    nat.call("sd_lambda_return", p(_c(reward)), p(term), p(cont_logit), p(last), p(boot), int(brs), int(boot_t_stride),
-             p(ret), p(cont_out), p(weight_out), N, T, float(disc), float(lamb), stream())
+    cs = cont_logit.stride() if cont_logit is not None else (T, 1)
+    for t in (term, last, cont_out, weight_out):
+        if t is not None:
+            _c(t)
+    nat.call("sd_lambda_return_strided", p(reward), reward.stride(0), reward.stride(1), p(term), p(cont_logit),
+             cs[0], cs[1], p(last), p(boot), int(brs), int(boot_t_stride), p(ret), p(cont_out), p(weight_out), N, T,
+             float(disc), float(lamb), stream())
     return ret
 
 

@@ -222,17 +222,19 @@ def heads_nograd(heads, x, fast=False, firsts_out=None):
         return [h.logits_nograd(x, fast) for h in heads]
     x = x.reshape(-1, x.shape[-1])
     M, n, U = x.shape[0], len(heads), shape[0]
-    w = torch.stack([f.weight for f in firsts])  # (n, U, F)
-    b = torch.stack([f.bias for f in firsts])  # (n, U)
     h0 = torch.empty(n, M, U, dtype=torch.float32, device=x.device)
     if fast and FUSED_HEADS and U % 64 == 0:
         p0 = torch.empty(n, U // 64, M, dtype=torch.float32, device=x.device)
-        if K.mlp_layer(x.expand(n, M, x.shape[1]), w, h0, bias=b, part_out=p0):
+        # per-entry weights: the heads' parameters are read in place (no stacked copies)
+        if K.mlp_layer(x.expand(n, M, x.shape[1]), [f.weight for f in firsts], h0, bias=[f.bias for f in firsts],
+                       part_out=p0):
             if firsts_out is not None:
                 firsts_out.append(h0)
             out = _heads_rest_fused(heads, h0, p0)
             if out is not None:
                 return out
+    w = torch.stack([f.weight for f in firsts])  # (n, U, F)
+    b = torch.stack([f.bias for f in firsts])  # (n, U)
     K.gemm(x.expand(n, M, x.shape[1]), w.transpose(1, 2), h0, bias=b, fast=fast)
     if firsts_out is not None:
         firsts_out.append(h0)
@@ -243,9 +245,9 @@ def heads_nograd(heads, x, fast=False, firsts_out=None):
 def _heads_rest_fused(heads, h0, p0):
     """Layers 1.. and the output layer of every head after the batched first layer, each a sd_gemm_bf16x3_mlp launch
     batched over the heads that share it: heads with the same depth run their hidden layers together (their
-    activations are consecutive slices of one buffer), and the output layer of a depth group is one launch with the
-    output weights zero-padded to the group's widest head (the continue head's single logit rides with the reward
-    head's 255). Returns None when a shape falls outside the fused kernel."""
+    activations are consecutive slices of one buffer), and the output layer of a depth group is one launch as wide as
+    the group's widest head (the continue head's single logit rides with the reward head's 255; per-entry weight rows,
+    so nothing is stacked or zero-padded). Returns None when a shape falls outside the fused kernel."""
     n, M, U = h0.shape
     dev = h0.device
     depth = [h.mlp.n for h in heads]
@@ -257,9 +259,9 @@ def _heads_rest_fused(heads, h0, p0):
         if pos != list(range(pos[0], pos[0] + len(pos))):
             return None
         sl = slice(pos[0], pos[0] + len(pos))
-        w = torch.stack([heads[i].mlp._mods[layer][0].weight for i in idx])
-        b = torch.stack([heads[i].mlp._mods[layer][0].bias for i in idx])
-        nw = torch.stack([heads[i].mlp._mods[layer - 1][1].weight for i in idx])
+        w = [heads[i].mlp._mods[layer][0].weight for i in idx]
+        b = [heads[i].mlp._mods[layer][0].bias for i in idx]
+        nw = [heads[i].mlp._mods[layer - 1][1].weight for i in idx]
         h = torch.empty(len(idx), M, U, dtype=torch.float32, device=dev)
         pt = torch.empty(len(idx), U // 64, M, dtype=torch.float32, device=dev)
         if not K.mlp_layer(prev_h[sl], w, h, bias=b, norm_w=nw, part_in=prev_p[sl], part_out=pt):
@@ -274,14 +276,10 @@ def _heads_rest_fused(heads, h0, p0):
             return None
         sl = slice(pos[0], pos[0] + len(pos))
         no = max(heads[i].last.weight.shape[0] for i in idx)
-        no_p = max(no, 64)
-        w = torch.zeros(len(idx), no_p, U, dtype=torch.float32, device=dev)
-        b = torch.zeros(len(idx), no_p, dtype=torch.float32, device=dev)
-        for j, i in enumerate(idx):
-            r = heads[i].last.weight.shape[0]
-            w[j, :r] = heads[i].last.weight
-            b[j, :r] = heads[i].last.bias
-        nw = torch.stack([heads[i].mlp._mods[dep - 1][1].weight for i in idx])
+        no_p = max(no, 64)  # the launch's width; a narrower head's columns past its rows come out 0
+        w = [heads[i].last.weight for i in idx]
+        b = [heads[i].last.bias for i in idx]
+        nw = [heads[i].mlp._mods[dep - 1][1].weight for i in idx]
         lg = torch.empty(len(idx), M, no_p, dtype=torch.float32, device=dev)
         if not K.mlp_layer(src_h[sl], w, lg, bias=b, norm_w=nw, part_in=src_p[sl]):
             return None

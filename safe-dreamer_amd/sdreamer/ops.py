@@ -197,6 +197,22 @@ def block_linear(x, wp, b):
 POOL_COMPACT = os.environ.get("SDREAMER_POOL_COMPACT", "1") != "0"
 
 
+class CatIntoFn(torch.autograd.Function):
+    """torch.cat([a, b], -1) written into a caller-owned buffer (holder[0]) and returned with autograd: RSSM.get_feat
+    (rssm.py:211-217) straight into the imagination's start slot, so the start state is never copied again."""
+
+    @staticmethod
+    def forward(ctx, a, b, holder):
+        out = holder[0]
+        torch.cat([a, b], -1, out=out)
+        ctx.split = a.shape[-1]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[..., :ctx.split], g[..., ctx.split:], None
+
+
 class ConvPoolNormFn(torch.autograd.Function):
     """One ConvEncoder stage: Conv2dSamePad -> MaxPool2d(2) -> RMSNorm2D -> SiLU (networks.py:201-216), NHWC.
     Forward on the exact f32 MFMA kernels (the posterior samples depend on it); both backward contractions on the
@@ -355,7 +371,7 @@ class RepvalLossFn(torch.autograd.Function):
 class ImagACLossFn(torch.autograd.Function):
     """Imagined policy and value losses (dreamer.py:623-636, 653-671) in one launch each way (sd_imag_ac_loss_fwd /
     _bwd): rows are the H * N time-major imagined steps; value logits vl (H*N, NB), logpi / ent (H*N) with gradients;
-    ret (N, H), weight (N, H1), val (N, H1), slow (H, N), scale (device scalar) detached. Returns (policy, value, adv):
+    ret (N, H), weight (N, H1), val (H1, N) time-major, slow (H, N), scale (device scalar) detached. Returns (policy, value, adv):
     the two losses (means of the kernel's row terms) and adv (N, H) = (ret - val[:, :H]) / scale (no gradient)."""
 
     @staticmethod

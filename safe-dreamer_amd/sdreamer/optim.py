@@ -76,6 +76,9 @@ class LaProp(torch.optim.Optimizer):
         # (tensor index, device scalar) gating one tensor (DreamerPro's prototype freeze); -1 = none
         self.grad_scale = 1.0
         self.gate = (-1, None)
+        # the fused step zeroes every gradient it reads (sd_agc_laprop_step zero_grads): a graph-replayed update then
+        # needs no zero_grad launch at its start
+        self.zero_grads_after = False
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False, centered=False))
         self.arena = arena if arena is not None else FlatArena(params, params[0].device)
         dev = self.arena.data.device
@@ -105,7 +108,7 @@ class LaProp(torch.optim.Optimizer):
                  K.p(a.chunk_beg), K.p(a.chunk_end), K.p(a.chunk_tensor), K.p(a.tensor_chunk0), a.nchunks,
                  a.ntensors, K.p(self.workspace), K.p(self.scalars), K.p(self.grad_norms), self.agc, self.pmin,
                  self.base_lr, self.warmup, self.betas[0], self.betas[1], self.eps, float(self.grad_scale),
-                 int(self.gate[0]), K.p(self.gate[1]), K.stream())
+                 int(self.gate[0]), K.p(self.gate[1]), int(self.zero_grads_after), K.stream())
 
     def current_lr(self):
         """lr the NEXT step will use (LambdaLR semantics; host-side bookkeeping, no device sync)."""

@@ -187,3 +187,34 @@ def test_wgrad_fused_bias(R, O, I):
     assert ((dw.double().cpu() - ref).abs() <= bound).all()
     dref = db0.double() + dy.double().sum(0)
     assert torch.allclose(db.double().cpu(), dref, rtol=1e-5, atol=1e-4 * float(dy.abs().sum(0).max()) * 1e-2)
+
+
+@pytest.mark.parametrize("rms", [False, True])
+def test_gemm_bf16x3_mlp_entries(rms):
+    """sd_gemm_bf16x3_mlp's per-entry operands (sd_mlp_ext.w_ptr / bias_ptr / norm_w_ptr / w_rows): separate weight
+    tensors of different row counts in one launch, bit-identical to the stacked, zero-padded batch (what
+    networks._heads_rest_fused did before), columns past an entry's rows exactly 0."""
+    from sdreamer import kernels as kern
+    g = torch.Generator().manual_seed(7)
+    M, K, N = 1500, 256, 255
+    rows = [255, 1, 255, 64]
+    n = len(rows)
+    x = (torch.randn(n if rms else 1, M, K, generator=g) * 2).cuda()
+    ws = [(torch.randn(r, K, generator=g) / 16).cuda() for r in rows]
+    bs = [torch.randn(r, generator=g).cuda() for r in rows]
+    nws = [(1 + 0.1 * torch.randn(K, generator=g)).cuda() for _ in rows]
+    pin = torch.stack([(x[:, :, c:c + 64] ** 2).sum(-1) for c in range(0, K, 64)], 1).contiguous() if rms else None
+    xd = x if rms else x.expand(n, M, K)
+    wst = torch.zeros(n, N, K, device="cuda")
+    bst = torch.zeros(n, N, device="cuda")
+    for j, (w, b) in enumerate(zip(ws, bs)):
+        wst[j, :w.shape[0]] = w
+        bst[j, :w.shape[0]] = b
+    ref = torch.empty(n, M, N, device="cuda")
+    got = torch.full((n, M, N), float("nan"), device="cuda")
+    kw = dict(part_in=pin) if rms else {}
+    assert kern.mlp_layer(xd, wst, ref, bias=bst, norm_w=torch.stack(nws) if rms else None, **kw)
+    assert kern.mlp_layer(xd, ws, got, bias=bs, norm_w=nws if rms else None, **kw)
+    assert torch.equal(got, ref)
+    for j, r in enumerate(rows):
+        assert not got[j, :, r:].any()

@@ -313,6 +313,15 @@ def test_lambda_return_and_ema():
     ret = K.lambda_return(rew.to(DEV), val.to(DEV), disc, 0.95, cont_logit=cl.to(DEV), cont_out=co, weight_out=wo)
     close(ret, ref, 1e-5, "ret")
     close(wo, wref, 1e-6, "weight")
+    # time-major inputs read in place (sd_lambda_return_strided: the imagined heads' (T, N) outputs, the continue
+    # logit a strided column of a wider logit matrix): bit-identical to the row-major call
+    rew_tm, val_tm = rew.t().contiguous().to(DEV), val.t().contiguous().to(DEV)
+    wide = torch.zeros(T * N, 3, device=DEV)
+    wide[:, 1] = cl.t().reshape(-1).to(DEV)
+    co2, wo2 = torch.empty(N, T, device=DEV), torch.empty(N, T, device=DEV)
+    ret2 = K.lambda_return(rew_tm.t(), val_tm, disc, 0.95, cont_logit=wide[:, 1].view(T, N).t(), cont_out=co2,
+                           weight_out=wo2, boot_row_stride=1, boot_t_stride=N)
+    assert torch.equal(ret2, ret) and torch.equal(wo2, wo) and torch.equal(co2, co)
     ema = torch.tensor([0.3, 2.0])
     ema_d = ema.to(DEV)
     os_ = torch.empty(2, device=DEV)
@@ -392,7 +401,7 @@ def test_imag_ac_loss_fused():
     (2.0 * pol + 0.5 * vlos).backward()
     vd, ld, ed = (t.to(DEV).requires_grad_() for t in (vl, logpi, ent))
     p_, v_, a_ = ops.ImagACLossFn.apply(vd, ld, ed, bins.to(DEV), ret.to(DEV), slow.to(DEV), weight.to(DEV),
-                                        val.to(DEV), scale.to(DEV), coef)
+                                        val.t().contiguous().to(DEV), scale.to(DEV), coef)  # values time-major
     close(p_, pol, 1e-5, "policy")
     close(v_, vlos, 1e-5, "value")
     close(a_, adv, 1e-6, "adv")
@@ -518,6 +527,16 @@ def test_laprop_grad_scale_and_gate():
     gated = run(1.0, 0.0, 1.0, False)
     zeroed = run(1.0, None, 1.0, True)
     assert all(torch.equal(a, b) for a, b in zip(gated, zeroed))
+    # zero_grads_after (graph-replayed updates: zero_grad folded into the step): the same parameters, every gradient 0
+    params = [torch.nn.Parameter(p.clone().to(DEV)) for p in p0]
+    opt = LaProp(params, lr=4e-5, warmup=0)
+    opt.zero_grads_after = True
+    for it in range(2):
+        for i, g in enumerate(g0):
+            params[i].grad.add_(g.to(DEV) * (it + 1))  # accumulates onto the zeros the previous step left
+        opt.step()
+    assert all(torch.equal(a.detach().cpu(), b) for a, b in zip(params, ref))
+    assert not opt.arena.grad.any()
 
 
 def test_polyak():
