@@ -371,10 +371,22 @@ typedef struct sd_rssm_scan {
   /* saved activations (written by fwd, read by bwd) */
   float *s_in, *h_in, *x0p, *x1p, *r0, *r1, *xcat, *hp, *hh, *rh, *gates, *deter, *op, *oo, *ro, *logit, *stoch;
   /* backward */
-  const float *d_stoch, *d_deter, *d_logit;  /* (T,B,SK) (T,B,D) (T,B,SK) incoming grads; each may be NULL */
+  const float *d_stoch, *d_deter, *d_logit;  /* (T,B,SK) (T,B,D) (T,B,SK) incoming grads (bm_grads: (B,T,.)); each
+                                                may be NULL */
   float* dl;                       /* out (T,B,SK): total d logit (incl. the straight-through sample gradient) */
   float *d_o, *d_op, *d_gates, *d_hh, *d_hp, *d_xcat, *d_x0p, *d_x1p;  /* (T,B,.) */
   float* work;                     /* >= sd_rssm_scan_work_floats(d) floats */
+  /* optional forward layout (0 / NULL: the layouts above) */
+  int bm_inputs;                   /* x2 / eproj batch-major (B,T,U), computed on the caller's batch-major rows */
+  long ld_wod;                     /* row stride of WoD: the full obs_net_0 weight (U, D+E) read in place; 0 = D */
+  float *post_stoch, *post_deter, *post_logit;  /* (B,T,.) batch-major copies of stoch / deter / logit (RSSM.observe's
+                                                   outputs, rssm.py:140-156); stoch may then be NULL */
+  /* optional backward layout: bm_grads = d_stoch / d_deter / d_logit batch-major (B,T,.), plus second summands
+     d_stoch2 / d_deter2 (batch-major rows b*T + t with row stride ld_g2, e.g. the two halves of a (B,T,SK+D) feat
+     gradient; each may be NULL): the posterior gradient d_stoch + d_stoch2 is formed where it is read */
+  int bm_grads;
+  const float *d_stoch2, *d_deter2;
+  long ld_g2;
 } sd_rssm_scan;
 int sd_rssm_scan_work_floats(const sd_rssm_scan* d);
 int sd_rssm_scan_fwd(const sd_rssm_scan* d, sd_stream stream);

@@ -259,6 +259,12 @@ __global__ void k_init(sd_rssm_scan d) {
 
 // hp[t] = BlockLinear(dyn_hid_0)([h_g | x0 | x1 | x2]) + bh, with x0 = silu(rms(x0p)), x1 = silu(rms(x1p)) built
 // in the prologue (rssm.py:52-63). grid (D/16); also the per-tile row sums of hp^2 for the next norm.
+// row (t, b) of the hoisted per-step inputs x2 / eproj: time-major (T, B, U), or batch-major (B, T, U) when
+// d.bm_inputs (computed on the batch-major rows, no transpose)
+SD_DEV long in_row(const sd_rssm_scan& d, int t, int b) {
+  return d.bm_inputs ? (long)b * d.T + t : (long)t * d.B + b;
+}
+
 template <int CPW, int NG>
 __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
@@ -275,7 +281,7 @@ __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   ld_row(h, d.h_in + (long)t * B * D + (long)row * D + (long)g * Dg, Dg, rv, t32);
   ld_slabs<NU, KSM>(x0, w.x0s + (long)row * UH, (long)B * UH, d.ks_d, UH, rv, t32);
   ld_slabs<NU, KSM>(x1, w.x1s + (long)row * UH, (long)B * UH, d.ks_s, UH, rv, t32);
-  ld_row(x2v, d.x2 + tBU + (long)row * UH, UH, rv, t32);
+  ld_row(x2v, d.x2 + in_row(d, t, row) * UH, UH, rv, t32);
   ld_row(b0v, d.b0, UH, true, t32);
   ld_row(b1v, d.b1, UH, true, t32);
   ld_row(n0v, d.n0, UH, true, t32);
@@ -379,6 +385,7 @@ __global__ __launch_bounds__(NTHR) void k_gate(sd_rssm_scan d, Work w, int t) {
     const float u = sigmoidf_(ua - 1.f);
     const float out = u * cc + (1.f - u) * hprev;
     d.deter[(long)t * B * D + (long)er * D + col] = out;
+    if (d.post_deter) d.post_deter[((long)er * d.T + t) * D + col] = out;  // batch-major copy (RSSM.observe's output)
     if (t + 1 < d.T) d.h_in[(long)(t + 1) * B * D + (long)er * D + col] = rnext ? 0.f : out;
   }
 }
@@ -402,7 +409,7 @@ __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
   const long tBU = (long)t * B * UH;
   f32x4 x[NU], e[NU], nv[NU];
   ld_slabs<NU, KSM>(x, w.ops + (long)row * UH, (long)B * UH, d.ks_d, UH, rv, t32);
-  ld_row(e, d.eproj + tBU + (long)row * UH, UH, rv, t32);
+  ld_row(e, d.eproj + in_row(d, t, row) * UH, UH, rv, t32);
   ld_row(nv, d.no, UH, true, t32);
   // sampler operands + noise, independent of the contraction
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
@@ -444,7 +451,12 @@ __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
         const float yv = ((lt == idx ? 1.f : 0.f) - ys) + ys;
         const long o = (long)t * B * SK + (long)er * SK + n0 + lt;
         d.logit[o] = l;
-        d.stoch[o] = yv;
+        if (d.stoch) d.stoch[o] = yv;
+        if (d.post_logit) {  // batch-major copies (RSSM.observe's outputs)
+          const long ob = ((long)er * d.T + t) * SK + n0 + lt;
+          d.post_logit[ob] = l;
+          d.post_stoch[ob] = yv;
+        }
         if (t + 1 < d.T) d.s_in[o + (long)B * SK] = rnext[k] ? 0.f : yv;
       }
     }
@@ -464,6 +476,15 @@ SD_DEV float sampler_bwd(float l, float gn, float ds, float unimix, int lt) {
   return unimix_backward<KD>(ys * (ds - sd), p, pp, nl, true, unimix);
 }
 
+// incoming gradient of posterior element (t, row, col) of a width-W output: time-major, or batch-major (bm_grads) plus
+// an optional second summand g2 (rows of ld_g2 floats), summed as g + g2 (the caller's former torch.add order)
+SD_DEV float in_grad(const sd_rssm_scan& d, const float* g, const float* g2, int t, int row, int col, int W) {
+  if (!d.bm_grads) return g ? g[((long)t * d.B + row) * W + col] : 0.f;
+  const long r = (long)row * d.T + t;
+  const float a = g ? g[r * W + col] : 0.f;
+  return g2 ? a + g2[r * d.ld_g2 + col] : a;
+}
+
 // dl[T-1] = d_logit + sampler backward (no carry yet). Elementwise, teams of KD lanes.
 template <int KD>
 __global__ __launch_bounds__(256) void k_sbwd_last(sd_rssm_scan d) {
@@ -475,9 +496,9 @@ __global__ __launch_bounds__(256) void k_sbwd_last(sd_rssm_scan d) {
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
   const float l = v ? d.logit[o] : 0.f;
   const float gn = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)t, (uint64_t)((long)row * S + s + d.group_offset) * KD + lt);
-  const float ds = v && d.d_stoch ? d.d_stoch[o] : 0.f;
+  const float ds = v ? in_grad(d, d.d_stoch, d.d_stoch2, t, row, k, SK) : 0.f;
   const float dl = sampler_bwd<KD>(l, gn, ds, d.unimix, lt);
-  if (v) d.dl[o] = (d.d_logit ? d.d_logit[o] : 0.f) + dl;
+  if (v) d.dl[o] = in_grad(d, d.d_logit, nullptr, t, row, k, SK) + dl;
 }
 
 // d_o = dl[t] . Wl   (dl built by the previous launch). grid (U/16)
@@ -529,7 +550,7 @@ __global__ __launch_bounds__(NTHR) void k_dgru(sd_rssm_scan d, Work w, int t) {
   const long gb = (long)t * B * 3 * D + (long)er * 3 * D + (long)g * 3 * Dg;
   float dh0 = 0.f, ra = 0.f, ca = 0.f, ua = 0.f, hv = 0.f;
   if (ev) {
-    dh0 = (d.d_deter ? d.d_deter[od] : 0.f) + w.ch[(long)er * D + col];
+    dh0 = in_grad(d, d.d_deter, d.d_deter2, t, er, col, D) + w.ch[(long)er * D + col];
     ra = d.gates[gb + j];
     ca = d.gates[gb + Dg + j];
     ua = d.gates[gb + 2 * Dg + j];
@@ -736,8 +757,8 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
       const long o = (long)tp * B * SK + (long)er * SK + n0 + lt;
       if (ev) {
         e0[k] = d.logit[o];
-        e1[k] = d.d_stoch ? d.d_stoch[o] : 0.f;
-        e2[k] = d.d_logit ? d.d_logit[o] : 0.f;
+        e1[k] = in_grad(d, d.d_stoch, d.d_stoch2, tp, er, n0 + lt, SK);
+        e2[k] = in_grad(d, d.d_logit, nullptr, tp, er, n0 + lt, SK);
       }
       gn[k] = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)tp,
                         (uint64_t)((long)er * S + n0 / KD + d.group_offset) * KD + lt);
@@ -811,6 +832,9 @@ int check(const sd_rssm_scan* d) {
       d->SK % (d->ks_s * 16))
     return SD_ESHAPE;
   if (!d->work) return SD_EARG;
+  if (d->ld_wod < 0 || (d->ld_wod > 0 && (d->ld_wod < d->D || d->ld_wod % 4))) return SD_EARG;
+  if ((d->post_logit != nullptr) != (d->post_stoch != nullptr)) return SD_EARG;
+  if ((d->d_stoch2 || d->d_deter2) && (!d->bm_grads || d->ld_g2 < 1)) return SD_EARG;
   return SD_OK;
 }
 
@@ -831,6 +855,7 @@ extern "C" int sd_rssm_scan_work_floats(const sd_rssm_scan* d) {
 extern "C" int sd_rssm_scan_fwd(const sd_rssm_scan* dp, sd_stream stream_) {
   int rc = check(dp);
   if (rc) return rc;
+  if (!dp->stoch && !dp->post_stoch) return SD_EARG;  // the sample goes somewhere
   hipStream_t st = (hipStream_t)stream_;
   const sd_rssm_scan& d = *dp;
   const Work w = work_layout(d, d.work);
@@ -842,6 +867,7 @@ extern "C" int sd_rssm_scan_fwd(const sd_rssm_scan* dp, sd_stream stream_) {
   const size_t lds_hid = core1 + (size_t)MR * (Ig + 4) * 4;
   const size_t lds_gate = core_lds_floats<3>() * 4 + (size_t)MR * (Dg + 4) * 4;
   const long BD = (long)B * D, BS = (long)B * SK;
+  const long wod_ld = d.ld_wod > 0 ? d.ld_wod : D;
 
   k_init<<<64, 256, 0, st>>>(d);
   SD_LAUNCH_CHECK();
@@ -863,7 +889,7 @@ extern "C" int sd_rssm_scan_fwd(const sd_rssm_scan* dp, sd_stream stream_) {
                  k_gate<NG, NG><<<D / 16, NTHR, lds_gate, st>>>(d, w, t));
     SD_LAUNCH_CHECK();
     {
-      SlabProb po{d.deter + t * BD, D, d.WoD, D, w.ops, nullptr};
+      SlabProb po{d.deter + t * BD, D, d.WoD, wod_ld, w.ops, nullptr};
       SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset + (t + 1) * B};
       const int np = t + 1 < d.T ? 2 : 1;
       SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, np), NTHR, core1, st>>>(po, px, B, UH, span_d));
@@ -898,6 +924,7 @@ extern "C" int sd_rssm_scan_step_kernel(const sd_rssm_scan* dp, int which, int t
   const size_t lds_hid = core1 + (size_t)MR * (Ig + 4) * 4;
   const size_t lds_gate = core_lds_floats<3>() * 4 + (size_t)MR * (Dg + 4) * 4;
   const long BD = (long)B * D, BS = (long)B * SK;
+  const long wod_ld = d.ld_wod > 0 ? d.ld_wod : D;
   if (which == 0) {
     SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr};
     SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(UH / 16, d.ks_s, 1), NTHR, core1, st>>>(p, p, B, UH, span_s));
@@ -908,7 +935,7 @@ extern "C" int sd_rssm_scan_step_kernel(const sd_rssm_scan* dp, int which, int t
     SD_NG_SWITCH(Dg, if (!(raise_lds<k_gate<NG, NG>>(lds_gate))) return SD_EARG;
                  k_gate<NG, NG><<<D / 16, NTHR, lds_gate, st>>>(d, w, t));
   } else if (which == 3) {
-    SlabProb po{d.deter + t * BD, D, d.WoD, D, w.ops, nullptr};
+    SlabProb po{d.deter + t * BD, D, d.WoD, wod_ld, w.ops, nullptr};
     SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset + (t + 1) * B};
     const int np = t + 1 < d.T ? 2 : 1;
     SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, np), NTHR, core1, st>>>(po, px, B, UH, span_d));

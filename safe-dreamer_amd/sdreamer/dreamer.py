@@ -815,15 +815,15 @@ class Dreamer(nn.Module):
         self._mark("repval_wait")
         g_feat = st["feat_r"].grad
         lg = [l.grad if l.grad is not None else torch.zeros_like(l) for l in leaves]
-        # summed straight into the scan's time-major layout (one kernel each; the scan backward's own transposes of
-        # these two gradients become no-ops): (B, T, .) views of (T, B, .) storage
-        B, T = g_feat.shape[:2]
-        gs = torch.empty(T, B, SK, dtype=g_feat.dtype, device=g_feat.device)
-        torch.add(lg[0].reshape(B, T, SK).transpose(0, 1), g_feat[..., :SK].transpose(0, 1), out=gs)
-        gd = torch.empty(T, B, g_feat.shape[-1] - SK, dtype=g_feat.dtype, device=g_feat.device)
-        torch.add(lg[1].transpose(0, 1), g_feat[..., SK:].transpose(0, 1), out=gd)
-        g_stoch = gs.transpose(0, 1).reshape(leaves[0].shape)
-        g_deter = gd.transpose(0, 1)
+        # the posterior gradient is leaf gradient + replay-value feat gradient: the feat gradient's halves go to the
+        # scan backward as second summands (RSSM._bwd_extra), added where the scan reads them (no add launches)
+        g_stoch, g_deter = lg[0], lg[1]
+        if g_feat is not None:
+            if self.rssm.takes_extra_grads(g_feat.shape[0]):
+                self.rssm._bwd_extra = (g_feat[..., :SK], g_feat[..., SK:])
+            else:  # 16-row scan chunks (B > 16): each chunk's backward sees its slice of the summed gradient
+                g_stoch = lg[0] + g_feat[..., :SK].reshape(lg[0].shape)
+                g_deter = lg[1] + g_feat[..., SK:]
         st["scan_wgrads"] = []
         if defer:
             with ops.defer_wgrads(st["scan_wgrads"]):

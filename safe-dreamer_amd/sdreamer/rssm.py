@@ -97,6 +97,7 @@ class RSSM(nn.Module):
         self._discrete = int(config.discrete)
         self._unimix_ratio = float(config.unimix_ratio)
         self._bwd_tr = None  # scan_bwd_weights() computed ahead of the scan backward (Dreamer._ph_wm), or None
+        self._bwd_extra = None  # (d_stoch2, d_deter2): second posterior-gradient summands for the next backward
         self._initial = str(config.initial)
         self._device = torch.device(config.device)
         self._act_dim = int(act_dim)
@@ -161,6 +162,10 @@ class RSSM(nn.Module):
         deter = torch.zeros(batch_size, self._deter, dtype=torch.float32, device=self._device)
         stoch = torch.zeros(batch_size, self._stoch, self._discrete, dtype=torch.float32, device=self._device)
         return stoch, deter
+
+    def takes_extra_grads(self, B):
+        """observe() on B rows is one ObserveScan (not 16-row chunks), so its backward can take _bwd_extra"""
+        return not (B > 16 and _fused_scan_ok(self, 16))
 
     def get_feat(self, stoch, deter):  # rssm.py:211-217
         return torch.cat([stoch.reshape(*stoch.shape[:-2], self.flat_stoch), deter], -1)
@@ -299,15 +304,20 @@ class ObserveScan(torch.autograd.Function):
         f32 = torch.float32
         M = T * B
         rt = reset.t().contiguous()  # (T, B) uint8
-        # ---- hoisted, recurrence-free work over all T*B rows
-        act_t = action.transpose(0, 1).reshape(M, A).contiguous()
-        a_n = K.action_norm(K.mask_rows(act_t, rt.reshape(M)))
+        fused = _fused_scan_ok(rssm, B)
+        # ---- hoisted, recurrence-free work over all T*B rows. Fused scan: on the batch-major rows b*T + t, read by
+        # the scan in place (bm_inputs); per-op path: time-major rows. The (M, E) embedding is never transposed
+        # (emb_t: batch-major rows, see _wgrads).
+        emb_t = embed.detach().reshape(M, E)
+        if fused:
+            a_n = K.action_norm(K.mask_rows(action.reshape(M, A).contiguous(), reset.reshape(M).contiguous()))
+            eproj = K.linear(emb_t, P["Wo"][:, D:], P["bo"])
+        else:
+            act_t = action.transpose(0, 1).reshape(M, A).contiguous()
+            a_n = K.action_norm(K.mask_rows(act_t, rt.reshape(M)))
+            eproj = K.linear(emb_t, P["Wo"][:, D:], P["bo"]).view(B, T, U).transpose(0, 1).reshape(M, U).contiguous()
         x2p = K.linear(a_n, P["W2"], P["b2"])
         x2, r2 = K.rmsnorm_fwd(x2p, P["n2"])
-        # embed half of obs_net_0 + bias on the batch-major rows, then the (M, U) result is made time-major: the
-        # (M, E) embedding itself is never transposed (emb_t: batch-major rows b*T + t, see _wgrads)
-        emb_t = embed.detach().reshape(M, E)
-        eproj = K.linear(emb_t, P["Wo"][:, D:], P["bo"]).view(B, T, U).transpose(0, 1).reshape(M, U).contiguous()
         # ---- per-step buffers (time-major)
         s_in = torch.empty(T, B, SK, dtype=f32, device=dev)
         h_in = torch.empty(T, B, D, dtype=f32, device=dev)
@@ -325,26 +335,31 @@ class ObserveScan(torch.autograd.Function):
         oo = torch.empty(T, B, U, dtype=f32, device=dev)
         ro = torch.empty(T, B, dtype=f32, device=dev)
         logit = torch.empty(T, B, SK, dtype=f32, device=dev)
-        stoch = torch.empty(T, B, SK, dtype=f32, device=dev)
-        fused = _fused_scan_ok(rssm, B)
         if fused:
-            WoD = P["Wo"][:, :D].contiguous()
+            # the posterior outputs written batch-major by the scan itself (the time-major deter / logit stay the
+            # backward's saved activations); obs_net_0's deter half read in place from the full weight
+            post = (torch.empty(B, T, S, Kd, dtype=f32, device=dev), torch.empty(B, T, D, dtype=f32, device=dev),
+                    torch.empty(B, T, S, Kd, dtype=f32, device=dev))
+            Wo = P["Wo"]
             d = _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, None, stream_id)
+            d.bm_inputs, d.ld_wod = 1, Wo.stride(0)
             work = torch.empty(_scan_work(d), dtype=f32, device=dev)
-            d.work, d.WoD = work.data_ptr(), WoD.data_ptr()
+            d.work, d.WoD = work.data_ptr(), Wo.data_ptr()
             d.stoch0, d.deter0 = stoch0.data_ptr(), deter0.data_ptr()
+            op = torch.empty(T, B, U, dtype=f32, device=dev)  # eproj stays the (embed half + bias) input
             for k, v in (("s_in", s_in), ("h_in", h_in), ("x0p", x0p), ("x1p", x1p), ("r0", r0), ("r1", r1),
                          ("xcat", xcat), ("hp", hp), ("hh", hh), ("rh", rh), ("gates", gates), ("deter", deter),
-                         ("op", op), ("oo", oo), ("ro", ro), ("logit", logit), ("stoch", stoch)):
+                         ("op", op), ("oo", oo), ("ro", ro), ("logit", logit), ("post_stoch", post[0]),
+                         ("post_deter", post[1]), ("post_logit", post[2])):
                 setattr(d, k, v.data_ptr())
-            op = torch.empty(T, B, U, dtype=f32, device=dev)  # eproj stays the (embed half + bias) input
-            d.op = op.data_ptr()
+            d.stoch = None
             nat.call("sd_rssm_scan_fwd", ctypes.addressof(d), K.stream())
             if SCAN_KEEP is not None:  # measurement aid (bench.py): the descriptor and every buffer it points to
-                SCAN_KEEP.update(desc=d, work=work, WoD=WoD, bufs=(s_in, h_in, x0p, x1p, r0, r1, xcat, hp, hh, rh,
-                                                                   gates, deter, op, oo, ro, logit, stoch, x2, eproj,
-                                                                   rt, stoch0, deter0), T=T, B=B)
+                SCAN_KEEP.update(desc=d, work=work, WoD=Wo, bufs=(s_in, h_in, x0p, x1p, r0, r1, xcat, hp, hh, rh,
+                                                                  gates, deter, op, oo, ro, logit, x2, eproj, rt,
+                                                                  stoch0, deter0) + post, T=T, B=B)
         else:
+            stoch = torch.empty(T, B, SK, dtype=f32, device=dev)
             xcat[:, :, 2 * U:] = x2.view(T, B, U)
         prev_s, prev_h = stoch0, deter0
         for t in (range(0) if fused else range(T)):
@@ -374,6 +389,7 @@ class ObserveScan(torch.autograd.Function):
         ctx.fused = fused
         if fused:
             ctx.x2 = x2
+            return post
         post_stoch = stoch.transpose(0, 1).reshape(B, T, S, Kd).contiguous()
         post_deter = deter.transpose(0, 1).contiguous()
         post_logit = logit.transpose(0, 1).reshape(B, T, S, Kd).contiguous()
@@ -398,11 +414,17 @@ class ObserveScan(torch.autograd.Function):
             return x.reshape(B, T, width).transpose(0, 1).contiguous()
 
         gb = ops.grad_buf
+        # second summands of the posterior gradient handed over by the caller (Dreamer._ph_scan_bwd: the replay-value
+        # feat gradient's stoch / deter halves), summed where the scan reads them
+        extra, rssm._bwd_extra = rssm._bwd_extra, None
         if ctx.fused:
             dl_all, d_op, d_gates, d_hp, d_x0p, d_x1p, norm_w = ObserveScan._bwd_fused(
-                ctx, d_stoch, d_deter, d_logit, rt, s_in, h_in, x0p, x1p, r0, r1, hp, rh, gates, op, ro, logit)
+                ctx, d_stoch, d_deter, d_logit, rt, s_in, h_in, x0p, x1p, r0, r1, hp, rh, gates, op, ro, logit, extra)
             return ObserveScan._wgrads(ctx, P, rt, a_n, x2p, r2, emb_t, s_in, h_in, xcat, hh, deter, oo, dl_all,
                                        d_op, d_gates, d_hp, d_x0p, d_x1p, None, norm_w)
+        if extra is not None:
+            d_stoch = extra[0].reshape(B, T, SK) + (0 if d_stoch is None else d_stoch.reshape(B, T, SK))
+            d_deter = extra[1] + (0 if d_deter is None else d_deter)
         ds_out = tm(d_stoch, SK)
         dd_out = tm(d_deter, D)
         dl_all = tm(d_logit, SK)  # becomes d logit (incl. the straight-through sample gradient) in place
@@ -441,7 +463,8 @@ class ObserveScan(torch.autograd.Function):
                                    d_gates, d_hp, d_x0p, d_x1p, d_x2)
 
     @staticmethod
-    def _bwd_fused(ctx, d_stoch, d_deter, d_logit, rt, s_in, h_in, x0p, x1p, r0, r1, hp, rh, gates, op, ro, logit):
+    def _bwd_fused(ctx, d_stoch, d_deter, d_logit, rt, s_in, h_in, x0p, x1p, r0, r1, hp, rh, gates, op, ro, logit,
+                   extra=None):
         """Serial part of the backward as sd_rssm_scan_bwd (6 fused launches per step) + the RMSNorm weight
         gradients of the four in-loop norms as (T*B)-row reductions."""
         rssm = ctx.rssm
@@ -453,10 +476,10 @@ class ObserveScan(torch.autograd.Function):
         dev = logit.device
         f32 = torch.float32
 
-        def tm(x, width):
-            return None if x is None else x.reshape(B, T, width).transpose(0, 1).contiguous()
+        def bm(x, width):  # the incoming gradients are read batch-major in place (bm_grads)
+            return None if x is None else x.reshape(B, T, width).contiguous()
 
-        ds_out, dd_out, dl_in = tm(d_stoch, SK), tm(d_deter, D), tm(d_logit, SK)
+        ds_out, dd_out, dl_in = bm(d_stoch, SK), bm(d_deter, D), bm(d_logit, SK)
         e = lambda *shape: (torch.full(shape, float("nan"), dtype=f32, device=dev) if _POISON  # noqa: E731
                             else torch.empty(*shape, dtype=f32, device=dev))
         dl, d_o, d_op, d_x0p, d_x1p = e(T, B, SK), e(T, B, U), e(T, B, U), e(T, B, U), e(T, B, U)
@@ -473,6 +496,12 @@ class ObserveScan(torch.autograd.Function):
                                          ("d_xcat", d_xcat), ("d_x0p", d_x0p), ("d_x1p", d_x1p)]:
             setattr(d, k, v.data_ptr())
         d.d_stoch, d.d_deter, d.d_logit = K.p(ds_out), K.p(dd_out), K.p(dl_in)
+        d.bm_grads = 1
+        if extra is not None:
+            gs2, gd2 = extra
+            if gs2.stride(-1) != 1 or gd2.stride(-1) != 1 or gs2.stride(-2) != gd2.stride(-2):
+                raise ValueError("posterior gradient halves need unit column stride and one row stride")
+            d.d_stoch2, d.d_deter2, d.ld_g2 = gs2.data_ptr(), gd2.data_ptr(), gs2.stride(-2)
         nat.call("sd_rssm_scan_bwd", ctypes.addressof(d), K.stream())
         gb = ops.grad_buf
         f = lambda x: x.reshape(M, -1)  # noqa: E731
@@ -484,7 +513,8 @@ class ObserveScan(torch.autograd.Function):
             K.rmsnorm_bwd(f(hp), P["nh"], rh.reshape(M), f(d_hh), dw=gb(P["nh"]))
             K.rmsnorm_bwd(f(x0p), P["n0"], r0.reshape(M), f(d_xcat)[:, :U].contiguous(), dw=gb(P["n0"]))
             K.rmsnorm_bwd(f(x1p), P["n1"], r1.reshape(M), f(d_xcat)[:, U:2 * U].contiguous(), dw=gb(P["n1"]))
-            return d_xcat[:, :, 2 * U:].contiguous()
+            # the action branch ran on batch-major rows (ObserveScan.forward, fused path)
+            return d_xcat[:, :, 2 * U:].transpose(0, 1).contiguous()
 
         norm_w.tensors = (op, hp, x0p, x1p, ro, rh, r0, r1, d_o, d_hh, d_xcat)
         return dl, d_op, d_gates, d_hp, d_x0p, d_x1p, norm_w
