@@ -31,6 +31,9 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "imagined latent steps/sec at B16\u00b7L64\u00b7H15, 1/2/4/8 MI355X; WM-loss \u0394 vs ref"  # BASELINE.json
 PEAK_FP32_MFMA = 157.3  # TFLOP/s, MI355X_MICROARCH.md (dense f32 matrix = f32 vector peak)
 PEAK_HBM = 8000.0  # GB/s spec
+# split-bf16 ("bf16x3") kernels: three v_mfma_f32_16x16x32_bf16 per f32-equivalent product, so their f32-equivalent
+# peak is the dense bf16 MFMA peak (2.5 PFLOP/s, MI355X_MICROARCH.md) / 3
+PEAK_BF16X3 = 2500.0 / 3
 
 
 class _Sp:
@@ -320,9 +323,9 @@ def probe_specs(agent, cfg, K):
     ksd, kss = 4, 2
     out = []
 
-    def add(key, name, grid, bound, work, algo, label, how, launches):
+    def add(key, name, grid, bound, work, algo, label, how, launches, peak=None):
         out.append(dict(key=key, name=name, grid=list(grid), bound=bound, work=work, algo=algo, label=label, how=how,
-                        launches=launches))
+                        launches=launches, peak=peak))
 
     # encoder stage 2 forward (conv + pool + RMSNorm + SiLU, direct conv from an LDS patch)
     cp = dominant_probe(K)
@@ -330,14 +333,26 @@ def probe_specs(agent, cfg, K):
         pix = N * 32 * 32
         add("conv_stage2", "conv_fwd_direct_pool<48, 32, 5, 5, 1>", (N * 32 * 32 // 128, 1, 1), "mfma",
             2.0 * pix * 48 * 25 * 32, 4.0 * pix * 32 + N * 16 * 16 * (48 * 9 + 4), cp.label, ("launch", cp), 1)
-    # imagined heads' first layers: one split-bf16 GEMM, A = the imagined feats broadcast over 4 weights
+    # encoder stage 2 bwd-data (split-bf16 implicit GEMM over the flipped weight): sd_conv2d_dgrad_bf16x3(dout, wflip,
+    # din, Nb, Hs, Ws, Ci = dout channels, Co = din channels, kh, kw, pad, stream)
+    dg = K.LaunchProbe("sd_conv2d_dgrad_bf16x3", lambda a: a[6] == 48 and a[7] == 32,
+                       lambda a: 2.0 * a[3] * a[4] * a[5] * a[6] * a[7] * a[8] * a[9],
+                       label="conv_dgrad3<32> (encoder stage 2 bwd-data: dOut 48 ch -> dIn 32 ch at 32x32, 5x5 flipped "
+                             "weight; implicit GEMM, operands split to bf16 (hi, lo) in LDS, 3 v_mfma_f32_16x16x32_bf16 "
+                             "per f32-equivalent product)")
+    pix = N * 32 * 32
+    add("conv_stage2_dgrad", "conv_dgrad3<32>", (pix // 128, 1, 1), "mfma", 2.0 * pix * 48 * 25 * 32,
+        4.0 * (pix * 48 + pix * 32 + 25 * 48 * 32), dg.label, ("launch", dg), 1, peak=PEAK_BF16X3)
+    # imagined heads' first layers: one split-bf16 MLP-layer launch, A = the imagined feats broadcast over 4 weights
     M = N * (H + 1)
-    hp = K.LaunchProbe("sd_gemm_bf16x3", lambda a: a[0]._obj.batch == 4 and a[0]._obj.strideA == 0,
+    hp = K.LaunchProbe("sd_gemm_bf16x3_mlp", lambda a: a[0]._obj.batch == 4 and a[0]._obj.strideA == 0,
                        lambda a: 2.0 * a[0]._obj.M * a[0]._obj.N * a[0]._obj.K * a[0]._obj.batch,
-                       label="gemm3_kernel<128, 128> (imagined reward / continue / value / slow-value first layers: "
-                             "(M, F) x 4 (F, U) split-bf16, 3 bf16 MFMAs per f32-equivalent product)")
-    add("heads_l0", "gemm3_kernel<128, 128", (U // 128, M // 128, 4), "mfma",
-        2.0 * M * F * U * 4, 4.0 * (M * F + 4 * F * U + 4 * M * U), hp.label, ("launch", hp), 1)
+                       label="gemm3_mlp_kernel (imagined reward / continue / value / slow-value first layers: "
+                             "(M, F) x 4 (F, U) split-bf16, per-entry weights, row partials for the next layer's "
+                             "RMSNorm; 3 bf16 MFMAs per f32-equivalent product)")
+    add("heads_l0", "gemm3_mlp_kernel<false, true>", (U // 128, M // 128, 4), "mfma",
+        2.0 * M * F * U * 4, 4.0 * (M * F + 4 * F * U + 4 * M * U + 4 * (U // 64) * M), hp.label, ("launch", hp), 1,
+        peak=PEAK_BF16X3)
     # imagination step kernels
     imag = [("imag_k_lin", "k_lin<32, 32>", (U // 32, N // 32, 3), 3 * 2.0 * N * D * U,
              4.0 * (N * D + 3 * U * D + 3 * N * U + 2 * (U // 16) * N), IMAG_LABELS[0], 0),
@@ -398,7 +413,7 @@ def roofline_entries(specs, agent, cfg, table):
             if not scan.ok:
                 continue
             avg_us = scan.time(sp["how"][1])
-        peak = PEAK_FP32_MFMA if sp["bound"] == "mfma" else PEAK_HBM
+        peak = sp["peak"] or (PEAK_FP32_MFMA if sp["bound"] == "mfma" else PEAK_HBM)
         unit = "TFLOP/s" if sp["bound"] == "mfma" else "GB/s"
         achieved = sp["work"] / (avg_us * 1e-6) / (1e12 if unit == "TFLOP/s" else 1e9)
         e = {"key": sp["key"], "kernel": sp["label"], "symbol": sp["name"], "grid": sp["grid"], "bound": sp["bound"],
@@ -410,6 +425,7 @@ def roofline_entries(specs, agent, cfg, table):
             i, rw = row
             e.update(rank=i + 1, launches_per_update=rw["launches_per_update"],
                      trace_avg_us=rw["avg_us"], trace_ms_per_update=rw["ms_per_update"],
+                     frac_trace=sp["work"] / (rw["avg_us"] * 1e-6) / (1e12 if unit == "TFLOP/s" else 1e9) / peak,
                      traffic=rw.get("hbm_bytes"), trace_clock_ghz=rw.get("clock_ghz"), mfma_util=rw.get("mfma_util"),
                      l2_hit=rw.get("l2_hit"), traffic_source=f"{KERNEL_TABLE} (rocprofv3 --pmc FETCH_SIZE x2 + "
                                                              "WRITE_SIZE, per dispatch)")

@@ -202,7 +202,8 @@ def mlp_layer(x, w, out, bias=None, norm_w=None, part_in=None, part_out=None, ac
         e.act, e.eps = int(act), EPS
     if part_out is not None:
         e.part_out, e.stride_part_out = p(part_out), part_out.stride(0)
-    return nat.call_shaped("sd_gemm_bf16x3_mlp", ctypes.byref(d), ctypes.addressof(e), stream())
+    # byref (not addressof): a LaunchProbe's recorded arguments keep the extension struct alive for its replays
+    return nat.call_shaped("sd_gemm_bf16x3_mlp", ctypes.byref(d), ctypes.byref(e), stream())
 
 
 _MLP_MAXB = nat._define(nat.HEADER, "SD_MLP_MAXB")
@@ -241,7 +242,8 @@ def _mlp_layer_entries(x, ws, out, biases, norm_ws, part_in, part_out, act, alph
         e.act, e.eps = int(act), EPS
     if part_out is not None:
         e.part_out, e.stride_part_out = p(part_out), part_out.stride(0)
-    return nat.call_shaped("sd_gemm_bf16x3_mlp", ctypes.byref(d), ctypes.addressof(e), stream())
+    # byref (not addressof): a LaunchProbe's recorded arguments keep the extension struct alive for its replays
+    return nat.call_shaped("sd_gemm_bf16x3_mlp", ctypes.byref(d), ctypes.byref(e), stream())
 
 
 def mm(a, b, bias=None, out=None, **kw):
