@@ -794,6 +794,281 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
   }
 }
 
+// The actor MLP after layer 0 in ONE launch per 16-row tile (networks.py:313-377): hidden layers 1..L-1
+// (RMSNorm + SiLU of the previous layer, Linear), the output layer, the action sample and the x2 branch — what
+// k_rmslin x (L-1) + k_action do in L launches. An MLP row needs only its own previous-layer row, so a workgroup that
+// owns whole rows (all U = 256 columns: wave wc computes columns 64 wc .. 64 wc + 63) chains the layers through LDS
+// with no grid-wide dependency. N / 16 workgroups (64 at the bench shape): the chain is latency-bound either way, and
+// the CUs it leaves free run the update's filler phase beside the imagination.
+// Arithmetic is bit-identical to the unfused launches: the same k order per output element (lane quad q supplies
+// k = 32 kt + 8 q + s at MFMA step s, even steps into acc and odd steps into acc2, acc + acc2 at the end: the
+// gemm16_mainloop_fp order at one 16-column tile per wave), the same bias / 16-column row-partial epilogue
+// (ep_bias_part) and the same rstd summation order (wg_rstd). B fragments come straight from global memory (each
+// wave owns its columns: nothing to share through LDS), three k tiles in flight.
+#ifndef SD_FUSED_ACTOR
+#define SD_FUSED_ACTOR 1
+#endif
+constexpr int FA_LD = 256 + 4;  // LDS row stride of the 16 x 256 activation panels (floats)
+template <int NJ>
+SD_DEV void fa_bload(f32x4 (&b)[NJ][2], const float* W, int ncol0, int nrows, int k0, int l16, int q) {
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = ncol0 + 16 * j + l16;
+    const float* p = W + (long)n * 256 + k0 + 8 * q;
+    b[j][0] = n < nrows ? ld4(p) : zero4();
+    b[j][1] = n < nrows ? ld4(p + 4) : zero4();
+  }
+}
+// acc[j] (+ acc2[j]) = P[0:16, :] . W[ncol0 + 16 j + (0..15), :]^T over K = 256, A from the LDS panel P
+template <int NJ>
+SD_DEV void fa_layer(const float* P, const float* W, int ncol0, int nrows, f32x4 (&acc)[NJ], int l16, int q) {
+  constexpr int NKT = 256 / BK, RING = 3;
+  f32x4 acc2[NJ], b[RING][NJ][2];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] = acc2[j] = zero4();
+#pragma unroll
+  for (int u = 0; u < RING - 1; ++u) fa_bload<NJ>(b[u], W, ncol0, nrows, u * BK, l16, q);
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    // the loads of tile kt + RING - 1 go out before this tile's MFMAs (the scheduler would otherwise sink them to
+    // their use and wait on each L2 round trip)
+    if (kt + RING - 1 < NKT) fa_bload<NJ>(b[(kt + RING - 1) % RING], W, ncol0, nrows, (kt + RING - 1) * BK, l16, q);
+    __builtin_amdgcn_sched_barrier(0);
+    const float* pa = P + l16 * FA_LD + kt * BK + 8 * q;
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(pa), a1 = *reinterpret_cast<const f32x4*>(pa + 4);
+    const int c = kt % RING;
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float av = s < 4 ? a0[s & 3] : a1[s & 3], bv = b[c][j][s >> 2][s & 3];
+        if (s & 1)
+          acc2[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc2[j], 0, 0, 0);
+        else
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] += acc2[j];
+}
+// rs[row] from the 16 LDS row partials part[p][row] (wg_rstd's order), then P = silu(O * rs * nw)
+SD_DEV void fa_norm_panel(const float* O, const float (*part)[16], const float* nw, float eps, float* rs, float* P) {
+  const int tid = threadIdx.x;
+  if (tid < 16) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += part[g][tid];
+    rs[tid] = rsqrtf(t / 256.f + eps);
+  }
+  __syncthreads();
+  for (int i = tid; i < 16 * 64; i += 256) {
+    const int row = i / 64, k = 4 * (i % 64);
+    const f32x4 x = *reinterpret_cast<const f32x4*>(O + row * FA_LD + k), w = ld4(nw + k);
+    f32x4 y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = siluf_(x[j] * rs[row] * w[j]);
+    *reinterpret_cast<f32x4*>(P + row * FA_LD + k) = y;
+  }
+  __syncthreads();
+}
+__global__ __launch_bounds__(256) void k_actor(sd_imagine d, const float* X, const float* part_in, int np, float* act,
+                                               float* x2, int t, int want_x2) {
+  constexpr int BM = 16, RT = 256 / BM;
+  __shared__ __attribute__((aligned(16))) float P[BM * FA_LD], O[BM * FA_LD];
+  __shared__ float part[16][16], rs[BM], red[256];
+  __shared__ float tile[BM][33];
+  __shared__ float an[BM][17];
+  __shared__ float rsum[BM][RT + 1];
+  const int m0 = blockIdx.x * BM, U = d.U, A = d.A, L = d.actor_layers;
+  const int NO = d.act_discrete ? A : 2 * A;
+  const int tid = threadIdx.x, lane = tid & 63, wc = tid >> 6, l16 = lane & 15, q = lane >> 4;
+  // layer 1's input panel: silu(rms(X)) of the tile's rows (X = actor layer 0's pre-norm output)
+  wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
+  for (int i = tid; i < BM * 64; i += 256) {
+    const int row = i / 64, k = 4 * (i % 64), m = m0 + row;
+    const f32x4 x = m < d.N ? ld4(X + (long)m * U + k) : zero4(), w = ld4(d.na[0] + k);
+    f32x4 y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = siluf_(x[j] * rs[row] * w[j]);
+    *reinterpret_cast<f32x4*>(P + row * FA_LD + k) = y;
+  }
+  __syncthreads();
+  for (int l = 1; l < L; ++l) {
+    f32x4 acc[4];
+    fa_layer<4>(P, d.Wa[l], 64 * wc, 1 << 30, acc, l16, q);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = 64 * wc + 16 * j + l16;
+      const float bv = d.ba[l][n];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[j][r] + bv;
+        O[(4 * q + r) * FA_LD + n] = v;
+        const float s = group_sum<16>(v * v);
+        if (l16 == 0) part[4 * wc + j][4 * q + r] = s;
+      }
+    }
+    __syncthreads();
+    fa_norm_panel(O, part, d.na[l], d.eps, rs, P);
+  }
+  // output layer: waves 0-1 take columns 0..31 (NO <= 32 used; rows past NO read as 0)
+  if (wc < 2) {
+    f32x4 acc[1];
+    fa_layer<1>(P, d.Wao, 16 * wc, NO, acc, l16, q);
+    const int c = 16 * wc + l16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tile[4 * q + r][c] = acc[0][r] + (c < NO ? d.bao[c] : 0.f);
+  }
+  __syncthreads();
+  // action sample + action_norm + x2 = silu(rms(_dyn_in2(a_n))): k_action's epilogue
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+  if (d.act_discrete) {
+    for (int i = tid; i < BM * 16; i += 256) {
+      const int rl = i / 16, lt = i % 16;
+      const bool on = lt < A;
+      const long m = m0 + rl;
+      const float lg = on ? tile[rl][lt] : 0.f;
+      float p, pp, nl;
+      unimix_forward<16>(lg, on, A, d.act_unimix, p, pp, nl);
+      const float gn = on ? sd_gumbel(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lt)
+                          : 0.f;
+      float ys;
+      int idx;
+      st_soft<16>(nl, gn, on, ys, idx, lt);
+      if (on) {
+        const float a = ((lt == idx ? 1.f : 0.f) - ys) + ys;
+        if (m < d.N) act[m * A + lt] = a;
+        an[rl][lt] = a / fmaxf(fabsf(a), 1.f);
+      }
+    }
+  } else {
+    for (int i = tid; i < BM * A; i += 256) {
+      const int rl = i / A, j = i % A;
+      const long m = m0 + rl;
+      const float loc = tanhf(tile[rl][j]);
+      const float sc = (d.max_std - d.min_std) * sigmoidf_(tile[rl][A + j] + 2.f) + d.min_std;
+      const float a = loc + sd_normal(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + j) * sc;
+      if (m < d.N) act[m * A + j] = a;
+      an[rl][j] = a / fmaxf(fabsf(a), 1.f);
+    }
+  }
+  if (!want_x2) return;
+  __syncthreads();
+  float* xs = O;  // x2 pre-norm rows (row stride FA_LD)
+  {
+    const int c = tid;
+    float w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = j < A ? d.W2[(long)c * A + j] : 0.f;
+    const float b = d.b2[c];
+    for (int rl = 0; rl < BM; ++rl) {
+      float v = b;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j < A) v += an[rl][j] * w[j];
+      xs[rl * FA_LD + c] = v;
+    }
+  }
+  __syncthreads();
+  {
+    const int rl = tid / RT, pt = tid % RT;
+    float s = 0.f;
+    for (int c = pt; c < U; c += RT) s += xs[rl * FA_LD + c] * xs[rl * FA_LD + c];
+    rsum[rl][pt] = s;
+  }
+  __syncthreads();
+  {
+    const int c = tid;
+    const float wn = d.n2[c];
+    for (int rl = 0; rl < BM; ++rl) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < RT; ++k) s += rsum[rl][k];
+      const float r = rsqrtf(s / (float)U + d.eps);
+      if (m0 + rl < d.N) x2[(long)(m0 + rl) * U + c] = siluf_(xs[rl * FA_LD + c] * r * wn);
+    }
+  }
+}
+
+// img_net's hidden layers 1..L-1 + the prior logits + the unimix one-hot sample in ONE launch per (16-row tile,
+// SK / NCT logit columns): what k_rmslin x (L-1) + k_prior do in L launches (rssm.py:180-195). Every workgroup of a
+// row tile recomputes the tile's hidden rows (whole rows: the next norm needs them), then its logit columns (wave wc:
+// SK / NCT / 4 columns), then samples them by teams of KD lanes as k_prior does. Bit-identical to the unfused launches
+// (fa_layer's k order, ep_bias_part's partials, wg_rstd's sums). grid (NCT, N / 16).
+#ifndef SD_FUSED_PRIOR
+#define SD_FUSED_PRIOR 1
+#endif
+#ifndef SD_PRIOR_NCT
+#define SD_PRIOR_NCT 4
+#endif
+template <int KD, int NJ>
+__global__ __launch_bounds__(256) void k_imgprior(sd_imagine d, const float* X, const float* part_in, int np,
+                                                  float* snew, long ldf, int t) {
+  constexpr int BM = 16, BNW = 64 * NJ;  // logit columns per workgroup (4 waves x 16 NJ)
+  __shared__ __attribute__((aligned(16))) float P[BM * FA_LD], O[BM * FA_LD];
+  __shared__ float part[16][16], rs[BM], red[256];
+  __shared__ float tile[BM][BNW + 1];
+  const int n0 = blockIdx.x * BNW, m0 = blockIdx.y * BM, U = d.U, S = d.SK / KD, L = d.img_layers;
+  const int tid = threadIdx.x, lane = tid & 63, wc = tid >> 6, l16 = lane & 15, q = lane >> 4;
+  wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
+  for (int i = tid; i < BM * 64; i += 256) {
+    const int row = i / 64, k = 4 * (i % 64), m = m0 + row;
+    const f32x4 x = m < d.N ? ld4(X + (long)m * U + k) : zero4(), w = ld4(d.ni[0] + k);
+    f32x4 y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = siluf_(x[j] * rs[row] * w[j]);
+    *reinterpret_cast<f32x4*>(P + row * FA_LD + k) = y;
+  }
+  __syncthreads();
+  for (int l = 1; l < L; ++l) {
+    f32x4 acc[4];
+    fa_layer<4>(P, d.Wi[l], 64 * wc, 1 << 30, acc, l16, q);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = 64 * wc + 16 * j + l16;
+      const float bv = d.bi[l][n];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[j][r] + bv;
+        O[(4 * q + r) * FA_LD + n] = v;
+        const float s = group_sum<16>(v * v);
+        if (l16 == 0) part[4 * wc + j][4 * q + r] = s;
+      }
+    }
+    __syncthreads();
+    fa_norm_panel(O, part, d.ni[l], d.eps, rs, P);
+  }
+  {
+    f32x4 acc[NJ];
+    fa_layer<NJ>(P, d.Wl, n0 + 16 * NJ * wc, 1 << 30, acc, l16, q);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = 16 * NJ * wc + 16 * j + l16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tile[4 * q + r][c] = acc[j][r] + d.bl[n0 + c];
+    }
+  }
+  __syncthreads();
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+#pragma unroll
+  for (int k = 0; k < BM * BNW / 256; ++k) {
+    const int i = tid + 256 * k;
+    const int rl = i / BNW, c = i % BNW, lt = c % KD;
+    const long m = m0 + rl;
+    const int s = (n0 + c) / KD;
+    const float lg = tile[rl][c];
+    float p, pp, nl;
+    unimix_forward<KD>(lg, true, KD, d.unimix, p, pp, nl);
+    const float gn = sd_gumbel(seed, (uint32_t)d.stream_img, (uint32_t)t,
+                               (uint64_t)((m + d.row_offset) * S + s) * KD + lt);
+    float ys;
+    int idx;
+    st_soft<KD>(nl, gn, true, ys, idx, lt);
+    if (m < d.N) snew[m * ldf + n0 + c] = ((lt == idx ? 1.f : 0.f) - ys) + ys;
+  }
+}
+
 // ------------------------------------------------------------------------------------------- host side
 struct IWork {
   float *a[2], *pa[2], *ad, *x0p, *px0, *x1p, *px1, *x2, *hp, *ph, *i[2], *pi[2];
@@ -925,17 +1200,22 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       }
       SD_LAUNCH_CHECK();
     }
-    int cur = 0, npa = npU;
-    for (int l = 1; l < d.actor_layers; ++l) {
-      k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(l == 1 ? a0 : w.a[cur], d.na[l - 1], w.pa[cur], npa, U, d.Wa[l], d.ba[l],
-                                              w.a[cur ^ 1], w.pa[cur ^ 1], N, d.eps);
-      SD_LAUNCH_CHECK();
-      cur ^= 1;
-      npa = npR;
+    if (SD_FUSED_ACTOR) {  // hidden layers 1.. + output layer + action sample + x2 in one launch
+      k_actor<<<sd_cdiv(N, 16), 256, 0, st>>>(d, a0, w.pa[0], npU, d.actions + (long)t * N * d.A, w.x2, t,
+                                              last ? 0 : 1);
+    } else {
+      int cur = 0, npa = npU;
+      for (int l = 1; l < d.actor_layers; ++l) {
+        k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(l == 1 ? a0 : w.a[cur], d.na[l - 1], w.pa[cur], npa, U, d.Wa[l],
+                                                d.ba[l], w.a[cur ^ 1], w.pa[cur ^ 1], N, d.eps);
+        SD_LAUNCH_CHECK();
+        cur ^= 1;
+        npa = npR;
+      }
+      k_action<<<dim3(1, sd_cdiv(N, KA_BM)), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur],
+                                                d.na[d.actor_layers - 1], w.pa[cur], npa,
+                                                d.actions + (long)t * N * d.A, w.x2, t, last ? 0 : 1);
     }
-    k_action<<<dim3(1, sd_cdiv(N, KA_BM)), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur],
-                                              d.na[d.actor_layers - 1], w.pa[cur], npa,
-                                              d.actions + (long)t * N * d.A, w.x2, t, last ? 0 : 1);
     SD_LAUNCH_CHECK();
     if (last) break;
     k_hid<<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU,
@@ -950,20 +1230,34 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N);
       SD_LAUNCH_CHECK();
     }
-    int ci = 0, npi = U / KL3_PW;
-    for (int l = 1; l < d.img_layers; ++l) {
-      k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(w.i[ci], d.ni[l - 1], w.pi[ci], npi, U, d.Wi[l], d.bi[l], w.i[ci ^ 1],
-                                              w.pi[ci ^ 1], N, d.eps);
-      SD_LAUNCH_CHECK();
-      ci ^= 1;
-      npi = npR;
+    const int pj = SD_PRIOR_NCT > 0 && SK % (64 * SD_PRIOR_NCT) == 0 ? SK / (64 * SD_PRIOR_NCT) : 0;
+    if (SD_FUSED_PRIOR && (pj == 1 || pj == 2 || pj == 4)) {  // img_net hidden layers + prior + sample, one launch
+      const dim3 gp(SD_PRIOR_NCT, sd_cdiv(N, 16));
+      const int npi = U / KL3_PW;
+#define SD_PRIOR_LAUNCH(KD_, NJ_) \
+  k_imgprior<KD_, NJ_><<<gp, 256, 0, st>>>(d, w.i[0], w.pi[0], npi, feats(t + 1), F, t)
+      if (d.Kd == 16) {
+        if (pj == 1) SD_PRIOR_LAUNCH(16, 1); else if (pj == 2) SD_PRIOR_LAUNCH(16, 2); else SD_PRIOR_LAUNCH(16, 4);
+      } else {
+        if (pj == 1) SD_PRIOR_LAUNCH(32, 1); else if (pj == 2) SD_PRIOR_LAUNCH(32, 2); else SD_PRIOR_LAUNCH(32, 4);
+      }
+#undef SD_PRIOR_LAUNCH
+    } else {
+      int ci = 0, npi = U / KL3_PW;
+      for (int l = 1; l < d.img_layers; ++l) {
+        k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(w.i[ci], d.ni[l - 1], w.pi[ci], npi, U, d.Wi[l], d.bi[l],
+                                                w.i[ci ^ 1], w.pi[ci ^ 1], N, d.eps);
+        SD_LAUNCH_CHECK();
+        ci ^= 1;
+        npi = npR;
+      }
+      if (d.Kd == 16)
+        k_prior<16><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi,
+                                                                    feats(t + 1), F, t);
+      else
+        k_prior<32><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi,
+                                                                    feats(t + 1), F, t);
     }
-    if (d.Kd == 16)
-      k_prior<16><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi,
-                                                          feats(t + 1), F, t);
-    else
-      k_prior<32><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi,
-                                                          feats(t + 1), F, t);
     SD_LAUNCH_CHECK();
   }
   return SD_OK;

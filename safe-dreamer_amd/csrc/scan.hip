@@ -180,7 +180,7 @@ SD_DEV void st_row(float* rowp, const f32x4 (&v)[NI], int N, int t32) {
 
 // ------------------------------------------------------------------------------------------- scratch layout
 struct Work {
-  float *x0s, *x1s, *ops, *ssh, *dotp, *dxs, *dhin, *gq, *ch;
+  float *x0s, *x1s, *ops, *ssh, *dotp, *dxs, *dhin, *gq, *ch, *w1t;
   long total;
 };
 long al64(long n) { return (n + 63) / 64 * 64; }
@@ -190,7 +190,7 @@ Work work_layout(const sd_rssm_scan& d, float* base) {
   const long BU = (long)d.B * d.U;
   auto take = [&](long n) { float* p = base ? base + o : nullptr; o += al64(n); return p; };
   w.x0s = take(d.ks_d * BU);
-  w.x1s = take(d.ks_s * BU);
+  w.x1s = take(4L * BU);  // ks_s slabs, or k_logit_rows' LR_NG (= KSM = 4)
   w.ops = take(d.ks_d * BU);
   w.ssh = take((long)d.D);
   w.dotp = take((long)d.D);
@@ -198,6 +198,7 @@ Work work_layout(const sd_rssm_scan& d, float* base) {
   w.dhin = take((long)d.B * d.D);
   w.gq = take((long)d.B * d.D);
   w.ch = take((long)d.B * d.D);
+  w.w1t = take((long)d.SK * d.U);  // _dyn_in1's weight transposed (SK, U): k_logit_rows' gather rows
   w.total = o;
   return w;
 }
@@ -243,8 +244,13 @@ __global__ void k_zero(float* p, long n) {
   if (i < n) p[i] = 0.f;
 }
 
-__global__ void k_init(sd_rssm_scan d) {
-  const long nS = (long)d.B * d.SK, nD = (long)d.B * d.D;
+// (and w1t = W1^T for k_logit_rows)
+__global__ void k_init(sd_rssm_scan d, float* w1t) {
+  const long nS = (long)d.B * d.SK, nD = (long)d.B * d.D, nW = w1t ? (long)d.SK * d.U : 0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nW; i += (long)gridDim.x * blockDim.x) {
+    const long k = i / d.U, c = i % d.U;  // w1t[k][c] = W1[c][k]
+    w1t[i] = d.W1[c * d.SK + k];
+  }
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nS + nD; i += (long)gridDim.x * blockDim.x) {
     if (i < nS) {
       const int row = (int)(i / d.SK);
@@ -460,6 +466,117 @@ __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
         if (t + 1 < d.T) d.s_in[o + (long)B * SK] = rnext[k] ? 0.f : yv;
       }
     }
+  }
+}
+
+// k_logit by rows, with the next step's _dyn_in1 folded in: workgroup (g, b) takes batch row b and the CPG
+// categoricals g*CPG.. of the obs_net logits (rssm.py:172-177): obs_net RMSNorm + SiLU of its row, the CPG*KD logits
+// (fp32 dot products, K = U split over TPC lanes), the unimix one-hot ST sample (distributions.py:16-33), and then
+// slab g of x1p[t+1] = the sample's _dyn_in1 pre-activation (rssm.py:52-56). A straight-through one-hot row holds one
+// nonzero per categorical (((k == idx) - ys) + ys is exactly 0 off the index), so its contraction with W1 is a gather
+// of CPG rows of W1^T: the NG = S / CPG slabs of a row sum (in k_hid's prologue, fixed order) to the dense product.
+// That removes the x1p k_slab launch from every step (4 dependent launches per step instead of 5).
+constexpr int LR_NG = 4;  // slabs of x1p (== KSM: k_hid sums up to KSM slabs)
+template <int KD, int CPG>
+__global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int t) {
+  constexpr int NC = CPG * KD, TPC = NTHR / NC, KPT = UH / TPC, NQ = KPT / 4;
+  static_assert(NTHR % NC == 0 && UH % (4 * TPC) == 0, "column split");
+  __shared__ __attribute__((aligned(16))) float y[UH];
+  __shared__ float red[NW], lg[NC], hv[CPG];
+  __shared__ int hot[CPG];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int B = d.B, SK = d.SK, S = SK / KD, g = blockIdx.x, b = blockIdx.y, n0 = g * NC;
+  const long tBU = (long)t * B * UH;
+  // independent of the contraction: the column's weight slice, bias, noise, reset mask
+  const int col = tid / TPC, kp = tid % TPC;
+  f32x4 wv[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) wv[i] = ld4(d.Wl + (long)(n0 + col) * UH + kp * KPT + 4 * i);
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+  const bool ts = tid < NC;
+  const int lt = tid % KD;
+  float blv = 0.f, gn = 0.f;
+  if (ts) {
+    blv = d.bl[n0 + tid];
+    gn = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)t,
+                   (uint64_t)((long)b * S + g * CPG + tid / KD + d.group_offset) * KD + lt);
+  }
+  const bool rnext = t + 1 < d.T && d.reset[(t + 1) * B + b];
+  // obs_net_0 output row (sum of the deter-half slabs + the hoisted embed half with bias), RMSNorm + SiLU
+  float x = 0.f, nw = 0.f;
+  if (tid < UH) {
+    float part[KSM];
+#pragma unroll
+    for (int s = 0; s < KSM; ++s) part[s] = s < d.ks_d ? w.ops[(long)s * B * UH + (long)b * UH + tid] : 0.f;
+    x = part[0];
+#pragma unroll
+    for (int s = 1; s < KSM; ++s) x += part[s];
+    x += d.eproj[in_row(d, t, b) * UH + tid];
+    nw = d.no[tid];
+  }
+  float ss = wave_sum(x * x);
+  if (lane == 0) red[wave] = ss;
+  __syncthreads();
+  ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < UH / 64; ++i) ss += red[i];
+  const float r = rsqrtf(ss / (float)UH + d.eps);
+  if (tid < UH) {
+    const float yv = siluf_(x * r * nw);
+    y[tid] = yv;
+    if (g == 0) {
+      d.op[tBU + (long)b * UH + tid] = x;
+      d.oo[tBU + (long)b * UH + tid] = yv;
+      if (tid == 0) d.ro[(long)t * B + b] = r;
+    }
+  }
+  __syncthreads();
+  // logits: TPC adjacent lanes per column, KPT k each, fixed-order pairwise combine
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const f32x4 yy = *reinterpret_cast<const f32x4*>(y + kp * KPT + 4 * i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = fmaf(yy[j], wv[i][j], acc);
+  }
+#pragma unroll
+  for (int o = 1; o < TPC; o <<= 1) acc += __shfl_xor(acc, o, 64);
+  if (kp == 0) lg[col] = acc;
+  __syncthreads();
+  if (ts) {
+    const float l = lg[tid] + blv;
+    float p, pp, nl;
+    unimix_forward<KD>(l, true, KD, d.unimix, p, pp, nl);
+    float ysoft;
+    int idx;
+    st_soft<KD>(nl, gn, true, ysoft, idx, lt);
+    const float yv = ((lt == idx ? 1.f : 0.f) - ysoft) + ysoft;
+    const long o = (long)t * B * SK + (long)b * SK + n0 + tid;
+    d.logit[o] = l;
+    if (d.stoch) d.stoch[o] = yv;
+    if (d.post_logit) {
+      const long ob = ((long)b * d.T + t) * SK + n0 + tid;
+      d.post_logit[ob] = l;
+      d.post_stoch[ob] = yv;
+    }
+    if (t + 1 < d.T) d.s_in[o + (long)B * SK] = rnext ? 0.f : yv;
+    if (lt == idx) {
+      hot[tid / KD] = tid;  // local column of the categorical's nonzero
+      hv[tid / KD] = yv;
+    }
+  }
+  if (t + 1 >= d.T) return;
+  __syncthreads();
+  if (tid < UH) {  // slab g of x1p[t+1]: sum over the group's categoricals of v_s * W1^T[hot_s]
+    float v = 0.f;
+    if (!rnext) {
+      float wr[CPG];
+#pragma unroll
+      for (int s = 0; s < CPG; ++s) wr[s] = w.w1t[(long)(n0 + hot[s]) * UH + tid];
+#pragma unroll
+      for (int s = 0; s < CPG; ++s) v = fmaf(hv[s], wr[s], v);
+    }
+    w.x1s[(long)g * B * UH + (long)b * UH + tid] = v;
   }
 }
 
@@ -727,19 +844,36 @@ __global__ __launch_bounds__(NTHR) void k_dx01(sd_rssm_scan d, Work w, int t) {
 // carry_h = mask(d_hin + d_x0p . W0) and carry_s = mask(d_x1p . W1) into step t-1 (rssm.py:161-165 backward); the
 // carry_s workgroups (one categorical each) then run the sampler backward of step t-1:
 // dl[t-1] = d_logit[t-1] + ST-backward(logit[t-1], d_stoch[t-1] + carry_s). grid (D/KD + S)
+// The A operand d_x0p (carry_h workgroups) / d_x1p (carry_s workgroups) is built by the prologue, as k_dx01 builds it:
+// sum of the G d_xcat slabs of k_dhp + the _dyn_in0 / _dyn_in1 RMSNorm-SiLU backward, 16 rows into an LDS panel. The
+// first workgroup of each half also writes its d_xcat part and d_x0p / d_x1p (read by the deferred weight gradients);
+// the second carry_h workgroup writes the x2 part of d_xcat. So k_dx01 runs only at t = 0 (no k_carry there).
 template <int KD>
 __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_THREAD_IDS
-  constexpr int NT = KD / 16, NE = (MR * KD + NTHR - 1) / NTHR;
+  constexpr int NT = KD / 16, NE = (MR * KD + NTHR - 1) / NTHR, GM = 8, X = 3 * UH, ldp = UH + 4;
   const int B = d.B, D = d.D, SK = d.SK, S = SK / KD;
   const bool p0 = (int)blockIdx.x < D / KD;
-  const int n0 = (p0 ? blockIdx.x : blockIdx.x - D / KD) * KD;
+  const int wid = p0 ? blockIdx.x : blockIdx.x - D / KD, n0 = wid * KD;
   Core<NT, 2> core;
   const float* wt[NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i) wt[i] = (p0 ? d.W0T : d.W1T) + (long)(n0 + 16 * i + l16) * UH;
   core.load_b(wt, UH / 16, wave, q);
+  // prologue loads: the G slabs of this half's d_xcat part, its pre-norm input and norm weight
+  const int row = tid >> 5, t32 = tid & 31;
+  const bool rv = row < B;
+  const long tB = (long)t * B;
+  const int hoff = p0 ? 0 : UH;
+  const bool wx2 = p0 && wid == 1;  // the x2 part's writer
+  f32x4 part[GM][NU], xv[NU], nv[NU];
+#pragma unroll
+  for (int g = 0; g < GM; ++g)
+    ld_row(part[g], w.dxs + (long)g * B * X + (long)row * X + (wx2 ? 2 * UH : hoff), UH, rv && g < d.G, t32);
+  const float rr = rv ? (p0 ? d.r0 : d.r1)[tB + row] : 0.f;
+  ld_row(xv, (p0 ? d.x0p : d.x1p) + (tB + row) * UH, UH, rv, t32);
+  ld_row(nv, p0 ? d.n0 : d.n1, UH, true, t32);
   // epilogue operands: element i = (row er, column lt) of the 16 x KD tile
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
   const int tp = t - 1;
@@ -764,7 +898,49 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
                         (uint64_t)((long)er * S + n0 / KD + d.group_offset) * KD + lt);
     }
   }
-  core.run_glb((p0 ? d.d_x0p : d.d_x1p) + (long)t * B * UH, UH, B, UH / 16, wave, l16, q);
+  // d_xcat part = sum of the slabs (k_dx01's order); the x2 writer stores its part and then rebuilds x0's
+  f32x4 dx[NU];
+#pragma unroll
+  for (int i = 0; i < NU; ++i) {
+    dx[i] = part[0][i];
+#pragma unroll
+    for (int g = 1; g < GM; ++g) dx[i] += part[g][i];
+  }
+  if (wx2) {
+    if (rv) st_row(d.d_xcat + (tB + row) * X + 2 * UH, dx, UH, t32);
+#pragma unroll
+    for (int g = 0; g < GM; ++g) ld_row(part[g], w.dxs + (long)g * B * X + (long)row * X, UH, rv && g < d.G, t32);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      dx[i] = part[0][i];
+#pragma unroll
+      for (int g = 1; g < GM; ++g) dx[i] += part[g][i];
+    }
+  }
+  float dot = 0.f;
+  f32x4 gg[NU], xh[NU];
+#pragma unroll
+  for (int i = 0; i < NU; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      xh[i][k] = xv[i][k] * rr;
+      gg[i][k] = dx[i][k] * dsilu(xh[i][k] * nv[i][k]) * nv[i][k];
+      dot += gg[i][k] * xh[i][k];
+    }
+  dot = group_sum<32>(dot) / (float)UH;
+  f32x4 o[NU];
+#pragma unroll
+  for (int i = 0; i < NU; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[i][k] = rv ? rr * (gg[i][k] - xh[i][k] * dot) : 0.f;
+  float* P = smem + core_lds_floats<NT>();
+  st_row(P + row * ldp, o, UH, t32);
+  if (rv && wid == 0) {
+    st_row(d.d_xcat + (tB + row) * X + hoff, dx, UH, t32);
+    st_row((p0 ? d.d_x0p : d.d_x1p) + (tB + row) * UH, o, UH, t32);
+  }
+  __syncthreads();
+  core.run_lds(P, ldp, UH / 16, wave, l16, q);
   float* C = smem + NW * NT * 256;
   core.reduce(smem, C, tid, wave, lane);
 #pragma unroll
@@ -845,6 +1021,57 @@ int check(const sd_rssm_scan* d) {
     default: return SD_ESHAPE;                                \
   }
 
+#ifndef SD_SCAN_LROWS
+#define SD_SCAN_LROWS 1
+#endif
+// the forward's per-step phases (0: x1p k_slab, 1: k_hid, 2: k_gate, 3: obs_net_0 + next x0p k_slab, 4: logits +
+// sampler [+ next x1p slabs when lrows]); one definition for sd_rssm_scan_fwd and the measurement aid
+int fwd_phase(const sd_rssm_scan& d, const Work& w, bool lrows, int which, int t, hipStream_t st) {
+  const int B = d.B, D = d.D, SK = d.SK, Dg = D / d.G, Ig = Dg + 3 * UH;
+  const int ks_s = lrows ? LR_NG : d.ks_s;
+  const int span_d = D / d.ks_d, span_s = SK / ks_s;
+  const int cp_d = cpw_for(span_d), cp_s = cpw_for(span_s), cp_h = cpw_for(Ig);
+  if (cp_d < 0 || cp_s < 0 || cp_h < 0) return SD_ESHAPE;
+  const size_t core1 = core_lds_floats<1>() * 4;
+  const size_t lds_hid = core1 + (size_t)MR * (Ig + 4) * 4;
+  const size_t lds_gate = core_lds_floats<3>() * 4 + (size_t)MR * (Dg + 4) * 4;
+  const long BD = (long)B * D, BS = (long)B * SK;
+  const long wod_ld = d.ld_wod > 0 ? d.ld_wod : D;
+  sd_rssm_scan dd = d;
+  dd.ks_s = ks_s;  // x1p slabs k_hid sums
+  if (which == 0) {
+    SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr};
+    SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(UH / 16, ks_s, 1), NTHR, core1, st>>>(p, p, B, UH, span_s));
+  } else if (which == 1) {
+    SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG>>(lds_hid))) return SD_EARG;
+                                   k_hid<CP, NG><<<D / 16, NTHR, lds_hid, st>>>(dd, w, t)));
+  } else if (which == 2) {
+    SD_NG_SWITCH(Dg, if (!(raise_lds<k_gate<NG, NG>>(lds_gate))) return SD_EARG;
+                 k_gate<NG, NG><<<D / 16, NTHR, lds_gate, st>>>(dd, w, t));
+  } else if (which == 3) {
+    SlabProb po{d.deter + t * BD, D, d.WoD, wod_ld, w.ops, nullptr};
+    SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset + (t + 1) * B};
+    const int np = t + 1 < d.T ? 2 : 1;
+    SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, np), NTHR, core1, st>>>(po, px, B, UH, span_d));
+  } else if (lrows) {
+    const dim3 gr(LR_NG, B);
+#define SD_LR(KD_, CPG_) k_logit_rows<KD_, CPG_><<<gr, NTHR, 0, st>>>(d, w, t)
+    if (d.Kd == 16) { if (SK == 512) SD_LR(16, 8); else SD_LR(16, 16); }
+    else if (d.Kd == 32) { if (SK == 512) SD_LR(32, 4); else SD_LR(32, 8); }
+    else { if (SK == 512) SD_LR(64, 2); else SD_LR(64, 4); }
+#undef SD_LR
+  } else {
+    SD_KD_SWITCH(d.Kd, {
+      const size_t lds = core_lds_floats<KD / 16>() * 4 + (size_t)MR * (UH + 4) * 4;
+      if (!(raise_lds<k_logit<KD>>(lds))) return SD_EARG;
+      k_logit<KD><<<SK / KD, NTHR, lds, st>>>(d, w, t);
+    });
+  }
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+bool use_lrows(const sd_rssm_scan& d) { return SD_SCAN_LROWS && (d.SK / d.Kd) % LR_NG == 0; }
+
 }  // namespace
 
 extern "C" int sd_rssm_scan_work_floats(const sd_rssm_scan* d) {
@@ -859,95 +1086,39 @@ extern "C" int sd_rssm_scan_fwd(const sd_rssm_scan* dp, sd_stream stream_) {
   hipStream_t st = (hipStream_t)stream_;
   const sd_rssm_scan& d = *dp;
   const Work w = work_layout(d, d.work);
-  const int B = d.B, D = d.D, SK = d.SK, Dg = D / d.G, Ig = Dg + 3 * UH;
-  const int span_d = D / d.ks_d, span_s = SK / d.ks_s;
-  const int cp_d = cpw_for(span_d), cp_s = cpw_for(span_s), cp_h = cpw_for(Ig);
-  if (cp_d < 0 || cp_s < 0 || cp_h < 0) return SD_ESHAPE;
-  const size_t core1 = core_lds_floats<1>() * 4;
-  const size_t lds_hid = core1 + (size_t)MR * (Ig + 4) * 4;
-  const size_t lds_gate = core_lds_floats<3>() * 4 + (size_t)MR * (Dg + 4) * 4;
-  const long BD = (long)B * D, BS = (long)B * SK;
-  const long wod_ld = d.ld_wod > 0 ? d.ld_wod : D;
-
-  k_init<<<64, 256, 0, st>>>(d);
+  const int B = d.B, D = d.D;
+  const int cp_d = cpw_for(D / d.ks_d);
+  if (cp_d < 0) return SD_ESHAPE;
+  const bool lrows = use_lrows(d);
+  k_init<<<lrows ? 256 : 64, 256, 0, st>>>(d, lrows ? w.w1t : nullptr);
   SD_LAUNCH_CHECK();
   {  // x0p(0) = h_in[0] . W0^T
     SlabProb p{d.h_in, D, d.W0, D, w.x0s, nullptr};
-    SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, 1), NTHR, core1, st>>>(p, p, B, UH, span_d));
+    SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, 1), NTHR, core_lds_floats<1>() * 4, st>>>(p, p, B, UH,
+                                                                                                    D / d.ks_d));
     SD_LAUNCH_CHECK();
   }
   for (int t = 0; t < d.T; ++t) {
-    {
-      SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr};
-      SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(UH / 16, d.ks_s, 1), NTHR, core1, st>>>(p, p, B, UH, span_s));
-      SD_LAUNCH_CHECK();
+    for (int which = 0; which < 5; ++which) {
+      if (which == 0 && lrows && t > 0) continue;  // x1p[t] slabs written by step t-1's k_logit_rows
+      rc = fwd_phase(d, w, lrows, which, t, st);
+      if (rc) return rc;
     }
-    SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG>>(lds_hid))) return SD_EARG;
-                                   k_hid<CP, NG><<<D / 16, NTHR, lds_hid, st>>>(d, w, t)));
-    SD_LAUNCH_CHECK();
-    SD_NG_SWITCH(Dg, if (!(raise_lds<k_gate<NG, NG>>(lds_gate))) return SD_EARG;
-                 k_gate<NG, NG><<<D / 16, NTHR, lds_gate, st>>>(d, w, t));
-    SD_LAUNCH_CHECK();
-    {
-      SlabProb po{d.deter + t * BD, D, d.WoD, wod_ld, w.ops, nullptr};
-      SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset + (t + 1) * B};
-      const int np = t + 1 < d.T ? 2 : 1;
-      SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, np), NTHR, core1, st>>>(po, px, B, UH, span_d));
-      SD_LAUNCH_CHECK();
-    }
-    SD_KD_SWITCH(d.Kd, {
-      const size_t lds = core_lds_floats<KD / 16>() * 4 + (size_t)MR * (UH + 4) * 4;
-      if (!(raise_lds<k_logit<KD>>(lds))) return SD_EARG;
-      k_logit<KD><<<SK / KD, NTHR, lds, st>>>(d, w, t);
-    });
-    SD_LAUNCH_CHECK();
   }
   return SD_OK;
 }
 
 // One launch of forward step t's phase `which` exactly as sd_rssm_scan_fwd issues it (same descriptor, workspace and
-// grid): 0 = k_slab (x1p), 1 = k_hid, 2 = k_gate, 3 = k_slab (obs_net_0 deter half + next x0p), 4 = k_logit. A
-// measurement aid (bench.py times the scan's phases with it, after a full sd_rssm_scan_fwd on the same descriptor);
-// only t = T - 1 rewrites exactly the values the run wrote (the workspace slabs hold the last step's partials).
+// grid): 0 = k_slab (x1p; issued only at t = 0 when k_logit_rows writes the next step's x1p slabs), 1 = k_hid,
+// 2 = k_gate, 3 = k_slab (obs_net_0 deter half + next x0p), 4 = k_logit / k_logit_rows. A measurement aid (bench.py
+// times the scan's phases with it, after a full sd_rssm_scan_fwd on the same descriptor); only t = T - 1 rewrites
+// exactly the values the run wrote (the workspace slabs hold the last step's partials).
 extern "C" int sd_rssm_scan_step_kernel(const sd_rssm_scan* dp, int which, int t, sd_stream stream_) {
   int rc = check(dp);
   if (rc) return rc;
   const sd_rssm_scan& d = *dp;
   if (t < 0 || t >= d.T || which < 0 || which > 4) return SD_EARG;
-  hipStream_t st = (hipStream_t)stream_;
-  const Work w = work_layout(d, d.work);
-  const int B = d.B, D = d.D, SK = d.SK, Dg = D / d.G, Ig = Dg + 3 * UH;
-  const int span_d = D / d.ks_d, span_s = SK / d.ks_s;
-  const int cp_d = cpw_for(span_d), cp_s = cpw_for(span_s), cp_h = cpw_for(Ig);
-  if (cp_d < 0 || cp_s < 0 || cp_h < 0) return SD_ESHAPE;
-  const size_t core1 = core_lds_floats<1>() * 4;
-  const size_t lds_hid = core1 + (size_t)MR * (Ig + 4) * 4;
-  const size_t lds_gate = core_lds_floats<3>() * 4 + (size_t)MR * (Dg + 4) * 4;
-  const long BD = (long)B * D, BS = (long)B * SK;
-  const long wod_ld = d.ld_wod > 0 ? d.ld_wod : D;
-  if (which == 0) {
-    SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr};
-    SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(UH / 16, d.ks_s, 1), NTHR, core1, st>>>(p, p, B, UH, span_s));
-  } else if (which == 1) {
-    SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG>>(lds_hid))) return SD_EARG;
-                                   k_hid<CP, NG><<<D / 16, NTHR, lds_hid, st>>>(d, w, t)));
-  } else if (which == 2) {
-    SD_NG_SWITCH(Dg, if (!(raise_lds<k_gate<NG, NG>>(lds_gate))) return SD_EARG;
-                 k_gate<NG, NG><<<D / 16, NTHR, lds_gate, st>>>(d, w, t));
-  } else if (which == 3) {
-    SlabProb po{d.deter + t * BD, D, d.WoD, wod_ld, w.ops, nullptr};
-    SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset + (t + 1) * B};
-    const int np = t + 1 < d.T ? 2 : 1;
-    SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, np), NTHR, core1, st>>>(po, px, B, UH, span_d));
-  } else {
-    SD_KD_SWITCH(d.Kd, {
-      const size_t lds = core_lds_floats<KD / 16>() * 4 + (size_t)MR * (UH + 4) * 4;
-      if (!(raise_lds<k_logit<KD>>(lds))) return SD_EARG;
-      k_logit<KD><<<SK / KD, NTHR, lds, st>>>(d, w, t);
-    });
-  }
-  SD_LAUNCH_CHECK();
-  return SD_OK;
+  return fwd_phase(d, work_layout(d, d.work), use_lrows(d), which, t, (hipStream_t)stream_);
 }
 
 extern "C" int sd_rssm_scan_bwd(const sd_rssm_scan* dp, sd_stream stream_) {
@@ -986,12 +1157,13 @@ extern "C" int sd_rssm_scan_bwd(const sd_rssm_scan* dp, sd_stream stream_) {
     SD_NG_SWITCH(Dg, if (!(raise_lds<k_dhp<NG, NG>>(lds_dhp))) return SD_EARG;
                  k_dhp<NG, NG><<<NX + D / 16, NTHR, lds_dhp, st>>>(d, w, t));
     SD_LAUNCH_CHECK();
-    k_dx01<<<B, NTHR, 0, st>>>(d, w, t);
-    SD_LAUNCH_CHECK();
-    if (t > 0) {
-      SD_KD_SWITCH(d.Kd, k_carry<KD><<<D / KD + SK / KD, NTHR, core_lds_floats<KD / 16>() * 4, st>>>(d, w, t));
-      SD_LAUNCH_CHECK();
+    if (t > 0) {  // k_carry builds d_x0p / d_x1p itself (the k_dx01 work in its prologue)
+      SD_KD_SWITCH(d.Kd, k_carry<KD><<<D / KD + SK / KD, NTHR,
+                                       core_lds_floats<KD / 16>() * 4 + (size_t)MR * (UH + 4) * 4, st>>>(d, w, t));
+    } else {
+      k_dx01<<<B, NTHR, 0, st>>>(d, w, t);
     }
+    SD_LAUNCH_CHECK();
   }
   return SD_OK;
 }

@@ -15,6 +15,7 @@ Differences by design (documented in DESIGN.md):
 """
 from __future__ import annotations
 
+import contextlib
 import copy
 import ctypes
 import math
@@ -57,6 +58,10 @@ REUSE_H0 = os.environ.get("SDREAMER_REUSE_H0", "1") != "0"
 # SDREAMER_PRIO=1 (schedule knob): graph-replayed updates run the critical chain on high-priority streams and the filler
 # phases (M1, S2-S4) on normal-priority ones
 STREAM_PRIO = os.environ.get("SDREAMER_PRIO", "0") == "1"
+# SDREAMER_AC_DEFER=1 (schedule knob): the actor / value weight-gradient contractions of phase S2 (the imagined
+# trajectories' large (H*N)-row GEMMs) are queued and run at the start of S3, beside the encoder backward, instead of
+# beside the scan backward (M2a, the latency-bound chain S2 slows)
+AC_DEFER = os.environ.get("SDREAMER_AC_DEFER", "0") == "1"
 
 
 def _symexp_bins(n, device):  # symexp_twohot bins, distributions.py:242-251
@@ -543,7 +548,11 @@ class Dreamer(nn.Module):
             gM1, _ = cap(lambda: self._ph_wm(st, defer=DEFER_WM), main_cap)
             gR, _ = cap(lambda: self._ph_repval(st), main_cap)
             gM2a, _ = cap(lambda: self._ph_scan_bwd(st, defer=True), main_cap)
-            gS3, _ = cap(lambda: self._flush(st["scan_wgrads"], "side:scan_wgrads"), side_cap)
+            if AC_DEFER:  # S2 captured before S3: its queued weight gradients are flushed at the start of S3
+                st["rr"]["ac_wgrads"] = []
+                gS2, (post, keys, mvec) = cap(lambda: self._side_ac_metrics(st), side_cap)
+            gS3, _ = cap(lambda: self._flush(st["rr"].get("ac_wgrads", []) + st["scan_wgrads"], "side:scan_wgrads"),
+                         side_cap)
             gM2b, _ = cap(lambda: self._ph_encoder_bwd_hi(st, defer=True), main_cap)
             if S4_MAIN:
                 st["enc_wgrads_main"] = st["enc_wgrads"][:S4_MAIN]
@@ -551,7 +560,8 @@ class Dreamer(nn.Module):
             gS4, _ = cap(lambda: self._flush(st["enc_wgrads"], "side:enc_wgrads"), side_cap)
             gM2c, _ = cap(lambda: self._ph_encoder_bwd_lo(st), main_cap)
             gM2d = cap(lambda: self._main_tail(st), main_cap)[0] if (DEFER_WM or S4_MAIN) else None
-            gS2, (post, keys, mvec) = cap(lambda: self._side_ac_metrics(st), side_cap)
+            if not AC_DEFER:
+                gS2, (post, keys, mvec) = cap(lambda: self._side_ac_metrics(st), side_cap)
             self._optimizer.zero_grads_after = True
             gM3, _ = cap(lambda: self._core_step(st), main_cap)
             self._optimizer.zero_grads_after = False  # eager steps (step()) keep the PyTorch semantics
@@ -647,7 +657,7 @@ class Dreamer(nn.Module):
         if dp:  # bucketed sum all-reduce of the gradient arena, overlapping the backward phases still running
             ev_main, ev_s4 = torch.cuda.Event(), torch.cuda.Event()
             ev_main.record(main)
-            self._allreduce_bucket("ac", ev_side[0])
+            self._allreduce_bucket("ac", ev_side[1] if AC_DEFER else ev_side[0])
             if DEFER_WM:  # the prior's img_net weight gradients are in M2d: the RSSM bucket also waits for main
                 self._allreduce_bucket("rssm", ev_side[1], ev_main)
             else:
@@ -1096,7 +1106,8 @@ class Dreamer(nn.Module):
         losses["policy"], losses["value"], adv = ops.ImagACLossFn.apply(
             vl, logpi, ent, self.vbins, ret, i_slow[:H], weight, rr["i_val"], rr["ret_scale"], self.act_entropy)
         rr["adv"] = adv
-        (losses["policy"] * self._loss_scales["policy"] + losses["value"] * self._loss_scales["value"]).backward()
+        with ops.defer_wgrads(rr["ac_wgrads"]) if "ac_wgrads" in rr else contextlib.nullcontext():
+            (losses["policy"] * self._loss_scales["policy"] + losses["value"] * self._loss_scales["value"]).backward()
         with torch.no_grad():
             ret_normed = (ret - rr["ret_offset"]) / rr["ret_scale"]
             metrics["ret"] = ret_normed.mean()
