@@ -333,16 +333,17 @@ def probe_specs(agent, cfg, K):
         pix = N * 32 * 32
         add("conv_stage2", "conv_fwd_direct_pool<48, 32, 5, 5, 1>", (N * 32 * 32 // 128, 1, 1), "mfma",
             2.0 * pix * 48 * 25 * 32, 4.0 * pix * 32 + N * 16 * 16 * (48 * 9 + 4), cp.label, ("launch", cp), 1)
-    # encoder stage 2 bwd-data (split-bf16 implicit GEMM over the flipped weight): sd_conv2d_dgrad_bf16x3(dout, wflip,
-    # din, Nb, Hs, Ws, Ci = dout channels, Co = din channels, kh, kw, pad, stream)
-    dg = K.LaunchProbe("sd_conv2d_dgrad_bf16x3", lambda a: a[6] == 48 and a[7] == 32,
+    # encoder stage 2 bwd-data (split-bf16 direct conv from a pre-split dOut patch in LDS): sd_conv2d_dgrad_direct(dout,
+    # wsplit, din, Nb, Hs, Ws, Ci = dout channels, Co = din channels, kh, kw, pad, stream)
+    dg = K.LaunchProbe("sd_conv2d_dgrad_direct", lambda a: a[6] == 48 and a[7] == 32,
                        lambda a: 2.0 * a[3] * a[4] * a[5] * a[6] * a[7] * a[8] * a[9],
-                       label="conv_dgrad3<32> (encoder stage 2 bwd-data: dOut 48 ch -> dIn 32 ch at 32x32, 5x5 flipped "
-                             "weight; implicit GEMM, operands split to bf16 (hi, lo) in LDS, 3 v_mfma_f32_16x16x32_bf16 "
-                             "per f32-equivalent product)")
+                       label="conv_dgrad3_direct<48, 2, 5, 5> (encoder stage 2 bwd-data: dOut 48 ch -> dIn 32 ch at "
+                             "32x32, 5x5 flipped weight; direct conv, the dOut patch of 4 rows split once into (hi, lo) "
+                             "bf16 planes in LDS, pre-split weight from L2, 3 v_mfma_f32_16x16x32_bf16 per "
+                             "f32-equivalent product)")
     pix = N * 32 * 32
-    add("conv_stage2_dgrad", "conv_dgrad3<32>", (pix // 128, 1, 1), "mfma", 2.0 * pix * 48 * 25 * 32,
-        4.0 * (pix * 48 + pix * 32 + 25 * 48 * 32), dg.label, ("launch", dg), 1, peak=PEAK_BF16X3)
+    add("conv_stage2_dgrad", "conv_dgrad3_direct<48, 2, 5, 5>", (pix // 128, 1, 1), "mfma", 2.0 * pix * 48 * 25 * 32,
+        4.0 * (pix * 48 + pix * 32) + 2.0 * 2 * 32 * 1216, dg.label, ("launch", dg), 1, peak=PEAK_BF16X3)
     # imagined heads' first layers: one split-bf16 MLP-layer launch, A = the imagined feats broadcast over 4 weights
     M = N * (H + 1)
     hp = K.LaunchProbe("sd_gemm_bf16x3_mlp", lambda a: a[0]._obj.batch == 4 and a[0]._obj.strideA == 0,

@@ -230,6 +230,29 @@ int sd_conv2d_dgrad_bf16x3(const float* dout, const float* wflip, float* din, in
 int sd_conv2d_wgrad_bf16x3_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int ups);
 int sd_conv2d_wgrad_bf16x3(const float* in, const float* dout, float* dw_db, float* workspace, long ws_floats,
                            int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad, sd_stream stream);
+/* The same bwd-data as a direct convolution (csrc/conv.hip conv_dgrad3_direct: each workgroup stages its dOut patch
+ * once, split to bf16 planes; same products and order per k as sd_conv2d_dgrad_bf16x3, k summed in the same order).
+ * wsplit = sd_conv_split_weight(wflip, rows = Co, K = kh*kw*Ci). Instantiated for the 5x5 pad-2 stages of the
+ * BASELINE encoders' two large bwd-data stages (dOut -> dIn channels 48->32 at 32x32, 64->48 at 16x16);
+ * SD_ESHAPE otherwise (the caller then takes sd_conv2d_dgrad_bf16x3). Replaces conv_dgrad's role in the backward of
+ * Conv2dSamePad (networks.py:59-85). */
+int sd_conv2d_dgrad_direct(const float* dout, const void* wsplit, float* din, int Nb, int Hs, int Ws, int Ci, int Co,
+                           int kh, int kw, int pad, sd_stream stream);
+/* sd_conv2d_fwd_pool on the fp32-accurate three-way split-bf16 path (csrc/conv.hip conv_fwd6_direct_pool, gemm6_core.h
+ * "bf16x6": six bf16 MFMAs per product, <= 2^-26 |ab| dropped per product, fp32-level error): a direct convolution from
+ * the tile's input patch staged once in LDS as three bf16 planes. wsplit3 = sd_conv_split3_weight(w, rows = Co,
+ * K = kh*kw*Ci). Instantiated for the 5x5 pad-2 stages 32->48 at 32x32 and 48->64 at 16x16 (SD_ESHAPE otherwise:
+ * the caller takes sd_conv2d_fwd_pool). Replaces ConvEncoder's Conv2dSamePad -> MaxPool2d -> RMSNorm2D -> SiLU stage
+ * (networks.py:201-216). */
+int sd_conv2d_fwd_pool6(const float* in, const void* wsplit3, const float* bias, const float* nw, float* pooled,
+                        uint8_t* amax, float* y, float* rstd, int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw,
+                        int pad, float eps, int nchw_flat, sd_stream stream);
+/* wsplit3 = [plane][rows][KP] bf16 three-way split (a0 = bf16(w), a1 = bf16(w - a0), a2 = bf16(w - a0 - a1)) of a
+ * (rows, K) fp32 matrix, KP = K rounded up to 32, zero past K: 6 * rows * KP bytes */
+int sd_conv_split3_weight(const float* w, void* wsplit, int rows, int K, sd_stream stream);
+/* wsplit = [plane][rows][KP] bf16 (hi = bf16(w), lo = bf16(w - hi), KP = K rounded up to 32, zero past K) of a
+ * (rows, K) fp32 matrix: 4 * rows * KP bytes */
+int sd_conv_split_weight(const float* w, void* wsplit, int rows, int K, sd_stream stream);
 /* Wf[ci][ky][kx][co] = W[co][kh-1-ky][kw-1-kx][ci]  (input-gradient conv weights) */
 int sd_conv_flip_weight(const float* w, float* wf, int Co, int kh, int kw, int Ci, sd_stream stream);
 /* backward of nearest 2x upsample: din (Nb,H,W,C) = 2x2 sums of du (Nb,2H,2W,C) */

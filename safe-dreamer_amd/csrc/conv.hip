@@ -13,6 +13,7 @@
 #include <stdlib.h>
 
 #include "gemm3_core.h"
+#include "gemm6_core.h"
 #include "gemm_core.h"
 #include "sdhip.h"
 
@@ -513,6 +514,128 @@ __global__ __launch_bounds__(256) void conv_fwd_direct_pool(GemmArgs g, Geom G, 
   }
 }
 
+// conv_fwd_direct_pool on the fp32-accurate three-way split-bf16 path (gemm6_core.h: a = a0 + a1 + a2, six
+// v_mfma_f32_16x16x32_bf16 per 32-deep k chunk, smallest terms first, <= 2^-26 |ab| dropped per product; 2.67x the
+// f32 MFMA rate). The 128-pixel tile's input patch is staged once, split into three bf16 planes (pixel stride CI + 8
+// bf16: conflict-free ds_read_b128 fragments), and every tap reads its shifted window from there; the weight comes
+// pre-split ([plane][BN][KP] bf16, sd_conv_split3_weight) straight from L2, one k chunk ahead. A lane's 8 k values of
+// a chunk are 8 consecutive channels of one tap (CI % 8 == 0), so CI need not be a multiple of 32. Wave w owns tile
+// pixels 32w..32w+31 (two 16-pixel tiles) x all BN channels; the epilogue (pool + RMSNorm + SiLU) is
+// conv_fwd16_pool's, staged in the patch area.
+template <int BN, int CI, int LW, int KS>
+__global__ __launch_bounds__(256, 2) void conv_fwd6_direct_pool(GemmArgs g, Geom G, int lhw,
+                                                                 const __bf16* __restrict__ wsp, const float* nw,
+                                                                 float* pooled, uint8_t* amax, float* y, float* rstd,
+                                                                 float eps, int nchw_flat) {
+  constexpr int W = 1 << LW, R = 128 / W, PH = R + KS - 1, PW = W + KS - 1, CP = CI + 8, PAD = KS / 2;
+  constexpr int PLANE = PH * PW * CP, K = KS * KS * CI, NKC = (K + 31) / 32, KP = NKC * 32, TN = BN / 16;
+  constexpr int CI4 = CI / 4, NEL = PH * PW * CI4, NE = (NEL + 255) / 256;
+  static_assert(CI % 8 == 0 && 128 % W == 0 && BN % 16 == 0, "geometry");
+  static_assert(128 * (BN + 1) * 4 <= 3 * PLANE * 2, "epilogue tile fits the patch area");
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  extern __shared__ __attribute__((aligned(16))) __bf16 patch6[];  // [plane][PH][PW][CP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, q = lane >> 4;
+  const int bm0 = blockIdx.x * 128, n = bm0 >> lhw, y0 = (bm0 & ((1 << lhw) - 1)) >> LW;
+  {
+    f32x4 v[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int i = tid + 256 * e, c4 = i % CI4, pix = i / CI4, pc = pix % PW, pr = pix / PW;
+      const int yy = y0 + pr - PAD, xx = pc - PAD;
+      v[e] = (i < NEL && (unsigned)yy < (unsigned)G.Hs && (unsigned)xx < (unsigned)W)
+                 ? *reinterpret_cast<const f32x4*>(G.in + (((long)n * G.Hs + yy) * W + xx) * CI + 4 * c4)
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int i = tid + 256 * e;
+      if (i < NEL) {
+        const int c4 = i % CI4, pix = i / CI4;
+        float h0, h1, h2, h3, m0, m1, m2, m3;
+        const u32x2 h{bf16_pair(v[e][0], v[e][1], h0, h1), bf16_pair(v[e][2], v[e][3], h2, h3)};
+        const float r0 = v[e][0] - h0, r1 = v[e][1] - h1, r2 = v[e][2] - h2, r3 = v[e][3] - h3;
+        const u32x2 m{bf16_pair(r0, r1, m0, m1), bf16_pair(r2, r3, m2, m3)};
+        const f32x4 l{r0 - m0, r1 - m1, r2 - m2, r3 - m3};
+        __bf16* dst = patch6 + pix * CP + 4 * c4;
+        *reinterpret_cast<u32x2*>(dst) = h;
+        *reinterpret_cast<u32x2*>(dst + PLANE) = m;
+        *reinterpret_cast<bf16x4*>(dst + 2 * PLANE) = __builtin_convertvector(l, bf16x4);
+      }
+    }
+  }
+  int pbase[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int p = 32 * wave + 16 * mt + l16;
+    pbase[mt] = ((p >> LW) * PW + (p & (W - 1))) * CP;
+  }
+  const __bf16* wl = wsp + (long)l16 * KP + 8 * q;
+  bf16x8 b[2][TN][3];
+  auto bload = [&](int kc, int s) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        b[s][j][pl] = *reinterpret_cast<const bf16x8*>(wl + ((long)pl * BN + 16 * j) * KP + 32 * kc);
+  };
+  f32x4 acc[2][TN];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bload(0, 0);
+  __syncthreads();
+  auto chunk = [&](int kc, int s) {
+    if (kc + 1 < NKC) bload(kc + 1, s ^ 1);
+    int k0 = 32 * kc + 8 * q;
+    k0 = k0 < K ? k0 : K - 8;  // past K: any in-patch address (the weight is zero there)
+    const int tap = k0 / CI, c0 = k0 - tap * CI, ky = tap / KS, kx = tap - ky * KS;
+    const int off = (ky * PW + kx) * CP + c0;
+    bf16x8 a[2][3];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) a[mt][pl] = *reinterpret_cast<const bf16x8*>(patch6 + pl * PLANE + pbase[mt] + off);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x4 c = acc[mt][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][2], b[s][j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][1], b[s][j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][0], b[s][j][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][1], b[s][j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][0], b[s][j][1], c, 0, 0, 0);
+        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][0], b[s][j][0], c, 0, 0, 0);
+      }
+  };
+  int kc = 0;
+  for (; kc + 2 <= NKC; kc += 2) {
+    chunk(kc, 0);
+    chunk(kc + 1, 1);
+  }
+  if (kc < NKC) chunk(kc, 0);
+  __syncthreads();  // every wave is done reading the patch
+  pool_epilogue<BN, 32>(acc, reinterpret_cast<float*>(patch6), g, G, LW, lhw, bm0, nw, pooled, amax, y, rstd, eps,
+                        nchw_flat);
+}
+
+// [plane][n][KP] three-way split-bf16 image (gemm6_core.h split) of a (rows, K) fp32 matrix, zero past K
+__global__ __launch_bounds__(256) void split3_weight(const float* __restrict__ w, __bf16* __restrict__ out, int rows,
+                                                     int K, int KP) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)rows * KP) return;
+  const int r = (int)(i / KP), k = (int)(i % KP);
+  const float v = k < K ? w[(long)r * K + k] : 0.f;
+  const __bf16 a0 = (__bf16)v;
+  const float r1 = v - (float)a0;
+  const __bf16 a1 = (__bf16)r1;
+  const long pl = (long)rows * KP;
+  out[i] = a0;
+  out[pl + i] = a1;
+  out[2 * pl + i] = (__bf16)(r1 - (float)a1);
+}
+
 // Direct forward for the 4-channel (padded RGB) first stage: K = 25 taps x 4 channels, so one
 // v_mfma_f32_16x16x4_f32 step is exactly one tap (lane (l16, q) supplies channel q of pixel l16's tap sample) and
 // nothing is padded to a 32-wide k tile. The whole weight (BN x 100 floats) lives in registers (each lane keeps its
@@ -834,6 +957,125 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad3(GemmArgs g, Geom G, int lw
   f32x4 acc[2][BN / 16];
   sdb::gemm3_mainloop<BM, BN, 32, BN>(la, lb, 0, g.K, acc);
   sdb::gemm3_epilogue<BM, BN, 32, BN>(g, acc, bm0, 0, 0, 0);
+}
+
+// bwd-data as a DIRECT convolution on split-bf16 MFMAs: conv_dgrad3's contraction (dIn = conv_same(dOut, flipped W),
+// K = (ky, kx, c) with c contiguous), but each workgroup stages its dOut patch (R image rows + the kh-1 / kw-1 halo,
+// zero outside the image) ONCE in LDS, split to (hi, lo) bf16 planes on the way in, and every tap reads its shifted
+// window from there: each dOut element is loaded and split once per workgroup instead of once per tap it feeds
+// (conv_dgrad3's im2col staging re-split it up to kh*kw times: VALU-bound, 0.2 of the bf16x3 peak). The B operand
+// comes pre-split ([plane][n][KP] bf16, sd_conv_split_weight) straight from global memory (L2-resident, 16 B per lane
+// per plane), one k chunk ahead. M = R*W output pixels per workgroup (128), 4 waves x 2 16-pixel tiles, NT 16-channel
+// tiles of dIn; per 32-deep k chunk a lane's 8 k values are 8 consecutive channels of one tap (CIN % 8 == 0), one
+// ds_read_b128 per plane. Products: lo_a*hi_b + hi_a*lo_b + hi_a*hi_b (gemm3_mainloop's order), f32 accumulation.
+template <int CIN, int NT, int LW, int KS>
+__global__ __launch_bounds__(256, 2) void conv_dgrad3_direct(const float* __restrict__ dout,
+                                                              const __bf16* __restrict__ wsp, float* __restrict__ din,
+                                                              int Nb, int H, int pad) {
+  constexpr int W = 1 << LW, R = 128 / W, PH = R + KS - 1, PW = W + KS - 1, CP = CIN + 8;
+  constexpr int PLANE = PH * PW * CP, K = KS * KS * CIN, NKC = (K + 31) / 32, KP = NKC * 32, NOUT = 16 * NT;
+  constexpr int CIN4 = CIN / 4, NEL = PH * PW * CIN4, NE = (NEL + 255) / 256;
+  static_assert(CIN % 8 == 0 && R >= 1 && 128 % W == 0, "geometry");
+  extern __shared__ __attribute__((aligned(16))) __bf16 patch[];  // [plane][PH][PW][CP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, q = lane >> 4;
+  const int rows_per_img = H / R, n = blockIdx.x / rows_per_img, y0 = (blockIdx.x % rows_per_img) * R;
+  // stage the patch: every load first, then split + store
+  {
+    f32x4 v[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int i = tid + 256 * e, c4 = i % CIN4, pix = i / CIN4, pc = pix % PW, pr = pix / PW;
+      const int y = y0 + pr - pad, x = pc - pad;
+      v[e] = (i < NEL && y >= 0 && y < H && x >= 0 && x < W)
+                 ? *reinterpret_cast<const f32x4*>(dout + (((long)n * H + y) * W + x) * CIN + 4 * c4)
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int i = tid + 256 * e;
+      if (i < NEL) {
+        const int c4 = i % CIN4, pix = i / CIN4;
+        sdb::bf16x4 hi, lo;
+        sdb::split2(v[e], hi, lo);
+        *reinterpret_cast<sdb::bf16x4*>(patch + pix * CP + 4 * c4) = hi;
+        *reinterpret_cast<sdb::bf16x4*>(patch + PLANE + pix * CP + 4 * c4) = lo;
+      }
+    }
+  }
+  // this lane's two pixel tiles: pixel p = 32 wave + 16 mt + l16 -> patch-local (row, x)
+  int pbase[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int p = 32 * wave + 16 * mt + l16;
+    pbase[mt] = ((p >> LW) * PW + (p & (W - 1))) * CP;
+  }
+  const __bf16* wh = wsp + (long)l16 * KP + 8 * q;
+  const __bf16* wl = wh + (long)NOUT * KP;
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  bf16x8 bh[2][NT], bl[2][NT];
+  auto bload = [&](int kc, int s) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      bh[s][j] = *reinterpret_cast<const bf16x8*>(wh + (long)16 * j * KP + 32 * kc);
+      bl[s][j] = *reinterpret_cast<const bf16x8*>(wl + (long)16 * j * KP + 32 * kc);
+    }
+  };
+  f32x4 acc[2][NT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bload(0, 0);
+  __syncthreads();
+  auto chunk = [&](int kc, int s) {
+    if (kc + 1 < NKC) bload(kc + 1, s ^ 1);
+    int k0 = 32 * kc + 8 * q;
+    k0 = k0 < K ? k0 : K - 8;  // past K: any in-patch address (B is zero there)
+    const int tap = k0 / CIN, c0 = k0 - tap * CIN, ky = tap / KS, kx = tap - ky * KS;
+    const int off = (ky * PW + kx) * CP + c0;
+    bf16x8 ah[2], al[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      ah[mt] = *reinterpret_cast<const bf16x8*>(patch + pbase[mt] + off);
+      al[mt] = *reinterpret_cast<const bf16x8*>(patch + PLANE + pbase[mt] + off);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mt], bh[s][j], acc[mt][j], 0, 0, 0);
+        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bl[s][j], acc[mt][j], 0, 0, 0);
+        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bh[s][j], acc[mt][j], 0, 0, 0);
+      }
+  };
+  int kc = 0;
+  for (; kc + 2 <= NKC; kc += 2) {
+    chunk(kc, 0);
+    chunk(kc + 1, 1);
+  }
+  if (kc < NKC) chunk(kc, 0);
+  // acc[mt][j][r]: pixel 32 wave + 16 mt + 4 q + r, channel 16 j + l16
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int p = 32 * wave + 16 * mt + 4 * q + r, y = y0 + (p >> LW), x = p & (W - 1);
+      float* o = din + (((long)n * H + y) * W + x) * NOUT + l16;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) o[16 * j] = acc[mt][j][r];
+    }
+}
+
+// [plane][n][KP] bf16 split image of a (rows, K) fp32 matrix, KP = K rounded up to 32, zero past K
+__global__ __launch_bounds__(256) void split_weight(const float* __restrict__ w, __bf16* __restrict__ out, int rows,
+                                                    int K, int KP) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)rows * KP) return;
+  const int r = (int)(i / KP), k = (int)(i % KP);
+  const float v = k < K ? w[(long)r * K + k] : 0.f;
+  const __bf16 hi = (__bf16)v;
+  out[i] = hi;
+  out[(long)rows * KP + i] = (__bf16)(v - (float)hi);
 }
 
 // out[e] = sum_s ws[s * n + e] in a fixed order; 64 outputs per workgroup (one per lane), the 4 waves take every
@@ -1667,6 +1909,96 @@ extern "C" int sd_conv2d_dgrad_bf16x3(const float* dout, const float* wflip, flo
   }
   SD_LAUNCH_CHECK();
   return SD_OK;
+}
+
+extern "C" int sd_conv_split3_weight(const float* w, void* wsplit, int rows, int K, sd_stream stream_) {
+  if (rows <= 0 || K <= 0 || !w || !wsplit) return SD_EARG;
+  const int KP = (K + 31) / 32 * 32;
+  const long total = (long)rows * KP;
+  split3_weight<<<(int)((total + 255) / 256), 256, 0, (hipStream_t)stream_>>>(w, static_cast<__bf16*>(wsplit), rows,
+                                                                               K, KP);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+namespace {
+template <int BN, int CI, int LW>
+int fwd6_launch(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, const float* nw, float* pooled,
+                uint8_t* amax, float* y, float* rstd, float eps, int nchw_flat, hipStream_t s) {
+  constexpr int W = 1 << LW, R = 128 / W, KS = 5;
+  const size_t lds = (size_t)3 * (R + KS - 1) * (W + KS - 1) * (CI + 8) * 2;
+  static bool raised = false;
+  if (!raised && lds > 65536) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_fwd6_direct_pool<BN, CI, LW, KS>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return SD_EARG;
+    raised = true;
+  }
+  conv_fwd6_direct_pool<BN, CI, LW, KS><<<g.M / 128, 256, lds, s>>>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps,
+                                                                   nchw_flat);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+}  // namespace
+
+extern "C" int sd_conv2d_fwd_pool6(const float* in, const void* wsplit3, const float* bias, const float* nw,
+                                   float* pooled, uint8_t* amax, float* y, float* rstd, int Nb, int Hs, int Ws, int Ci,
+                                   int Co, int kh, int kw, int pad, float eps, int nchw_flat, sd_stream stream_) {
+  hipStream_t s = (hipStream_t)stream_;
+  if (Nb <= 0) return SD_OK;
+  if (kh != 5 || kw != 5 || pad != 2 || Hs != Ws || Hs % 2 || !al16(in) || !al16(wsplit3)) return SD_ESHAPE;
+  Geom G{in, Nb, Hs, Ws, Ci, Hs, Ws, kh, kw, pad, 0};
+  GemmArgs g{};
+  g.bias = bias; g.M = Nb * Hs * Ws; g.N = Co; g.K = kh * kw * Ci;
+  const int lhw = ilog2_exact(Hs * Ws);
+  if (lhw < 0 || g.M % 128) return SD_ESHAPE;
+  const __bf16* wsp = static_cast<const __bf16*>(wsplit3);
+  // a 128-pixel tile is 128 / Ws whole rows of one image
+  if (Co == 48 && Ci == 32 && Ws == 32)
+    return fwd6_launch<48, 32, 5>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps, nchw_flat, s);
+  if (Co == 64 && Ci == 48 && Ws == 16)
+    return fwd6_launch<64, 48, 4>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps, nchw_flat, s);
+  return SD_ESHAPE;
+}
+
+extern "C" int sd_conv_split_weight(const float* w, void* wsplit, int rows, int K, sd_stream stream_) {
+  if (rows <= 0 || K <= 0 || !w || !wsplit) return SD_EARG;
+  const int KP = (K + 31) / 32 * 32;
+  const long total = (long)rows * KP;
+  split_weight<<<(int)((total + 255) / 256), 256, 0, (hipStream_t)stream_>>>(w, static_cast<__bf16*>(wsplit), rows, K,
+                                                                              KP);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+namespace {
+template <int CIN, int NT, int LW>
+int dgrad_direct_launch(const float* dout, const __bf16* wsp, float* din, int Nb, int H, int pad, hipStream_t s) {
+  constexpr int W = 1 << LW, R = 128 / W, KS = 5;
+  const size_t lds = (size_t)2 * (R + KS - 1) * (W + KS - 1) * (CIN + 8) * 2;
+  static bool raised = false;
+  if (!raised && lds > 65536) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_dgrad3_direct<CIN, NT, LW, KS>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return SD_EARG;
+    raised = true;
+  }
+  conv_dgrad3_direct<CIN, NT, LW, KS><<<Nb * (H / R), 256, lds, s>>>(dout, wsp, din, Nb, H, pad);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+}  // namespace
+
+extern "C" int sd_conv2d_dgrad_direct(const float* dout, const void* wsplit, float* din, int Nb, int Hs, int Ws,
+                                      int Ci, int Co, int kh, int kw, int pad, sd_stream stream_) {
+  hipStream_t s = (hipStream_t)stream_;
+  if (Nb <= 0) return SD_OK;
+  if (kh != 5 || kw != 5 || pad != 2 || Hs != Ws || !al16(dout) || !al16(wsplit) || !al16(din)) return SD_ESHAPE;
+  const __bf16* wsp = static_cast<const __bf16*>(wsplit);
+  // a workgroup takes 128 / Ws whole rows of one image
+  if (Ci == 48 && Co == 32 && Ws == 32) return dgrad_direct_launch<48, 2, 5>(dout, wsp, din, Nb, Hs, pad, s);
+  if (Ci == 64 && Co == 48 && Ws == 16) return dgrad_direct_launch<64, 3, 4>(dout, wsp, din, Nb, Hs, pad, s);
+  return SD_ESHAPE;
 }
 
 extern "C" int sd_conv2d_wgrad_bf16x3_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int ups) {

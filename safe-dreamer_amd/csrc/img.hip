@@ -805,8 +805,8 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
 // gemm16_mainloop_fp order at one 16-column tile per wave), the same bias / 16-column row-partial epilogue
 // (ep_bias_part) and the same rstd summation order (wg_rstd). B fragments come straight from global memory (each
 // wave owns its columns: nothing to share through LDS), three k tiles in flight.
-#ifndef SD_FUSED_ACTOR
-#define SD_FUSED_ACTOR 1
+#ifndef SD_FUSED_ACTOR  // measured slower (imagination alone 2.57 -> 2.68 ms): 64 workgroups are MFMA-bound
+#define SD_FUSED_ACTOR 0
 #endif
 constexpr int FA_LD = 256 + 4;  // LDS row stride of the 16 x 256 activation panels (floats)
 template <int NJ>
@@ -996,8 +996,8 @@ __global__ __launch_bounds__(256) void k_actor(sd_imagine d, const float* X, con
 // row tile recomputes the tile's hidden rows (whole rows: the next norm needs them), then its logit columns (wave wc:
 // SK / NCT / 4 columns), then samples them by teams of KD lanes as k_prior does. Bit-identical to the unfused launches
 // (fa_layer's k order, ep_bias_part's partials, wg_rstd's sums). grid (NCT, N / 16).
-#ifndef SD_FUSED_PRIOR
-#define SD_FUSED_PRIOR 1
+#ifndef SD_FUSED_PRIOR  // measured slower (2.68 -> 2.85 ms with the fused actor): 4x recomputed hidden layer
+#define SD_FUSED_PRIOR 0
 #endif
 #ifndef SD_PRIOR_NCT
 #define SD_PRIOR_NCT 4

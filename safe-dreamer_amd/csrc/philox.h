@@ -35,6 +35,9 @@ __device__ __forceinline__ sd_u32x4 sd_philox4x32_10(uint32_t c0, uint32_t c1, u
 __device__ __forceinline__ double sd_u01(uint32_t w) { return ((double)(w >> 8) + 0.5) * (1.0 / 16777216.0); }
 
 __device__ __forceinline__ float sd_gumbel(uint64_t seed, uint32_t stream, uint32_t step, uint64_t idx) {
+#ifdef SD_TIMING_CHEAP_NOISE  // measurement-only build (tools/ab_variants.sh): what the noise costs the chains
+  return (float)((idx * 2654435761u + step) & 1023u) * 1e-3f;
+#endif
   const uint64_t q = idx >> 2;
   sd_u32x4 r = sd_philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), step, stream, (uint32_t)seed,
                                 (uint32_t)(seed >> 32));
@@ -45,6 +48,9 @@ __device__ __forceinline__ float sd_gumbel(uint64_t seed, uint32_t stream, uint3
 }
 
 __device__ __forceinline__ float sd_normal(uint64_t seed, uint32_t stream, uint32_t step, uint64_t idx) {
+#ifdef SD_TIMING_CHEAP_NOISE
+  return (float)((idx * 2654435761u + step) & 1023u) * 1e-3f - 0.5f;
+#endif
   sd_u32x4 r = sd_philox4x32_10((uint32_t)idx, (uint32_t)(idx >> 32), step, stream, (uint32_t)seed,
                                 (uint32_t)(seed >> 32));
   const double u1 = sd_u01(r.x), u2 = sd_u01(r.y);

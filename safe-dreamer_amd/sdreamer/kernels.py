@@ -451,9 +451,10 @@ def conv2d_fwd(x, w, b, ups=0, pad=None, out=None):
     return out
 
 
-def conv2d_dgrad(dout, w, pad=None, fast=True):
+def conv2d_dgrad(dout, w, pad=None, fast=True, direct=True):
     """Input gradient of a stride-1 conv: conv_same(dOut, flipped W). dout (Nb, H, W, Co), w (Co, kh, kw, Ci) ->
-    (Nb, H, W, Ci). fast: split-bf16 MFMA kernel (sd_conv2d_dgrad_bf16x3) where its shape constraints hold."""
+    (Nb, H, W, Ci). fast: split-bf16 MFMA kernels where their shape constraints hold — the direct kernel
+    (sd_conv2d_dgrad_direct) first unless direct=False, then the implicit GEMM (sd_conv2d_dgrad_bf16x3)."""
     Co, kh, kw, Ci = w.shape
     pad = kh - 1 - (kh - 1) // 2 if pad is None else pad
     wf = _FLIP.get(w.data_ptr())
@@ -462,6 +463,13 @@ def conv2d_dgrad(dout, w, pad=None, fast=True):
     if fast and FAST_GEMM:
         Nb, H, W, _ = dout.shape
         din = torch.empty(Nb, H, W, Ci, dtype=torch.float32, device=dout.device)
+        if direct and DIRECT_DGRAD:  # the dOut patch staged once per workgroup (same products and order per k)
+            ws = _SPLIT.get(w.data_ptr())
+            if ws is None:
+                ws = conv_split_weight(wf)
+            if nat.call_shaped("sd_conv2d_dgrad_direct", p(_c(dout)), p(ws), p(din), Nb, H, W, Co, Ci, kh, kw, pad,
+                               stream()):
+                return din
         if nat.call_shaped("sd_conv2d_dgrad_bf16x3", p(_c(dout)), p(wf), p(din), Nb, H, W, Co, Ci, kh, kw, pad,
                            stream()):
             return din
@@ -520,6 +528,12 @@ def conv2d_wgrad_pool(x, dpool, amax, kh, kw, pad=None):
 
 
 _FLIP = {}  # weight data_ptr -> flipped weight, built ahead of the backward (set_flip_cache)
+_SPLIT = {}  # weight data_ptr -> split-bf16 image of the flipped weight (sd_conv_split_weight), same lifetime
+# SDREAMER_CONV6=0: the encoder stages' forward on the exact f32 MFMA kernels instead of the fp32-accurate three-way
+# split-bf16 direct kernel (sd_conv2d_fwd_pool6; A/B and parity knob)
+CONV6 = os.environ.get("SDREAMER_CONV6", "1") != "0"
+# SDREAMER_DIRECT_DGRAD=0: the encoder's bwd-data on the implicit-GEMM split-bf16 kernel (A/B knob)
+DIRECT_DGRAD = os.environ.get("SDREAMER_DIRECT_DGRAD", "1") != "0"
 
 
 def set_flip_cache(weights):
@@ -527,13 +541,27 @@ def set_flip_cache(weights):
     the imagined returns, off the encoder backward's chain); valid until clear_flip_cache (the optimizer step changes
     the weights). Returns the flipped tensors (the caller keeps them alive)."""
     _FLIP.clear()
+    _SPLIT.clear()
     for w in weights:
         _FLIP[w.data_ptr()] = conv_flip_weight(w)
-    return list(_FLIP.values())
+        if FAST_GEMM and DIRECT_DGRAD:
+            _SPLIT[w.data_ptr()] = conv_split_weight(_FLIP[w.data_ptr()])
+    return list(_FLIP.values()) + list(_SPLIT.values())
 
 
 def clear_flip_cache():
     _FLIP.clear()
+    _SPLIT.clear()
+
+
+def conv_split_weight(wf):
+    """[plane][Ci][KP] bf16 (hi, lo) image of a flipped weight wf (Ci, kh, kw, Co), KP = kh*kw*Co rounded up to 32
+    (sd_conv_split_weight), the B operand of sd_conv2d_dgrad_direct; held as int16 storage."""
+    rows, K = wf.shape[0], wf[0].numel()
+    KP = -(-K // 32) * 32
+    ws = torch.empty(2 * rows * KP, dtype=torch.int16, device=wf.device)
+    nat.call("sd_conv_split_weight", p(_c(wf)), p(ws), rows, K, stream())
+    return ws
 
 
 def conv_flip_weight(w):
@@ -587,6 +615,13 @@ def conv2d_fwd_pool(x, w, b, nw, nchw_flat=False):
     amax = torch.empty(Nb, H // 2, W // 2, Co, dtype=torch.uint8, device=x.device)
     y = torch.empty_like(pooled)
     rstd = torch.empty(Nb, H // 2, W // 2, dtype=torch.float32, device=x.device)
+    if CONV6:  # fp32-accurate three-way split-bf16 direct kernel where instantiated
+        K = kh * kw * Ci
+        ws = torch.empty(3 * Co * (-(-K // 32) * 32), dtype=torch.int16, device=x.device)
+        nat.call("sd_conv_split3_weight", p(_c(w)), p(ws), Co, K, stream())
+        if nat.call_shaped("sd_conv2d_fwd_pool6", p(_c(x)), p(ws), p(b), p(nw), p(pooled), p(amax), p(y), p(rstd),
+                           Nb, H, W, Ci, Co, kh, kw, (kh - 1) // 2, EPS, int(nchw_flat), stream()):
+            return y, pooled, amax, rstd
     ok = nat.call_shaped("sd_conv2d_fwd_pool", p(_c(x)), p(_c(w)), p(b), p(nw), p(pooled), p(amax), p(y), p(rstd),
                          Nb, H, W, Ci, Co, kh, kw, (kh - 1) // 2, EPS, int(nchw_flat), stream())
     return (y, pooled, amax, rstd) if ok else None

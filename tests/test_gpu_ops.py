@@ -251,12 +251,14 @@ def test_conv_pool_norm(ci, co, hw, nb):
 
 @pytest.mark.parametrize("ci,co,hw,nb,nchw", [(4, 32, 64, 2, False), (32, 48, 32, 4, True), (48, 64, 16, 8, False),
                                              (64, 16, 8, 16, True), (16, 64, 8, 2, True)])
-def test_conv_pool_fused_matches_two_launches(ci, co, hw, nb, nchw):
+def test_conv_pool_fused_matches_two_launches(ci, co, hw, nb, nchw, monkeypatch):
     """sd_conv2d_fwd_pool vs sd_conv2d_fwd + sd_pool_rms_fwd: same k order (the implicit-GEMM kernels and the stage-2
     direct kernel), so the pooled values and argmax are bit-exact; rstd / y differ only in the channel-sum order
     (1e-6 relative). The 4-channel direct kernel (stage 1) contracts one tap per MFMA step instead of the 32-wide
-    k tiles' interleave: pooled within 1e-6, argmax equal except on near-ties."""
+    k tiles' interleave: pooled within 1e-6, argmax equal except on near-ties. (The f32 kernels: the bf16x6 direct
+    kernel has its own test below.)"""
     from sdreamer import kernels as K
+    monkeypatch.setattr(K, "CONV6", False)
     x = (torch.rand(nb, hw, hw, ci, generator=_g(ci)) - 0.5).to(DEV)
     w = (torch.randn(co, 5, 5, ci, generator=_g(co)) / (ci * 25) ** 0.5).to(DEV)
     b = (0.1 * torch.randn(co, generator=_g(1))).to(DEV)
@@ -573,6 +575,54 @@ def test_conv_backward_bf16x3(ci, co, hw, nb):
     assert ((dw - dw_ref).abs() - bound).max().item() <= 0, "wgrad"
     if K.nat.fns["sd_conv2d_wgrad_bf16x3_slabs"](nb, hw, hw, ci, co, 5, 5, 0) > 0:  # the split kernel's range
         assert (dw - dw_ref).abs().max().item() > 0, "wgrad took the f32 path"
+
+
+@pytest.mark.parametrize("ci,co,hw,nb,nchw", [(32, 48, 32, 4, False), (48, 64, 16, 8, True), (48, 64, 16, 1, False)])
+def test_conv_pool_bf16x6_matches_f32(ci, co, hw, nb, nchw, monkeypatch):
+    """The encoder stage forward on the three-way split-bf16 direct kernel (sd_conv2d_fwd_pool6) against the exact
+    f32 kernel: an fp32-accurate contraction (each product's dropped terms <= 2^-26 |ab|), so the conv outputs agree
+    to fp32 rounding: |pooled - ref| <= 2e-6 * (the same contraction on |x|, |w|) + 1e-7; argmax equal except where
+    the window's top two conv outputs are that close; NaN inputs propagate the same way."""
+    from sdreamer import kernels as K
+    x = (torch.rand(nb, hw, hw, ci, generator=_g(ci)) - 0.5).to(DEV)
+    w = (torch.randn(co, 5, 5, ci, generator=_g(co)) / (ci * 25) ** 0.5).to(DEV)
+    b = (0.1 * torch.randn(co, generator=_g(1))).to(DEV)
+    nw = (1 + 0.1 * torch.randn(co, generator=_g(2))).to(DEV)
+    x[0, 1, 1, 0] = float("nan")
+    monkeypatch.setattr(K, "CONV6", True)
+    six = K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)
+    monkeypatch.setattr(K, "CONV6", False)
+    ref = K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)
+    conv_abs = K.conv2d_fwd(x.abs().nan_to_num(), w.abs(), None)  # (nb, hw, hw, co) bound operand
+    bound = 2e-6 * F.max_pool2d(conv_abs.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1) + 1e-7
+    y6, p6, a6, r6 = six
+    yr, pr, ar, rr = ref
+    assert torch.equal(p6.isnan(), pr.isnan()) and torch.equal(y6.isnan(), yr.isnan())
+    assert ((p6 - pr).nan_to_num().abs() - bound).max().item() <= 0, "pooled"
+    assert (p6 - pr).nan_to_num().abs().max().item() > 0, "pool6 took the f32 path"
+    assert (a6 == ar).float().mean().item() > 0.999, "amax"
+    close(r6.nan_to_num(), rr.nan_to_num(), 1e-5, "rstd")
+    close(y6.nan_to_num(), yr.nan_to_num(), 1e-5, "y")
+
+
+@pytest.mark.parametrize("cd,ci,hw,nb", [(48, 32, 32, 8), (64, 48, 16, 16), (48, 32, 32, 1)])
+def test_conv_dgrad_direct_matches_implicit_gemm(cd, ci, hw, nb):
+    """The direct bwd-data kernel (sd_conv2d_dgrad_direct: dOut patch staged once per workgroup) against the
+    implicit-GEMM one (sd_conv2d_dgrad_bf16x3): the same (hi, lo) splits, the same three products per k and the same k
+    order, so bit for bit the same dIn; and both within the split-bf16 bound of the f32 kernel."""
+    from sdreamer import kernels as K
+    w = (torch.randn(cd, 5, 5, ci, generator=_g(cd + ci)) / (ci * 25) ** 0.5).to(DEV)
+    dy = torch.randn(nb, hw, hw, cd, generator=_g(hw)).to(DEV)
+    wf = K.conv_flip_weight(w)
+    ws = K.conv_split_weight(wf)
+    dx = torch.empty(nb, hw, hw, ci, device=DEV)
+    assert K.nat.call_shaped("sd_conv2d_dgrad_direct", K.p(dy), K.p(ws), K.p(dx), nb, hw, hw, cd, ci, 5, 5, 2,
+                             K.stream()), "direct kernel not instantiated for this shape"
+    dx_gemm = K.conv2d_dgrad(dy, w, fast=True, direct=False)
+    assert torch.equal(dx, dx_gemm)
+    dx_ref = K.conv2d_dgrad(dy, w, fast=False)
+    bound = 4e-5 * K.conv2d_dgrad(dy.abs(), w.abs(), fast=False) + 1e-6
+    assert ((dx - dx_ref).abs() - bound).max().item() <= 0
 
 
 @pytest.mark.parametrize("ci,co,hw,nb", [(4, 32, 64, 3), (32, 48, 32, 2)])
