@@ -453,8 +453,10 @@ typedef struct sd_imagine {
 int sd_imagine_work_floats(const sd_imagine* d);
 int sd_imagine_run(const sd_imagine* d, sd_stream stream);
 /* Measurement aid (bench.py roofline): one launch of step t's largest contractions exactly as sd_imagine_run issues
- * them, after a run on the same descriptor/workspace (idempotent): which = 0: img_net_0 + _dyn_in0 + actor layer 0's
- * deter part (three (N, D) x (D, U) GEMMs, k_lin), 1: _dyn_hid (k_hid), 2: _dyn_gru + GRU (k_gate). 0 <= t < H1 - 1. */
+ * them, after a run on the same descriptor/workspace: which = 0: img_net_0 + _dyn_in0 + actor layer 0's deter part
+ * (three (N, D) x (D, U) GEMMs, k_lin), 1: _dyn_hid (k_hid), 2: _dyn_gru + GRU (k_gate). 0 <= t < H1 - 1. Launches 0
+ * and 1 rewrite workspace values only; launch 2 reads the workspace's last _dyn_hid output and writes feats(t + 1)'s
+ * deter, so only t = H1 - 2 reproduces the run's values (other t overwrite the trajectory: time it, keep no output). */
 int sd_imagine_step_kernel(const sd_imagine* d, int which, int t, sd_stream stream);
 
 /* InfoNCE representation loss (dreamer.py:533-542): cross_entropy(logits - rowmax(logits), arange) on an (n, ncol)

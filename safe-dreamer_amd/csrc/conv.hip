@@ -1009,15 +1009,24 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad3_direct(const float* __rest
     const int p = 32 * wave + 16 * mt + l16;
     pbase[mt] = ((p >> LW) * PW + (p & (W - 1))) * CP;
   }
-  const __bf16* wh = wsp + (long)l16 * KP + 8 * q;
-  const __bf16* wl = wh + (long)NOUT * KP;
+  // B: one k chunk of the pre-split weight ([plane][NOUT][32] bf16, 16-B pieces) per LDS stage, double-buffered and
+  // shared by the 4 waves (each wave reading its fragments from global memory itself made the L1 path the bound)
   typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-  bf16x8 bh[2][NT], bl[2][NT];
-  auto bload = [&](int kc, int s) {
+  constexpr int BROW = 40, SB = 2 * NOUT * BROW, NPC = 8 * NOUT, NPT = (NPC + 255) / 256;
+  __bf16* bst = patch + 2 * PLANE;
+  bf16x8 br[NPT];
+  auto bload = [&](int kc) {
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      bh[s][j] = *reinterpret_cast<const bf16x8*>(wh + (long)16 * j * KP + 32 * kc);
-      bl[s][j] = *reinterpret_cast<const bf16x8*>(wl + (long)16 * j * KP + 32 * kc);
+    for (int u = 0; u < NPT; ++u) {
+      const int i = tid + 256 * u;
+      if (i < NPC) br[u] = *reinterpret_cast<const bf16x8*>(wsp + (long)(i >> 2) * KP + 32 * kc + 8 * (i & 3));
+    }
+  };
+  auto bstore = [&](int stage) {
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int i = tid + 256 * u;
+      if (i < NPC) *reinterpret_cast<bf16x8*>(bst + stage * SB + (i >> 2) * BROW + 8 * (i & 3)) = br[u];
     }
   };
   f32x4 acc[2][NT];
@@ -1025,10 +1034,18 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad3_direct(const float* __rest
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bload(0, 0);
+  bload(0);
+  bstore(0);
+  if (NKC > 1) bload(1);
   __syncthreads();
-  auto chunk = [&](int kc, int s) {
-    if (kc + 1 < NKC) bload(kc + 1, s ^ 1);
+  for (int kc = 0; kc < NKC; ++kc) {
+    const __bf16* bs = bst + (kc & 1) * SB + l16 * BROW + 8 * q;
+    bf16x8 bh[NT], bl[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(bs + 16 * j * BROW);
+      bl[j] = *reinterpret_cast<const bf16x8*>(bs + (NOUT + 16 * j) * BROW);
+    }
     int k0 = 32 * kc + 8 * q;
     k0 = k0 < K ? k0 : K - 8;  // past K: any in-patch address (B is zero there)
     const int tap = k0 / CIN, c0 = k0 - tap * CIN, ky = tap / KS, kx = tap - ky * KS;
@@ -1039,21 +1056,18 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad3_direct(const float* __rest
       ah[mt] = *reinterpret_cast<const bf16x8*>(patch + pbase[mt] + off);
       al[mt] = *reinterpret_cast<const bf16x8*>(patch + PLANE + pbase[mt] + off);
     }
+    if (kc + 1 < NKC) bstore((kc + 1) & 1);  // chunk kc+1 (loaded one iteration ago) into the other stage
+    if (kc + 2 < NKC) bload(kc + 2);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mt], bh[s][j], acc[mt][j], 0, 0, 0);
-        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bl[s][j], acc[mt][j], 0, 0, 0);
-        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bh[s][j], acc[mt][j], 0, 0, 0);
+        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mt], bh[j], acc[mt][j], 0, 0, 0);
+        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bl[j], acc[mt][j], 0, 0, 0);
+        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bh[j], acc[mt][j], 0, 0, 0);
       }
-  };
-  int kc = 0;
-  for (; kc + 2 <= NKC; kc += 2) {
-    chunk(kc, 0);
-    chunk(kc + 1, 1);
+    __syncthreads();
   }
-  if (kc < NKC) chunk(kc, 0);
   // acc[mt][j][r]: pixel 32 wave + 16 mt + 4 q + r, channel 16 j + l16
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -1975,7 +1989,7 @@ namespace {
 template <int CIN, int NT, int LW>
 int dgrad_direct_launch(const float* dout, const __bf16* wsp, float* din, int Nb, int H, int pad, hipStream_t s) {
   constexpr int W = 1 << LW, R = 128 / W, KS = 5;
-  const size_t lds = (size_t)2 * (R + KS - 1) * (W + KS - 1) * (CIN + 8) * 2;
+  const size_t lds = (size_t)2 * (R + KS - 1) * (W + KS - 1) * (CIN + 8) * 2 + (size_t)2 * 2 * (16 * NT) * 40 * 2;
   static bool raised = false;
   if (!raised && lds > 65536) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_dgrad3_direct<CIN, NT, LW, KS>),

@@ -477,6 +477,9 @@ __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
 // of CPG rows of W1^T: the NG = S / CPG slabs of a row sum (in k_hid's prologue, fixed order) to the dense product.
 // That removes the x1p k_slab launch from every step (4 dependent launches per step instead of 5).
 constexpr int LR_NG = 4;  // slabs of x1p (== KSM: k_hid sums up to KSM slabs)
+#ifndef LR_STAGE
+#define LR_STAGE 1
+#endif
 template <int KD, int CPG>
 __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int t) {
   constexpr int NC = CPG * KD, TPC = NTHR / NC, KPT = UH / TPC, NQ = KPT / 4;
@@ -487,6 +490,18 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int B = d.B, SK = d.SK, S = SK / KD, g = blockIdx.x, b = blockIdx.y, n0 = g * NC;
   const long tBU = (long)t * B * UH;
+  // the gather's candidate rows — W1^T rows n0 .. n0 + NC (the group's categoricals x every index) — are loaded
+  // before the sample exists and staged in LDS (LR_STAGE: NC x U floats), so the gather after the sampler is an LDS
+  // read instead of a dependent global round trip
+  constexpr bool STAGE = LR_STAGE && NC * UH * 4 <= 131072;
+  constexpr int NW1 = STAGE ? NC * UH / 4 / NTHR : 1;
+  extern __shared__ __attribute__((aligned(16))) float w1s[];
+  f32x4 w1r[NW1];
+  const bool more = t + 1 < d.T;
+  if (STAGE && more) {
+#pragma unroll
+    for (int i = 0; i < NW1; ++i) w1r[i] = ld4(w.w1t + (long)n0 * UH + 4 * (tid + NTHR * i));
+  }
   // independent of the contraction: the column's weight slice, bias, noise, reset mask
   const int col = tid / TPC, kp = tid % TPC;
   f32x4 wv[NQ];
@@ -565,14 +580,18 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
       hv[tid / KD] = yv;
     }
   }
-  if (t + 1 >= d.T) return;
+  if (!more) return;
+  if (STAGE) {
+#pragma unroll
+    for (int i = 0; i < NW1; ++i) *reinterpret_cast<f32x4*>(w1s + 4 * (tid + NTHR * i)) = w1r[i];
+  }
   __syncthreads();
   if (tid < UH) {  // slab g of x1p[t+1]: sum over the group's categoricals of v_s * W1^T[hot_s]
     float v = 0.f;
     if (!rnext) {
       float wr[CPG];
 #pragma unroll
-      for (int s = 0; s < CPG; ++s) wr[s] = w.w1t[(long)(n0 + hot[s]) * UH + tid];
+      for (int s = 0; s < CPG; ++s) wr[s] = STAGE ? w1s[hot[s] * UH + tid] : w.w1t[(long)(n0 + hot[s]) * UH + tid];
 #pragma unroll
       for (int s = 0; s < CPG; ++s) v = fmaf(hv[s], wr[s], v);
     }
@@ -1055,7 +1074,12 @@ int fwd_phase(const sd_rssm_scan& d, const Work& w, bool lrows, int which, int t
     SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, np), NTHR, core1, st>>>(po, px, B, UH, span_d));
   } else if (lrows) {
     const dim3 gr(LR_NG, B);
-#define SD_LR(KD_, CPG_) k_logit_rows<KD_, CPG_><<<gr, NTHR, 0, st>>>(d, w, t)
+#define SD_LR(KD_, CPG_)                                                                                 \
+  do {                                                                                                    \
+    constexpr size_t lds = LR_STAGE && (size_t)CPG_ * KD_ * UH * 4 <= 131072 ? (size_t)CPG_ * KD_ * UH * 4 : 0; \
+    if (!(raise_lds<k_logit_rows<KD_, CPG_>>(lds))) return SD_EARG;                                       \
+    k_logit_rows<KD_, CPG_><<<gr, NTHR, lds, st>>>(d, w, t);                                              \
+  } while (0)
     if (d.Kd == 16) { if (SK == 512) SD_LR(16, 8); else SD_LR(16, 16); }
     else if (d.Kd == 32) { if (SK == 512) SD_LR(32, 4); else SD_LR(32, 8); }
     else { if (SK == 512) SD_LR(64, 2); else SD_LR(64, 4); }

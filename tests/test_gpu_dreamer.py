@@ -118,6 +118,7 @@ def test_update_matches_reference(name):
         dv = compare_indices(ps.argmax(-1).cpu().numpy(), z[f"u{u}_post_idx"],
                              lambda: post_margins(ref_logit, seed, unimix), f"u{u} posterior indices")
         keep_rows = ~dv
+        report[f"u{u}_post_flips"] = int(dv.sum())
         pdv = pd.detach().cpu().numpy()[..., ::4]
         assert_close(pdv, z[f"u{u}_post_deter"], 1e-4, 1e-5, f"u{u} post_deter", mask=~keep_rows[..., None])
         pl = ag._last["post_logit"].detach().cpu().numpy()
@@ -138,6 +139,8 @@ def test_update_matches_reference(name):
         start_bad = dv.reshape(-1)  # imagination starts from the posterior rows (b, t): a flipped start diverges
         idv = compare_indices(iidx, z[f"u{u}_imag_idx"], imargin, f"u{u} imagined indices")
         idv = idv | start_bad[:, None]
+        report[f"u{u}_imag_flips"] = int(idv.sum())
+        print(name, report, flush=True)  # (on a failure below, the flips so far)
         assert_close(ifeat[..., SK::16], z[f"u{u}_imag_deter"], 1e-4, 1e-5, f"u{u} imag_deter", mask=idv[..., None])
         iact = ag._last["imag_action_tm"].detach().transpose(0, 1).cpu().numpy()
         assert_close(iact, z[f"u{u}_imag_action"], 1e-4, 1e-5, f"u{u} imag_action", mask=idv[..., None])

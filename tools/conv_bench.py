@@ -35,9 +35,22 @@ def main():
         fl = 2.0 * Nb * H * H * Co * 25 * Ci
         wf = K.conv_flip_weight(w)
         nw = torch.ones(Co, device="cuda")
+        ws = K.conv_split_weight(wf)
+        K.set_flip_cache([w])  # the update's state: flipped + split weights cached ahead of the backward
+
+        def fpool6():
+            K.CONV6 = True
+            try:
+                return K.conv2d_fwd_pool(x, w, b, nw)
+            finally:
+                K.CONV6 = False
+
+        del ws
         for name, fn in (("fwd", lambda: K.conv2d_fwd(x, w, b)), ("fpool", lambda: K.conv2d_fwd_pool(x, w, b, nw)),
+                         ("fpool6", fpool6),
                          ("dgrad", lambda: K.conv2d_fwd(dy, wf, None)),
-                         ("dgrad3", lambda: K.conv2d_dgrad(dy, w, pad=2, fast=True)),
+                         ("dgrad3", lambda: K.conv2d_dgrad(dy, w, pad=2, fast=True, direct=False)),
+                         ("dgrad3d", lambda: K.conv2d_dgrad(dy, w, pad=2, fast=True)),
                          ("wgrad", lambda: K.conv2d_wgrad(x, dy, 5, 5, fast=False)),
                          ("wgrad3", lambda: K.conv2d_wgrad(x, dy, 5, 5, fast=True))):
             us = timeit(fn)
