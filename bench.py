@@ -214,7 +214,7 @@ def wm_loss_parity_full(name="C2_walker_r2"):
 # The committed kernel table of this build (tools/profile_round.sh -> tools/kernel_table.py: the rocprofv3 kernel trace
 # of a bench run, windowed to its timed steps, joined with the separate --pmc passes). Named explicitly, never "the
 # newest file": its rows rank the update's launch shapes by time per update and carry their counter traffic.
-KERNEL_TABLE = "profiles/r03b_kernel_table.json"
+KERNEL_TABLE = "profiles/r03x_kernel_table.json"
 
 
 def clock_probe(nwg=256, iters=20000, reps=3):
@@ -320,7 +320,7 @@ def probe_specs(agent, cfg, K):
     B, L, H = int(cfg.batch_size), int(cfg.batch_length), int(cfg.model.imag_horizon)
     N, D, U, SK, G, A = B * L, r._deter, r._hidden, r.flat_stoch, r._blocks, agent.act_dim
     Dg, Ig, F = D // G, D // G + 3 * U, SK + D
-    ksd, kss = 4, 2
+    ksd, kss = 4, 4  # split-K slabs of x0p (k_slab) and x1p (k_logit_rows) that k_hid sums
     out = []
 
     def add(key, name, grid, bound, work, algo, label, how, launches, peak=None):
@@ -369,13 +369,12 @@ def probe_specs(agent, cfg, K):
              "prologue)", 1),
             ("scan_k_gate", "k_gate<2, 2>", (D // 16, 1, 1), 4.0 * (3 * D * Dg + 8 * B * D),
              "scan k_gate (_dyn_gru BlockLinear + GRU epilogue, M = B rows)", 2),
-            ("scan_k_logit", "k_logit<%d>" % r._discrete, (SK // r._discrete, 1, 1),
-             4.0 * (SK * U + (ksd + 1) * B * U + 3 * B * SK + 2 * B * U),
-             "scan k_logit (obs_net RMSNorm + logits + unimix one-hot sampler)", 4),
+            ("scan_k_logit", "k_logit_rows<%d, %d>" % (r._discrete, SK // (4 * r._discrete)), (4, B, 1),
+             4.0 * (2 * SK * U + (ksd + 1) * B * U + 5 * B * SK + 6 * B * U),
+             "scan k_logit_rows (RSSM.observe step: obs_net RMSNorm + logits + unimix one-hot sampler by (categorical "
+             "group, row), and the next step's _dyn_in1 as a gather of the sampled W1^T rows, staged in LDS)", 4),
             ("scan_k_slab_obs", "k_slab<4>", (U // 16, ksd, 2), 4.0 * (2 * U * D + B * D + 2 * ksd * B * U),
-             "scan k_slab (obs_net_0 deter half + next _dyn_in0, split-K slabs)", 3),
-            ("scan_k_slab_x1", "k_slab<2>", (U // 16, kss, 1), 4.0 * (U * SK + B * SK + kss * B * U),
-             "scan k_slab (_dyn_in1 on the sampled stoch, split-K slabs)", 0)]
+             "scan k_slab (obs_net_0 deter half + next _dyn_in0, split-K slabs)", 3)]
     for key, name, grid, algo, label, which in scan:
         add(key, name, grid, "hbm", algo, algo, label, ("scan", which), L)
     return out
@@ -513,18 +512,19 @@ def phase_rooflines(agent, cfg, cfg_name, ms_update, table=None, reps=10):
                         "frac": f_img / (ms_img * 1e-3) / 1e12 / 157.3, "work": f_img,
                         "what": f"_imagine_tm: N={N} start rows, H={H} img_steps + {H + 1} actor samples, alone"},
         # the weights stream from L2/MALL, so the HBM fraction is no bound; the real bound is the dependent launch
-        # chain: 5 fused launches per step, each >= one kernel boundary (1.45 us between trivial kernels,
+        # chain: 4 fused launches per step, each >= one kernel boundary (1.45 us between trivial kernels,
         # MI355X_MICROARCH.md price list row 'boundary') plus its dependent prologue load (~1 us, an L2 round trip)
-        "observe_scan": {"bound": "launch latency", "ms": ms_obs, "launches": 5 * L,
-                         "latency_floor_ms": 5 * L * (1.45 + 1.0) * 1e-3,
-                         "frac": 5 * L * (1.45 + 1.0) * 1e-3 / ms_obs,
+        "observe_scan": {"bound": "launch latency", "ms": ms_obs, "launches": 4 * L,
+                         "latency_floor_ms": 4 * L * (1.45 + 1.0) * 1e-3,
+                         "frac": 4 * L * (1.45 + 1.0) * 1e-3 / ms_obs,
                          "weight_stream_GBps": b_obs / (ms_obs * 1e-3) / 1e9, "work": b_obs,
-                         "what": f"RSSM.observe forward, B={B} L={L}: 5 dependent launches per step; weight bytes "
+                         "what": f"RSSM.observe forward, B={B} L={L}: 4 dependent launches per step; weight bytes "
                                  "(Deter + obs_net once per step) over the phase time as weight_stream_GBps"},
     }
     if table:  # counter bytes of the scan forward's kernels (k_slab / k_hid / k_gate / k_logit of the fused scan) from the
         # committed PMC passes, per update, over the live phase time: the 'achieved HBM GB/s on the recurrent scan'
-        scan_rows = [rw for rw in table["rows"] if rw["kernel"].split("<")[0] in ("k_slab", "k_logit", "k_init") or
+        scan_rows = [rw for rw in table["rows"]
+                     if rw["kernel"].split("<")[0] in ("k_slab", "k_logit", "k_logit_rows", "k_init") or
                      rw["kernel"] in ("k_hid<8, 2>", "k_gate<2, 2>")]
         cb = sum(rw.get("hbm_bytes", 0.0) * rw["launches_per_update"] for rw in scan_rows)
         tm = sum(rw["ms_per_update"] for rw in scan_rows)

@@ -328,6 +328,11 @@ int sd_trace_mark(int tag, sd_stream stream);
  * (2 * nwg int64) receive per workgroup (shader cycles, 100 MHz ticks) around the loop: clock = cycles / ticks * 0.1 GHz.
  * sink (nwg floats) is never written in practice. */
 int sd_clock_probe(long long* stamps, float* sink, int nwg, int iters, sd_stream stream);
+/* Scheduling aid: a stream whose workgroups run only on CUs [first_cu, first_cu + ncu) (hipExtStreamCreateWithCUMask),
+ * for the update's filler phases, so they leave the rest of the chip to the latency-bound chain beside them
+ * (SDREAMER_FILL_CUS, dreamer.py). sd_stream_destroy releases it. */
+int sd_stream_create_cumask(int first_cu, int ncu, sd_stream* out);
+int sd_stream_destroy(sd_stream stream);
 /* Dreamer.preprocess + ConvEncoder's "-0.5": out = in/255 - shift (dreamer.py:710-713, networks.py:224) */
 int sd_u8_to_f32(const uint8_t* in, float* out, long n, float shift, sd_stream stream);
 /* NHWC channel pad + shift: out[p][c] = in[p][c] - shift (c < C), 0 (C <= c < Cp). The ConvEncoder input

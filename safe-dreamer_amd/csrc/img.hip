@@ -663,6 +663,17 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
   __shared__ float tile[BM][BN + 1];
   __shared__ float rs[BM], red[256];
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, U = d.U, S = d.SK / KD;
+  // the sampler's Gumbel noise depends on no operand: drawn first, so its Philox + f64 logs overlap the loads and
+  // the MFMAs instead of following them
+  constexpr int NK = BM * BN / 256;
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+  float gns[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int i = threadIdx.x + 256 * k, rl = i / BN, c = i % BN;
+    gns[k] = sd_gumbel(seed, (uint32_t)d.stream_img, (uint32_t)t,
+                       (uint64_t)((m0 + rl + d.row_offset) * S + (n0 + c) / KD) * KD + c % KD);
+  }
   wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
   const ARms<BM> a0(X, U, nw, rs, m0, d.N, U);
   const BRows<BN> b0(d.Wl, U, n0, BN, 0);
@@ -675,21 +686,17 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
     tile[4 * L.q + r][c] = acc[0][0][r] + d.bl[n0 + c];
   }
   __syncthreads();
-  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
 #pragma unroll
-  for (int k = 0; k < BM * BN / 256; ++k) {
+  for (int k = 0; k < NK; ++k) {
     const int i = threadIdx.x + 256 * k;
     const int rl = i / BN, c = i % BN, lt = c % KD;
     const long m = m0 + rl;
-    const int s = (n0 + c) / KD;
     const float l = tile[rl][c];
     float p, pp, nl;
     unimix_forward<KD>(l, true, KD, d.unimix, p, pp, nl);
-    const float gn = sd_gumbel(seed, (uint32_t)d.stream_img, (uint32_t)t,
-                               (uint64_t)((m + d.row_offset) * S + s) * KD + lt);
     float ys;
     int idx;
-    st_soft<KD>(nl, gn, true, ys, idx, lt);
+    st_soft<KD>(nl, gns[k], true, ys, idx, lt);
     if (m < d.N) snew[m * ldf + n0 + c] = ((lt == idx ? 1.f : 0.f) - ys) + ys;
   }
 }
@@ -712,6 +719,17 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
   const int m0 = blockIdx.y * BM, U = d.U, A = d.A;
   const int NO = d.act_discrete ? A : 2 * A;
   __shared__ float rs[BM], red[256];
+  const int tid = threadIdx.x;
+  // the action noise (one value per thread) depends on no operand: drawn before the contraction
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+  float nz = 0.f;
+  if (d.act_discrete) {
+    static_assert(BM * 16 <= 256, "one sampler element per thread");
+    const int lt = tid % 16;
+    if (lt < A) nz = sd_gumbel(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m0 + tid / 16 + d.row_offset) * A + lt);
+  } else if (tid < BM * A) {
+    nz = sd_normal(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m0 + tid / A + d.row_offset) * A + tid % A);
+  }
   wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
   const ARms<BM> a0(X, U, nw, rs, m0, d.N, U);
   const BRows<BN> b0(d.Wao, U, 0, BN, 0, NO);  // the output weight's NO rows, zeros past them
@@ -724,37 +742,31 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
     tile[L.wr * 16 + 4 * L.q + r][c] = acc[0][0][r] + (c < NO ? d.bao[c] : 0.f);
   }
   __syncthreads();
-  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
-  const int tid = threadIdx.x;
   if (d.act_discrete) {  // team of 16 lanes per row (A <= 16), one-hot ST sample with the actor's unimix
-    for (int i = tid; i < BM * 16; i += 256) {
-      const int rl = i / 16, lt = i % 16;
+    {
+      const int i = tid, rl = i / 16, lt = i % 16;
       const bool on = lt < A;
       const long m = m0 + rl;
       const float l = on ? tile[rl][lt] : 0.f;
       float p, pp, nl;
       unimix_forward<16>(l, on, A, d.act_unimix, p, pp, nl);
-      const float gn = on ? sd_gumbel(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lt)
-                          : 0.f;
       float ys;
       int idx;
-      st_soft<16>(nl, gn, on, ys, idx, lt);
+      st_soft<16>(nl, nz, on, ys, idx, lt);
       if (on) {
         const float a = ((lt == idx ? 1.f : 0.f) - ys) + ys;
         if (m < d.N) act[m * A + lt] = a;
         an[rl][lt] = a / fmaxf(fabsf(a), 1.f);
       }
     }
-  } else {
-    for (int i = tid; i < BM * A; i += 256) {
-      const int rl = i / A, j = i % A;
-      const long m = m0 + rl;
-      const float loc = tanhf(tile[rl][j]);
-      const float sc = (d.max_std - d.min_std) * sigmoidf_(tile[rl][A + j] + 2.f) + d.min_std;
-      const float a = loc + sd_normal(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + j) * sc;
-      if (m < d.N) act[m * A + j] = a;
-      an[rl][j] = a / fmaxf(fabsf(a), 1.f);
-    }
+  } else if (tid < BM * A) {
+    const int rl = tid / A, j = tid % A;
+    const long m = m0 + rl;
+    const float loc = tanhf(tile[rl][j]);
+    const float sc = (d.max_std - d.min_std) * sigmoidf_(tile[rl][A + j] + 2.f) + d.min_std;
+    const float a = loc + nz * sc;
+    if (m < d.N) act[m * A + j] = a;
+    an[rl][j] = a / fmaxf(fabsf(a), 1.f);
   }
   if (!want_x2) return;
   __syncthreads();

@@ -58,6 +58,10 @@ REUSE_H0 = os.environ.get("SDREAMER_REUSE_H0", "1") != "0"
 # SDREAMER_PRIO=1 (schedule knob): graph-replayed updates run the critical chain on high-priority streams and the filler
 # phases (M1, S2-S4) on normal-priority ones
 STREAM_PRIO = os.environ.get("SDREAMER_PRIO", "0") == "1"
+# SDREAMER_FILL_CUS=first:count (schedule knob): the filler phases (M1 beside the imagination, S2-S4 beside the backward)
+# replay on streams whose workgroups may run only on CUs [first, first + count) (sd_stream_create_cumask), so the
+# latency-bound chain beside them keeps the other CUs to itself; the chain's own streams stay unmasked
+FILL_CUS = os.environ.get("SDREAMER_FILL_CUS", "")
 # SDREAMER_AC_DEFER=1 (schedule knob): the actor / value weight-gradient contractions of phase S2 (the imagined
 # trajectories' large (H*N)-row GEMMs) are queued and run at the start of S3, beside the encoder backward, instead of
 # beside the scan backward (M2a, the latency-bound chain S2 slows)
@@ -592,6 +596,17 @@ class Dreamer(nn.Module):
                 self._prio_streams = (mk(-1), mk(-1), mk(0), mk(0))
             main, side, fill, side_fill = self._prio_streams
             main.wait_stream(caller)
+        elif FILL_CUS and self.use_side_stream:
+            if self._prio_streams is None:
+                first, count = (int(v) for v in FILL_CUS.split(":"))
+                mk = []
+                for _ in range(2):
+                    h = ctypes.c_void_p()
+                    nat.call("sd_stream_create_cumask", first, count, ctypes.addressof(h))
+                    mk.append(torch.cuda.ExternalStream(h.value, device=self.device))
+                self._prio_streams = tuple(mk)
+            main, side = caller, self._side
+            fill, side_fill = self._prio_streams
         else:
             main = caller
             side = self._side if self.use_side_stream else main
