@@ -178,6 +178,12 @@ SD_DEV void st_row(float* rowp, const f32x4 (&v)[NI], int N, int t32) {
   }
 }
 
+constexpr int KSM = 4;         // max split-K slabs
+#ifndef SD_LR_NG
+#define SD_LR_NG 4
+#endif
+constexpr int LR_NG = SD_LR_NG;                 // x1p slabs written by k_logit_rows (categorical groups per row)
+constexpr int KS1 = LR_NG > KSM ? LR_NG : KSM;  // max x1p slabs k_hid sums
 // ------------------------------------------------------------------------------------------- scratch layout
 struct Work {
   float *x0s, *x1s, *ops, *ssh, *dotp, *dxs, *dhin, *gq, *ch, *w1t;
@@ -190,7 +196,7 @@ Work work_layout(const sd_rssm_scan& d, float* base) {
   const long BU = (long)d.B * d.U;
   auto take = [&](long n) { float* p = base ? base + o : nullptr; o += al64(n); return p; };
   w.x0s = take(d.ks_d * BU);
-  w.x1s = take(4L * BU);  // ks_s slabs, or k_logit_rows' LR_NG (= KSM = 4)
+  w.x1s = take((long)KS1 * BU);  // ks_s slabs, or k_logit_rows' LR_NG
   w.ops = take(d.ks_d * BU);
   w.ssh = take((long)d.D);
   w.dotp = take((long)d.D);
@@ -205,7 +211,6 @@ Work work_layout(const sd_rssm_scan& d, float* base) {
 
 constexpr int UH = 256;        // hidden width of the fused path (base.yaml: hidden 256)
 constexpr int NU = UH / 128;   // float4 columns per prologue thread over a hidden row
-constexpr int KSM = 4;         // max split-K slabs
 
 // ------------------------------------------------------------------------------------------- forward kernels
 struct SlabProb {
@@ -286,7 +291,7 @@ __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   f32x4 h[NG], x0[NU], x1[NU], x2v[NU], b0v[NU], b1v[NU], n0v[NU], n1v[NU];
   ld_row(h, d.h_in + (long)t * B * D + (long)row * D + (long)g * Dg, Dg, rv, t32);
   ld_slabs<NU, KSM>(x0, w.x0s + (long)row * UH, (long)B * UH, d.ks_d, UH, rv, t32);
-  ld_slabs<NU, KSM>(x1, w.x1s + (long)row * UH, (long)B * UH, d.ks_s, UH, rv, t32);
+  ld_slabs<NU, KS1>(x1, w.x1s + (long)row * UH, (long)B * UH, d.ks_s, UH, rv, t32);
   ld_row(x2v, d.x2 + in_row(d, t, row) * UH, UH, rv, t32);
   ld_row(b0v, d.b0, UH, true, t32);
   ld_row(b1v, d.b1, UH, true, t32);
@@ -476,7 +481,6 @@ __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
 // nonzero per categorical (((k == idx) - ys) + ys is exactly 0 off the index), so its contraction with W1 is a gather
 // of CPG rows of W1^T: the NG = S / CPG slabs of a row sum (in k_hid's prologue, fixed order) to the dense product.
 // That removes the x1p k_slab launch from every step (4 dependent launches per step instead of 5).
-constexpr int LR_NG = 4;  // slabs of x1p (== KSM: k_hid sums up to KSM slabs)
 #ifndef LR_STAGE
 #define LR_STAGE 0  // measured slower in the update: 9.8 vs 8.9 us (128 KB of LDS: one workgroup per CU)
 #endif
@@ -1080,9 +1084,10 @@ int fwd_phase(const sd_rssm_scan& d, const Work& w, bool lrows, int which, int t
     if (!(raise_lds<k_logit_rows<KD_, CPG_>>(lds))) return SD_EARG;                                       \
     k_logit_rows<KD_, CPG_><<<gr, NTHR, lds, st>>>(d, w, t);                                              \
   } while (0)
-    if (d.Kd == 16) { if (SK == 512) SD_LR(16, 8); else SD_LR(16, 16); }
-    else if (d.Kd == 32) { if (SK == 512) SD_LR(32, 4); else SD_LR(32, 8); }
-    else { if (SK == 512) SD_LR(64, 2); else SD_LR(64, 4); }
+    // CPG = S / LR_NG categoricals per workgroup
+    if (d.Kd == 16) { if (SK == 512) SD_LR(16, 512 / (LR_NG * 16)); else SD_LR(16, 1024 / (LR_NG * 16)); }
+    else if (d.Kd == 32) { if (SK == 512) SD_LR(32, 512 / (LR_NG * 32)); else SD_LR(32, 1024 / (LR_NG * 32)); }
+    else { if (SK == 512) SD_LR(64, 512 / (LR_NG * 64)); else SD_LR(64, 1024 / (LR_NG * 64)); }
 #undef SD_LR
   } else {
     SD_KD_SWITCH(d.Kd, {
