@@ -320,7 +320,7 @@ def probe_specs(agent, cfg, K):
     B, L, H = int(cfg.batch_size), int(cfg.batch_length), int(cfg.model.imag_horizon)
     N, D, U, SK, G, A = B * L, r._deter, r._hidden, r.flat_stoch, r._blocks, agent.act_dim
     Dg, Ig, F = D // G, D // G + 3 * U, SK + D
-    ksd, kss = 4, 4  # split-K slabs of x0p (k_slab) and x1p (k_logit_rows) that k_hid sums
+    ksd, kss = 4, 8  # split-K slabs of x0p (k_slab) and x1p (k_logit_rows' categorical groups, SD_LR_NG) k_hid sums
     out = []
 
     def add(key, name, grid, bound, work, algo, label, how, launches, peak=None):
@@ -369,7 +369,7 @@ def probe_specs(agent, cfg, K):
              "prologue)", 1),
             ("scan_k_gate", "k_gate<2, 2>", (D // 16, 1, 1), 4.0 * (3 * D * Dg + 8 * B * D),
              "scan k_gate (_dyn_gru BlockLinear + GRU epilogue, M = B rows)", 2),
-            ("scan_k_logit", "k_logit_rows<%d, %d>" % (r._discrete, SK // (4 * r._discrete)), (4, B, 1),
+            ("scan_k_logit", "k_logit_rows<%d, %d>" % (r._discrete, SK // (kss * r._discrete)), (kss, B, 1),
              4.0 * (2 * SK * U + (ksd + 1) * B * U + 5 * B * SK + 6 * B * U),
              "scan k_logit_rows (RSSM.observe step: obs_net RMSNorm + logits + unimix one-hot sampler by (categorical "
              "group, row), and the next step's _dyn_in1 as a gather of the sampled W1^T rows, staged in LDS)", 4),

@@ -180,10 +180,11 @@ SD_DEV void st_row(float* rowp, const f32x4 (&v)[NI], int N, int t32) {
 
 constexpr int KSM = 4;         // max split-K slabs
 #ifndef SD_LR_NG
-#define SD_LR_NG 4
+#define SD_LR_NG 8  // 4: 12.03 / 12.01 ms, 8: 11.98 / 11.95 ms per update (same box, profiles/r03ng_env.txt)
 #endif
 constexpr int LR_NG = SD_LR_NG;                 // x1p slabs written by k_logit_rows (categorical groups per row)
 constexpr int KS1 = LR_NG > KSM ? LR_NG : KSM;  // max x1p slabs k_hid sums
+constexpr int lr_cpg(int SK, int KD) { return SK / (LR_NG * KD) > 0 ? SK / (LR_NG * KD) : 1; }
 // ------------------------------------------------------------------------------------------- scratch layout
 struct Work {
   float *x0s, *x1s, *ops, *ssh, *dotp, *dxs, *dhin, *gq, *ch, *w1t;
@@ -1084,10 +1085,10 @@ int fwd_phase(const sd_rssm_scan& d, const Work& w, bool lrows, int which, int t
     if (!(raise_lds<k_logit_rows<KD_, CPG_>>(lds))) return SD_EARG;                                       \
     k_logit_rows<KD_, CPG_><<<gr, NTHR, lds, st>>>(d, w, t);                                              \
   } while (0)
-    // CPG = S / LR_NG categoricals per workgroup
-    if (d.Kd == 16) { if (SK == 512) SD_LR(16, 512 / (LR_NG * 16)); else SD_LR(16, 1024 / (LR_NG * 16)); }
-    else if (d.Kd == 32) { if (SK == 512) SD_LR(32, 512 / (LR_NG * 32)); else SD_LR(32, 1024 / (LR_NG * 32)); }
-    else { if (SK == 512) SD_LR(64, 512 / (LR_NG * 64)); else SD_LR(64, 1024 / (LR_NG * 64)); }
+    // CPG = S / LR_NG categoricals per workgroup (use_lrows: S % LR_NG == 0, so CPG >= 1 where it launches)
+    if (d.Kd == 16) { if (SK == 512) SD_LR(16, lr_cpg(512, 16)); else SD_LR(16, lr_cpg(1024, 16)); }
+    else if (d.Kd == 32) { if (SK == 512) SD_LR(32, lr_cpg(512, 32)); else SD_LR(32, lr_cpg(1024, 32)); }
+    else { if (SK == 512) SD_LR(64, lr_cpg(512, 64)); else SD_LR(64, lr_cpg(1024, 64)); }
 #undef SD_LR
   } else {
     SD_KD_SWITCH(d.Kd, {
