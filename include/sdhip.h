@@ -454,9 +454,15 @@ typedef struct sd_imagine {
                          t_begin == 0 chunk also writes the pre-split images of _dyn_hid / _dyn_gru into `work`) */
   float* actor_h0;    /* optional (H1, N, U): actor layer 0's pre-norm output of every step, feat . Wa0^T + ba0 in
                          fp32 (null: kept in `work` only); the policy loss's actor forward starts from it */
+  const float* noise_img; /* optional (H1 - 1, N, SK): the prior samples' Gumbel noise, drawn ahead by
+                             sd_imagine_noise (null: drawn inside the sampler); the same values either way */
 } sd_imagine;
 int sd_imagine_work_floats(const sd_imagine* d);
 int sd_imagine_run(const sd_imagine* d, sd_stream stream);
+/* noise (H1 - 1, N, SK) = the Gumbel noise of every imagined prior sample (Philox stream d->stream_img, step t, element
+ * (row + row_offset) * SK + k; the effective seed read on the device as sd_imagine_run reads it): one full-chip launch
+ * instead of the per-step sampler epilogues computing it. */
+int sd_imagine_noise(const sd_imagine* d, float* noise, sd_stream stream);
 /* Measurement aid (bench.py roofline): one launch of step t's largest contractions exactly as sd_imagine_run issues
  * them, after a run on the same descriptor/workspace: which = 0: img_net_0 + _dyn_in0 + actor layer 0's deter part
  * (three (N, D) x (D, U) GEMMs, k_lin), 1: _dyn_hid (k_hid), 2: _dyn_gru + GRU (k_gate). 0 <= t < H1 - 1. Launches 0

@@ -671,8 +671,11 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     const int i = threadIdx.x + 256 * k, rl = i / BN, c = i % BN;
-    gns[k] = sd_gumbel(seed, (uint32_t)d.stream_img, (uint32_t)t,
-                       (uint64_t)((m0 + rl + d.row_offset) * S + (n0 + c) / KD) * KD + c % KD);
+    if (d.noise_img)  // drawn ahead (sd_imagine_noise): the same values
+      gns[k] = m0 + rl < d.N ? d.noise_img[((long)t * d.N + m0 + rl) * d.SK + n0 + c] : 0.f;
+    else
+      gns[k] = sd_gumbel(seed, (uint32_t)d.stream_img, (uint32_t)t,
+                         (uint64_t)((m0 + rl + d.row_offset) * S + (n0 + c) / KD) * KD + c % KD);
   }
   wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
   const ARms<BM> a0(X, U, nw, rs, m0, d.N, U);
@@ -1081,6 +1084,22 @@ __global__ __launch_bounds__(256) void k_imgprior(sd_imagine d, const float* X, 
   }
 }
 
+// noise[t][m][k] = sd_gumbel(seed, stream_img, t, (m + row_offset) * SK + k) for t < H1 - 1: one thread per 4
+// consecutive k, which share one Philox block (sd_gumbel's word idx & 3), one float4 store
+__global__ __launch_bounds__(256) void k_imag_noise(sd_imagine d, float* noise) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x, per_t = (long)d.N * d.SK / 4;
+  if (i >= (long)(d.H1 - 1) * per_t) return;
+  const int t = (int)(i / per_t);
+  const long r = i - (long)t * per_t, m = r / (d.SK / 4), k = 4 * (r % (d.SK / 4));
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+  const uint64_t q = ((uint64_t)(m + d.row_offset) * d.SK + k) >> 2;
+  const sd_u32x4 w = sd_philox4x32_10((uint32_t)q, (uint32_t)(q >> 32), (uint32_t)t, (uint32_t)d.stream_img,
+                                      (uint32_t)seed, (uint32_t)(seed >> 32));
+  const f32x4 g{(float)(-log(-log(sd_u01(w.x)))), (float)(-log(-log(sd_u01(w.y)))),
+                (float)(-log(-log(sd_u01(w.z)))), (float)(-log(-log(sd_u01(w.w))))};
+  *reinterpret_cast<f32x4*>(noise + 4 * i) = g;
+}
+
 // ------------------------------------------------------------------------------------------- host side
 struct IWork {
   float *a[2], *pa[2], *ad, *x0p, *px0, *x1p, *px1, *x2, *hp, *ph, *i[2], *pi[2];
@@ -1124,6 +1143,17 @@ int icheck(const sd_imagine* d) {
 }
 
 }  // namespace
+
+extern "C" int sd_imagine_noise(const sd_imagine* dp, float* noise, sd_stream stream_) {
+  const int rc = icheck(dp);
+  if (rc) return rc;
+  if (!noise || ((uintptr_t)noise & 15)) return SD_EARG;
+  const long n = (long)(dp->H1 - 1) * dp->N * dp->SK / 4;
+  if (n <= 0) return SD_OK;
+  k_imag_noise<<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream_>>>(*dp, noise);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
 
 extern "C" int sd_imagine_work_floats(const sd_imagine* d) {
   if (!d) return SD_EARG;

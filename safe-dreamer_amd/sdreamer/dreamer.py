@@ -58,6 +58,9 @@ REUSE_H0 = os.environ.get("SDREAMER_REUSE_H0", "1") != "0"
 # SDREAMER_PRIO=1 (schedule knob): graph-replayed updates run the critical chain on high-priority streams and the filler
 # phases (M1, S2-S4) on normal-priority ones
 STREAM_PRIO = os.environ.get("SDREAMER_PRIO", "0") == "1"
+# SDREAMER_IMAG_NOISE=0: the imagined prior samples draw their Gumbel noise inside the sampler epilogue (per step)
+# instead of from one sd_imagine_noise launch ahead of the rollout (same values; A/B knob)
+IMAG_NOISE = os.environ.get("SDREAMER_IMAG_NOISE", "1") != "0"
 # SDREAMER_FILL_CUS=first:count (schedule knob): the filler phases (M1 beside the imagination, S2-S4 beside the backward)
 # replay on streams whose workgroups may run only on CUs [first, first + count) (sd_stream_create_cumask), so the
 # latency-bound chain beside them keeps the other CUs to itself; the chain's own streams stay unmasked
@@ -1190,9 +1193,14 @@ class Dreamer(nn.Module):
             raise nat.NativeError(f"sd_imagine_work_floats failed with status {nwork}")
         work = torch.empty(nwork, dtype=torch.float32, device=feats.device)
         d.work = work.data_ptr()
+        noise = None
+        if IMAG_NOISE and H1 > 1:  # the prior samples' Gumbel noise drawn in one full-chip launch up front
+            noise = torch.empty((H1 - 1) * N * r.flat_stoch, dtype=torch.float32, device=feats.device)
+            d.noise_img = noise.data_ptr()
+            nat.call("sd_imagine_noise", ctypes.addressof(d), noise.data_ptr(), K.stream())
         bounds = list(chunks) if chunks else [0, H1]
         if keep is not None:  # measurement aid (bench.py): the descriptor and every buffer it points to
-            keep.update(desc=d, work=work, wo=wo, feats=feats, actions=actions, P=P)
+            keep.update(desc=d, work=work, wo=wo, feats=feats, actions=actions, P=P, noise=noise)
         events = []
         for t0, t1 in zip(bounds[:-1], bounds[1:]):
             d.t_begin, d.t_end = int(t0), int(t1)
