@@ -426,7 +426,9 @@ def roofline_entries(specs, agent, cfg, table):
             e.update(rank=i + 1, launches_per_update=rw["launches_per_update"],
                      trace_avg_us=rw["avg_us"], trace_ms_per_update=rw["ms_per_update"],
                      frac_trace=sp["work"] / (rw["avg_us"] * 1e-6) / (1e12 if unit == "TFLOP/s" else 1e9) / peak,
-                     traffic=rw.get("hbm_bytes"), trace_clock_ghz=rw.get("clock_ghz"), mfma_util=rw.get("mfma_util"),
+                     traffic=rw.get("hbm_bytes"), mfma_util=rw.get("mfma_util"),
+                     trace_clock_ghz=rw.get("clock_ghz") if (rw.get("clock_ghz") or 9.0) <= 2.4 else None,
+                     trace_clock_source=rw.get("clock_source"),
                      l2_hit=rw.get("l2_hit"), traffic_source=f"{KERNEL_TABLE} (rocprofv3 --pmc FETCH_SIZE x2 + "
                                                              "WRITE_SIZE, per dispatch)")
             if e["traffic"]:

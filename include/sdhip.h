@@ -415,6 +415,15 @@ typedef struct sd_rssm_scan {
   int bm_grads;
   const float *d_stoch2, *d_deter2;
   long ld_g2;
+  /* rows per workgroup tile (1..16; 0 = 16): every step kernel runs ceil(B / row_tile) row tiles side by side in its
+     grid (rows are independent sequences, rssm.py:146-151), so B > 16 is one scan and B = 16 with row_tile 8 uses
+     twice the workgroups */
+  int row_tile;
+  /* measurement aid (a build with -DSD_SCAN_TRACE only; NULL otherwise): per launch slot and workgroup 4 timestamps
+     (s_memrealtime, 100 MHz): entry, operands staged, contraction reduced, exit. Slot = t * 8 + phase (forward) or
+     (T + t) * 8 + phase (backward); trace_slot is set per launch by the library */
+  unsigned long long* trace;
+  int trace_slot;
 } sd_rssm_scan;
 int sd_rssm_scan_work_floats(const sd_rssm_scan* d);
 int sd_rssm_scan_fwd(const sd_rssm_scan* d, sd_stream stream);

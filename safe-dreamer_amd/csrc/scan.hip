@@ -101,6 +101,30 @@ struct Core {
 template <int NT>
 constexpr int core_lds_floats() { return NW * NT * 256 + MR * 16 * NT; }
 
+// Phase timestamps (measurement build, -DSD_SCAN_TRACE): thread 0 of every workgroup keeps entry / operands staged /
+// contraction reduced / exit (s_memrealtime, 100 MHz) and stores them at exit into trace[slot][workgroup][4].
+#ifdef SD_SCAN_TRACE
+constexpr int TR_WG = 2048;  // workgroup slots per launch
+#define SD_TR_BEGIN unsigned long long tr_[4] = {__builtin_amdgcn_s_memrealtime(), 0ull, 0ull, 0ull};
+#define SD_TR(k) tr_[k] = __builtin_amdgcn_s_memrealtime();
+#define SD_TR_END(buf, slot)                                                                               \
+  if (threadIdx.x == 0 && (buf)) {                                                                         \
+    tr_[3] = __builtin_amdgcn_s_memrealtime();                                                             \
+    const long wg_ = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);           \
+    unsigned long long* o_ = (buf) + ((long)(slot) * TR_WG + wg_) * 4;                                     \
+    for (int i_ = 0; i_ < 4; ++i_) o_[i_] = tr_[i_];                                                        \
+  }
+#else
+#define SD_TR_BEGIN
+#define SD_TR(k)
+#define SD_TR_END(buf, slot)
+#endif
+
+// row tile of a workgroup (grid z): batch rows rb .. rb + nr (d.row_tile rows, normalised on the host)
+#define SD_ROW_TILE                                               \
+  const int rb = (int)blockIdx.z * d.row_tile, nr = min(d.row_tile, d.B - rb); \
+  (void)rb; (void)nr;
+
 #define SD_THREAD_IDS                                      \
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6; \
   const int l16 = lane & 15, q = lane >> 4;                \
@@ -191,16 +215,19 @@ struct Work {
   long total;
 };
 long al64(long n) { return (n + 63) / 64 * 64; }
+int row_tile_of(const sd_rssm_scan& d) { return d.row_tile > 0 ? d.row_tile : MR; }
+int row_tiles(const sd_rssm_scan& d) { return (d.B + row_tile_of(d) - 1) / row_tile_of(d); }
 Work work_layout(const sd_rssm_scan& d, float* base) {
   Work w;
   long o = 0;
+  const long NT = row_tiles(d);
   const long BU = (long)d.B * d.U;
   auto take = [&](long n) { float* p = base ? base + o : nullptr; o += al64(n); return p; };
   w.x0s = take(d.ks_d * BU);
   w.x1s = take((long)KS1 * BU);  // ks_s slabs, or k_logit_rows' LR_NG
   w.ops = take(d.ks_d * BU);
-  w.ssh = take((long)d.D);
-  w.dotp = take((long)d.D);
+  w.ssh = take(NT * d.D);   // per row tile: (D/16 column tiles) x 16 row partials
+  w.dotp = take(NT * d.D);
   w.dxs = take((long)d.G * d.B * 3 * d.U);
   w.dhin = take((long)d.B * d.D);
   w.gq = take((long)d.B * d.D);
@@ -221,27 +248,35 @@ struct SlabProb {
   long ldw;
   float* out;                 // slab s at out + s*M*N
   const unsigned char* mask;  // rows whose input is reset (output row forced to 0), or null
+  unsigned long long* trace;  // SD_SCAN_TRACE builds: phase timestamps (sd_rssm_scan.trace), slot below
+  int slot;
 };
 
-// plain M=16 GEMM into split-K slabs: out[s][m][n] = A[m, span_s] . W[n, span_s]; grid (N/16, ks, nprob)
+// row-tiled GEMM into split-K slabs: out[s][m][n] = A[m, span_s] . W[n, span_s]; grid (N/16, ks * row tiles, nprob)
+// (blockIdx.y = s + ks * row tile: the row tiles of one column tile stay 16 * ks blocks apart, i.e. on one XCD)
 template <int CPW>
-__global__ __launch_bounds__(NTHR) void k_slab(SlabProb p0, SlabProb p1, int M, int N, int span) {
+__global__ __launch_bounds__(NTHR) void k_slab(SlabProb p0, SlabProb p1, int M, int N, int span, int ks, int rt) {
   extern __shared__ float smem[];
   SD_THREAD_IDS
+  SD_TR_BEGIN
   const SlabProb p = blockIdx.z ? p1 : p0;
-  const int n0 = blockIdx.x * 16, s = blockIdx.y, kb = s * span, nch = span / 16;
+  const int s = (int)blockIdx.y % ks, rb = ((int)blockIdx.y / ks) * rt, nr = min(rt, M - rb);
+  const int n0 = blockIdx.x * 16, kb = s * span, nch = span / 16;
   Core<1, CPW> core;
   const float* wt[1] = {p.W + (long)(n0 + l16) * p.ldw + kb};
   core.load_b(wt, nch, wave, q);
   const int erow = tid >> 4;
-  const bool masked = tid < 256 && erow < M && p.mask && p.mask[erow];
-  core.run_glb(p.A + kb, p.lda, M, nch, wave, l16, q);
+  const bool masked = tid < 256 && erow < nr && p.mask && p.mask[rb + erow];
+  core.run_glb(p.A + (long)rb * p.lda + kb, p.lda, nr, nch, wave, l16, q);
+  SD_TR(1)
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
-  if (tid < 256 && erow < M) {
+  SD_TR(2)
+  if (tid < 256 && erow < nr) {
     const int c = tid & 15;
-    p.out[(long)s * M * N + (long)erow * N + n0 + c] = masked ? 0.f : C[erow * 16 + c];
+    p.out[(long)s * M * N + (long)(rb + erow) * N + n0 + c] = masked ? 0.f : C[erow * 16 + c];
   }
+  SD_TR_END(p.trace, p.slot)
 }
 
 // s_in[0] = mask(stoch0), h_in[0] = mask(deter0)   (rssm.py:161-165 on the initial state)
@@ -280,20 +315,22 @@ SD_DEV long in_row(const sd_rssm_scan& d, int t, int b) {
 template <int CPW, int NG>
 __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
+  SD_TR_BEGIN
   SD_THREAD_IDS
+  SD_ROW_TILE
   const int B = d.B, D = d.D, Dg = D / d.G, Ig = Dg + 3 * UH, ldp = Ig + 4;
   const int tile = blockIdx.x, n0 = tile * 16, g = n0 / Dg;
   Core<1, CPW> core;
   const float* wt[1] = {d.Wh + (long)(n0 + l16) * Ig};
   core.load_b(wt, Ig / 16, wave, q);
-  const int row = tid >> 5, t32 = tid & 31;
-  const bool rv = row < B;
+  const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
+  const bool rv = row < nr;
   const long tBU = (long)t * B * UH;
   f32x4 h[NG], x0[NU], x1[NU], x2v[NU], b0v[NU], b1v[NU], n0v[NU], n1v[NU];
-  ld_row(h, d.h_in + (long)t * B * D + (long)row * D + (long)g * Dg, Dg, rv, t32);
-  ld_slabs<NU, KSM>(x0, w.x0s + (long)row * UH, (long)B * UH, d.ks_d, UH, rv, t32);
-  ld_slabs<NU, KS1>(x1, w.x1s + (long)row * UH, (long)B * UH, d.ks_s, UH, rv, t32);
-  ld_row(x2v, d.x2 + in_row(d, t, row) * UH, UH, rv, t32);
+  ld_row(h, d.h_in + (long)t * B * D + (long)gr * D + (long)g * Dg, Dg, rv, t32);
+  ld_slabs<NU, KSM>(x0, w.x0s + (long)gr * UH, (long)B * UH, d.ks_d, UH, rv, t32);
+  ld_slabs<NU, KS1>(x1, w.x1s + (long)gr * UH, (long)B * UH, d.ks_s, UH, rv, t32);
+  ld_row(x2v, d.x2 + in_row(d, t, gr) * UH, UH, rv, t32);
   ld_row(b0v, d.b0, UH, true, t32);
   ld_row(b1v, d.b1, UH, true, t32);
   ld_row(n0v, d.n0, UH, true, t32);
@@ -313,30 +350,33 @@ __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   st_row(P + Dg + UH, y1, UH, t32);
   st_row(P + Dg + 2 * UH, x2v, UH, t32);
   if (rv && tile < 3) {
-    float* xc = d.xcat + 3 * tBU + (long)row * 3 * UH;
+    float* xc = d.xcat + 3 * tBU + (long)gr * 3 * UH;
     if (tile == 0) {
-      st_row(d.x0p + tBU + (long)row * UH, x0, UH, t32);
+      st_row(d.x0p + tBU + (long)gr * UH, x0, UH, t32);
       st_row(xc, y0, UH, t32);
-      if (t32 == 0) d.r0[(long)t * B + row] = r0;
+      if (t32 == 0) d.r0[(long)t * B + gr] = r0;
     } else if (tile == 1) {
-      st_row(d.x1p + tBU + (long)row * UH, x1, UH, t32);
+      st_row(d.x1p + tBU + (long)gr * UH, x1, UH, t32);
       st_row(xc + UH, y1, UH, t32);
-      if (t32 == 0) d.r1[(long)t * B + row] = r1;
+      if (t32 == 0) d.r1[(long)t * B + gr] = r1;
     } else {
       st_row(xc + 2 * UH, x2v, UH, t32);
     }
   }
   __syncthreads();
+  SD_TR(1)
   core.run_lds(smem + core_lds_floats<1>(), ldp, Ig / 16, wave, l16, q);
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
+  SD_TR(2)
   if (tid < 256) {
     const int er = tid >> 4, c = tid & 15;
     const float v = C[er * 16 + c] + bhv;
-    if (er < B) d.hp[(long)t * B * D + (long)er * D + n0 + c] = v;
-    const float ss = group_sum<16>(er < B ? v * v : 0.f);
-    if (c == 0) w.ssh[tile * MR + er] = ss;
+    if (er < nr) d.hp[(long)t * B * D + (long)(rb + er) * D + n0 + c] = v;
+    const float ss = group_sum<16>(er < nr ? v * v : 0.f);
+    if (c == 0) w.ssh[((long)blockIdx.z * (D / 16) + tile) * MR + er] = ss;
   }
+  SD_TR_END(d.trace, d.trace_slot)
 }
 
 // gates = BlockLinear(dyn_gru)(silu(rms(hp))) + bg; deter = GRU(gates, h_in) (rssm.py:65-75); h_in[t+1] masked.
@@ -344,23 +384,25 @@ __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
 template <int CPW, int NG>
 __global__ __launch_bounds__(NTHR) void k_gate(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
+  SD_TR_BEGIN
   SD_THREAD_IDS
+  SD_ROW_TILE
   const int B = d.B, D = d.D, Dg = D / d.G, ldp = Dg + 4;
   const int tile = blockIdx.x, n0 = tile * 16, g = n0 / Dg, j0 = n0 % Dg;
   Core<3, CPW> core;
   const float* wg = d.Wg + (long)g * 3 * Dg * Dg;
   const float* wt[3] = {wg + (long)(j0 + l16) * Dg, wg + (long)(Dg + j0 + l16) * Dg, wg + (long)(2 * Dg + j0 + l16) * Dg};
   core.load_b(wt, Dg / 16, wave, q);
-  const int row = tid >> 5, t32 = tid & 31;
-  const bool rv = row < B;
+  const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
+  const bool rv = row < nr;
   float pv[8];
-  ld_parts(pv, w.ssh, D / 16, row, t32);
+  ld_parts(pv, w.ssh + (long)blockIdx.z * D, D / 16, row, t32);
   f32x4 hv[NG], nv[NG];
-  ld_row(hv, d.hp + (long)t * B * D + (long)row * D + (long)g * Dg, Dg, rv, t32);
+  ld_row(hv, d.hp + (long)t * B * D + (long)gr * D + (long)g * Dg, Dg, rv, t32);
   ld_row(nv, d.nh + (long)g * Dg, Dg, true, t32);
   // epilogue operands (thread = (row er, column c))
-  const int er = (tid >> 4) & 15, c = tid & 15, j = j0 + c, col = n0 + c;
-  const bool ev = tid < 256 && er < B;
+  const int er = (tid >> 4) & 15, c = tid & 15, j = j0 + c, col = n0 + c, ger = rb + er;
+  const bool ev = tid < 256 && er < nr;
   const float* bg = d.bg + (long)g * 3 * Dg;
   float bra = 0.f, bca = 0.f, bua = 0.f, hprev = 0.f;
   bool rnext = false;
@@ -368,38 +410,41 @@ __global__ __launch_bounds__(NTHR) void k_gate(sd_rssm_scan d, Work w, int t) {
     bra = bg[j];
     bca = bg[Dg + j];
     bua = bg[2 * Dg + j];
-    hprev = d.h_in[(long)t * B * D + (long)er * D + col];
-    rnext = t + 1 < d.T && d.reset[(t + 1) * B + er];
+    hprev = d.h_in[(long)t * B * D + (long)ger * D + col];
+    rnext = t + 1 < d.T && d.reset[(t + 1) * B + ger];
   }
   const float r = rsqrtf(sum_parts(pv) / (float)D + d.eps);
-  if (rv && t32 == 0 && tile == 0) d.rh[(long)t * B + row] = r;
+  if (rv && t32 == 0 && tile == 0) d.rh[(long)t * B + gr] = r;
   f32x4 y[NG];
 #pragma unroll
   for (int i = 0; i < NG; ++i)
 #pragma unroll
     for (int k = 0; k < 4; ++k) y[i][k] = rv ? siluf_(hv[i][k] * r * nv[i][k]) : 0.f;
   st_row(smem + core_lds_floats<3>() + row * ldp, y, Dg, t32);
-  if (rv && j0 == 0) st_row(d.hh + (long)t * B * D + (long)row * D + (long)g * Dg, y, Dg, t32);
+  if (rv && j0 == 0) st_row(d.hh + (long)t * B * D + (long)gr * D + (long)g * Dg, y, Dg, t32);
   __syncthreads();
+  SD_TR(1)
   core.run_lds(smem + core_lds_floats<3>(), ldp, Dg / 16, wave, l16, q);
   float* C = smem + NW * 3 * 256;
   core.reduce(smem, C, tid, wave, lane);
+  SD_TR(2)
   if (ev) {
     const float ra = C[er * 48 + c] + bra;
     const float ca = C[er * 48 + 16 + c] + bca;
     const float ua = C[er * 48 + 32 + c] + bua;
-    float* gr = d.gates + (long)t * B * 3 * D + (long)er * 3 * D + (long)g * 3 * Dg;
-    gr[j] = ra;
-    gr[Dg + j] = ca;
-    gr[2 * Dg + j] = ua;
+    float* gw = d.gates + (long)t * B * 3 * D + (long)ger * 3 * D + (long)g * 3 * Dg;
+    gw[j] = ra;
+    gw[Dg + j] = ca;
+    gw[2 * Dg + j] = ua;
     const float rs = sigmoidf_(ra);
     const float cc = tanhf(rs * ca);
     const float u = sigmoidf_(ua - 1.f);
     const float out = u * cc + (1.f - u) * hprev;
-    d.deter[(long)t * B * D + (long)er * D + col] = out;
-    if (d.post_deter) d.post_deter[((long)er * d.T + t) * D + col] = out;  // batch-major copy (RSSM.observe's output)
-    if (t + 1 < d.T) d.h_in[(long)(t + 1) * B * D + (long)er * D + col] = rnext ? 0.f : out;
+    d.deter[(long)t * B * D + (long)ger * D + col] = out;
+    if (d.post_deter) d.post_deter[((long)ger * d.T + t) * D + col] = out;  // batch-major copy (RSSM.observe's output)
+    if (t + 1 < d.T) d.h_in[(long)(t + 1) * B * D + (long)ger * D + col] = rnext ? 0.f : out;
   }
+  SD_TR_END(d.trace, d.trace_slot)
 }
 
 // logits = obs_net_logit(silu(rms(op))) and the straight-through unimix one-hot sample (rssm.py:172-177,
@@ -408,6 +453,7 @@ template <int KD>
 __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_THREAD_IDS
+  SD_ROW_TILE
   constexpr int NT = KD / 16, NE = (MR * KD + NTHR - 1) / NTHR;
   const int B = d.B, SK = d.SK, S = SK / KD, ldp = UH + 4;
   const int s = blockIdx.x, n0 = s * KD;
@@ -416,12 +462,12 @@ __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
 #pragma unroll
   for (int i = 0; i < NT; ++i) wt[i] = d.Wl + (long)(n0 + 16 * i + l16) * UH;
   core.load_b(wt, UH / 16, wave, q);
-  const int row = tid >> 5, t32 = tid & 31;
-  const bool rv = row < B;
+  const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
+  const bool rv = row < nr;
   const long tBU = (long)t * B * UH;
   f32x4 x[NU], e[NU], nv[NU];
-  ld_slabs<NU, KSM>(x, w.ops + (long)row * UH, (long)B * UH, d.ks_d, UH, rv, t32);
-  ld_row(e, d.eproj + in_row(d, t, row) * UH, UH, rv, t32);
+  ld_slabs<NU, KSM>(x, w.ops + (long)gr * UH, (long)B * UH, d.ks_d, UH, rv, t32);
+  ld_row(e, d.eproj + in_row(d, t, gr) * UH, UH, rv, t32);
   ld_row(nv, d.no, UH, true, t32);
   // sampler operands + noise, independent of the contraction
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
@@ -431,8 +477,9 @@ __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
   for (int k = 0; k < NE; ++k) {
     const int i = tid + NTHR * k, er = (i / KD) & 15, lt = i % KD;
     blv[k] = d.bl[n0 + lt];
-    gn[k] = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)t, (uint64_t)((long)er * S + s + d.group_offset) * KD + lt);
-    rnext[k] = er < B && t + 1 < d.T && d.reset[(t + 1) * B + er];
+    gn[k] = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)t,
+                      (uint64_t)((long)(rb + er) * S + s + d.group_offset) * KD + lt);
+    rnext[k] = er < nr && t + 1 < d.T && d.reset[(t + 1) * B + rb + er];
   }
 #pragma unroll
   for (int i = 0; i < NU; ++i) x[i] += e[i];
@@ -440,9 +487,9 @@ __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
   const float r = rms_silu_rows(x, nv, UH, d.eps, rv, y);
   st_row(smem + core_lds_floats<NT>() + row * ldp, y, UH, t32);
   if (rv && s == 0) {
-    st_row(d.op + tBU + (long)row * UH, x, UH, t32);
-    st_row(d.oo + tBU + (long)row * UH, y, UH, t32);
-    if (t32 == 0) d.ro[(long)t * B + row] = r;
+    st_row(d.op + tBU + (long)gr * UH, x, UH, t32);
+    st_row(d.oo + tBU + (long)gr * UH, y, UH, t32);
+    if (t32 == 0) d.ro[(long)t * B + gr] = r;
   }
   __syncthreads();
   core.run_lds(smem + core_lds_floats<NT>(), ldp, UH / 16, wave, l16, q);
@@ -459,13 +506,13 @@ __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
       float ys;
       int idx;
       st_soft<KD>(nl, gn[k], true, ys, idx, lt);
-      if (er < B) {
+      if (er < nr) {
         const float yv = ((lt == idx ? 1.f : 0.f) - ys) + ys;
-        const long o = (long)t * B * SK + (long)er * SK + n0 + lt;
+        const long o = (long)t * B * SK + (long)(rb + er) * SK + n0 + lt;
         d.logit[o] = l;
         if (d.stoch) d.stoch[o] = yv;
         if (d.post_logit) {  // batch-major copies (RSSM.observe's outputs)
-          const long ob = ((long)er * d.T + t) * SK + n0 + lt;
+          const long ob = ((long)(rb + er) * d.T + t) * SK + n0 + lt;
           d.post_logit[ob] = l;
           d.post_stoch[ob] = yv;
         }
@@ -492,6 +539,7 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
   __shared__ __attribute__((aligned(16))) float y[UH];
   __shared__ float red[NW], lg[NC], hv[CPG];
   __shared__ int hot[CPG];
+  SD_TR_BEGIN
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int B = d.B, SK = d.SK, S = SK / KD, g = blockIdx.x, b = blockIdx.y, n0 = g * NC;
   const long tBU = (long)t * B * UH;
@@ -537,6 +585,7 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
   float ss = wave_sum(x * x);
   if (lane == 0) red[wave] = ss;
   __syncthreads();
+  SD_TR(1)
   ss = 0.f;
 #pragma unroll
   for (int i = 0; i < UH / 64; ++i) ss += red[i];
@@ -563,6 +612,7 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
   for (int o = 1; o < TPC; o <<= 1) acc += __shfl_xor(acc, o, 64);
   if (kp == 0) lg[col] = acc;
   __syncthreads();
+  SD_TR(2)
   if (ts) {
     const float l = lg[tid] + blv;
     float p, pp, nl;
@@ -585,7 +635,10 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
       hv[tid / KD] = yv;
     }
   }
-  if (!more) return;
+  if (!more) {
+    SD_TR_END(d.trace, d.trace_slot)
+    return;
+  }
   if (STAGE) {
 #pragma unroll
     for (int i = 0; i < NW1; ++i) *reinterpret_cast<f32x4*>(w1s + 4 * (tid + NTHR * i)) = w1r[i];
@@ -602,6 +655,7 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
     }
     w.x1s[(long)g * B * UH + (long)b * UH + tid] = v;
   }
+  SD_TR_END(d.trace, d.trace_slot)
 }
 
 // ------------------------------------------------------------------------------------------- backward kernels
@@ -646,7 +700,9 @@ __global__ __launch_bounds__(256) void k_sbwd_last(sd_rssm_scan d) {
 template <int CPW, int NS>
 __global__ __launch_bounds__(NTHR) void k_dlogit(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
+  SD_TR_BEGIN
   SD_THREAD_IDS
+  SD_ROW_TILE
   const int B = d.B, SK = d.SK, ldp = SK + 4;
   const int n0 = blockIdx.x * 16;
   Core<1, CPW> core;
@@ -654,44 +710,49 @@ __global__ __launch_bounds__(NTHR) void k_dlogit(sd_rssm_scan d, Work w, int t) 
   core.load_b(wt, SK / 16, wave, q);
   const int row = tid >> 5, t32 = tid & 31;
   f32x4 v[NS];
-  ld_row(v, d.dl + (long)t * B * SK + (long)row * SK, SK, row < B, t32);
+  ld_row(v, d.dl + (long)t * B * SK + (long)(rb + row) * SK, SK, row < nr, t32);
   st_row(smem + core_lds_floats<1>() + row * ldp, v, SK, t32);
   __syncthreads();
+  SD_TR(1)
   core.run_lds(smem + core_lds_floats<1>(), ldp, SK / 16, wave, l16, q);
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
+  SD_TR(2)
   if (tid < 256) {
     const int er = tid >> 4, c = tid & 15;
-    if (er < B) d.d_o[(long)t * B * UH + (long)er * UH + n0 + c] = C[er * 16 + c];
+    if (er < nr) d.d_o[(long)t * B * UH + (long)(rb + er) * UH + n0 + c] = C[er * 16 + c];
   }
+  SD_TR_END(d.trace, d.trace_slot)
 }
 
 // d_op = RMSNorm-SiLU backward (prologue); dh = d_deter + carry_h + d_op . Wo[:, :D]; GRU backward (epilogue).
 // grid (D/16)
 __global__ __launch_bounds__(NTHR) void k_dgru(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
+  SD_TR_BEGIN
   SD_THREAD_IDS
+  SD_ROW_TILE
   const int B = d.B, D = d.D, Dg = D / d.G, ldp = UH + 4;
   const int tile = blockIdx.x, n0 = tile * 16;
   Core<1, 2> core;
   const float* wt[1] = {d.WoDT + (long)(n0 + l16) * UH};
   core.load_b(wt, UH / 16, wave, q);
-  const int row = tid >> 5, t32 = tid & 31;
-  const bool rv = row < B;
+  const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
+  const bool rv = row < nr;
   const long tBU = (long)t * B * UH;
   f32x4 xv[NU], dy[NU], nv[NU];
-  ld_row(xv, d.op + tBU + (long)row * UH, UH, rv, t32);
-  ld_row(dy, d.d_o + tBU + (long)row * UH, UH, rv, t32);
+  ld_row(xv, d.op + tBU + (long)gr * UH, UH, rv, t32);
+  ld_row(dy, d.d_o + tBU + (long)gr * UH, UH, rv, t32);
   ld_row(nv, d.no, UH, true, t32);
-  const float r = rv ? d.ro[(long)t * B + row] : 0.f;
+  const float r = rv ? d.ro[(long)t * B + gr] : 0.f;
   // epilogue operands
-  const int er = (tid >> 4) & 15, c = tid & 15, col = n0 + c, g = col / Dg, j = col % Dg;
-  const bool ev = tid < 256 && er < B;
-  const long od = (long)t * B * D + (long)er * D + col;
-  const long gb = (long)t * B * 3 * D + (long)er * 3 * D + (long)g * 3 * Dg;
+  const int er = (tid >> 4) & 15, c = tid & 15, col = n0 + c, g = col / Dg, j = col % Dg, ger = rb + er;
+  const bool ev = tid < 256 && er < nr;
+  const long od = (long)t * B * D + (long)ger * D + col;
+  const long gb = (long)t * B * 3 * D + (long)ger * 3 * D + (long)g * 3 * Dg;
   float dh0 = 0.f, ra = 0.f, ca = 0.f, ua = 0.f, hv = 0.f;
   if (ev) {
-    dh0 = in_grad(d, d.d_deter, d.d_deter2, t, er, col, D) + w.ch[(long)er * D + col];
+    dh0 = in_grad(d, d.d_deter, d.d_deter2, t, ger, col, D) + w.ch[(long)ger * D + col];
     ra = d.gates[gb + j];
     ca = d.gates[gb + Dg + j];
     ua = d.gates[gb + 2 * Dg + j];
@@ -714,11 +775,13 @@ __global__ __launch_bounds__(NTHR) void k_dgru(sd_rssm_scan d, Work w, int t) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) o[i][k] = rv ? r * (gq[i][k] - xv[i][k] * r * dot) : 0.f;
   st_row(smem + core_lds_floats<1>() + row * ldp, o, UH, t32);
-  if (rv && tile == 0) st_row(d.d_op + tBU + (long)row * UH, o, UH, t32);
+  if (rv && tile == 0) st_row(d.d_op + tBU + (long)gr * UH, o, UH, t32);
   __syncthreads();
+  SD_TR(1)
   core.run_lds(smem + core_lds_floats<1>(), ldp, UH / 16, wave, l16, q);
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
+  SD_TR(2)
   if (ev) {
     const float dh = dh0 + C[er * 16 + c];
     const float rs = sigmoidf_(ra);
@@ -728,8 +791,9 @@ __global__ __launch_bounds__(NTHR) void k_dgru(sd_rssm_scan d, Work w, int t) {
     d.d_gates[gb + j] = dtc * ca * rs * (1.f - rs);
     d.d_gates[gb + Dg + j] = dtc * rs;
     d.d_gates[gb + 2 * Dg + j] = dh * (cc - hv) * u * (1.f - u);
-    w.dhin[(long)er * D + col] = dh * (1.f - u);
+    w.dhin[(long)ger * D + col] = dh * (1.f - u);
   }
+  SD_TR_END(d.trace, d.trace_slot)
 }
 
 // d_hh = d_gates_g . Wg[g] (block GEMM); epilogue: RMSNorm-SiLU backward pieces of dyn_hid's norm (g*w and the
@@ -737,35 +801,40 @@ __global__ __launch_bounds__(NTHR) void k_dgru(sd_rssm_scan d, Work w, int t) {
 template <int CPW>
 __global__ __launch_bounds__(NTHR) void k_dhh(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
+  SD_TR_BEGIN
   SD_THREAD_IDS
+  SD_ROW_TILE
   const int B = d.B, D = d.D, Dg = D / d.G;
   const int tile = blockIdx.x, n0 = tile * 16, g = n0 / Dg, j0 = n0 % Dg;
   Core<1, CPW> core;
   const float* wt[1] = {d.WgT + ((long)g * Dg + j0 + l16) * 3 * Dg};
   core.load_b(wt, 3 * Dg / 16, wave, q);
-  const int er = (tid >> 4) & 15, c = tid & 15, col = n0 + c;
-  const bool ev = tid < 256 && er < B;
-  const long o = (long)t * B * D + (long)er * D + col;
+  const int er = (tid >> 4) & 15, c = tid & 15, col = n0 + c, ger = rb + er;
+  const bool ev = tid < 256 && er < nr;
+  const long o = (long)t * B * D + (long)ger * D + col;
   float xh = 0.f, wv = 0.f;
   if (ev) {
-    xh = d.hp[o] * d.rh[(long)t * B + er];
+    xh = d.hp[o] * d.rh[(long)t * B + ger];
     wv = d.nh[col];
   }
-  core.run_glb(d.d_gates + (long)t * B * 3 * D + (long)g * 3 * Dg, 3 * (long)D, B, 3 * Dg / 16, wave, l16, q);
+  core.run_glb(d.d_gates + ((long)t * B + rb) * 3 * D + (long)g * 3 * Dg, 3 * (long)D, nr, 3 * Dg / 16, wave, l16, q);
+  SD_TR(1)
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
+  SD_TR(2)
   if (tid < 256) {
     float part = 0.f;
     if (ev) {
       const float dy = C[er * 16 + c];
       d.d_hh[o] = dy;
       const float gq = dy * dsilu(xh * wv) * wv;
-      w.gq[(long)er * D + col] = gq;
+      w.gq[(long)ger * D + col] = gq;
       part = gq * xh;
     }
     part = group_sum<16>(part);
-    if (c == 0) w.dotp[tile * MR + er] = part;
+    if (c == 0) w.dotp[((long)blockIdx.z * (D / 16) + tile) * MR + er] = part;
   }
+  SD_TR_END(d.trace, d.trace_slot)
 }
 
 // d_hp_g = RMSNorm backward (prologue, from g*w and the row partials); then two problems in one grid:
@@ -774,7 +843,9 @@ __global__ __launch_bounds__(NTHR) void k_dhh(sd_rssm_scan d, Work w, int t) {
 template <int CPW, int NG>
 __global__ __launch_bounds__(NTHR) void k_dhp(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
+  SD_TR_BEGIN
   SD_THREAD_IDS
+  SD_ROW_TILE
   const int B = d.B, D = d.D, Dg = D / d.G, ldp = Dg + 4, X = 3 * UH;
   const int NX = (X / 16) * d.G;
   const int blk = blockIdx.x;
@@ -793,18 +864,18 @@ __global__ __launch_bounds__(NTHR) void k_dhp(sd_rssm_scan d, Work w, int t) {
   Core<1, CPW> core;
   const float* wt[1] = {wrow};
   core.load_b(wt, Dg / 16, wave, q);
-  const int row = tid >> 5, t32 = tid & 31;
-  const bool rv = row < B;
+  const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
+  const bool rv = row < nr;
   float pv[8];
-  ld_parts(pv, w.dotp, D / 16, row, t32);
-  const long ob = (long)row * D + (long)g * Dg;
+  ld_parts(pv, w.dotp + (long)blockIdx.z * D, D / 16, row, t32);
+  const long ob = (long)gr * D + (long)g * Dg;
   f32x4 gq[NG], xv[NG];
   ld_row(gq, w.gq + ob, Dg, rv, t32);
   ld_row(xv, d.hp + (long)t * B * D + ob, Dg, rv, t32);
-  const float r = rv ? d.rh[(long)t * B + row] : 0.f;
-  const int er = (tid >> 4) & 15, c = tid & 15;
-  const bool ev = tid < 256 && er < B;
-  const float dh_old = (!p0 && ev) ? w.dhin[(long)er * D + n0 + c] : 0.f;
+  const float r = rv ? d.rh[(long)t * B + gr] : 0.f;
+  const int er = (tid >> 4) & 15, c = tid & 15, ger = rb + er;
+  const bool ev = tid < 256 && er < nr;
+  const float dh_old = (!p0 && ev) ? w.dhin[(long)ger * D + n0 + c] : 0.f;
   const float dot = sum_parts(pv) / (float)D;
   f32x4 o[NG];
 #pragma unroll
@@ -814,13 +885,16 @@ __global__ __launch_bounds__(NTHR) void k_dhp(sd_rssm_scan d, Work w, int t) {
   st_row(smem + core_lds_floats<1>() + row * ldp, o, Dg, t32);
   if (rv && !p0 && (n0 % Dg) == 0) st_row(d.d_hp + (long)t * B * D + ob, o, Dg, t32);
   __syncthreads();
+  SD_TR(1)
   core.run_lds(smem + core_lds_floats<1>(), ldp, Dg / 16, wave, l16, q);
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
+  SD_TR(2)
   if (ev) {
-    if (p0) w.dxs[(long)g * B * X + (long)er * X + n0 + c] = C[er * 16 + c];
-    else w.dhin[(long)er * D + n0 + c] = dh_old + C[er * 16 + c];
+    if (p0) w.dxs[(long)g * B * X + (long)ger * X + n0 + c] = C[er * 16 + c];
+    else w.dhin[(long)ger * D + n0 + c] = dh_old + C[er * 16 + c];
   }
+  SD_TR_END(d.trace, d.trace_slot)
 }
 
 // d_xcat = sum over blocks of the slabs; d_x0p / d_x1p = RMSNorm-SiLU backward of the _dyn_in0 / _dyn_in1 norms.
@@ -875,7 +949,9 @@ __global__ __launch_bounds__(NTHR) void k_dx01(sd_rssm_scan d, Work w, int t) {
 template <int KD>
 __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
+  SD_TR_BEGIN
   SD_THREAD_IDS
+  SD_ROW_TILE
   constexpr int NT = KD / 16, NE = (MR * KD + NTHR - 1) / NTHR, GM = 8, X = 3 * UH, ldp = UH + 4;
   const int B = d.B, D = d.D, SK = d.SK, S = SK / KD;
   const bool p0 = (int)blockIdx.x < D / KD;
@@ -886,17 +962,17 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   for (int i = 0; i < NT; ++i) wt[i] = (p0 ? d.W0T : d.W1T) + (long)(n0 + 16 * i + l16) * UH;
   core.load_b(wt, UH / 16, wave, q);
   // prologue loads: the G slabs of this half's d_xcat part, its pre-norm input and norm weight
-  const int row = tid >> 5, t32 = tid & 31;
-  const bool rv = row < B;
+  const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
+  const bool rv = row < nr;
   const long tB = (long)t * B;
   const int hoff = p0 ? 0 : UH;
   const bool wx2 = p0 && wid == 1;  // the x2 part's writer
   f32x4 part[GM][NU], xv[NU], nv[NU];
 #pragma unroll
   for (int g = 0; g < GM; ++g)
-    ld_row(part[g], w.dxs + (long)g * B * X + (long)row * X + (wx2 ? 2 * UH : hoff), UH, rv && g < d.G, t32);
-  const float rr = rv ? (p0 ? d.r0 : d.r1)[tB + row] : 0.f;
-  ld_row(xv, (p0 ? d.x0p : d.x1p) + (tB + row) * UH, UH, rv, t32);
+    ld_row(part[g], w.dxs + (long)g * B * X + (long)gr * X + (wx2 ? 2 * UH : hoff), UH, rv && g < d.G, t32);
+  const float rr = rv ? (p0 ? d.r0 : d.r1)[tB + gr] : 0.f;
+  ld_row(xv, (p0 ? d.x0p : d.x1p) + (tB + gr) * UH, UH, rv, t32);
   ld_row(nv, p0 ? d.n0 : d.n1, UH, true, t32);
   // epilogue operands: element i = (row er, column lt) of the 16 x KD tile
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
@@ -905,21 +981,21 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   bool rs[NE];
 #pragma unroll
   for (int k = 0; k < NE; ++k) {
-    const int i = tid + NTHR * k, er = (i / KD) & 15, lt = i % KD;
-    const bool ev = i < MR * KD && er < B;
-    rs[k] = ev && d.reset[t * B + er];
+    const int i = tid + NTHR * k, er = (i / KD) & 15, lt = i % KD, ger = rb + er;
+    const bool ev = i < MR * KD && er < nr;
+    rs[k] = ev && d.reset[t * B + ger];
     e0[k] = e1[k] = e2[k] = gn[k] = 0.f;
     if (p0) {
-      if (ev) e0[k] = w.dhin[(long)er * D + n0 + lt];
+      if (ev) e0[k] = w.dhin[(long)ger * D + n0 + lt];
     } else {
-      const long o = (long)tp * B * SK + (long)er * SK + n0 + lt;
+      const long o = (long)tp * B * SK + (long)ger * SK + n0 + lt;
       if (ev) {
         e0[k] = d.logit[o];
-        e1[k] = in_grad(d, d.d_stoch, d.d_stoch2, tp, er, n0 + lt, SK);
-        e2[k] = in_grad(d, d.d_logit, nullptr, tp, er, n0 + lt, SK);
+        e1[k] = in_grad(d, d.d_stoch, d.d_stoch2, tp, ger, n0 + lt, SK);
+        e2[k] = in_grad(d, d.d_logit, nullptr, tp, ger, n0 + lt, SK);
       }
       gn[k] = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)tp,
-                        (uint64_t)((long)er * S + n0 / KD + d.group_offset) * KD + lt);
+                        (uint64_t)((long)ger * S + n0 / KD + d.group_offset) * KD + lt);
     }
   }
   // d_xcat part = sum of the slabs (k_dx01's order); the x2 writer stores its part and then rebuilds x0's
@@ -931,9 +1007,9 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
     for (int g = 1; g < GM; ++g) dx[i] += part[g][i];
   }
   if (wx2) {
-    if (rv) st_row(d.d_xcat + (tB + row) * X + 2 * UH, dx, UH, t32);
+    if (rv) st_row(d.d_xcat + (tB + gr) * X + 2 * UH, dx, UH, t32);
 #pragma unroll
-    for (int g = 0; g < GM; ++g) ld_row(part[g], w.dxs + (long)g * B * X + (long)row * X, UH, rv && g < d.G, t32);
+    for (int g = 0; g < GM; ++g) ld_row(part[g], w.dxs + (long)g * B * X + (long)gr * X, UH, rv && g < d.G, t32);
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
       dx[i] = part[0][i];
@@ -960,28 +1036,31 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   float* P = smem + core_lds_floats<NT>();
   st_row(P + row * ldp, o, UH, t32);
   if (rv && wid == 0) {
-    st_row(d.d_xcat + (tB + row) * X + hoff, dx, UH, t32);
-    st_row((p0 ? d.d_x0p : d.d_x1p) + (tB + row) * UH, o, UH, t32);
+    st_row(d.d_xcat + (tB + gr) * X + hoff, dx, UH, t32);
+    st_row((p0 ? d.d_x0p : d.d_x1p) + (tB + gr) * UH, o, UH, t32);
   }
   __syncthreads();
+  SD_TR(1)
   core.run_lds(P, ldp, UH / 16, wave, l16, q);
   float* C = smem + NW * NT * 256;
   core.reduce(smem, C, tid, wave, lane);
+  SD_TR(2)
 #pragma unroll
   for (int k = 0; k < NE; ++k) {
     const int i = tid + NTHR * k;
     if (i < MR * KD) {
-      const int er = i / KD, lt = i % KD;
-      const bool ev = er < B;
+      const int er = i / KD, lt = i % KD, ger = rb + er;
+      const bool ev = er < nr;
       if (p0) {
-        if (ev) w.ch[(long)er * D + n0 + lt] = rs[k] ? 0.f : e0[k] + C[er * KD + lt];
+        if (ev) w.ch[(long)ger * D + n0 + lt] = rs[k] ? 0.f : e0[k] + C[er * KD + lt];
       } else {
         const float cs = rs[k] ? 0.f : C[er * KD + lt];
         const float dlv = sampler_bwd<KD>(e0[k], gn[k], ev ? e1[k] + cs : 0.f, d.unimix, lt);
-        if (ev) d.dl[(long)tp * B * SK + (long)er * SK + n0 + lt] = e2[k] + dlv;
+        if (ev) d.dl[(long)tp * B * SK + (long)ger * SK + n0 + lt] = e2[k] + dlv;
       }
     }
   }
+  SD_TR_END(d.trace, d.trace_slot)
 }
 
 // ------------------------------------------------------------------------------------------- host side
@@ -1023,7 +1102,8 @@ bool raise_lds(size_t bytes) {
 
 int check(const sd_rssm_scan* d) {
   if (!d) return SD_EARG;
-  if (d->B < 1 || d->B > MR || d->T < 1 || d->G < 1 || d->G > 8 || d->D % d->G) return SD_ESHAPE;
+  if (d->B < 1 || d->B > 4096 || d->T < 1 || d->G < 1 || d->G > 8 || d->D % d->G) return SD_ESHAPE;
+  if (d->row_tile < 0 || d->row_tile > MR) return SD_EARG;
   const int Dg = d->D / d->G;
   if (d->U != UH || (Dg != 256 && Dg != 512) || (d->SK != 512 && d->SK != 1024) || d->D > 4096) return SD_ESHAPE;
   if (d->Kd != 16 && d->Kd != 32 && d->Kd != 64) return SD_ESHAPE;
@@ -1063,27 +1143,30 @@ int fwd_phase(const sd_rssm_scan& d, const Work& w, bool lrows, int which, int t
   const long wod_ld = d.ld_wod > 0 ? d.ld_wod : D;
   sd_rssm_scan dd = d;
   dd.ks_s = ks_s;  // x1p slabs k_hid sums
+  const int rt = dd.row_tile = row_tile_of(d), nt = row_tiles(d);
+  dd.trace_slot = t * 8 + which;
   if (which == 0) {
-    SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr};
-    SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(UH / 16, ks_s, 1), NTHR, core1, st>>>(p, p, B, UH, span_s));
+    SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr, d.trace, dd.trace_slot};
+    SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(UH / 16, ks_s * nt, 1), NTHR, core1, st>>>(p, p, B, UH, span_s, ks_s, rt));
   } else if (which == 1) {
     SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG>>(lds_hid))) return SD_EARG;
-                                   k_hid<CP, NG><<<D / 16, NTHR, lds_hid, st>>>(dd, w, t)));
+                                   k_hid<CP, NG><<<dim3(D / 16, 1, nt), NTHR, lds_hid, st>>>(dd, w, t)));
   } else if (which == 2) {
     SD_NG_SWITCH(Dg, if (!(raise_lds<k_gate<NG, NG>>(lds_gate))) return SD_EARG;
-                 k_gate<NG, NG><<<D / 16, NTHR, lds_gate, st>>>(dd, w, t));
+                 k_gate<NG, NG><<<dim3(D / 16, 1, nt), NTHR, lds_gate, st>>>(dd, w, t));
   } else if (which == 3) {
-    SlabProb po{d.deter + t * BD, D, d.WoD, wod_ld, w.ops, nullptr};
-    SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset + (t + 1) * B};
+    SlabProb po{d.deter + t * BD, D, d.WoD, wod_ld, w.ops, nullptr, d.trace, dd.trace_slot};
+    SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset + (t + 1) * B, d.trace, dd.trace_slot};
     const int np = t + 1 < d.T ? 2 : 1;
-    SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, np), NTHR, core1, st>>>(po, px, B, UH, span_d));
+    SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d * nt, np), NTHR, core1, st>>>(po, px, B, UH, span_d,
+                                                                                        d.ks_d, rt));
   } else if (lrows) {
     const dim3 gr(LR_NG, B);
 #define SD_LR(KD_, CPG_)                                                                                 \
   do {                                                                                                    \
     constexpr size_t lds = LR_STAGE && (size_t)CPG_ * KD_ * UH * 4 <= 131072 ? (size_t)CPG_ * KD_ * UH * 4 : 0; \
     if (!(raise_lds<k_logit_rows<KD_, CPG_>>(lds))) return SD_EARG;                                       \
-    k_logit_rows<KD_, CPG_><<<gr, NTHR, lds, st>>>(d, w, t);                                              \
+    k_logit_rows<KD_, CPG_><<<gr, NTHR, lds, st>>>(dd, w, t);                                             \
   } while (0)
     // CPG = S / LR_NG categoricals per workgroup (use_lrows: S % LR_NG == 0, so CPG >= 1 where it launches)
     if (d.Kd == 16) { if (SK == 512) SD_LR(16, lr_cpg(512, 16)); else SD_LR(16, lr_cpg(1024, 16)); }
@@ -1094,7 +1177,7 @@ int fwd_phase(const sd_rssm_scan& d, const Work& w, bool lrows, int which, int t
     SD_KD_SWITCH(d.Kd, {
       const size_t lds = core_lds_floats<KD / 16>() * 4 + (size_t)MR * (UH + 4) * 4;
       if (!(raise_lds<k_logit<KD>>(lds))) return SD_EARG;
-      k_logit<KD><<<SK / KD, NTHR, lds, st>>>(d, w, t);
+      k_logit<KD><<<dim3(SK / KD, 1, nt), NTHR, lds, st>>>(dd, w, t);
     });
   }
   SD_LAUNCH_CHECK();
@@ -1123,9 +1206,9 @@ extern "C" int sd_rssm_scan_fwd(const sd_rssm_scan* dp, sd_stream stream_) {
   k_init<<<lrows ? 256 : 64, 256, 0, st>>>(d, lrows ? w.w1t : nullptr);
   SD_LAUNCH_CHECK();
   {  // x0p(0) = h_in[0] . W0^T
-    SlabProb p{d.h_in, D, d.W0, D, w.x0s, nullptr};
-    SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d, 1), NTHR, core_lds_floats<1>() * 4, st>>>(p, p, B, UH,
-                                                                                                    D / d.ks_d));
+    SlabProb p{d.h_in, D, d.W0, D, w.x0s, nullptr, nullptr, 0};
+    SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d * row_tiles(d), 1), NTHR, core_lds_floats<1>() * 4, st>>>(
+                            p, p, B, UH, D / d.ks_d, d.ks_d, row_tile_of(d)));
     SD_LAUNCH_CHECK();
   }
   for (int t = 0; t < d.T; ++t) {
@@ -1155,7 +1238,9 @@ extern "C" int sd_rssm_scan_bwd(const sd_rssm_scan* dp, sd_stream stream_) {
   int rc = check(dp);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream_;
-  const sd_rssm_scan& d = *dp;
+  sd_rssm_scan d = *dp;
+  d.row_tile = row_tile_of(*dp);
+  const int nt = row_tiles(d);
   const Work w = work_layout(d, d.work);
   const int B = d.B, D = d.D, SK = d.SK, Dg = D / d.G;
   const int cp_g3 = cpw_for(3 * Dg);
@@ -1172,23 +1257,28 @@ extern "C" int sd_rssm_scan_bwd(const sd_rssm_scan* dp, sd_stream stream_) {
   SD_KD_SWITCH(d.Kd, k_sbwd_last<KD><<<(int)(((long)B * SK + 255) / 256), 256, 0, st>>>(d));
   SD_LAUNCH_CHECK();
   for (int t = d.T - 1; t >= 0; --t) {
+    d.trace_slot = (d.T + t) * 8;
     if (SK == 512) {
       if (!(raise_lds<k_dlogit<4, 4>>(lds_dl))) return SD_EARG;
-      k_dlogit<4, 4><<<UH / 16, NTHR, lds_dl, st>>>(d, w, t);
+      k_dlogit<4, 4><<<dim3(UH / 16, 1, nt), NTHR, lds_dl, st>>>(d, w, t);
     } else {
       if (!(raise_lds<k_dlogit<8, 8>>(lds_dl))) return SD_EARG;
-      k_dlogit<8, 8><<<UH / 16, NTHR, lds_dl, st>>>(d, w, t);
+      k_dlogit<8, 8><<<dim3(UH / 16, 1, nt), NTHR, lds_dl, st>>>(d, w, t);
     }
     SD_LAUNCH_CHECK();
-    k_dgru<<<D / 16, NTHR, lds_dgru, st>>>(d, w, t);
+    d.trace_slot = (d.T + t) * 8 + 1;
+    k_dgru<<<dim3(D / 16, 1, nt), NTHR, lds_dgru, st>>>(d, w, t);
     SD_LAUNCH_CHECK();
-    SD_CPW_SWITCH(cp_g3, k_dhh<CP><<<D / 16, NTHR, core1, st>>>(d, w, t));
+    d.trace_slot = (d.T + t) * 8 + 2;
+    SD_CPW_SWITCH(cp_g3, k_dhh<CP><<<dim3(D / 16, 1, nt), NTHR, core1, st>>>(d, w, t));
     SD_LAUNCH_CHECK();
+    d.trace_slot = (d.T + t) * 8 + 3;
     SD_NG_SWITCH(Dg, if (!(raise_lds<k_dhp<NG, NG>>(lds_dhp))) return SD_EARG;
-                 k_dhp<NG, NG><<<NX + D / 16, NTHR, lds_dhp, st>>>(d, w, t));
+                 k_dhp<NG, NG><<<dim3(NX + D / 16, 1, nt), NTHR, lds_dhp, st>>>(d, w, t));
     SD_LAUNCH_CHECK();
+    d.trace_slot = (d.T + t) * 8 + 4;
     if (t > 0) {  // k_carry builds d_x0p / d_x1p itself (the k_dx01 work in its prologue)
-      SD_KD_SWITCH(d.Kd, k_carry<KD><<<D / KD + SK / KD, NTHR,
+      SD_KD_SWITCH(d.Kd, k_carry<KD><<<dim3(D / KD + SK / KD, 1, nt), NTHR,
                                        core_lds_floats<KD / 16>() * 4 + (size_t)MR * (UH + 4) * 4, st>>>(d, w, t));
     } else {
       k_dx01<<<B, NTHR, 0, st>>>(d, w, t);

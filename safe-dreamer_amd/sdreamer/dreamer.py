@@ -87,6 +87,24 @@ def _tstats(t, prefix):  # tools.tensorstats (tools.py:275-281), resolved with t
     return K.tensorstats(t, prefix)
 
 
+
+_CUMASK = {}  # device -> the two CU-masked filler streams of SDREAMER_FILL_CUS (created once per process, never leaked
+# per agent: tests and benches build several agents)
+
+
+def _cumask_streams(device):
+    key = str(device)
+    if key not in _CUMASK:
+        first, count = (int(v) for v in FILL_CUS.split(":"))
+        mk = []
+        for _ in range(2):
+            h = ctypes.c_void_p()
+            nat.call("sd_stream_create_cumask", first, count, ctypes.addressof(h))
+            mk.append(torch.cuda.ExternalStream(h.value, device=device))
+        _CUMASK[key] = tuple(mk)
+    return _CUMASK[key]
+
+
 class Dreamer(nn.Module):
     def __init__(self, config, obs_space, act_space, rank=0, world=1):
         super().__init__()
@@ -601,13 +619,7 @@ class Dreamer(nn.Module):
             main.wait_stream(caller)
         elif FILL_CUS and self.use_side_stream:
             if self._prio_streams is None:
-                first, count = (int(v) for v in FILL_CUS.split(":"))
-                mk = []
-                for _ in range(2):
-                    h = ctypes.c_void_p()
-                    nat.call("sd_stream_create_cumask", first, count, ctypes.addressof(h))
-                    mk.append(torch.cuda.ExternalStream(h.value, device=self.device))
-                self._prio_streams = tuple(mk)
+                self._prio_streams = _cumask_streams(self.device)
             main, side = caller, self._side
             fill, side_fill = self._prio_streams
         else:

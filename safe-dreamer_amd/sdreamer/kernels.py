@@ -784,14 +784,19 @@ def tensorstats(t, prefix):
 def metric_vector(values):
     """(len(values),) float32 device tensor: values are Stat or tensors (a tensor = its mean); one sd_multi_stats call
     (two launches) per SD_MAX_STATS terms (normally one)."""
-    reqs = []
+    reqs, empty = [], []
     for i, v in enumerate(values):
         for t, kind, sc in (v.terms if isinstance(v, Stat) else [(v, STAT_MEAN, 1.0)]):
             t = t.detach()
+            if t.numel() == 0:  # torch semantics: mean / std / min / max of nothing is NaN (sd_multi_stats needs n > 0)
+                empty.append(i)
+                continue
             if t.dtype != torch.float32:
                 t = t.float()
             reqs.append((_c(t), kind, sc, i))
     out = torch.empty(len(values), dtype=torch.float32, device=reqs[0][0].device if reqs else "cuda")
+    if not reqs:
+        return out.fill_(float("nan"))
     cap = len(nat.Stats().r)
     chunk = _STAT_CHUNK
     for lo in range(0, len(reqs), cap):
@@ -808,6 +813,8 @@ def metric_vector(values):
         nat.call("sd_multi_stats", ctypes.addressof(st), p(ws), p(dst), len(values), stream())
         if lo:  # a second table's slots add to the first's
             out.add_(dst)
+    if empty:
+        out.index_fill_(0, torch.tensor(sorted(set(empty)), device=out.device), float("nan"))
     return out
 
 

@@ -228,10 +228,10 @@ def heads_nograd(heads, x, fast=False, firsts_out=None):
         # per-entry weights: the heads' parameters are read in place (no stacked copies)
         if K.mlp_layer(x.expand(n, M, x.shape[1]), [f.weight for f in firsts], h0, bias=[f.bias for f in firsts],
                        part_out=p0):
-            if firsts_out is not None:
-                firsts_out.append(h0)
             out = _heads_rest_fused(heads, h0, p0)
             if out is not None:
+                if firsts_out is not None:
+                    firsts_out.append(h0)
                 return out
     w = torch.stack([f.weight for f in firsts])  # (n, U, F)
     b = torch.stack([f.bias for f in firsts])  # (n, U)

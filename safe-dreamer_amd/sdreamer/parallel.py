@@ -232,8 +232,8 @@ def barlow(x1, x2, lambd, world):
 
 
 def infonce(x1, x2, world):
-    """InfoNCE (dreamer.py:533-542) with every rank's rows as negatives: x2 of all ranks is gathered (one sum
-    all-reduce of a zero-padded buffer), this rank's rows are labelled with their global column."""
+    """InfoNCE (dreamer.py:533-542) with every rank's rows as negatives: x2 of all ranks is gathered (one
+    all_gather_into_tensor, all_gather_rows), this rank's rows are labelled with their global column."""
     x2 = x2.detach().contiguous()
     if world > 1 and is_dist():
         x2g = all_gather_rows(x2, world)

@@ -32,12 +32,16 @@ STREAM_OBS_AUG = 7  # DreamerPro's augmented-view posterior scan
 FUSED_SCAN = os.environ.get("SDREAMER_FUSED_SCAN", "1") != "0"
 # debugging aid: fill the fused backward's scratch tensors with NaN so any element read before it is written shows
 _POISON = os.environ.get("SDREAMER_DEBUG_POISON", "0") != "0"
+# rows per workgroup tile of the fused scan (csrc/scan.hip row_tile): every B rows run as ceil(B / tile) tiles in the
+# same launches; 0 = the 16-row MFMA tile
+SCAN_ROW_TILE = int(os.environ.get("SDREAMER_SCAN_ROWTILE", "0"))
+SCAN_TRACE = None  # uint64 device tensor: per-launch / per-workgroup phase timestamps (tools/scan_trace.py)
 
 
 def _fused_scan_ok(rssm, B):
     """Shapes csrc/scan.hip is instantiated for (every BASELINE config); others take the per-op HIP kernels."""
     D, U, G, SK, Kd = rssm._deter, rssm._hidden, rssm._blocks, rssm.flat_stoch, rssm._discrete
-    if not FUSED_SCAN or B > 16 or G > 8 or D % G or D > 4096:
+    if not FUSED_SCAN or B > 4096 or G > 8 or D % G or D > 4096:
         return False
     return U == 256 and D // G in (256, 512) and SK in (512, 1024) and Kd in (16, 32, 64) and D % Kd == 0 and \
         D % 64 == 0
@@ -48,6 +52,9 @@ def _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, work, stream_id=S
     D, U, SK, Kd, G = rssm._deter, rssm._hidden, rssm.flat_stoch, rssm._discrete, rssm._blocks
     d.B, d.T, d.D, d.U, d.SK, d.Kd, d.G = B, T, D, U, SK, Kd, G
     d.ks_d, d.ks_s = 4, 2  # K splits of the D-wide / SK-wide step GEMMs (slabs summed by the consumer)
+    d.row_tile = SCAN_ROW_TILE
+    if SCAN_TRACE is not None:  # measurement aid (tools/scan_trace.py, a -DSD_SCAN_TRACE build of the library)
+        d.trace = SCAN_TRACE.data_ptr()
     d.eps, d.unimix = K.EPS, rssm._unimix_ratio
     sh, sp = K.seed_args(seed)
     d.seed, d.seed_ptr, d.stream_id, d.group_offset = sh, sp, int(stream_id), int(row_offset) * rssm._stoch
@@ -164,8 +171,8 @@ class RSSM(nn.Module):
         return stoch, deter
 
     def takes_extra_grads(self, B):
-        """observe() on B rows is one ObserveScan (not 16-row chunks), so its backward can take _bwd_extra"""
-        return not (B > 16 and _fused_scan_ok(self, 16))
+        """observe() on B rows is one ObserveScan, so its backward can take _bwd_extra"""
+        return True
 
     def get_feat(self, stoch, deter):  # rssm.py:211-217
         return torch.cat([stoch.reshape(*stoch.shape[:-2], self.flat_stoch), deter], -1)
@@ -177,13 +184,7 @@ class RSSM(nn.Module):
         r = reset.reshape(B, T).to(torch.uint8)
         stoch0, deter0 = initial
         s0 = stoch0.reshape(B, -1)
-        if B > 16 and _fused_scan_ok(self, 16):
-            # rows are independent: batches above the fused scan's 16-row tile run as 16-row scans (each its own
-            # autograd node; noise indexed by global row, weight gradients accumulate)
-            outs = [ObserveScan.apply(embed[c:c + 16], action[c:c + 16], r[c:c + 16].contiguous(),
-                                      s0[c:c + 16].contiguous(), deter0[c:c + 16].contiguous(), self, seed,
-                                      int(row_offset) + c, stream_id) for c in range(0, B, 16)]
-            return tuple(torch.cat([o[i] for o in outs], 0) for i in range(3))
+        # rows are independent sequences: B > 16 runs as row tiles side by side inside every scan launch
         return ObserveScan.apply(embed, action, r, s0.contiguous(), deter0.contiguous(), self, seed, int(row_offset),
                                  stream_id)
 
@@ -499,9 +500,15 @@ class ObserveScan(torch.autograd.Function):
         d.bm_grads = 1
         if extra is not None:
             gs2, gd2 = extra
-            if gs2.stride(-1) != 1 or gd2.stride(-1) != 1 or gs2.stride(-2) != gd2.stride(-2):
-                raise ValueError("posterior gradient halves need unit column stride and one row stride")
-            d.d_stoch2, d.d_deter2, d.ld_g2 = gs2.data_ptr(), gd2.data_ptr(), gs2.stride(-2)
+            # the kernels index row (b, t) as (b*T + t) * ld_g2: unit column stride, one row stride for both halves,
+            # and the (B, T) rows evenly spaced; otherwise the explicit adds (the caller's former torch.add order)
+            if gs2.stride(-1) == 1 and gd2.stride(-1) == 1 and gs2.stride(-2) == gd2.stride(-2) and \
+                    gs2.stride(-3) == T * gs2.stride(-2) and gd2.stride(-3) == T * gd2.stride(-2):
+                d.d_stoch2, d.d_deter2, d.ld_g2 = gs2.data_ptr(), gd2.data_ptr(), gs2.stride(-2)
+            else:
+                ds_out = (0 if ds_out is None else ds_out) + gs2.reshape(B, T, SK)
+                dd_out = (0 if dd_out is None else dd_out) + gd2.reshape(B, T, D)
+                d.d_stoch, d.d_deter = ds_out.data_ptr(), dd_out.data_ptr()
         nat.call("sd_rssm_scan_bwd", ctypes.addressof(d), K.stream())
         gb = ops.grad_buf
         f = lambda x: x.reshape(M, -1)  # noqa: E731

@@ -452,6 +452,42 @@ def test_barlow_dist_steps(Nr, E):
     close(xg.grad, xr.grad, 1e-5, "dx1")
 
 
+@pytest.mark.parametrize("Nr,E", [(512, 1024), (96, 64)])
+def test_barlow_dist_steps_two_shards(Nr, E):
+    """The sharded arithmetic of parallel.barlow_dist on the GPU launches, 2 ranks simulated in one process: each half
+    of the rows runs colsums / center / finish / the loss backward with Nt = 2 R != R, the two all-reduces replaced
+    by sums of the halves' tensors. Loss and c of every shard equal the full-batch torch fp32 definition
+    (dreamer.py:525-532), and the ranks' dx1 rows (scaled by world) over world equal its gradient."""
+    from sdreamer import parallel
+    BS = parallel.BarlowSteps
+    world, R = 2, Nr // 2
+    x1 = torch.randn(Nr, E, generator=_g(5)) * 2 + 0.5
+    x2 = torch.randn(Nr, E, generator=_g(6)) - 0.25
+    xr = x1.clone().requires_grad_()
+    x1n = (xr - xr.mean(0)) / (xr.std(0) + 1e-8)
+    x2n = (x2 - x2.mean(0)) / (x2.std(0) + 1e-8)
+    c_ref = torch.mm(x1n.T, x2n) / Nr
+    off = ~torch.eye(E, dtype=torch.bool)
+    loss = (torch.diagonal(c_ref) - 1).pow(2).sum() + 5e-4 * c_ref[off].pow(2).sum()
+    loss.backward()
+    Nt = float(Nr)
+    shards = [(x1[r * R:(r + 1) * R].to(DEV), x2[r * R:(r + 1) * R].to(DEV)) for r in range(world)]
+    sums = sum(BS.colsums(a, b) for a, b in shards)  # all-reduce 1
+    cen = [BS.center(a, b, sums, Nt) for a, b in shards]
+    stats = sum(s for _, _, s in cen)  # all-reduce 2
+    dx = []
+    for (a, _), (_, d2, _) in zip(shards, cen):
+        c, st, n2, z2 = BS.finish(stats, sums, Nt, d2)
+        close(c, c_ref, 1e-5, "c")
+        close(n2, x2n[len(dx) * R:(len(dx) + 1) * R], 1e-5, "n2 rows")
+        xg = a.clone().requires_grad_()
+        ld = parallel._DistBarlowLoss.apply(xg, c, sums, st, n2, z2, 5e-4, Nt, world)
+        close(ld, loss, 1e-5, "loss")
+        ld.backward()
+        dx.append(xg.grad)
+    close(torch.cat(dx) / world, xr.grad, 1e-5, "dx1 (mean over ranks)")
+
+
 @pytest.mark.parametrize("warmup", [1000, 0])
 def test_laprop_agc_step(warmup):
     """sd_agc_laprop_step (AGC agc.py:15-53 + LaProp laprop.py:85-116 + LambdaLR warm-up dreamer.py:214-225) vs the

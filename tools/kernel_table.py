@@ -22,6 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_table import _db, counters, short  # noqa: E402
 
 MARK_US = []
+LONG_US = 300.0  # dispatches at least this long carry their own GRBM-derived clock
 
 
 def window(tdir):
@@ -65,15 +66,30 @@ def main(tdir, steps, out_json, *pdirs):
         if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
             r["hbm_bytes"] = 1024.0 * (2 * c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0))
         if "GRBM_GUI_ACTIVE" in c:
-            clk = c["GRBM_GUI_ACTIVE"] / 8 / avg  # cycles per ns = GHz
-            r["clock_ghz"] = clk
-            if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
-                r["mfma_util"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * clk * avg)
+            r["_grbm_clk"] = c["GRBM_GUI_ACTIVE"] / 8 / avg  # cycles per ns = GHz (trustworthy >= 0.3 ms only)
+            r["_mfma_busy"] = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
         if "TCC_HIT_sum" in c:
             h, m = c["TCC_HIT_sum"], c.get("TCC_MISS_sum", 0.0)
             r["l2_hit"] = h / (h + m) if h + m else None
         rows.append(r)
-    res = {"empty_dispatch_us": MARK_US, "steps": steps, "window_ms_per_update": span / steps / 1e6, "kernel_ms_per_update": total / steps / 1e6,
+    # GRBM_GUI_ACTIVE / duration reads high (4-6 GHz) on dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md); those
+    # rows take the median clock of this run's >= 0.3 ms dispatches (same run, same DVFS state), and MFMA utilisation
+    # is derived from whichever clock the row carries
+    long_clk = sorted(r["_grbm_clk"] for r in rows if "_grbm_clk" in r and r["avg_us"] >= LONG_US)
+    ref_clk = long_clk[len(long_clk) // 2] if long_clk else None
+    for r in rows:
+        g = r.pop("_grbm_clk", None)
+        busy = r.pop("_mfma_busy", None)
+        if g is None:
+            continue
+        if r["avg_us"] >= LONG_US or ref_clk is None:
+            clk, r["clock_source"] = g, "GRBM_GUI_ACTIVE / duration"
+        else:
+            clk, r["clock_source"] = ref_clk, f"median of the >= {LONG_US:.0f} us dispatches"
+        r["clock_ghz"] = clk
+        if busy is not None:
+            r["mfma_util"] = busy / (1024 * clk * r["avg_us"] * 1e3)
+    res = {"empty_dispatch_us": MARK_US, "reference_clock_ghz": ref_clk, "steps": steps, "window_ms_per_update": span / steps / 1e6, "kernel_ms_per_update": total / steps / 1e6,
            "trace_dir": os.path.basename(os.path.normpath(tdir)), "rows": rows}
     json.dump(res, open(out_json, "w"), indent=1)
     print(f"timed window: {span / steps / 1e6:.3f} ms per update ({steps} updates); kernel time "
