@@ -422,7 +422,7 @@ typedef struct sd_rssm_scan {
   /* measurement aid (a build with -DSD_SCAN_TRACE only; NULL otherwise): per launch slot and workgroup 4 timestamps
      (s_memrealtime, 100 MHz): entry, operands staged, contraction reduced, exit. Slot = t * 8 + phase (forward) or
      (T + t) * 8 + phase (backward); trace_slot is set per launch by the library */
-  unsigned long long* trace;
+  uint64_t* trace;
   int trace_slot;
 } sd_rssm_scan;
 int sd_rssm_scan_work_floats(const sd_rssm_scan* d);

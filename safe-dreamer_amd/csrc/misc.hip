@@ -582,7 +582,8 @@ extern "C" int sd_infonce_bwd(const float* logits, long ld, int n, int ncol, lon
 // ---- replay slices (utils/buffer.py:27-53 semantics, HBM storage laid out (capacity, env, row)): every key of a
 // batch of B slices gathered in ONE launch straight into the consumer's buffers, and the latent write-back as one
 // scatter. Slice b starts at (t0, e) = starts[pick[b]]; key k copies steps j = 0..steps-1 of time (t0 + shift + j) %
-// cap (data keys: shift 1, the action one step back: shift 0, the initial latent: steps 1, shift 0).
+// cap (data keys: shift 1, the action one step back: shift 0, the initial latent: steps 1, shift 0). A storage row
+// that several slices write back takes the value of the slice with the largest b.
 namespace {
 __global__ __launch_bounds__(256) void slices_kernel(sd_slice_keys ks, const int64_t* __restrict__ starts,
                                                      const int64_t* __restrict__ pick, int B, int L, long cap, int E,
@@ -594,6 +595,14 @@ __global__ __launch_bounds__(256) void slices_kernel(sd_slice_keys ks, const int
   if (b >= B || j >= key.steps) return;
   const int64_t t0 = starts[2 * pick[b]], e = starts[2 * pick[b] + 1];
   const long t = (t0 + key.shift + j) % cap;
+  if (scatter) {
+    // overlapping slices write one storage row several times: the slice with the largest b wins (a sequential
+    // scatter in row order), so the write-back is deterministic (torch's index_put with duplicates is not)
+    for (int b2 = b + 1; b2 < B; ++b2) {
+      const int64_t s2 = starts[2 * pick[b2]];
+      if (starts[2 * pick[b2] + 1] == e && ((t - s2 - key.shift) % cap + cap) % cap < key.steps) return;
+    }
+  }
   if (k == 0 && threadIdx.x == 0 && t_out && !scatter) {  // index of the data rows for the write-back
     const long tt = (t0 + 1 + j) % cap;
     t_out[(long)b * L + j] = tt;

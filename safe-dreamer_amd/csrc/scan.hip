@@ -105,13 +105,13 @@ constexpr int core_lds_floats() { return NW * NT * 256 + MR * 16 * NT; }
 // contraction reduced / exit (s_memrealtime, 100 MHz) and stores them at exit into trace[slot][workgroup][4].
 #ifdef SD_SCAN_TRACE
 constexpr int TR_WG = 2048;  // workgroup slots per launch
-#define SD_TR_BEGIN unsigned long long tr_[4] = {__builtin_amdgcn_s_memrealtime(), 0ull, 0ull, 0ull};
+#define SD_TR_BEGIN uint64_t tr_[4] = {__builtin_amdgcn_s_memrealtime(), 0ull, 0ull, 0ull};
 #define SD_TR(k) tr_[k] = __builtin_amdgcn_s_memrealtime();
 #define SD_TR_END(buf, slot)                                                                               \
   if (threadIdx.x == 0 && (buf)) {                                                                         \
     tr_[3] = __builtin_amdgcn_s_memrealtime();                                                             \
     const long wg_ = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);           \
-    unsigned long long* o_ = (buf) + ((long)(slot) * TR_WG + wg_) * 4;                                     \
+    uint64_t* o_ = (buf) + ((long)(slot) * TR_WG + wg_) * 4;                                     \
     for (int i_ = 0; i_ < 4; ++i_) o_[i_] = tr_[i_];                                                        \
   }
 #else
@@ -248,7 +248,7 @@ struct SlabProb {
   long ldw;
   float* out;                 // slab s at out + s*M*N
   const unsigned char* mask;  // rows whose input is reset (output row forced to 0), or null
-  unsigned long long* trace;  // SD_SCAN_TRACE builds: phase timestamps (sd_rssm_scan.trace), slot below
+  uint64_t* trace;            // SD_SCAN_TRACE builds: phase timestamps (sd_rssm_scan.trace), slot below
   int slot;
 };
 

@@ -55,6 +55,8 @@ def _parse_struct(path, name):
         toks = decl.replace("const ", "").replace("*", " ").replace(",", " , ").split()
         if toks[0] == "unsigned":
             toks = toks[1:]
+        if toks[:2] == ["long", "long"]:  # one type of two words
+            toks = ["long"] + toks[2:]
         base, names = toks[0], [t for t in toks[1:] if t != ","]
         for n in names:
             typ = c_ptr if is_ptr else scalars[base]

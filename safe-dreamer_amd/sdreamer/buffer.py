@@ -148,12 +148,24 @@ class Buffer:
             self._last = None
             return
         t_idx, e_idx = index
+        keep = self._last_writer(t_idx, e_idx).reshape(-1)
+        ti, ei = t_idx.reshape(-1)[keep], e_idx.reshape(-1)[keep]
         if "stoch" in self._store:
-            self._store["stoch"][t_idx.reshape(-1), e_idx.reshape(-1)] = stoch.reshape(-1, *stoch.shape[2:]).to(
-                self.storage_device)
+            self._store["stoch"][ti, ei] = stoch.reshape(-1, *stoch.shape[2:]).to(self.storage_device)[keep]
         if "deter" in self._store:
-            self._store["deter"][t_idx.reshape(-1), e_idx.reshape(-1)] = deter.reshape(-1, deter.shape[-1]).to(
-                self.storage_device)
+            self._store["deter"][ti, ei] = deter.reshape(-1, deter.shape[-1]).to(self.storage_device)[keep]
+
+    def _last_writer(self, t_idx, e_idx):
+        """(B, L) bool: False where a later slice (larger b) writes the same storage row. Overlapping slices make the
+        write-back hit one row several times; index_put with duplicate indices picks an arbitrary one on the GPU, so
+        the slice with the largest b wins here (a sequential scatter in row order), as in sd_replay_slices."""
+        B, L = t_idx.shape
+        start, env = t_idx[:, :1], e_idx[:, :1]  # slices are consecutive (mod cap) from their first row
+        cover = ((t_idx[:, :, None] - start.reshape(1, 1, B)) % self.cap < L) & \
+            (env.reshape(B, 1, 1) == env.reshape(1, 1, B))
+        later = torch.arange(B, device=t_idx.device)
+        cover &= (later.reshape(1, 1, B) > later.reshape(B, 1, 1))
+        return ~cover.any(-1)
 
     def count(self):
         if self._store is None:

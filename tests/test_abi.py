@@ -44,7 +44,7 @@ def test_gemm_desc_layout_matches_c():
 
 @pytest.mark.parametrize("cname,pyname,probe", [
     ("sd_rssm_scan", "ScanDesc", ["B", "eps", "seed", "seed_ptr", "group_offset", "W0", "WlT", "reset", "stoch", "dl",
-                                  "work"]),
+                                  "work", "ld_g2", "row_tile", "trace", "trace_slot"]),
     ("sd_imagine", "ImagineDesc", ["eps", "seed", "seed_ptr", "row_offset", "Wa", "Wao", "Wl", "feats", "work",
                                    "t_end", "actor_h0"]),
     ("sd_stat_req", "StatReq", ["x", "n", "kind", "out", "scale"]),

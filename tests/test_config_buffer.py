@@ -63,3 +63,25 @@ def test_buffer_update_writes_back():
     assert torch.all(buf._store["stoch"][t_idx, e_idx] == 7.0)
     assert torch.all(buf._store["deter"][t_idx, e_idx] == -2.0)
     assert buf.count() == 40 * 4
+
+
+def test_buffer_update_overlapping_slices_last_row_wins():
+    """Overlapping slices write one storage row several times; the slice with the largest b wins (deterministic,
+    the rule sd_replay_slices' scatter follows)."""
+    buf, src = _buffer()
+    L = buf.batch_length
+    # slices 0 and 2 overlap on env 1 (starts 3 and 5), slice 1 on env 2 is disjoint, slice 3 repeats slice 0
+    t0 = torch.tensor([3, 10, 5, 3])
+    env = torch.tensor([1, 2, 1, 1])
+    B = len(t0)
+    t_idx = (t0[:, None] + 1 + torch.arange(L)[None]) % buf.cap
+    e_idx = env[:, None].expand(B, L)
+    st = torch.arange(B, dtype=torch.float32).reshape(B, 1, 1, 1).expand(B, L, 3, 4).contiguous()
+    de = torch.arange(B, dtype=torch.float32).reshape(B, 1, 1).expand(B, L, 5).contiguous()
+    buf.update([t_idx, e_idx], st, de)
+    for b in range(B):
+        for j in range(L):
+            t, e = int(t_idx[b, j]), int(env[b])
+            writers = [b2 for b2 in range(B) if int(env[b2]) == e and t in t_idx[b2].tolist()]
+            assert float(buf._store["deter"][t, e, 0]) == max(writers)
+            assert float(buf._store["stoch"][t, e, 0, 0]) == max(writers)

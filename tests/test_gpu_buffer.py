@@ -38,9 +38,11 @@ def test_sample_into_and_writeback_match_reference_semantics():
             assert torch.equal(dst[k], data[k]), (it, k)
         assert torch.equal(dst_init[0], initial[0]) and torch.equal(dst_init[1], initial[1])
         assert torch.equal(idx_b[0], index[0]) and torch.equal(idx_b[1], index[1])
-        # overlapping slices write the same (t, e) twice (index_put leaves the winner unspecified, as does the
-        # scatter): make the written value a function of (t, e) so every writer agrees
-        key = (index[0] * 7 + index[1] + 100 * it).float()
+        # overlapping slices write the same (t, e) twice: both paths keep the slice with the largest b (values that
+        # differ per slice row, so a wrong winner shows)
+        B, L = index[0].shape
+        key = (torch.arange(B, device=index[0].device)[:, None] * 1000 + torch.arange(L, device=index[0].device)[None]
+               + 100 * it).float()
         post_s = key[..., None, None].expand(*index[0].shape, 4, 5).contiguous()
         post_d = key[..., None].expand(*index[0].shape, 7).contiguous() * 0.5
         a.update(index, post_s, post_d)
