@@ -160,20 +160,22 @@ SD_DEV void ld_slabs(f32x4 (&v)[NI], const float* rowp, long sstride, int ks, in
     for (int s = 1; s < KS; ++s) v[i] += part[s][i];
   }
 }
-// per-tile row partials part[i*16 + row], i < tiles <= 32*NP
+// per-tile row partials, row-major: part[row * tiles + i], i < tiles <= 128*NP (tiles % 4 == 0): a row's partials
+// are one contiguous run, read as float4s by the row's 32 threads (the column-major layout cost 64 cache lines per
+// wave instruction)
 template <int NP>
-SD_DEV void ld_parts(float (&v)[NP], const float* part, int tiles, int row, int t32) {
+SD_DEV void ld_parts(f32x4 (&v)[NP], const float* rowp, int tiles, int t32) {
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
-    const int i = t32 + 32 * j;
-    v[j] = i < tiles ? part[i * MR + row] : 0.f;
+    const int i = 4 * (t32 + 32 * j);
+    v[j] = i < tiles ? *reinterpret_cast<const f32x4*>(rowp + i) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 }
 template <int NP>
-SD_DEV float sum_parts(const float (&v)[NP]) {
+SD_DEV float sum_parts(const f32x4 (&v)[NP]) {
   float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < NP; ++j) s += v[j];
+  for (int j = 0; j < NP; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
   return group_sum<32>(s);
 }
 SD_DEV float sumsq4(f32x4 x) { return x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]; }
@@ -312,7 +314,9 @@ SD_DEV long in_row(const sd_rssm_scan& d, int t, int b) {
   return d.bm_inputs ? (long)b * d.T + t : (long)t * d.B + b;
 }
 
-template <int CPW, int NG>
+// X0F: x0 = silu(rms(x0p)) was formed by the previous step's k_logit_rows (written into xcat), read as it stands;
+// otherwise (t = 0, or the k_logit path) summed from the split-K slabs and normalised here
+template <int CPW, int NG, bool X0F>
 __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_TR_BEGIN
@@ -328,21 +332,30 @@ __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   const long tBU = (long)t * B * UH;
   f32x4 h[NG], x0[NU], x1[NU], x2v[NU], b0v[NU], b1v[NU], n0v[NU], n1v[NU];
   ld_row(h, d.h_in + (long)t * B * D + (long)gr * D + (long)g * Dg, Dg, rv, t32);
-  ld_slabs<NU, KSM>(x0, w.x0s + (long)gr * UH, (long)B * UH, d.ks_d, UH, rv, t32);
+  if constexpr (X0F) {
+    ld_row(x0, d.xcat + 3 * tBU + (long)gr * 3 * UH, UH, rv, t32);
+  } else {
+    ld_slabs<NU, KSM>(x0, w.x0s + (long)gr * UH, (long)B * UH, d.ks_d, UH, rv, t32);
+    ld_row(b0v, d.b0, UH, true, t32);
+    ld_row(n0v, d.n0, UH, true, t32);
+  }
   ld_slabs<NU, KS1>(x1, w.x1s + (long)gr * UH, (long)B * UH, d.ks_s, UH, rv, t32);
   ld_row(x2v, d.x2 + in_row(d, t, gr) * UH, UH, rv, t32);
-  ld_row(b0v, d.b0, UH, true, t32);
   ld_row(b1v, d.b1, UH, true, t32);
-  ld_row(n0v, d.n0, UH, true, t32);
   ld_row(n1v, d.n1, UH, true, t32);
   const float bhv = d.bh[n0 + (tid & 15)];
 #pragma unroll
-  for (int i = 0; i < NU; ++i) {
-    x0[i] += b0v[i];
-    x1[i] += b1v[i];
-  }
+  for (int i = 0; i < NU; ++i) x1[i] += b1v[i];
   f32x4 y0[NU], y1[NU];
-  const float r0 = rms_silu_rows(x0, n0v, UH, d.eps, rv, y0);
+  float r0 = 0.f;
+  if constexpr (X0F) {
+#pragma unroll
+    for (int i = 0; i < NU; ++i) y0[i] = x0[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < NU; ++i) x0[i] += b0v[i];
+    r0 = rms_silu_rows(x0, n0v, UH, d.eps, rv, y0);
+  }
   const float r1 = rms_silu_rows(x1, n1v, UH, d.eps, rv, y1);
   float* P = smem + core_lds_floats<1>() + row * ldp;
   st_row(P, h, Dg, t32);
@@ -352,9 +365,11 @@ __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   if (rv && tile < 3) {
     float* xc = d.xcat + 3 * tBU + (long)gr * 3 * UH;
     if (tile == 0) {
-      st_row(d.x0p + tBU + (long)gr * UH, x0, UH, t32);
-      st_row(xc, y0, UH, t32);
-      if (t32 == 0) d.r0[(long)t * B + gr] = r0;
+      if (!X0F) {  // (X0F: written by the previous step's k_logit_rows)
+        st_row(d.x0p + tBU + (long)gr * UH, x0, UH, t32);
+        st_row(xc, y0, UH, t32);
+        if (t32 == 0) d.r0[(long)t * B + gr] = r0;
+      }
     } else if (tile == 1) {
       st_row(d.x1p + tBU + (long)gr * UH, x1, UH, t32);
       st_row(xc + UH, y1, UH, t32);
@@ -374,7 +389,7 @@ __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
     const float v = C[er * 16 + c] + bhv;
     if (er < nr) d.hp[(long)t * B * D + (long)(rb + er) * D + n0 + c] = v;
     const float ss = group_sum<16>(er < nr ? v * v : 0.f);
-    if (c == 0) w.ssh[((long)blockIdx.z * (D / 16) + tile) * MR + er] = ss;
+    if (c == 0) w.ssh[((long)blockIdx.z * MR + er) * (D / 16) + tile] = ss;
   }
   SD_TR_END(d.trace, d.trace_slot)
 }
@@ -395,8 +410,8 @@ __global__ __launch_bounds__(NTHR) void k_gate(sd_rssm_scan d, Work w, int t) {
   core.load_b(wt, Dg / 16, wave, q);
   const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
   const bool rv = row < nr;
-  float pv[8];
-  ld_parts(pv, w.ssh + (long)blockIdx.z * D, D / 16, row, t32);
+  f32x4 pv[2];
+  ld_parts(pv, w.ssh + ((long)blockIdx.z * MR + row) * (D / 16), D / 16, t32);
   f32x4 hv[NG], nv[NG];
   ld_row(hv, d.hp + (long)t * B * D + (long)gr * D + (long)g * Dg, Dg, rv, t32);
   ld_row(nv, d.nh + (long)g * Dg, Dg, true, t32);
@@ -537,7 +552,7 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
   constexpr int NC = CPG * KD, TPC = NTHR / NC, KPT = UH / TPC, NQ = KPT / 4;
   static_assert(NTHR % NC == 0 && UH % (4 * TPC) == 0, "column split");
   __shared__ __attribute__((aligned(16))) float y[UH];
-  __shared__ float red[NW], lg[NC], hv[CPG];
+  __shared__ float red[NW], red0[NW], lg[NC], hv[CPG];
   __shared__ int hot[CPG];
   SD_TR_BEGIN
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -582,14 +597,43 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
     x += d.eproj[in_row(d, t, b) * UH + tid];
     nw = d.no[tid];
   }
+  // one workgroup per row also forms the NEXT step's x0 = silu(rms(x0p)), x0p = sum of the _dyn_in0 slabs k_slab
+  // wrote before this launch + b0 (rssm.py:52-56), so k_hid stages the finished row instead of every column tile
+  // summing the slabs and normalising again (same slab order and bias add as k_hid's own path)
+  const bool x0w = more && g == (gridDim.x > 1 ? 1 : 0);
+  float x0v = 0.f, n0w = 0.f;
+  if (x0w && tid < UH) {
+    float part[KSM];
+#pragma unroll
+    for (int s = 0; s < KSM; ++s) part[s] = s < d.ks_d ? w.x0s[(long)s * B * UH + (long)b * UH + tid] : 0.f;
+    x0v = part[0];
+#pragma unroll
+    for (int s = 1; s < KSM; ++s) x0v += part[s];
+    x0v += d.b0[tid];
+    n0w = d.n0[tid];
+  }
   float ss = wave_sum(x * x);
-  if (lane == 0) red[wave] = ss;
+  const float ss0 = wave_sum(x0v * x0v);
+  if (lane == 0) {
+    red[wave] = ss;
+    red0[wave] = ss0;
+  }
   __syncthreads();
   SD_TR(1)
   ss = 0.f;
 #pragma unroll
   for (int i = 0; i < UH / 64; ++i) ss += red[i];
   const float r = rsqrtf(ss / (float)UH + d.eps);
+  if (x0w && tid < UH) {
+    float s0 = 0.f;
+#pragma unroll
+    for (int i = 0; i < UH / 64; ++i) s0 += red0[i];
+    const float r0 = rsqrtf(s0 / (float)UH + d.eps);
+    const long o = (long)(t + 1) * B * UH + (long)b * UH + tid;
+    d.x0p[o] = x0v;
+    d.xcat[2 * (long)(t + 1) * B * UH + o + (long)b * 2 * UH] = siluf_(x0v * r0 * n0w);  // xcat (T, B, 3U), cols 0..U
+    if (tid == 0) d.r0[(long)(t + 1) * B + b] = r0;
+  }
   if (tid < UH) {
     const float yv = siluf_(x * r * nw);
     y[tid] = yv;
@@ -832,7 +876,7 @@ __global__ __launch_bounds__(NTHR) void k_dhh(sd_rssm_scan d, Work w, int t) {
       part = gq * xh;
     }
     part = group_sum<16>(part);
-    if (c == 0) w.dotp[((long)blockIdx.z * (D / 16) + tile) * MR + er] = part;
+    if (c == 0) w.dotp[((long)blockIdx.z * MR + er) * (D / 16) + tile] = part;
   }
   SD_TR_END(d.trace, d.trace_slot)
 }
@@ -866,8 +910,8 @@ __global__ __launch_bounds__(NTHR) void k_dhp(sd_rssm_scan d, Work w, int t) {
   core.load_b(wt, Dg / 16, wave, q);
   const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
   const bool rv = row < nr;
-  float pv[8];
-  ld_parts(pv, w.dotp + (long)blockIdx.z * D, D / 16, row, t32);
+  f32x4 pv[2];
+  ld_parts(pv, w.dotp + ((long)blockIdx.z * MR + row) * (D / 16), D / 16, t32);
   const long ob = (long)gr * D + (long)g * Dg;
   f32x4 gq[NG], xv[NG];
   ld_row(gq, w.gq + ob, Dg, rv, t32);
@@ -1149,8 +1193,14 @@ int fwd_phase(const sd_rssm_scan& d, const Work& w, bool lrows, int which, int t
     SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr, d.trace, dd.trace_slot};
     SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(UH / 16, ks_s * nt, 1), NTHR, core1, st>>>(p, p, B, UH, span_s, ks_s, rt));
   } else if (which == 1) {
-    SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG>>(lds_hid))) return SD_EARG;
-                                   k_hid<CP, NG><<<dim3(D / 16, 1, nt), NTHR, lds_hid, st>>>(dd, w, t)));
+    // x0 finished by the previous step's k_logit_rows (lrows, t > 0)
+    if (lrows && t > 0) {
+      SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG, true>>(lds_hid))) return SD_EARG;
+                                     k_hid<CP, NG, true><<<dim3(D / 16, 1, nt), NTHR, lds_hid, st>>>(dd, w, t)));
+    } else {
+      SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG, false>>(lds_hid))) return SD_EARG;
+                                     k_hid<CP, NG, false><<<dim3(D / 16, 1, nt), NTHR, lds_hid, st>>>(dd, w, t)));
+    }
   } else if (which == 2) {
     SD_NG_SWITCH(Dg, if (!(raise_lds<k_gate<NG, NG>>(lds_gate))) return SD_EARG;
                  k_gate<NG, NG><<<dim3(D / 16, 1, nt), NTHR, lds_gate, st>>>(dd, w, t));

@@ -35,6 +35,9 @@ _POISON = os.environ.get("SDREAMER_DEBUG_POISON", "0") != "0"
 # rows per workgroup tile of the fused scan (csrc/scan.hip row_tile): every B rows run as ceil(B / tile) tiles in the
 # same launches; 0 = the 16-row MFMA tile
 SCAN_ROW_TILE = int(os.environ.get("SDREAMER_SCAN_ROWTILE", "0"))
+# per direction (forward / backward launches), overriding SCAN_ROW_TILE when set
+SCAN_ROW_TILE_FWD = int(os.environ.get("SDREAMER_SCAN_ROWTILE_FWD", "-1"))
+SCAN_ROW_TILE_BWD = int(os.environ.get("SDREAMER_SCAN_ROWTILE_BWD", "-1"))
 SCAN_TRACE = None  # uint64 device tensor: per-launch / per-workgroup phase timestamps (tools/scan_trace.py)
 
 
@@ -47,12 +50,13 @@ def _fused_scan_ok(rssm, B):
         D % 64 == 0
 
 
-def _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, work, stream_id=STREAM_OBS):
+def _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, work, stream_id=STREAM_OBS, bwd=False):
     d = nat.ScanDesc()
     D, U, SK, Kd, G = rssm._deter, rssm._hidden, rssm.flat_stoch, rssm._discrete, rssm._blocks
     d.B, d.T, d.D, d.U, d.SK, d.Kd, d.G = B, T, D, U, SK, Kd, G
     d.ks_d, d.ks_s = 4, 2  # K splits of the D-wide / SK-wide step GEMMs (slabs summed by the consumer)
-    d.row_tile = SCAN_ROW_TILE
+    side = SCAN_ROW_TILE_BWD if bwd else SCAN_ROW_TILE_FWD
+    d.row_tile = side if side >= 0 else SCAN_ROW_TILE
     if SCAN_TRACE is not None:  # measurement aid (tools/scan_trace.py, a -DSD_SCAN_TRACE build of the library)
         d.trace = SCAN_TRACE.data_ptr()
     d.eps, d.unimix = K.EPS, rssm._unimix_ratio
@@ -487,7 +491,7 @@ class ObserveScan(torch.autograd.Function):
         d_gates, d_hh, d_hp, d_xcat = e(T, B, 3 * D), e(T, B, D), e(T, B, D), e(T, B, 3 * U)
         tr = rssm._bwd_tr if rssm._bwd_tr is not None else rssm.scan_bwd_weights()
         x2 = ctx.x2
-        d = _scan_desc(rssm, P, B, T, ctx.seed, ctx.row_offset, rt, x2, x2, None, ctx.stream_id)
+        d = _scan_desc(rssm, P, B, T, ctx.seed, ctx.row_offset, rt, x2, x2, None, ctx.stream_id, bwd=True)
         work = e(_scan_work(d))
         d.work = work.data_ptr()
         for k, v in list(tr.items()) + [("s_in", s_in), ("h_in", h_in), ("x0p", x0p), ("x1p", x1p), ("r0", r0),
