@@ -881,61 +881,75 @@ __global__ __launch_bounds__(NTHR) void k_dhh(sd_rssm_scan d, Work w, int t) {
   SD_TR_END(d.trace, d.trace_slot)
 }
 
-// d_hp_g = RMSNorm backward (prologue, from g*w and the row partials); then two problems in one grid:
-//   P0: d_xcat slab g = d_hp_g . Wsh[g-rows]   ((3U/16) * G workgroups)
-//   P1: d_hin[:, g] += d_hp_g . Wbd[g]          (D/16 workgroups)
-template <int CPW, int NG>
+// d_xcat slabs k_dhp writes: slab s covers G / KX consecutive blocks (KX = 8 = G: one per block). Fewer slabs mean
+// fewer, larger P0 workgroups and less for k_carry to stage (each of its workgroups sums KX slabs of 16 rows)
+#ifndef SD_SCAN_KX
+#define SD_SCAN_KX 8
+#endif
+__host__ __device__ inline int kx_of(int G) { return G % SD_SCAN_KX == 0 ? SD_SCAN_KX : G; }
+
+// d_hp = RMSNorm backward (prologue, from g*w and the row partials) over the workgroup's K span; then two problems in
+// one grid:
+//   P0: d_xcat slab s = d_hp[:, blocks of s] . Wsh[those rows]   ((3U/16) * KX workgroups, K = G/KX blocks)
+//   P1: d_hin[:, g] += d_hp_g . Wbd[g]                            (D/16 workgroups, K = one block)
+// CPW / NGX cover the longest span (P0); P1 masks the chunks past its block.
+template <int CPW, int NGX>
 __global__ __launch_bounds__(NTHR) void k_dhp(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_TR_BEGIN
   SD_THREAD_IDS
   SD_ROW_TILE
-  const int B = d.B, D = d.D, Dg = D / d.G, ldp = Dg + 4, X = 3 * UH;
-  const int NX = (X / 16) * d.G;
+  const int B = d.B, D = d.D, Dg = D / d.G, X = 3 * UH;
+  const int KX = kx_of(d.G), NX = (X / 16) * KX;
   const int blk = blockIdx.x;
   const bool p0 = blk < NX;
-  int g, n0;
+  int n0, k0, K, sl = 0;
   const float* wrow;
   if (p0) {
-    g = blk / (X / 16);
+    sl = blk / (X / 16);
     n0 = (blk % (X / 16)) * 16;
-    wrow = d.WshT + (long)(n0 + l16) * D + (long)g * Dg;
+    K = (d.G / KX) * Dg;
+    k0 = sl * K;
+    wrow = d.WshT + (long)(n0 + l16) * D + k0;
   } else {
     n0 = (blk - NX) * 16;
-    g = n0 / Dg;
+    const int g = n0 / Dg;
+    K = Dg;
+    k0 = g * Dg;
     wrow = d.WbdT + ((long)g * Dg + n0 % Dg + l16) * Dg;
   }
+  const int ldp = K + 4;
   Core<1, CPW> core;
   const float* wt[1] = {wrow};
-  core.load_b(wt, Dg / 16, wave, q);
+  core.load_b(wt, K / 16, wave, q);
   const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
   const bool rv = row < nr;
   f32x4 pv[2];
   ld_parts(pv, w.dotp + ((long)blockIdx.z * MR + row) * (D / 16), D / 16, t32);
-  const long ob = (long)gr * D + (long)g * Dg;
-  f32x4 gq[NG], xv[NG];
-  ld_row(gq, w.gq + ob, Dg, rv, t32);
-  ld_row(xv, d.hp + (long)t * B * D + ob, Dg, rv, t32);
+  const long ob = (long)gr * D + k0;
+  f32x4 gq[NGX], xv[NGX];
+  ld_row(gq, w.gq + ob, K, rv, t32);
+  ld_row(xv, d.hp + (long)t * B * D + ob, K, rv, t32);
   const float r = rv ? d.rh[(long)t * B + gr] : 0.f;
   const int er = (tid >> 4) & 15, c = tid & 15, ger = rb + er;
   const bool ev = tid < 256 && er < nr;
   const float dh_old = (!p0 && ev) ? w.dhin[(long)ger * D + n0 + c] : 0.f;
   const float dot = sum_parts(pv) / (float)D;
-  f32x4 o[NG];
+  f32x4 o[NGX];
 #pragma unroll
-  for (int i = 0; i < NG; ++i)
+  for (int i = 0; i < NGX; ++i)
 #pragma unroll
     for (int k = 0; k < 4; ++k) o[i][k] = rv ? r * (gq[i][k] - xv[i][k] * r * dot) : 0.f;
-  st_row(smem + core_lds_floats<1>() + row * ldp, o, Dg, t32);
-  if (rv && !p0 && (n0 % Dg) == 0) st_row(d.d_hp + (long)t * B * D + ob, o, Dg, t32);
+  st_row(smem + core_lds_floats<1>() + row * ldp, o, K, t32);
+  if (rv && !p0 && (n0 % Dg) == 0) st_row(d.d_hp + (long)t * B * D + ob, o, K, t32);
   __syncthreads();
   SD_TR(1)
-  core.run_lds(smem + core_lds_floats<1>(), ldp, Dg / 16, wave, l16, q);
+  core.run_lds(smem + core_lds_floats<1>(), ldp, K / 16, wave, l16, q);
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
   SD_TR(2)
   if (ev) {
-    if (p0) w.dxs[(long)g * B * X + (long)ger * X + n0 + c] = C[er * 16 + c];
+    if (p0) w.dxs[(long)sl * B * X + (long)ger * X + n0 + c] = C[er * 16 + c];
     else w.dhin[(long)ger * D + n0 + c] = dh_old + C[er * 16 + c];
   }
   SD_TR_END(d.trace, d.trace_slot)
@@ -956,7 +970,7 @@ __global__ __launch_bounds__(NTHR) void k_dx01(sd_rssm_scan d, Work w, int t) {
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
       const int c = tid + NTHR * k;
-      part[g][k] = (g < d.G && c < X) ? w.dxs[(long)g * B * X + (long)b * X + c] : 0.f;
+      part[g][k] = (g < kx_of(d.G) && c < X) ? w.dxs[(long)g * B * X + (long)b * X + c] : 0.f;
     }
   const int half = wave >> 2, ht = tid & 255;
   const float* x = (half ? d.x1p : d.x0p) + (tB + b) * UH;
@@ -1014,7 +1028,7 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   f32x4 part[GM][NU], xv[NU], nv[NU];
 #pragma unroll
   for (int g = 0; g < GM; ++g)
-    ld_row(part[g], w.dxs + (long)g * B * X + (long)gr * X + (wx2 ? 2 * UH : hoff), UH, rv && g < d.G, t32);
+    ld_row(part[g], w.dxs + (long)g * B * X + (long)gr * X + (wx2 ? 2 * UH : hoff), UH, rv && g < kx_of(d.G), t32);
   const float rr = rv ? (p0 ? d.r0 : d.r1)[tB + gr] : 0.f;
   ld_row(xv, (p0 ? d.x0p : d.x1p) + (tB + gr) * UH, UH, rv, t32);
   ld_row(nv, p0 ? d.n0 : d.n1, UH, true, t32);
@@ -1053,7 +1067,8 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   if (wx2) {
     if (rv) st_row(d.d_xcat + (tB + gr) * X + 2 * UH, dx, UH, t32);
 #pragma unroll
-    for (int g = 0; g < GM; ++g) ld_row(part[g], w.dxs + (long)g * B * X + (long)gr * X, UH, rv && g < d.G, t32);
+    for (int g = 0; g < GM; ++g)
+      ld_row(part[g], w.dxs + (long)g * B * X + (long)gr * X, UH, rv && g < kx_of(d.G), t32);
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
       dx[i] = part[0][i];
@@ -1298,12 +1313,13 @@ extern "C" int sd_rssm_scan_bwd(const sd_rssm_scan* dp, sd_stream stream_) {
   const size_t core1 = core_lds_floats<1>() * 4;
   const size_t lds_dl = core1 + (size_t)MR * (SK + 4) * 4;
   const size_t lds_dgru = core1 + (size_t)MR * (UH + 4) * 4;
-  const size_t lds_dhp = core1 + (size_t)MR * (Dg + 4) * 4;
+  const int kspan = (d.G / kx_of(d.G)) * Dg;  // k_dhp's longest K span (P0)
+  const size_t lds_dhp = core1 + (size_t)MR * (kspan + 4) * 4;
   // carry of the step after T-1 is zero. A kernel, not hipMemsetAsync: in a captured HIP graph the memset node was
   // observed not to be ordered before the first k_dgru (garbage carry in replays)
   k_zero<<<sd_cdiv(B * D, 256), 256, 0, st>>>(w.ch, (long)B * D);
   SD_LAUNCH_CHECK();
-  const int NX = (3 * UH / 16) * d.G;
+  const int NX = (3 * UH / 16) * kx_of(d.G);
   SD_KD_SWITCH(d.Kd, k_sbwd_last<KD><<<(int)(((long)B * SK + 255) / 256), 256, 0, st>>>(d));
   SD_LAUNCH_CHECK();
   for (int t = d.T - 1; t >= 0; --t) {
@@ -1323,8 +1339,8 @@ extern "C" int sd_rssm_scan_bwd(const sd_rssm_scan* dp, sd_stream stream_) {
     SD_CPW_SWITCH(cp_g3, k_dhh<CP><<<dim3(D / 16, 1, nt), NTHR, core1, st>>>(d, w, t));
     SD_LAUNCH_CHECK();
     d.trace_slot = (d.T + t) * 8 + 3;
-    SD_NG_SWITCH(Dg, if (!(raise_lds<k_dhp<NG, NG>>(lds_dhp))) return SD_EARG;
-                 k_dhp<NG, NG><<<dim3(NX + D / 16, 1, nt), NTHR, lds_dhp, st>>>(d, w, t));
+    SD_CPW_SWITCH(kspan / 128, if (!(raise_lds<k_dhp<CP, CP>>(lds_dhp))) return SD_EARG;
+                  k_dhp<CP, CP><<<dim3(NX + D / 16, 1, nt), NTHR, lds_dhp, st>>>(d, w, t));
     SD_LAUNCH_CHECK();
     d.trace_slot = (d.T + t) * 8 + 4;
     if (t > 0) {  // k_carry builds d_x0p / d_x1p itself (the k_dx01 work in its prologue)
