@@ -465,6 +465,8 @@ typedef struct sd_imagine {
                          fp32 (null: kept in `work` only); the policy loss's actor forward starts from it */
   const float* noise_img; /* optional (H1 - 1, N, SK): the prior samples' Gumbel noise, drawn ahead by
                              sd_imagine_noise (null: drawn inside the sampler); the same values either way */
+  uint64_t* trace;        /* measurement aid, -DSD_SCAN_TRACE builds only (NULL otherwise): per launch slot
+                             (t * 16 + launch of the step) and workgroup, entry / staged / contracted / exit timestamps */
 } sd_imagine;
 int sd_imagine_work_floats(const sd_imagine* d);
 int sd_imagine_run(const sd_imagine* d, sd_stream stream);

@@ -95,3 +95,29 @@ SD_DEV float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x))
 SD_DEV float siluf_(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 static inline int sd_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// Phase timestamps (measurement build, -DSD_SCAN_TRACE; scan.hip and img.hip kernels): thread 0 of every workgroup keeps entry / operands staged /
+// contraction reduced / exit (s_memrealtime, 100 MHz) and stores them at exit into trace[slot][workgroup][4].
+#ifdef SD_SCAN_TRACE
+constexpr int TR_WG = 2048;  // workgroup slots per launch
+#define SD_TR_BEGIN uint64_t tr_[4] = {__builtin_amdgcn_s_memrealtime(), 0ull, 0ull, 0ull};
+#define SD_TR(k) tr_[k] = __builtin_amdgcn_s_memrealtime();
+#define SD_TR_END(buf, slot)                                                                               \
+  if (threadIdx.x == 0 && (buf)) {                                                                         \
+    tr_[3] = __builtin_amdgcn_s_memrealtime();                                                             \
+    const long wg_ = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);           \
+    if (wg_ < TR_WG) {                                                                                     \
+      uint64_t* o_ = (buf) + ((long)(slot) * TR_WG + wg_) * 4;                                             \
+      for (int i_ = 0; i_ < 4; ++i_) o_[i_] = tr_[i_];                                                      \
+    }                                                                                                      \
+  }
+#else
+#define SD_TR_BEGIN
+#define SD_TR(k)
+#define SD_TR_END(buf, slot)
+#endif
+// a launch's trace destination (img.hip kernels: the buffer of sd_imagine.trace, slot t * 16 + launch of the step)
+struct Tr {
+  uint64_t* p;
+  int slot;
+};

@@ -390,7 +390,8 @@ constexpr int KL2_WN = KL2_BN / 2, KL2_PW = KL2_WN < 32 ? KL2_WN : 32;
 constexpr int KL3_WN = KL3_BN / (4 / (KL3_BM / 16)), KL3_PW = KL3_WN < 32 ? KL3_WN : 32;  // its row-partial width
 // grouped plain-A linear layers (N = 256 each): out = A . W^T + b (+ add), with row partials. grid (N/BN, M/BM, nprob)
 template <int BM, int BN>
-__global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2, int M) {
+__global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2, int M, Tr tr) {
+  SD_TR_BEGIN
   constexpr int WN = BN / (4 / (BM / 16));
   int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
   if (KL_XCD) xcd_tile(tx, ty, tz);
@@ -399,8 +400,11 @@ __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2,
   const APlain<BM> a0(p.A, p.lda, m0, M, p.K);
   const BRows<BN> b0(p.W, p.ldw, n0, BN, 0);
   f32x4 acc[1][WN / 16];
+  SD_TR(1)
   mainloop<F6_LIN, FP_LIN, BM, BN, 16, WN, pf_of(KL_PF)>(a0, b0, 0, p.K, acc);
+  SD_TR(2)
   ep_bias_part<BM, BN, WN, (WN < 32 ? WN : 32)>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
+  SD_TR_END(tr.p, tr.slot)
 }
 
 // The step's K = S*Kd contractions (actor layer 0's stoch part + _dyn_in1) read a straight-through one-hot sample:
@@ -425,7 +429,8 @@ struct OneHotProb {
   float* part;       // (U / 16, M)
 };
 __global__ __launch_bounds__(256) void k_onehot_lin(const float* X, long ldx, int SK, int Kd, OneHotProb p0,
-                                                    OneHotProb p1, int nprob, int M) {
+                                                    OneHotProb p1, int nprob, int M, Tr tr) {
+  SD_TR_BEGIN
   constexpr int U = 256;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long m = (long)blockIdx.x * 4 + wave;
@@ -449,6 +454,7 @@ __global__ __launch_bounds__(256) void k_onehot_lin(const float* X, long ldx, in
     many = cnt > 1;
   }
   const bool dense = __any(many);
+  SD_TR(1)
   const int c = 4 * lane;
 #pragma unroll 1
   for (int pr = 0; pr < nprob; ++pr) {
@@ -491,6 +497,8 @@ __global__ __launch_bounds__(256) void k_onehot_lin(const float* X, long ldx, in
     ss += __shfl_xor(ss, 2, 64);
     if ((lane & 3) == 0 && p.part) p.part[(long)(lane >> 2) * M + m] = ss;
   }
+  SD_TR(2)
+  SD_TR_END(tr.p, tr.slot)
 }
 // WT (K, U) = W[:, 0:K]^T for a (U, ldw) weight
 __global__ __launch_bounds__(256) void k_transpose_w(const float* W, long ldw, int U, int K, float* WT) {
@@ -510,16 +518,20 @@ constexpr int KR_WN = 64 / (4 / (KR_BM / 16)), KR_PW = KR_WN < 32 ? KR_WN : 32;
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw, const float* part_in, int np, int K,
                                                 const float* W, const float* bias, float* out, float* part, int M,
-                                                float eps) {
+                                                float eps, Tr tr) {
+  SD_TR_BEGIN
   constexpr int WN = BN / (4 / (BM / 16));
   __shared__ float rs[BM], red[256];
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   wg_rstd<BM, 8>(part_in, np, M, m0, K, eps, rs, red);
+  SD_TR(1)
   const ARms<BM> a0(X, K, nw, rs, m0, M, K);
   const BRows<BN> b0(W, K, n0, BN, 0);
   f32x4 acc[1][WN / 16];
   mainloop<F6_RMSLIN, FP_RMSLIN, BM, BN, 16, WN, pf_of(FP_RMSLIN ? 2 : 3), true>(a0, b0, 0, K, acc);
+  SD_TR(2)
   ep_bias_part<BM, BN, WN, (WN < 32 ? WN : 32)>(acc, bias, out, gridDim.x * BN, part, M, m0, n0);
+  SD_TR_END(tr.p, tr.slot)
 }
 
 // k_hid tiling knobs: 64 or 32 rows per workgroup, single-stage LDS loop, register budget (waves per SIMD)
@@ -557,13 +569,15 @@ SD_DEV void hid_seg(const OpA& a0, const OpB& b0, int K, f32x4 (&acc)[1][WN / 16
 // grid (D/64, M/64); row partials per 64 columns (D/64 of them) for the gate norm.
 __global__ __launch_bounds__(256, KH_WAVES) void k_hid(sd_imagine d, const float* h, long ldh, const float* x0p, const float* x1p,
                                              const float* px0, const float* px1, int npx0, int npx1, const float* x2, float* hp,
-                                             float* ph, const __bf16* wh6) {
+                                             float* ph, const __bf16* wh6, Tr tr) {
+  SD_TR_BEGIN
   constexpr int BM = KH_BM, BN = 64, WN = BN / (4 / (BM / 16));
   __shared__ float rs0[BM], rs1[BM], red[256];
   const int Dg = d.D / d.G, U = d.U, Ig = Dg + 3 * U, M = d.N;
   const int n0 = xcd_col(blockIdx.x, gridDim.x, Dg / BN) * BN, m0 = blockIdx.y * BM, g = n0 / Dg;
   wg_rstd<BM, 8>(px0, npx0, M, m0, U, d.eps, rs0, red);
   wg_rstd<BM, 8>(px1, npx1, M, m0, U, d.eps, rs1, red);
+  SD_TR(1)
   const float* Wseg = d.Wh + (long)n0 * Ig;  // rows n0.. of Wh viewed as (D, Ig)
   const int ct = n0 / BN, nkt = Ig / BK6;
   // the four K segments of [h_g | x0 | x1 | x2]: B from the pre-split image (KH_PRE) or split while staged
@@ -590,7 +604,9 @@ __global__ __launch_bounds__(256, KH_WAVES) void k_hid(sd_imagine d, const float
     const APlain<BM> a0(x2, U, m0, M, U);
     hid_seg<BM, BN, WN>(a0, bseg(Dg + 2 * U), U, acc, true);
   }
+  SD_TR(2)
   ep_bias_part<BM, BN, WN, KH_PW>(acc, d.bh, hp, d.D, ph, M, m0, n0);
+  SD_TR_END(tr.p, tr.slot)
 }
 
 // gates = BlockLinear(dyn_gru)(silu(rms(hp))) + bg; deter' = GRU (rssm.py:65-75) -> feats[t+1][:, SK:].
@@ -610,12 +626,14 @@ SD_DEV auto gate_b(const __bf16* wg6, int ct, int nkt, const float* Wblk, int Dg
 #define KG_WAVES 4
 #endif
 __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const float* hp, const float* ph, int nph,
-                                              const float* hold, float* hnew, long ldf, const __bf16* wg6) {
+                                              const float* hold, float* hnew, long ldf, const __bf16* wg6, Tr tr) {
+  SD_TR_BEGIN
   constexpr int BM = 64, BN = 96;
   const int Dg = d.D / d.G;
   const int c0 = xcd_col(blockIdx.x, gridDim.x, Dg / 32) * 32, m0 = blockIdx.y * BM, g = c0 / Dg, j0 = c0 % Dg;
   __shared__ float rs[BM], red[256];
   wg_rstd<BM, 16>(ph, nph, d.N, m0, d.D, d.eps, rs, red);
+  SD_TR(1)
   const ARms<BM> a0(hp + (long)g * Dg, d.D, d.nh + (long)g * Dg, rs, m0, d.N, Dg);
   constexpr bool PRE = KG_PRE && KG_1S && F6_GATE;
   using OpB = std::conditional_t<PRE, BPre6<BN>, BRows<BN>>;
@@ -633,6 +651,7 @@ __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const floa
   } else {
     mainloop<F6_GATE, FP_GATE, BM, BN, 16, BN, pf_of(KG_PF)>(a0, b0, 0, Dg, acc);
   }
+  SD_TR(2)
   const Lane L = lane_ids<BN, BN>();
   const float* bg = d.bg + (long)g * 3 * Dg;
 #pragma unroll
@@ -650,6 +669,7 @@ __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const floa
       hnew[m * ldf + col] = u * cc + (1.f - u) * hold[m * ldf + col];
     }
   }
+  SD_TR_END(tr.p, tr.slot)
 }
 
 // prior logits = img_net_logit(silu(rms(x))) and the unimix one-hot ST sample -> feats[t+1][:, :SK].
@@ -658,7 +678,8 @@ __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const floa
 // by teams of KD threads.
 template <int KD>
 __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, const float* nw, const float* part_in,
-                                               int np, float* snew, long ldf, int t) {
+                                               int np, float* snew, long ldf, int t, Tr tr) {
+  SD_TR_BEGIN
   constexpr int BM = 16, BN = 64, WN = 16;
   __shared__ float tile[BM][BN + 1];
   __shared__ float rs[BM], red[256];
@@ -678,10 +699,12 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
                          (uint64_t)((m0 + rl + d.row_offset) * S + (n0 + c) / KD) * KD + c % KD);
   }
   wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
+  SD_TR(1)
   const ARms<BM> a0(X, U, nw, rs, m0, d.N, U);
   const BRows<BN> b0(d.Wl, U, n0, BN, 0);
   f32x4 acc[1][1];
   mainloop<F6_PRIOR, FP_PRIOR, BM, BN, 16, WN, pf_of(FP_PRIOR ? 2 : 3)>(a0, b0, 0, U, acc);
+  SD_TR(2)
   const Lane L = lane_ids<BN, WN>();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -702,6 +725,7 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
     st_soft<KD>(nl, gns[k], true, ys, idx, lt);
     if (m < d.N) snew[m * ldf + n0 + c] = ((lt == idx ? 1.f : 0.f) - ys) + ys;
   }
+  SD_TR_END(tr.p, tr.slot)
 }
 
 // actor output layer + action sample (bounded normal: loc = tanh, scale in [min_std, max_std]; or unimix one-hot),
@@ -713,7 +737,8 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
 #endif
 constexpr int KA_BN = KA_BM == 16 ? 64 : 32;  // 4 waves of 16 columns x 16 rows or 2 x 2 waves
 __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, const float* nw, const float* part_in,
-                                                int np, float* act, float* x2, int t, int want_x2) {
+                                                int np, float* act, float* x2, int t, int want_x2, Tr tr) {
+  SD_TR_BEGIN
   constexpr int BM = KA_BM, BN = KA_BN, WN = 16, RT = 256 / BM;  // RT threads per row in the row-sum pass
   __shared__ float tile[BM][BN + 1];
   __shared__ float an[BM][17];
@@ -734,10 +759,12 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
     nz = sd_normal(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m0 + tid / A + d.row_offset) * A + tid % A);
   }
   wg_rstd<BM, 8>(part_in, np, d.N, m0, U, d.eps, rs, red);
+  SD_TR(1)
   const ARms<BM> a0(X, U, nw, rs, m0, d.N, U);
   const BRows<BN> b0(d.Wao, U, 0, BN, 0, NO);  // the output weight's NO rows, zeros past them
   f32x4 acc[1][1];
   mainloop<F6_ACTION, FP_ACTION, BM, BN, 16, WN, pf_of(FP_ACTION ? 2 : 3)>(a0, b0, 0, U, acc);
+  SD_TR(2)
   const Lane L = lane_ids<BN, WN>();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -771,7 +798,10 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
     if (m < d.N) act[m * A + j] = a;
     an[rl][j] = a / fmaxf(fabsf(a), 1.f);
   }
-  if (!want_x2) return;
+  if (!want_x2) {
+    SD_TR_END(tr.p, tr.slot)
+    return;
+  }
   __syncthreads();
   // x2p[row][c] = a_n[row] . W2[c] + b2[c]; thread c = tid (U == 256 columns), all 32 rows
   {
@@ -807,6 +837,7 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
       if (m0 + rl < d.N) x2[(long)(m0 + rl) * U + c] = siluf_(xs[rl][c] * rs * wn);
     }
   }
+  SD_TR_END(tr.p, tr.slot)
 }
 
 // The actor MLP after layer 0 in ONE launch per 16-row tile (networks.py:313-377): hidden layers 1..L-1
@@ -1178,13 +1209,14 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
     LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};
     LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
     LinProb pd{feats(t + 1) + SK, F, D, d.Wa[0] + SK, F, nullptr, w.ad, U, nullptr, nullptr};
-    k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N);
+    k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, Tr{});
   } else if (which == 1) {
     k_hid<<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU, w.x2, w.hp,
-                                                       w.ph, w.wh6);
+                                                       w.ph, w.wh6, Tr{});
   } else {
     // k_gate reads hold = feats(t) deter and writes feats(t + 1) deter: the same values again
-    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F, w.wg6);
+    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F, w.wg6,
+                                                         Tr{});
   }
   SD_LAUNCH_CHECK();
   return SD_OK;
@@ -1224,11 +1256,12 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     LinProb p{feats(0) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
     LinProb pd{feats(0) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
     // the 3-problem launch's tile, so x0p's row partials have one width for every step
-    k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 2), 256, 0, st>>>(p, pd, pd, N);
+    k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 2), 256, 0, st>>>(p, pd, pd, N, Tr{});
     SD_LAUNCH_CHECK();
   }
   for (int t = d.t_begin; t < t_end; ++t) {
     const bool last = t == d.H1 - 1;
+    auto tr = [&](int k) { return Tr{d.trace, t * 16 + k}; };  // launch k of step t (measurement builds)
     // actor layer 0's output: the caller's per-step buffer when given (read again by the policy loss), else scratch
     float* a0 = d.actor_h0 ? d.actor_h0 + (long)t * N * U : w.a[0];
     {  // actor layer 0, stoch part (+ deter part); _dyn_in1 on stoch
@@ -1236,9 +1269,9 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       LinProb px{feats(t), F, SK, d.W1, SK, d.b1, w.x1p, U, w.px1, nullptr};
       if (KL_ONEHOT && d.SK / d.Kd <= 64) {
         const OneHotProb oa{w.waT, d.ba[0], w.ad, a0, w.pa[0]}, ox{w.w1T, d.b1, nullptr, w.x1p, w.px1};
-        k_onehot_lin<<<sd_cdiv(N, 4), 256, 0, st>>>(feats(t), F, SK, d.Kd, oa, ox, last ? 1 : 2, N);
+        k_onehot_lin<<<sd_cdiv(N, 4), 256, 0, st>>>(feats(t), F, SK, d.Kd, oa, ox, last ? 1 : 2, N, tr(0));
       } else {
-        k_lin<32, KL2_BN><<<dim3(U / KL2_BN, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, px, N);
+        k_lin<32, KL2_BN><<<dim3(U / KL2_BN, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, px, N, tr(0));
       }
       SD_LAUNCH_CHECK();
     }
@@ -1249,27 +1282,28 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       int cur = 0, npa = npU;
       for (int l = 1; l < d.actor_layers; ++l) {
         k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(l == 1 ? a0 : w.a[cur], d.na[l - 1], w.pa[cur], npa, U, d.Wa[l],
-                                                d.ba[l], w.a[cur ^ 1], w.pa[cur ^ 1], N, d.eps);
+                                                d.ba[l], w.a[cur ^ 1], w.pa[cur ^ 1], N, d.eps, tr(l));
         SD_LAUNCH_CHECK();
         cur ^= 1;
         npa = npR;
       }
       k_action<<<dim3(1, sd_cdiv(N, KA_BM)), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur],
                                                 d.na[d.actor_layers - 1], w.pa[cur], npa,
-                                                d.actions + (long)t * N * d.A, w.x2, t, last ? 0 : 1);
+                                                d.actions + (long)t * N * d.A, w.x2, t, last ? 0 : 1, tr(4));
     }
     SD_LAUNCH_CHECK();
     if (last) break;
     k_hid<<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU,
-                                                         w.x2, w.hp, w.ph, w.wh6);
+                                                         w.x2, w.hp, w.ph, w.wh6, tr(5));
     SD_LAUNCH_CHECK();
-    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F, w.wg6);
+    k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F, w.wg6,
+                                                         tr(6));
     SD_LAUNCH_CHECK();
     {  // img_net_0, the next step's _dyn_in0 and the deter part of its actor layer 0 share A = deter'
       LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};
       LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
       LinProb pd{feats(t + 1) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
-      k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N);
+      k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, tr(7));
       SD_LAUNCH_CHECK();
     }
     const int pj = SD_PRIOR_NCT > 0 && SK % (64 * SD_PRIOR_NCT) == 0 ? SK / (64 * SD_PRIOR_NCT) : 0;
@@ -1288,17 +1322,17 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       int ci = 0, npi = U / KL3_PW;
       for (int l = 1; l < d.img_layers; ++l) {
         k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(w.i[ci], d.ni[l - 1], w.pi[ci], npi, U, d.Wi[l], d.bi[l],
-                                                w.i[ci ^ 1], w.pi[ci ^ 1], N, d.eps);
+                                                w.i[ci ^ 1], w.pi[ci ^ 1], N, d.eps, tr(7 + l));
         SD_LAUNCH_CHECK();
         ci ^= 1;
         npi = npR;
       }
       if (d.Kd == 16)
         k_prior<16><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi,
-                                                                    feats(t + 1), F, t);
+                                                                    feats(t + 1), F, t, tr(12));
       else
         k_prior<32><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi,
-                                                                    feats(t + 1), F, t);
+                                                                    feats(t + 1), F, t, tr(12));
     }
     SD_LAUNCH_CHECK();
   }

@@ -101,25 +101,6 @@ struct Core {
 template <int NT>
 constexpr int core_lds_floats() { return NW * NT * 256 + MR * 16 * NT; }
 
-// Phase timestamps (measurement build, -DSD_SCAN_TRACE): thread 0 of every workgroup keeps entry / operands staged /
-// contraction reduced / exit (s_memrealtime, 100 MHz) and stores them at exit into trace[slot][workgroup][4].
-#ifdef SD_SCAN_TRACE
-constexpr int TR_WG = 2048;  // workgroup slots per launch
-#define SD_TR_BEGIN uint64_t tr_[4] = {__builtin_amdgcn_s_memrealtime(), 0ull, 0ull, 0ull};
-#define SD_TR(k) tr_[k] = __builtin_amdgcn_s_memrealtime();
-#define SD_TR_END(buf, slot)                                                                               \
-  if (threadIdx.x == 0 && (buf)) {                                                                         \
-    tr_[3] = __builtin_amdgcn_s_memrealtime();                                                             \
-    const long wg_ = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);           \
-    uint64_t* o_ = (buf) + ((long)(slot) * TR_WG + wg_) * 4;                                     \
-    for (int i_ = 0; i_ < 4; ++i_) o_[i_] = tr_[i_];                                                        \
-  }
-#else
-#define SD_TR_BEGIN
-#define SD_TR(k)
-#define SD_TR_END(buf, slot)
-#endif
-
 // row tile of a workgroup (grid z): batch rows rb .. rb + nr (d.row_tile rows, normalised on the host)
 #define SD_ROW_TILE                                               \
   const int rb = (int)blockIdx.z * d.row_tile, nr = min(d.row_tile, d.B - rb); \

@@ -88,6 +88,7 @@ def _tstats(t, prefix):  # tools.tensorstats (tools.py:275-281), resolved with t
 
 
 
+IMAG_TRACE = None  # uint64 device tensor: per-launch / per-workgroup phase timestamps of the fused imagination
 _CUMASK = {}  # device -> the two CU-masked filler streams of SDREAMER_FILL_CUS (created once per process, never leaked
 # per agent: tests and benches build several agents)
 
@@ -1197,6 +1198,8 @@ class Dreamer(nn.Module):
             d.Wi[i], d.bi[i], d.ni[i] = lin.weight.data_ptr(), lin.bias.data_ptr(), norm.weight.data_ptr()
         d.Wl, d.bl = last.weight.data_ptr(), last.bias.data_ptr()
         d.feats, d.actions = feats.data_ptr(), actions.data_ptr()
+        if IMAG_TRACE is not None:  # measurement aid (tools/imag_trace.py, a -DSD_SCAN_TRACE build of the library)
+            d.trace = IMAG_TRACE.data_ptr()
         if actor_h0 is not None:
             assert actor_h0.is_contiguous() and tuple(actor_h0.shape) == (H1, N, r._hidden), actor_h0.shape
             d.actor_h0 = actor_h0.data_ptr()

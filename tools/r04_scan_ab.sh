@@ -17,3 +17,4 @@ for kx in 4 2; do
 done
 bash tools/ab_env.sh 2 "" "SDREAMER_SCAN_ROWTILE_FWD=8" "SDHIP_LIB=$L/_lib_kx4/libsdhip.so" \
   "SDHIP_LIB=$L/_lib_kx2/libsdhip.so" > $O/ab.txt 2>&1 || exit 1
+timeout -k 10 200 python tools/imag_trace.py > $O/imag_trace.txt 2>&1 || exit 1
