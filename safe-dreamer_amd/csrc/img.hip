@@ -840,6 +840,94 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
   SD_TR_END(tr.p, tr.slot)
 }
 
+// k_action by rows (KA_ROWS): one wave per row, 4 rows per workgroup (N / 4 workgroups: 256 at the bench shape instead
+// of 64 16-row tiles). The chain has no workgroup barrier: the row's RMSNorm from the producer's partials, the actor
+// output layer as fp32 dot products (4 columns per lane, one wave reduction per output), the action sample (bounded
+// normal / unimix one-hot on lanes 0..15), action_norm, and the next Deter step's action branch x2 = silu(rms(a_n .
+// W2^T + b2)) for the lane's 4 columns. Same noise indices as k_action; fp32 dot products in a different summation
+// order than the MFMA tile (parity: continuous actions to tolerance, one-hot samples exact off near-ties).
+#ifndef KA_ROWS
+#define KA_ROWS 1
+#endif
+__global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* X, const float* nw,
+                                                     const float* part_in, int np, float* act, float* x2, int t,
+                                                     int want_x2, Tr tr) {
+  SD_TR_BEGIN
+  constexpr int U = 256;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long m = (long)blockIdx.x * 4 + wave;
+  const int A = d.A, NO = d.act_discrete ? A : 2 * A, M = d.N;
+  const bool live = m < M;
+  const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+  // operand loads first: the row's partials, its 4 columns, the norm weight, the output layer's rows
+  const float pv = (live && lane < np) ? part_in[(long)lane * M + m] : 0.f;
+  const f32x4 xv = live ? ld4(X + m * U + 4 * lane) : zero4();
+  const f32x4 wn = ld4(nw + 4 * lane);
+  f32x4 wo[32];
+#pragma unroll
+  for (int o = 0; o < 32; ++o) wo[o] = o < NO ? ld4(d.Wao + (long)o * U + 4 * lane) : zero4();
+  float nz = 0.f;  // the action noise of element (m, lane)
+  if (d.act_discrete) {
+    if (lane < A) nz = sd_gumbel(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lane);
+  } else if (lane < A) {
+    nz = sd_normal(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lane);
+  }
+  const float rs = rsqrtf(wave_sum(pv) / (float)U + d.eps);
+  SD_TR(1)
+  f32x4 y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) y[j] = siluf_(xv[j] * rs * wn[j]);
+  float lo = 0.f;  // lane o < NO ends with logit o
+#pragma unroll
+  for (int o = 0; o < 32; ++o) {
+    if (o < NO) {  // uniform
+      float pdot = y[0] * wo[o][0];
+      pdot = fmaf(y[1], wo[o][1], pdot);
+      pdot = fmaf(y[2], wo[o][2], pdot);
+      pdot = fmaf(y[3], wo[o][3], pdot);
+      const float v = wave_sum(pdot) + d.bao[o];
+      if (lane == o) lo = v;
+    }
+  }
+  SD_TR(2)
+  float a = 0.f;  // lane j < A: action element j
+  if (d.act_discrete) {
+    const bool on = lane < A;
+    float p, pp, nl;
+    unimix_forward<16>(lo, on, A, d.act_unimix, p, pp, nl);  // lanes 0..15 form the team
+    float ys;
+    int idx;
+    st_soft<16>(nl, nz, on, ys, idx, lane & 15);
+    if (on) a = ((lane == idx ? 1.f : 0.f) - ys) + ys;
+  } else {
+    const float ls = __shfl(lo, lane + A, 64);  // the scale logit of element lane
+    if (lane < A) {
+      const float loc = tanhf(lo);
+      const float sc = (d.max_std - d.min_std) * sigmoidf_(ls + 2.f) + d.min_std;
+      a = loc + nz * sc;
+    }
+  }
+  if (live && lane < A) act[m * A + lane] = a;
+  if (!want_x2) {
+    SD_TR_END(tr.p, tr.slot)
+    return;
+  }
+  const float an = a / fmaxf(fabsf(a), 1.f);
+  f32x4 xp = ld4(d.b2 + 4 * lane);
+  for (int j = 0; j < A; ++j) {
+    const float aj = __shfl(an, j, 64);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) xp[e] += aj * d.W2[(long)(4 * lane + e) * A + j];
+  }
+  const float r2 = rsqrtf(wave_sum(xp[0] * xp[0] + xp[1] * xp[1] + xp[2] * xp[2] + xp[3] * xp[3]) / (float)U + d.eps);
+  const f32x4 n2 = ld4(d.n2 + 4 * lane);
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = siluf_(xp[e] * r2 * n2[e]);
+  if (live) *reinterpret_cast<f32x4*>(x2 + m * U + 4 * lane) = o;
+  SD_TR_END(tr.p, tr.slot)
+}
+
 // The actor MLP after layer 0 in ONE launch per 16-row tile (networks.py:313-377): hidden layers 1..L-1
 // (RMSNorm + SiLU of the previous layer, Linear), the output layer, the action sample and the x2 branch — what
 // k_rmslin x (L-1) + k_action do in L launches. An MLP row needs only its own previous-layer row, so a workgroup that
@@ -1287,9 +1375,14 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
         cur ^= 1;
         npa = npR;
       }
-      k_action<<<dim3(1, sd_cdiv(N, KA_BM)), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur],
-                                                d.na[d.actor_layers - 1], w.pa[cur], npa,
-                                                d.actions + (long)t * N * d.A, w.x2, t, last ? 0 : 1, tr(4));
+      if (KA_ROWS)
+        k_action_rows<<<sd_cdiv(N, 4), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur], d.na[d.actor_layers - 1],
+                                                     w.pa[cur], npa, d.actions + (long)t * N * d.A, w.x2, t,
+                                                     last ? 0 : 1, tr(4));
+      else
+        k_action<<<dim3(1, sd_cdiv(N, KA_BM)), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur],
+                                                  d.na[d.actor_layers - 1], w.pa[cur], npa,
+                                                  d.actions + (long)t * N * d.A, w.x2, t, last ? 0 : 1, tr(4));
     }
     SD_LAUNCH_CHECK();
     if (last) break;
