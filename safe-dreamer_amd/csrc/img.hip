@@ -534,6 +534,128 @@ __global__ __launch_bounds__(256) void k_rmslin(const float* X, const float* nw,
   SD_TR_END(tr.p, tr.slot)
 }
 
+// ------------------------------------------------------------------------------------------- 16 x 64 register tiles
+// The short-K (K = U = 256) layers on 16-row tiles — the actor / img_net hidden layers (k_rmslin) and the prior logits
+// (k_prior) — measured as latency chains: an LDS-staged k loop of 8 tiles with a barrier each. Here each workgroup
+// stages the RMSNorm + SiLU'd A panel (16 rows x K, from the producer's row partials) into LDS ONCE, every wave loads
+// its weight fragments straight into registers at entry (column tile w % 4, K part w / 4: K / KS per wave), the MFMAs
+// run from registers + LDS with no further barrier, and the KS k-parts are summed in a fixed order through LDS.
+// v_mfma_f32_16x16x4_f32 (exact fp32 products): lane (l16, q) supplies k = 16c + 4q + j at MFMA j of chunk c.
+template <int NWV>
+struct RTile {
+  static constexpr int U = 256, KS = NWV / 4, KP = U / KS, NCH = KP / 16, LDP = U + 4;
+  f32x4 b[NCH];
+  f32x4 acc;
+  // weight rows of this wave's column tile (n0 + 16 (w % 4) + l16), its K part
+  SD_DEV void load_w(const float* W, long ldw, int n0) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    const float* p = W + (long)(n0 + 16 * (w % 4) + l16) * ldw + (w / 4) * KP + 4 * q;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) b[c] = ld4(p + 16 * c);
+  }
+  // panel P[16][LDP] = silu(X[m0 + r] * rstd_r * nw), rstd from np <= 16 partials part[p * M + m]; threads 0..255:
+  // row tid / 16, 16 columns each (the row's 16 threads reduce its partials: no barrier before the norm)
+  SD_DEV static void stage(float* P, const float* X, long ldx, const float* nw, const float* part, int np, int M,
+                           int m0, float eps) {
+    const int tid = threadIdx.x;
+    if (tid < 256) {
+      const int r = tid >> 4, j = tid & 15;
+      const long m = m0 + r;
+      const bool rv = m < M;
+      const float pv = (rv && j < np) ? part[(long)j * M + m] : 0.f;
+      f32x4 x[4], w[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[i] = rv ? ld4(X + m * ldx + 16 * j + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
+        w[i] = ld4(nw + 16 * j + 4 * i);
+      }
+      const float rs = rsqrtf(group_sum<16>(pv) / (float)U + eps);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f32x4 y;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = rv ? siluf_(x[i][e] * rs * w[i][e]) : 0.f;
+        *reinterpret_cast<f32x4*>(P + r * LDP + 16 * j + 4 * i) = y;
+      }
+    }
+  }
+  SD_DEV void mma(const float* P) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* a = P + l16 * LDP + (w / 4) * KP + 4 * q;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const f32x4 av = ld4(a + 16 * c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], b[c][j], acc, 0, 0, 0);
+    }
+  }
+  // sum of the KS k-parts into tile T[16][64 + 1] (row 4q + r, column 16 (w % 4) + l16), in k-part order
+  SD_DEV void reduce(float* red, float* T) const {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+    if (KS > 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(w * 4 + r) * 64 + lane] = acc[r];
+      __syncthreads();
+      if (w < 4) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = red[(w * 4 + r) * 64 + lane];
+#pragma unroll
+          for (int k = 1; k < KS; ++k) v += red[((w + 4 * k) * 4 + r) * 64 + lane];
+          T[(4 * q + r) * 65 + 16 * w + l16] = v;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[(4 * q + r) * 65 + 16 * w + l16] = acc[r];
+    }
+    __syncthreads();
+  }
+};
+
+#ifndef KR_RW  // k_rmslin as register tiles (RTile<8>); 0: the LDS-staged k loop
+#define KR_RW 1
+#endif
+#ifndef KP_RW  // k_prior as register tiles (RTile<16>, one sampler element per thread); 0: the LDS-staged k loop
+#define KP_RW 1
+#endif
+// k_rmslin on RTile<8>: 512 threads, grid (U / 64, M / 16); the same outputs and 16-column row partials (part[p * M +
+// m], p = column / 16) as k_rmslin<16, 64>
+__global__ __launch_bounds__(512) void k_rmslin_rw(const float* X, const float* nw, const float* part_in, int np,
+                                                   const float* W, const float* bias, float* out, float* part, int M,
+                                                   float eps, Tr tr) {
+  SD_TR_BEGIN
+  using RT = RTile<8>;
+  __shared__ __attribute__((aligned(16))) float P[16 * RT::LDP];
+  __shared__ float red[8 * 4 * 64];
+  __shared__ float T[16 * 65];
+  const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 16;
+  RT rt;
+  rt.load_w(W, RT::U, n0);
+  RT::stage(P, X, RT::U, nw, part_in, np, M, m0, eps);
+  __syncthreads();
+  SD_TR(1)
+  rt.mma(P);
+  rt.reduce(red, T);
+  SD_TR(2)
+  const int tid = threadIdx.x;
+  if (tid < 256) {  // row tid / 16, columns 4 (tid % 16) .. +3
+    const int r = tid >> 4, j = tid & 15;
+    const long m = m0 + r;
+    const f32x4 bv = ld4(bias + n0 + 4 * j);
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = T[r * 65 + 4 * j + e] + bv[e];
+    if (m < M) *reinterpret_cast<f32x4*>(out + m * RT::U + n0 + 4 * j) = v;
+    float ss = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    ss += __shfl_xor(ss, 1, 64);
+    ss += __shfl_xor(ss, 2, 64);  // 4 threads = 16 columns
+    if ((j & 3) == 0 && m < M) part[(long)(n0 / 16 + (j >> 2)) * M + m] = ss;
+  }
+  SD_TR_END(tr.p, tr.slot)
+}
+
 // k_hid tiling knobs: 64 or 32 rows per workgroup, single-stage LDS loop, register budget (waves per SIMD)
 #ifndef KH_BM
 #define KH_BM 64
@@ -728,6 +850,45 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
   SD_TR_END(tr.p, tr.slot)
 }
 
+// k_prior on RTile<16>: 1024 threads, grid (SK / 64, M / 16); one sampler element per thread (row tid / 64, column
+// tid % 64: teams of KD lanes), the noise drawn / read before the contraction
+template <int KD>
+__global__ __launch_bounds__(1024) void k_prior_rw(sd_imagine d, const float* X, const float* nw, const float* part_in,
+                                                   int np, float* snew, long ldf, int t, Tr tr) {
+  SD_TR_BEGIN
+  using RT = RTile<16>;
+  __shared__ __attribute__((aligned(16))) float P[16 * RT::LDP];
+  __shared__ float red[16 * 4 * 64];
+  __shared__ float T[16 * 65];
+  const int tid = threadIdx.x, n0 = blockIdx.x * 64, m0 = blockIdx.y * 16, S = d.SK / KD;
+  const int rl = tid >> 6, c = tid & 63, lt = c % KD;
+  const long m = m0 + rl;
+  RT rt;
+  rt.load_w(d.Wl, RT::U, n0);
+  float gn;
+  if (d.noise_img) {  // drawn ahead (sd_imagine_noise): the same values
+    gn = m < d.N ? d.noise_img[((long)t * d.N + m) * d.SK + n0 + c] : 0.f;
+  } else {
+    const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+    gn = sd_gumbel(seed, (uint32_t)d.stream_img, (uint32_t)t, (uint64_t)((m + d.row_offset) * S + (n0 + c) / KD) * KD + lt);
+  }
+  const float blv = d.bl[n0 + c];
+  RT::stage(P, X, RT::U, nw, part_in, np, d.N, m0, d.eps);
+  __syncthreads();
+  SD_TR(1)
+  rt.mma(P);
+  rt.reduce(red, T);
+  SD_TR(2)
+  const float l = T[rl * 65 + c] + blv;
+  float p, pp, nl;
+  unimix_forward<KD>(l, true, KD, d.unimix, p, pp, nl);
+  float ys;
+  int idx;
+  st_soft<KD>(nl, gn, true, ys, idx, lt);
+  if (m < d.N) snew[m * ldf + n0 + c] = ((lt == idx ? 1.f : 0.f) - ys) + ys;
+  SD_TR_END(tr.p, tr.slot)
+}
+
 // actor output layer + action sample (bounded normal: loc = tanh, scale in [min_std, max_std]; or unimix one-hot),
 // action_norm, and the action branch of the next Deter step: x2 = silu(rms(_dyn_in2(a_n))) (rssm.py:40-46).
 // BM = KA_BM rows (16: 64 workgroups at N = 1,024 — the sampler and the x2 epilogue loop over the tile's rows, so
@@ -853,19 +1014,28 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
                                                      const float* part_in, int np, float* act, float* x2, int t,
                                                      int want_x2, Tr tr) {
   SD_TR_BEGIN
-  constexpr int U = 256;
+  constexpr int U = 256, MO = 32, MA = 16;  // <= 32 output logits (2A or A), <= 16 actions
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long m = (long)blockIdx.x * 4 + wave;
   const int A = d.A, NO = d.act_discrete ? A : 2 * A, M = d.N;
   const bool live = m < M;
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
-  // operand loads first: the row's partials, its 4 columns, the norm weight, the output layer's rows
+  // every operand load first: the row's partials, its 4 columns, the norm weight, the output layer's rows, and the
+  // action branch's weights W2[4 lane + e][j]
   const float pv = (live && lane < np) ? part_in[(long)lane * M + m] : 0.f;
   const f32x4 xv = live ? ld4(X + m * U + 4 * lane) : zero4();
   const f32x4 wn = ld4(nw + 4 * lane);
-  f32x4 wo[32];
+  f32x4 wo[MO];
 #pragma unroll
-  for (int o = 0; o < 32; ++o) wo[o] = o < NO ? ld4(d.Wao + (long)o * U + 4 * lane) : zero4();
+  for (int o = 0; o < MO; ++o) wo[o] = o < NO ? ld4(d.Wao + (long)o * U + 4 * lane) : zero4();
+  const float bo = lane < NO ? d.bao[lane] : 0.f;
+  f32x4 w2[MA];  // w2[j][e] = W2[4 lane + e][j]
+  const bool x2w = want_x2 != 0;
+#pragma unroll
+  for (int j = 0; j < MA; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w2[j][e] = (x2w && j < A) ? d.W2[(long)(4 * lane + e) * A + j] : 0.f;
+  const f32x4 b2 = ld4(d.b2 + 4 * lane), n2 = ld4(d.n2 + 4 * lane);
   float nz = 0.f;  // the action noise of element (m, lane)
   if (d.act_discrete) {
     if (lane < A) nz = sd_gumbel(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lane);
@@ -877,18 +1047,25 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
   f32x4 y;
 #pragma unroll
   for (int j = 0; j < 4; ++j) y[j] = siluf_(xv[j] * rs * wn[j]);
-  float lo = 0.f;  // lane o < NO ends with logit o
+  // the NO dot products, reduced over the wave stage by stage (independent shuffles in flight together)
+  float pd[MO];
 #pragma unroll
-  for (int o = 0; o < 32; ++o) {
-    if (o < NO) {  // uniform
-      float pdot = y[0] * wo[o][0];
-      pdot = fmaf(y[1], wo[o][1], pdot);
-      pdot = fmaf(y[2], wo[o][2], pdot);
-      pdot = fmaf(y[3], wo[o][3], pdot);
-      const float v = wave_sum(pdot) + d.bao[o];
-      if (lane == o) lo = v;
-    }
+  for (int o = 0; o < MO; ++o) {
+    float v = y[0] * wo[o][0];
+    v = fmaf(y[1], wo[o][1], v);
+    v = fmaf(y[2], wo[o][2], v);
+    pd[o] = fmaf(y[3], wo[o][3], v);
   }
+#pragma unroll
+  for (int sh = 32; sh > 0; sh >>= 1)
+#pragma unroll
+    for (int o = 0; o < MO; ++o)
+      if (o < NO) pd[o] += __shfl_xor(pd[o], sh, 64);
+  float lo = 0.f;  // lane o < NO: logit o
+#pragma unroll
+  for (int o = 0; o < MO; ++o)
+    if (lane == o) lo = pd[o];
+  lo += bo;
   SD_TR(2)
   float a = 0.f;  // lane j < A: action element j
   if (d.act_discrete) {
@@ -908,19 +1085,23 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
     }
   }
   if (live && lane < A) act[m * A + lane] = a;
-  if (!want_x2) {
+  if (!x2w) {
     SD_TR_END(tr.p, tr.slot)
     return;
   }
   const float an = a / fmaxf(fabsf(a), 1.f);
-  f32x4 xp = ld4(d.b2 + 4 * lane);
-  for (int j = 0; j < A; ++j) {
-    const float aj = __shfl(an, j, 64);
+  float anj[MA];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) xp[e] += aj * d.W2[(long)(4 * lane + e) * A + j];
-  }
+  for (int j = 0; j < MA; ++j) anj[j] = __shfl(an, j, 64);
+  // x2p[4 lane + e] = b2 + sum_j a_n[j] W2[4 lane + e][j] (k_action's order: b2 first, then j = 0, 1, ...)
+  f32x4 xp = b2;
+#pragma unroll
+  for (int j = 0; j < MA; ++j)
+    if (j < A) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xp[e] += anj[j] * w2[j][e];
+    }
   const float r2 = rsqrtf(wave_sum(xp[0] * xp[0] + xp[1] * xp[1] + xp[2] * xp[2] + xp[3] * xp[3]) / (float)U + d.eps);
-  const f32x4 n2 = ld4(d.n2 + 4 * lane);
   f32x4 o;
 #pragma unroll
   for (int e = 0; e < 4; ++e) o[e] = siluf_(xp[e] * r2 * n2[e]);
@@ -1369,8 +1550,13 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     } else {
       int cur = 0, npa = npU;
       for (int l = 1; l < d.actor_layers; ++l) {
-        k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(l == 1 ? a0 : w.a[cur], d.na[l - 1], w.pa[cur], npa, U, d.Wa[l],
-                                                d.ba[l], w.a[cur ^ 1], w.pa[cur ^ 1], N, d.eps, tr(l));
+        if (KR_RW && U == 256 && npa <= 16)
+          k_rmslin_rw<<<dim3(U / 64, sd_cdiv(N, 16)), 512, 0, st>>>(l == 1 ? a0 : w.a[cur], d.na[l - 1], w.pa[cur],
+                                                                     npa, d.Wa[l], d.ba[l], w.a[cur ^ 1],
+                                                                     w.pa[cur ^ 1], N, d.eps, tr(l));
+        else
+          k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(l == 1 ? a0 : w.a[cur], d.na[l - 1], w.pa[cur], npa, U, d.Wa[l],
+                                                  d.ba[l], w.a[cur ^ 1], w.pa[cur ^ 1], N, d.eps, tr(l));
         SD_LAUNCH_CHECK();
         cur ^= 1;
         npa = npR;
@@ -1414,18 +1600,32 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     } else {
       int ci = 0, npi = U / KL3_PW;
       for (int l = 1; l < d.img_layers; ++l) {
-        k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(w.i[ci], d.ni[l - 1], w.pi[ci], npi, U, d.Wi[l], d.bi[l],
-                                                w.i[ci ^ 1], w.pi[ci ^ 1], N, d.eps, tr(7 + l));
+        if (KR_RW && U == 256 && npi <= 16)
+          k_rmslin_rw<<<dim3(U / 64, sd_cdiv(N, 16)), 512, 0, st>>>(w.i[ci], d.ni[l - 1], w.pi[ci], npi, d.Wi[l],
+                                                                     d.bi[l], w.i[ci ^ 1], w.pi[ci ^ 1], N, d.eps,
+                                                                     tr(7 + l));
+        else
+          k_rmslin<KR_BM, 64><<<gr, 256, 0, st>>>(w.i[ci], d.ni[l - 1], w.pi[ci], npi, U, d.Wi[l], d.bi[l],
+                                                  w.i[ci ^ 1], w.pi[ci ^ 1], N, d.eps, tr(7 + l));
         SD_LAUNCH_CHECK();
         ci ^= 1;
         npi = npR;
       }
-      if (d.Kd == 16)
-        k_prior<16><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi,
-                                                                    feats(t + 1), F, t, tr(12));
-      else
-        k_prior<32><<<dim3(SK / 64, sd_cdiv(N, 16)), 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi,
-                                                                    feats(t + 1), F, t, tr(12));
+      const dim3 gpr(SK / 64, sd_cdiv(N, 16));
+      if (KP_RW && U == 256 && npi <= 16) {
+        if (d.Kd == 16)
+          k_prior_rw<16><<<gpr, 1024, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi, feats(t + 1), F, t,
+                                               tr(12));
+        else
+          k_prior_rw<32><<<gpr, 1024, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi, feats(t + 1), F, t,
+                                               tr(12));
+      } else if (d.Kd == 16) {
+        k_prior<16><<<gpr, 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi, feats(t + 1), F, t,
+                                          tr(12));
+      } else {
+        k_prior<32><<<gpr, 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi, feats(t + 1), F, t,
+                                          tr(12));
+      }
     }
     SD_LAUNCH_CHECK();
   }
