@@ -684,16 +684,28 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
 }
 
 // ------------------------------------------------------------------------------------------- backward kernels
-// straight-through sampler backward of one categorical (team of KD lanes): d logits += d/dl <ds, y_soft>
+// straight-through sampler backward of one categorical (team of KD lanes): d logits += d/dl <ds, y_soft>. The part
+// that needs only the logit and the noise (sampler_fwd) can run before the incoming gradient exists (k_carry: before
+// its contraction); sampler_bwd_tail finishes it.
+struct STFwd {
+  float p, pp, nl, ys;
+};
+template <int KD>
+SD_DEV STFwd sampler_fwd(float l, float gn, float unimix, int lt) {
+  STFwd f;
+  unimix_forward<KD>(l, true, KD, unimix, f.p, f.pp, f.nl);
+  int idx;
+  st_soft<KD>(f.nl, gn, true, f.ys, idx, lt);
+  return f;
+}
+template <int KD>
+SD_DEV float sampler_bwd_tail(const STFwd& f, float ds, float unimix) {
+  const float sd = group_sum<KD>(ds * f.ys);
+  return unimix_backward<KD>(f.ys * (ds - sd), f.p, f.pp, f.nl, true, unimix);
+}
 template <int KD>
 SD_DEV float sampler_bwd(float l, float gn, float ds, float unimix, int lt) {
-  float p, pp, nl;
-  unimix_forward<KD>(l, true, KD, unimix, p, pp, nl);
-  float ys;
-  int idx;
-  st_soft<KD>(nl, gn, true, ys, idx, lt);
-  const float sd = group_sum<KD>(ds * ys);
-  return unimix_backward<KD>(ys * (ds - sd), p, pp, nl, true, unimix);
+  return sampler_bwd_tail<KD>(sampler_fwd<KD>(l, gn, unimix, lt), ds, unimix);
 }
 
 // incoming gradient of posterior element (t, row, col) of a width-W output: time-major, or batch-major (bm_grads) plus
@@ -1037,6 +1049,14 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
                         (uint64_t)((long)ger * S + n0 / KD + d.group_offset) * KD + lt);
     }
   }
+  // the sampler's forward half of step t - 1 (carry_s workgroups): needs only the logit and the noise, so it runs
+  // here, beside the prologue loads, instead of after the contraction
+  STFwd sf[NE];
+  if (!p0) {
+#pragma unroll
+    for (int k = 0; k < NE; ++k)
+      if (tid + NTHR * k < MR * KD) sf[k] = sampler_fwd<KD>(e0[k], gn[k], d.unimix, (tid + NTHR * k) % KD);
+  }
   // d_xcat part = sum of the slabs (k_dx01's order); the x2 writer stores its part and then rebuilds x0's
   f32x4 dx[NU];
 #pragma unroll
@@ -1095,7 +1115,7 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
         if (ev) w.ch[(long)ger * D + n0 + lt] = rs[k] ? 0.f : e0[k] + C[er * KD + lt];
       } else {
         const float cs = rs[k] ? 0.f : C[er * KD + lt];
-        const float dlv = sampler_bwd<KD>(e0[k], gn[k], ev ? e1[k] + cs : 0.f, d.unimix, lt);
+        const float dlv = sampler_bwd_tail<KD>(sf[k], ev ? e1[k] + cs : 0.f, d.unimix);
         if (ev) d.dl[(long)tp * B * SK + (long)ger * SK + n0 + lt] = e2[k] + dlv;
       }
     }
