@@ -175,9 +175,15 @@ struct KC3Rms {
   }
 };
 
-template <bool RMS, bool POUT>
-__global__ __launch_bounds__(256, 2) void gemm3_mlp_kernel(GemmArgs g, MlpExt e) {
-  constexpr int BM = 128, BN = 128, WM = 64, WN = 64, TM = WM / 16, TN = WN / 16;
+// BN = 128: 2 x 2 waves of 64 x 64 (2 workgroups per CU). BN = 256 (the heads' 256-column layers): 2 x 2 waves of
+// 64 x 128, one workgroup per CU — each B fragment read from LDS feeds 4 row tiles and each A fragment 8 column tiles,
+// 1.33x the MFMAs per LDS byte of the 64 x 64 wave tile (whose main loop the LDS traffic bounds: MFMA busy ~0.35)
+#ifndef SD_MLP_WIDE
+#define SD_MLP_WIDE 1
+#endif
+template <bool RMS, bool POUT, int BN>
+__global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void gemm3_mlp_kernel(GemmArgs g, MlpExt e) {
+  constexpr int BM = 128, WM = 64, WN = BN / 2, TM = WM / 16, TN = WN / 16, NP = WN / 64;
   int tx, ty, tz;
   g3_tile(g, tx, ty, tz);
   const int bn0 = tx * BN, bm0 = ty * BM, b = tz;
@@ -212,11 +218,13 @@ __global__ __launch_bounds__(256, 2) void gemm3_mlp_kernel(GemmArgs g, MlpExt e)
   float* C = g.C + (long)b * g.sC;
   const float* bpb = pick_b(e.bp, b);
   const float* bias = bpb ? bpb : g.bias ? g.bias + (long)b * g.sBias : nullptr;
-  float ss[TM][4];
+  float ss[NP][TM][4];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int p = 0; p < NP; ++p)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ss[i][r] = 0.f;
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ss[p][i][r] = 0.f;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = bn0 + wc * WN + 16 * j + l16;
@@ -228,23 +236,26 @@ __global__ __launch_bounds__(256, 2) void gemm3_mlp_kernel(GemmArgs g, MlpExt e)
         const int m = bm0 + wr * WM + 16 * i + 4 * q + r;
         const float v = g.alpha * acc[i][j][r] + bv;
         if (m < g.M && n < g.N) C[(long)m * g.ldc + n] = v;
-        ss[i][r] += n < g.N ? v * v : 0.f;
+        ss[j / 4][i][r] += n < g.N ? v * v : 0.f;
       }
   }
-  if (POUT) {  // partial (64 columns of this wave) of every row's sum of squares
-    float* pout = e.pout + (long)b * e.sPout + (long)((bn0 + wc * WN) / 64) * g.M;
+  if (POUT) {  // partials (per 64 columns) of every row's sum of squares
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int p = 0; p < NP; ++p) {
+      float* pout = e.pout + (long)b * e.sPout + (long)((bn0 + wc * WN) / 64 + p) * g.M;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = ss[i][r];
-        v += __shfl_xor(v, 1, 64);
-        v += __shfl_xor(v, 2, 64);
-        v += __shfl_xor(v, 4, 64);
-        v += __shfl_xor(v, 8, 64);
-        const int m = bm0 + wr * WM + 16 * i + 4 * q + r;
-        if (l16 == 0 && m < g.M) pout[m] = v;
-      }
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = ss[p][i][r];
+          v += __shfl_xor(v, 1, 64);
+          v += __shfl_xor(v, 2, 64);
+          v += __shfl_xor(v, 4, 64);
+          v += __shfl_xor(v, 8, 64);
+          const int m = bm0 + wr * WM + 16 * i + 4 * q + r;
+          if (l16 == 0 && m < g.M) pout[m] = v;
+        }
+    }
   }
 }
 
@@ -287,12 +298,20 @@ extern "C" int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd
     e.nwp[b] = x->norm_w_ptr[b];
     e.wrows[b] = x->w_rows[b];
   }
-  dim3 grid(sd_cdiv(g.N, 128), sd_cdiv(g.M, 128), g.batch);
   hipStream_t st = (hipStream_t)stream_;
-  if (rms && pout) gemm3_mlp_kernel<true, true><<<grid, 256, 0, st>>>(g, e);
-  else if (rms) gemm3_mlp_kernel<true, false><<<grid, 256, 0, st>>>(g, e);
-  else if (pout) gemm3_mlp_kernel<false, true><<<grid, 256, 0, st>>>(g, e);
-  else gemm3_mlp_kernel<false, false><<<grid, 256, 0, st>>>(g, e);
+  // 256-column tiles where the layer is exactly that wide (every imagined head's hidden layers), else 128
+  const bool wide = SD_MLP_WIDE && g.N % 256 == 0;
+#define SD_MLP_LAUNCH(BN_)                                                                             \
+  do {                                                                                                 \
+    const dim3 grid(sd_cdiv(g.N, BN_), sd_cdiv(g.M, 128), g.batch);                                    \
+    if (rms && pout) gemm3_mlp_kernel<true, true, BN_><<<grid, 256, 0, st>>>(g, e);                    \
+    else if (rms) gemm3_mlp_kernel<true, false, BN_><<<grid, 256, 0, st>>>(g, e);                      \
+    else if (pout) gemm3_mlp_kernel<false, true, BN_><<<grid, 256, 0, st>>>(g, e);                     \
+    else gemm3_mlp_kernel<false, false, BN_><<<grid, 256, 0, st>>>(g, e);                              \
+  } while (0)
+  if (wide) SD_MLP_LAUNCH(256);
+  else SD_MLP_LAUNCH(128);
+#undef SD_MLP_LAUNCH
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
