@@ -36,10 +36,20 @@ SD_DEV float dsilu(float z) {
 }
 
 // ------------------------------------------------------------------------------------------- contraction core
-// acc[t] += A[0:16, span] . W_t[n_t + 0:16, span]^T.  Wave w owns k chunks c = w, w+8, ...; lane group q = lane>>4
-// supplies k = 16c + 4q .. +3 as one float4 and the MFMA consumes them in 4 steps (a permuted but consistent k order).
+// acc[t] += A[0:16, span] . W_t[n_t + 0:16, span]^T.  Wave w owns 16-deep k chunks; lane group q = lane>>4 supplies
+// k = 16c + 4q .. +3 as one float4 and the MFMA consumes them in 4 steps (a permuted but consistent k order).
+// SD_CORE_PAIR: a wave's chunks come in adjacent pairs (2w, 2w + 1, 2w + 16, 2w + 17, ...), so the two loads it issues
+// back to back for a row cover one whole 128-B line (with single chunks c = w, w + 8, ... each 128-B line of a weight
+// row was split between two waves' loads, issued at different times).
+#ifndef SD_CORE_PAIR
+#define SD_CORE_PAIR 1
+#endif
+SD_DEV int core_chunk(int wave, int c) {
+  return SD_CORE_PAIR ? 2 * (wave + NW * (c >> 1)) + (c & 1) : wave + NW * c;
+}
 template <int NT, int CPW>
 struct Core {
+  static_assert(!SD_CORE_PAIR || CPW % 2 == 0, "chunk pairs");
   f32x4 b[CPW][NT];
   f32x4 acc[NT];
 
@@ -47,7 +57,7 @@ struct Core {
   SD_DEV void load_b(const float* const* Wt, int nch, int wave, int q) {
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
-      const int ch = wave + NW * c;
+      const int ch = core_chunk(wave, c);
 #pragma unroll
       for (int t = 0; t < NT; ++t) b[c][t] = ch < nch ? ld4(Wt[t] + ch * 16 + 4 * q) : zero4();
     }
@@ -64,7 +74,7 @@ struct Core {
   SD_DEV void run_lds(const float* P, int lda, int nch, int wave, int l16, int q) {
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
-      const int ch = wave + NW * c;
+      const int ch = core_chunk(wave, c);
       if (ch < nch) mma(ld4(P + l16 * lda + ch * 16 + 4 * q), c);
     }
   }
@@ -73,12 +83,12 @@ struct Core {
     f32x4 a[CPW];
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
-      const int ch = wave + NW * c;
+      const int ch = core_chunk(wave, c);
       a[c] = (ch < nch && l16 < M) ? ld4(A + (long)l16 * lda + ch * 16 + 4 * q) : zero4();
     }
 #pragma unroll
     for (int c = 0; c < CPW; ++c)
-      if (wave + NW * c < nch) mma(a[c], c);
+      if (core_chunk(wave, c) < nch) mma(a[c], c);
   }
   // sum the 8 waves' partial tiles into C (16 x 16NT, row-major) in LDS
   SD_DEV void reduce(float* red, float* C, int tid, int wave, int lane) {
