@@ -506,6 +506,10 @@ typedef struct sd_slice_keys {
   sd_slice_key k[SD_MAX_SLICE_KEYS];
   int n;
 } sd_slice_keys;
+/* Replay slice picks (utils/buffer.py:27-42's random slice choice): pick[b] = uniform integer in [0, nstarts) from the
+ * counter-based Philox stream (seed, stream 8, step = draw, index b) — the buffer's sampling without a host RNG or a
+ * torch generator kernel; `draw` counts the buffer's sample calls. */
+int sd_replay_pick(uint64_t seed, uint32_t draw, long nstarts, int B, int64_t* pick, sd_stream stream);
 int sd_replay_slices(const sd_slice_keys* keys, const int64_t* starts, const int64_t* pick, int B, int L, long cap,
                      int E, int64_t* t_idx, int64_t* e_idx, int scatter, sd_stream stream);
 

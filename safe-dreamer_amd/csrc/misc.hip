@@ -621,6 +621,21 @@ __global__ __launch_bounds__(256) void slices_kernel(sd_slice_keys ks, const int
 }
 }  // namespace
 
+namespace {
+__global__ void replay_pick_kernel(uint64_t seed, uint32_t draw, long nstarts, int B, int64_t* __restrict__ pick) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) pick[b] = sd_uniform_int(seed, SD_STREAM_REPLAY, draw, (uint64_t)b, (int)nstarts);
+}
+}  // namespace
+
+extern "C" int sd_replay_pick(uint64_t seed, uint32_t draw, long nstarts, int B, int64_t* pick, sd_stream s) {
+  if (B < 0 || nstarts < 1 || nstarts > 0x7fffffffL || (B > 0 && !pick)) return SD_EARG;
+  if (B == 0) return SD_OK;
+  replay_pick_kernel<<<(B + 255) / 256, 256, 0, (hipStream_t)s>>>(seed, draw, nstarts, B, pick);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
 extern "C" int sd_replay_slices(const sd_slice_keys* keys, const int64_t* starts, const int64_t* pick, int B, int L,
                                 long cap, int E, int64_t* t_idx, int64_t* e_idx, int scatter, sd_stream s) {
   if (!keys || keys->n < 0 || keys->n > SD_MAX_SLICE_KEYS) return SD_EARG;

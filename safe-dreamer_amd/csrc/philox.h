@@ -13,6 +13,7 @@
 #define SD_STREAM_POLICY 4
 #define SD_STREAM_POLICY_ACT 5
 #define SD_STREAM_AUG 6
+#define SD_STREAM_REPLAY 8  // replay slice picks (sd_replay_pick); 7 is DreamerPro's augmented posterior scan
 
 struct sd_u32x4 { uint32_t x, y, z, w; };
 

@@ -92,7 +92,7 @@ class Stats(ctypes.Structure):
 
 _CTYPES = {
     "int": c_int, "long": c_long, "float": c_float, "double": ctypes.c_double, "uint64_t": ctypes.c_uint64,
-    "sd_stream": c_ptr, "void": None,
+    "uint32_t": ctypes.c_uint32, "sd_stream": c_ptr, "void": None,
 }
 
 

@@ -27,6 +27,7 @@ class Buffer:
         self._starts = None
         self._gen = torch.Generator(device=self.storage_device)
         self._gen.manual_seed(int(seed))
+        self._seed, self._draws = int(seed), 0  # device storage: picks from the Philox stream (sd_replay_pick)
 
     def _alloc(self, td):
         E = next(iter(td.values())).shape[0]
@@ -77,11 +78,24 @@ class Buffer:
         self._starts = torch.stack([order[idx[:, 0]], idx[:, 1]], 1)
         self._dirty = False
 
+    def _pick(self):
+        """B slice indices into the valid-start table: a device Philox draw on GPU storage (one launch, no torch RNG
+        kernel), torch's generator on CPU storage."""
+        B, V = self.batch_size, self._starts.shape[0]
+        if self.storage_device.type != "cuda":
+            return torch.randint(0, V, (B,), device=self.storage_device, generator=self._gen)
+        from . import _native as nat
+        from . import kernels as K
+        pick = torch.empty(B, dtype=torch.int64, device=self.storage_device)
+        nat.call("sd_replay_pick", self._seed & 0xFFFFFFFFFFFFFFFF, self._draws & 0xFFFFFFFF, V, B, K.p(pick), K.stream())
+        self._draws += 1
+        return pick
+
     def sample(self):
         if self._dirty:
             self._build_starts()
         B, L1 = self.batch_size, self.batch_length + 1
-        pick = torch.randint(0, self._starts.shape[0], (B,), device=self.storage_device, generator=self._gen)
+        pick = self._pick()
         st = self._starts[pick]
         t_idx = (st[:, :1] + torch.arange(L1, device=self.storage_device)[None]) % self.cap  # (B, L+1)
         e_idx = st[:, 1:2].expand(B, L1)
@@ -116,7 +130,7 @@ class Buffer:
         if self._dirty:
             self._build_starts()
         B, L = self.batch_size, self.batch_length
-        pick = torch.randint(0, self._starts.shape[0], (B,), device=self.storage_device, generator=self._gen)
+        pick = self._pick()
         pairs = [(v, dst[k], L, 0 if k == "action" else 1) for k, v in self._store.items()
                  if k not in ("stoch", "deter")]
         if dst_initial is not None and "stoch" in self._store:
