@@ -233,6 +233,27 @@ __global__ __launch_bounds__(256) void k_presplit6(const float* W, int rows, int
   split3_store(out + (((long)(n / BN) * nkt + k / BK6) * BN + n % BN) * PRE_ROW + k % BK6, ld4(W + (long)n * K + k));
 }
 
+// Pre-split ACTIVATION images (KH_APRE): the same BPre6 tile layout for a (rows, K) activation — tile (row / 64,
+// col / 32), row % 64 — written once by the producer, so the k_hid tiles that read a row (D / 64 column tiles of it)
+// copy its planes instead of each splitting it again (split3 of the same fp32 value: bit-identical operands).
+#ifndef KH_APRE
+#define KH_APRE 1
+#endif
+SD_DEV long pre_off(long row, int col, int K) {
+  return (((row >> 6) * (K / BK6) + col / BK6) * 64 + (row & 63)) * PRE_ROW + (col % BK6);
+}
+// 4 consecutive columns (col % 4 == 0) of one row
+SD_DEV void pre_store4(__bf16* img, long row, int col, int K, f32x4 v) { split3_store(img + pre_off(row, col, K), v); }
+// the image of a strided (rows, K) fp32 matrix (feats(0)'s deter at the first step)
+__global__ __launch_bounds__(256) void k_presplit_rows(const float* X, long ldx, int rows, int K, __bf16* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int nq = K / 4;
+  if (i >= (long)rows * nq) return;
+  const long r = i / nq;
+  const int k = 4 * (int)(i % nq);
+  pre_store4(out, r, k, K, ld4(X + r * ldx + k));
+}
+
 // ------------------------------------------------------------------------------------------- contraction
 // F6: the bf16x6 main loop (gemm6_core.h: fp32-accurate, 2.67x the fp32 MFMA rate) instead of v_mfma_f32_16x16x4_f32.
 // ES (early store) applies to the fp32 loop only.
@@ -427,6 +448,9 @@ struct OneHotProb {
   const float* add;  // optional (M, U)
   float* out;        // (M, U)
   float* part;       // (U / 16, M)
+  const float* nw;   // optional: RMSNorm weight -> img = pre-split image of silu(rms(out) * nw) (KH_APRE)
+  __bf16* img;
+  float eps;
 };
 __global__ __launch_bounds__(256) void k_onehot_lin(const float* X, long ldx, int SK, int Kd, OneHotProb p0,
                                                     OneHotProb p1, int nprob, int M, Tr tr) {
@@ -496,6 +520,17 @@ __global__ __launch_bounds__(256) void k_onehot_lin(const float* X, long ldx, in
     ss += __shfl_xor(ss, 1, 64);
     ss += __shfl_xor(ss, 2, 64);
     if ((lane & 3) == 0 && p.part) p.part[(long)(lane >> 2) * M + m] = ss;
+    if (p.img) {  // the row's normalised output, split once for k_hid (a wave holds the whole row)
+      float s4 = ss;
+#pragma unroll
+      for (int o2 = 4; o2 < 64; o2 <<= 1) s4 += __shfl_xor(s4, o2, 64);
+      const float rs = rsqrtf(s4 / (float)U + p.eps);
+      const f32x4 w = ld4(p.nw + c);
+      f32x4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = siluf_(o[e] * rs * w[e]);
+      pre_store4(p.img, m, c, U, y);
+    }
   }
   SD_TR(2)
   SD_TR_END(tr.p, tr.slot)
@@ -689,16 +724,19 @@ SD_DEV void hid_seg(const OpA& a0, const OpB& b0, int K, f32x4 (&acc)[1][WN / 16
 // hp = BlockLinear(dyn_hid_0)([h_g | x0 | x1 | x2]) + bh with x0 = silu(rms(x0p)), x1 = silu(rms(x1p)) applied by the
 // A loaders (rssm.py:52-63): four main loops over the input segments accumulate into one tile. BM = BN = 64,
 // grid (D/64, M/64); row partials per 64 columns (D/64 of them) for the gate norm.
+template <bool APRE>
 __global__ __launch_bounds__(256, KH_WAVES) void k_hid(sd_imagine d, const float* h, long ldh, const float* x0p, const float* x1p,
                                              const float* px0, const float* px1, int npx0, int npx1, const float* x2, float* hp,
-                                             float* ph, const __bf16* wh6, Tr tr) {
+                                             float* ph, const __bf16* wh6, const __bf16* himg, const __bf16* x1img,
+                                             const __bf16* x2img, Tr tr) {
   SD_TR_BEGIN
   constexpr int BM = KH_BM, BN = 64, WN = BN / (4 / (BM / 16));
+  static_assert(!APRE || BM == 64, "pre-split activation images are in 64-row tiles");
   __shared__ float rs0[BM], rs1[BM], red[256];
   const int Dg = d.D / d.G, U = d.U, Ig = Dg + 3 * U, M = d.N;
   const int n0 = xcd_col(blockIdx.x, gridDim.x, Dg / BN) * BN, m0 = blockIdx.y * BM, g = n0 / Dg;
   wg_rstd<BM, 8>(px0, npx0, M, m0, U, d.eps, rs0, red);
-  wg_rstd<BM, 8>(px1, npx1, M, m0, U, d.eps, rs1, red);
+  if (!APRE) wg_rstd<BM, 8>(px1, npx1, M, m0, U, d.eps, rs1, red);
   SD_TR(1)
   const float* Wseg = d.Wh + (long)n0 * Ig;  // rows n0.. of Wh viewed as (D, Ig)
   const int ct = n0 / BN, nkt = Ig / BK6;
@@ -710,7 +748,9 @@ __global__ __launch_bounds__(256, KH_WAVES) void k_hid(sd_imagine d, const float
       return BRows<BN>(Wseg + k0, Ig, 0, BN, 0);
   };
   f32x4 acc[1][WN / 16];
-  {
+  if constexpr (APRE) {  // h, x1 and x2 from their producers' pre-split images (64-row tiles of m0 / 64)
+    hid_seg<BM, BN, WN>(BPre6<BM>(himg, m0 / BM, d.D / BK6, g * Dg / BK6), bseg(0), Dg, acc, false);
+  } else {
     const APlain<BM> a0(h + (long)g * Dg, ldh, m0, M, Dg);
     hid_seg<BM, BN, WN>(a0, bseg(0), Dg, acc, false);
   }
@@ -718,13 +758,18 @@ __global__ __launch_bounds__(256, KH_WAVES) void k_hid(sd_imagine d, const float
     const ARms<BM> a0(x0p, U, d.n0, rs0, m0, M, U);
     hid_seg<BM, BN, WN>(a0, bseg(Dg), U, acc, true);
   }
-  {
-    const ARms<BM> a0(x1p, U, d.n1, rs1, m0, M, U);
-    hid_seg<BM, BN, WN>(a0, bseg(Dg + U), U, acc, true);
-  }
-  {
-    const APlain<BM> a0(x2, U, m0, M, U);
-    hid_seg<BM, BN, WN>(a0, bseg(Dg + 2 * U), U, acc, true);
+  if constexpr (APRE) {
+    hid_seg<BM, BN, WN>(BPre6<BM>(x1img, m0 / BM, U / BK6, 0), bseg(Dg + U), U, acc, true);
+    hid_seg<BM, BN, WN>(BPre6<BM>(x2img, m0 / BM, U / BK6, 0), bseg(Dg + 2 * U), U, acc, true);
+  } else {
+    {
+      const ARms<BM> a0(x1p, U, d.n1, rs1, m0, M, U);
+      hid_seg<BM, BN, WN>(a0, bseg(Dg + U), U, acc, true);
+    }
+    {
+      const APlain<BM> a0(x2, U, m0, M, U);
+      hid_seg<BM, BN, WN>(a0, bseg(Dg + 2 * U), U, acc, true);
+    }
   }
   SD_TR(2)
   ep_bias_part<BM, BN, WN, KH_PW>(acc, d.bh, hp, d.D, ph, M, m0, n0);
@@ -748,7 +793,8 @@ SD_DEV auto gate_b(const __bf16* wg6, int ct, int nkt, const float* Wblk, int Dg
 #define KG_WAVES 4
 #endif
 __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const float* hp, const float* ph, int nph,
-                                              const float* hold, float* hnew, long ldf, const __bf16* wg6, Tr tr) {
+                                              const float* hold, float* hnew, long ldf, const __bf16* wg6,
+                                              __bf16* himg, Tr tr) {
   SD_TR_BEGIN
   constexpr int BM = 64, BN = 96;
   const int Dg = d.D / d.G;
@@ -776,6 +822,7 @@ __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const floa
   SD_TR(2)
   const Lane L = lane_ids<BN, BN>();
   const float* bg = d.bg + (long)g * 3 * Dg;
+  float hv_[2][4] = {};
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int c = 16 * j + L.l16, jj = j0 + c, col = c0 + c;
@@ -788,7 +835,24 @@ __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const floa
       const float rs = sigmoidf_(ra);
       const float cc = tanhf(rs * ca);
       const float u = sigmoidf_(ua - 1.f);
-      hnew[m * ldf + col] = u * cc + (1.f - u) * hold[m * ldf + col];
+      const float hv = u * cc + (1.f - u) * hold[m * ldf + col];
+      hnew[m * ldf + col] = hv;
+      hv_[j][r] = hv;
+    }
+  }
+  if (himg) {  // the 64 x 32 tile of the new deter is exactly one pre-split image tile: staged in LDS, split, written
+    constexpr int STG = (BM + BN) * LROW6;
+    float* T = reinterpret_cast<float*>(sd_smem6<STG>());  // the main loop's image, free now
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[(L.wr * 16 + 4 * L.q + r) * 36 + 16 * j + L.l16] = hv_[j][r];
+    __syncthreads();
+    const int row = threadIdx.x >> 2, c8 = (threadIdx.x & 3) * 8;
+    if (m0 + row < d.N) {
+      pre_store4(himg, m0 + row, c0 + c8, d.D, *reinterpret_cast<const f32x4*>(T + row * 36 + c8));
+      pre_store4(himg, m0 + row, c0 + c8 + 4, d.D, *reinterpret_cast<const f32x4*>(T + row * 36 + c8 + 4));
     }
   }
   SD_TR_END(tr.p, tr.slot)
@@ -1012,7 +1076,7 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
 #endif
 __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* X, const float* nw,
                                                      const float* part_in, int np, float* act, float* x2, int t,
-                                                     int want_x2, Tr tr) {
+                                                     int want_x2, __bf16* x2img, Tr tr) {
   SD_TR_BEGIN
   constexpr int U = 256, MO = 32, MA = 16;  // <= 32 output logits (2A or A), <= 16 actions
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1105,7 +1169,10 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
   f32x4 o;
 #pragma unroll
   for (int e = 0; e < 4; ++e) o[e] = siluf_(xp[e] * r2 * n2[e]);
-  if (live) *reinterpret_cast<f32x4*>(x2 + m * U + 4 * lane) = o;
+  if (live) {
+    *reinterpret_cast<f32x4*>(x2 + m * U + 4 * lane) = o;
+    if (x2img) pre_store4(x2img, m, 4 * lane, U, o);
+  }
   SD_TR_END(tr.p, tr.slot)
 }
 
@@ -1405,6 +1472,7 @@ struct IWork {
   float *a[2], *pa[2], *ad, *x0p, *px0, *x1p, *px1, *x2, *hp, *ph, *i[2], *pi[2];
   __bf16 *wh6, *wg6;  // pre-split _dyn_hid / _dyn_gru weights (BPre6 images, 3 bf16 per element)
   float *waT, *w1T;   // actor layer 0's stoch columns and _dyn_in1, transposed (SK, U) for k_onehot_lin
+  __bf16 *h6, *x16, *x26;  // pre-split activation images (KH_APRE): deter, silu(rms(x1p)), x2; rows padded to 64
   long total;
 };
 long al64(long n) { return (n + 63) / 64 * 64; }
@@ -1426,6 +1494,10 @@ IWork iwork(const sd_imagine& d, float* base) {
   w.wg6 = reinterpret_cast<__bf16*>(take((long)3 * d.D * (d.D / d.G) * 3 / 2));
   w.waT = take((long)d.SK * d.U);
   w.w1T = take((long)d.SK * d.U);
+  const long rows = (d.N + 63L) / 64 * 64;
+  w.h6 = reinterpret_cast<__bf16*>(take(rows * d.D * 3 / 2));
+  w.x16 = reinterpret_cast<__bf16*>(take(rows * d.U * 3 / 2));
+  w.x26 = reinterpret_cast<__bf16*>(take(rows * d.U * 3 / 2));
   w.total = o;
   return w;
 }
@@ -1480,12 +1552,13 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
     LinProb pd{feats(t + 1) + SK, F, D, d.Wa[0] + SK, F, nullptr, w.ad, U, nullptr, nullptr};
     k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, Tr{});
   } else if (which == 1) {
-    k_hid<<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU, w.x2, w.hp,
-                                                       w.ph, w.wh6, Tr{});
+    k_hid<false><<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1,
+                                                                 U / KL3_PW, npU, w.x2, w.hp, w.ph, w.wh6, nullptr,
+                                                                 nullptr, nullptr, Tr{});
   } else {
     // k_gate reads hold = feats(t) deter and writes feats(t + 1) deter: the same values again
     k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F, w.wg6,
-                                                         Tr{});
+                                                         nullptr, Tr{});
   }
   SD_LAUNCH_CHECK();
   return SD_OK;
@@ -1507,6 +1580,14 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   // reads deter' (img_net_0 / _dyn_in0), the stoch part (+ bias + deter part, row partials) after the prior sample
   const float* Wa0d = d.Wa[0] + SK;  // (U, F) columns SK.. of the actor's first weight
   const int t_end = d.t_end > 0 ? d.t_end : d.H1;
+  // k_hid reads deter / x1 / x2 from pre-split images when every producer writes one (k_gate, k_onehot_lin,
+  // k_action_rows)
+  const bool apre = KH_APRE && KH_1S && F6_HID && KH_PRE && KH_BM == 64 && KL_ONEHOT && d.SK / d.Kd <= 64 && KA_ROWS &&
+                    !SD_FUSED_ACTOR;
+  if (d.t_begin == 0 && apre) {  // the start state's deter image
+    k_presplit_rows<<<(int)sd_cdiv((long)N * D / 4, 256), 256, 0, st>>>(feats(0) + SK, F, N, D, w.h6);
+    SD_LAUNCH_CHECK();
+  }
   if (d.t_begin == 0 && KH_PRE && F6_HID) {  // _dyn_hid's weight split into its bf16 planes once per imagination
     const long Ig = D / d.G + 3L * U;
     k_presplit6<64><<<(int)sd_cdiv((long)D * Ig / 4, 256), 256, 0, st>>>(d.Wh, D, (int)Ig, w.wh6);
@@ -1537,7 +1618,8 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       LinProb pa{feats(t), F, SK, d.Wa[0], F, d.ba[0], a0, U, w.pa[0], w.ad};
       LinProb px{feats(t), F, SK, d.W1, SK, d.b1, w.x1p, U, w.px1, nullptr};
       if (KL_ONEHOT && d.SK / d.Kd <= 64) {
-        const OneHotProb oa{w.waT, d.ba[0], w.ad, a0, w.pa[0]}, ox{w.w1T, d.b1, nullptr, w.x1p, w.px1};
+        const OneHotProb oa{w.waT, d.ba[0], w.ad, a0, w.pa[0], nullptr, nullptr, 0.f},
+            ox{w.w1T, d.b1, nullptr, w.x1p, w.px1, apre ? d.n1 : nullptr, apre ? w.x16 : nullptr, d.eps};
         k_onehot_lin<<<sd_cdiv(N, 4), 256, 0, st>>>(feats(t), F, SK, d.Kd, oa, ox, last ? 1 : 2, N, tr(0));
       } else {
         k_lin<32, KL2_BN><<<dim3(U / KL2_BN, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, px, N, tr(0));
@@ -1564,7 +1646,7 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       if (KA_ROWS)
         k_action_rows<<<sd_cdiv(N, 4), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur], d.na[d.actor_layers - 1],
                                                      w.pa[cur], npa, d.actions + (long)t * N * d.A, w.x2, t,
-                                                     last ? 0 : 1, tr(4));
+                                                     last ? 0 : 1, apre ? w.x26 : nullptr, tr(4));
       else
         k_action<<<dim3(1, sd_cdiv(N, KA_BM)), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur],
                                                   d.na[d.actor_layers - 1], w.pa[cur], npa,
@@ -1572,11 +1654,17 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     }
     SD_LAUNCH_CHECK();
     if (last) break;
-    k_hid<<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1, U / KL3_PW, npU,
-                                                         w.x2, w.hp, w.ph, w.wh6, tr(5));
+    if (apre)
+      k_hid<true><<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1,
+                                                                  U / KL3_PW, npU, w.x2, w.hp, w.ph, w.wh6, w.h6,
+                                                                  w.x16, w.x26, tr(5));
+    else
+      k_hid<false><<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1,
+                                                                   U / KL3_PW, npU, w.x2, w.hp, w.ph, w.wh6, nullptr,
+                                                                   nullptr, nullptr, tr(5));
     SD_LAUNCH_CHECK();
     k_gate<<<dim3(D / 32, sd_cdiv(N, 64)), 256, 0, st>>>(d, w.hp, w.ph, D / KH_PW, feats(t) + SK, feats(t + 1) + SK, F, w.wg6,
-                                                         tr(6));
+                                                         apre ? w.h6 : nullptr, tr(6));
     SD_LAUNCH_CHECK();
     {  // img_net_0, the next step's _dyn_in0 and the deter part of its actor layer 0 share A = deter'
       LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};
