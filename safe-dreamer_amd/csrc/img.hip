@@ -12,6 +12,7 @@
 //   * independent contractions that share an A operand grouped into one launch (actor layer 0 with _dyn_in1,
 //     img_net_0 with the next step's _dyn_in0).
 // Results land directly in the reference's (H1, N, F) feat and (H1, N, A) action layouts.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -521,10 +522,20 @@ __global__ __launch_bounds__(256) void k_onehot_lin(const float* X, long ldx, in
     ss += __shfl_xor(ss, 2, 64);
     if ((lane & 3) == 0 && p.part) p.part[(long)(lane >> 2) * M + m] = ss;
     if (p.img) {  // the row's normalised output, split once for k_hid (a wave holds the whole row)
-      float s4 = ss;
+      // rstd exactly as k_hid's wg_rstd<64, 8> forms it from these 16 partials (lane 4 p holds partial p): 4 groups
+      // g of partials g, g + 4, g + 8, g + 12, summed in that order, then the groups in order -> bit-identical x1
+      float pp[16];
 #pragma unroll
-      for (int o2 = 4; o2 < 64; o2 <<= 1) s4 += __shfl_xor(s4, o2, 64);
-      const float rs = rsqrtf(s4 / (float)U + p.eps);
+      for (int q = 0; q < 16; ++q) pp[q] = __shfl(ss, 4 * q, 64);
+      float tsum = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float sg = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sg += pp[g + 4 * k];
+        tsum += sg;
+      }
+      const float rs = rsqrtf(tsum / (float)U + p.eps);
       const f32x4 w = ld4(p.nw + c);
       f32x4 y;
 #pragma unroll
@@ -1582,8 +1593,9 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   const int t_end = d.t_end > 0 ? d.t_end : d.H1;
   // k_hid reads deter / x1 / x2 from pre-split images when every producer writes one (k_gate, k_onehot_lin,
   // k_action_rows)
+  // (SDHIP_KH_NOAPRE set: the in-loader split, for tests comparing the two — bit-identical)
   const bool apre = KH_APRE && KH_1S && F6_HID && KH_PRE && KH_BM == 64 && KL_ONEHOT && d.SK / d.Kd <= 64 && KA_ROWS &&
-                    !SD_FUSED_ACTOR;
+                    !SD_FUSED_ACTOR && U / KL2_PW == 16 && !getenv("SDHIP_KH_NOAPRE");
   if (d.t_begin == 0 && apre) {  // the start state's deter image
     k_presplit_rows<<<(int)sd_cdiv((long)N * D / 4, 256), 256, 0, st>>>(feats(0) + SK, F, N, D, w.h6);
     SD_LAUNCH_CHECK();

@@ -61,3 +61,20 @@ def test_fused_imagination_deterministic():
     a = _run(ag, start, 5, True)
     b = _run(ag, start, 5, True)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("name,N", [("walker_r2", 192), ("atari_r2", 100), ("maze_r2", 128)])
+def test_presplit_images_bit_identical(name, N):
+    """k_hid reading deter / x1 / x2 from their producers' pre-split bf16x3 images (KH_APRE) gives exactly the
+    imagination of the in-loader split (SDHIP_KH_NOAPRE): the same fp32 values are split, x1's rstd is summed in
+    wg_rstd's order."""
+    import os
+    ag, z, spec, obs = build_agent(name)
+    start = _start(ag, N, 11)
+    a = _run(ag, start, 6, True)
+    os.environ["SDHIP_KH_NOAPRE"] = "1"
+    try:
+        b = _run(ag, start, 6, True)
+    finally:
+        del os.environ["SDHIP_KH_NOAPRE"]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
