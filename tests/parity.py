@@ -69,6 +69,17 @@ def ulp(x):
     return np.spacing(np.abs(np.asarray(x, np.float32))).astype(np.float64)
 
 
+def bound_ratio(got, ref, rtol, atol, mask=None):
+    """max over elements of |got - ref| / (atol + rtol |ref|): the fraction of assert_close's bound used (<= 1 passes)"""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    bound = np.broadcast_to(np.asarray(atol, np.float64), ref.shape) + rtol * np.abs(ref)
+    r = np.abs(got - ref) / np.maximum(bound, 1e-300)
+    if mask is not None:
+        r = np.where(mask, 0.0, r)
+    return float(r.max()) if r.size else 0.0
+
+
 def assert_close(got, ref, rtol, atol, what, mask=None):
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)

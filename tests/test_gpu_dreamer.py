@@ -11,13 +11,15 @@ and runs two full updates (WM fwd+bwd, imagination, actor/critic, AGC+LaProp). S
   * parameters after each LaProp step: <= 2e-3 relative to the step size (LaProp normalises the gradient).
 """
 import copy
+import json
+import os
 
 import numpy as np
 import pytest
 import torch
 
 from golden_io import CASES, batch, case_overrides, initial, load_case, sample_idx
-from parity import assert_close, compare_indices, imag_margins, post_margins, ulp
+from parity import assert_close, bound_ratio, compare_indices, imag_margins, post_margins, ulp
 from sdreamer.config import load_config
 
 pytestmark = pytest.mark.gpu
@@ -105,6 +107,7 @@ def test_update_matches_reference(name):
     _, _, _, params0, _ = load_case(name)
     prev = {k: params0[k].reshape(-1)[sample_idx(k, params0[k].size)] for k in spec.shapes}
     report = {}
+    bounds = {}
     for u in range(2):
         seed = int(z[f"u{u}_seed"])
         data = batch(z, u, obs, DEV)
@@ -185,12 +188,19 @@ def test_update_matches_reference(name):
             assert_close(v, v_ref, 2e-2, 2e-4 * np.abs(v_ref).max() + 1e-30, f"u{u} exp_avg_sq {k}")
             tiny = np.sqrt(v_ref) < 1e-3 * np.sqrt(v_ref).max()
             assert_close(m, m_ref, 2e-2, 1e-2 * np.abs(m_ref).max() + 1e-30, f"u{u} exp_avg {k}", mask=tiny)
+            for what, br in (("v", bound_ratio(v, v_ref, 2e-2, 2e-4 * np.abs(v_ref).max() + 1e-30)),
+                             ("m", bound_ratio(m, m_ref, 2e-2, 1e-2 * np.abs(m_ref).max() + 1e-30, mask=tiny))):
+                if br > bounds.get(what, ("", 0.0))[1]:
+                    bounds[what] = (k, br)
             flat = sd[k].detach().reshape(-1).cpu().numpy()
             got = flat[sample_idx(k, flat.size)]
             ref = z[f"u{u}_p_{k}__s"]
             d_got, d_ref = got.astype(np.float64) - prev[k], ref.astype(np.float64) - prev[k]
             assert_close(d_got, d_ref, 2e-2, 1e-2 * np.abs(d_ref).max() + 4 * ulp(ref), f"u{u} parameter step {k}",
                          mask=tiny)
+            br = bound_ratio(d_got, d_ref, 2e-2, 1e-2 * np.abs(d_ref).max() + 4 * ulp(ref), mask=tiny)
+            if br > bounds.get("step", ("", 0.0))[1]:
+                bounds["step"] = (k, br)
             nz_ = (~tiny) & (np.abs(d_ref) > 0)
             if nz_.any():
                 worst = max(worst, float((np.abs(d_got - d_ref)[nz_] / np.abs(d_ref)[nz_]).max()))
@@ -201,7 +211,13 @@ def test_update_matches_reference(name):
             flat = sd[sk].detach().reshape(-1).cpu().numpy()
             ref = z[f"u{u}_p_{sk}__s"]
             assert_close(flat[sample_idx(sk, flat.size)], ref, 0.0, 4 * ulp(ref) + 1e-12, f"u{u} slow critic {sk}")
+    report["bound_ratio"] = {k: {"tensor": t, "ratio": r} for k, (t, r) in bounds.items()}
     print(name, report)
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "golden")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, f"{name}{'_f32' if os.environ.get('SDREAMER_FAST_GEMM') == '0' else ''}.json"),
+              "w") as f:
+        json.dump(report, f, indent=1, sort_keys=True)
 
 
 @pytest.mark.parametrize("name", ["walker_r2", "walker_r2aug", "walker_pro"])
