@@ -928,7 +928,7 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
 // k_prior on RTile<16>: 1024 threads, grid (SK / 64, M / 16); one sampler element per thread (row tid / 64, column
 // tid % 64: teams of KD lanes), the noise drawn / read before the contraction
 template <int KD>
-__global__ __launch_bounds__(1024) void k_prior_rw(sd_imagine d, const float* X, const float* nw, const float* part_in,
+__global__ __launch_bounds__(1024, 8) void k_prior_rw(sd_imagine d, const float* X, const float* nw, const float* part_in,
                                                    int np, float* snew, long ldf, int t, Tr tr) {
   SD_TR_BEGIN
   using RT = RTile<16>;
@@ -1085,18 +1085,19 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
 #ifndef KA_ROWS
 #define KA_ROWS 1
 #endif
+template <int MO>  // >= the output logits (2A or A): 16 or 32
 __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* X, const float* nw,
                                                      const float* part_in, int np, float* act, float* x2, int t,
                                                      int want_x2, __bf16* x2img, Tr tr) {
   SD_TR_BEGIN
-  constexpr int U = 256, MO = 32, MA = 16;  // <= 32 output logits (2A or A), <= 16 actions
+  constexpr int U = 256, MA = 16;  // <= 16 actions
+  __shared__ float w2s[U * MA];    // _dyn_in2's weight (U, A), staged coalesced while the logits chain runs
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long m = (long)blockIdx.x * 4 + wave;
   const int A = d.A, NO = d.act_discrete ? A : 2 * A, M = d.N;
   const bool live = m < M;
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
-  // every operand load first: the row's partials, its 4 columns, the norm weight, the output layer's rows, and the
-  // action branch's weights W2[4 lane + e][j]
+  // operand loads first: the row's partials, its 4 columns, the norm weight, the output layer's rows
   const float pv = (live && lane < np) ? part_in[(long)lane * M + m] : 0.f;
   const f32x4 xv = live ? ld4(X + m * U + 4 * lane) : zero4();
   const f32x4 wn = ld4(nw + 4 * lane);
@@ -1104,12 +1105,9 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
 #pragma unroll
   for (int o = 0; o < MO; ++o) wo[o] = o < NO ? ld4(d.Wao + (long)o * U + 4 * lane) : zero4();
   const float bo = lane < NO ? d.bao[lane] : 0.f;
-  f32x4 w2[MA];  // w2[j][e] = W2[4 lane + e][j]
   const bool x2w = want_x2 != 0;
-#pragma unroll
-  for (int j = 0; j < MA; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) w2[j][e] = (x2w && j < A) ? d.W2[(long)(4 * lane + e) * A + j] : 0.f;
+  if (x2w)
+    for (int i = threadIdx.x; i < U * A; i += 256) w2s[i] = d.W2[i];
   const f32x4 b2 = ld4(d.b2 + 4 * lane), n2 = ld4(d.n2 + 4 * lane);
   float nz = 0.f;  // the action noise of element (m, lane)
   if (d.act_discrete) {
@@ -1160,10 +1158,11 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
     }
   }
   if (live && lane < A) act[m * A + lane] = a;
-  if (!x2w) {
+  if (!x2w) {  // (uniform over the launch)
     SD_TR_END(tr.p, tr.slot)
     return;
   }
+  __syncthreads();  // w2s staged
   const float an = a / fmaxf(fabsf(a), 1.f);
   float anj[MA];
 #pragma unroll
@@ -1174,7 +1173,7 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
   for (int j = 0; j < MA; ++j)
     if (j < A) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) xp[e] += anj[j] * w2[j][e];
+      for (int e = 0; e < 4; ++e) xp[e] += anj[j] * w2s[(4 * lane + e) * A + j];
     }
   const float r2 = rsqrtf(wave_sum(xp[0] * xp[0] + xp[1] * xp[1] + xp[2] * xp[2] + xp[3] * xp[3]) / (float)U + d.eps);
   f32x4 o;
@@ -1655,10 +1654,16 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
         cur ^= 1;
         npa = npR;
       }
-      if (KA_ROWS)
-        k_action_rows<<<sd_cdiv(N, 4), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur], d.na[d.actor_layers - 1],
-                                                     w.pa[cur], npa, d.actions + (long)t * N * d.A, w.x2, t,
-                                                     last ? 0 : 1, apre ? w.x26 : nullptr, tr(4));
+      if (KA_ROWS) {
+        const float* xa = d.actor_layers == 1 ? a0 : w.a[cur];
+        float* acts = d.actions + (long)t * N * d.A;
+        if ((d.act_discrete ? d.A : 2 * d.A) <= 16)
+          k_action_rows<16><<<sd_cdiv(N, 4), 256, 0, st>>>(d, xa, d.na[d.actor_layers - 1], w.pa[cur], npa, acts,
+                                                           w.x2, t, last ? 0 : 1, apre ? w.x26 : nullptr, tr(4));
+        else
+          k_action_rows<32><<<sd_cdiv(N, 4), 256, 0, st>>>(d, xa, d.na[d.actor_layers - 1], w.pa[cur], npa, acts,
+                                                           w.x2, t, last ? 0 : 1, apre ? w.x26 : nullptr, tr(4));
+      }
       else
         k_action<<<dim3(1, sd_cdiv(N, KA_BM)), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur],
                                                   d.na[d.actor_layers - 1], w.pa[cur], npa,
