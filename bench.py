@@ -134,6 +134,12 @@ def cpu_baseline(cfg, n_updates, threads, A=6, discrete=False):
     return statistics.median(times)
 
 
+# the parity legs run a fresh agent's FIRST update, which is eager (graphs are captured after two eager updates); the
+# timed updates replay the graphs. tests/test_gpu_graph_fullsize.py pins graph replay == eager bit for bit (metrics,
+# parameters, replay storage over 5 updates at C2 / C4 / C5), which is what carries these numbers to the timed path.
+EAGER_NOTE = "eager first update; graph replay == eager bit-exact (tests/test_gpu_graph_fullsize.py, C2/C4/C5)"
+
+
 def wm_loss_parity():
     """'WM-loss Δ vs ref' (BASELINE.json metric): the product's first update on the walker r2dreamer golden case —
     the reference's own update() outputs, generated by tests/golden/gen_golden.py — with the reference weights, batch,
@@ -164,7 +170,8 @@ def wm_loss_parity():
     wm_ref = sum(scales[k] * float(z[f"u0_m_loss/{k}"]) for k in scales)
     return {"wm_loss_rel_err": abs(wm - wm_ref) / abs(wm_ref), "max_term_rel_err": max(terms.values()),
             "terms": terms, "case": f"tests/golden/{name}.npz (reference update() outputs, "
-                                    f"B{int(z['meta_B'])} L{int(z['meta_T'])} H{int(z['meta_H'])})"}
+                                    f"B{int(z['meta_B'])} L{int(z['meta_T'])} H{int(z['meta_H'])})",
+            "path": EAGER_NOTE}
 
 
 def wm_loss_parity_full(name="C2_walker_r2"):
@@ -208,7 +215,7 @@ def wm_loss_parity_full(name="C2_walker_r2"):
     return {"wm_loss_rel_err": abs(wm - wm_ref) / abs(wm_ref), "max_term_rel_err": max(terms.values()),
             "terms": terms, "posterior_index_mismatches": flips, "posterior_indices": int(z["post_idx"].size),
             "case": f"{os.path.relpath(fixture_path(name), ROOT)} (the reference's own update() outputs at "
-                    f"B{B} L{L} H{H}, same weights / batch / noise seed)"}
+                    f"B{B} L{L} H{H}, same weights / batch / noise seed)", "path": EAGER_NOTE}
 
 
 # The committed kernel table of this build (tools/profile_round.sh -> tools/kernel_table.py: the rocprofv3 kernel trace

@@ -3,6 +3,6 @@
 # timeline of a replayed update. Output under gpurun_out/<tag>_*.
 set -o pipefail
 T=$1
-for ph in P S1 M2a; do
+for ph in P S1 M2a M1 S2; do
   bash tools/phase_trace.sh ${T}_$ph $ph || exit 1
 done
