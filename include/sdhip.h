@@ -514,9 +514,12 @@ int sd_replay_slices(const sd_slice_keys* keys, const int64_t* starts, const int
                      int E, int64_t* t_idx, int64_t* e_idx, int scatter, sd_stream stream);
 
 /* r2dreamer augmentation (dreamer.py:716-729,845-880): (B*T, H, W, C) f32 images replicate-padded by `pad` and
- * shifted by Philox integer shifts in [0, 2 pad] (stream 6, per slice row if same_across_time else per image). */
+ * shifted by Philox integer shifts in [0, 2 pad] (stream 6, per slice row if same_across_time else per image);
+ * bilinear = the reference's aug.bilinear: 0 = grid_sample nearest (the exact integer gather), 1 = grid_sample
+ * bilinear's f32 arithmetic (neighbour weights of float-rounding size, bit-exact with torch's CPU kernel). */
 int sd_random_translate(const float* in, float* out, int B, int T, int H, int W, int C, int pad, uint64_t seed,
-                        const uint64_t* seed_ptr, long row_offset, int same_across_time, sd_stream stream);
+                        const uint64_t* seed_ptr, long row_offset, int same_across_time, int bilinear,
+                        sd_stream stream);
 
 /* Profiling aid: store the device wall clock (constant rate, sd_wall_clock_khz) into buf[idx] when `stream` reaches
  * this point; capturable into a HIP graph. Not part of the reference interface. */

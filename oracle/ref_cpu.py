@@ -16,6 +16,11 @@ import torch.nn.functional as F
 
 from . import noise as nz
 
+# arithmetic type of the restatement: float32 (the reference's) everywhere in the tests; tools/grad_attrib.py sets
+# float64 to get the exact-arithmetic answer the f32 results are each an approximation of (inputs that the reference
+# forms in f32 — images / 255, the augmentation's grid_sample, Philox noise — stay f32 values)
+DT = torch.float32
+
 # --------------------------------------------------------------------------------------------------------
 # distributions (world_model/distributions.py)
 # --------------------------------------------------------------------------------------------------------
@@ -31,9 +36,9 @@ def symexp(x):  # distributions.py:12-13
 
 def unimix_logits(logits, unimix):
     """OneHotDist.__init__ (distributions.py:17-22) + Categorical logit normalisation (torch)."""
-    probs = F.softmax(logits.float(), dim=-1)
+    probs = F.softmax(logits.to(DT), dim=-1)
     uniform = unimix / probs.shape[-1]
-    probs = probs * (1.0 - unimix) + torch.ones_like(probs, dtype=torch.float32) * uniform
+    probs = probs * (1.0 - unimix) + torch.ones_like(probs, dtype=DT) * uniform
     lg = torch.log(probs)
     return lg - lg.logsumexp(dim=-1, keepdim=True)
 
@@ -81,15 +86,15 @@ def kl_cat(left, right):  # distributions.py:266-271
 
 def twohot_bins(bin_num=255):  # distributions.py:242-251
     if bin_num % 2 == 1:
-        half = torch.linspace(-20, 0, (bin_num - 1) // 2 + 1, dtype=torch.float32)
+        half = torch.linspace(-20, 0, (bin_num - 1) // 2 + 1, dtype=DT)
         half = symexp(half)
         return torch.concatenate([half, -half[:-1].flip(dims=(0,))], 0)
-    half = symexp(torch.linspace(-20, 0, bin_num // 2, dtype=torch.float32))
+    half = symexp(torch.linspace(-20, 0, bin_num // 2, dtype=DT))
     return torch.concatenate([half, -half.flip(dims=(0,))], 0)
 
 
 def twohot_mode(logits, bins):  # TwoHot.mode, distributions.py:78-98
-    probs = F.softmax(logits.float(), dim=-1)
+    probs = F.softmax(logits.to(DT), dim=-1)
     n = logits.shape[-1]
     if n % 2 == 1:
         m = (n - 1) // 2
@@ -102,7 +107,7 @@ def twohot_mode(logits, bins):  # TwoHot.mode, distributions.py:78-98
 
 
 def twohot_log_prob(logits, bins, target):  # TwoHot.log_prob, distributions.py:100-129
-    logits = logits.float()
+    logits = logits.to(DT)
     target = target.squeeze(-1)
     ts = target.detach()
     nb = len(bins)
@@ -111,26 +116,26 @@ def twohot_log_prob(logits, bins, target):  # TwoHot.log_prob, distributions.py:
     below = torch.clamp(below, 0, nb - 1)
     above = torch.clamp(above, 0, nb - 1)
     equal = below == above
-    one = torch.tensor(1.0, dtype=torch.float32)
+    one = torch.tensor(1.0, dtype=DT)
     d_below = torch.where(equal, one, (bins[below] - ts).abs())
     d_above = torch.where(equal, one, (bins[above] - ts).abs())
     total = d_below + d_above
     w_below = d_above / total
     w_above = d_below / total
-    target_dist = (F.one_hot(below, nb).float() * w_below.unsqueeze(-1)
-                   + F.one_hot(above, nb).float() * w_above.unsqueeze(-1))
+    target_dist = (F.one_hot(below, nb).to(DT) * w_below.unsqueeze(-1)
+                   + F.one_hot(above, nb).to(DT) * w_above.unsqueeze(-1))
     log_pred = logits - torch.logsumexp(logits, dim=-1, keepdim=True)
     return (target_dist * log_pred).sum(-1)
 
 
 def bernoulli_log_prob(logits, value):  # torchd.Bernoulli(logits).log_prob, summed by Independent(…, 1)
-    return (-F.binary_cross_entropy_with_logits(logits.float(), value, reduction="none")).sum(-1)
+    return (-F.binary_cross_entropy_with_logits(logits.to(DT), value, reduction="none")).sum(-1)
 
 
 def bounded_normal_params(x, min_std, max_std):  # distributions.py:217-222
     mean, std = torch.chunk(x, 2, dim=-1)
     std = (max_std - min_std) * torch.sigmoid(std + 2.0) + min_std
-    return torch.tanh(mean.float()), std.float()
+    return torch.tanh(mean.to(DT)), std.to(DT)
 
 
 def normal_log_prob(loc, scale, value):  # torchd.Normal.log_prob, summed by Independent
@@ -357,8 +362,9 @@ def random_translate(img, shifts, pad, bilinear):
     """Dreamer.random_translate (dreamer.py:845-880) on (B, T, H, W, C) images with given integer shifts (B, T, 2)
     = (x, y) in [0, 2 pad]: out[y][x] = in[clamp(y + sy - pad)][clamp(x + sx - pad)]. The reference samples the
     replicate-padded image with grid_sample at exactly those pixel centres; bilinear mode does so through float
-    grid arithmetic, whose last-bit weights (|d| ~ 6e-8) are reproduced here so the oracle tracks the reference's
-    gradients to the golden tolerance. The HIP kernel performs the exact integer gather."""
+    grid arithmetic, whose last-bit weights (|d| ~ 6e-8) are reproduced here (torch's own grid_sample) so the oracle
+    tracks the reference's gradients to the golden tolerance. The HIP kernel restates that f32 arithmetic
+    (sd_random_translate, bilinear = 1) and is pinned bit-exact against this function."""
     B, T, H, W, C = img.shape
     x = F.pad(img.reshape(B * T, H, W, C).permute(0, 3, 1, 2), (pad, pad, pad, pad), mode="replicate")
     Hp, Wp = H + 2 * pad, W + 2 * pad
@@ -371,8 +377,8 @@ def random_translate(img, shifts, pad, bilinear):
     gx = torch.linspace(-1.0 + 1.0 / Wp, 1.0 - 1.0 / Wp, Wp)[:W]
     grid = torch.stack([gx[None, :].expand(H, W), gy[:, None].expand(H, W)], -1)[None]  # (1, H, W, 2): (x, y)
     off = shifts.reshape(B * T, 1, 1, 2).float() * 2.0 / torch.tensor([Wp, Hp], dtype=torch.float32)
-    out = F.grid_sample(x, grid + off, mode="bilinear", padding_mode="zeros", align_corners=False)
-    return out.permute(0, 2, 3, 1).reshape(B, T, H, W, C)
+    out = F.grid_sample(x.float(), grid + off, mode="bilinear", padding_mode="zeros", align_corners=False)
+    return out.permute(0, 2, 3, 1).reshape(B, T, H, W, C).to(img.dtype)
 
 
 class Oracle:
@@ -521,7 +527,7 @@ class Oracle:
         s = self.s
         data = {k: v.unsqueeze(1) for k, v in obs.items() if k != "is_first"}
         if "image" in data and data["image"].dtype == torch.uint8:
-            data["image"] = data["image"].float() / 255.0  # Dreamer.preprocess, dreamer.py:710-713
+            data["image"] = (data["image"].float() / 255.0).to(DT)  # Dreamer.preprocess, dreamer.py:710-713
         embed = self.encode(data)[:, 0]
         B = embed.shape[0]
         rs = obs["is_first"].reshape(B)
@@ -535,7 +541,7 @@ class Oracle:
         logits = self.head_logits("actor", self.get_feat(stoch, deter))
         if eval:
             if s.discrete:
-                action = F.one_hot(logits.argmax(-1), s.A).float()
+                action = F.one_hot(logits.argmax(-1), s.A).to(DT)
             else:
                 action = torch.tanh(logits[:, :s.A])
         else:
@@ -570,8 +576,8 @@ class Oracle:
 
 @torch.no_grad()
 def lambda_return(last, term, reward, value, boot, disc, lamb):  # Dreamer._lambda_return, dreamer.py:694-707
-    live = (1 - term.float())[:, 1:] * disc
-    cont = (1 - last.float())[:, 1:] * lamb
+    live = (1 - term.to(DT))[:, 1:] * disc
+    cont = (1 - last.to(DT))[:, 1:] * lamb
     interm = reward[:, 1:] + (1 - cont) * live * boot[:, 1:]
     out = [boot[:, -1]]
     for i in reversed(range(live.shape[1])):
@@ -580,7 +586,7 @@ def lambda_return(last, term, reward, value, boot, disc, lamb):  # Dreamer._lamb
 
 
 def return_ema(ema_vals, x, alpha=1e-2):  # ReturnEMA.__call__, networks.py:416-422 (mutates ema_vals)
-    q = torch.quantile(torch.flatten(x.detach()), torch.tensor([0.05, 0.95]))
+    q = torch.quantile(torch.flatten(x.detach()), torch.tensor([0.05, 0.95], dtype=x.dtype))
     ema_vals.copy_(alpha * q.detach() + (1 - alpha) * ema_vals)
     scale = torch.clip(ema_vals[1] - ema_vals[0], min=1.0)
     return ema_vals[0].detach(), scale.detach()
@@ -603,14 +609,14 @@ class OracleAgent:
         self.s = spec
         self.P = {}
         for k in spec.shapes:
-            self.P[k] = torch.tensor(params[k], dtype=torch.float32).requires_grad_(True)
+            self.P[k] = torch.tensor(params[k], dtype=DT).requires_grad_(True)
         for k, sk in spec.slow_names.items():
             v = params.get(sk, params[k])
-            self.P[sk] = torch.tensor(v, dtype=torch.float32)
+            self.P[sk] = torch.tensor(v, dtype=DT)
         for k, ek in spec.ema_names.items():  # DreamerPro's EMA encoder / projection (not trainable)
-            self.P[ek] = torch.tensor(params.get(ek, params[k]), dtype=torch.float32)
+            self.P[ek] = torch.tensor(params.get(ek, params[k]), dtype=DT)
         self.ema_updates = 0
-        self.ema_vals = torch.zeros(2, dtype=torch.float32)
+        self.ema_vals = torch.zeros(2, dtype=DT)
         self.model = Oracle(spec, self.P)
         c = spec.cfg
         self.lr0 = float(c.lr)
@@ -669,7 +675,7 @@ class OracleAgent:
             x = x.reshape(*BT, *x.shape[1:])
             splits = torch.split(x, [s.obs_shapes[k][-1] for k in s.dec_cnn_keys], -1)
             for k, mode in zip(s.dec_cnn_keys, splits):
-                dist = (mode.float() - data[k]) ** 2  # MSEDist(agg=sum), distributions.py:146-155
+                dist = (mode.to(DT) - data[k]) ** 2  # MSEDist(agg=sum), distributions.py:146-155
                 out[k] = torch.mean(dist.sum(list(range(dist.dim()))[2:]))
         if s.dec_mlp_keys:
             feat = torch.cat([post_stoch.reshape(*post_deter.shape[:-1], -1), post_deter], -1)
@@ -679,7 +685,7 @@ class OracleAgent:
                 x = F.silu(rms(F.linear(x, P[f"{pre}_linear{i}.weight"], P[f"{pre}_linear{i}.bias"]), P[f"{pre}_norm{i}.weight"]))
             x = F.linear(x, P["decoder._mlp.last.weight"], P["decoder._mlp.last.bias"])
             for k, mode in zip(s.dec_mlp_keys, torch.split(x, s.dec_mlp_split, -1)):
-                d = (mode.float() - symlog(data[k])) ** 2.0  # SymlogDist(mse, sum), distributions.py:174-190
+                d = (mode.to(DT) - symlog(data[k])) ** 2.0  # SymlogDist(mse, sum), distributions.py:174-190
                 d = torch.where(d < 1e-8, 0, d)
                 out[k] = torch.mean(d.sum(list(range(d.dim()))[2:]))
         return out
@@ -745,8 +751,8 @@ class OracleAgent:
             losses.update(self.proto_loss(ps_aug, pd_aug, embed_aug, ema))
         else:
             raise NotImplementedError(s.rep_loss)
-        losses["rew"] = torch.mean(-twohot_log_prob(M.head_logits("reward", feat), M.rbins, data["reward"].float()))
-        cont = 1.0 - data["is_terminal"].float()
+        losses["rew"] = torch.mean(-twohot_log_prob(M.head_logits("reward", feat), M.rbins, data["reward"].to(DT)))
+        cont = 1.0 - data["is_terminal"].to(DT)
         losses["con"] = torch.mean(-bernoulli_log_prob(M.head_logits("cont", feat), cont))
         metrics["dyn_entropy"] = torch.mean(cat_entropy(unimix_logits(prior_logit, s.unimix)).sum(-1))
         metrics["rep_entropy"] = torch.mean(cat_entropy(unimix_logits(post_logit, s.unimix)).sum(-1))
@@ -758,7 +764,7 @@ class OracleAgent:
         imag_feat, imag_action = M.imagine(start, H1, seed, row_offset * T, rec)
         imag_feat, imag_action = imag_feat.detach(), imag_action.detach()
         imag_reward = twohot_mode(M.head_logits("reward", imag_feat, Pd), M.rbins)
-        imag_cont = torch.sigmoid(M.head_logits("cont", imag_feat, Pd).float())  # Bernoulli.mean
+        imag_cont = torch.sigmoid(M.head_logits("cont", imag_feat, Pd).to(DT))  # Bernoulli.mean
         imag_value = twohot_mode(M.head_logits("value", imag_feat, Pd), M.bins)
         imag_slow_value = twohot_mode(M.head_logits("slow_value", imag_feat, Pd), M.bins)
         disc = 1 - 1 / int(c.horizon)
@@ -799,7 +805,7 @@ class OracleAgent:
         metrics.update(tensorstats(imag_action, "action"))
 
         # replay value (dreamer.py:638-664)
-        last, term, reward = data["is_last"].float(), data["is_terminal"].float(), data["reward"].float()
+        last, term, reward = data["is_last"].to(DT), data["is_terminal"].to(DT), data["reward"].to(DT)
         boot = ret[:, 0].reshape(B, T, 1)
         value = twohot_mode(M.head_logits("value", feat, Pd), M.bins)
         slow_value = twohot_mode(M.head_logits("slow_value", feat, Pd), M.bins)

@@ -649,15 +649,36 @@ extern "C" int sd_replay_slices(const sd_slice_keys* keys, const int64_t* starts
 }
 
 // ---- r2dreamer image augmentation (Dreamer._augment_images / random_translate, dreamer.py:716-729,845-880):
-// replicate-pad by `pad`, shift by an integer (sx, sy) in [0, 2 pad] per slice (same_across_time) or per image, i.e.
-// out[y][x] = in[clamp(y + sy - pad)][clamp(x + sx - pad)] — the reference's grid_sample samples exactly those
-// pixel centres (its grid is built on them; bilinear weights are 1/0 up to float rounding). Shifts from Philox
-// (SD_STREAM_AUG, step 0): index (row * 2 + axis) or ((row * T + t) * 2 + axis), axis 0 = x, 1 = y; row = global
-// slice row (row_offset + b).
+// replicate-pad by `pad`, shift by an integer (sx, sy) in [0, 2 pad] per slice (same_across_time) or per image.
+// Shifts from Philox (SD_STREAM_AUG, step 0): index (row * 2 + axis) or ((row * T + t) * 2 + axis), axis 0 = x,
+// 1 = y; row = global slice row (row_offset + b).
+//   nearest (aug.bilinear False): out[y][x] = in[clamp(y + sy - pad)][clamp(x + sx - pad)], the pixel centres the
+//     reference's grid lands on;
+//   bilinear (aug.bilinear True, the default): the reference's F.grid_sample(bilinear, zeros, align_corners False)
+//     arithmetic restated in f32 — the linspace grid (fma(step, k, start) below half, fma(-step, n-1-k, end) above),
+//     + shift * 2 / padded size, unnormalised as fma(g + 1, size / 2, -0.5), corner weights from floor, and the
+//     four corners accumulated as one fma chain (nw first). The grid misses the pixel centres by float rounding,
+//     so weights of ~6e-8 mix in the neighbours; the restatement reproduces them bit for bit (torch CPU, pinned by
+//     tests/test_gpu_ops.py::test_random_translate_bilinear_matches_grid_sample). The Barlow targets are
+//     sensitive enough to those last bits that the first conv layer's gradient moves visibly without them.
 namespace {
+// torch.linspace(-1 + 1/n, 1 - 1/n, n)[k] in f32 (CPU kernel: f32 step, fma from the nearer end)
+SD_DEV float grid_coord(int n, int k) {
+  const float start = (float)(-1.0 + 1.0 / n), end = (float)(1.0 - 1.0 / n);
+  const float step = __fdiv_rn(__fsub_rn(end, start), (float)(n - 1));
+  return k < n / 2 ? __builtin_fmaf(step, (float)k, start) : __builtin_fmaf(-step, (float)(n - 1 - k), end);
+}
+
+// padded-image pixel (zeros outside the padded frame, replicate edges inside)
+SD_DEV float padded_px(const float* img, int H, int W, int C, int pad, int yp, int xp, int c) {
+  if (yp < 0 || yp >= H + 2 * pad || xp < 0 || xp >= W + 2 * pad) return 0.f;
+  const int yy = min(max(yp - pad, 0), H - 1), xx = min(max(xp - pad, 0), W - 1);
+  return img[((long)yy * W + xx) * C + c];
+}
+
 __global__ void random_translate_kernel(const float* __restrict__ in, float* __restrict__ out, int N, int T, int H,
                                         int W, int C, int pad, uint64_t seed, const uint64_t* seed_ptr,
-                                        long row_offset, int same_across_time) {
+                                        long row_offset, int same_across_time, int bilinear) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)N * H * W * C;
   if (i >= total) return;
@@ -672,19 +693,37 @@ __global__ void random_translate_kernel(const float* __restrict__ in, float* __r
   const uint64_t base = same_across_time ? (uint64_t)(row_offset + b) * 2 : ((uint64_t)(row_offset + b) * T + t) * 2;
   const int sx = sd_uniform_int(sd, SD_STREAM_AUG, 0, base, 2 * pad + 1);
   const int sy = sd_uniform_int(sd, SD_STREAM_AUG, 0, base + 1, 2 * pad + 1);
-  const int yy = min(max(y + sy - pad, 0), H - 1), xx = min(max(x + sx - pad, 0), W - 1);
-  out[i] = in[(((long)n * H + yy) * W + xx) * C + c];
+  const float* img = in + (long)n * H * W * C;
+  if (!bilinear) {
+    const int yy = min(max(y + sy - pad, 0), H - 1), xx = min(max(x + sx - pad, 0), W - 1);
+    out[i] = img[((long)yy * W + xx) * C + c];
+    return;
+  }
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  const float gx = __fadd_rn(grid_coord(Wp, x), __fdiv_rn((float)sx * 2.f, (float)Wp));
+  const float gy = __fadd_rn(grid_coord(Hp, y), __fdiv_rn((float)sy * 2.f, (float)Hp));
+  const float ix = __builtin_fmaf(__fadd_rn(gx, 1.f), (float)Wp * 0.5f, -0.5f);
+  const float iy = __builtin_fmaf(__fadd_rn(gy, 1.f), (float)Hp * 0.5f, -0.5f);
+  const float x0 = floorf(ix), y0 = floorf(iy);
+  const float we = __fsub_rn(ix, x0), ww = __fsub_rn(1.f, we), ws = __fsub_rn(iy, y0), wn = __fsub_rn(1.f, ws);
+  const int xi = (int)x0, yi = (int)y0;
+  const float nw = padded_px(img, H, W, C, pad, yi, xi, c), ne = padded_px(img, H, W, C, pad, yi, xi + 1, c);
+  const float sw = padded_px(img, H, W, C, pad, yi + 1, xi, c), se = padded_px(img, H, W, C, pad, yi + 1, xi + 1, c);
+  float v = __fmul_rn(nw, __fmul_rn(wn, ww));
+  v = __builtin_fmaf(ne, __fmul_rn(wn, we), v);
+  v = __builtin_fmaf(sw, __fmul_rn(ws, ww), v);
+  out[i] = __builtin_fmaf(se, __fmul_rn(ws, we), v);
 }
 }  // namespace
 
 extern "C" int sd_random_translate(const float* in, float* out, int B, int T, int H, int W, int C, int pad,
                                    uint64_t seed, const uint64_t* seed_ptr, long row_offset, int same_across_time,
-                                   sd_stream s) {
+                                   int bilinear, sd_stream s) {
   const long total = (long)B * T * H * W * C;
   if (total <= 0) return SD_OK;
   if (pad < 0) return SD_EARG;
   random_translate_kernel<<<nb(total), 256, 0, (hipStream_t)s>>>(in, out, B * T, T, H, W, C, pad, seed, seed_ptr,
-                                                                 row_offset, same_across_time);
+                                                                 row_offset, same_across_time, bilinear);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

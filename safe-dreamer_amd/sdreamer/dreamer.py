@@ -165,14 +165,15 @@ class Dreamer(nn.Module):
             self.barlow_lambd = float(config.r2dreamer.lambd)
             aug = config.r2dreamer.aug
             # Barlow target from a translated view (dreamer.py:506-520): (pad, same_across_time) or None
-            self.r2_aug = (int(aug.max_delta), bool(aug.same_across_time)) if \
+            self.r2_aug = (int(aug.max_delta), bool(aug.same_across_time), bool(aug.get("bilinear", False))) if \
                 (self.rep_loss == "r2dreamer" and bool(aug.enabled)) else None
         elif self.rep_loss == "dreamerpro":  # dreamer.py:131-162
             dpc = config.dreamer_pro
             self._pro = dict(warm_up=int(dpc.warm_up), tau=float(dpc.temperature), eps=float(dpc.sinkhorn_eps),
                              iters=int(dpc.sinkhorn_iters), every=int(dpc.ema_update_every),
                              frac=float(dpc.ema_update_fraction), freeze=int(dpc.freeze_prototypes_iters),
-                             pad=int(dpc.aug.max_delta), same=bool(dpc.aug.same_across_time))
+                             pad=int(dpc.aug.max_delta), same=bool(dpc.aug.same_across_time),
+                             bilinear=bool(dpc.aug.get("bilinear", False)))
             self._prototypes = nn.Parameter(torch.randn(int(dpc.num_prototypes), int(dpc.proto_dim)))
             self.obs_proj = Linear(self.embed_size, int(dpc.proto_dim))
             self.feat_proj = Linear(self.rssm.feat_size, int(dpc.proto_dim))
@@ -960,9 +961,9 @@ class Dreamer(nn.Module):
             x1 = self.prj(feat.reshape(B * T, -1))
             if self.r2_aug is not None:  # encoder on a randomly translated view, no gradient (dreamer.py:506-520)
                 with torch.no_grad():
-                    pad, same = self.r2_aug
+                    pad, same, bil = self.r2_aug
                     aug = dict(data)
-                    aug["image"] = K.random_translate(data["image"], pad, seed, ro, same)
+                    aug["image"] = K.random_translate(data["image"], pad, seed, ro, same, bil)
                     x2 = self.encoder(aug).reshape(B * T, -1)
             else:
                 x2 = embed.reshape(B * T, -1).detach()
@@ -988,8 +989,8 @@ class Dreamer(nn.Module):
         with torch.no_grad():
             aug = {k: torch.cat([v, v], 0) for k, v in data.items()}
             img = data["image"]
-            aug["image"] = torch.cat([K.random_translate(img, c["pad"], seed, ro, c["same"]),
-                                      K.random_translate(img, c["pad"], seed, Bg + ro, c["same"])], 0)
+            aug["image"] = torch.cat([K.random_translate(img, c["pad"], seed, ro, c["same"], c["bilinear"]),
+                                      K.random_translate(img, c["pad"], seed, Bg + ro, c["same"], c["bilinear"])], 0)
             ema = self._ema_obs_proj(self._ema_encoder(aug))
             ema = ema / ema.norm(dim=-1, keepdim=True).clamp_min(1e-12)
         embed = self.encoder(aug)

@@ -572,14 +572,15 @@ def conv_flip_weight(w):
     return wf
 
 
-def random_translate(img, pad, seed, row_offset=0, same_across_time=True):
+def random_translate(img, pad, seed, row_offset=0, same_across_time=True, bilinear=True):
     """Dreamer.random_translate (dreamer.py:845-880) on preprocessed (B, T, H, W, C) f32 images (NHWC, as the
-    reference permutes back): replicate pad + Philox integer shift per slice row (or per image)."""
+    reference permutes back): replicate pad + Philox integer shift per slice row (or per image), sampled like the
+    reference's grid_sample (bilinear: its f32 grid arithmetic, bit-exact with torch's CPU kernel; else nearest)."""
     B, T, H, W, C = img.shape
     out = torch.empty_like(img)
     sh, sp = seed_args(seed)
     nat.call("sd_random_translate", p(_c(img)), p(out), B, T, H, W, C, int(pad), sh, sp, int(row_offset),
-             int(bool(same_across_time)), stream())
+             int(bool(same_across_time)), int(bool(bilinear)), stream())
     return out
 
 

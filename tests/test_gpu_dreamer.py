@@ -82,6 +82,9 @@ class _OracleRun:
         return self.keeps[u]
 
 
+F64_BOUND = 0.1  # fraction of the golden's m / v bounds the product may use against the float64 moments
+
+
 def _opt_samples(ag, spec):
     """name -> (exp_avg, exp_avg_sq) sampled like the golden u*_st_* (LaProp state index i = _named_params[i])."""
     sd = ag._optimizer.state_dict()["state"]
@@ -107,7 +110,9 @@ def test_update_matches_reference(name):
     _, _, _, params0, _ = load_case(name)
     prev = {k: params0[k].reshape(-1)[sample_idx(k, params0[k].size)] for k in spec.shapes}
     report = {}
-    bounds = {}
+    bounds, bounds64 = {}, {}
+    f64p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "f64", f"{name}.npz")
+    f64 = np.load(f64p) if os.path.exists(f64p) else None
     for u in range(2):
         seed = int(z[f"u{u}_seed"])
         data = batch(z, u, obs, DEV)
@@ -180,6 +185,23 @@ def test_update_matches_reference(name):
         # a flipped step sign (2x), a skipped AGC clip (1/scale^2 in v) or a skipped Polyak still fail
         # (tools/sabotage_optim.sh).
         opt = _opt_samples(ag, spec)
+        # distance from EXACT arithmetic: the float64 moments of the same update (tests/golden/gen_f64_moments.py).
+        # The golden (the reference's own f32 run) sits up to 0.50 of the bounds above from them (walker_r2aug's
+        # first conv layer, tools/grad_attrib.py); the product must stay within F64_BOUND of them
+        if f64 is not None:
+            for k in spec.shapes:
+                m, v = opt[k]
+                m64, v64 = f64[f"u{u}_{k}__m"], f64[f"u{u}_{k}__v"]
+                tiny64 = np.sqrt(v64) < 1e-3 * np.sqrt(v64).max()
+                for what, br in (("v", bound_ratio(v, v64, 2e-2, 2e-4 * np.abs(v64).max() + 1e-30)),
+                                 ("m", bound_ratio(m, m64, 2e-2, 1e-2 * np.abs(m64).max() + 1e-30, mask=tiny64))):
+                    if br > bounds64.get(what, ("", 0.0))[1]:
+                        bounds64[what] = (k, br)
+        if os.environ.get("SDREAMER_DUMP_OPT"):  # sampled LaProp moments, for tools/grad_attrib.py
+            d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "golden")
+            os.makedirs(d, exist_ok=True)
+            np.savez(os.path.join(d, f"{name}_opt_u{u}.npz"),
+                     **{f"{k}__{w}": a for k, (m_, v_) in opt.items() for w, a in (("m", m_), ("v", v_))})
         sd = ag.state_dict()
         worst = 0.0
         for k in spec.shapes:
@@ -212,6 +234,8 @@ def test_update_matches_reference(name):
             ref = z[f"u{u}_p_{sk}__s"]
             assert_close(flat[sample_idx(sk, flat.size)], ref, 0.0, 4 * ulp(ref) + 1e-12, f"u{u} slow critic {sk}")
     report["bound_ratio"] = {k: {"tensor": t, "ratio": r} for k, (t, r) in bounds.items()}
+    report["bound_ratio_f64"] = {k: {"tensor": t, "ratio": r} for k, (t, r) in bounds64.items()}
+    assert all(r <= F64_BOUND for _, r in bounds64.values()), ("moments vs exact arithmetic", bounds64)
     print(name, report)
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "golden")
     os.makedirs(out, exist_ok=True)

@@ -45,11 +45,26 @@ def test_random_translate_bit_exact(same):
     from sdreamer import kernels as K
     B, T, H, W, C, pad, seed, ro = 3, 4, 16, 12, 3, 3, 4242, 5
     img = torch.rand(B, T, H, W, C, generator=_g(3))
-    out = K.random_translate(img.to(DEV), pad, seed, ro, same).cpu()
+    out = K.random_translate(img.to(DEV), pad, seed, ro, same, bilinear=False).cpu()
     sh = torch.from_numpy(nz.aug_shifts(seed, B, ro, T, pad, same))
     assert torch.equal(out, R.random_translate(img, sh, pad, False))
     if same:
         assert (sh == sh[:, :1]).all()
+
+
+@pytest.mark.parametrize("H,W,C,pad", [(64, 64, 3, 3), (64, 64, 3, 4), (9, 7, 2, 3), (32, 32, 1, 2)])
+def test_random_translate_bilinear_matches_grid_sample(H, W, C, pad):
+    """aug.bilinear (the config default): sd_random_translate restates F.grid_sample(bilinear, zeros, align_corners
+    False) on the replicate-padded image with the reference's linspace grid + shift (dreamer.py:845-880); the
+    oracle runs torch's own CPU grid_sample. Bit-exact, including the ~6e-8 neighbour weights of the float grid."""
+    from sdreamer import kernels as K
+    B, T, seed, ro = 4, 5, 777, 3
+    img = (torch.randint(0, 256, (B, T, H, W, C), generator=_g(H + pad)).float() / 255.0)
+    out = K.random_translate(img.to(DEV), pad, seed, ro, False, bilinear=True).cpu()
+    sh = torch.from_numpy(nz.aug_shifts(seed, B, ro, T, pad, False))
+    ref = R.random_translate(img, sh, pad, True)
+    assert torch.equal(out, ref), (out - ref).abs().max()
+    assert not torch.equal(ref, R.random_translate(img, sh, pad, False))  # the neighbour weights do mix in
 
 
 @pytest.mark.parametrize("M,N", [(7, 256), (1024, 256), (33, 2048), (5, 4096), (100, 48), (64, 32), (3, 512)])

@@ -102,3 +102,22 @@ def test_random_translate_restatement():
     big = nz.aug_shifts(1, 4096, 0, 1, pad, True)
     assert big.min() == 0 and big.max() == 2 * pad
     assert np.abs(np.bincount(big.reshape(-1), minlength=2 * pad + 1) / big.size - 1 / (2 * pad + 1)).max() < 0.02
+
+
+def test_f64_moments_fixture_reproduces():
+    """tests/golden/f64/*.npz (the exact-arithmetic LaProp moments the GPU test bounds the product against) come from
+    tests/golden/gen_f64_moments.py: regenerate one case and compare; the float32 run of the same oracle stays within
+    the golden's tolerance of the golden (it is the reference's arithmetic)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from gen_f64_moments import moments
+    name = "walker_r2"
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "f64", f"{name}.npz"))
+    torch.set_num_threads(8)
+    res = moments(name, torch.float64)
+    assert [f for _, f in res] == [0, 0]
+    for u, (mom, _) in enumerate(res):
+        for k, (m, v) in mom.items():
+            np.testing.assert_allclose(m, fx[f"u{u}_{k}__m"], rtol=1e-9, atol=1e-15)
+            np.testing.assert_allclose(v, fx[f"u{u}_{k}__v"], rtol=1e-9, atol=1e-20)
