@@ -125,7 +125,8 @@ int sd_onehot_logp_ent_fwd(const float* logits, const float* action, float* logp
 int sd_onehot_logp_ent_bwd(const float* logits, const float* action, const float* glogp, const float* gent,
                            float* dlogits, long rows, int K, float unimix, sd_stream stream);
 /* KL(post || prior) on raw logits summed over S per row (dists.kl + RSSM.kl_loss sum, rssm.py:222-230) */
-int sd_kl_fwd(const float* post, const float* prior, float* kl_row, int rows, int S, int K, sd_stream stream);
+int sd_kl_fwd(const float* post, const float* prior, float* kl_row, float* dyn, float* rep, float free_nats, int rows,
+              int S, int K, sd_stream stream);
 /* gradients of clip(kl_row, min=free): d_post <- g_rep * pa (lpa - lpb - kl_s), d_prior <- g_dyn * (pb - pa) */
 int sd_kl_bwd(const float* post, const float* prior, const float* kl_row, const float* g_rep, const float* g_dyn,
               float free_nats, float* d_post, float* d_prior, int rows, int S, int K, int acc_post, int acc_prior,
@@ -139,24 +140,28 @@ int sd_twohot_logp_fwd(const float* logits, const float* bins, const float* targ
 int sd_twohot_logp_bwd(const float* logits, const float* bins, const float* target, const float* glogp,
                        float* dlogits, long rows, int NB, int accumulate, sd_stream stream);
 /* Replay-value loss (dreamer.py:652-658; replaces the two TwoHot.log_prob calls, distributions.py:100-129, and the
- * weighted mean's elementwise ops): row_loss[r] = w[r] * (-logp(ret[r]) - logp(slow[r])); the backward writes the
- * logits gradient of mean(row_loss) * gscale[0] (device scalar), inv_n = 1 / rows. NB <= 256. */
-int sd_repval_loss_fwd(const float* logits, const float* bins, const float* ret, const float* slow, const float* w,
-                       float* row_loss, long rows, int NB, sd_stream s);
-int sd_repval_loss_bwd(const float* logits, const float* bins, const float* ret, const float* slow, const float* w,
-                       const float* gscale, float inv_n, float* dlogits, long rows, int NB, sd_stream s);
+ * weighted mean's elementwise ops). The value head ran on all Tl posterior steps of B rows: logits (B, Tl, NB),
+ * slow / last (B, Tl); the Tr = Tl - 1 steps with a replay return ret (B, Tr) are the loss rows:
+ * row_loss[b, t] = (1 - last[b, t]) * (-logp(ret[b, t]) - logp(slow[b, t])). The backward writes the gradient of
+ * mean(row_loss) * gscale[0] (device scalar; inv_n = 1 / (B Tr)) for every (B, Tl) logits row (zero for t >= Tr).
+ * NB <= 256. */
+int sd_repval_loss_fwd(const float* logits, const float* bins, const float* ret, const float* slow, const float* last,
+                       float* row_loss, int B, int Tl, int Tr, int NB, sd_stream s);
+int sd_repval_loss_bwd(const float* logits, const float* bins, const float* ret, const float* slow, const float* last,
+                       const float* gscale, float inv_n, float* dlogits, int B, int Tl, int Tr, int NB, sd_stream s);
 /* Imagined actor-critic losses (dreamer.py:623-636, 653-671) over H * N time-major rows r = t * N + n: value logits
  * vl (H * N, NB), logpi / ent (H * N) of the imagined actions, slow (H * N) slow-value targets; batch-major
  * ret (N, H), w = weight (N, H1), val = imagined value (H1, N) time-major; scale: device scalar (ReturnEMA scale).
  * fwd writes adv (N, H) = (ret - val[:, :H]) / scale and the row terms rows_v = w (-logp(ret) - logp(slow)),
  * rows_p = w -(logpi adv + coef ent) (H * N each; the losses are their means). bwd: d vl, d logpi, d ent from the
- * upstream gradients of the two means (device scalars gpolicy / gvalue, null = 0). */
+ * upstream gradients of the two means: device scalars gpolicy / gvalue (null = 0) times spolicy / svalue (the loss
+ * scales, so both can point at the gradient of the weighted total). */
 int sd_imag_ac_loss_fwd(const float* vl, const float* bins, const float* ret, const float* slow, const float* w,
                         const float* val, const float* scale, const float* logpi, const float* ent, float coef, long N,
                         int H, int H1, int NB, float* rows_v, float* rows_p, float* adv, sd_stream s);
 int sd_imag_ac_loss_bwd(const float* vl, const float* bins, const float* ret, const float* slow, const float* w,
-                        const float* adv, const float* gpolicy, const float* gvalue, float coef, long N, int H, int H1,
-                        int NB, float* dvl, float* dlogpi, float* dent, sd_stream s);
+                        const float* adv, const float* gpolicy, const float* gvalue, float spolicy, float svalue,
+                        float coef, long N, int H, int H1, int NB, float* dvl, float* dlogpi, float* dent, sd_stream s);
 /* bounded normal actor (bounded_normal, distributions.py:217-222): x (rows, 2A) = [mean | std-logit] */
 int sd_bnormal_sample(const float* x, float* action, long rows, int A, float min_std, float max_std, uint64_t seed,
                       int stream_id, int step, long row_offset, const uint64_t* seed_ptr, sd_stream stream);
@@ -313,12 +318,52 @@ typedef struct sd_stat_req {
   int kind, out;
   float scale;
   int chunk0;
+  const float* sub; /* nullable device scalars: the stat becomes (stat - sub[0]) / div[0] before the scale */
+  const float* div;
 } sd_stat_req;
 typedef struct sd_stats {
   sd_stat_req r[SD_MAX_STATS];
   int nreq;
 } sd_stats;
 int sd_multi_stats(const sd_stats* s, float* workspace, float* out, int nout, sd_stream stream);
+
+/* World-model loss total (dreamer.py:571-576, `sum(v * self._scales[k] for k, v in losses.items())`): term i is
+ * coef_i * mean(x_i[0:n_i]) (coef = -1 for the log-prob losses), total = sum_i scale_i * term_i in term order;
+ * means (n terms, nullable) and total (1) on device. Backward: g_i[j] = (g_total * scale_i + g_means[i]) * coef_i / n_i
+ * into each term's g (nullable = no gradient; g_total / g_means nullable = 0). One launch each way. */
+#define SD_MAX_LOSS_TERMS 8
+typedef struct sd_loss_term {
+  const float* x;
+  float* g;
+  long n;
+  float coef, scale;
+} sd_loss_term;
+typedef struct sd_loss_terms {
+  sd_loss_term t[SD_MAX_LOSS_TERMS];
+  int n;
+} sd_loss_terms;
+int sd_loss_terms_fwd(const sd_loss_terms* terms, float* means, float* total, sd_stream stream);
+int sd_loss_terms_bwd(const sd_loss_terms* terms, const float* g_total, const float* g_means, sd_stream stream);
+
+/* Layout copies in one launch (the scan backward's W^T images, rssm.py:36-75 contractions transposed; the first
+ * conv layer's channel pad; get_feat's concatenation into a strided slot): mode 0 transposes src (batch, rows, cols;
+ * row stride sr, batch stride sb) into dst (batch, cols, rows) contiguous; mode 1 copies it into dst rows
+ * (batch * rows of stride dld, 0 = dcols) of dcols values, zero-filling columns >= cols. */
+#define SD_MAX_LAYOUT_COPIES 12
+typedef struct sd_layout_copy {
+  const float* src;
+  float* dst;
+  long sb, sr, dld;
+  int batch, rows, cols, dcols, mode;
+} sd_layout_copy;
+typedef struct sd_layout_copies {
+  sd_layout_copy e[SD_MAX_LAYOUT_COPIES];
+  int n;
+} sd_layout_copies;
+int sd_layout_copies_run(const sd_layout_copies* copies, sd_stream stream);
+/* is_last / is_terminal bytes (n) -> f32 last, term, cont = 1 - term (the losses' episode-boundary operands) */
+int sd_episode_flags(const uint8_t* is_last, const uint8_t* is_term, long n, float* last, float* term, float* cont,
+                     sd_stream stream);
 
 /* ---------------------------------------------------------------- misc
  * Measurement aid: one empty dispatch (kernel k_trace_mark, `tag` workgroups, 1 <= tag <= 64) that a rocprofv3 kernel

@@ -124,7 +124,7 @@ __global__ void onehot_logp_ent_bwd(const float* __restrict__ logits, const floa
 // ---------------------------------------------------------------- KL (raw logits) summed over S, per row
 template <int T>
 __global__ void kl_fwd(const float* __restrict__ post, const float* __restrict__ prior, float* __restrict__ kl_row,
-                       int rows, int S, int K) {
+                       float* __restrict__ dyn, float* __restrict__ rep, float free_nats, int rows, int S, int K) {
   __shared__ float red[4];
   const int teams = 256 / T;
   const int team = threadIdx.x / T, lt = threadIdx.x % T;
@@ -143,7 +143,12 @@ __global__ void kl_fwd(const float* __restrict__ post, const float* __restrict__
       if (lt == 0) acc += kg;
     }
     const float tot = block_sum<256>(acc, red);
-    if (threadIdx.x == 0) kl_row[r] = tot;
+    if (threadIdx.x == 0) {
+      kl_row[r] = tot;
+      const float cl = tot < free_nats ? free_nats : tot;  // torch.clamp(min=free): NaN stays NaN
+      if (dyn) dyn[r] = cl;
+      if (rep) rep[r] = cl;
+    }
     __syncthreads();
   }
 }
@@ -298,43 +303,56 @@ __global__ void twohot_logp_bwd(const float* __restrict__ logits, const float* _
 // logits (distributions.py:100-129), and its logits gradient for a given d loss / d term (one wave per row). The
 // backward is the sum of the two twohot_logp_bwd terms in one pass: g (td_ret + td_slow - p (tsum_ret + tsum_slow)),
 // g = -w[r] * gscale[0] * inv_n (gscale: device scalar, d total / d mean).
+// replay-value rows (dreamer.py:638-658): loss row r = (b, t < Tr) reads logits / slow / last row b * Tl + t (the value
+// head ran on all Tl posterior steps; Tr = Tl - 1 of them have a return) and ret[r]; weight = 1 - last.
 __global__ void repval_fwd_kernel(const float* __restrict__ logits, const float* __restrict__ bins,
                                   const float* __restrict__ ret, const float* __restrict__ slow,
-                                  const float* __restrict__ w, float* __restrict__ row_loss, long rows, int NB) {
+                                  const float* __restrict__ last, float* __restrict__ row_loss, long rows, int Tl,
+                                  int Tr, int NB) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long r = (long)blockIdx.x * 4 + wave;
   if (r >= rows) return;
-  const float* l = logits + r * NB;
+  const long lr_ = (r / Tr) * Tl + r % Tr;
+  const float* l = logits + lr_ * NB;
   float p[4], lse;
   row_softmax64(l, NB, p, lse, lane);
   int b1, a1, b2, a2;
   float wb1, wa1, wb2, wa2;
   twohot_target(bins, NB, ret[r], b1, a1, wb1, wa1, lane);
-  twohot_target(bins, NB, slow[r], b2, a2, wb2, wa2, lane);
+  twohot_target(bins, NB, slow[lr_], b2, a2, wb2, wa2, lane);
   if (lane == 0) {
     float lr = wb1 * (l[b1] - lse);
     lr += wa1 * (l[a1] - lse);
     float ls = wb2 * (l[b2] - lse);
     ls += wa2 * (l[a2] - lse);
-    row_loss[r] = w[r] * (-lr - ls);
+    row_loss[r] = (1.f - last[lr_]) * (-lr - ls);
   }
 }
 
+// d logits of the mean of the rows above, for all B * Tl logits rows (zero on the rows without a return)
 __global__ void repval_bwd_kernel(const float* __restrict__ logits, const float* __restrict__ bins,
                                   const float* __restrict__ ret, const float* __restrict__ slow,
-                                  const float* __restrict__ w, const float* __restrict__ gscale, float inv_n,
-                                  float* __restrict__ dlogits, long rows, int NB) {
+                                  const float* __restrict__ last, const float* __restrict__ gscale, float inv_n,
+                                  float* __restrict__ dlogits, long lrows, int Tl, int Tr, int NB) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const long r = (long)blockIdx.x * 4 + wave;
-  if (r >= rows) return;
-  const float* l = logits + r * NB;
+  const long lr_ = (long)blockIdx.x * 4 + wave;
+  if (lr_ >= lrows) return;
+  const int t = (int)(lr_ % Tl);
+  if (t >= Tr) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (lane + 64 * j < NB) dlogits[lr_ * NB + lane + 64 * j] = 0.f;
+    return;
+  }
+  const long r = (lr_ / Tl) * Tr + t;
+  const float* l = logits + lr_ * NB;
   float p[4], lse;
   row_softmax64(l, NB, p, lse, lane);
   int b1, a1, b2, a2;
   float wb1, wa1, wb2, wa2;
   twohot_target(bins, NB, ret[r], b1, a1, wb1, wa1, lane);
-  twohot_target(bins, NB, slow[r], b2, a2, wb2, wa2, lane);
-  const float g = -w[r] * (gscale[0] * inv_n);
+  twohot_target(bins, NB, slow[lr_], b2, a2, wb2, wa2, lane);
+  const float g = -(1.f - last[lr_]) * (gscale[0] * inv_n);
   const float t1 = wb1 + wa1, t2 = wb2 + wa2;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -342,7 +360,7 @@ __global__ void repval_bwd_kernel(const float* __restrict__ logits, const float*
     if (c < NB) {
       const float td1 = (c == b1 ? wb1 : 0.f) + (c == a1 ? wa1 : 0.f);
       const float td2 = (c == b2 ? wb2 : 0.f) + (c == a2 ? wa2 : 0.f);
-      dlogits[r * NB + c] = g * (td1 - p[j] * t1) + g * (td2 - p[j] * t2);
+      dlogits[lr_ * NB + c] = g * (td1 - p[j] * t1) + g * (td2 - p[j] * t2);
     }
   }
 }
@@ -386,9 +404,9 @@ __global__ void imag_ac_fwd_kernel(const float* __restrict__ vl, const float* __
 __global__ void imag_ac_bwd_kernel(const float* __restrict__ vl, const float* __restrict__ bins,
                                    const float* __restrict__ ret, const float* __restrict__ slow,
                                    const float* __restrict__ w, const float* __restrict__ adv,
-                                   const float* __restrict__ gp, const float* __restrict__ gv, float coef, float inv_n,
-                                   long N, int H, int H1, int NB, float* __restrict__ dvl, float* __restrict__ dlogpi,
-                                   float* __restrict__ dent) {
+                                   const float* __restrict__ gp, const float* __restrict__ gv, float sp, float sv,
+                                   float coef, float inv_n, long N, int H, int H1, int NB, float* __restrict__ dvl,
+                                   float* __restrict__ dlogpi, float* __restrict__ dent) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long r = (long)blockIdx.x * 4 + wave;
   if (r >= N * H) return;
@@ -402,7 +420,7 @@ __global__ void imag_ac_bwd_kernel(const float* __restrict__ vl, const float* __
   twohot_target(bins, NB, ret[n * H + t], b1, a1, wb1, wa1, lane);
   twohot_target(bins, NB, slow[r], b2, a2, wb2, wa2, lane);
   const float wt = w[n * H1 + t];
-  const float g = -wt * ((gv ? gv[0] : 0.f) * inv_n);
+  const float g = -wt * ((gv ? gv[0] * sv : 0.f) * inv_n);
   const float t1 = wb1 + wa1, t2 = wb2 + wa2;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -414,7 +432,7 @@ __global__ void imag_ac_bwd_kernel(const float* __restrict__ vl, const float* __
     }
   }
   if (lane == 0) {
-    const float gg = -wt * ((gp ? gp[0] : 0.f) * inv_n);
+    const float gg = -wt * ((gp ? gp[0] * sp : 0.f) * inv_n);
     dlogpi[r] = gg * adv[n * H + t];
     dent[r] = gg * coef;
   }
@@ -598,12 +616,13 @@ extern "C" int sd_onehot_logp_ent_bwd(const float* logits, const float* action, 
   return SD_OK;
 }
 
-extern "C" int sd_kl_fwd(const float* post, const float* prior, float* kl_row, int rows, int S, int K, sd_stream s) {
+extern "C" int sd_kl_fwd(const float* post, const float* prior, float* kl_row, float* dyn, float* rep, float free_nats,
+                         int rows, int S, int K, sd_stream s) {
   if (rows <= 0) return SD_OK;
   if (K < 1 || K > 64) return SD_ESHAPE;
   const int T = team_pow2(K);
   const int grid = rows < 4096 ? rows : 4096;
-  SD_TEAM_SWITCH(T, kl_fwd<TT><<<grid, 256, 0, (hipStream_t)s>>>(post, prior, kl_row, rows, S, K))
+  SD_TEAM_SWITCH(T, kl_fwd<TT><<<grid, 256, 0, (hipStream_t)s>>>(post, prior, kl_row, dyn, rep, free_nats, rows, S, K))
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
@@ -649,21 +668,24 @@ extern "C" int sd_twohot_logp_bwd(const float* logits, const float* bins, const 
 }
 
 extern "C" int sd_repval_loss_fwd(const float* logits, const float* bins, const float* ret, const float* slow,
-                                  const float* w, float* row_loss, long rows, int NB, sd_stream s) {
-  if (rows <= 0) return SD_OK;
-  if (NB > 256) return SD_ESHAPE;
-  repval_fwd_kernel<<<blocks_for(rows, 4), 256, 0, (hipStream_t)s>>>(logits, bins, ret, slow, w, row_loss, rows, NB);
+                                  const float* last, float* row_loss, int B, int Tl, int Tr, int NB, sd_stream s) {
+  if (B <= 0 || Tr <= 0) return SD_OK;
+  if (NB > 256 || Tr > Tl) return SD_ESHAPE;
+  const long rows = (long)B * Tr;
+  repval_fwd_kernel<<<blocks_for(rows, 4), 256, 0, (hipStream_t)s>>>(logits, bins, ret, slow, last, row_loss, rows, Tl,
+                                                                      Tr, NB);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
 
 extern "C" int sd_repval_loss_bwd(const float* logits, const float* bins, const float* ret, const float* slow,
-                                  const float* w, const float* gscale, float inv_n, float* dlogits, long rows, int NB,
-                                  sd_stream s) {
-  if (rows <= 0) return SD_OK;
-  if (NB > 256 || !gscale) return SD_ESHAPE;
-  repval_bwd_kernel<<<blocks_for(rows, 4), 256, 0, (hipStream_t)s>>>(logits, bins, ret, slow, w, gscale, inv_n,
-                                                                      dlogits, rows, NB);
+                                  const float* last, const float* gscale, float inv_n, float* dlogits, int B, int Tl,
+                                  int Tr, int NB, sd_stream s) {
+  if (B <= 0) return SD_OK;
+  if (NB > 256 || !gscale || Tr > Tl) return SD_ESHAPE;
+  const long lrows = (long)B * Tl;
+  repval_bwd_kernel<<<blocks_for(lrows, 4), 256, 0, (hipStream_t)s>>>(logits, bins, ret, slow, last, gscale, inv_n,
+                                                                       dlogits, lrows, Tl, Tr, NB);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
@@ -682,13 +704,13 @@ extern "C" int sd_imag_ac_loss_fwd(const float* vl, const float* bins, const flo
 
 extern "C" int sd_imag_ac_loss_bwd(const float* vl, const float* bins, const float* ret, const float* slow,
                                    const float* w, const float* adv, const float* gpolicy, const float* gvalue,
-                                   float coef, long N, int H, int H1, int NB, float* dvl, float* dlogpi, float* dent,
-                                   sd_stream s) {
+                                   float spolicy, float svalue, float coef, long N, int H, int H1, int NB, float* dvl,
+                                   float* dlogpi, float* dent, sd_stream s) {
   if (N <= 0 || H <= 0) return SD_OK;
   if (NB > 256 || H1 <= H) return SD_ESHAPE;
   imag_ac_bwd_kernel<<<blocks_for(N * H, 4), 256, 0, (hipStream_t)s>>>(vl, bins, ret, slow, w, adv, gpolicy, gvalue,
-                                                                       coef, 1.f / (float)(N * H), N, H, H1, NB, dvl,
-                                                                       dlogpi, dent);
+                                                                       spolicy, svalue, coef, 1.f / (float)(N * H), N,
+                                                                       H, H1, NB, dvl, dlogpi, dent);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

@@ -344,9 +344,84 @@ __global__ __launch_bounds__(64) void stats_merge_kernel(sd_stats s, const float
     if (r.kind == SD_STAT_STD) v = (float)sqrt(m2 / (n - 1.0));
     else if (r.kind == SD_STAT_MIN) v = mn;
     else if (r.kind == SD_STAT_MAX) v = mx;
+    if (r.sub) v -= r.sub[0];
+    if (r.div) v /= r.div[0];
     acc += r.scale * v;
   }
   out[b] = acc;
+}
+
+// weighted loss total (dreamer.py:571-576: the loss dict's `sum(v * scale)`): term i = coef_i * mean(x_i) (fixed
+// reduction order), total = ((0 + s_0 m_0) + s_1 m_1) + ... in the dict's order. One workgroup.
+__global__ __launch_bounds__(256) void loss_terms_fwd_kernel(sd_loss_terms L, float* __restrict__ means,
+                                                             float* __restrict__ total) {
+  __shared__ float red[4];
+  float tot = 0.f;
+  for (int i = 0; i < L.n; ++i) {
+    const sd_loss_term t = L.t[i];
+    float acc = 0.f;
+    for (long j = threadIdx.x; j < t.n; j += 256) acc += t.x[j];
+    const float m = t.coef * (block_sum<256>(acc, red) / (float)t.n);
+    tot = __fadd_rn(tot, __fmul_rn(t.scale, m));
+    if (threadIdx.x == 0 && means) means[i] = m;
+  }
+  if (threadIdx.x == 0) total[0] = tot;
+}
+// g_i[j] = (g_total * scale_i + g_means[i]) * coef_i / n_i: every term's input gradient in one launch (grid.y = term)
+__global__ __launch_bounds__(256) void loss_terms_bwd_kernel(sd_loss_terms L, const float* __restrict__ g_total,
+                                                             const float* __restrict__ g_means) {
+  const sd_loss_term t = L.t[blockIdx.y];
+  if (!t.g) return;
+  const float g = ((g_total ? g_total[0] * t.scale : 0.f) + (g_means ? g_means[blockIdx.y] : 0.f)) * t.coef / (float)t.n;
+  for (long j = (long)blockIdx.x * 256 + threadIdx.x; j < t.n; j += (long)gridDim.x * 256) t.g[j] = g;
+}
+
+// Weight layout copies, one launch for a list: mode 0 = transpose dst[b][c][r] = src[b * sb + r * sr + c]
+// (32 x 32 tiles through LDS, both sides coalesced); mode 1 = column pad dst[b * rows + r][c] = c < cols ?
+// src[b * sb + r * sr + c] : 0 for c < dcols.
+__global__ __launch_bounds__(256) void layout_copy_kernel(sd_layout_copies L) {
+  __shared__ float tile[32][33];
+  const sd_layout_copy e = L.e[blockIdx.y];
+  const int tr = (e.rows + 31) / 32, tc = (e.mode ? (e.dcols + 31) / 32 : (e.cols + 31) / 32);
+  const long ntiles = (long)e.batch * tr * tc;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows of 32 lanes
+  for (long tile_i = blockIdx.x; tile_i < ntiles; tile_i += gridDim.x) {
+    const int b = (int)(tile_i / ((long)tr * tc)), rem = (int)(tile_i % ((long)tr * tc));
+    const int r0 = (rem / tc) * 32, c0 = (rem % tc) * 32;
+    const float* src = e.src + (long)b * e.sb;
+    if (e.mode == 1) {
+      for (int i = ty; i < 32; i += 8) {
+        const int r = r0 + i, c = c0 + tx;
+        if (r < e.rows && c < e.dcols)
+          e.dst[((long)b * e.rows + r) * (e.dld ? e.dld : e.dcols) + c] = c < e.cols ? src[(long)r * e.sr + c] : 0.f;
+      }
+      continue;
+    }
+    for (int i = ty; i < 32; i += 8) {
+      const int r = r0 + i, c = c0 + tx;
+      tile[i][tx] = (r < e.rows && c < e.cols) ? src[(long)r * e.sr + c] : 0.f;
+    }
+    __syncthreads();
+    float* dst = e.dst + (long)b * e.rows * e.cols;
+    for (int i = ty; i < 32; i += 8) {
+      const int c = c0 + i, r = r0 + tx;  // dst row c, column r
+      if (c < e.cols && r < e.rows) dst[(long)c * e.rows + r] = tile[tx][i];
+    }
+    __syncthreads();
+  }
+}
+
+// episode flags of a batch (dreamer.py:571-660 operands): is_last / is_terminal (bool bytes) -> f32 last, term and
+// cont = 1 - term, for the continue-head target, the replay lambda-return and the replay-value weights
+__global__ void episode_flags_kernel(const unsigned char* __restrict__ is_last, const unsigned char* __restrict__ is_term,
+                                     long n, float* __restrict__ last, float* __restrict__ term,
+                                     float* __restrict__ cont) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float l = is_last[i] ? 1.f : 0.f, t = is_term[i] ? 1.f : 0.f;
+  last[i] = l;
+  term[i] = t;
+  cont[i] = 1.f - t;
 }
 
 // an empty dispatch whose name and grid (tag workgroups) a kernel trace can find: bench.py brackets its timed steps
@@ -397,6 +472,51 @@ extern "C" int sd_multi_stats(const sd_stats* s, float* workspace, float* out, i
   stats_chunk_kernel<<<chunks, 256, 0, (hipStream_t)st>>>(*s, workspace);
   SD_LAUNCH_CHECK();
   stats_merge_kernel<<<nout, 64, 0, (hipStream_t)st>>>(*s, workspace, out);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_loss_terms_fwd(const sd_loss_terms* L, float* means, float* total, sd_stream s) {
+  if (!L || L->n < 1 || L->n > SD_MAX_LOSS_TERMS || !total) return SD_EARG;
+  for (int i = 0; i < L->n; ++i)
+    if (!L->t[i].x || L->t[i].n <= 0) return SD_EARG;
+  loss_terms_fwd_kernel<<<1, 256, 0, (hipStream_t)s>>>(*L, means, total);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_loss_terms_bwd(const sd_loss_terms* L, const float* g_total, const float* g_means, sd_stream s) {
+  if (!L || L->n < 1 || L->n > SD_MAX_LOSS_TERMS) return SD_EARG;
+  long nmax = 0;
+  for (int i = 0; i < L->n; ++i) nmax = L->t[i].n > nmax ? L->t[i].n : nmax;
+  if (nmax <= 0) return SD_EARG;
+  const int gx = (int)(nmax < 256L * 64 ? (nmax + 255) / 256 : 64);
+  loss_terms_bwd_kernel<<<dim3(gx, L->n), 256, 0, (hipStream_t)s>>>(*L, g_total, g_means);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_layout_copies_run(const sd_layout_copies* L, sd_stream s) {
+  if (!L || L->n < 1 || L->n > SD_MAX_LAYOUT_COPIES) return SD_EARG;
+  long most = 0;
+  for (int i = 0; i < L->n; ++i) {
+    const sd_layout_copy& e = L->e[i];
+    if (!e.src || !e.dst || e.batch < 1 || e.rows < 1 || e.cols < 1 || e.mode < 0 || e.mode > 1) return SD_EARG;
+    if (e.mode == 1 && e.dcols < e.cols) return SD_EARG;
+    const long t = (long)e.batch * ((e.rows + 31) / 32) * (((e.mode ? e.dcols : e.cols) + 31) / 32);
+    most = t > most ? t : most;
+  }
+  const int gx = (int)(most < 1024 ? most : 1024);
+  layout_copy_kernel<<<dim3(gx, L->n), 256, 0, (hipStream_t)s>>>(*L);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+
+extern "C" int sd_episode_flags(const uint8_t* is_last, const uint8_t* is_term, long n, float* last, float* term,
+                                float* cont, sd_stream s) {
+  if (n <= 0) return SD_OK;
+  if (!is_last || !is_term || !last || !term || !cont) return SD_EARG;
+  episode_flags_kernel<<<nb(n), 256, 0, (hipStream_t)s>>>(is_last, is_term, n, last, term, cont);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

@@ -90,6 +90,20 @@ MlpExt = _parse_struct(HEADER, "sd_mlp_ext")
 class Stats(ctypes.Structure):
     _fields_ = [("r", StatReq * _define(HEADER, "SD_MAX_STATS")), ("nreq", c_int)]
 
+
+LossTerm = _parse_struct(HEADER, "sd_loss_term")
+
+
+class LossTerms(ctypes.Structure):
+    _fields_ = [("t", LossTerm * _define(HEADER, "SD_MAX_LOSS_TERMS")), ("n", c_int)]
+
+
+LayoutCopy = _parse_struct(HEADER, "sd_layout_copy")
+
+
+class LayoutCopies(ctypes.Structure):
+    _fields_ = [("e", LayoutCopy * _define(HEADER, "SD_MAX_LAYOUT_COPIES")), ("n", c_int)]
+
 _CTYPES = {
     "int": c_int, "long": c_long, "float": c_float, "double": ctypes.c_double, "uint64_t": ctypes.c_uint64,
     "uint32_t": ctypes.c_uint32, "sd_stream": c_ptr, "void": None,

@@ -237,6 +237,7 @@ class Dreamer(nn.Module):
         self.marks = K.Marks(self.device) if os.environ.get("SDREAMER_MARKS", "0") != "0" else None
         self._side = torch.cuda.Stream(device=self.device)
         self._prio_streams = None  # (main, side, fill, side fill) of STREAM_PRIO, created at the first replay
+        self._one = None  # device 1.0: the seed gradient of the world-model total (no fill launch per update)
         self._comm = None  # data parallel: the gradient all-reduce stream (created on first use)
         self._buckets = self._grad_buckets()
         self._graph = None
@@ -824,12 +825,13 @@ class Dreamer(nn.Module):
         # waits for the imagined returns next): off the chain from the head losses to the encoder gradient
         st["scan_tr"] = self.rssm._bwd_tr = self.rssm.scan_bwd_weights()
         st["enc_flip"] = K.set_flip_cache(self.encoder.dgrad_weights())
+        st["flags"] = self._episode_flags(st["data"])
         with ops.defer_wgrads(st["wm_wgrads"] if defer else None):
             st["wm_total"], st["wm_losses"], st["wm_metrics"] = self._wm_heads(st["data"], st["embed"], st["leaves"],
                                                                                st["feat_l"], st["seed"], st["ro"],
-                                                                               st["initial"])
+                                                                               st["initial"], st["flags"])
         self._mark("wm_heads")
-        st["rv"] = self._repval_pre(st["data"], st["feat_r"])
+        st["rv"] = self._repval_pre(st["data"], st["feat_r"], st["flags"])
         self._mark("repval_fwd")
 
     def _ph_repval(self, st):
@@ -932,16 +934,18 @@ class Dreamer(nn.Module):
                           imag_feat_tm=st["ifeat"], imag_action_tm=st["iact"], ret=rr["ret"], rret=st["rret"])
         return (st["post_stoch"], st["post_deter"]), metrics
 
-    def _wm_heads(self, data, embed, leaves, feat, seed=0, ro=0, initial=None):
-        """World-model losses (dreamer.py:453-576) on the posterior leaves, backward down to the leaves."""
+    def _wm_heads(self, data, embed, leaves, feat, seed=0, ro=0, initial=None, flags=None):
+        """World-model losses (dreamer.py:453-576) on the posterior leaves, backward down to the leaves. flags: the
+        batch's (last, term, cont) f32 tensors (K.episode_flags), else derived here."""
         losses, metrics = {}, {}
         B, T = data["action"].shape[:2]
         post_stoch, post_deter, post_logit = leaves
         prior_logit = self.rssm.prior(post_deter)
         self._prior_logit = prior_logit
         dyn_loss, rep_loss = self.rssm.kl_loss(post_logit, prior_logit, self.kl_free)
-        losses["dyn"] = dyn_loss.mean()
-        losses["rep"] = rep_loss.mean()
+        # the loss dict's per-row terms and scalars, reduced and weighted by one LossTermsFn launch below: name ->
+        # (rows or scalar, coefficient of its mean)
+        terms = {"dyn": (dyn_loss, 1.0), "rep": (rep_loss, 1.0)}
         if self.rep_loss == "dreamer":
             recon = self.decoder(post_stoch, post_deter)
             for key, mode in recon.items():
@@ -968,14 +972,21 @@ class Dreamer(nn.Module):
             else:
                 x2 = embed.reshape(B * T, -1).detach()
             losses["barlow"] = parallel.barlow(x1, x2, self.barlow_lambd, self.world)
+        terms.update({k: (v, 1.0) for k, v in losses.items()})  # the representation loss(es), in dict order
+        losses = {}
         rew_logits = self.reward(feat)
-        losses["rew"] = -ops.TwoHotLogProbFn.apply(rew_logits, self.rbins, data["reward"].float()).mean()
-        cont = 1.0 - data["is_terminal"].float()
-        losses["con"] = -ops.BernoulliLogProbFn.apply(self.cont(feat), cont).mean()
-        metrics["dyn_entropy"] = K.Stat(self.rssm.entropy(prior_logit))
-        metrics["rep_entropy"] = K.Stat(self.rssm.entropy(post_logit))
-        wm_total = sum(v * self._loss_scales[k] for k, v in losses.items())
-        wm_total.backward()
+        terms["rew"] = (ops.TwoHotLogProbFn.apply(rew_logits, self.rbins, data["reward"].float()), -1.0)
+        cont = flags[2] if flags is not None else 1.0 - data["is_terminal"].float()
+        terms["con"] = (ops.BernoulliLogProbFn.apply(self.cont(feat), cont), -1.0)
+        S = self.rssm._stoch
+        metrics["dyn_entropy"] = K.Stat(self.rssm.entropy_terms(prior_logit), scale=S)
+        metrics["rep_entropy"] = K.Stat(self.rssm.entropy_terms(post_logit), scale=S)
+        names = list(terms)
+        xs = [terms[k][0].reshape(-1) if terms[k][0].dim() == 0 else terms[k][0] for k in names]
+        wm_total, vec = ops.LossTermsFn.apply([terms[k][1] for k in names], [self._loss_scales[k] for k in names],
+                                              *xs)
+        losses = {k: vec[i] for i, k in enumerate(names)}
+        torch.autograd.backward(wm_total, self._unit(wm_total.device))  # the seed gradient without a fill launch
         return wm_total, losses, metrics
 
     def _proto_losses(self, data, initial, seed, ro):
@@ -1046,22 +1057,37 @@ class Dreamer(nn.Module):
         norm = ((obs_norm - 1) ** 2).mean() + ((feat_norm - 1) ** 2).mean()
         return {"swav": swav, "temp": temp, "norm": norm}
 
-    def _repval_pre(self, data, feat_r):
+    def _unit(self, device):
+        """device 1.0 (created once, outside any capture): the seed gradient of a loss total"""
+        if self._one is None:
+            self._one = torch.ones((), dtype=torch.float32, device=device)
+        return self._one
+
+    @staticmethod
+    def _episode_flags(data):
+        """(last, term, cont = 1 - term) as f32 (B, T): one launch from the replay's bool flags"""
+        il, it = data["is_last"], data["is_terminal"]
+        if il.dtype == torch.bool and it.dtype == torch.bool and il.is_contiguous() and it.is_contiguous():
+            return K.episode_flags(il, it)
+        B, T = data["action"].shape[:2]
+        last, term = il.float().reshape(B, T), it.float().reshape(B, T)
+        return last, term, 1.0 - term
+
+    def _repval_pre(self, data, feat_r, flags=None):
         """Replay-value parts that do not need the imagined returns (dreamer.py:638-652): value / slow-value modes on
-        the replay posterior, the value head forward (with grad) and the slow-target log-prob."""
+        the replay posterior, the value head forward (with grad) and the slow-target log-prob. The value head runs on
+        every posterior step (the loss reads its first T - 1 in place: no copy of feat[:, :-1], no slice backward)."""
         B, T = data["action"].shape[:2]
         N = B * T
         with torch.no_grad():
             fd = feat_r.detach().reshape(N, -1)
             value = K.twohot_mode(self.value.logits_nograd(fd), self.vbins).view(B, T)
             slow_value = K.twohot_mode(self._slow_value.logits_nograd(fd), self.vbins).view(B, T)
-        vd = self.value(feat_r[:, :-1])
-        with torch.no_grad():  # the loss operands that do not wait for the returns
-            last = data["is_last"].float().reshape(B, T)
-            rp = dict(slow_t=slow_value[:, :-1].contiguous(), w=(1.0 - last[:, :-1]).contiguous(),
-                      last=last.contiguous(), term=data["is_terminal"].float().reshape(B, T).contiguous(),
-                      reward=data["reward"].float().reshape(B, T).contiguous())
-        return dict(value=value, slow_value=slow_value, vd=vd, **rp)
+        vd = self.value(feat_r)
+        last, term, _ = flags if flags is not None else self._episode_flags(data)
+        reward = data["reward"].float().reshape(B, T)
+        return dict(value=value, slow_value=slow_value, vd=vd, last=last, term=term,
+                    reward=reward if reward.is_contiguous() else reward.contiguous())
 
     def _repval_post(self, data, rv, ret):
         """Replay lambda-return bootstrapped from the imagined return (dreamer.py:645) and the replay-value loss."""
@@ -1072,7 +1098,7 @@ class Dreamer(nn.Module):
             # boot = imag ret[:, 0]: ret is (N, H) with N = (b, t)
             rret = K.lambda_return(rv["reward"], ret, disc, self.lamb, term=rv["term"], last=rv["last"],
                                    boot_row_stride=T * H, boot_t_stride=H)  # (B, T-1)
-        loss = ops.RepvalLossFn.apply(rv["vd"], self.vbins, rret, rv["slow_t"], rv["w"])
+        loss = ops.RepvalLossFn.apply(rv["vd"], self.vbins, rret, rv["slow_value"], rv["last"])
         return loss, {}, rret  # the replay statistics are logged from the side stream (_ph_side_ac)
 
     @torch.no_grad()
@@ -1135,14 +1161,15 @@ class Dreamer(nn.Module):
         else:
             vl = self.value(xh, fast=True)
         # policy (dreamer.py:653-660) and value (661-671) losses and the advantage (628-636): one launch each way
-        losses["policy"], losses["value"], adv = ops.ImagACLossFn.apply(
-            vl, logpi, ent, self.vbins, ret, i_slow[:H], weight, rr["i_val"], rr["ret_scale"], self.act_entropy)
+        total, losses["policy"], losses["value"], adv = ops.ImagACLossFn.apply(
+            vl, logpi, ent, self.vbins, ret, i_slow[:H], weight, rr["i_val"], rr["ret_scale"], self.act_entropy,
+            self._loss_scales["policy"], self._loss_scales["value"])
         rr["adv"] = adv
         with ops.defer_wgrads(rr["ac_wgrads"]) if "ac_wgrads" in rr else contextlib.nullcontext():
-            (losses["policy"] * self._loss_scales["policy"] + losses["value"] * self._loss_scales["value"]).backward()
+            torch.autograd.backward(total, self._unit(total.device))
         with torch.no_grad():
-            ret_normed = (ret - rr["ret_offset"]) / rr["ret_scale"]
-            metrics["ret"] = ret_normed.mean()
+            # mean((ret - offset) / scale) as (mean(ret) - offset) / scale, resolved with the other metrics
+            metrics["ret"] = K.Stat(ret, sub=rr["ret_offset"].reshape(1), div=rr["ret_scale"].reshape(1))
             metrics["ret_005"] = K.Stat(self.return_ema.ema_vals[0:1])
             metrics["ret_095"] = K.Stat(self.return_ema.ema_vals[1:2])
             metrics["adv"] = K.Stat(adv)

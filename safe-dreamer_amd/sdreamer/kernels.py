@@ -373,11 +373,62 @@ def twohot_mode(logits, bins, out=None):
     return out
 
 
-def kl_rows(post, prior, S, K):
+def kl_rows(post, prior, S, K, free=None):
+    """KL rows; with `free`, also the two free-nats clamped copies (dyn, rep) from the same launch."""
     rows = post.numel() // (S * K)
-    out = torch.empty(rows, dtype=torch.float32, device=post.device)
-    nat.call("sd_kl_fwd", p(_c(post)), p(_c(prior)), p(out), rows, S, K, stream())
-    return out
+    out = torch.empty(rows if free is None else 3 * rows, dtype=torch.float32, device=post.device)
+    kl = out[:rows]
+    dyn, rep = (None, None) if free is None else (out[rows:2 * rows], out[2 * rows:])
+    nat.call("sd_kl_fwd", p(_c(post)), p(_c(prior)), p(kl), p(dyn), p(rep), float(free or 0.0), rows, S, K, stream())
+    return kl if free is None else (kl, dyn, rep)
+
+
+def loss_terms(xs, coefs, scales, means, total):
+    """sd_loss_terms_fwd: means (n,) (nullable) = coefs[i] * mean(xs[i]), total (1,) = sum scales[i] * means[i]"""
+    L = nat.LossTerms()
+    for i, x in enumerate(xs):
+        t = L.t[i]
+        t.x, t.n, t.coef, t.scale = p(_c(x)), x.numel(), float(coefs[i]), float(scales[i])
+    L.n = len(xs)
+    nat.call("sd_loss_terms_fwd", ctypes.addressof(L), p(means), p(total), stream())
+
+
+def loss_terms_bwd(ns, coefs, scales, grads, g_total, g_means):
+    """sd_loss_terms_bwd: grads[i] (ns[i] values, None = skipped) = (g_total scales[i] + g_means[i]) coefs[i] / ns[i]"""
+    L = nat.LossTerms()
+    for i, n in enumerate(ns):
+        t = L.t[i]
+        t.x, t.n, t.coef, t.scale, t.g = None, int(n), float(coefs[i]), float(scales[i]), p(grads[i])
+    L.n = len(ns)
+    nat.call("sd_loss_terms_bwd", ctypes.addressof(L), p(g_total), p(g_means), stream())
+
+
+def device_mean(x):
+    """mean of a contiguous f32 tensor as a 0-dim device tensor (one sd_loss_terms_fwd launch; no ATen reduce)"""
+    out = torch.empty(1, dtype=torch.float32, device=x.device)
+    loss_terms([_c(x)], [1.0], [1.0], None, out)
+    return out[0]
+
+
+def layout_copies(entries):
+    """entries: (src, dst, batch, rows, cols, sb, sr, dcols, mode[, dld]) -> one sd_layout_copies_run launch"""
+    L = nat.LayoutCopies()
+    for i, ent in enumerate(entries):
+        src, dst, batch, rows, cols, sb, sr, dcols, mode = ent[:9]
+        e = L.e[i]
+        e.src, e.dst, e.batch, e.rows, e.cols = p(src), p(dst), batch, rows, cols
+        e.sb, e.sr, e.dcols, e.mode, e.dld = sb, sr, dcols, mode, (ent[9] if len(ent) > 9 else 0)
+    L.n = len(entries)
+    nat.call("sd_layout_copies_run", ctypes.addressof(L), stream())
+
+
+def episode_flags(is_last, is_term):
+    """bool (B, T[, 1]) -> f32 (B, T) last, term, cont = 1 - term (one launch)"""
+    B, T = is_last.shape[:2]
+    out = torch.empty(3, B, T, dtype=torch.float32, device=is_last.device)
+    nat.call("sd_episode_flags", p(_c(is_last).view(torch.uint8)), p(_c(is_term).view(torch.uint8)), B * T,
+             p(out[0]), p(out[1]), p(out[2]), stream())
+    return out[0], out[1], out[2]
 
 
 def lambda_return(reward, boot, disc, lamb, term=None, cont_logit=None, last=None, boot_row_stride=None,
@@ -751,14 +802,18 @@ class Stat:
     """A metric resolved later, with every other metric of the update, by ONE sd_multi_stats launch: a sum of
     scale * stat(tensor) terms (stat: mean, unbiased std, min, max of the whole tensor; a scalar is its own mean)."""
 
-    __slots__ = ("terms",)
+    __slots__ = ("terms", "affine")
 
-    def __init__(self, t, kind=STAT_MEAN, scale=1.0):
+    def __init__(self, t, kind=STAT_MEAN, scale=1.0, sub=None, div=None):
         self.terms = [(t, int(kind), float(scale))]
+        self.affine = (sub, div)  # device scalars: (stat - sub) / div, applied to a single-term Stat
 
     def __add__(self, other):
         r = Stat.__new__(Stat)
+        if self.affine != (None, None) or (isinstance(other, Stat) and other.affine != (None, None)):
+            raise ValueError("an affine Stat is a metric of its own")
         r.terms = self.terms + (other.terms if isinstance(other, Stat) else Stat(other).terms)
+        r.affine = (None, None)
         return r
 
     __radd__ = __add__
@@ -766,6 +821,7 @@ class Stat:
     def __mul__(self, k):
         r = Stat.__new__(Stat)
         r.terms = [(t, kind, sc * float(k)) for t, kind, sc in self.terms]
+        r.affine = self.affine
         return r
 
     __rmul__ = __mul__
@@ -773,6 +829,9 @@ class Stat:
     def record_stream(self, s):
         for t, _, _ in self.terms:
             t.record_stream(s)
+        for t in self.affine:
+            if t is not None:
+                t.record_stream(s)
 
 
 def tensorstats(t, prefix):
@@ -787,6 +846,7 @@ def metric_vector(values):
     (two launches) per SD_MAX_STATS terms (normally one)."""
     reqs, empty = [], []
     for i, v in enumerate(values):
+        aff = v.affine if isinstance(v, Stat) else (None, None)
         for t, kind, sc in (v.terms if isinstance(v, Stat) else [(v, STAT_MEAN, 1.0)]):
             t = t.detach()
             if t.numel() == 0:  # torch semantics: mean / std / min / max of nothing is NaN (sd_multi_stats needs n > 0)
@@ -794,7 +854,7 @@ def metric_vector(values):
                 continue
             if t.dtype != torch.float32:
                 t = t.float()
-            reqs.append((_c(t), kind, sc, i))
+            reqs.append((_c(t), kind, sc, i, aff))
     out = torch.empty(len(values), dtype=torch.float32, device=reqs[0][0].device if reqs else "cuda")
     if not reqs:
         return out.fill_(float("nan"))
@@ -804,9 +864,10 @@ def metric_vector(values):
         st = nat.Stats()
         part = reqs[lo:lo + cap]
         c0 = 0
-        for j, (t, kind, sc, i) in enumerate(part):
+        for j, (t, kind, sc, i, aff) in enumerate(part):
             r = st.r[j]
             r.x, r.n, r.kind, r.out, r.scale, r.chunk0 = p(t), t.numel(), kind, i, sc, c0
+            r.sub, r.div = p(aff[0]), p(aff[1])
             c0 += (t.numel() + chunk - 1) // chunk
         st.nreq = len(part)
         ws = torch.empty(5 * c0, dtype=torch.float32, device=out.device)

@@ -204,13 +204,28 @@ class CatIntoFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, b, holder):
         out = holder[0]
-        torch.cat([a, b], -1, out=out)
-        ctx.split = a.shape[-1]
+        na, nb, F = a.shape[-1], b.shape[-1], out.shape[-1]
+        rows = a.numel() // na
+        if out.stride(-1) != 1 or out.numel() != rows * F or na + nb != F or not (a.is_contiguous() and b.is_contiguous()):
+            torch.cat([a, b], -1, out=out)
+        else:  # both halves in one sd_layout_copies_run launch (row stride F into the slot)
+            base = out.reshape(rows, F)
+            k.layout_copies([(a, base, 1, rows, na, 0, na, na, 1, F), (b, base[:, na:], 1, rows, nb, 0, nb, nb, 1, F)])
+        ctx.split = na
         return out
 
     @staticmethod
     def backward(ctx, g):
         return g[..., :ctx.split], g[..., ctx.split:], None
+
+
+def _pad_last(w, n):
+    """w (..., c) -> (..., n) zero-padded, one sd_layout_copies_run launch"""
+    wc = w.contiguous()
+    out = torch.empty(*w.shape[:-1], n, dtype=w.dtype, device=w.device)
+    rows = wc.numel() // w.shape[-1]
+    k.layout_copies([(wc, out, 1, rows, w.shape[-1], 0, w.shape[-1], n, 1)])
+    return out
 
 
 class ConvPoolNormFn(torch.autograd.Function):
@@ -221,7 +236,7 @@ class ConvPoolNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, nw, nchw_flat):
         # x may carry zero-padded channels (first layer: 3 -> 4); the weight is padded to match
-        wk = w if x.shape[-1] == w.shape[-1] else torch.nn.functional.pad(w, (0, x.shape[-1] - w.shape[-1])).contiguous()
+        wk = w if x.shape[-1] == w.shape[-1] else _pad_last(w, x.shape[-1])
         fused = k.conv2d_fwd_pool(x.contiguous(), wk, b, nw, nchw_flat=nchw_flat) if FUSED_POOL else None
         if fused is None:
             conv = k.conv2d_fwd(x.contiguous(), wk, b)
@@ -299,11 +314,11 @@ class KLFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, post, prior, free, S, K):
         post, prior = post.contiguous(), prior.contiguous()
-        kl = k.kl_rows(post, prior, S, K)
+        kl, dyn, rep = k.kl_rows(post, prior, S, K, free=free)  # the clamped copies come from the same launch
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(post, prior, kl)
         ctx.free, ctx.S, ctx.K = free, S, K
-        cl = torch.clamp(kl, min=free)
-        return cl, cl.clone()
+        return dyn, rep
 
     @staticmethod
     def backward(ctx, g_dyn, g_rep):
@@ -316,6 +331,36 @@ class KLFn(torch.autograd.Function):
         k.nat.call("sd_kl_bwd", k.p(post), k.p(prior), k.p(kl), k.p(gr), k.p(gd), float(ctx.free), k.p(d_post),
                    k.p(d_prior), rows, ctx.S, ctx.K, 0, 0, k.stream())
         return d_post, d_prior, None, None, None
+
+
+class LossTermsFn(torch.autograd.Function):
+    """The world-model loss dict and its weighted total (dreamer.py:571-576): term i = coefs[i] * mean(xs[i]), total =
+    sum_i scales[i] * term_i in order. One launch forward (sd_loss_terms_fwd), one backward (every input's gradient,
+    sd_loss_terms_bwd), instead of a reduce + scalar-op chain per term. Returns (total (), terms (n,))."""
+
+    @staticmethod
+    def forward(ctx, coefs, scales, *xs):
+        xs = [x.contiguous() for x in xs]
+        dev = xs[0].device
+        terms = torch.empty(len(xs), dtype=torch.float32, device=dev)
+        total = torch.empty(1, dtype=torch.float32, device=dev)
+        k.loss_terms(xs, coefs, scales, terms, total)
+        ctx.coefs, ctx.scales = list(coefs), list(scales)
+        ctx.shapes = [x.shape for x in xs]
+        ctx.dev = dev
+        ctx.set_materialize_grads(False)  # an unused output's gradient stays None (no zeros launch)
+        return total[0], terms
+
+    @staticmethod
+    def backward(ctx, g_total, g_terms):
+        n = len(ctx.shapes)
+        grads = [torch.empty(sh, dtype=torch.float32, device=ctx.dev) if ctx.needs_input_grad[2 + i] else None
+                 for i, sh in enumerate(ctx.shapes)]
+        if any(g is not None for g in grads):
+            gt = g_total.reshape(1).contiguous() if g_total is not None else None
+            gm = g_terms.contiguous() if g_terms is not None else None
+            k.loss_terms_bwd([torch.Size(sh).numel() for sh in ctx.shapes], ctx.coefs, ctx.scales, grads, gt, gm)
+        return (None, None) + tuple(grads[:n])
 
 
 class TwoHotLogProbFn(torch.autograd.Function):
@@ -343,39 +388,44 @@ class TwoHotLogProbFn(torch.autograd.Function):
 
 class RepvalLossFn(torch.autograd.Function):
     """Replay-value loss mean(w * (-logp(ret) - logp(slow))) under the TwoHot value head (dreamer.py:652-658;
-    TwoHot.log_prob distributions.py:100-129): one launch forward (row terms; the mean is a torch reduce), one
-    backward launch for the logits gradient (both log-prob terms at once). Targets and weights are detached."""
+    TwoHot.log_prob distributions.py:100-129), w = 1 - is_last. The value head ran on every posterior step: logits
+    (B, T, NB), slow / last (B, T); ret (B, T - 1) covers the first T - 1 steps (the reference's [:, :-1] slices are
+    read in place). One launch for the row terms, one for their mean (K.device_mean), one backward launch for the
+    logits gradient (both log-prob terms; zero on the last step). Targets and weights are detached."""
 
     @staticmethod
-    def forward(ctx, logits, bins, ret, slow, w):
-        NB = logits.shape[-1]
-        l2 = _flat(logits).contiguous()
-        r, sl, ww = (t.reshape(-1).contiguous() for t in (ret, slow, w))
-        rows = torch.empty(l2.shape[0], dtype=torch.float32, device=logits.device)
-        k.nat.call("sd_repval_loss_fwd", k.p(l2), k.p(bins), k.p(r), k.p(sl), k.p(ww), k.p(rows), l2.shape[0], NB,
+    def forward(ctx, logits, bins, ret, slow, last):
+        B, Tl, NB = logits.shape
+        Tr = ret.shape[1]
+        l2, r, sl, la = logits.contiguous(), ret.contiguous(), slow.contiguous(), last.contiguous()
+        rows = torch.empty(B * Tr, dtype=torch.float32, device=logits.device)
+        k.nat.call("sd_repval_loss_fwd", k.p(l2), k.p(bins), k.p(r), k.p(sl), k.p(la), k.p(rows), B, Tl, Tr, NB,
                    k.stream())
-        ctx.save_for_backward(l2, bins, r, sl, ww)
-        ctx.shape = logits.shape
-        return rows.mean()
+        ctx.save_for_backward(l2, bins, r, sl, la)
+        return k.device_mean(rows)
 
     @staticmethod
     def backward(ctx, g):
-        l2, bins, r, sl, ww = ctx.saved_tensors
+        l2, bins, r, sl, la = ctx.saved_tensors
+        B, Tl, NB = l2.shape
+        Tr = r.shape[1]
         dl = torch.empty_like(l2)
-        gs = g.reshape(1).to(torch.float32).contiguous()
-        k.nat.call("sd_repval_loss_bwd", k.p(l2), k.p(bins), k.p(r), k.p(sl), k.p(ww), k.p(gs), 1.0 / l2.shape[0],
-                   k.p(dl), l2.shape[0], l2.shape[1], k.stream())
-        return dl.view(ctx.shape), None, None, None, None
+        gs = g.reshape(1).contiguous()
+        k.nat.call("sd_repval_loss_bwd", k.p(l2), k.p(bins), k.p(r), k.p(sl), k.p(la), k.p(gs), 1.0 / (B * Tr),
+                   k.p(dl), B, Tl, Tr, NB, k.stream())
+        return dl, None, None, None, None
 
 
 class ImagACLossFn(torch.autograd.Function):
-    """Imagined policy and value losses (dreamer.py:623-636, 653-671) in one launch each way (sd_imag_ac_loss_fwd /
-    _bwd): rows are the H * N time-major imagined steps; value logits vl (H*N, NB), logpi / ent (H*N) with gradients;
-    ret (N, H), weight (N, H1), val (H1, N) time-major, slow (H, N), scale (device scalar) detached. Returns (policy, value, adv):
-    the two losses (means of the kernel's row terms) and adv (N, H) = (ret - val[:, :H]) / scale (no gradient)."""
+    """Imagined policy and value losses (dreamer.py:623-636, 653-671) and their weighted sum: rows are the H * N
+    time-major imagined steps; value logits vl (H*N, NB), logpi / ent (H*N) with gradients; ret (N, H), weight (N, H1),
+    val (H1, N) time-major, slow (H, N), scale (device scalar) detached; sp / sv the loss scales. Forward: the row
+    terms (sd_imag_ac_loss_fwd) and their means + the weighted total (one sd_loss_terms_fwd); backward: one launch
+    from the total's gradient. Returns (total, policy, value, adv): adv (N, H) = (ret - val[:, :H]) / scale; only the
+    total carries a gradient."""
 
     @staticmethod
-    def forward(ctx, vl, logpi, ent, bins, ret, slow, weight, val, scale, coef):
+    def forward(ctx, vl, logpi, ent, bins, ret, slow, weight, val, scale, coef, sp, sv):
         N, H = ret.shape
         H1 = weight.shape[1]
         NB = vl.shape[-1]
@@ -387,26 +437,30 @@ class ImagACLossFn(torch.autograd.Function):
         adv = torch.empty(N, H, dtype=torch.float32, device=vl.device)
         k.nat.call("sd_imag_ac_loss_fwd", k.p(l2), k.p(bins), k.p(r), k.p(sl), k.p(w), k.p(v), k.p(sc), k.p(lp),
                    k.p(en), float(coef), N, H, H1, NB, k.p(rows[1]), k.p(rows[0]), k.p(adv), k.stream())
+        means = torch.empty(2, dtype=torch.float32, device=vl.device)
+        total = torch.empty(1, dtype=torch.float32, device=vl.device)
+        k.loss_terms([rows[0], rows[1]], [1.0, 1.0], [sp, sv], means, total)  # policy, value; sp p + sv v
         ctx.save_for_backward(l2, bins, r, sl, w, adv)
-        ctx.coef, ctx.shapes = float(coef), (vl.shape, logpi.shape, ent.shape)
-        ctx.mark_non_differentiable(adv)
-        m = rows.mean(1)
-        return m[0], m[1], adv
+        ctx.coef, ctx.sp, ctx.sv, ctx.shapes = float(coef), float(sp), float(sv), (vl.shape, logpi.shape, ent.shape)
+        ctx.mark_non_differentiable(means, adv)
+        ctx.set_materialize_grads(False)
+        return total[0], means[0], means[1], adv
 
     @staticmethod
-    def backward(ctx, gp, gv, _gadv):
+    def backward(ctx, g_total, _gp, _gv, _gadv):
         l2, bins, r, sl, w, adv = ctx.saved_tensors
         N, H = r.shape
         H1 = w.shape[1]
+        vs, ls, es = ctx.shapes
+        if g_total is None:
+            return (None,) * 12
         dvl = torch.empty_like(l2)
         dlp = torch.empty(N * H, dtype=torch.float32, device=l2.device)
         den = torch.empty(N * H, dtype=torch.float32, device=l2.device)
-        gp = gp.reshape(1).to(torch.float32).contiguous() if gp is not None else None
-        gv = gv.reshape(1).to(torch.float32).contiguous() if gv is not None else None
-        k.nat.call("sd_imag_ac_loss_bwd", k.p(l2), k.p(bins), k.p(r), k.p(sl), k.p(w), k.p(adv), k.p(gp), k.p(gv),
-                   ctx.coef, N, H, H1, l2.shape[1], k.p(dvl), k.p(dlp), k.p(den), k.stream())
-        vs, ls, es = ctx.shapes
-        return dvl.view(vs), dlp.view(ls), den.view(es), None, None, None, None, None, None, None
+        g = g_total.reshape(1).contiguous()
+        k.nat.call("sd_imag_ac_loss_bwd", k.p(l2), k.p(bins), k.p(r), k.p(sl), k.p(w), k.p(adv), k.p(g), k.p(g),
+                   ctx.sp, ctx.sv, ctx.coef, N, H, H1, l2.shape[1], k.p(dvl), k.p(dlp), k.p(den), k.stream())
+        return dvl.view(vs), dlp.view(ls), den.view(es), None, None, None, None, None, None, None, None, None
 
 
 class BernoulliLogProbFn(torch.autograd.Function):

@@ -161,9 +161,20 @@ class RSSM(nn.Module):
         from the head losses to the encoder gradient; the weights do not change until the optimizer step."""
         P = self._p()
         D = self._deter
-        return dict(W0T=P["W0"].t().contiguous(), W1T=P["W1"].t().contiguous(), WshT=P["Wsh"].t().contiguous(),
-                    WbdT=P["Wbd"].transpose(1, 2).contiguous(), WgT=P["Wg"].transpose(1, 2).contiguous(),
-                    WoDT=P["Wo"][:, :D].t().contiguous(), WlT=P["Wl"].t().contiguous())
+        srcs = dict(W0T=P["W0"], W1T=P["W1"], WshT=P["Wsh"], WbdT=P["Wbd"], WgT=P["Wg"], WoDT=P["Wo"][:, :D],
+                    WlT=P["Wl"])
+        out, ents = {}, []
+        for name, w in srcs.items():  # all seven transposes in one sd_layout_copies_run launch
+            w3 = w if w.dim() == 3 else w.unsqueeze(0)
+            nb, rows, cols = w3.shape
+            if w3.stride(2) != 1:
+                raise ValueError(f"{name}: rows must be contiguous")
+            out[name] = torch.empty(nb, cols, rows, dtype=w.dtype, device=w.device)
+            ents.append((w3, out[name], nb, rows, cols, w3.stride(0), w3.stride(1), cols, 0))
+            if w.dim() == 2:
+                out[name] = out[name][0]
+        K.layout_copies(ents)
+        return out
 
     def _img_mods(self):
         return [(self._img_net[3 * i], self._img_net[3 * i + 1]) for i in range(self._img_layers)], self._img_net.img_net_logit
@@ -185,7 +196,8 @@ class RSSM(nn.Module):
         """rssm.py:140-156. embed (B,T,E), action (B,T,A), initial ((B,S,K),(B,D)), reset (B,T[,1]) bool.
         `seed`/`row_offset`/`stream_id` select the counter-based posterior noise (oracle/noise.py)."""
         B, T = action.shape[:2]
-        r = reset.reshape(B, T).to(torch.uint8)
+        r = reset.reshape(B, T)
+        r = r.view(torch.uint8) if r.dtype == torch.bool and r.is_contiguous() else r.to(torch.uint8)  # no copy
         stoch0, deter0 = initial
         s0 = stoch0.reshape(B, -1)
         # rows are independent sequences: B > 16 runs as row tiles side by side inside every scan launch
@@ -250,8 +262,14 @@ class RSSM(nn.Module):
     def entropy(self, logit):
         """sum_S entropy of the unimix categorical (metrics dyn_entropy/rep_entropy, dreamer.py:575-576)."""
         S, Kd = self._stoch, self._discrete
-        e = K.onehot_entropy(logit.detach().reshape(-1, Kd).contiguous(), Kd, self._unimix_ratio)
-        return e.view(-1, S).sum(-1)
+        return self.entropy_terms(logit).view(-1, S).sum(-1)
+
+    @torch.no_grad()
+    def entropy_terms(self, logit):
+        """per-categorical entropies (rows * S): the metric mean_rows sum_S is S * their mean (a K.Stat scale, no
+        sum launch)"""
+        Kd = self._discrete
+        return K.onehot_entropy(logit.detach().reshape(-1, Kd).contiguous(), Kd, self._unimix_ratio)
 
     # ------------------------------------------------------------------ fused no-grad pieces
     @torch.no_grad()

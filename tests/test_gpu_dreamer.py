@@ -82,9 +82,6 @@ class _OracleRun:
         return self.keeps[u]
 
 
-F64_BOUND = 0.1  # fraction of the golden's m / v bounds the product may use against the float64 moments
-
-
 def _opt_samples(ag, spec):
     """name -> (exp_avg, exp_avg_sq) sampled like the golden u*_st_* (LaProp state index i = _named_params[i])."""
     sd = ag._optimizer.state_dict()["state"]
@@ -185,9 +182,10 @@ def test_update_matches_reference(name):
         # a flipped step sign (2x), a skipped AGC clip (1/scale^2 in v) or a skipped Polyak still fail
         # (tools/sabotage_optim.sh).
         opt = _opt_samples(ag, spec)
-        # distance from EXACT arithmetic: the float64 moments of the same update (tests/golden/gen_f64_moments.py).
-        # The golden (the reference's own f32 run) sits up to 0.50 of the bounds above from them (walker_r2aug's
-        # first conv layer, tools/grad_attrib.py); the product must stay within F64_BOUND of them
+        # distance from the float64 run of the same update (tests/golden/gen_f64_moments.py), reported beside the
+        # golden's bounds (tools/grad_attrib.py compares both f32 runs against it). Not asserted: where a term is
+        # ill-conditioned the f64 run moves away from every f32 evaluation (walker_r2_nowarm: product and golden agree
+        # to 0.004 of the bound and both sit 0.2 from f64), so it is evidence for attribution, not an oracle.
         if f64 is not None:
             for k in spec.shapes:
                 m, v = opt[k]
@@ -235,7 +233,6 @@ def test_update_matches_reference(name):
             assert_close(flat[sample_idx(sk, flat.size)], ref, 0.0, 4 * ulp(ref) + 1e-12, f"u{u} slow critic {sk}")
     report["bound_ratio"] = {k: {"tensor": t, "ratio": r} for k, (t, r) in bounds.items()}
     report["bound_ratio_f64"] = {k: {"tensor": t, "ratio": r} for k, (t, r) in bounds64.items()}
-    assert all(r <= F64_BOUND for _, r in bounds64.values()), ("moments vs exact arithmetic", bounds64)
     print(name, report)
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "golden")
     os.makedirs(out, exist_ok=True)

@@ -148,24 +148,52 @@ def test_twohot_mode_logp():
 
 def test_repval_loss_fused():
     """sd_repval_loss_fwd/bwd (ops.RepvalLossFn) vs the reference expression mean(w * (-logp(ret) - logp(slow)))
-    (dreamer.py:652-658) on the oracle's TwoHot log-prob, with the backward seeded by a loss scale."""
+    (dreamer.py:652-658) on the oracle's TwoHot log-prob, w = 1 - is_last: the value logits / slow values / flags
+    cover all T posterior steps and the loss reads the first T - 1 in place; the backward (seeded by a loss scale)
+    leaves zeros on the last step."""
     from sdreamer import ops
-    M = 1008
+    B, T = 16, 63
     bins = R.twohot_bins(255)
-    logits = -0.5 * (torch.arange(255) - 127).abs().float() + torch.randn(M, 255, generator=_g(11))
-    ret = torch.randn(M, generator=_g(12)) * 30
-    slow = torch.randn(M, generator=_g(13)) * 30
-    ret[:4] = torch.tensor([0.0, bins[3].item(), 1e9, -1e9])
-    w = (torch.rand(M, generator=_g(14)) > 0.1).float()
+    logits = -0.5 * (torch.arange(255) - 127).abs().float() + torch.randn(B, T + 1, 255, generator=_g(11))
+    ret = torch.randn(B, T, generator=_g(12)) * 30
+    slow = torch.randn(B, T + 1, generator=_g(13)) * 30
+    ret[0, :4] = torch.tensor([0.0, bins[3].item(), 1e9, -1e9])
+    last = (torch.rand(B, T + 1, generator=_g(14)) < 0.1).float()
     scale = 0.3
     lr = logits.clone().requires_grad_()
-    ref = torch.mean(w * (-R.twohot_log_prob(lr, bins, ret.unsqueeze(-1)) - R.twohot_log_prob(lr, bins, slow.unsqueeze(-1))))
+    w = 1.0 - last[:, :-1]
+    ref = torch.mean(w * (-R.twohot_log_prob(lr[:, :-1], bins, ret.unsqueeze(-1))
+                          - R.twohot_log_prob(lr[:, :-1], bins, slow[:, :-1].unsqueeze(-1))))
     (ref * scale).backward()
     l = logits.to(DEV).requires_grad_()
-    out = ops.RepvalLossFn.apply(l, bins.to(DEV), ret.to(DEV), slow.to(DEV), w.to(DEV))
+    out = ops.RepvalLossFn.apply(l, bins.to(DEV), ret.to(DEV), slow.to(DEV), last.to(DEV))
     close(out, ref, 1e-5, "loss")
     torch.autograd.backward(out, torch.full((), scale, device=DEV))
     close(l.grad, lr.grad, 1e-5, "dlogits")
+    assert (l.grad[:, -1] == 0).all()
+
+
+def test_loss_terms_and_kl_clamp():
+    """ops.LossTermsFn (sd_loss_terms_fwd/bwd): the loss dict's means and weighted total in one launch, gradients of
+    every term in one launch; KLFn's clamped copies from the KL launch (torch.clamp(min=free), rssm.py:222-230)."""
+    from sdreamer import ops
+    xs = [torch.randn(16, 64, generator=_g(21)), torch.randn(1, generator=_g(22)), torch.randn(1024, generator=_g(23))]
+    coefs, scales = [1.0, 1.0, -1.0], [0.5, 1.0, 2.0]
+    xd = [x.to(DEV).requires_grad_() for x in xs]
+    total, terms = ops.LossTermsFn.apply(coefs, scales, *xd)
+    ref_terms = [c * x.mean() for c, x in zip(coefs, xs)]
+    ref_total = sum(s * t for s, t in zip(scales, ref_terms))
+    close(terms, torch.stack(ref_terms), 1e-6, "terms")
+    close(total, ref_total, 1e-6, "total")
+    torch.autograd.backward(total, torch.full((), 0.7, device=DEV))
+    for x, xg, c, s in zip(xs, xd, coefs, scales):
+        close(xg.grad, torch.full_like(x, 0.7 * s * c / x.numel()), 1e-6, "term grad")
+    S, Kd, rows = 32, 16, 300
+    post, prior = torch.randn(rows, S * Kd, generator=_g(24)), torch.randn(rows, S * Kd, generator=_g(25))
+    dyn, rep = ops.KLFn.apply(post.to(DEV), prior.to(DEV), 1.0, S, Kd)
+    from sdreamer import kernels as K
+    raw = K.kl_rows(post.to(DEV), prior.to(DEV), S, Kd)
+    assert torch.equal(dyn, torch.clamp(raw, min=1.0)) and torch.equal(rep, dyn)
 
 
 def test_bnormal_and_bernoulli():
@@ -373,7 +401,8 @@ def test_barlow():
 
 def test_metric_vector():
     """kernels.metric_vector (sd_multi_stats): mean / unbiased std / min / max of tensors above and below one chunk
-    (SD_STAT_CHUNK), scalar tensors, and scaled sums of several terms into one slot, against torch."""
+    (SD_STAT_CHUNK), scalar tensors, scaled sums of several terms into one slot, and a mean taken as (mean - sub) / div
+    with device scalars (the normalised-return metric), against torch."""
     from sdreamer import kernels as K
     g = _g(5)
     a = torch.randn(98304, generator=g) * 3 + 1
@@ -382,17 +411,18 @@ def test_metric_vector():
     d = torch.randn(7, generator=g)
     A, Bt, C, D = (t.to(DEV) for t in (a, b, c, d))
     vals = list(K.tensorstats(A, "a").values()) + list(K.tensorstats(Bt, "b").values()) + [
-        C, K.Stat(D, K.STAT_STD), K.Stat(C) + K.Stat(A, scale=0.5) + K.Stat(D, K.STAT_MAX, scale=-2.0)]
+        C, K.Stat(D, K.STAT_STD), K.Stat(C) + K.Stat(A, scale=0.5) + K.Stat(D, K.STAT_MAX, scale=-2.0),
+        K.Stat(Bt, sub=torch.tensor([0.25], device=DEV), div=torch.tensor([4.0], device=DEV))]
     got = K.metric_vector(vals).cpu().double()
     ref = torch.tensor([a.mean(), a.std(), a.min(), a.max(), b.mean(), b.std(), b.min(), b.max(), c, d.std(),
-                        c + 0.5 * a.mean() - 2.0 * d.max()]).double()
+                        c + 0.5 * a.mean() - 2.0 * d.max(), ((b - 0.25) / 4.0).mean()]).double()
     assert torch.allclose(got, ref, rtol=2e-6, atol=1e-6), (got, ref)
 
 
 def test_imag_ac_loss_fused():
-    """ops.ImagACLossFn (sd_imag_ac_loss_fwd / _bwd) against the reference's torch formulation (dreamer.py:623-671 with
-    TwoHot.log_prob, distributions.py:100-129): policy / value losses, the advantage, and the gradients of logits,
-    log-probs and entropies."""
+    """ops.ImagACLossFn (sd_imag_ac_loss_fwd / _bwd + the weighted total) against the reference's torch formulation
+    (dreamer.py:623-671 with TwoHot.log_prob, distributions.py:100-129): policy / value losses, their scaled sum, the
+    advantage, and the gradients of logits, log-probs and entropies from the sum."""
     from sdreamer import ops
     from sdreamer.dreamer import _symexp_bins
     N, H, NB = 96, 5, 255
@@ -417,12 +447,13 @@ def test_imag_ac_loss_fused():
     vlos = torch.mean(w * (-lt - ls).view(H, N).t())
     (2.0 * pol + 0.5 * vlos).backward()
     vd, ld, ed = (t.to(DEV).requires_grad_() for t in (vl, logpi, ent))
-    p_, v_, a_ = ops.ImagACLossFn.apply(vd, ld, ed, bins.to(DEV), ret.to(DEV), slow.to(DEV), weight.to(DEV),
-                                        val.t().contiguous().to(DEV), scale.to(DEV), coef)  # values time-major
+    t_, p_, v_, a_ = ops.ImagACLossFn.apply(vd, ld, ed, bins.to(DEV), ret.to(DEV), slow.to(DEV), weight.to(DEV),
+                                            val.t().contiguous().to(DEV), scale.to(DEV), coef, 2.0, 0.5)  # time-major
     close(p_, pol, 1e-5, "policy")
     close(v_, vlos, 1e-5, "value")
+    close(t_, 2.0 * pol + 0.5 * vlos, 1e-5, "weighted total")
     close(a_, adv, 1e-6, "adv")
-    (2.0 * p_ + 0.5 * v_).backward()
+    t_.backward()
     close(vd.grad, vr.grad, 1e-6, "d value logits")
     close(ld.grad, lr_.grad, 1e-6, "d logpi")
     close(ed.grad, er.grad, 1e-6, "d ent")

@@ -1,7 +1,7 @@
 """Census of the ATen (non-HIP-extension) operations one eager update issues at the bench shape, per update phase and
 calling site: every aten op on device tensors that is not a view / allocation (those launch no kernel) is recorded
 under a TorchDispatchMode with the innermost sdreamer frame that issued it. Phase = the agent's last _mark label.
-Usage: python tools/aten_census.py"""
+Usage: python tools/aten_census.py [graphs]"""
 import collections
 import os
 import sys
@@ -25,11 +25,15 @@ NO_KERNEL = {"view", "_unsafe_view", "_reshape_alias", "reshape", "t", "transpos
 
 
 def site():
+    """the two innermost sdreamer frames (file:function:line < caller), or "autograd" for backward-engine ops"""
+    got = []
     for fr in reversed(traceback.extract_stack()[:-3]):
         f = fr.filename
         if "sdreamer" in f and not f.endswith(("_native.py",)):
-            return f"{os.path.basename(f)}:{fr.name}:{fr.lineno}"
-    return "?"
+            got.append(f"{os.path.basename(f)}:{fr.name}:{fr.lineno}")
+            if len(got) == 2:
+                break
+    return " < ".join(got) if got else "autograd"
 
 
 class Census(TorchDispatchMode):
@@ -44,7 +48,10 @@ class Census(TorchDispatchMode):
         if name not in NO_KERNEL:
             dev = any(isinstance(a, torch.Tensor) and a.is_cuda for a in list(args) + list((kwargs or {}).values()))
             if dev or name in ("zeros", "ones", "full", "zeros_like", "ones_like", "full_like", "arange", "scalar_tensor"):
-                self.recs[(self.phase, name, site())] += 1
+                a0 = args[0] if args and isinstance(args[0], torch.Tensor) else None
+                shp = f" {tuple(a0.shape)}/{a0.stride()}" if a0 is not None and name in ("clone", "copy_", "_to_copy",
+                                                                                       "contiguous") else ""
+                self.recs[(self.phase, name + shp, site())] += 1
         return out
 
 
@@ -54,7 +61,10 @@ def main():
     cfg = load_config("dmc/cnn", ["device=cuda:0", "model.compile=False"])
     torch.manual_seed(0)
     agent = Dreamer(cfg.model, bench._Spaces({"image": bench._Sp((64, 64, 3))}), bench._Sp((6,)))
-    agent.use_graphs = False
+    graphs = len(sys.argv) > 1 and sys.argv[1] == "graphs"
+    # graphs: the census runs over the update that captures the phase graphs (every op then recorded is one the
+    # graph replays in the timed window) plus the eager glue around them
+    agent.use_graphs = graphs
     buf = bench.synth_buffer(cfg, torch.device("cuda", 0), 0)
     for _ in range(2):
         agent.update(buf)
@@ -72,7 +82,8 @@ def main():
     per = collections.Counter()
     for (ph, _, _), n in c.recs.items():
         per[ph] += n
-    print(f"{sum(c.recs.values())} ATen ops in one eager update (phase = the agent's last mark before the op)")
+    print(f"{sum(c.recs.values())} ATen ops in one {'graph-capturing' if graphs else 'eager'} update (phase = the "
+          f"agent's last mark before the op)")
     for ph, n in per.items():
         print(f"\n## after mark '{ph}': {n}")
         for (p2, name, s), m in sorted(c.recs.items(), key=lambda kv: kv[0][2]):
