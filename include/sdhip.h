@@ -99,6 +99,10 @@ int sd_rmsnorm_fwd_ld(const float* x, const float* w, float* y, long ldy, float*
 int sd_rmsnorm_bwd_blocks(int M, int N);
 int sd_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* dy, float* dx, float* dw,
                    float* dw_partial, int M, int N, int act, int accumulate_dx, int accumulate_dw, sd_stream stream);
+/* the same with dy rows of stride ldy (a column block of a wider gradient read in place) */
+int sd_rmsnorm_bwd_ld(const float* x, const float* w, const float* rstd, const float* dy, long ldy, float* dx,
+                      float* dw, float* dw_partial, int M, int N, int act, int accumulate_dx, int accumulate_dw,
+                      sd_stream stream);
 /* out[n] (+)= sum_r in[r*ld + n] (fixed-order column sums; bias gradients) */
 int sd_colsum(const float* in, float* out, int R, int N, long ld, int accumulate, sd_stream stream);
 /* two-pass variant for long columns: workspace >= sd_colsum_chunks(R) * N floats */
@@ -209,9 +213,19 @@ int sd_return_ema(const float* x, int n, float* ema, float* offset_scale, float*
  * the input through nn.Upsample(2, nearest) (ConvDecoder, networks.py:259-265). */
 int sd_conv2d_fwd(const float* in, const float* w, const float* bias, float* out, int Nb, int Hs, int Ws, int Ci,
                   int Co, int kh, int kw, int pad, int ups, sd_stream stream);
+/* Optional accumulation target of the bwd-weight entry points below: when acc is non-null the [dW | db] result is
+ * ADDED into the parameter gradients (dw (Co, kh, kw, ci_w), ci_w <= Ci: the input's padded channels dropped; db
+ * (Co)) by the launch's final reduction instead of being written to dw_db (which is then scratch for the paths
+ * without a reduction) — no separate add launches. */
+typedef struct sd_wgrad_acc {
+  float* dw;
+  float* db;
+  int ci_w;
+} sd_wgrad_acc;
 /* dw_db (Co, kh*kw*Ci + 1) = [dW | d bias]; ksplit > 1 needs workspace >= ksplit*Co*(kh*kw*Ci+1) floats */
 int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db, float* workspace, long ws_floats, int ksplit,
-                    int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad, int ups, sd_stream stream);
+                    int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad, int ups, const sd_wgrad_acc* acc,
+                    sd_stream stream);
 /* partial-slab count sd_conv2d_wgrad uses for this request (workspace >= slabs * Co * (kh*kw*Ci + 1) floats when
  * slabs > 1): stride-1 convs with Co % 16 == 0 take a direct kernel (dy rows + input patch staged in LDS, no im2col
  * re-reads) whose split is fixed by the library; others use `ksplit` over the im2col implicit GEMM. */
@@ -223,7 +237,7 @@ int sd_conv2d_wgrad_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw
 int sd_conv2d_wgrad_pool_slabs(int Nb, int H, int W, int Ci, int Co, int kh, int kw);
 int sd_conv2d_wgrad_pool(const float* in, const float* dpool, const uint8_t* amax, float* dw_db, float* workspace,
                          long ws_floats, int Nb, int H, int W, int Ci, int Co, int kh, int kw, int pad,
-                         sd_stream stream);
+                         const sd_wgrad_acc* acc, sd_stream stream);
 /* Split-bf16 (bf16x3, ~1e-5 relative) backward convolutions (csrc/conv.hip, gemm3_core.h). SD_ESHAPE when the
  * shape is outside the kernels (the caller then takes the f32 path). dgrad: same arguments as sd_conv2d_fwd with
  * in = dOut (Ci channels), w = the flipped weight (sd_conv_flip_weight), out = dIn (Co channels), ups = 0.
@@ -234,7 +248,8 @@ int sd_conv2d_dgrad_bf16x3(const float* dout, const float* wflip, float* din, in
                            int kh, int kw, int pad, sd_stream stream);
 int sd_conv2d_wgrad_bf16x3_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int ups);
 int sd_conv2d_wgrad_bf16x3(const float* in, const float* dout, float* dw_db, float* workspace, long ws_floats,
-                           int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad, sd_stream stream);
+                           int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad, const sd_wgrad_acc* acc,
+                           sd_stream stream);
 /* The same bwd-data as a direct convolution (csrc/conv.hip conv_dgrad3_direct: each workgroup stages its dOut patch
  * once, split to bf16 planes; same products and order per k as sd_conv2d_dgrad_bf16x3, k summed in the same order).
  * wsplit = sd_conv_split_weight(wflip, rows = Co, K = kh*kw*Ci). Instantiated for the 5x5 pad-2 stages of the
@@ -438,7 +453,7 @@ typedef struct sd_rssm_scan {
   const float *Wl, *bl;        /* obs_net_logit: (SK,U) (SK) */
   const float *W0T, *W1T, *WshT, *WbdT, *WgT, *WoDT, *WlT;  /* backward: (D,U) (SK,U) (3U,D) (G,Dg,Dg) (G,Dg,3Dg) (D,U) (U,SK) */
   /* inputs */
-  const unsigned char* reset;  /* (T,B) */
+  const unsigned char* reset;  /* (T,B), or (B,T) with reset_bm */
   const float *stoch0, *deter0;/* (B,SK) (B,D) */
   const float *x2, *eproj;     /* (T,B,U): action branch output; embed half of obs_net_0 + bias */
   /* saved activations (written by fwd, read by bwd) */
@@ -469,6 +484,9 @@ typedef struct sd_rssm_scan {
      (T + t) * 8 + phase (backward); trace_slot is set per launch by the library */
   uint64_t* trace;
   int trace_slot;
+  int reset_bm; /* 1: reset is (B, T) batch-major (the replay batch's is_first, read in place); 0: (T, B) */
+  float* d_op_bm; /* optional backward output: a batch-major (B, T, U) copy of d_op (the embed gradient's operand) */
+  float* d_x2_bm; /* optional backward output: a batch-major (B, T, U) copy of d_xcat's x2 block (action branch) */
 } sd_rssm_scan;
 int sd_rssm_scan_work_floats(const sd_rssm_scan* d);
 int sd_rssm_scan_fwd(const sd_rssm_scan* d, sd_stream stream);

@@ -1094,8 +1094,10 @@ __global__ __launch_bounds__(256) void split_weight(const float* __restrict__ w,
 
 // out[e] = sum_s ws[s * n + e] in a fixed order; 64 outputs per workgroup (one per lane), the 4 waves take every
 // 4th slab and are summed through LDS.
+// acc.dw set: out is not written; the sums are added into the parameter gradients (element e = (co, j) of the
+// (Co, J + 1) [dW | db] layout, J = taps * cx channels; channels >= acc.ci_w dropped)
 __global__ __launch_bounds__(256) void slab_reduce(const float* __restrict__ ws, int slabs, long n,
-                                                   float* __restrict__ out) {
+                                                   float* __restrict__ out, sd_wgrad_acc acc, int J, int cx) {
   __shared__ float part[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long e = (long)blockIdx.x * 64 + lane;
@@ -1111,7 +1113,21 @@ __global__ __launch_bounds__(256) void slab_reduce(const float* __restrict__ ws,
   }
   part[wave][lane] = v;
   __syncthreads();
-  if (wave == 0 && e < n) out[e] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  if (wave == 0 && e < n) {
+    const float r = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    if (!acc.dw) {
+      out[e] = r;
+    } else {
+      const long co = e / (J + 1);
+      const int j = (int)(e - co * (J + 1));
+      if (j == J) {
+        acc.db[co] += r;
+      } else {
+        const int tap = j / cx, c = j - tap * cx;
+        if (c < acc.ci_w) acc.dw[(co * (J / cx) + tap) * acc.ci_w + c] += r;
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------- direct split-bf16 bwd-weight
@@ -1541,7 +1557,7 @@ bool direct_plan(int Nb, int H, int W, int Ci, int Co, int kh, int kw, int ups, 
 
 int wgrad_direct(const float* in, const float* dout, float* dw_db, float* ws, long ws_floats, int Nb, int H, int W,
                  int Ci, int Co, int kh, int kw, int pad, int J, int lw, const DirectPlan& pl, hipStream_t s,
-                 const uint8_t* amax = nullptr) {
+                 const uint8_t* amax, sd_wgrad_acc acc) {
   DirectW d;
   d.x = in; d.dy = dout; d.amax = amax; d.Nb = Nb; d.H = H; d.W = W; d.Ci = Ci; d.Co = Co; d.kh = kh; d.kw = kw; d.pad = pad;
   d.lw = lw; d.J = J; d.R = pl.R;
@@ -1580,7 +1596,7 @@ int wgrad_direct(const float* in, const float* dout, float* dw_db, float* ws, lo
   if (!launched) return SD_ESHAPE;
   SD_LAUNCH_CHECK();
   const long total = (long)Co * (J + 1);  // fixed-order sum of the row-block slabs (4 waves x unrolled loads)
-  slab_reduce<<<(int)((total + 63) / 64), 256, 0, s>>>(ws, pl.slabs, total, dw_db);
+  slab_reduce<<<(int)((total + 63) / 64), 256, 0, s>>>(ws, pl.slabs, total, dw_db, acc, J, Ci);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
@@ -1682,9 +1698,11 @@ extern "C" int sd_conv2d_fwd_pool(const float* in, const float* w, const float* 
 
 extern "C" int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db, float* workspace, long ws_floats,
                                int ksplit, int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad, int ups,
-                               sd_stream stream_) {
+                               const sd_wgrad_acc* acc_p, sd_stream stream_) {
   hipStream_t s = (hipStream_t)stream_;
   if (Nb <= 0) return SD_OK;
+  const sd_wgrad_acc acc = acc_p ? *acc_p : sd_wgrad_acc{nullptr, nullptr, 0};
+  if (acc.dw && (!acc.db || acc.ci_w < 1 || acc.ci_w > Ci || !dw_db)) return SD_EARG;
   Geom G{in, Nb, Hs, Ws, Ci, Hs << ups, Ws << ups, kh, kw, pad, ups};
   const int J = kh * kw * Ci;
   GemmArgs g{};
@@ -1701,7 +1719,8 @@ extern "C" int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db,
   const int lw = ilog2_exact(G.Wg), lhw = ilog2_exact(G.Hg * G.Wg);
   DirectPlan pl;
   if (va && vb && direct_plan(Nb, Hs, Ws, Ci, Co, kh, kw, ups, pl))
-    return wgrad_direct(in, dout, dw_db, workspace, ws_floats, Nb, Hs, Ws, Ci, Co, kh, kw, pad, J, lw, pl, s);
+    return wgrad_direct(in, dout, dw_db, workspace, ws_floats, Nb, Hs, Ws, Ci, Co, kh, kw, pad, J, lw, pl, s, nullptr,
+                        acc);
   if (conv_algo() == 2 && va && vb && lw >= 0 && lhw >= 0 && (Co == 16 || Co == 32 || Co == 48 || Co == 64)) {
     const dim3 grid(sd_cdiv(g.N, 128), 1, ks);
     switch (Co) {
@@ -1717,6 +1736,11 @@ extern "C" int sd_conv2d_wgrad(const float* in, const float* dout, float* dw_db,
     long total = (long)g.M * g.N;
     int blocks = (int)((total + 255) / 256);
     gemm_reduce_kernel<<<blocks, 256, 0, s>>>(g);
+    SD_LAUNCH_CHECK();
+  }
+  if (acc.dw) {  // the implicit-GEMM path wrote dw_db: one pass adds it into the gradients
+    const long total = (long)Co * (J + 1);
+    slab_reduce<<<(int)((total + 63) / 64), 256, 0, s>>>(dw_db, 1, total, nullptr, acc, J, Ci);
     SD_LAUNCH_CHECK();
   }
   return SD_OK;
@@ -1745,15 +1769,17 @@ extern "C" int sd_conv2d_wgrad_pool_slabs(int Nb, int H, int W, int Ci, int Co, 
 }
 extern "C" int sd_conv2d_wgrad_pool(const float* in, const float* dpool, const uint8_t* amax, float* dw_db,
                                     float* workspace, long ws_floats, int Nb, int H, int W, int Ci, int Co, int kh,
-                                    int kw, int pad, sd_stream stream_) {
+                                    int kw, int pad, const sd_wgrad_acc* acc_p, sd_stream stream_) {
   if (Nb <= 0) return SD_OK;
+  const sd_wgrad_acc acc = acc_p ? *acc_p : sd_wgrad_acc{nullptr, nullptr, 0};
+  if (acc.dw && (!acc.db || acc.ci_w < 1 || acc.ci_w > Ci)) return SD_EARG;
   DirectPlan pl;
   if (!pool_plan(Nb, H, W, Ci, Co, kh, kw, pl))
     return SD_ESHAPE;
   // amax is read as uint32 words (4 pooled pixels' argmax bytes per load)
   if (!al16(dpool) || !al16(in) || Co % 4 || Ci % 4 || !amax || reinterpret_cast<uintptr_t>(amax) % 4) return SD_EARG;
   return wgrad_direct(in, dpool, dw_db, workspace, ws_floats, Nb, H, W, Ci, Co, kh, kw, pad, kh * kw * Ci,
-                      ilog2_exact(W), pl, (hipStream_t)stream_, amax);
+                      ilog2_exact(W), pl, (hipStream_t)stream_, amax, acc);
 }
 
 extern "C" int sd_conv_flip_weight(const float* w, float* wf, int Co, int kh, int kw, int Ci, sd_stream s) {
@@ -1861,7 +1887,7 @@ bool direct3_plan(int Nb, int H, int W, int Ci, int Co, int kh, int kw, int ups,
 }
 
 int wgrad3_direct(const float* in, const float* dout, float* dw_db, float* ws, long ws_floats, int Nb, int H, int W,
-                  int Ci, int Co, int kh, int kw, int pad, const DirectPlan& pl, hipStream_t s) {
+                  int Ci, int Co, int kh, int kw, int pad, const DirectPlan& pl, hipStream_t s, sd_wgrad_acc acc) {
   DirectW3 d;
   d.x = in; d.dy = dout; d.Nb = Nb; d.H = H; d.W = W; d.Ci = Ci; d.Co = Co; d.kh = kh; d.kw = kw; d.pad = pad;
   d.lw = ilog2_exact(W); d.J = kh * kw * Ci; d.R = pl.R;
@@ -1894,7 +1920,7 @@ int wgrad3_direct(const float* in, const float* dout, float* dw_db, float* ws, l
   if (!launched) return SD_ESHAPE;
   SD_LAUNCH_CHECK();
   const long n = (long)Co * (d.J + 1);
-  slab_reduce<<<(int)((n + 63) / 64), 256, 0, s>>>(ws, pl.slabs, n, dw_db);
+  slab_reduce<<<(int)((n + 63) / 64), 256, 0, s>>>(ws, pl.slabs, n, dw_db, acc, d.J, Ci);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
@@ -2023,10 +2049,12 @@ extern "C" int sd_conv2d_wgrad_bf16x3_slabs(int Nb, int Hs, int Ws, int Ci, int 
 
 extern "C" int sd_conv2d_wgrad_bf16x3(const float* in, const float* dout, float* dw_db, float* workspace,
                                       long ws_floats, int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad,
-                                      sd_stream stream_) {
+                                      const sd_wgrad_acc* acc_p, sd_stream stream_) {
   hipStream_t s = (hipStream_t)stream_;
   if (Nb <= 0) return SD_OK;
+  const sd_wgrad_acc acc = acc_p ? *acc_p : sd_wgrad_acc{nullptr, nullptr, 0};
+  if (acc.dw && (!acc.db || acc.ci_w < 1 || acc.ci_w > Ci)) return SD_EARG;
   DirectPlan pl;
   if (!direct3_plan(Nb, Hs, Ws, Ci, Co, kh, kw, 0, pl) || !al16(in) || !al16(dout)) return SD_ESHAPE;
-  return wgrad3_direct(in, dout, dw_db, workspace, ws_floats, Nb, Hs, Ws, Ci, Co, kh, kw, pad, pl, s);
+  return wgrad3_direct(in, dout, dw_db, workspace, ws_floats, Nb, Hs, Ws, Ci, Co, kh, kw, pad, pl, s, acc);
 }

@@ -58,7 +58,7 @@ template <int TEAM, int VPT>
 __global__ __launch_bounds__(256) void rms_bwd(const float* __restrict__ x, const float* __restrict__ w,
                                                const float* __restrict__ rstd, const float* __restrict__ dy,
                                                float* __restrict__ dx, float* __restrict__ dw_part, int M, int N,
-                                               int act, int accumulate_dx) {
+                                               int act, int accumulate_dx, long ldy) {
   constexpr int TPB = 256 / TEAM;
   __shared__ float red[4];
   __shared__ float wpart[TEAM == 256 ? 1 : TPB * TEAM * VPT];
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void rms_bwd(const float* __restrict__ x, cons
   for (int j = 0; j < VPT; ++j) dwacc[j] = 0.f;
   for (long row = (long)blockIdx.x * TPB + team; row < M; row += (long)gridDim.x * TPB) {
     const float* xr = x + row * N;
-    const float* dyr = dy + row * N;
+    const float* dyr = dy + row * ldy;
     const float r = rstd[row];
     float xh[VPT], g[VPT];
     float dot = 0.f;
@@ -250,15 +250,21 @@ extern "C" int sd_rmsnorm_bwd_blocks(int M, int N) {
 extern "C" int sd_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* dy, float* dx,
                               float* dw, float* dw_partial, int M, int N, int act, int accumulate_dx,
                               int accumulate_dw, sd_stream stream_) {
+  return sd_rmsnorm_bwd_ld(x, w, rstd, dy, N, dx, dw, dw_partial, M, N, act, accumulate_dx, accumulate_dw, stream_);
+}
+
+extern "C" int sd_rmsnorm_bwd_ld(const float* x, const float* w, const float* rstd, const float* dy, long ldy,
+                                 float* dx, float* dw, float* dw_partial, int M, int N, int act, int accumulate_dx,
+                                 int accumulate_dw, sd_stream stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (M <= 0) return SD_OK;
   if (N <= 0 || N > 4096) return SD_ESHAPE;
   const int team = team_for(N);
   float* part = dw ? dw_partial : nullptr;
   int grid;
-  if (team == 16) { grid = grid_bwd<16>(M); SD_RMS_DISPATCH(rms_bwd, 16, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
-  else if (team == 64) { grid = grid_bwd<64>(M); SD_RMS_DISPATCH(rms_bwd, 64, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
-  else { grid = grid_bwd<256>(M); SD_RMS_DISPATCH(rms_bwd, 256, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx) }
+  if (team == 16) { grid = grid_bwd<16>(M); SD_RMS_DISPATCH(rms_bwd, 16, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx, ldy) }
+  else if (team == 64) { grid = grid_bwd<64>(M); SD_RMS_DISPATCH(rms_bwd, 64, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx, ldy) }
+  else { grid = grid_bwd<256>(M); SD_RMS_DISPATCH(rms_bwd, 256, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx, ldy) }
   SD_LAUNCH_CHECK();
   if (dw) return sd_colsum_ws(dw_partial, dw, grid, N, N, accumulate_dw, nullptr, stream_);
   return SD_OK;

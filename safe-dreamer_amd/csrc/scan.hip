@@ -234,15 +234,21 @@ constexpr int UH = 256;        // hidden width of the fused path (base.yaml: hid
 constexpr int NU = UH / 128;   // float4 columns per prologue thread over a hidden row
 
 // ------------------------------------------------------------------------------------------- forward kernels
+// reset flag of (step t, batch row b): (T, B) time-major, or (B, T) batch-major when d.reset_bm (read in place)
+SD_DEV bool reset_at(const sd_rssm_scan& d, int t, int b) {
+  return d.reset[d.reset_bm ? (long)b * d.T + t : (long)t * d.B + b] != 0;
+}
+
 struct SlabProb {
   const float* A;
   long lda;
   const float* W;
   long ldw;
   float* out;                 // slab s at out + s*M*N
-  const unsigned char* mask;  // rows whose input is reset (output row forced to 0), or null
+  const unsigned char* mask;  // rows whose input is reset (output row forced to 0), or null; row r at mask[r * mstride]
   uint64_t* trace;            // SD_SCAN_TRACE builds: phase timestamps (sd_rssm_scan.trace), slot below
   int slot;
+  int mstride;
 };
 
 // row-tiled GEMM into split-K slabs: out[s][m][n] = A[m, span_s] . W[n, span_s]; grid (N/16, ks * row tiles, nprob)
@@ -259,7 +265,7 @@ __global__ __launch_bounds__(NTHR) void k_slab(SlabProb p0, SlabProb p1, int M, 
   const float* wt[1] = {p.W + (long)(n0 + l16) * p.ldw + kb};
   core.load_b(wt, nch, wave, q);
   const int erow = tid >> 4;
-  const bool masked = tid < 256 && erow < nr && p.mask && p.mask[rb + erow];
+  const bool masked = tid < 256 && erow < nr && p.mask && p.mask[(long)(rb + erow) * p.mstride];
   core.run_glb(p.A + (long)rb * p.lda + kb, p.lda, nr, nch, wave, l16, q);
   SD_TR(1)
   float* C = smem + NW * 256;
@@ -288,11 +294,11 @@ __global__ void k_init(sd_rssm_scan d, float* w1t) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nS + nD; i += (long)gridDim.x * blockDim.x) {
     if (i < nS) {
       const int row = (int)(i / d.SK);
-      d.s_in[i] = d.reset[row] ? 0.f : d.stoch0[i];
+      d.s_in[i] = reset_at(d, 0, row) ? 0.f : d.stoch0[i];
     } else {
       const long j = i - nS;
       const int row = (int)(j / d.D);
-      d.h_in[j] = d.reset[row] ? 0.f : d.deter0[j];
+      d.h_in[j] = reset_at(d, 0, row) ? 0.f : d.deter0[j];
     }
   }
 }
@@ -417,7 +423,7 @@ __global__ __launch_bounds__(NTHR) void k_gate(sd_rssm_scan d, Work w, int t) {
     bca = bg[Dg + j];
     bua = bg[2 * Dg + j];
     hprev = d.h_in[(long)t * B * D + (long)ger * D + col];
-    rnext = t + 1 < d.T && d.reset[(t + 1) * B + ger];
+    rnext = t + 1 < d.T && reset_at(d, t + 1, ger);
   }
   const float r = rsqrtf(sum_parts(pv) / (float)D + d.eps);
   if (rv && t32 == 0 && tile == 0) d.rh[(long)t * B + gr] = r;
@@ -485,7 +491,7 @@ __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
     blv[k] = d.bl[n0 + lt];
     gn[k] = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)t,
                       (uint64_t)((long)(rb + er) * S + s + d.group_offset) * KD + lt);
-    rnext[k] = er < nr && t + 1 < d.T && d.reset[(t + 1) * B + rb + er];
+    rnext[k] = er < nr && t + 1 < d.T && reset_at(d, t + 1, rb + er);
   }
 #pragma unroll
   for (int i = 0; i < NU; ++i) x[i] += e[i];
@@ -575,7 +581,7 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
     gn = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)t,
                    (uint64_t)((long)b * S + g * CPG + tid / KD + d.group_offset) * KD + lt);
   }
-  const bool rnext = t + 1 < d.T && d.reset[(t + 1) * B + b];
+  const bool rnext = t + 1 < d.T && reset_at(d, t + 1, b);
   // obs_net_0 output row (sum of the deter-half slabs + the hoisted embed half with bias), RMSNorm + SiLU
   float x = 0.f, nw = 0.f;
   if (tid < UH) {
@@ -822,7 +828,10 @@ __global__ __launch_bounds__(NTHR) void k_dgru(sd_rssm_scan d, Work w, int t) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) o[i][k] = rv ? r * (gq[i][k] - xv[i][k] * r * dot) : 0.f;
   st_row(smem + core_lds_floats<1>() + row * ldp, o, UH, t32);
-  if (rv && tile == 0) st_row(d.d_op + tBU + (long)gr * UH, o, UH, t32);
+  if (rv && tile == 0) {
+    st_row(d.d_op + tBU + (long)gr * UH, o, UH, t32);
+    if (d.d_op_bm) st_row(d.d_op_bm + ((long)gr * d.T + t) * UH, o, UH, t32);
+  }
   __syncthreads();
   SD_TR(1)
   core.run_lds(smem + core_lds_floats<1>(), ldp, UH / 16, wave, l16, q);
@@ -988,6 +997,7 @@ __global__ __launch_bounds__(NTHR) void k_dx01(sd_rssm_scan d, Work w, int t) {
     if (c < X) {
       dx[c] = v;
       d.d_xcat[(tB + b) * X + c] = v;
+      if (d.d_x2_bm && c >= 2 * d.U) d.d_x2_bm[((long)b * d.T + t) * d.U + (c - 2 * d.U)] = v;
     }
   }
   __syncthreads();
@@ -1044,7 +1054,7 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   for (int k = 0; k < NE; ++k) {
     const int i = tid + NTHR * k, er = (i / KD) & 15, lt = i % KD, ger = rb + er;
     const bool ev = i < MR * KD && er < nr;
-    rs[k] = ev && d.reset[t * B + ger];
+    rs[k] = ev && reset_at(d, t, ger);
     e0[k] = e1[k] = e2[k] = gn[k] = 0.f;
     if (p0) {
       if (ev) e0[k] = w.dhin[(long)ger * D + n0 + lt];
@@ -1076,7 +1086,10 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
     for (int g = 1; g < GM; ++g) dx[i] += part[g][i];
   }
   if (wx2) {
-    if (rv) st_row(d.d_xcat + (tB + gr) * X + 2 * UH, dx, UH, t32);
+    if (rv) {
+      st_row(d.d_xcat + (tB + gr) * X + 2 * UH, dx, UH, t32);
+      if (d.d_x2_bm) st_row(d.d_x2_bm + ((long)gr * d.T + t) * UH, dx, UH, t32);
+    }
 #pragma unroll
     for (int g = 0; g < GM; ++g)
       ld_row(part[g], w.dxs + (long)g * B * X + (long)gr * X, UH, rv && g < kx_of(d.G), t32);
@@ -1216,7 +1229,7 @@ int fwd_phase(const sd_rssm_scan& d, const Work& w, bool lrows, int which, int t
   const int rt = dd.row_tile = row_tile_of(d), nt = row_tiles(d);
   dd.trace_slot = t * 8 + which;
   if (which == 0) {
-    SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr, d.trace, dd.trace_slot};
+    SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr, d.trace, dd.trace_slot, 1};
     SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(UH / 16, ks_s * nt, 1), NTHR, core1, st>>>(p, p, B, UH, span_s, ks_s, rt));
   } else if (which == 1) {
     // x0 finished by the previous step's k_logit_rows (lrows, t > 0)
@@ -1231,8 +1244,9 @@ int fwd_phase(const sd_rssm_scan& d, const Work& w, bool lrows, int which, int t
     SD_NG_SWITCH(Dg, if (!(raise_lds<k_gate<NG, NG>>(lds_gate))) return SD_EARG;
                  k_gate<NG, NG><<<dim3(D / 16, 1, nt), NTHR, lds_gate, st>>>(dd, w, t));
   } else if (which == 3) {
-    SlabProb po{d.deter + t * BD, D, d.WoD, wod_ld, w.ops, nullptr, d.trace, dd.trace_slot};
-    SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset + (t + 1) * B, d.trace, dd.trace_slot};
+    SlabProb po{d.deter + t * BD, D, d.WoD, wod_ld, w.ops, nullptr, d.trace, dd.trace_slot, 1};
+    SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset_bm ? d.reset + (t + 1) : d.reset + (t + 1) * B, d.trace,
+                dd.trace_slot, d.reset_bm ? d.T : 1};
     const int np = t + 1 < d.T ? 2 : 1;
     SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d * nt, np), NTHR, core1, st>>>(po, px, B, UH, span_d,
                                                                                         d.ks_d, rt));
@@ -1282,7 +1296,7 @@ extern "C" int sd_rssm_scan_fwd(const sd_rssm_scan* dp, sd_stream stream_) {
   k_init<<<lrows ? 256 : 64, 256, 0, st>>>(d, lrows ? w.w1t : nullptr);
   SD_LAUNCH_CHECK();
   {  // x0p(0) = h_in[0] . W0^T
-    SlabProb p{d.h_in, D, d.W0, D, w.x0s, nullptr, nullptr, 0};
+    SlabProb p{d.h_in, D, d.W0, D, w.x0s, nullptr, nullptr, 0, 1};
     SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d * row_tiles(d), 1), NTHR, core_lds_floats<1>() * 4, st>>>(
                             p, p, B, UH, D / d.ks_d, d.ks_d, row_tile_of(d)));
     SD_LAUNCH_CHECK();

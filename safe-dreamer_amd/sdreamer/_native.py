@@ -98,6 +98,7 @@ class LossTerms(ctypes.Structure):
     _fields_ = [("t", LossTerm * _define(HEADER, "SD_MAX_LOSS_TERMS")), ("n", c_int)]
 
 
+WgradAcc = _parse_struct(HEADER, "sd_wgrad_acc")
 LayoutCopy = _parse_struct(HEADER, "sd_layout_copy")
 
 

@@ -605,10 +605,14 @@ class Dreamer(nn.Module):
                 self._g_in[k].copy_(v)
             for dst, src in zip(self._g_init, initial):
                 dst.copy_(src)
-        self._seed_dev.fill_(int(seed) & 0x7FFFFFFFFFFFFFFF)
+        # the update's noise seed into the graphs' device scalar as a pinned host-to-device copy (no fill kernel; the
+        # caching host allocator keeps the pinned block until the copy has run)
+        self._seed_dev.copy_(torch.tensor([int(seed) & 0x7FFFFFFFFFFFFFFF], dtype=torch.int64).pin_memory(),
+                             non_blocking=True)
         if self.rep_loss == "dreamerpro":
             self._ema_updates += 1
-            self._proto_gate.fill_(0.0 if self._protos_frozen() else 1.0)
+            self._proto_gate.copy_(torch.tensor([0.0 if self._protos_frozen() else 1.0]).pin_memory()
+                                   .reshape(self._proto_gate.shape), non_blocking=True)
         gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gS2, gM3 = self._graph
         caller = torch.cuda.current_stream()
         if STREAM_PRIO and self.use_side_stream:
@@ -793,10 +797,15 @@ class Dreamer(nn.Module):
         else:
             feat_l = self.rssm.get_feat(leaves[0], leaves[1])
         feat_r = feat_l.detach().requires_grad_(True)  # replay-value leaf (side stream)
+        # every head reading the feat (reward, continue, projector, replay value) adds its input gradient into one
+        # (B, T, F) buffer (ops.DxSink): the scan backward reads its two halves in place
+        fsink = ops.DxSink(feat_l)
+        ops.sink(feat_l, fsink)
+        ops.sink(feat_r, fsink)
         return dict(data=data, initial=initial, seed=seed, ro=ro, embed=embed, embed_l=embed_l,
                     enc_split=split[0] if split else None, post_stoch=post_stoch,
                     post_deter=post_deter, post_logit=post_logit, leaves=leaves, feat_l=feat_l, feat_r=feat_r,
-                    ifeats=ifeats)
+                    ifeats=ifeats, fsink=fsink)
 
     def _ph_side_returns(self, st):
         """side: imagination (dreamer.py:578-597), imagined heads, lambda-returns + ReturnEMA (598-636)."""
@@ -857,24 +866,30 @@ class Dreamer(nn.Module):
         SK = self.rssm.flat_stoch
         leaves = st["leaves"]
         self._mark("repval_wait")
-        g_feat = st["feat_r"].grad
-        lg = [l.grad if l.grad is not None else torch.zeros_like(l) for l in leaves]
-        # the posterior gradient is leaf gradient + replay-value feat gradient: the feat gradient's halves go to the
-        # scan backward as second summands (RSSM._bwd_extra), added where the scan reads them (no add launches)
-        g_stoch, g_deter = lg[0], lg[1]
+        fs = st.get("fsink")
+        g_feat = fs.buf if fs is not None and fs.written else None
+        if st["feat_r"].grad is not None:  # a head outside the sink (none on the benched path)
+            g_feat = st["feat_r"].grad if g_feat is None else g_feat + st["feat_r"].grad
+        # the posterior gradient is leaf gradient + feat gradient: the feat gradient's halves go to the scan backward
+        # as second summands (RSSM._bwd_extra), added where the scan reads them (no add launches); missing leaf
+        # gradients stay None (the scan treats them as zero)
+        g_stoch, g_deter, g_logit = (l.grad for l in leaves)
         if g_feat is not None:
             if self.rssm.takes_extra_grads(g_feat.shape[0]):
                 self.rssm._bwd_extra = (g_feat[..., :SK], g_feat[..., SK:])
-            else:  # 16-row scan chunks (B > 16): each chunk's backward sees its slice of the summed gradient
-                g_stoch = lg[0] + g_feat[..., :SK].reshape(lg[0].shape)
-                g_deter = lg[1] + g_feat[..., SK:]
+            else:
+                g_stoch = g_feat[..., :SK].reshape(leaves[0].shape) + (0 if g_stoch is None else g_stoch)
+                g_deter = g_feat[..., SK:] + (0 if g_deter is None else g_deter)
+        outs = [(o, g) for o, g in zip((st["post_stoch"], st["post_deter"], st["post_logit"]), (g_stoch, g_deter, g_logit))
+                if g is not None]
         st["scan_wgrads"] = []
+        if not outs:  # nothing reads the posterior (no gradient): the extra summands alone drive the scan backward
+            outs = [(st["post_logit"], torch.zeros_like(st["post_logit"]))]
         if defer:
             with ops.defer_wgrads(st["scan_wgrads"]):
-                torch.autograd.backward([st["post_stoch"], st["post_deter"], st["post_logit"]],
-                                        [g_stoch, g_deter, lg[2]])
+                torch.autograd.backward([o for o, _ in outs], [g for _, g in outs])
         else:
-            torch.autograd.backward([st["post_stoch"], st["post_deter"], st["post_logit"]], [g_stoch, g_deter, lg[2]])
+            torch.autograd.backward([o for o, _ in outs], [g for _, g in outs])
         self.rssm._bwd_tr = None
         self._mark("scan_bwd")
 
@@ -957,12 +972,12 @@ class Dreamer(nn.Module):
                     d = torch.where(d < 1e-8, torch.zeros_like(d), d)
                     losses[key] = d.sum(list(range(2, d.dim()))).mean()
         elif self.rep_loss == "infonce":  # dreamer.py:533-542
-            x1 = self.prj(feat.reshape(B * T, -1))
+            x1 = self.prj(feat).reshape(B * T, -1)
             losses["infonce"] = parallel.infonce(x1, embed.reshape(B * T, -1), self.world)
         elif self.rep_loss == "dreamerpro":  # dreamer.py:543-566
             losses.update(self._proto_losses(data, initial, seed, ro))
         else:
-            x1 = self.prj(feat.reshape(B * T, -1))
+            x1 = self.prj(feat).reshape(B * T, -1)
             if self.r2_aug is not None:  # encoder on a randomly translated view, no gradient (dreamer.py:506-520)
                 with torch.no_grad():
                     pad, same, bil = self.r2_aug

@@ -279,13 +279,16 @@ def rmsnorm_fwd(x, w, act=1, y=None, rstd=None):
 def rmsnorm_bwd(x, w, rstd, dy, act=1, dx=None, dw=None, accumulate_dx=False, accumulate_dw=True):
     N = x.shape[-1]
     M = x.numel() // N
-    dy = _c(dy)
+    if dy.dim() == 2 and dy.shape[1] == N and dy.stride(1) == 1 and not dy.is_contiguous():
+        ldy = dy.stride(0)  # a column block of a wider gradient, read in place
+    else:
+        dy, ldy = _c(dy), N
     dx = torch.empty_like(x) if dx is None else dx
     part = None
     if dw is not None:
         nb = nat.fns["sd_rmsnorm_bwd_blocks"](M, N)
         part = torch.empty(nb * N, dtype=torch.float32, device=x.device)
-    nat.call("sd_rmsnorm_bwd", p(x), p(w), p(rstd), p(dy), p(dx), p(dw), p(part), M, N, int(act),
+    nat.call("sd_rmsnorm_bwd_ld", p(x), p(w), p(rstd), p(dy), ldy, p(dx), p(dw), p(part), M, N, int(act),
              int(accumulate_dx), int(accumulate_dw), stream())
     return dx
 
@@ -527,21 +530,32 @@ def conv2d_dgrad(dout, w, pad=None, fast=True, direct=True):
     return conv2d_fwd(dout, wf, None, pad=pad)
 
 
-def conv2d_wgrad(x, dout, kh, kw, ups=0, pad=None, fast=True):
+def _wgrad_acc(acc):
+    """(dw, db, ci_w) -> sd_wgrad_acc address (the launch adds [dW | db] into them), or None"""
+    if acc is None:
+        return None, None
+    a = nat.WgradAcc()
+    a.dw, a.db, a.ci_w = p(_c(acc[0])), p(_c(acc[1])), int(acc[2])
+    return a, ctypes.addressof(a)
+
+
+def conv2d_wgrad(x, dout, kh, kw, ups=0, pad=None, fast=True, acc=None):
     """returns (Co, kh*kw*Ci + 1) = [dW | db]. fast: split-bf16 direct kernel (sd_conv2d_wgrad_bf16x3) where eligible
-    (Ci >= 16; the 4-channel first layer keeps the f32 direct kernel)."""
+    (Ci >= 16; the 4-channel first layer keeps the f32 direct kernel). acc = (dw, db, ci_w): the result is added into
+    those parameter gradients by the launch's own reduction instead (returns None)."""
     Nb, H, W, Ci = x.shape
     Co = dout.shape[-1]
     pad = (kh - 1) // 2 if pad is None else pad
     J = kh * kw * Ci
+    keep, ap = _wgrad_acc(acc)
     if fast and FAST_GEMM:
         ks = nat.fns["sd_conv2d_wgrad_bf16x3_slabs"](Nb, H, W, Ci, Co, kh, kw, ups)
         if ks > 0:
             out = torch.empty(Co, J + 1, dtype=torch.float32, device=x.device)
             ws = torch.empty(ks * Co * (J + 1), dtype=torch.float32, device=x.device) if ks > 1 else None
             if nat.call_shaped("sd_conv2d_wgrad_bf16x3", p(_c(x)), p(_c(dout)), p(out), p(ws),
-                               ws.numel() if ws is not None else 0, Nb, H, W, Ci, Co, kh, kw, pad, stream()):
-                return out
+                               ws.numel() if ws is not None else 0, Nb, H, W, Ci, Co, kh, kw, pad, ap, stream()):
+                return None if acc is not None else out
     pixels = dout.numel() // Co
     ks = max(1, min(256, pixels // 4096))
     tiles = -(-Co // 64) * -(-(J + 1) // 64)
@@ -550,8 +564,9 @@ def conv2d_wgrad(x, dout, kh, kw, ups=0, pad=None, fast=True):
     ks = nat.fns["sd_conv2d_wgrad_slabs"](Nb, H, W, Ci, Co, kh, kw, ups, ks)
     ws = torch.empty(ks * Co * (J + 1), dtype=torch.float32, device=x.device) if ks > 1 else None
     nat.call("sd_conv2d_wgrad", p(_c(x)), p(_c(dout)), p(out), p(ws), ws.numel() if ws is not None else 0, ks,
-             Nb, H, W, Ci, Co, kh, kw, pad, ups, stream())
-    return out
+             Nb, H, W, Ci, Co, kh, kw, pad, ups, ap, stream())
+    del keep
+    return None if acc is not None else out
 
 
 def conv2d_wgrad_pool_slabs(x, Co, kh, kw):
@@ -560,7 +575,7 @@ def conv2d_wgrad_pool_slabs(x, Co, kh, kw):
     return nat.fns["sd_conv2d_wgrad_pool_slabs"](Nb, H, W, Ci, Co, kh, kw)
 
 
-def conv2d_wgrad_pool(x, dpool, amax, kh, kw, pad=None):
+def conv2d_wgrad_pool(x, dpool, amax, kh, kw, pad=None, acc=None):
     """[dW | db] (Co, kh*kw*Ci + 1) of a pooled stage from the max-pool backward's pooled-resolution gradient and the
     forward's argmax (the f32 direct kernel expands them while staging; the same products as conv2d_wgrad on the
     expanded gradient, summed in 512-pixel row blocks instead of 128: reordered f32 sums, ~2e-5 relative)."""
@@ -573,9 +588,11 @@ def conv2d_wgrad_pool(x, dpool, amax, kh, kw, pad=None):
         raise nat.NativeError("sd_conv2d_wgrad_pool: shape outside the direct kernel")
     out = torch.empty(Co, J + 1, dtype=torch.float32, device=x.device)
     ws = torch.empty(ks * Co * (J + 1), dtype=torch.float32, device=x.device)
+    keep, ap = _wgrad_acc(acc)
     nat.call("sd_conv2d_wgrad_pool", p(_c(x)), p(_c(dpool)), p(_c(amax)), p(out), p(ws), ws.numel(), Nb, H, W, Ci, Co,
-             kh, kw, pad, stream())
-    return out
+             kh, kw, pad, ap, stream())
+    del keep
+    return None if acc is not None else out
 
 
 _FLIP = {}  # weight data_ptr -> flipped weight, built ahead of the backward (set_flip_cache)

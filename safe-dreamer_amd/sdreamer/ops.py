@@ -61,9 +61,28 @@ def flush_wgrads(bucket):
     bucket.clear()
 
 
+class DxSink:
+    """One input-gradient buffer shared by several linear layers that read the same tensor x (the world-model heads
+    and the replay value head on the posterior feat, dreamer.py:571-660): each layer's backward adds its x gradient
+    into `buf` inside its own GEMM (beta = 1 after the first writer) and returns no gradient to autograd, so the
+    pairwise autograd adds, the slice-backward copies of the concatenated feat and the leaf-gradient copies are never
+    launched. Mark an input with `sink(x, s)`; `written` tells whether any layer's gradient arrived."""
+
+    def __init__(self, like):
+        self.buf = torch.empty(like.shape, dtype=torch.float32, device=like.device)
+        self.written = False
+
+
+def sink(x, s):
+    """x with its linear layers' input gradients routed into DxSink s (the attribute does not survive a view)"""
+    x._dx_sink = s
+    return x
+
+
 class LinearFn(torch.autograd.Function):
     """nn.Linear (y = x W^T + b). Gradients on the split-bf16 GEMM (k.gemm fast=True, ~1e-5 relative); the forward
-    too when `fast` (imagined-trajectory heads: no sampled index depends on them)."""
+    too when `fast` (imagined-trajectory heads: no sampled index depends on them). An input marked with a DxSink gets
+    its gradient accumulated there instead of returned."""
 
     @staticmethod
     def forward(ctx, x, w, b, fast=False):
@@ -71,6 +90,7 @@ class LinearFn(torch.autograd.Function):
         y = k.mm(x2, w.t(), bias=b, fast=fast)
         ctx.save_for_backward(x2, w, b)
         ctx.in_shape = x.shape
+        ctx.dx_sink = getattr(x, "_dx_sink", None)
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -78,7 +98,11 @@ class LinearFn(torch.autograd.Function):
         x2, w, b = ctx.saved_tensors
         dy2 = _flat(dy).contiguous()
         dx = None
-        if ctx.needs_input_grad[0]:
+        sk = ctx.dx_sink
+        if sk is not None:
+            k.mm(dy2, w, out=sk.buf.view(-1, w.shape[1]), beta=1.0 if sk.written else 0.0, fast=True)
+            sk.written = True
+        elif ctx.needs_input_grad[0]:
             dx = k.mm(dy2, w, fast=True).view(ctx.in_shape)
 
         def wgrad():
@@ -212,10 +236,13 @@ class CatIntoFn(torch.autograd.Function):
             base = out.reshape(rows, F)
             k.layout_copies([(a, base, 1, rows, na, 0, na, na, 1, F), (b, base[:, na:], 1, rows, nb, 0, nb, nb, 1, F)])
         ctx.split = na
+        ctx.set_materialize_grads(False)  # consumers that route their gradient into a DxSink send none here
         return out
 
     @staticmethod
     def backward(ctx, g):
+        if g is None:
+            return None, None, None
         return g[..., :ctx.split], g[..., ctx.split:], None
 
 
@@ -254,24 +281,23 @@ class ConvPoolNormFn(torch.autograd.Function):
         x, w, b, nw, pooled, amax, rstd = ctx.saved_tensors
         Nb, H, W, _ = x.shape
         Co, kh, kw, Ci = w.shape
+        acc = (grad_buf(w), grad_buf(b), Ci)  # the bwd-weight launches add into the gradients themselves
         if not ctx.needs_input_grad[0] and POOL_COMPACT and k.conv2d_wgrad_pool_slabs(x, Co, kh, kw) > 0:
             # first stage (no input gradient): the bwd-weight kernel expands the pooled gradient + argmax itself, so
             # the full-resolution conv gradient (3/4 zeros) is never written or read
             dpool = k.pool_rms_bwd_compact(pooled, amax, nw, rstd, dy.contiguous(), grad_buf(nw), nchw_flat=ctx.nchw_flat)
-            dwdb = k.conv2d_wgrad_pool(x, dpool, amax, kh, kw)
+            k.conv2d_wgrad_pool(x, dpool, amax, kh, kw, acc=acc)
             dconv = None
         else:
             dconv = k.pool_rms_bwd(pooled, amax, nw, rstd, dy.contiguous(), H, W, grad_buf(nw), nchw_flat=ctx.nchw_flat)
-            dwdb = None
         Cx = x.shape[-1]
 
-        def wgrad(dwdb=dwdb):
-            if dwdb is None:
-                dwdb = k.conv2d_wgrad(x, dconv, kh, kw)
-            grad_buf(w).add_(dwdb[:, :-1].reshape(Co, kh, kw, Cx)[..., :Ci])
-            grad_buf(b).add_(dwdb[:, -1])
+        def wgrad():
+            k.conv2d_wgrad(x, dconv, kh, kw, acc=acc)
 
-        if _DEFER is not None and dwdb is None:  # queued: only the data gradient continues the backward chain
+        if dconv is None:
+            pass
+        elif _DEFER is not None:  # queued: only the data gradient continues the backward chain
             _DEFER.append((wgrad, (x, dconv)))
         else:
             wgrad()
@@ -297,9 +323,7 @@ class UpConvFn(torch.autograd.Function):
         x, w, b = ctx.saved_tensors
         Co, kh, kw, Ci = w.shape
         dy = dy.contiguous()
-        dwdb = k.conv2d_wgrad(x, dy, kh, kw, ups=1)
-        grad_buf(w).add_(dwdb[:, :-1].reshape(w.shape))
-        grad_buf(b).add_(dwdb[:, -1])
+        k.conv2d_wgrad(x, dy, kh, kw, ups=1, acc=(grad_buf(w), grad_buf(b), Ci))
         dx = None
         if ctx.needs_input_grad[0]:
             du = k.conv2d_dgrad(dy, w)

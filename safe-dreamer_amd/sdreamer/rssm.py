@@ -66,6 +66,7 @@ def _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, work, stream_id=S
         setattr(d, k, P[k].data_ptr())
     d.no = P["no"].data_ptr()
     d.reset, d.x2, d.eproj = rt.data_ptr(), x2.data_ptr(), eproj.data_ptr()
+    d.reset_bm = 1  # the fused scan (this descriptor's only user) reads the batch-major (B, T) flags in place
     d.work = K.p(work)
     return d
 
@@ -326,8 +327,10 @@ class ObserveScan(torch.autograd.Function):
         dev = embed.device
         f32 = torch.float32
         M = T * B
-        rt = reset.t().contiguous()  # (T, B) uint8
         fused = _fused_scan_ok(rssm, B)
+        # reset flags: the fused scan reads the batch's (B, T) bytes in place (sd_rssm_scan.reset_bm); the per-op
+        # path walks time-major rows
+        rt = reset.contiguous() if fused else reset.t().contiguous()
         # ---- hoisted, recurrence-free work over all T*B rows. Fused scan: on the batch-major rows b*T + t, read by
         # the scan in place (bm_inputs); per-op path: time-major rows. The (M, E) embedding is never transposed
         # (emb_t: batch-major rows, see _wgrads).
@@ -408,6 +411,7 @@ class ObserveScan(torch.autograd.Function):
         ctx.save_for_backward(rt, a_n, x2p, r2, emb_t, s_in, h_in, x0p, x1p, r0, r1, xcat, hp, hh, rh, gates, deter,
                               op, oo, ro, logit)
         ctx.rssm, ctx.seed, ctx.row_offset, ctx.stream_id = rssm, seed, row_offset, stream_id
+        ctx.set_materialize_grads(False)  # a posterior output without a gradient reaches the backward as None
         ctx.dims = (B, T, A, E)
         ctx.fused = fused
         if fused:
@@ -506,6 +510,8 @@ class ObserveScan(torch.autograd.Function):
         e = lambda *shape: (torch.full(shape, float("nan"), dtype=f32, device=dev) if _POISON  # noqa: E731
                             else torch.empty(*shape, dtype=f32, device=dev))
         dl, d_o, d_op, d_x0p, d_x1p = e(T, B, SK), e(T, B, U), e(T, B, U), e(T, B, U), e(T, B, U)
+        ctx.d_op_b = e(B, T, U)  # the batch-major copy k_dgru writes beside d_op (operand of the embed gradient)
+        ctx.d_x2_b = e(B, T, U)  # the action branch's input gradient, batch-major (k_carry / k_dx01)
         d_gates, d_hh, d_hp, d_xcat = e(T, B, 3 * D), e(T, B, D), e(T, B, D), e(T, B, 3 * U)
         tr = rssm._bwd_tr if rssm._bwd_tr is not None else rssm.scan_bwd_weights()
         x2 = ctx.x2
@@ -519,6 +525,7 @@ class ObserveScan(torch.autograd.Function):
                                          ("d_xcat", d_xcat), ("d_x0p", d_x0p), ("d_x1p", d_x1p)]:
             setattr(d, k, v.data_ptr())
         d.d_stoch, d.d_deter, d.d_logit = K.p(ds_out), K.p(dd_out), K.p(dl_in)
+        d.d_op_bm, d.d_x2_bm = ctx.d_op_b.data_ptr(), ctx.d_x2_b.data_ptr()
         d.bm_grads = 1
         if extra is not None:
             gs2, gd2 = extra
@@ -540,10 +547,11 @@ class ObserveScan(torch.autograd.Function):
             the way to the encoder's gradient reads them)"""
             K.rmsnorm_bwd(f(op), P["no"], ro.reshape(M), f(d_o), dw=gb(P["no"]))
             K.rmsnorm_bwd(f(hp), P["nh"], rh.reshape(M), f(d_hh), dw=gb(P["nh"]))
-            K.rmsnorm_bwd(f(x0p), P["n0"], r0.reshape(M), f(d_xcat)[:, :U].contiguous(), dw=gb(P["n0"]))
-            K.rmsnorm_bwd(f(x1p), P["n1"], r1.reshape(M), f(d_xcat)[:, U:2 * U].contiguous(), dw=gb(P["n1"]))
-            # the action branch ran on batch-major rows (ObserveScan.forward, fused path)
-            return d_xcat[:, :, 2 * U:].transpose(0, 1).contiguous()
+            K.rmsnorm_bwd(f(x0p), P["n0"], r0.reshape(M), f(d_xcat)[:, :U], dw=gb(P["n0"]))  # column blocks in place
+            K.rmsnorm_bwd(f(x1p), P["n1"], r1.reshape(M), f(d_xcat)[:, U:2 * U], dw=gb(P["n1"]))
+            # the action branch ran on batch-major rows (ObserveScan.forward, fused path): k_carry / k_dx01 wrote
+            # its gradient batch-major too (d_x2_bm)
+            return ctx.d_x2_b
 
         norm_w.tensors = (op, hp, x0p, x1p, ro, rh, r0, r1, d_o, d_hh, d_xcat)
         return dl, d_op, d_gates, d_hp, d_x0p, d_x1p, norm_w
@@ -561,7 +569,8 @@ class ObserveScan(torch.autograd.Function):
         gb = ops.grad_buf
         f = lambda x: x.reshape(M, -1)  # noqa: E731
         # batch-major d_op (a (M, U) copy), so the embed gradient comes out in the encoder's (B, T, E) order directly
-        d_op_b = d_op.transpose(0, 1).reshape(M, -1).contiguous()
+        d_op_b = getattr(ctx, "d_op_b", None)
+        d_op_b = d_op.transpose(0, 1).reshape(M, -1).contiguous() if d_op_b is None else d_op_b.view(M, -1)
         d_emb = K.mm(d_op_b, P["Wo"][:, D:], fast=True)  # (M, E): the only output the encoder waits for
 
         def wgrads(d_x2=d_x2):
