@@ -17,5 +17,5 @@ db() { find $1 -name "*.db" | head -1; }
 python3 tools/prof_summary.py $(db /tmp/kt_$T) 15 > gpurun_out/${T}_kernel_summary.md
 python3 tools/roofline_traffic.py $(db /tmp/p2_$T) $(db /tmp/p3_$T) gpurun_out/${T}_roofline_traffic.json > /dev/null
 python3 tools/pmc_table.py /tmp/kt_$T /tmp/p1_$T /tmp/p2_$T /tmp/p3_$T /tmp/p4_$T > gpurun_out/${T}_pmc.md
-python3 tools/kernel_table.py /tmp/kt_$T 10 gpurun_out/${T}_kernel_table.json /tmp/p1_$T /tmp/p2_$T /tmp/p3_$T /tmp/p4_$T > gpurun_out/${T}_kernel_table.md
+KT_BENCH_LOG=gpurun_out/${T}_profiled_bench.log python3 tools/kernel_table.py /tmp/kt_$T 10 gpurun_out/${T}_kernel_table.json /tmp/p1_$T /tmp/p2_$T /tmp/p3_$T /tmp/p4_$T > gpurun_out/${T}_kernel_table.md
 head -8 gpurun_out/${T}_kernel_summary.md
