@@ -398,6 +398,10 @@ int sd_u8_to_f32(const uint8_t* in, float* out, long n, float shift, sd_stream s
 /* NHWC channel pad + shift: out[p][c] = in[p][c] - shift (c < C), 0 (C <= c < Cp). The ConvEncoder input
  * (obs - 0.5, networks.py:224) padded 3 -> 4 channels so the first conv takes the float4 / direct-wgrad paths. */
 int sd_pad_channels(const float* in, float* out, long pixels, int C, int Cp, float shift, sd_stream stream);
+/* Both float forms of a uint8 NHWC image in one launch: img = in / 255 (Dreamer.preprocess, nullable when nothing
+ * reads it) and enc = in / 255 - shift zero-padded to Cp channels (the ConvEncoder input, networks.py:224). */
+int sd_u8_image_inputs(const uint8_t* in, float* img, float* enc, long pixels, int C, int Cp, float shift,
+                       sd_stream stream);
 /* symlog (distributions.py:8-9) for MLP-encoder inputs (networks.py:333-334) */
 int sd_symlog(const float* x, float* y, long n, sd_stream stream);
 int sd_fill_gumbel(float* out, long n, uint64_t seed, int stream_id, int step, long offset, sd_stream stream);

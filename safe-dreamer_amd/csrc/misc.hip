@@ -17,6 +17,24 @@ __global__ void u8_to_f32(const uint8_t* __restrict__ in, float* __restrict__ ou
   if (i < n) out[i] = (float)in[i] / 255.0f - shift;
 }
 
+// the replay image to both float forms in one pass: img[p][c] = u8 / 255 (Dreamer.preprocess; nullable) and the
+// ConvEncoder input enc[p][c] = u8 / 255 - shift, zero-padded to Cp channels (the same two roundings as
+// sd_u8_to_f32 followed by sd_pad_channels). One thread per pixel.
+__global__ void u8_image_inputs_kernel(const uint8_t* __restrict__ in, float* __restrict__ img, float* __restrict__ enc,
+                                       long pixels, int C, int Cp, float shift) {
+  const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= pixels) return;
+  for (int c = 0; c < Cp; ++c) {
+    float v = 0.f;
+    if (c < C) {
+      const float f = (float)in[pix * C + c] / 255.0f;
+      if (img) img[pix * C + c] = f;
+      v = f - shift;
+    }
+    enc[pix * Cp + c] = v;
+  }
+}
+
 // out[p][c] = in[p][c] - shift for c < C, 0 for C <= c < Cp (channel-pad an NHWC image to a float4 multiple)
 __global__ void pad_channels_kernel(const float* __restrict__ in, float* __restrict__ out, long pixels, int C, int Cp,
                                     float shift) {
@@ -531,6 +549,14 @@ extern "C" int sd_trace_mark(int tag, sd_stream s) {
 extern "C" int sd_u8_to_f32(const uint8_t* in, float* out, long n, float shift, sd_stream s) {
   if (n <= 0) return SD_OK;
   u8_to_f32<<<nb(n), 256, 0, (hipStream_t)s>>>(in, out, n, shift);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
+extern "C" int sd_u8_image_inputs(const uint8_t* in, float* img, float* enc, long pixels, int C, int Cp, float shift,
+                                  sd_stream s) {
+  if (pixels <= 0) return SD_OK;
+  if (C < 1 || Cp < C || !in || !enc) return SD_EARG;
+  u8_image_inputs_kernel<<<nb(pixels), 256, 0, (hipStream_t)s>>>(in, img, enc, pixels, C, Cp, shift);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

@@ -308,9 +308,20 @@ class Dreamer(nn.Module):
         return self.rep_loss == "dreamerpro" and self._ema_updates < self._pro["freeze"]
 
     @torch.no_grad()
-    def preprocess(self, data):  # dreamer.py:709-713
+    def preprocess(self, data, enc_input=False):  # dreamer.py:709-713
+        """enc_input: also form the ConvEncoder's input (image / 255 - 0.5, channel-padded) in the same launch
+        ("__enc_image", read by MultiEncoder); the f32 image itself is then written only when a loss reads it
+        (decoder, augmented views), else "image" stays the uint8 replay bytes."""
         if "image" in data and data["image"].dtype == torch.uint8:
-            data["image"] = K.u8_to_f32(data["image"].contiguous())
+            u8 = data["image"].contiguous()
+            C = u8.shape[-1]
+            if enc_input and C % 4 and self.encoder.cnn_shapes and list(self.encoder.cnn_shapes) == ["image"]:
+                need = self.rep_loss in ("dreamer", "dreamerpro") or getattr(self, "r2_aug", None) is not None
+                f, data["__enc_image"] = K.u8_image_inputs(u8, (C + 3) // 4 * 4, 0.5, need_f32=need)
+                if f is not None:
+                    data["image"] = f
+            else:
+                data["image"] = K.u8_to_f32(u8)
         return data
 
     @torch.no_grad()
@@ -434,7 +445,7 @@ class Dreamer(nn.Module):
         self._eager_updates += 1
         if self.marks is not None:
             self.marks.reset()
-        p_data = self.preprocess(dict(data))
+        p_data = self.preprocess(dict(data), enc_input=True)
         self._update_slow_target()
         if self.rep_loss == "dreamerpro":
             self.ema_update()
@@ -505,7 +516,7 @@ class Dreamer(nn.Module):
         """Graph phase P (main): preprocess, Polyak, zero_grad, encoder + posterior scan."""
         if self.marks is not None:
             self.marks.reset()
-        p_data = self.preprocess(dict(data))
+        p_data = self.preprocess(dict(data), enc_input=True)
         self._polyak()
         if self.rep_loss == "dreamerpro":  # replays run with ema_update_every == 1 and past update 0
             self._ema_apply(self._pro["frac"])
@@ -981,7 +992,7 @@ class Dreamer(nn.Module):
             if self.r2_aug is not None:  # encoder on a randomly translated view, no gradient (dreamer.py:506-520)
                 with torch.no_grad():
                     pad, same, bil = self.r2_aug
-                    aug = dict(data)
+                    aug = {k: v for k, v in data.items() if k != "__enc_image"}  # the encoder re-forms its input
                     aug["image"] = K.random_translate(data["image"], pad, seed, ro, same, bil)
                     x2 = self.encoder(aug).reshape(B * T, -1)
             else:
@@ -1013,7 +1024,7 @@ class Dreamer(nn.Module):
         B, T = data["action"].shape[:2]
         Bg = B * self.world
         with torch.no_grad():
-            aug = {k: torch.cat([v, v], 0) for k, v in data.items()}
+            aug = {k: torch.cat([v, v], 0) for k, v in data.items() if k != "__enc_image"}
             img = data["image"]
             aug["image"] = torch.cat([K.random_translate(img, c["pad"], seed, ro, c["same"], c["bilinear"]),
                                       K.random_translate(img, c["pad"], seed, Bg + ro, c["same"], c["bilinear"])], 0)

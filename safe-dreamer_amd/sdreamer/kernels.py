@@ -467,6 +467,17 @@ def u8_to_f32(img, shift=0.0, out=None):
     return out
 
 
+def u8_image_inputs(img, Cp, shift, need_f32=True):
+    """uint8 (..., H, W, C) -> (img / 255 as f32 or None, encoder input img / 255 - shift padded to Cp channels), one
+    launch"""
+    C = img.shape[-1]
+    pixels = img.numel() // C
+    f = torch.empty(img.shape, dtype=torch.float32, device=img.device) if need_f32 else None
+    enc = torch.empty(*img.shape[:-1], Cp, dtype=torch.float32, device=img.device)
+    nat.call("sd_u8_image_inputs", p(_c(img)), p(f), p(enc), pixels, C, Cp, float(shift), stream())
+    return f, enc
+
+
 def pad_channels(x, Cp, shift=0.0):
     """NHWC (..., C) -> (..., Cp): x - shift, zero channels appended."""
     x = _c(x)

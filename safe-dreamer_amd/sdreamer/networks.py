@@ -362,10 +362,15 @@ class MultiEncoder(nn.Module):
         outs = []
         for kind, enc in zip(self.kinds, self.encoders):
             if kind == "cnn":
-                img = torch.cat([obs[k] for k in self.cnn_shapes], -1) if len(self.cnn_shapes) > 1 else obs[next(iter(self.cnn_shapes))]
+                pre = obs.get("__enc_image")  # formed by Dreamer.preprocess(enc_input=True) from the uint8 bytes
+                img = pre if pre is not None else (
+                    torch.cat([obs[k] for k in self.cnn_shapes], -1) if len(self.cnn_shapes) > 1
+                    else obs[next(iter(self.cnn_shapes))])
                 BT = img.shape[:-3]
                 x = img.reshape(-1, *img.shape[-3:])
-                if x.shape[-1] % 4:  # obs - 0.5 (networks.py:224), zero-padded to a float4 channel multiple
+                if pre is not None:
+                    pass
+                elif x.shape[-1] % 4:  # obs - 0.5 (networks.py:224), zero-padded to a float4 channel multiple
                     x = K.pad_channels(x.contiguous(), (x.shape[-1] + 3) // 4 * 4, 0.5)
                 else:
                     x = x - 0.5  # ConvEncoder.forward, networks.py:224
