@@ -14,6 +14,9 @@ using namespace sdb;
 #define SD_G3_FP 0
 #endif
 
+#ifndef SD_G3_M256  // 256 x 128 tiles for the weight-gradient shape (gemm3_run)
+#define SD_G3_M256 0  // measured slower: actor L0 dW 250.7 vs 194.2 us (1 workgroup per CU hides less latency)
+#endif
 #ifndef SD_G3_XCD  // XCD-contiguous tile order (below)
 #define SD_G3_XCD 1
 #endif
@@ -43,7 +46,7 @@ SD_DEV void g3_tile(const GemmArgs& g, int& tx, int& ty, int& tz) {
 }
 
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool VA, bool VB, bool RS = false>
-__global__ __launch_bounds__(256, 2) void gemm3_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256, (BM >= 256 ? 1 : 2)) void gemm3_kernel(GemmArgs g) {
   int tx, ty, tz;
   g3_tile(g, tx, ty, tz);
   const int bn0 = tx * BN, bm0 = ty * BM;
@@ -102,6 +105,7 @@ void launch3_tile(const GemmArgs& g, bool va, bool vb, hipStream_t st) {
 template <bool AK, bool BKC>
 void launch3_layout(const GemmArgs& g, int tile, bool va, bool vb, hipStream_t st) {
   if (tile == 0) launch3_tile<128, 128, 64, 64, AK, BKC>(g, va, vb, st);
+  else if (tile == 2 && !AK && !BKC) launch3_tile<256, 128, 128, 64, AK, BKC>(g, va, vb, st);
   else launch3_tile<64, 64, 32, 32, AK, BKC>(g, va, vb, st);
 }
 
@@ -359,11 +363,15 @@ int gemm3_run(const sd_gemm_desc* d, float* workspace, long workspace_floats, fl
   const bool va = al16_3(d->A) && d->lda % 4 == 0 && (d->batch == 1 || d->strideA % 4 == 0);
   const bool vb = al16_3(d->B) && d->ldb % 4 == 0 && (d->batch == 1 || d->strideB % 4 == 0);
   int tile = d->tile;
-  if (tile != 0 && tile != 1) {
+  const bool ak = d->a_kcontig != 0, bk = d->b_kcontig != 0;
+  if (tile != 0 && tile != 1 && tile != 2) {
     const long tiles128 = (long)sd_cdiv(d->M, 128) * sd_cdiv(d->N, 128) * d->batch * ks;
     tile = tiles128 >= 256 ? 0 : 1;
+    // weight-gradient shape (M <= 256 output rows, long split K, both operands rows-contiguous: dW = dy^T x): one
+    // 256-row tile covers every M, so each k chunk of x is read once instead of once per 128-row tile
+    if (SD_G3_M256 && !ak && !bk && d->M > 128 && d->M <= 256 && ks > 1 && g.kchunk >= 512 && tile == 0) tile = 2;
   }
-  const bool ak = d->a_kcontig != 0, bk = d->b_kcontig != 0;
+  if (tile == 2 && (ak || bk)) tile = 0;
   if (ak && bk) launch3_layout<true, true>(g, tile, va, vb, stream);
   else if (ak) launch3_layout<true, false>(g, tile, va, vb, stream);
   else if (bk) launch3_layout<false, true>(g, tile, va, vb, stream);

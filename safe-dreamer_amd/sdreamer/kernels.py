@@ -77,14 +77,28 @@ def _auto_split(M, N, K, batch):
 FAST_GEMM = os.environ.get("SDREAMER_FAST_GEMM", "1") != "0"
 
 
+# workgroups a long-K split-bf16 GEMM aims for: 512 (2 per CU). Alone the 256 x 2560 x 15360 weight gradient runs
+# faster with more (1024: 157 vs 192 us), but in the update, beside the latency-bound scan backward, 512 measured
+# best (11.70 vs 11.80 ms at 1024, 11.76 at 2048 per update; gpurun_out r04v)
+_G3_WG_TARGET = int(os.environ.get("SDREAMER_G3_WGS", "512"))
+
+
 def _fast_split(M, N, K, batch):
-    """K split for the split-bf16 kernel: ~512 workgroups of 128x128 tiles (2 per CU) when K is long; the launcher
-    falls back to 64x64 tiles below 256 workgroups."""
+    """K split for the split-bf16 kernel: ~_G3_WG_TARGET workgroups of 128x128 tiles when K is long, preferring a
+    split that cuts K into equal whole 32-deep tiles; the launcher falls back to 64x64 tiles below 256 workgroups.
+    (The 256 x 2560 x 15360 weight gradient alone: 13 splits 192 us, 20 157 us, 30 155 us, 60 186 us —
+    tools/wgrad_sweep.py.)"""
     tiles = -(-M // 128) * -(-N // 128) * batch
     if tiles >= 256:
         return 1
     if K >= 1024:
-        return max(1, min(K // 512, -(-512 // tiles), 32))
+        cap = max(1, min(K // 512, -(-_G3_WG_TARGET // tiles), 32))
+        if K % 32 == 0:
+            kt = K // 32
+            even = [d for d in range(cap, 0, -1) if kt % d == 0]
+            if even and even[0] * 2 > cap:
+                return even[0]
+        return cap
     # short K (e.g. the replay-value head on ~1k rows): 64x64 tiles, split so the launch still has ~256 workgroups
     t64 = -(-M // 64) * -(-N // 64) * batch
     if t64 >= 128 or K < 256:
