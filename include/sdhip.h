@@ -532,15 +532,18 @@ typedef struct sd_imagine {
                          fp32 (null: kept in `work` only); the policy loss's actor forward starts from it */
   const float* noise_img; /* optional (H1 - 1, N, SK): the prior samples' Gumbel noise, drawn ahead by
                              sd_imagine_noise (null: drawn inside the sampler); the same values either way */
+  const float* noise_act; /* optional (H1, N, A): the action samples' noise (N(0,1) for a bounded-normal actor, Gumbel
+                             for one-hot; stream stream_act, step t), drawn ahead by sd_imagine_noise */
   uint64_t* trace;        /* measurement aid, -DSD_SCAN_TRACE builds only (NULL otherwise): per launch slot
                              (t * 16 + launch of the step) and workgroup, entry / staged / contracted / exit timestamps */
 } sd_imagine;
 int sd_imagine_work_floats(const sd_imagine* d);
 int sd_imagine_run(const sd_imagine* d, sd_stream stream);
 /* noise (H1 - 1, N, SK) = the Gumbel noise of every imagined prior sample (Philox stream d->stream_img, step t, element
- * (row + row_offset) * SK + k; the effective seed read on the device as sd_imagine_run reads it): one full-chip launch
- * instead of the per-step sampler epilogues computing it. */
-int sd_imagine_noise(const sd_imagine* d, float* noise, sd_stream stream);
+ * (row + row_offset) * SK + k; the effective seed read on the device as sd_imagine_run reads it), and when noise_act
+ * is non-null (H1, N, A) the action samples' noise (stream d->stream_act, element (row + row_offset) * A + j): one
+ * full-chip launch instead of the per-step sampler epilogues computing them (the f64 transforms leave the chain). */
+int sd_imagine_noise(const sd_imagine* d, float* noise, float* noise_act, sd_stream stream);
 /* Measurement aid (bench.py roofline): one launch of step t's largest contractions exactly as sd_imagine_run issues
  * them, after a run on the same descriptor/workspace: which = 0: img_net_0 + _dyn_in0 + actor layer 0's deter part
  * (three (N, D) x (D, U) GEMMs, k_lin), 1: _dyn_hid (k_hid), 2: _dyn_gru + GRU (k_gate). 0 <= t < H1 - 1. Launches 0

@@ -226,12 +226,13 @@ __global__ __launch_bounds__(256) void k_presplit6_gate(const float* Wg, int D, 
   split3_store(out + (((long)ct * nkt + k / BK6) * 96 + lr) * PRE_ROW + k % BK6, ld4(Wg + wrow * Dg + k));
 }
 template <int BN>
-__global__ __launch_bounds__(256) void k_presplit6(const float* W, int rows, int K, __bf16* out) {
+__global__ __launch_bounds__(256) void k_presplit6(const float* W, int rows, int K, __bf16* out, long ldw = 0) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   const int nq = K / 4;
   if (i >= (long)rows * nq) return;
   const int n = (int)(i / nq), k = 4 * (int)(i % nq), nkt = K / BK6;
-  split3_store(out + (((long)(n / BN) * nkt + k / BK6) * BN + n % BN) * PRE_ROW + k % BK6, ld4(W + (long)n * K + k));
+  split3_store(out + (((long)(n / BN) * nkt + k / BK6) * BN + n % BN) * PRE_ROW + k % BK6,
+               ld4(W + (long)n * (ldw ? ldw : K) + k));
 }
 
 // Pre-split ACTIVATION images (KH_APRE): the same BPre6 tile layout for a (rows, K) activation — tile (row / 64,
@@ -426,6 +427,33 @@ __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2,
   mainloop<F6_LIN, FP_LIN, BM, BN, 16, WN, pf_of(KL_PF)>(a0, b0, 0, p.K, acc);
   SD_TR(2)
   ep_bias_part<BM, BN, WN, (WN < 32 ? WN : 32)>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
+  SD_TR_END(tr.p, tr.slot)
+}
+
+// k_lin on the bf16x6 path with both operands pre-split (KL_PRE): A = deter' from the image k_gate already wrote for
+// the next k_hid (64-row tiles), B = the three weights' images (built once per imagination), so the main loop only
+// copies bf16 planes into LDS (no split VALU) and runs at the bf16 MFMA rate (six products per fp32 product:
+// fp32-accurate, gemm6_core.h). Same outputs and row partials (KL3_PW wide) as k_lin<KL3_BM, KL3_BN>.
+#ifndef KL_PRE
+#define KL_PRE 1
+#endif
+template <int BN>
+__global__ __launch_bounds__(256) void k_lin6(const __bf16* aimg, int K, const __bf16* w0, const __bf16* w1,
+                                              const __bf16* w2, LinProb p0, LinProb p1, LinProb p2, int M, Tr tr) {
+  SD_TR_BEGIN
+  constexpr int BM = 64, WN = BN;  // 4 waves x 16 rows, each the tile's BN columns
+  static_assert(WN % KL3_PW == 0, "row partials");
+  int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
+  if (KL_XCD) xcd_tile(tx, ty, tz);
+  const LinProb p = tz == 0 ? p0 : (tz == 1 ? p1 : p2);
+  const __bf16* wimg = tz == 0 ? w0 : (tz == 1 ? w1 : w2);
+  const int n0 = tx * BN, m0 = ty * BM;
+  f32x4 acc[1][WN / 16];
+  SD_TR(1)
+  mainloop<true, FP_LIN, BM, BN, 16, WN, pf_of(KL_PF)>(BPre6<BM>(aimg, m0 / BM, K / BK6, 0),
+                                                      BPre6<BN>(wimg, tx, K / BK6, 0), 0, K, acc);
+  SD_TR(2)
+  ep_bias_part<BM, BN, WN, KL3_PW>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
   SD_TR_END(tr.p, tr.slot)
 }
 
@@ -1109,8 +1137,10 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
   if (x2w)
     for (int i = threadIdx.x; i < U * A; i += 256) w2s[i] = d.W2[i];
   const f32x4 b2 = ld4(d.b2 + 4 * lane), n2 = ld4(d.n2 + 4 * lane);
-  float nz = 0.f;  // the action noise of element (m, lane)
-  if (d.act_discrete) {
+  float nz = 0.f;  // the action noise of element (m, lane): drawn ahead (sd_imagine_noise) or here
+  if (d.noise_act) {
+    if (live && lane < A) nz = d.noise_act[((long)t * M + m) * A + lane];
+  } else if (d.act_discrete) {
     if (lane < A) nz = sd_gumbel(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lane);
   } else if (lane < A) {
     nz = sd_normal(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lane);
@@ -1463,8 +1493,18 @@ __global__ __launch_bounds__(256) void k_imgprior(sd_imagine d, const float* X, 
 
 // noise[t][m][k] = sd_gumbel(seed, stream_img, t, (m + row_offset) * SK + k) for t < H1 - 1: one thread per 4
 // consecutive k, which share one Philox block (sd_gumbel's word idx & 3), one float4 store
-__global__ __launch_bounds__(256) void k_imag_noise(sd_imagine d, float* noise) {
+__global__ __launch_bounds__(256) void k_imag_noise(sd_imagine d, float* noise, float* noise_act) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x, per_t = (long)d.N * d.SK / 4;
+  const long nact = noise_act ? (long)d.H1 * d.N * d.A : 0;
+  if (i < nact) {  // the action noise: the value k_action_rows would draw for (step, row, element)
+    const int t = (int)(i / ((long)d.N * d.A));
+    const long r = i - (long)t * d.N * d.A, m = r / d.A;
+    const int j = (int)(r % d.A);
+    const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+    const uint64_t e = (uint64_t)(m + d.row_offset) * d.A + j;
+    noise_act[i] = d.act_discrete ? sd_gumbel(seed, (uint32_t)d.stream_act, (uint32_t)t, e)
+                                  : sd_normal(seed, (uint32_t)d.stream_act, (uint32_t)t, e);
+  }
   if (i >= (long)(d.H1 - 1) * per_t) return;
   const int t = (int)(i / per_t);
   const long r = i - (long)t * per_t, m = r / (d.SK / 4), k = 4 * (r % (d.SK / 4));
@@ -1483,6 +1523,7 @@ struct IWork {
   __bf16 *wh6, *wg6;  // pre-split _dyn_hid / _dyn_gru weights (BPre6 images, 3 bf16 per element)
   float *waT, *w1T;   // actor layer 0's stoch columns and _dyn_in1, transposed (SK, U) for k_onehot_lin
   __bf16 *h6, *x16, *x26;  // pre-split activation images (KH_APRE): deter, silu(rms(x1p)), x2; rows padded to 64
+  __bf16 *wi6, *w06, *wad6;  // pre-split img_net_0 / _dyn_in0 / actor layer 0 (deter columns) weights (KL_PRE)
   long total;
 };
 long al64(long n) { return (n + 63) / 64 * 64; }
@@ -1508,6 +1549,9 @@ IWork iwork(const sd_imagine& d, float* base) {
   w.h6 = reinterpret_cast<__bf16*>(take(rows * d.D * 3 / 2));
   w.x16 = reinterpret_cast<__bf16*>(take(rows * d.U * 3 / 2));
   w.x26 = reinterpret_cast<__bf16*>(take(rows * d.U * 3 / 2));
+  w.wi6 = reinterpret_cast<__bf16*>(take((long)d.U * d.D * 3 / 2));
+  w.w06 = reinterpret_cast<__bf16*>(take((long)d.U * d.D * 3 / 2));
+  w.wad6 = reinterpret_cast<__bf16*>(take((long)d.U * d.D * 3 / 2));
   w.total = o;
   return w;
 }
@@ -1526,13 +1570,14 @@ int icheck(const sd_imagine* d) {
 
 }  // namespace
 
-extern "C" int sd_imagine_noise(const sd_imagine* dp, float* noise, sd_stream stream_) {
+extern "C" int sd_imagine_noise(const sd_imagine* dp, float* noise, float* noise_act, sd_stream stream_) {
   const int rc = icheck(dp);
   if (rc) return rc;
   if (!noise || ((uintptr_t)noise & 15)) return SD_EARG;
-  const long n = (long)(dp->H1 - 1) * dp->N * dp->SK / 4;
+  long n = (long)(dp->H1 - 1) * dp->N * dp->SK / 4;
+  if (noise_act) n = n > (long)dp->H1 * dp->N * dp->A ? n : (long)dp->H1 * dp->N * dp->A;
   if (n <= 0) return SD_OK;
-  k_imag_noise<<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream_>>>(*dp, noise);
+  k_imag_noise<<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream_>>>(*dp, noise, noise_act);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
@@ -1613,11 +1658,25 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     k_presplit6_gate<<<(int)sd_cdiv((long)3 * D * (D / d.G) / 4, 256), 256, 0, st>>>(d.Wg, D, D / d.G, w.wg6);
     SD_LAUNCH_CHECK();
   }
+  // the deter contractions (img_net_0, _dyn_in0, actor layer 0's deter part) on pre-split operands: A is the deter
+  // image (apre), B the weights split once here (SDHIP_KL_NOPRE set: the fp32 k_lin, for A/B and tests)
+  const bool lpre = KL_PRE && apre && U % KL3_BN == 0 && D % BK6 == 0 && !getenv("SDHIP_KL_NOPRE");
+  if (d.t_begin == 0 && lpre) {
+    const int gsz = (int)sd_cdiv((long)U * D / 4, 256);
+    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.Wi[0], U, D, w.wi6, D);
+    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.W0, U, D, w.w06, D);
+    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(Wa0d, U, D, w.wad6, F);
+    SD_LAUNCH_CHECK();
+  }
   if (d.t_begin == 0) {  // x0p(0) = h0 . W0^T + b0 and the deter part of actor layer 0 at t = 0
     LinProb p{feats(0) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
     LinProb pd{feats(0) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
     // the 3-problem launch's tile, so x0p's row partials have one width for every step
-    k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 2), 256, 0, st>>>(p, pd, pd, N, Tr{});
+    if (lpre)
+      k_lin6<KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, 64), 2), 256, 0, st>>>(w.h6, D, w.w06, w.wad6, w.wad6, p, pd, pd,
+                                                                         N, Tr{});
+    else
+      k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 2), 256, 0, st>>>(p, pd, pd, N, Tr{});
     SD_LAUNCH_CHECK();
   }
   for (int t = d.t_begin; t < t_end; ++t) {
@@ -1687,7 +1746,11 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};
       LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
       LinProb pd{feats(t + 1) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
-      k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, tr(7));
+      if (lpre)
+        k_lin6<KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, 64), 3), 256, 0, st>>>(w.h6, D, w.wi6, w.w06, w.wad6, pi, px,
+                                                                           pd, N, tr(7));
+      else
+        k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, tr(7));
       SD_LAUNCH_CHECK();
     }
     const int pj = SD_PRIOR_NCT > 0 && SK % (64 * SD_PRIOR_NCT) == 0 ? SK / (64 * SD_PRIOR_NCT) : 0;

@@ -1263,10 +1263,12 @@ class Dreamer(nn.Module):
         work = torch.empty(nwork, dtype=torch.float32, device=feats.device)
         d.work = work.data_ptr()
         noise = None
-        if IMAG_NOISE and H1 > 1:  # the prior samples' Gumbel noise drawn in one full-chip launch up front
-            noise = torch.empty((H1 - 1) * N * r.flat_stoch, dtype=torch.float32, device=feats.device)
-            d.noise_img = noise.data_ptr()
-            nat.call("sd_imagine_noise", ctypes.addressof(d), noise.data_ptr(), K.stream())
+        if IMAG_NOISE and H1 > 1:  # the prior samples' and actions' noise drawn in one full-chip launch up front
+            noise = torch.empty((H1 - 1) * N * r.flat_stoch + H1 * N * self.act_dim, dtype=torch.float32,
+                                device=feats.device)
+            nact = noise[(H1 - 1) * N * r.flat_stoch:]
+            d.noise_img, d.noise_act = noise.data_ptr(), nact.data_ptr()
+            nat.call("sd_imagine_noise", ctypes.addressof(d), noise.data_ptr(), nact.data_ptr(), K.stream())
         bounds = list(chunks) if chunks else [0, H1]
         if keep is not None:  # measurement aid (bench.py): the descriptor and every buffer it points to
             keep.update(desc=d, work=work, wo=wo, feats=feats, actions=actions, P=P, noise=noise)
