@@ -14,6 +14,13 @@ using namespace sdb;
 #define SD_G3_FP 0
 #endif
 
+#ifndef SD_G3_D2  // two-deep register prefetch main loop (gemm3_core.h gemm3_mainloop_d2): 1 = 128-row tiles, 2 = all
+#define SD_G3_D2 0
+#endif
+template <int BM>
+constexpr bool g3_d2() {
+  return SD_G3_D2 >= 2 || (SD_G3_D2 == 1 && BM >= 128);
+}
 #ifndef SD_G3_M256  // 256 x 128 tiles for the weight-gradient shape (gemm3_run)
 #define SD_G3_M256 0  // measured slower: actor L0 dW 250.7 vs 194.2 us (1 workgroup per CU hides less latency)
 #endif
@@ -62,11 +69,21 @@ __global__ __launch_bounds__(256, (BM >= 256 ? 1 : 2)) void gemm3_kernel(GemmArg
   f32x4 acc[WM / 16][WN / 16];
   if constexpr (RS) {  // weight gradient: also the row sums of A (the bias gradient), written by column tile 0
     static_assert(!AK, "row sums need the rows-contiguous A loader");
-    RowSumOp<OA> ra(la);
-    gemm3_mainloop<BM, BN, WM, WN>(ra, lb, kbeg, kend, acc);
+    f32x4 rsum[OA::NV];
+#pragma unroll
+    for (int v = 0; v < OA::NV; ++v) rsum[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (g3_d2<BM>()) {
+      OA la2 = la;
+      OB lb2 = lb;
+      RowSumOp<OA> ra(la, rsum), ra2(la2, rsum);
+      gemm3_mainloop_d2<BM, BN, WM, WN>(ra, lb, ra2, lb2, kbeg, kend, acc);
+    } else {
+      RowSumOp<OA> ra(la, rsum);
+      gemm3_mainloop<BM, BN, WM, WN>(ra, lb, kbeg, kend, acc);
+    }
     if (tx == 0) {
       __shared__ float part[(BK / 4) * BM], rows[BM];
-      row_sums_km3<BM>(ra, part, rows);
+      row_sums_km3<BM>(rsum, part, rows);
       for (int r = threadIdx.x; r < BM; r += 256) {
         const int m = bm0 + r;
         if (m >= g.M) continue;
@@ -78,6 +95,10 @@ __global__ __launch_bounds__(256, (BM >= 256 ? 1 : 2)) void gemm3_kernel(GemmArg
     }
   } else if (SD_G3_FP) {
     gemm3_mainloop_fp<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
+  } else if (g3_d2<BM>()) {
+    OA la2 = la;
+    OB lb2 = lb;
+    gemm3_mainloop_d2<BM, BN, WM, WN>(la, lb, la2, lb2, kbeg, kend, acc);
   } else {
     gemm3_mainloop<BM, BN, WM, WN>(la, lb, kbeg, kend, acc);
   }
@@ -212,10 +233,22 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void gemm3_mlp_kernel(GemmA
   if constexpr (RMS) {
     const float* nwb = pick_b(e.nwp, b);
     KC3Rms<BM> la(A, g.lda, g.M, bm0, nwb ? nwb : e.nw + (long)b * e.sNw, rs, e.act);
-    gemm3_mainloop<BM, BN, WM, WN>(la, lb, 0, g.K, acc);
+    if constexpr (g3_d2<BM>()) {
+      KC3Rms<BM> la2 = la;
+      KC3<BN, true> lb2 = lb;
+      gemm3_mainloop_d2<BM, BN, WM, WN>(la, lb, la2, lb2, 0, g.K, acc);
+    } else {
+      gemm3_mainloop<BM, BN, WM, WN>(la, lb, 0, g.K, acc);
+    }
   } else {
     KC3<BM, true> la(A, g.lda, g.M, bm0);
-    gemm3_mainloop<BM, BN, WM, WN>(la, lb, 0, g.K, acc);
+    if constexpr (g3_d2<BM>()) {
+      KC3<BM, true> la2 = la;
+      KC3<BN, true> lb2 = lb;
+      gemm3_mainloop_d2<BM, BN, WM, WN>(la, lb, la2, lb2, 0, g.K, acc);
+    } else {
+      gemm3_mainloop<BM, BN, WM, WN>(la, lb, 0, g.K, acc);
+    }
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave / (BN / WN), wc = wave % (BN / WN), l16 = lane & 15, q = lane >> 4;

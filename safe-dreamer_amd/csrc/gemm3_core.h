@@ -143,32 +143,31 @@ struct KM3 {
 };
 
 // Row sums of an A loader's tiles over the K loop, in a fixed order: per thread in rowsum_add, then over the BK / 4
-// k-quads of a row in row_sums. Wraps the loader: load() also accumulates.
+// k-quads of a row in row_sums_km3. Wraps the loader; the tile is added when it is staged into LDS (k-tile order, the
+// loads' registers are consumed there anyway), not when its loads are issued — adding at issue made every k tile wait
+// for its own loads before the MFMAs. Two wrappers may share one accumulator (gemm3_mainloop_d2's register sets).
 template <class Op>
 struct RowSumOp {
   Op& op;
-  f32x4 acc[Op::NV];
+  f32x4 (&acc)[Op::NV];
   static constexpr int NVv = Op::NV;
-  SD_DEV explicit RowSumOp(Op& o) : op(o) {
-#pragma unroll
-    for (int v = 0; v < Op::NV; ++v) acc[v] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  SD_DEV void load(int k0, int kend) {
-    op.load(k0, kend);
+  SD_DEV RowSumOp(Op& o, f32x4 (&a)[Op::NV]) : op(o), acc(a) {}
+  SD_DEV void load(int k0, int kend) { op.load(k0, kend); }
+  SD_DEV void store(__bf16* lds) {
     op.rowsum_add(acc);
+    op.store(lds);
   }
-  SD_DEV void store(__bf16* lds) const { op.store(lds); }
 };
 // KM3<ROWS> block i = (rq = i % (ROWS / 4), kq = i / (ROWS / 4)) holds rows 4rq..4rq+3; part: LDS (BK / 4) x ROWS
-template <int ROWS, class R>
-SD_DEV void row_sums_km3(const R& rs, float* part, float* out_rows) {
+template <int ROWS, int NV>
+SD_DEV void row_sums_km3(const f32x4 (&acc)[NV], float* part, float* out_rows) {
 #pragma unroll
-  for (int v = 0; v < R::NVv; ++v) {
+  for (int v = 0; v < NV; ++v) {
     const int i = threadIdx.x + v * 256;
     if (i < ROWS * BK / 16) {
       const int rq = i % (ROWS / 4), kq = i / (ROWS / 4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) part[kq * ROWS + 4 * rq + j] = rs.acc[v][j];
+      for (int j = 0; j < 4; ++j) part[kq * ROWS + 4 * rq + j] = acc[v][j];
     }
   }
   __syncthreads();
@@ -243,6 +242,83 @@ SD_DEV void gemm3_mainloop(OpA& la, OpB& lb, int kbeg, int kend, f32x4 (&acc)[WM
     }
     __syncthreads();
   }
+}
+
+// Two-deep register prefetch: two register sets per operand (the loader copied), so tile kt+2's global loads are in
+// flight across tile kt+1's MFMAs as well as tile kt's — two k tiles of L2 latency cover instead of one. Same LDS
+// double buffer, products and k order as gemm3_mainloop (bit-identical results). Iteration kt: MFMAs on LDS stage
+// kt & 1, stage tile kt+1 from register set X, reissue X's loads for tile kt+3; unrolled by two so X and Y swap.
+// (la, lb) and (la2, lb2) are the two register sets: copies of one loader (RowSumOp: each wraps its own copy).
+template <int BM, int BN, int WM, int WN, class OpA, class OpB>
+SD_DEV void gemm3_mainloop_d2(OpA& la, OpB& lb, OpA& la2, OpB& lb2, int kbeg, int kend,
+                              f32x4 (&acc)[WM / 16][WN / 16]) {
+  constexpr int WAVES_N = BN / WN;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+  constexpr int SA = BM * LROW, STAGE = (BM + BN) * LROW;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WAVES_N, wc = wave % WAVES_N;
+  const int l16 = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk <= 0) return;
+  la.load(kbeg, kend);
+  lb.load(kbeg, kend);
+  if (nk > 1) {
+    la2.load(kbeg + BK, kend);
+    lb2.load(kbeg + BK, kend);
+  }
+  la.store(smem);
+  lb.store(smem + SA);
+  if (nk > 2) {
+    la.load(kbeg + 2 * BK, kend);
+    lb.load(kbeg + 2 * BK, kend);
+  }
+  __syncthreads();
+  auto step = [&](int kt, OpA& xa, OpB& xb) {  // x: the register set holding tile kt+1
+    const __bf16* cur = smem + (kt & 1) * STAGE;
+    bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const __bf16* p = cur + (wr * WM + 16 * i + l16) * LROW + 8 * q;
+      ah[i] = *reinterpret_cast<const bf16x8*>(p);
+      al[i] = *reinterpret_cast<const bf16x8*>(p + BK);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const __bf16* p = cur + SA + (wc * WN + 16 * j + l16) * LROW + 8 * q;
+      bh[j] = *reinterpret_cast<const bf16x8*>(p);
+      bl[j] = *reinterpret_cast<const bf16x8*>(p + BK);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+    if (kt + 1 < nk) {
+      __bf16* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+      xa.store(nxt);
+      xb.store(nxt + SA);
+    }
+    if (kt + 3 < nk) {
+      xa.load(kbeg + (kt + 3) * BK, kend);
+      xb.load(kbeg + (kt + 3) * BK, kend);
+    }
+    __syncthreads();
+  };
+  int kt = 0;
+  for (; kt + 2 <= nk; kt += 2) {
+    step(kt, la2, lb2);
+    step(kt + 1, la, lb);
+  }
+  if (kt < nk) step(kt, la2, lb2);
 }
 
 // Fragment-prefetch form (gemm_core.h gemm16_mainloop_fp): iteration kt reads tile kt+1's fragments from LDS before

@@ -41,3 +41,19 @@ for label, M, N, K, ak, bk in SHAPES:
     t3 = timeit(lambda: k.gemm(a, b, out, fast=True))
     print(f"{label:34s} f32 {t32*1e3:8.1f} us {fl/t32/1e9:6.1f} TF | bf16x3 {t3*1e3:8.1f} us {fl/t3/1e9:6.1f} TF"
           f" | x{t32/t3:4.2f}", flush=True)
+
+# the update's own launches: the four imagined heads' first layer in one MLP launch (A broadcast, per-entry weights,
+# row partials out), and the weight + bias gradient of the actor / value layer 0 (K-split by the default heuristic)
+M, K, U = 16384, 2560, 256
+x = torch.randn(M, K, device="cuda")
+ws = [torch.randn(U, K, device="cuda") * 0.02 for _ in range(4)]
+bs = [torch.randn(U, device="cuda") for _ in range(4)]
+out = torch.empty(4, M, U, device="cuda")
+pout = torch.empty(4, U // 64, M, device="cuda")
+t = timeit(lambda: k.mlp_layer(x[None].expand(4, M, K), ws, out, bias=bs, part_out=pout))
+print(f"{'heads L0 mlp 4x16384x256x2560':34s} bf16x3 {t*1e3:8.1f} us {4*2.0*M*U*K/t/1e9:6.1f} TF", flush=True)
+R, O, I = 15360, 256, 2560
+dy, xx = torch.randn(R, O, device="cuda"), torch.randn(R, I, device="cuda")
+dw, db = torch.zeros(O, I, device="cuda"), torch.zeros(O, device="cuda")
+t = timeit(lambda: k.wgrad(dy, xx, dw, db))
+print(f"{'wgrad+bias 256x2560x15360':34s} bf16x3 {t*1e3:8.1f} us {2.0*R*O*I/t/1e9:6.1f} TF", flush=True)

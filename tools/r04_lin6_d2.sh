@@ -1,0 +1,17 @@
+#!/bin/bash
+# k_lin6 / action-noise validation (tools/r04_lin6.sh) plus the two-deep-prefetch gemm3 variants: GEMM tests on the
+# default and the all-tiles variant, shape timings, whole-update A/B. -> gpurun_out/$1
+set -o pipefail
+O=gpurun_out/$1; mkdir -p $O
+L=safe-dreamer_amd/sdreamer
+T="python -u -m pytest -q -x --timeout 300 --timeout-method thread"
+timeout -k 10 400 $T tests/test_gpu_imagine.py > $O/imagine.txt 2>&1 || exit 1
+timeout -k 10 400 $T tests/test_gpu_dreamer.py -k "test_update_matches_reference" > $O/golden.txt 2>&1 || exit 1
+timeout -k 10 300 $T tests/test_gpu_gemm.py > $O/gemm.txt 2>&1 || exit 1
+SDHIP_LIB=$L/_lib_d2a/libsdhip.so timeout -k 10 300 $T tests/test_gpu_gemm.py > $O/gemm_d2a.txt 2>&1 || exit 1
+timeout -k 10 200 python tools/imag_trace.py > $O/imag_trace.txt 2>&1 || exit 1
+timeout -k 10 120 python tools/gemm3_bench.py > $O/g3_default.txt 2>&1 || exit 1
+SDHIP_LIB=$L/_lib_d2/libsdhip.so timeout -k 10 120 python tools/gemm3_bench.py > $O/g3_d2.txt 2>&1 || exit 1
+SDHIP_LIB=$L/_lib_d2a/libsdhip.so timeout -k 10 120 python tools/gemm3_bench.py > $O/g3_d2a.txt 2>&1 || exit 1
+bash tools/ab_env.sh 3 "" "SDHIP_KL_NOPRE=1" "SDHIP_LIB=$L/_lib_d2/libsdhip.so" "SDHIP_LIB=$L/_lib_d2a/libsdhip.so" \
+  > $O/ab.txt 2>&1
