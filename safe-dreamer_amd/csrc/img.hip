@@ -688,11 +688,70 @@ struct RTile {
   }
 };
 
+// RTile<16>'s partition (16 virtual waves: column tile v % 4, k part v / 4) on 8 waves: wave w runs virtual waves w
+// and w + 8 (same column tile, k parts w / 4 and w / 4 + 2) with one accumulator each, and the k parts are summed in
+// RTile<16>'s order — bit-identical results with half the threads per workgroup (k_prior_rw<.., 512>).
+struct RTile16h {
+  static constexpr int U = 256, KS = 4, KP = U / KS, NCH = KP / 16, LDP = U + 4;
+  f32x4 b[2][NCH];
+  f32x4 acc[2];
+  SD_DEV void load_w(const float* W, long ldw, int n0) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int v = w + 8 * h;
+      const float* p = W + (long)(n0 + 16 * (v % 4) + l16) * ldw + (v / 4) * KP + 4 * q;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) b[h][c] = ld4(p + 16 * c);
+    }
+  }
+  SD_DEV static void stage(float* P, const float* X, long ldx, const float* nw, const float* part, int np, int M,
+                           int m0, float eps) {
+    RTile<16>::stage(P, X, ldx, nw, part, np, M, m0, eps);
+  }
+  SD_DEV void mma(const float* P) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int v = w + 8 * h;
+      acc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* a = P + l16 * LDP + (v / 4) * KP + 4 * q;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const f32x4 av = ld4(a + 16 * c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], b[h][c][j], acc[h], 0, 0, 0);
+      }
+    }
+  }
+  SD_DEV void reduce(float* red, float* T) const {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[((w + 8 * h) * 4 + r) * 64 + lane] = acc[h][r];
+    __syncthreads();
+    if (w < 4) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = red[(w * 4 + r) * 64 + lane];
+#pragma unroll
+        for (int k = 1; k < KS; ++k) v += red[((w + 4 * k) * 4 + r) * 64 + lane];
+        T[(4 * q + r) * 65 + 16 * w + l16] = v;
+      }
+    }
+    __syncthreads();
+  }
+};
+
 #ifndef KR_RW  // k_rmslin as register tiles (RTile<8>); 0: the LDS-staged k loop
 #define KR_RW 1
 #endif
 #ifndef KP_RW  // k_prior as register tiles (RTile<16>, one sampler element per thread); 0: the LDS-staged k loop
 #define KP_RW 1
+#endif
+#ifndef KP_NT  // k_prior_rw threads per workgroup: 1024 (RTile<16>) or 512 (RTile16h, two sampler elements per thread)
+#define KP_NT 1024
 #endif
 // k_rmslin on RTile<8>: 512 threads, grid (U / 64, M / 16); the same outputs and 16-column row partials (part[p * M +
 // m], p = column / 16) as k_rmslin<16, 64>
@@ -953,42 +1012,54 @@ __global__ __launch_bounds__(256) void k_prior(sd_imagine d, const float* X, con
   SD_TR_END(tr.p, tr.slot)
 }
 
-// k_prior on RTile<16>: 1024 threads, grid (SK / 64, M / 16); one sampler element per thread (row tid / 64, column
-// tid % 64: teams of KD lanes), the noise drawn / read before the contraction
-template <int KD>
-__global__ __launch_bounds__(1024, 8) void k_prior_rw(sd_imagine d, const float* X, const float* nw, const float* part_in,
-                                                   int np, float* snew, long ldf, int t, Tr tr) {
+// k_prior on RTile<16>: grid (SK / 64, M / 16); NT = 1024 threads (one sampler element per thread: row i / 64, column
+// i % 64, teams of KD lanes) or NT = 512 (RTile16h, the same sums; elements tid and tid + 512); the noise drawn / read
+// before the contraction
+template <int KD, int NT>
+__global__ __launch_bounds__(NT, NT == 1024 ? 8 : 4) void k_prior_rw(sd_imagine d, const float* X, const float* nw,
+                                                                   const float* part_in, int np, float* snew, long ldf,
+                                                                   int t, Tr tr) {
   SD_TR_BEGIN
-  using RT = RTile<16>;
+  using RT = typename std::conditional<NT == 1024, RTile<16>, RTile16h>::type;
+  constexpr int PE = 1024 / NT;  // sampler elements per thread
   __shared__ __attribute__((aligned(16))) float P[16 * RT::LDP];
   __shared__ float red[16 * 4 * 64];
   __shared__ float T[16 * 65];
   const int tid = threadIdx.x, n0 = blockIdx.x * 64, m0 = blockIdx.y * 16, S = d.SK / KD;
-  const int rl = tid >> 6, c = tid & 63, lt = c % KD;
-  const long m = m0 + rl;
   RT rt;
   rt.load_w(d.Wl, RT::U, n0);
-  float gn;
-  if (d.noise_img) {  // drawn ahead (sd_imagine_noise): the same values
-    gn = m < d.N ? d.noise_img[((long)t * d.N + m) * d.SK + n0 + c] : 0.f;
-  } else {
-    const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
-    gn = sd_gumbel(seed, (uint32_t)d.stream_img, (uint32_t)t, (uint64_t)((m + d.row_offset) * S + (n0 + c) / KD) * KD + lt);
+  float gn[PE], blv[PE];
+#pragma unroll
+  for (int e = 0; e < PE; ++e) {
+    const int i = tid + NT * e, rl = i >> 6, c = i & 63, lt = c % KD;
+    const long m = m0 + rl;
+    if (d.noise_img) {  // drawn ahead (sd_imagine_noise): the same values
+      gn[e] = m < d.N ? d.noise_img[((long)t * d.N + m) * d.SK + n0 + c] : 0.f;
+    } else {
+      const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+      gn[e] = sd_gumbel(seed, (uint32_t)d.stream_img, (uint32_t)t,
+                        (uint64_t)((m + d.row_offset) * S + (n0 + c) / KD) * KD + lt);
+    }
+    blv[e] = d.bl[n0 + c];
   }
-  const float blv = d.bl[n0 + c];
   RT::stage(P, X, RT::U, nw, part_in, np, d.N, m0, d.eps);
   __syncthreads();
   SD_TR(1)
   rt.mma(P);
   rt.reduce(red, T);
   SD_TR(2)
-  const float l = T[rl * 65 + c] + blv;
-  float p, pp, nl;
-  unimix_forward<KD>(l, true, KD, d.unimix, p, pp, nl);
-  float ys;
-  int idx;
-  st_soft<KD>(nl, gn, true, ys, idx, lt);
-  if (m < d.N) snew[m * ldf + n0 + c] = ((lt == idx ? 1.f : 0.f) - ys) + ys;
+#pragma unroll
+  for (int e = 0; e < PE; ++e) {
+    const int i = tid + NT * e, rl = i >> 6, c = i & 63, lt = c % KD;
+    const long m = m0 + rl;
+    const float l = T[rl * 65 + c] + blv[e];
+    float p, pp, nl;
+    unimix_forward<KD>(l, true, KD, d.unimix, p, pp, nl);
+    float ys;
+    int idx;
+    st_soft<KD>(nl, gn[e], true, ys, idx, lt);
+    if (m < d.N) snew[m * ldf + n0 + c] = ((lt == idx ? 1.f : 0.f) - ys) + ys;
+  }
   SD_TR_END(tr.p, tr.slot)
 }
 
@@ -1782,10 +1853,10 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       const dim3 gpr(SK / 64, sd_cdiv(N, 16));
       if (KP_RW && U == 256 && npi <= 16) {
         if (d.Kd == 16)
-          k_prior_rw<16><<<gpr, 1024, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi, feats(t + 1), F, t,
+          k_prior_rw<16, KP_NT><<<gpr, KP_NT, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi, feats(t + 1), F, t,
                                                tr(12));
         else
-          k_prior_rw<32><<<gpr, 1024, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi, feats(t + 1), F, t,
+          k_prior_rw<32, KP_NT><<<gpr, KP_NT, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi, feats(t + 1), F, t,
                                                tr(12));
       } else if (d.Kd == 16) {
         k_prior<16><<<gpr, 256, 0, st>>>(d, w.i[ci], d.ni[d.img_layers - 1], w.pi[ci], npi, feats(t + 1), F, t,
