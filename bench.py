@@ -221,7 +221,7 @@ def wm_loss_parity_full(name="C2_walker_r2"):
 # The committed kernel table of this build (tools/profile_round.sh -> tools/kernel_table.py: the rocprofv3 kernel trace
 # of a bench run, windowed to its timed steps, joined with the separate --pmc passes). Named explicitly, never "the
 # newest file": its rows rank the update's launch shapes by time per update and carry their counter traffic.
-KERNEL_TABLE = "profiles/r04w_kernel_table.json"
+KERNEL_TABLE = "profiles/r04y_kernel_table.json"
 
 
 def clock_probe(nwg=256, iters=20000, reps=3):
@@ -362,8 +362,11 @@ def probe_specs(agent, cfg, K):
         2.0 * M * F * U * 4, 4.0 * (M * F + 4 * F * U + 4 * M * U + 4 * (U // 64) * M), hp.label, ("launch", hp), 1,
         peak=PEAK_BF16X3)
     # imagination step kernels
-    imag = [("imag_k_lin", "k_lin<32, 32>", (U // 32, N // 32, 3), 3 * 2.0 * N * D * U,
-             4.0 * (N * D + 3 * U * D + 3 * N * U + 2 * (U // 16) * N), IMAG_LABELS[0], 0),
+    # k_lin6 (pre-split deter image + weight images, 64-row tiles) unless SDHIP_KL_NOPRE selects the fp32 k_lin
+    lin6 = not os.environ.get("SDHIP_KL_NOPRE")
+    imag = [("imag_k_lin", "k_lin6<32>" if lin6 else "k_lin<32, 32>", (U // 32, N // (64 if lin6 else 32), 3),
+             3 * 2.0 * N * D * U, 4.0 * (N * D + 3 * U * D + 3 * N * U + 2 * (U // 16) * N),
+             IMAG_LABELS[3 if lin6 else 0], 0),
             ("imag_k_hid", "k_hid", (D // 64, N // 64, 1), 2.0 * N * D * Ig,
              4.0 * (N * D + 3 * N * U + D * Ig + N * D + N * D // 64), IMAG_LABELS[1], 1),
             ("imag_k_gate", "k_gate", (D // 32, N // 64, 1), 2.0 * N * 3 * D * Dg,
@@ -393,7 +396,19 @@ IMAG_LABELS = {
     1: "k_hid (imagination step: _dyn_hid BlockLinear, K = Dg + 3U per block, RMSNorm + SiLU of x0 / x1 in the A "
        "loader; bf16x6)",
     2: "k_gate (imagination step: _dyn_gru BlockLinear + GRU epilogue, RMSNorm + SiLU of hp in the A loader; bf16x6)",
+    3: "k_lin6<32> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
+       "GEMMs in one launch on pre-split bf16x6 operands — the deter image k_gate writes, weight images split once per "
+       "imagination — RMSNorm row partials in the epilogue; 6 v_mfma_f32_16x16x32_bf16 per f32-equivalent product)",
 }
+
+
+def _kernel_is(row_name, name):
+    """A kernel-table row's name (demangled, or the mangled symbol of a kernel in an anonymous namespace) is `name`
+    (the table's spelling: 'k_lin6<32>', or a bare 'k_hid' for a mangled row)."""
+    if row_name.startswith(name):
+        return True
+    base = name.split("<")[0]
+    return row_name.startswith("_Z") and (f"{len(base)}{base}I" in row_name or f"{len(base)}{base}E" in row_name)
 
 
 def roofline_entries(specs, agent, cfg, table):
@@ -427,7 +442,7 @@ def roofline_entries(specs, agent, cfg, table):
              "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak, "avg_us": avg_us,
              "work_per_launch": sp["work"], "algorithmic_bytes": sp["algo"], "traffic": None}
         row = next(((i, rw) for i, rw in enumerate(rows)
-                    if rw["kernel"].startswith(sp["name"]) and rw["grid"] == sp["grid"]), None)
+                    if _kernel_is(rw["kernel"], sp["name"]) and rw["grid"] == sp["grid"]), None)
         if row:
             i, rw = row
             e.update(rank=i + 1, launches_per_update=rw["launches_per_update"],

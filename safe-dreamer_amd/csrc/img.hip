@@ -1658,7 +1658,19 @@ extern "C" int sd_imagine_work_floats(const sd_imagine* d) {
   return (int)iwork(*d, nullptr).total;
 }
 
-// One launch of step t's k_lin (img_net_0 + _dyn_in0 + actor layer 0's deter part: which = 0), k_hid (1) or
+// k_hid reads deter / x1 / x2 from pre-split images when every producer writes one (k_gate, k_onehot_lin,
+// k_action_rows); SDHIP_KH_NOAPRE set: the in-loader split, for tests comparing the two — bit-identical
+static bool img_apre(const sd_imagine& d) {
+  return KH_APRE && KH_1S && F6_HID && KH_PRE && KH_BM == 64 && KL_ONEHOT && d.SK / d.Kd <= 64 && KA_ROWS &&
+         !SD_FUSED_ACTOR && d.U / KL2_PW == 16 && !getenv("SDHIP_KH_NOAPRE");
+}
+// the deter contractions on pre-split operands (k_lin6): A the deter image (img_apre), B the weights split once per
+// imagination; SDHIP_KL_NOPRE set: the fp32 k_lin, for A/B and tests
+static bool img_lpre(const sd_imagine& d) {
+  return KL_PRE && img_apre(d) && d.U % KL3_BN == 0 && d.D % BK6 == 0 && !getenv("SDHIP_KL_NOPRE");
+}
+
+// One launch of step t's k_lin / k_lin6 (img_net_0 + _dyn_in0 + actor layer 0's deter part: which = 0), k_hid (1) or
 // k_gate (2), exactly as sd_imagine_run issues it (same descriptor and workspace; the launch recomputes the values that
 // run already wrote, so it can be repeated): bench.py times the dominant kernel of the update this way.
 extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd_stream stream_) {
@@ -1676,7 +1688,11 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
     LinProb pi{feats(t + 1) + SK, F, D, d.Wi[0], D, d.bi[0], w.i[0], U, w.pi[0], nullptr};
     LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
     LinProb pd{feats(t + 1) + SK, F, D, d.Wa[0] + SK, F, nullptr, w.ad, U, nullptr, nullptr};
-    k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, Tr{});
+    if (img_lpre(d))  // the images the run built (the deter image holds its last step: the timing is the same)
+      k_lin6<KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, 64), 3), 256, 0, st>>>(w.h6, D, w.wi6, w.w06, w.wad6, pi, px, pd,
+                                                                         N, Tr{});
+    else
+      k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, Tr{});
   } else if (which == 1) {
     k_hid<false><<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1,
                                                                  U / KL3_PW, npU, w.x2, w.hp, w.ph, w.wh6, nullptr,
@@ -1706,11 +1722,7 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   // reads deter' (img_net_0 / _dyn_in0), the stoch part (+ bias + deter part, row partials) after the prior sample
   const float* Wa0d = d.Wa[0] + SK;  // (U, F) columns SK.. of the actor's first weight
   const int t_end = d.t_end > 0 ? d.t_end : d.H1;
-  // k_hid reads deter / x1 / x2 from pre-split images when every producer writes one (k_gate, k_onehot_lin,
-  // k_action_rows)
-  // (SDHIP_KH_NOAPRE set: the in-loader split, for tests comparing the two — bit-identical)
-  const bool apre = KH_APRE && KH_1S && F6_HID && KH_PRE && KH_BM == 64 && KL_ONEHOT && d.SK / d.Kd <= 64 && KA_ROWS &&
-                    !SD_FUSED_ACTOR && U / KL2_PW == 16 && !getenv("SDHIP_KH_NOAPRE");
+  const bool apre = img_apre(d);  // pre-split k_hid operands
   if (d.t_begin == 0 && apre) {  // the start state's deter image
     k_presplit_rows<<<(int)sd_cdiv((long)N * D / 4, 256), 256, 0, st>>>(feats(0) + SK, F, N, D, w.h6);
     SD_LAUNCH_CHECK();
@@ -1729,9 +1741,8 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     k_presplit6_gate<<<(int)sd_cdiv((long)3 * D * (D / d.G) / 4, 256), 256, 0, st>>>(d.Wg, D, D / d.G, w.wg6);
     SD_LAUNCH_CHECK();
   }
-  // the deter contractions (img_net_0, _dyn_in0, actor layer 0's deter part) on pre-split operands: A is the deter
-  // image (apre), B the weights split once here (SDHIP_KL_NOPRE set: the fp32 k_lin, for A/B and tests)
-  const bool lpre = KL_PRE && apre && U % KL3_BN == 0 && D % BK6 == 0 && !getenv("SDHIP_KL_NOPRE");
+  // the deter contractions (img_net_0, _dyn_in0, actor layer 0's deter part) on pre-split operands (k_lin6)
+  const bool lpre = img_lpre(d);
   if (d.t_begin == 0 && lpre) {
     const int gsz = (int)sd_cdiv((long)U * D / 4, 256);
     k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.Wi[0], U, D, w.wi6, D);

@@ -18,6 +18,14 @@ SDHIP_LIB=$L/_lib_d2/libsdhip.so timeout -k 10 120 python tools/gemm3_bench.py >
 SDHIP_LIB=$L/_lib_d2a/libsdhip.so timeout -k 10 120 python tools/gemm3_bench.py > $O/g3_d2a.txt 2>&1 || exit 1
 bash tools/ab_env.sh 3 "" "SDHIP_KL_NOPRE=1" "SDHIP_LIB=$L/_lib_d2/libsdhip.so" "SDHIP_LIB=$L/_lib_d2a/libsdhip.so" \
   "SDHIP_LIB=$L/_lib_kp512/libsdhip.so" > $O/ab.txt 2>&1
+for i in 1 2; do  # C4 (atari-like, 2048 imagined rows, 32x32 stoch): the prior sampler's grid is 4x C2's
+  for e in "" "SDHIP_LIB=$L/_lib_kp512/libsdhip.so"; do
+    ms=$(env $e timeout -k 10 240 python3 bench.py --config dmc/atari_breakout --no-cpu-baseline --no-roofline \
+      2>/dev/null | tail -1 | python3 -c "import json,sys; print(round(json.loads(sys.stdin.read())['ms_per_step'], 3))") \
+      || exit 1
+    echo "[c4 ${e:-default}] $ms" >> $O/ab_c4.txt
+  done
+done
 # C2 vs C4 kernel tables of the same build on the same box (where C4's extra time goes)
 R=$PWD
 for c in cnn atari_breakout; do
