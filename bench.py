@@ -364,7 +364,7 @@ def probe_specs(agent, cfg, K):
     # imagination step kernels
     # k_lin6 (pre-split deter image + weight images, 64-row tiles) unless SDHIP_KL_NOPRE selects the fp32 k_lin
     lin6 = not os.environ.get("SDHIP_KL_NOPRE")
-    imag = [("imag_k_lin", "k_lin6<32>" if lin6 else "k_lin<32, 32>", (U // 32, N // (64 if lin6 else 32), 3),
+    imag = [("imag_k_lin", "k_lin6<64, 32>" if lin6 else "k_lin<32, 32>", (U // 32, N // (64 if lin6 else 32), 3),
              3 * 2.0 * N * D * U, 4.0 * (N * D + 3 * U * D + 3 * N * U + 2 * (U // 16) * N),
              IMAG_LABELS[3 if lin6 else 0], 0),
             ("imag_k_hid", "k_hid", (D // 64, N // 64, 1), 2.0 * N * D * Ig,
@@ -396,7 +396,7 @@ IMAG_LABELS = {
     1: "k_hid (imagination step: _dyn_hid BlockLinear, K = Dg + 3U per block, RMSNorm + SiLU of x0 / x1 in the A "
        "loader; bf16x6)",
     2: "k_gate (imagination step: _dyn_gru BlockLinear + GRU epilogue, RMSNorm + SiLU of hp in the A loader; bf16x6)",
-    3: "k_lin6<32> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
+    3: "k_lin6<64, 32> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
        "GEMMs in one launch on pre-split bf16x6 operands — the deter image k_gate writes, weight images split once per "
        "imagination — RMSNorm row partials in the epilogue; 6 v_mfma_f32_16x16x32_bf16 per f32-equivalent product)",
 }

@@ -190,16 +190,18 @@ struct BRows {
 // contraction is bit-identical to BRows + store6 on the fp32 weight.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int PRE_ROW = 3 * BK6;  // bf16 per row of a pre-split tile
-template <int BN>
+// TH: the image's tile height when it is taller than the BN rows read (rows sub .. sub + BN - 1 of each TH-row tile)
+template <int BN, int TH = BN>
 struct BPre6 {
   static constexpr int PCS = BN * PRE_ROW / 8, NV = (PCS + 255) / 256;  // 16-B pieces per tile
   u32x4 r[NV];
   const __bf16* tile0;
   SD_DEV BPre6() = default;
-  SD_DEV BPre6(const __bf16* pre, int ct, int nkt, int kt0) : tile0(pre + ((long)ct * nkt + kt0) * BN * PRE_ROW) {}
+  SD_DEV BPre6(const __bf16* pre, int ct, int nkt, int kt0, int sub = 0)
+      : tile0(pre + (((long)ct * nkt + kt0) * TH + sub) * PRE_ROW) {}
   SD_DEV static bool live(int v) { return 256 * (v + 1) <= PCS || threadIdx.x + 256 * v < PCS; }
   SD_DEV void load(int k0, int) {
-    const __bf16* t = tile0 + (long)(k0 / BK6) * BN * PRE_ROW;
+    const __bf16* t = tile0 + (long)(k0 / BK6) * TH * PRE_ROW;
 #pragma unroll
     for (int v = 0; v < NV; ++v)
       if (live(v)) r[v] = *reinterpret_cast<const u32x4*>(t + (threadIdx.x + 256 * v) * 8);
@@ -437,12 +439,15 @@ __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2,
 #ifndef KL_PRE
 #define KL_PRE 1
 #endif
-template <int BN>
+#ifndef KL6_BM  // k_lin6 row tile: 64 (4 waves x 16 rows) or 32 (2 x 2 waves, half of each 64-row image tile)
+#define KL6_BM 64
+#endif
+template <int BM, int BN>
 __global__ __launch_bounds__(256) void k_lin6(const __bf16* aimg, int K, const __bf16* w0, const __bf16* w1,
                                               const __bf16* w2, LinProb p0, LinProb p1, LinProb p2, int M, Tr tr) {
   SD_TR_BEGIN
-  constexpr int BM = 64, WN = BN;  // 4 waves x 16 rows, each the tile's BN columns
-  static_assert(WN % KL3_PW == 0, "row partials");
+  constexpr int WN = BN / (4 / (BM / 16));
+  static_assert(WN % KL3_PW == 0 && BM <= 64, "row partials; rows of one 64-row image tile");
   int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
   if (KL_XCD) xcd_tile(tx, ty, tz);
   const LinProb p = tz == 0 ? p0 : (tz == 1 ? p1 : p2);
@@ -450,7 +455,7 @@ __global__ __launch_bounds__(256) void k_lin6(const __bf16* aimg, int K, const _
   const int n0 = tx * BN, m0 = ty * BM;
   f32x4 acc[1][WN / 16];
   SD_TR(1)
-  mainloop<true, FP_LIN, BM, BN, 16, WN, pf_of(KL_PF)>(BPre6<BM>(aimg, m0 / BM, K / BK6, 0),
+  mainloop<true, FP_LIN, BM, BN, 16, WN, pf_of(KL_PF)>(BPre6<BM, 64>(aimg, m0 / 64, K / BK6, 0, m0 % 64),
                                                       BPre6<BN>(wimg, tx, K / BK6, 0), 0, K, acc);
   SD_TR(2)
   ep_bias_part<BM, BN, WN, KL3_PW>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
@@ -1689,7 +1694,7 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
     LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
     LinProb pd{feats(t + 1) + SK, F, D, d.Wa[0] + SK, F, nullptr, w.ad, U, nullptr, nullptr};
     if (img_lpre(d))  // the images the run built (the deter image holds its last step: the timing is the same)
-      k_lin6<KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, 64), 3), 256, 0, st>>>(w.h6, D, w.wi6, w.w06, w.wad6, pi, px, pd,
+      k_lin6<KL6_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL6_BM), 3), 256, 0, st>>>(w.h6, D, w.wi6, w.w06, w.wad6, pi, px, pd,
                                                                          N, Tr{});
     else
       k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, Tr{});
@@ -1755,7 +1760,7 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     LinProb pd{feats(0) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
     // the 3-problem launch's tile, so x0p's row partials have one width for every step
     if (lpre)
-      k_lin6<KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, 64), 2), 256, 0, st>>>(w.h6, D, w.w06, w.wad6, w.wad6, p, pd, pd,
+      k_lin6<KL6_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL6_BM), 2), 256, 0, st>>>(w.h6, D, w.w06, w.wad6, w.wad6, p, pd, pd,
                                                                          N, Tr{});
     else
       k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 2), 256, 0, st>>>(p, pd, pd, N, Tr{});
@@ -1829,7 +1834,7 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
       LinProb pd{feats(t + 1) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
       if (lpre)
-        k_lin6<KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, 64), 3), 256, 0, st>>>(w.h6, D, w.wi6, w.w06, w.wad6, pi, px,
+        k_lin6<KL6_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL6_BM), 3), 256, 0, st>>>(w.h6, D, w.wi6, w.w06, w.wad6, pi, px,
                                                                            pd, N, tr(7));
       else
         k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, tr(7));

@@ -15,4 +15,13 @@ for i in 1 2; do
     echo "[c4 ${e:-default}] $ms" >> gpurun_out/$T/ab_c4_wgs.txt
   done
 done
-bash tools/r04_final.sh $T
+bash tools/r04_final.sh $T || exit 1
+# k_lin6 on 32-row tiles (KL6_BM=32: 768 workgroups, 3 per CU, instead of 384 on 256 CUs): tests, trace, A/B
+L=safe-dreamer_amd/sdreamer
+O=gpurun_out/$T
+SDHIP_LIB=$L/_lib_kl32/libsdhip.so timeout -k 10 400 python -u -m pytest -q -x --timeout 300 --timeout-method thread \
+  tests/test_gpu_imagine.py > $O/imagine_kl32.txt 2>&1 || exit 1
+SDHIP_LIB=$L/_lib_trace_kl32/libsdhip.so timeout -k 10 200 python tools/imag_trace.py > $O/imag_trace_kl32.txt 2>&1 \
+  || exit 1
+timeout -k 10 200 python tools/imag_trace.py > $O/imag_trace.txt 2>&1 || exit 1
+bash tools/ab_env.sh 3 "" "SDHIP_LIB=$L/_lib_kl32/libsdhip.so" > $O/ab_kl32.txt 2>&1
