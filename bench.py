@@ -221,7 +221,7 @@ def wm_loss_parity_full(name="C2_walker_r2"):
 # The committed kernel table of this build (tools/profile_round.sh -> tools/kernel_table.py: the rocprofv3 kernel trace
 # of a bench run, windowed to its timed steps, joined with the separate --pmc passes). Named explicitly, never "the
 # newest file": its rows rank the update's launch shapes by time per update and carry their counter traffic.
-KERNEL_TABLE = "profiles/r04y_kernel_table.json"
+KERNEL_TABLE = "profiles/r04z_kernel_table.json"
 
 
 def clock_probe(nwg=256, iters=20000, reps=3):
@@ -358,13 +358,13 @@ def probe_specs(agent, cfg, K):
                        label="gemm3_mlp_kernel (imagined reward / continue / value / slow-value first layers: "
                              "(M, F) x 4 (F, U) split-bf16, per-entry weights, row partials for the next layer's "
                              "RMSNorm; 3 bf16 MFMAs per f32-equivalent product)")
-    add("heads_l0", "gemm3_mlp_kernel<false, true>", (U // 128, M // 128, 4), "mfma",
+    add("heads_l0", "gemm3_mlp_kernel<false, true, 128>", (U // 128, M // 128, 4), "mfma",
         2.0 * M * F * U * 4, 4.0 * (M * F + 4 * F * U + 4 * M * U + 4 * (U // 64) * M), hp.label, ("launch", hp), 1,
         peak=PEAK_BF16X3)
     # imagination step kernels
-    # k_lin6 (pre-split deter image + weight images, 64-row tiles) unless SDHIP_KL_NOPRE selects the fp32 k_lin
+    # k_lin6 (pre-split deter image + weight images, 32-row tiles) unless SDHIP_KL_NOPRE selects the fp32 k_lin
     lin6 = not os.environ.get("SDHIP_KL_NOPRE")
-    imag = [("imag_k_lin", "k_lin6<64, 32>" if lin6 else "k_lin<32, 32>", (U // 32, N // (64 if lin6 else 32), 3),
+    imag = [("imag_k_lin", "k_lin6<32, 32>" if lin6 else "k_lin<32, 32>", (U // 32, N // 32, 3),
              3 * 2.0 * N * D * U, 4.0 * (N * D + 3 * U * D + 3 * N * U + 2 * (U // 16) * N),
              IMAG_LABELS[3 if lin6 else 0], 0),
             ("imag_k_hid", "k_hid", (D // 64, N // 64, 1), 2.0 * N * D * Ig,
@@ -374,7 +374,7 @@ def probe_specs(agent, cfg, K):
     for key, name, grid, work, algo, label, which in imag:
         add(key, name, grid, "mfma", work, algo, label, ("imag", which), H)
     # observe-scan forward phases (M = B rows: weight-streaming, bytes-bound)
-    scan = [("scan_k_hid", "k_hid<8, 2>", (D // 16, 1, 1), 4.0 * (D * Ig + 2 * B * D + (ksd + kss + 1) * B * U),
+    scan = [("scan_k_hid", "k_hid<8, 2, true>", (D // 16, 1, 1), 4.0 * (D * Ig + 2 * B * D + (ksd + kss + 1) * B * U),
              "scan k_hid (RSSM.observe step: _dyn_hid BlockLinear, M = B rows, 16-column tiles; x0 / x1 RMSNorm + SiLU "
              "prologue)", 1),
             ("scan_k_gate", "k_gate<2, 2>", (D // 16, 1, 1), 4.0 * (3 * D * Dg + 8 * B * D),
@@ -396,7 +396,7 @@ IMAG_LABELS = {
     1: "k_hid (imagination step: _dyn_hid BlockLinear, K = Dg + 3U per block, RMSNorm + SiLU of x0 / x1 in the A "
        "loader; bf16x6)",
     2: "k_gate (imagination step: _dyn_gru BlockLinear + GRU epilogue, RMSNorm + SiLU of hp in the A loader; bf16x6)",
-    3: "k_lin6<64, 32> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
+    3: "k_lin6<32, 32> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
        "GEMMs in one launch on pre-split bf16x6 operands — the deter image k_gate writes, weight images split once per "
        "imagination — RMSNorm row partials in the epilogue; 6 v_mfma_f32_16x16x32_bf16 per f32-equivalent product)",
 }
@@ -404,7 +404,7 @@ IMAG_LABELS = {
 
 def _kernel_is(row_name, name):
     """A kernel-table row's name (demangled, or the mangled symbol of a kernel in an anonymous namespace) is `name`
-    (the table's spelling: 'k_lin6<32>', or a bare 'k_hid' for a mangled row)."""
+    (the table's spelling: 'k_lin6<32, 32>', or a bare 'k_hid' for a mangled row)."""
     if row_name.startswith(name):
         return True
     base = name.split("<")[0]
@@ -549,7 +549,7 @@ def phase_rooflines(agent, cfg, cfg_name, ms_update, table=None, reps=10):
         # committed PMC passes, per update, over the live phase time: the 'achieved HBM GB/s on the recurrent scan'
         scan_rows = [rw for rw in table["rows"]
                      if rw["kernel"].split("<")[0] in ("k_slab", "k_logit", "k_logit_rows", "k_init") or
-                     rw["kernel"] in ("k_hid<8, 2>", "k_gate<2, 2>")]
+                     rw["kernel"].startswith("k_hid<8, 2") or rw["kernel"] == "k_gate<2, 2>"]
         cb = sum(rw.get("hbm_bytes", 0.0) * rw["launches_per_update"] for rw in scan_rows)
         tm = sum(rw["ms_per_update"] for rw in scan_rows)
         hit = [(rw.get("l2_hit"), rw["ms_per_update"]) for rw in scan_rows if rw.get("l2_hit") is not None]

@@ -439,8 +439,8 @@ __global__ __launch_bounds__(256) void k_lin(LinProb p0, LinProb p1, LinProb p2,
 #ifndef KL_PRE
 #define KL_PRE 1
 #endif
-#ifndef KL6_BM  // k_lin6 row tile: 64 (4 waves x 16 rows) or 32 (2 x 2 waves, half of each 64-row image tile)
-#define KL6_BM 64
+#ifndef KL6_BM  // k_lin6 row tile: 32 (2 x 2 waves, half of each 64-row image tile: 768 workgroups, 3 per CU) or 64
+#define KL6_BM 32  // (4 waves x 16 rows: 384 workgroups, two on half the CUs) — step trace 37.8 -> 33.1 us, r04y
 #endif
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void k_lin6(const __bf16* aimg, int K, const __bf16* w0, const __bf16* w1,
