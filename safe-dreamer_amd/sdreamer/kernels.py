@@ -81,6 +81,11 @@ FAST_GEMM = os.environ.get("SDREAMER_FAST_GEMM", "1") != "0"
 # faster with more (1024: 157 vs 192 us), but in the update, beside the latency-bound scan backward, 512 measured
 # best (11.70 vs 11.80 ms at 1024, 11.76 at 2048 per update; gpurun_out r04v)
 _G3_WG_TARGET = int(os.environ.get("SDREAMER_G3_WGS", "512"))
+# longest K chunk (rows) a split-bf16 workgroup takes when that needs more splits than the workgroup target — at most
+# twice as many. The atari-like config's 256 x 3072 x 30720 weight gradients: 10 splits of 3072 rows -> 20 of 1536
+# (18.83 / 18.89 -> 18.74 / 18.81 ms per update at the equivalent 1024-workgroup target, gpurun_out r04y); the walker
+# config's shapes keep their splits (K <= 16384). 0 disables.
+_G3_CHUNK = int(os.environ.get("SDREAMER_G3_CHUNK", "1536"))
 
 
 def _fast_split(M, N, K, batch):
@@ -92,7 +97,10 @@ def _fast_split(M, N, K, batch):
     if tiles >= 256:
         return 1
     if K >= 1024:
-        cap = max(1, min(K // 512, -(-_G3_WG_TARGET // tiles), 32))
+        wg = -(-_G3_WG_TARGET // tiles)
+        if _G3_CHUNK > 0:
+            wg = max(wg, min(-(-K // _G3_CHUNK), 2 * wg))
+        cap = max(1, min(K // 512, wg, 32))
         if K % 32 == 0:
             kt = K // 32
             even = [d for d in range(cap, 0, -1) if kt % d == 0]
