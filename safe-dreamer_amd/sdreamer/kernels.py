@@ -82,10 +82,10 @@ FAST_GEMM = os.environ.get("SDREAMER_FAST_GEMM", "1") != "0"
 # best (11.70 vs 11.80 ms at 1024, 11.76 at 2048 per update; gpurun_out r04v)
 _G3_WG_TARGET = int(os.environ.get("SDREAMER_G3_WGS", "512"))
 # longest K chunk (rows) a split-bf16 workgroup takes when that needs more splits than the workgroup target — at most
-# twice as many. The atari-like config's 256 x 3072 x 30720 weight gradients: 10 splits of 3072 rows -> 20 of 1536
-# (18.83 / 18.89 -> 18.74 / 18.81 ms per update at the equivalent 1024-workgroup target, gpurun_out r04y); the walker
-# config's shapes keep their splits (K <= 16384). 0 disables.
-_G3_CHUNK = int(os.environ.get("SDREAMER_G3_CHUNK", "1536"))
+# twice as many (SDREAMER_G3_CHUNK, off). The atari-like config's 256 x 3072 x 30720 weight gradients go from 10
+# splits to 20 with 1536: 18.89 / 18.98 / 19.00 vs 18.89 / 18.89 / 18.85 ms per update, memory maze 74.30 vs 74.15
+# (gpurun_out r04c) — no gain.
+_G3_CHUNK = int(os.environ.get("SDREAMER_G3_CHUNK", "0"))
 
 
 def _fast_split(M, N, K, batch):
