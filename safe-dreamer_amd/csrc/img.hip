@@ -471,6 +471,9 @@ __global__ __launch_bounds__(256) void k_lin6(const __bf16* aimg, int K, const _
 #ifndef KL_ONEHOT
 #define KL_ONEHOT 1
 #endif
+#ifndef OH_SPLIT  // the two one-hot problems of a step as two grid rows (1) or one after the other per wave (0)
+#define OH_SPLIT 0
+#endif
 #ifndef OH_BATCH  // weight-row loads issued before their FMAs
 #define OH_BATCH 32
 #endif
@@ -514,8 +517,10 @@ __global__ __launch_bounds__(256) void k_onehot_lin(const float* X, long ldx, in
   const bool dense = __any(many);
   SD_TR(1)
   const int c = 4 * lane;
+  // OH_SPLIT: one problem per workgroup row of the grid (blockIdx.y), both gathers in flight at once; else in turn
+  const int pr0 = OH_SPLIT ? (int)blockIdx.y : 0, pr1 = OH_SPLIT ? pr0 + 1 : nprob;
 #pragma unroll 1
-  for (int pr = 0; pr < nprob; ++pr) {
+  for (int pr = pr0; pr < pr1; ++pr) {
     const OneHotProb& p = pr == 0 ? p0 : p1;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (!dense) {
@@ -1777,7 +1782,8 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       if (KL_ONEHOT && d.SK / d.Kd <= 64) {
         const OneHotProb oa{w.waT, d.ba[0], w.ad, a0, w.pa[0], nullptr, nullptr, 0.f},
             ox{w.w1T, d.b1, nullptr, w.x1p, w.px1, apre ? d.n1 : nullptr, apre ? w.x16 : nullptr, d.eps};
-        k_onehot_lin<<<sd_cdiv(N, 4), 256, 0, st>>>(feats(t), F, SK, d.Kd, oa, ox, last ? 1 : 2, N, tr(0));
+        k_onehot_lin<<<dim3(sd_cdiv(N, 4), OH_SPLIT ? (last ? 1 : 2) : 1), 256, 0, st>>>(feats(t), F, SK, d.Kd, oa, ox,
+                                                                                      last ? 1 : 2, N, tr(0));
       } else {
         k_lin<32, KL2_BN><<<dim3(U / KL2_BN, sd_cdiv(N, 32), last ? 1 : 2), 256, 0, st>>>(pa, px, px, N, tr(0));
       }
