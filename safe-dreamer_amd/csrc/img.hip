@@ -639,29 +639,48 @@ struct RTile {
   }
   // panel P[16][LDP] = silu(X[m0 + r] * rstd_r * nw), rstd from np <= 16 partials part[p * M + m]; threads 0..255:
   // row tid / 16, 16 columns each (the row's 16 threads reduce its partials: no barrier before the norm)
-  SD_DEV static void stage(float* P, const float* X, long ldx, const float* nw, const float* part, int np, int M,
-                           int m0, float eps) {
+  // the panel's operands in registers (threads 0..255): stage_load issues the loads, stage_store normalises and
+  // writes P — split so a caller can issue its weight loads in between (RT_LOADFIRST) and the panel does not wait on
+  // them (loads complete in issue order)
+  struct Panel {
+    f32x4 x[4], w[4];
+    float pv;
+  };
+  SD_DEV static void stage_load(Panel& q, const float* X, long ldx, const float* nw, const float* part, int np, int M,
+                                int m0) {
     const int tid = threadIdx.x;
     if (tid < 256) {
       const int r = tid >> 4, j = tid & 15;
       const long m = m0 + r;
       const bool rv = m < M;
-      const float pv = (rv && j < np) ? part[(long)j * M + m] : 0.f;
-      f32x4 x[4], w[4];
+      q.pv = (rv && j < np) ? part[(long)j * M + m] : 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        x[i] = rv ? ld4(X + m * ldx + 16 * j + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
-        w[i] = ld4(nw + 16 * j + 4 * i);
+        q.x[i] = rv ? ld4(X + m * ldx + 16 * j + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
+        q.w[i] = ld4(nw + 16 * j + 4 * i);
       }
-      const float rs = rsqrtf(group_sum<16>(pv) / (float)U + eps);
+    }
+  }
+  SD_DEV static void stage_store(const Panel& q, float* P, int M, int m0, float eps) {
+    const int tid = threadIdx.x;
+    if (tid < 256) {
+      const int r = tid >> 4, j = tid & 15;
+      const bool rv = m0 + r < M;
+      const float rs = rsqrtf(group_sum<16>(q.pv) / (float)U + eps);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         f32x4 y;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = rv ? siluf_(x[i][e] * rs * w[i][e]) : 0.f;
+        for (int e = 0; e < 4; ++e) y[e] = rv ? siluf_(q.x[i][e] * rs * q.w[i][e]) : 0.f;
         *reinterpret_cast<f32x4*>(P + r * LDP + 16 * j + 4 * i) = y;
       }
     }
+  }
+  SD_DEV static void stage(float* P, const float* X, long ldx, const float* nw, const float* part, int np, int M,
+                           int m0, float eps) {
+    Panel q;
+    stage_load(q, X, ldx, nw, part, np, M, m0);
+    stage_store(q, P, M, m0, eps);
   }
   SD_DEV void mma(const float* P) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
@@ -715,6 +734,14 @@ struct RTile16h {
       for (int c = 0; c < NCH; ++c) b[h][c] = ld4(p + 16 * c);
     }
   }
+  using Panel = RTile<16>::Panel;
+  SD_DEV static void stage_load(Panel& q, const float* X, long ldx, const float* nw, const float* part, int np, int M,
+                                int m0) {
+    RTile<16>::stage_load(q, X, ldx, nw, part, np, M, m0);
+  }
+  SD_DEV static void stage_store(const Panel& q, float* P, int M, int m0, float eps) {
+    RTile<16>::stage_store(q, P, M, m0, eps);
+  }
   SD_DEV static void stage(float* P, const float* X, long ldx, const float* nw, const float* part, int np, int M,
                            int m0, float eps) {
     RTile<16>::stage(P, X, ldx, nw, part, np, M, m0, eps);
@@ -754,6 +781,9 @@ struct RTile16h {
   }
 };
 
+#ifndef RT_LOADFIRST  // k_rmslin_rw issues the A panel's loads before its weight loads (k_prior_rw would spill: 64 VGPRs)
+#define RT_LOADFIRST 0
+#endif
 #ifndef KR_RW  // k_rmslin as register tiles (RTile<8>); 0: the LDS-staged k loop
 #define KR_RW 1
 #endif
@@ -775,8 +805,15 @@ __global__ __launch_bounds__(512) void k_rmslin_rw(const float* X, const float* 
   __shared__ float T[16 * 65];
   const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 16;
   RT rt;
-  rt.load_w(W, RT::U, n0);
-  RT::stage(P, X, RT::U, nw, part_in, np, M, m0, eps);
+  if (RT_LOADFIRST) {  // the panel's loads first: its normalisation waits only on them
+    typename RT::Panel q;
+    RT::stage_load(q, X, RT::U, nw, part_in, np, M, m0);
+    rt.load_w(W, RT::U, n0);
+    RT::stage_store(q, P, M, m0, eps);
+  } else {
+    rt.load_w(W, RT::U, n0);
+    RT::stage(P, X, RT::U, nw, part_in, np, M, m0, eps);
+  }
   __syncthreads();
   SD_TR(1)
   rt.mma(P);
