@@ -1231,6 +1231,9 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
 #ifndef KA_ROWS
 #define KA_ROWS 1
 #endif
+#ifndef KA_W2LATE  // k_action_rows stages _dyn_in2's weight into LDS after the logits instead of before
+#define KA_W2LATE 0
+#endif
 template <int MO>  // >= the output logits (2A or A): 16 or 32
 __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* X, const float* nw,
                                                      const float* part_in, int np, float* act, float* x2, int t,
@@ -1252,8 +1255,21 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
   for (int o = 0; o < MO; ++o) wo[o] = o < NO ? ld4(d.Wao + (long)o * U + 4 * lane) : zero4();
   const float bo = lane < NO ? d.bao[lane] : 0.f;
   const bool x2w = want_x2 != 0;
-  if (x2w)
-    for (int i = threadIdx.x; i < U * A; i += 256) w2s[i] = d.W2[i];
+  // _dyn_in2's weight: loaded here, stored into LDS only after the logits (KA_W2LATE), so the row's first
+  // dependent step does not wait on these loads too (loads complete in issue order)
+  constexpr int W2R = U * MA / 256;
+  float w2r[W2R];
+  if (x2w) {
+    if (KA_W2LATE) {
+#pragma unroll
+      for (int k = 0; k < W2R; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        w2r[k] = i < U * A ? d.W2[i] : 0.f;
+      }
+    } else {
+      for (int i = threadIdx.x; i < U * A; i += 256) w2s[i] = d.W2[i];
+    }
+  }
   const f32x4 b2 = ld4(d.b2 + 4 * lane), n2 = ld4(d.n2 + 4 * lane);
   float nz = 0.f;  // the action noise of element (m, lane): drawn ahead (sd_imagine_noise) or here
   if (d.noise_act) {
@@ -1309,6 +1325,13 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
   if (!x2w) {  // (uniform over the launch)
     SD_TR_END(tr.p, tr.slot)
     return;
+  }
+  if (KA_W2LATE) {
+#pragma unroll
+    for (int k = 0; k < W2R; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < U * A) w2s[i] = w2r[k];
+    }
   }
   __syncthreads();  // w2s staged
   const float an = a / fmaxf(fabsf(a), 1.f);
