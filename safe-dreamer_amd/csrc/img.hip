@@ -1231,8 +1231,8 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
 #ifndef KA_ROWS
 #define KA_ROWS 1
 #endif
-#ifndef KA_W2LATE  // k_action_rows stages _dyn_in2's weight into LDS after the logits instead of before
-#define KA_W2LATE 0
+#ifndef KA_W2LATE  // k_action_rows stages _dyn_in2's weight into LDS after the logits instead of before: measured no
+#define KA_W2LATE 0  // gain (span 11.00 vs 10.98 us, update 11.46 / 11.51 / 11.50 vs 11.50 / 11.54 / 11.51, profiles/r04w2)
 #endif
 template <int MO>  // >= the output logits (2A or A): 16 or 32
 __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* X, const float* nw,
