@@ -645,18 +645,21 @@ struct RTile {
   struct Panel {
     f32x4 x[4], w[4];
     float pv;
+    bool pok;  // pv is one of the np partials (else a clamped duplicate, masked in stage_store)
   };
   SD_DEV static void stage_load(Panel& q, const float* X, long ldx, const float* nw, const float* part, int np, int M,
                                 int m0) {
+    // unconditional loads (rows past M read row M - 1, partials past np read partial np - 1; stage_store masks
+    // them): a "cond ? load : 0" made hipcc branch around the load and drain the vector-memory queue at the join
     const int tid = threadIdx.x;
     if (tid < 256) {
       const int r = tid >> 4, j = tid & 15;
-      const long m = m0 + r;
-      const bool rv = m < M;
-      q.pv = (rv && j < np) ? part[(long)j * M + m] : 0.f;
+      const long m = m0 + r < M ? m0 + r : M - 1;
+      q.pv = part[(long)(j < np ? j : np - 1) * M + m];
+      q.pok = j < np;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        q.x[i] = rv ? ld4(X + m * ldx + 16 * j + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
+        q.x[i] = ld4(X + m * ldx + 16 * j + 4 * i);
         q.w[i] = ld4(nw + 16 * j + 4 * i);
       }
     }
@@ -666,7 +669,7 @@ struct RTile {
     if (tid < 256) {
       const int r = tid >> 4, j = tid & 15;
       const bool rv = m0 + r < M;
-      const float rs = rsqrtf(group_sum<16>(q.pv) / (float)U + eps);
+      const float rs = rsqrtf(group_sum<16>(q.pok ? q.pv : 0.f) / (float)U + eps);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         f32x4 y;
@@ -1078,18 +1081,22 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : 4) void k_prior_rw(sd_imagine 
   float gn[PE], blv[PE];
 #pragma unroll
   for (int e = 0; e < PE; ++e) {
-    const int i = tid + NT * e, rl = i >> 6, c = i & 63, lt = c % KD;
-    const long m = m0 + rl;
-    if (d.noise_img) {  // drawn ahead (sd_imagine_noise): the same values
-      gn[e] = m < d.N ? d.noise_img[((long)t * d.N + m) * d.SK + n0 + c] : 0.f;
-    } else {
-      const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
-      gn[e] = sd_gumbel(seed, (uint32_t)d.stream_img, (uint32_t)t,
-                        (uint64_t)((m + d.row_offset) * S + (n0 + c) / KD) * KD + lt);
-    }
+    const int i = tid + NT * e, rl = i >> 6, c = i & 63;
+    const long m = m0 + rl, mc = m < d.N ? m : d.N - 1;
+    // drawn ahead (sd_imagine_noise, the same values): one unconditional load (address select), else drawn below
+    gn[e] = *(d.noise_img ? d.noise_img + ((long)t * d.N + mc) * d.SK + n0 + c : d.bl + n0 + c);
     blv[e] = d.bl[n0 + c];
   }
-  RT::stage(P, X, RT::U, nw, part_in, np, d.N, m0, d.eps);
+  RT::stage(P, X, RT::U, nw, part_in, np, d.N, m0, d.eps);  // (its wait covers the noise loads issued before)
+  if (!d.noise_img) {
+    const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
+#pragma unroll
+    for (int e = 0; e < PE; ++e) {
+      const int i = tid + NT * e, rl = i >> 6, c = i & 63, lt = c % KD;
+      gn[e] = sd_gumbel(seed, (uint32_t)d.stream_img, (uint32_t)t,
+                        (uint64_t)((m0 + rl + d.row_offset) * S + (n0 + c) / KD) * KD + lt);
+    }
+  }
   __syncthreads();
   SD_TR(1)
   rt.mma(P);
@@ -1231,9 +1238,6 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
 #ifndef KA_ROWS
 #define KA_ROWS 1
 #endif
-#ifndef KA_W2LATE  // k_action_rows stages _dyn_in2's weight into LDS after the logits instead of before: measured no
-#define KA_W2LATE 0  // gain (span 11.00 vs 10.98 us, update 11.46 / 11.51 / 11.50 vs 11.50 / 11.54 / 11.51, profiles/r04w2)
-#endif
 template <int MO>  // >= the output logits (2A or A): 16 or 32
 __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* X, const float* nw,
                                                      const float* part_in, int np, float* act, float* x2, int t,
@@ -1246,39 +1250,40 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
   const int A = d.A, NO = d.act_discrete ? A : 2 * A, M = d.N;
   const bool live = m < M;
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
-  // operand loads first: the row's partials, its 4 columns, the norm weight, the output layer's rows
-  const float pv = (live && lane < np) ? part_in[(long)lane * M + m] : 0.f;
-  const f32x4 xv = live ? ld4(X + m * U + 4 * lane) : zero4();
+  // operand loads first, every one unconditional (clamped row / partial / output-row indices; values past them are
+  // masked where used — a "cond ? load : 0" made hipcc branch around each load and drain the queue at the join): the
+  // row's partials, its 4 columns, the norm weight, the output layer's rows, then _dyn_in2's weight (into registers,
+  // stored to LDS after the logits, so the logits chain waits on none of it) and the drawn-ahead action noise
+  const long mc = live ? m : M - 1;
+  const float pv_ = part_in[(long)(lane < np ? lane : np - 1) * M + mc];
+  const f32x4 xv = ld4(X + mc * U + 4 * lane);
   const f32x4 wn = ld4(nw + 4 * lane);
   f32x4 wo[MO];
 #pragma unroll
-  for (int o = 0; o < MO; ++o) wo[o] = o < NO ? ld4(d.Wao + (long)o * U + 4 * lane) : zero4();
-  const float bo = lane < NO ? d.bao[lane] : 0.f;
+  for (int o = 0; o < MO; ++o) wo[o] = ld4(d.Wao + (long)(o < NO ? o : NO - 1) * U + 4 * lane);
+  const float bo_ = d.bao[lane < NO ? lane : NO - 1];
   const bool x2w = want_x2 != 0;
-  // _dyn_in2's weight: loaded here, stored into LDS only after the logits (KA_W2LATE), so the row's first
-  // dependent step does not wait on these loads too (loads complete in issue order)
   constexpr int W2R = U * MA / 256;
   float w2r[W2R];
-  if (x2w) {
-    if (KA_W2LATE) {
 #pragma unroll
-      for (int k = 0; k < W2R; ++k) {
-        const int i = threadIdx.x + 256 * k;
-        w2r[k] = i < U * A ? d.W2[i] : 0.f;
-      }
-    } else {
-      for (int i = threadIdx.x; i < U * A; i += 256) w2s[i] = d.W2[i];
-    }
+  for (int k = 0; k < W2R; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    w2r[k] = d.W2[i < U * A ? i : U * A - 1];
   }
   const f32x4 b2 = ld4(d.b2 + 4 * lane), n2 = ld4(d.n2 + 4 * lane);
-  float nz = 0.f;  // the action noise of element (m, lane): drawn ahead (sd_imagine_noise) or here
-  if (d.noise_act) {
-    if (live && lane < A) nz = d.noise_act[((long)t * M + m) * A + lane];
-  } else if (d.act_discrete) {
-    if (lane < A) nz = sd_gumbel(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lane);
-  } else if (lane < A) {
-    nz = sd_normal(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lane);
+  const int la = lane < A ? lane : A - 1;
+  float nz = *(d.noise_act ? d.noise_act + ((long)t * M + mc) * A + la : d.b2);
+  if (!d.noise_act) {  // drawn here (the same counter-based values as the drawn-ahead noise)
+    nz = 0.f;
+    if (d.act_discrete) {
+      if (lane < A) nz = sd_gumbel(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lane);
+    } else if (lane < A) {
+      nz = sd_normal(seed, (uint32_t)d.stream_act, (uint32_t)t, (uint64_t)(m + d.row_offset) * A + lane);
+    }
+  } else if (!(live && lane < A)) {
+    nz = 0.f;
   }
+  const float pv = (live && lane < np) ? pv_ : 0.f, bo = lane < NO ? bo_ : 0.f;
   const float rs = rsqrtf(wave_sum(pv) / (float)U + d.eps);
   SD_TR(1)
   f32x4 y;
@@ -1298,10 +1303,10 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
 #pragma unroll
     for (int o = 0; o < MO; ++o)
       if (o < NO) pd[o] += __shfl_xor(pd[o], sh, 64);
-  float lo = 0.f;  // lane o < NO: logit o
+  float lo = 0.f;  // lane o < NO: logit o (lanes past NO: 0, as with the former zero rows)
 #pragma unroll
   for (int o = 0; o < MO; ++o)
-    if (lane == o) lo = pd[o];
+    if (lane == o && o < NO) lo = pd[o];
   lo += bo;
   SD_TR(2)
   float a = 0.f;  // lane j < A: action element j
@@ -1326,12 +1331,10 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
     SD_TR_END(tr.p, tr.slot)
     return;
   }
-  if (KA_W2LATE) {
 #pragma unroll
-    for (int k = 0; k < W2R; ++k) {
-      const int i = threadIdx.x + 256 * k;
-      if (i < U * A) w2s[i] = w2r[k];
-    }
+  for (int k = 0; k < W2R; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    if (i < U * A) w2s[i] = w2r[k];
   }
   __syncthreads();  // w2s staged
   const float an = a / fmaxf(fabsf(a), 1.f);

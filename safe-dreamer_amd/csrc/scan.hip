@@ -53,13 +53,16 @@ struct Core {
   f32x4 b[CPW][NT];
   f32x4 acc[NT];
 
-  // Wt[t]: row (n_t + l16) of a k-contiguous weight matrix, at the span's first k
+  // Wt[t]: row (n_t + l16) of a k-contiguous weight matrix, at the span's first k (a valid row for EVERY lane: the
+  // extra lanes of an 8-column tile point at a real row, their output columns are discarded). Chunks past nch load
+  // chunk nch - 1 and are never multiplied: every load is unconditional (no branch around it, so hipcc has no join at
+  // which to drain the queue — see "load helpers" below).
   SD_DEV void load_b(const float* const* Wt, int nch, int wave, int q) {
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
-      const int ch = core_chunk(wave, c);
+      const int ch = core_chunk(wave, c), chc = ch < nch ? ch : nch - 1;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) b[c][t] = ch < nch ? ld4(Wt[t] + ch * 16 + 4 * q) : zero4();
+      for (int t = 0; t < NT; ++t) b[c][t] = ld4(Wt[t] + chc * 16 + 4 * q);
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = zero4();
@@ -78,13 +81,15 @@ struct Core {
       if (ch < nch) mma(ld4(P + l16 * lda + ch * 16 + 4 * q), c);
     }
   }
-  // A straight from global memory (rows >= M are zero); all loads issued before the first MFMA
+  // A straight from global memory; rows >= M read row M - 1 (their output rows are discarded by the callers), all
+  // loads issued before the first MFMA
   SD_DEV void run_glb(const float* A, long lda, int M, int nch, int wave, int l16, int q) {
     f32x4 a[CPW];
+    const int lr = l16 < M ? l16 : M - 1;
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
-      const int ch = core_chunk(wave, c);
-      a[c] = (ch < nch && l16 < M) ? ld4(A + (long)l16 * lda + ch * 16 + 4 * q) : zero4();
+      const int ch = core_chunk(wave, c), chc = ch < nch ? ch : nch - 1;
+      a[c] = ld4(A + (long)lr * lda + chc * 16 + 4 * q);
     }
 #pragma unroll
     for (int c = 0; c < CPW; ++c)
@@ -121,52 +126,65 @@ constexpr int core_lds_floats() { return NW * NT * 256 + MR * 16 * NT; }
   const int l16 = lane & 15, q = lane >> 4;                \
   (void)l16; (void)q;
 
+// XCD-contiguous tiles: the dispatcher deals workgroup i to XCD i % 8, so tile (i % 8) * (n / 8) + i / 8 gives XCD x
+// the n / 8 consecutive column tiles [x n / 8, (x + 1) n / 8) (with 16-column tiles over D = 2048: exactly block x).
+// Each XCD then writes whole 128-B lines of every output row (two or four neighbouring tiles share a line), and the
+// lines left dirty at the launch's end are not split between XCDs. Speed only: any tile order gives the same result.
+#ifndef SD_SCAN_XCD
+#define SD_SCAN_XCD 1
+#endif
+SD_DEV int xcd_tile(int i, int n) { return (SD_SCAN_XCD && n % 8 == 0) ? (i % 8) * (n / 8) + i / 8 : i; }
+
 // ------------------------------------------------------------------------------------------- load helpers
 // Prologues use 32 threads per row (16 rows): thread t32 owns the float4 columns c = 4*t32 + 128*i. Every load a
-// launch needs is issued before the first use (compile-time trip counts, predicated), so a prologue costs one
-// memory round trip instead of one per slab / per column block.
+// launch needs is issued before the first use, and every load is UNCONDITIONAL: rows past the tile read a valid row
+// (the callers clamp the row index; those rows' results are discarded), slabs past ks read slab ks - 1 (masked when
+// summed). A predicated "cond ? load : 0" made hipcc branch around each load and drain the whole vector-memory queue
+// (s_waitcnt vmcnt(0)) at the join, so the weight stream issued first and the prologue loads behind it became two
+// dependent round trips (round 5: tools/isa_waits.py listed such drains in every scan kernel).
+// Rows are exactly 128 * NI floats wide (every caller's width: U = 256, D/G, S*Kd are multiples of 128).
 template <int NI>
-SD_DEV void ld_row(f32x4 (&v)[NI], const float* rowp, int N, bool rv, int t32) {
+SD_DEV void ld_row(f32x4 (&v)[NI], const float* rowp, int t32) {
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int c = 4 * t32 + 128 * i;
-    v[i] = (rv && c < N) ? ld4(rowp + c) : zero4();
+  for (int i = 0; i < NI; ++i) v[i] = ld4(rowp + 4 * t32 + 128 * i);
+}
+// KS <= slab loads of ks split-K slabs (sum_slabs adds the first ks in fixed order, after the launch's other loads)
+template <int NI, int KS>
+SD_DEV void ld_slabs(f32x4 (&part)[KS][NI], const float* rowp, long sstride, int ks, int t32) {
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int sc = s < ks ? s : ks - 1;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) part[s][i] = ld4(rowp + sc * sstride + 4 * t32 + 128 * i);
   }
 }
-// sum of ks <= KS split-K slabs (fixed order)
 template <int NI, int KS>
-SD_DEV void ld_slabs(f32x4 (&v)[NI], const float* rowp, long sstride, int ks, int N, bool rv, int t32) {
-  f32x4 part[KS][NI];
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int c = 4 * t32 + 128 * i;
-      part[s][i] = (rv && s < ks && c < N) ? ld4(rowp + s * sstride + c) : zero4();
-    }
+SD_DEV void sum_slabs(f32x4 (&v)[NI], const f32x4 (&part)[KS][NI], int ks) {
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     v[i] = part[0][i];
 #pragma unroll
-    for (int s = 1; s < KS; ++s) v[i] += part[s][i];
+    for (int s = 1; s < KS; ++s)
+      if (s < ks) v[i] += part[s][i];
   }
 }
 // per-tile row partials, row-major: part[row * tiles + i], i < tiles <= 128*NP (tiles % 4 == 0): a row's partials
 // are one contiguous run, read as float4s by the row's 32 threads (the column-major layout cost 64 cache lines per
-// wave instruction)
+// wave instruction); entries past `tiles` re-read the last float4 and are masked in sum_parts
 template <int NP>
 SD_DEV void ld_parts(f32x4 (&v)[NP], const float* rowp, int tiles, int t32) {
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
     const int i = 4 * (t32 + 32 * j);
-    v[j] = i < tiles ? *reinterpret_cast<const f32x4*>(rowp + i) : f32x4{0.f, 0.f, 0.f, 0.f};
+    v[j] = *reinterpret_cast<const f32x4*>(rowp + (i < tiles ? i : tiles - 4));
   }
 }
 template <int NP>
-SD_DEV float sum_parts(const f32x4 (&v)[NP]) {
+SD_DEV float sum_parts(const f32x4 (&v)[NP], int tiles, int t32) {
   float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < NP; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+  for (int j = 0; j < NP; ++j)
+    if (4 * (t32 + 32 * j) < tiles) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
   return group_sum<32>(s);
 }
 SD_DEV float sumsq4(f32x4 x) { return x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]; }
@@ -195,13 +213,31 @@ SD_DEV void st_row(float* rowp, const f32x4 (&v)[NI], int N, int t32) {
   }
 }
 
-constexpr int KSM = 4;         // max split-K slabs
+constexpr int KSM = 8;         // max split-K slabs (ks_d, ks_s)
 #ifndef SD_LR_NG
 #define SD_LR_NG 8  // 4: 12.03 / 12.01 ms, 8: 11.98 / 11.95 ms per update (same box, profiles/r03ng_env.txt)
 #endif
 constexpr int LR_NG = SD_LR_NG;                 // x1p slabs written by k_logit_rows (categorical groups per row)
 constexpr int KS1 = LR_NG > KSM ? LR_NG : KSM;  // max x1p slabs k_hid sums
 constexpr int lr_cpg(int SK, int KD) { return SK / (LR_NG * KD) > 0 ? SK / (LR_NG * KD) : 1; }
+// output columns per workgroup of k_hid / k_gate: 16, or 8 (twice the workgroups, half the weight rows each; the
+// 16-wide MFMA tile then carries 8 zero weight rows in k_hid, and r|c + u|0 gate rows in k_gate)
+#ifndef SD_SCAN_HCW
+#define SD_SCAN_HCW 16
+#endif
+#ifndef SD_SCAN_GCW
+#define SD_SCAN_GCW 8
+#endif
+// output columns per workgroup of k_dlogit / k_dgru / k_dhh (16 or 8)
+#ifndef SD_SCAN_DLCW
+#define SD_SCAN_DLCW 16
+#endif
+#ifndef SD_SCAN_DGCW
+#define SD_SCAN_DGCW 16
+#endif
+#ifndef SD_SCAN_DHCW
+#define SD_SCAN_DHCW 16
+#endif
 // ------------------------------------------------------------------------------------------- scratch layout
 struct Work {
   float *x0s, *x1s, *ops, *ssh, *dotp, *dxs, *dhin, *gq, *ch, *w1t;
@@ -219,8 +255,8 @@ Work work_layout(const sd_rssm_scan& d, float* base) {
   w.x0s = take(d.ks_d * BU);
   w.x1s = take((long)KS1 * BU);  // ks_s slabs, or k_logit_rows' LR_NG
   w.ops = take(d.ks_d * BU);
-  w.ssh = take(NT * d.D);   // per row tile: (D/16 column tiles) x 16 row partials
-  w.dotp = take(NT * d.D);
+  w.ssh = take(NT * MR * (d.D / 8));  // per row tile: 16 rows x (D/16 or D/8 column tiles) partials
+  w.dotp = take(NT * MR * (d.D / 8));  // per row tile: 16 rows x (D/16 or D/8 column tiles) partials
   w.dxs = take((long)d.G * d.B * 3 * d.U);
   w.dhin = take((long)d.B * d.D);
   w.gq = take((long)d.B * d.D);
@@ -238,6 +274,11 @@ constexpr int NU = UH / 128;   // float4 columns per prologue thread over a hidd
 SD_DEV bool reset_at(const sd_rssm_scan& d, int t, int b) {
   return d.reset[d.reset_bm ? (long)b * d.T + t : (long)t * d.B + b] != 0;
 }
+// the raw flag byte of (min(t, T - 1), b), for an unconditional load whose value is only tested later
+SD_DEV unsigned char reset_byte(const sd_rssm_scan& d, int t, int b) {
+  const int tc = t < d.T ? t : d.T - 1;
+  return d.reset[d.reset_bm ? (long)b * d.T + tc : (long)tc * d.B + b];
+}
 
 struct SlabProb {
   const float* A;
@@ -245,10 +286,11 @@ struct SlabProb {
   const float* W;
   long ldw;
   float* out;                 // slab s at out + s*M*N
-  const unsigned char* mask;  // rows whose input is reset (output row forced to 0), or null; row r at mask[r * mstride]
+  const unsigned char* mask;  // reset flags (a valid pointer even when unused); row r at mask[r * mstride]
   uint64_t* trace;            // SD_SCAN_TRACE builds: phase timestamps (sd_rssm_scan.trace), slot below
   int slot;
   int mstride;
+  int use_mask;               // 1: rows whose flag is set are forced to 0 (their input was reset)
 };
 
 // row-tiled GEMM into split-K slabs: out[s][m][n] = A[m, span_s] . W[n, span_s]; grid (N/16, ks * row tiles, nprob)
@@ -260,13 +302,14 @@ __global__ __launch_bounds__(NTHR) void k_slab(SlabProb p0, SlabProb p1, int M, 
   SD_TR_BEGIN
   const SlabProb p = blockIdx.z ? p1 : p0;
   const int s = (int)blockIdx.y % ks, rb = ((int)blockIdx.y / ks) * rt, nr = min(rt, M - rb);
-  const int n0 = blockIdx.x * 16, kb = s * span, nch = span / 16;
+  const int n0 = xcd_tile(blockIdx.x, gridDim.x) * 16, kb = s * span, nch = span / 16;
   Core<1, CPW> core;
   const float* wt[1] = {p.W + (long)(n0 + l16) * p.ldw + kb};
   core.load_b(wt, nch, wave, q);
   const int erow = tid >> 4;
-  const bool masked = tid < 256 && erow < nr && p.mask && p.mask[(long)(rb + erow) * p.mstride];
+  const unsigned char mflag = p.mask[(long)(rb + (erow < nr ? erow : nr - 1)) * p.mstride];  // read unconditionally
   core.run_glb(p.A + (long)rb * p.lda + kb, p.lda, nr, nch, wave, l16, q);
+  const bool masked = p.use_mask && mflag;
   SD_TR(1)
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
@@ -312,47 +355,54 @@ SD_DEV long in_row(const sd_rssm_scan& d, int t, int b) {
 }
 
 // X0F: x0 = silu(rms(x0p)) was formed by the previous step's k_logit_rows (written into xcat), read as it stands;
-// otherwise (t = 0, or the k_logit path) summed from the split-K slabs and normalised here
-template <int CPW, int NG, bool X0F>
+// otherwise (t = 0, or the k_logit path) summed from the split-K slabs and normalised here. CW: output columns per
+// workgroup (16 or 8; grid D / CW), the row partials of hp^2 then come per CW-column tile.
+template <int CPW, int NG, bool X0F, int CW>
 __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_TR_BEGIN
   SD_THREAD_IDS
   SD_ROW_TILE
   const int B = d.B, D = d.D, Dg = D / d.G, Ig = Dg + 3 * UH, ldp = Ig + 4;
-  const int tile = blockIdx.x, n0 = tile * 16, g = n0 / Dg;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x), n0 = tile * CW, g = n0 / Dg;
   Core<1, CPW> core;
-  const float* wt[1] = {d.Wh + (long)(n0 + l16) * Ig};
+  const float* wt[1] = {d.Wh + (long)(n0 + (l16 & (CW - 1))) * Ig};  // CW 8: lanes 8..15 repeat rows (discarded)
   core.load_b(wt, Ig / 16, wave, q);
   const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
   const bool rv = row < nr;
+  const int grc = rv ? gr : rb + nr - 1;  // rows past the tile read the tile's last row (results discarded)
   const long tBU = (long)t * B * UH;
   f32x4 h[NG], x0[NU], x1[NU], x2v[NU], b0v[NU], b1v[NU], n0v[NU], n1v[NU];
-  ld_row(h, d.h_in + (long)t * B * D + (long)gr * D + (long)g * Dg, Dg, rv, t32);
+  f32x4 x0p[X0F ? 1 : KSM][NU], x1p[KS1][NU];
+  ld_row(h, d.h_in + (long)t * B * D + (long)grc * D + (long)g * Dg, t32);
   if constexpr (X0F) {
-    ld_row(x0, d.xcat + 3 * tBU + (long)gr * 3 * UH, UH, rv, t32);
+    ld_row(x0, d.xcat + 3 * tBU + (long)grc * 3 * UH, t32);
   } else {
-    ld_slabs<NU, KSM>(x0, w.x0s + (long)gr * UH, (long)B * UH, d.ks_d, UH, rv, t32);
-    ld_row(b0v, d.b0, UH, true, t32);
-    ld_row(n0v, d.n0, UH, true, t32);
+    ld_slabs<NU, KSM>(x0p, w.x0s + (long)grc * UH, (long)B * UH, d.ks_d, t32);
+    ld_row(b0v, d.b0, t32);
+    ld_row(n0v, d.n0, t32);
   }
-  ld_slabs<NU, KS1>(x1, w.x1s + (long)gr * UH, (long)B * UH, d.ks_s, UH, rv, t32);
-  ld_row(x2v, d.x2 + in_row(d, t, gr) * UH, UH, rv, t32);
-  ld_row(b1v, d.b1, UH, true, t32);
-  ld_row(n1v, d.n1, UH, true, t32);
-  const float bhv = d.bh[n0 + (tid & 15)];
-#pragma unroll
-  for (int i = 0; i < NU; ++i) x1[i] += b1v[i];
+  ld_slabs<NU, KS1>(x1p, w.x1s + (long)grc * UH, (long)B * UH, d.ks_s, t32);
+  ld_row(b1v, d.b1, t32);
+  ld_row(n1v, d.n1, t32);
+  ld_row(x2v, d.x2 + in_row(d, t, grc) * UH, t32);
+  const int ec = tid & 15;
+  const float bhv = d.bh[n0 + (ec & (CW - 1))];
+  // every load is in flight: now the prologue arithmetic
   f32x4 y0[NU], y1[NU];
   float r0 = 0.f;
   if constexpr (X0F) {
 #pragma unroll
     for (int i = 0; i < NU; ++i) y0[i] = x0[i];
   } else {
+    sum_slabs(x0, x0p, d.ks_d);
 #pragma unroll
     for (int i = 0; i < NU; ++i) x0[i] += b0v[i];
     r0 = rms_silu_rows(x0, n0v, UH, d.eps, rv, y0);
   }
+  sum_slabs(x1, x1p, d.ks_s);
+#pragma unroll
+  for (int i = 0; i < NU; ++i) x1[i] += b1v[i];
   const float r1 = rms_silu_rows(x1, n1v, UH, d.eps, rv, y1);
   float* P = smem + core_lds_floats<1>() + row * ldp;
   st_row(P, h, Dg, t32);
@@ -383,67 +433,75 @@ __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   SD_TR(2)
   if (tid < 256) {
     const int er = tid >> 4, c = tid & 15;
+    const bool ok = er < nr && (CW == 16 || c < CW);
     const float v = C[er * 16 + c] + bhv;
-    if (er < nr) d.hp[(long)t * B * D + (long)(rb + er) * D + n0 + c] = v;
-    const float ss = group_sum<16>(er < nr ? v * v : 0.f);
-    if (c == 0) w.ssh[((long)blockIdx.z * MR + er) * (D / 16) + tile] = ss;
+    if (ok) d.hp[(long)t * B * D + (long)(rb + er) * D + n0 + c] = v;
+    const float ss = group_sum<16>(ok ? v * v : 0.f);
+    if (c == 0) w.ssh[((long)blockIdx.z * MR + er) * (D / CW) + tile] = ss;
   }
   SD_TR_END(d.trace, d.trace_slot)
 }
 
 // gates = BlockLinear(dyn_gru)(silu(rms(hp))) + bg; deter = GRU(gates, h_in) (rssm.py:65-75); h_in[t+1] masked.
-// grid (D/16): workgroup = 16 deter columns of one block, with their r / c / u gate rows (3 tiles).
-template <int CPW, int NG>
+// grid (D/CW): workgroup = CW deter columns of one block with their r / c / u gate rows: CW 16 = 3 MFMA tiles (r, c,
+// u); CW 8 = 2 tiles (r | c, u | zero rows). HCW: k_hid's column tile (D / HCW row partials of hp^2 per row).
+template <int CPW, int NG, int CW, int HCW>
 __global__ __launch_bounds__(NTHR) void k_gate(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_TR_BEGIN
   SD_THREAD_IDS
   SD_ROW_TILE
+  constexpr int NTL = CW == 16 ? 3 : 2, CL = 16 * NTL;
   const int B = d.B, D = d.D, Dg = D / d.G, ldp = Dg + 4;
-  const int tile = blockIdx.x, n0 = tile * 16, g = n0 / Dg, j0 = n0 % Dg;
-  Core<3, CPW> core;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x), n0 = tile * CW, g = n0 / Dg, j0 = n0 % Dg;
+  Core<NTL, CPW> core;
   const float* wg = d.Wg + (long)g * 3 * Dg * Dg;
-  const float* wt[3] = {wg + (long)(j0 + l16) * Dg, wg + (long)(Dg + j0 + l16) * Dg, wg + (long)(2 * Dg + j0 + l16) * Dg};
+  const float* wt[NTL];
+  if constexpr (CW == 16) {
+    wt[0] = wg + (long)(j0 + l16) * Dg;
+    wt[1] = wg + (long)(Dg + j0 + l16) * Dg;
+    wt[NTL - 1] = wg + (long)(2 * Dg + j0 + l16) * Dg;
+  } else {  // tile 1's lanes 8..15 repeat the u rows (their output columns are discarded)
+    wt[0] = wg + (long)(l16 < 8 ? j0 + l16 : Dg + j0 + l16 - 8) * Dg;
+    wt[NTL - 1] = wg + (long)(2 * Dg + j0 + (l16 & 7)) * Dg;
+  }
   core.load_b(wt, Dg / 16, wave, q);
   const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
   const bool rv = row < nr;
-  f32x4 pv[2];
-  ld_parts(pv, w.ssh + ((long)blockIdx.z * MR + row) * (D / 16), D / 16, t32);
+  const int grc = rv ? gr : rb + nr - 1;
+  constexpr int NPP = (4096 / HCW + 127) / 128;  // float4 partial loads per thread (D <= 4096)
+  f32x4 pv[NPP];
+  ld_parts(pv, w.ssh + ((long)blockIdx.z * MR + row) * (D / HCW), D / HCW, t32);
   f32x4 hv[NG], nv[NG];
-  ld_row(hv, d.hp + (long)t * B * D + (long)gr * D + (long)g * Dg, Dg, rv, t32);
-  ld_row(nv, d.nh + (long)g * Dg, Dg, true, t32);
-  // epilogue operands (thread = (row er, column c))
+  ld_row(hv, d.hp + (long)t * B * D + (long)grc * D + (long)g * Dg, t32);
+  ld_row(nv, d.nh + (long)g * Dg, t32);
+  // epilogue operands (thread = (row er, column c < CW)), read unconditionally at clamped indices
   const int er = (tid >> 4) & 15, c = tid & 15, j = j0 + c, col = n0 + c, ger = rb + er;
-  const bool ev = tid < 256 && er < nr;
+  const bool ev = tid < 256 && er < nr && (CW == 16 || c < CW);
+  const int cc_ = c & (CW - 1), gerc = er < nr ? ger : rb + nr - 1;
   const float* bg = d.bg + (long)g * 3 * Dg;
-  float bra = 0.f, bca = 0.f, bua = 0.f, hprev = 0.f;
-  bool rnext = false;
-  if (ev) {
-    bra = bg[j];
-    bca = bg[Dg + j];
-    bua = bg[2 * Dg + j];
-    hprev = d.h_in[(long)t * B * D + (long)ger * D + col];
-    rnext = t + 1 < d.T && reset_at(d, t + 1, ger);
-  }
-  const float r = rsqrtf(sum_parts(pv) / (float)D + d.eps);
+  const float bra = bg[j0 + cc_], bca = bg[Dg + j0 + cc_], bua = bg[2 * Dg + j0 + cc_];
+  const float hprev = d.h_in[(long)t * B * D + (long)gerc * D + n0 + cc_];
+  const unsigned char rflag = reset_byte(d, t + 1, gerc);
+  const float r = rsqrtf(sum_parts(pv, D / HCW, t32) / (float)D + d.eps);
   if (rv && t32 == 0 && tile == 0) d.rh[(long)t * B + gr] = r;
   f32x4 y[NG];
 #pragma unroll
   for (int i = 0; i < NG; ++i)
 #pragma unroll
     for (int k = 0; k < 4; ++k) y[i][k] = rv ? siluf_(hv[i][k] * r * nv[i][k]) : 0.f;
-  st_row(smem + core_lds_floats<3>() + row * ldp, y, Dg, t32);
+  st_row(smem + core_lds_floats<NTL>() + row * ldp, y, Dg, t32);
   if (rv && j0 == 0) st_row(d.hh + (long)t * B * D + (long)gr * D + (long)g * Dg, y, Dg, t32);
   __syncthreads();
   SD_TR(1)
-  core.run_lds(smem + core_lds_floats<3>(), ldp, Dg / 16, wave, l16, q);
-  float* C = smem + NW * 3 * 256;
+  core.run_lds(smem + core_lds_floats<NTL>(), ldp, Dg / 16, wave, l16, q);
+  float* C = smem + NW * NTL * 256;
   core.reduce(smem, C, tid, wave, lane);
   SD_TR(2)
   if (ev) {
-    const float ra = C[er * 48 + c] + bra;
-    const float ca = C[er * 48 + 16 + c] + bca;
-    const float ua = C[er * 48 + 32 + c] + bua;
+    const float ra = C[er * CL + c] + bra;
+    const float ca = C[er * CL + (CW == 16 ? 16 : 8) + c] + bca;
+    const float ua = C[er * CL + (CW == 16 ? 32 : 16) + c] + bua;
     float* gw = d.gates + (long)t * B * 3 * D + (long)ger * 3 * D + (long)g * 3 * Dg;
     gw[j] = ra;
     gw[Dg + j] = ca;
@@ -454,7 +512,7 @@ __global__ __launch_bounds__(NTHR) void k_gate(sd_rssm_scan d, Work w, int t) {
     const float out = u * cc + (1.f - u) * hprev;
     d.deter[(long)t * B * D + (long)ger * D + col] = out;
     if (d.post_deter) d.post_deter[((long)ger * d.T + t) * D + col] = out;  // batch-major copy (RSSM.observe's output)
-    if (t + 1 < d.T) d.h_in[(long)(t + 1) * B * D + (long)ger * D + col] = rnext ? 0.f : out;
+    if (t + 1 < d.T) d.h_in[(long)(t + 1) * B * D + (long)ger * D + col] = rflag ? 0.f : out;
   }
   SD_TR_END(d.trace, d.trace_slot)
 }
@@ -476,11 +534,13 @@ __global__ __launch_bounds__(NTHR) void k_logit(sd_rssm_scan d, Work w, int t) {
   core.load_b(wt, UH / 16, wave, q);
   const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
   const bool rv = row < nr;
+  const int grc = rv ? gr : rb + nr - 1;
   const long tBU = (long)t * B * UH;
-  f32x4 x[NU], e[NU], nv[NU];
-  ld_slabs<NU, KSM>(x, w.ops + (long)gr * UH, (long)B * UH, d.ks_d, UH, rv, t32);
-  ld_row(e, d.eproj + in_row(d, t, gr) * UH, UH, rv, t32);
-  ld_row(nv, d.no, UH, true, t32);
+  f32x4 x[NU], e[NU], nv[NU], xs[KSM][NU];
+  ld_slabs<NU, KSM>(xs, w.ops + (long)grc * UH, (long)B * UH, d.ks_d, t32);
+  ld_row(e, d.eproj + in_row(d, t, grc) * UH, t32);
+  ld_row(nv, d.no, t32);
+  sum_slabs(x, xs, d.ks_d);
   // sampler operands + noise, independent of the contraction
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
   float blv[NE], gn[NE];
@@ -575,39 +635,48 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
   const bool ts = tid < NC;
   const int lt = tid % KD;
-  float blv = 0.f, gn = 0.f;
-  if (ts) {
-    blv = d.bl[n0 + tid];
+  // every load of the launch is issued unconditionally (threads past U / NC read valid duplicates), values used later
+  const float blv = d.bl[n0 + (tid % NC)];
+  const unsigned char rflag = reset_byte(d, t + 1, b);
+  const int uc = tid % UH;
+  float part[KSM];
+#pragma unroll
+  for (int s = 0; s < KSM; ++s) part[s] = w.ops[(long)(s < d.ks_d ? s : d.ks_d - 1) * B * UH + (long)b * UH + uc];
+  const float ev_ = d.eproj[in_row(d, t, b) * UH + uc], nw_ = d.no[uc];
+  // one workgroup per row also forms the NEXT step's x0 = silu(rms(x0p)), x0p = sum of the _dyn_in0 slabs k_slab
+  // wrote before this launch + b0 (rssm.py:52-56), so k_hid stages the finished row instead of every column tile
+  // summing the slabs and normalising again (same slab order and bias add as k_hid's own path). Its loads come last:
+  // the branch around them may drain the queue, which by then holds nothing that is not needed anyway.
+  const bool x0w = more && g == (gridDim.x > 1 ? 1 : 0);
+  float part0[KSM], b0_ = 0.f, n0w = 0.f;
+  if (x0w) {
+#pragma unroll
+    for (int s = 0; s < KSM; ++s) part0[s] = w.x0s[(long)(s < d.ks_d ? s : d.ks_d - 1) * B * UH + (long)b * UH + uc];
+    b0_ = d.b0[uc];
+    n0w = d.n0[uc];
+  }
+  const bool rnext = t + 1 < d.T && rflag;
+  float gn = 0.f;
+  if (ts)
     gn = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)t,
                    (uint64_t)((long)b * S + g * CPG + tid / KD + d.group_offset) * KD + lt);
-  }
-  const bool rnext = t + 1 < d.T && reset_at(d, t + 1, b);
   // obs_net_0 output row (sum of the deter-half slabs + the hoisted embed half with bias), RMSNorm + SiLU
   float x = 0.f, nw = 0.f;
   if (tid < UH) {
-    float part[KSM];
-#pragma unroll
-    for (int s = 0; s < KSM; ++s) part[s] = s < d.ks_d ? w.ops[(long)s * B * UH + (long)b * UH + tid] : 0.f;
     x = part[0];
 #pragma unroll
-    for (int s = 1; s < KSM; ++s) x += part[s];
-    x += d.eproj[in_row(d, t, b) * UH + tid];
-    nw = d.no[tid];
+    for (int s = 1; s < KSM; ++s)
+      if (s < d.ks_d) x += part[s];
+    x += ev_;
+    nw = nw_;
   }
-  // one workgroup per row also forms the NEXT step's x0 = silu(rms(x0p)), x0p = sum of the _dyn_in0 slabs k_slab
-  // wrote before this launch + b0 (rssm.py:52-56), so k_hid stages the finished row instead of every column tile
-  // summing the slabs and normalising again (same slab order and bias add as k_hid's own path)
-  const bool x0w = more && g == (gridDim.x > 1 ? 1 : 0);
-  float x0v = 0.f, n0w = 0.f;
+  float x0v = 0.f;
   if (x0w && tid < UH) {
-    float part[KSM];
+    x0v = part0[0];
 #pragma unroll
-    for (int s = 0; s < KSM; ++s) part[s] = s < d.ks_d ? w.x0s[(long)s * B * UH + (long)b * UH + tid] : 0.f;
-    x0v = part[0];
-#pragma unroll
-    for (int s = 1; s < KSM; ++s) x0v += part[s];
-    x0v += d.b0[tid];
-    n0w = d.n0[tid];
+    for (int s = 1; s < KSM; ++s)
+      if (s < d.ks_d) x0v += part0[s];
+    x0v += b0_;
   }
   float ss = wave_sum(x * x);
   const float ss0 = wave_sum(x0v * x0v);
@@ -732,6 +801,23 @@ SD_DEV float in_grad(const sd_rssm_scan& d, const float* g, const float* g2, int
   const float a = g ? g[r * W + col] : 0.f;
   return g2 ? a + g2[r * d.ld_g2 + col] : a;
 }
+// the same as two unconditional loads (a missing summand reads `dummy`, any valid float) and a later combine, so the
+// loads can be issued with the rest of a launch's prologue (see "load helpers")
+struct InGrad {
+  float a, b;
+  SD_DEV void load(const sd_rssm_scan& d, const float* g, const float* g2, int t, int row, int col, int W,
+                   const float* dummy) {
+    const long r = d.bm_grads ? (long)row * d.T + t : (long)t * d.B + row;
+    const float* pa = g ? g + r * W + col : dummy;  // address selects, one load each
+    const float* pb = (d.bm_grads && g2) ? g2 + r * d.ld_g2 + col : dummy;
+    a = *pa;
+    b = *pb;
+  }
+  SD_DEV float value(const sd_rssm_scan& d, const float* g, const float* g2) const {
+    const float av = g ? a : 0.f;
+    return (d.bm_grads && g2) ? av + b : av;
+  }
+};
 
 // dl[T-1] = d_logit + sampler backward (no carry yet). Elementwise, teams of KD lanes.
 template <int KD>
@@ -749,21 +835,21 @@ __global__ __launch_bounds__(256) void k_sbwd_last(sd_rssm_scan d) {
   if (v) d.dl[o] = in_grad(d, d.d_logit, nullptr, t, row, k, SK) + dl;
 }
 
-// d_o = dl[t] . Wl   (dl built by the previous launch). grid (U/16)
-template <int CPW, int NS>
+// d_o = dl[t] . Wl   (dl built by the previous launch). grid (U/CW)
+template <int CPW, int NS, int CW>
 __global__ __launch_bounds__(NTHR) void k_dlogit(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_TR_BEGIN
   SD_THREAD_IDS
   SD_ROW_TILE
   const int B = d.B, SK = d.SK, ldp = SK + 4;
-  const int n0 = blockIdx.x * 16;
+  const int n0 = xcd_tile(blockIdx.x, gridDim.x) * CW;
   Core<1, CPW> core;
-  const float* wt[1] = {d.WlT + (long)(n0 + l16) * SK};
+  const float* wt[1] = {d.WlT + (long)(n0 + (l16 & (CW - 1))) * SK};
   core.load_b(wt, SK / 16, wave, q);
   const int row = tid >> 5, t32 = tid & 31;
   f32x4 v[NS];
-  ld_row(v, d.dl + (long)t * B * SK + (long)(rb + row) * SK, SK, row < nr, t32);
+  ld_row(v, d.dl + (long)t * B * SK + (long)(rb + (row < nr ? row : nr - 1)) * SK, t32);
   st_row(smem + core_lds_floats<1>() + row * ldp, v, SK, t32);
   __syncthreads();
   SD_TR(1)
@@ -773,44 +859,45 @@ __global__ __launch_bounds__(NTHR) void k_dlogit(sd_rssm_scan d, Work w, int t) 
   SD_TR(2)
   if (tid < 256) {
     const int er = tid >> 4, c = tid & 15;
-    if (er < nr) d.d_o[(long)t * B * UH + (long)(rb + er) * UH + n0 + c] = C[er * 16 + c];
+    if (er < nr && (CW == 16 || c < CW)) d.d_o[(long)t * B * UH + (long)(rb + er) * UH + n0 + c] = C[er * 16 + c];
   }
   SD_TR_END(d.trace, d.trace_slot)
 }
 
 // d_op = RMSNorm-SiLU backward (prologue); dh = d_deter + carry_h + d_op . Wo[:, :D]; GRU backward (epilogue).
-// grid (D/16)
+// grid (D/CW)
+template <int CW>
 __global__ __launch_bounds__(NTHR) void k_dgru(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_TR_BEGIN
   SD_THREAD_IDS
   SD_ROW_TILE
   const int B = d.B, D = d.D, Dg = D / d.G, ldp = UH + 4;
-  const int tile = blockIdx.x, n0 = tile * 16;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x), n0 = tile * CW;
   Core<1, 2> core;
-  const float* wt[1] = {d.WoDT + (long)(n0 + l16) * UH};
+  const float* wt[1] = {d.WoDT + (long)(n0 + (l16 & (CW - 1))) * UH};
   core.load_b(wt, UH / 16, wave, q);
   const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
   const bool rv = row < nr;
+  const int grc = rv ? gr : rb + nr - 1;
   const long tBU = (long)t * B * UH;
   f32x4 xv[NU], dy[NU], nv[NU];
-  ld_row(xv, d.op + tBU + (long)gr * UH, UH, rv, t32);
-  ld_row(dy, d.d_o + tBU + (long)gr * UH, UH, rv, t32);
-  ld_row(nv, d.no, UH, true, t32);
-  const float r = rv ? d.ro[(long)t * B + gr] : 0.f;
-  // epilogue operands
-  const int er = (tid >> 4) & 15, c = tid & 15, col = n0 + c, g = col / Dg, j = col % Dg, ger = rb + er;
-  const bool ev = tid < 256 && er < nr;
+  ld_row(xv, d.op + tBU + (long)grc * UH, t32);
+  ld_row(dy, d.d_o + tBU + (long)grc * UH, t32);
+  ld_row(nv, d.no, t32);
+  const float r_ = d.ro[(long)t * B + grc];
+  // epilogue operands, read unconditionally at clamped indices
+  const int er = (tid >> 4) & 15, c = tid & 15, col = n0 + (c & (CW - 1)), g = col / Dg, j = col % Dg;
+  const int ger = er < nr ? rb + er : rb + nr - 1;
+  const bool ev = tid < 256 && er < nr && (CW == 16 || c < CW);
   const long od = (long)t * B * D + (long)ger * D + col;
   const long gb = (long)t * B * 3 * D + (long)ger * 3 * D + (long)g * 3 * Dg;
-  float dh0 = 0.f, ra = 0.f, ca = 0.f, ua = 0.f, hv = 0.f;
-  if (ev) {
-    dh0 = in_grad(d, d.d_deter, d.d_deter2, t, ger, col, D) + w.ch[(long)ger * D + col];
-    ra = d.gates[gb + j];
-    ca = d.gates[gb + Dg + j];
-    ua = d.gates[gb + 2 * Dg + j];
-    hv = d.h_in[od];
-  }
+  InGrad ig;
+  ig.load(d, d.d_deter, d.d_deter2, t, ger, col, D, w.ch);
+  const float chv = w.ch[(long)ger * D + col];
+  const float ra = d.gates[gb + j], ca = d.gates[gb + Dg + j], ua = d.gates[gb + 2 * Dg + j];
+  const float hv = d.h_in[od];
+  const float r = rv ? r_ : 0.f;
   float dot = 0.f;
   f32x4 gq[NU];
 #pragma unroll
@@ -839,7 +926,7 @@ __global__ __launch_bounds__(NTHR) void k_dgru(sd_rssm_scan d, Work w, int t) {
   core.reduce(smem, C, tid, wave, lane);
   SD_TR(2)
   if (ev) {
-    const float dh = dh0 + C[er * 16 + c];
+    const float dh = (ig.value(d, d.d_deter, d.d_deter2) + chv) + C[er * 16 + c];
     const float rs = sigmoidf_(ra);
     const float cc = tanhf(rs * ca);
     const float u = sigmoidf_(ua - 1.f);
@@ -853,27 +940,25 @@ __global__ __launch_bounds__(NTHR) void k_dgru(sd_rssm_scan d, Work w, int t) {
 }
 
 // d_hh = d_gates_g . Wg[g] (block GEMM); epilogue: RMSNorm-SiLU backward pieces of dyn_hid's norm (g*w and the
-// per-tile row partials of sum g*xhat). grid (D/16)
-template <int CPW>
+// per-tile row partials of sum g*xhat). grid (D/CW)
+template <int CPW, int CW>
 __global__ __launch_bounds__(NTHR) void k_dhh(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_TR_BEGIN
   SD_THREAD_IDS
   SD_ROW_TILE
   const int B = d.B, D = d.D, Dg = D / d.G;
-  const int tile = blockIdx.x, n0 = tile * 16, g = n0 / Dg, j0 = n0 % Dg;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x), n0 = tile * CW, g = n0 / Dg, j0 = n0 % Dg;
   Core<1, CPW> core;
-  const float* wt[1] = {d.WgT + ((long)g * Dg + j0 + l16) * 3 * Dg};
+  const float* wt[1] = {d.WgT + ((long)g * Dg + j0 + (l16 & (CW - 1))) * 3 * Dg};
   core.load_b(wt, 3 * Dg / 16, wave, q);
-  const int er = (tid >> 4) & 15, c = tid & 15, col = n0 + c, ger = rb + er;
-  const bool ev = tid < 256 && er < nr;
+  const int er = (tid >> 4) & 15, c = tid & 15, col = n0 + (c & (CW - 1));
+  const int ger = er < nr ? rb + er : rb + nr - 1;
+  const bool ev = tid < 256 && er < nr && (CW == 16 || c < CW);
   const long o = (long)t * B * D + (long)ger * D + col;
-  float xh = 0.f, wv = 0.f;
-  if (ev) {
-    xh = d.hp[o] * d.rh[(long)t * B + ger];
-    wv = d.nh[col];
-  }
+  const float hpv = d.hp[o], rhv = d.rh[(long)t * B + ger], wv = d.nh[col];  // unconditional, clamped
   core.run_glb(d.d_gates + ((long)t * B + rb) * 3 * D + (long)g * 3 * Dg, 3 * (long)D, nr, 3 * Dg / 16, wave, l16, q);
+  const float xh = hpv * rhv;
   SD_TR(1)
   float* C = smem + NW * 256;
   core.reduce(smem, C, tid, wave, lane);
@@ -888,7 +973,7 @@ __global__ __launch_bounds__(NTHR) void k_dhh(sd_rssm_scan d, Work w, int t) {
       part = gq * xh;
     }
     part = group_sum<16>(part);
-    if (c == 0) w.dotp[((long)blockIdx.z * MR + er) * (D / 16) + tile] = part;
+    if (c == 0) w.dotp[((long)blockIdx.z * MR + er) * (D / CW) + tile] = part;
   }
   SD_TR_END(d.trace, d.trace_slot)
 }
@@ -904,8 +989,9 @@ __host__ __device__ inline int kx_of(int G) { return G % SD_SCAN_KX == 0 ? SD_SC
 // one grid:
 //   P0: d_xcat slab s = d_hp[:, blocks of s] . Wsh[those rows]   ((3U/16) * KX workgroups, K = G/KX blocks)
 //   P1: d_hin[:, g] += d_hp_g . Wbd[g]                            (D/16 workgroups, K = one block)
-// CPW / NGX cover the longest span (P0); P1 masks the chunks past its block.
-template <int CPW, int NGX>
+// CPW / NGX cover the longest span (P0); P1 masks the chunks past its block. DHC: k_dhh's column tile (D / DHC row
+// partials).
+template <int CPW, int NGX, int DHC>
 __global__ __launch_bounds__(NTHR) void k_dhp(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
   SD_TR_BEGIN
@@ -917,14 +1003,14 @@ __global__ __launch_bounds__(NTHR) void k_dhp(sd_rssm_scan d, Work w, int t) {
   const bool p0 = blk < NX;
   int n0, k0, K, sl = 0;
   const float* wrow;
-  if (p0) {
+  if (p0) {  // (X / 16 = 48 column tiles per slab: blk % 8 = tile % 8, so the remap stays within a slab)
     sl = blk / (X / 16);
-    n0 = (blk % (X / 16)) * 16;
+    n0 = xcd_tile(blk % (X / 16), X / 16) * 16;
     K = (d.G / KX) * Dg;
     k0 = sl * K;
     wrow = d.WshT + (long)(n0 + l16) * D + k0;
-  } else {
-    n0 = (blk - NX) * 16;
+  } else {  // (NX = 48 KX is a multiple of 8)
+    n0 = xcd_tile(blk - NX, D / 16) * 16;
     const int g = n0 / Dg;
     K = Dg;
     k0 = g * Dg;
@@ -936,17 +1022,20 @@ __global__ __launch_bounds__(NTHR) void k_dhp(sd_rssm_scan d, Work w, int t) {
   core.load_b(wt, K / 16, wave, q);
   const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
   const bool rv = row < nr;
-  f32x4 pv[2];
-  ld_parts(pv, w.dotp + ((long)blockIdx.z * MR + row) * (D / 16), D / 16, t32);
-  const long ob = (long)gr * D + k0;
-  f32x4 gq[NGX], xv[NGX];
-  ld_row(gq, w.gq + ob, K, rv, t32);
-  ld_row(xv, d.hp + (long)t * B * D + ob, K, rv, t32);
-  const float r = rv ? d.rh[(long)t * B + gr] : 0.f;
+  constexpr int NPP = (4096 / DHC + 127) / 128;
+  f32x4 pv[NPP];
+  ld_parts(pv, w.dotp + ((long)blockIdx.z * MR + row) * (D / DHC), D / DHC, t32);
+  const int grc = rv ? gr : rb + nr - 1;
+  const long ob = (long)gr * D + k0, obc = (long)grc * D + k0;
+  f32x4 gq[NGX], xv[NGX];  // (K = D/G = 128 * NGX on both problems: G / KX = 1)
+  ld_row(gq, w.gq + obc, t32);
+  ld_row(xv, d.hp + (long)t * B * D + obc, t32);
+  const float r_ = d.rh[(long)t * B + grc];
   const int er = (tid >> 4) & 15, c = tid & 15, ger = rb + er;
   const bool ev = tid < 256 && er < nr;
-  const float dh_old = (!p0 && ev) ? w.dhin[(long)ger * D + n0 + c] : 0.f;
-  const float dot = sum_parts(pv) / (float)D;
+  const float dh_ = w.dhin[(long)(er < nr ? ger : rb + nr - 1) * D + n0 + c];  // unconditional, used by P1 only
+  const float r = rv ? r_ : 0.f, dh_old = (!p0 && ev) ? dh_ : 0.f;
+  const float dot = sum_parts(pv, D / DHC, t32) / (float)D;
   f32x4 o[NGX];
 #pragma unroll
   for (int i = 0; i < NGX; ++i)
@@ -1026,48 +1115,57 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   constexpr int NT = KD / 16, NE = (MR * KD + NTHR - 1) / NTHR, GM = 8, X = 3 * UH, ldp = UH + 4;
   const int B = d.B, D = d.D, SK = d.SK, S = SK / KD;
   const bool p0 = (int)blockIdx.x < D / KD;
-  const int wid = p0 ? blockIdx.x : blockIdx.x - D / KD, n0 = wid * KD;
+  const int wid = p0 ? xcd_tile(blockIdx.x, D / KD) : xcd_tile(blockIdx.x - D / KD, SK / KD), n0 = wid * KD;
   Core<NT, 2> core;
   const float* wt[NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i) wt[i] = (p0 ? d.W0T : d.W1T) + (long)(n0 + 16 * i + l16) * UH;
   core.load_b(wt, UH / 16, wave, q);
-  // prologue loads: the G slabs of this half's d_xcat part, its pre-norm input and norm weight
+  // prologue loads: the G slabs of this half's d_xcat part, its pre-norm input and norm weight (unconditional, rows
+  // clamped; slabs past KX re-read slab KX - 1 and are not summed)
   const int row = tid >> 5, t32 = tid & 31, gr = rb + row;
   const bool rv = row < nr;
+  const int grc = rv ? gr : rb + nr - 1, KX = kx_of(d.G);
   const long tB = (long)t * B;
   const int hoff = p0 ? 0 : UH;
   const bool wx2 = p0 && wid == 1;  // the x2 part's writer
-  f32x4 part[GM][NU], xv[NU], nv[NU];
+  f32x4 part[GM][NU], part2[GM][NU], xv[NU], nv[NU];
 #pragma unroll
-  for (int g = 0; g < GM; ++g)
-    ld_row(part[g], w.dxs + (long)g * B * X + (long)gr * X + (wx2 ? 2 * UH : hoff), UH, rv && g < kx_of(d.G), t32);
-  const float rr = rv ? (p0 ? d.r0 : d.r1)[tB + gr] : 0.f;
-  ld_row(xv, (p0 ? d.x0p : d.x1p) + (tB + gr) * UH, UH, rv, t32);
-  ld_row(nv, p0 ? d.n0 : d.n1, UH, true, t32);
-  // epilogue operands: element i = (row er, column lt) of the 16 x KD tile
+  for (int g = 0; g < GM; ++g) ld_row(part[g], w.dxs + (long)(g < KX ? g : KX - 1) * B * X + (long)grc * X + hoff, t32);
+  const float rr_ = (p0 ? d.r0 : d.r1)[tB + grc];
+  ld_row(xv, (p0 ? d.x0p : d.x1p) + (tB + grc) * UH, t32);
+  ld_row(nv, p0 ? d.n0 : d.n1, t32);
+  // epilogue operands: element i = (row er, column lt) of the 16 x KD tile, read unconditionally (clamped rows; the
+  // carry_h workgroups read column 0 of the sampler operands and never use them)
   const uint64_t seed = d.seed + (d.seed_ptr ? *d.seed_ptr : 0ull);
   const int tp = t - 1;
-  float e0[NE], e1[NE], e2[NE], gn[NE];
+  float e0[NE], gn[NE];
+  InGrad e1[NE], e2[NE];
+  unsigned char rf[NE];
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {
+    const int i = tid + NTHR * k, er = (i / KD) & 15, lt = i % KD;
+    const int gerc = er < nr ? rb + er : rb + nr - 1, cs = p0 ? 0 : n0 + lt;
+    rf[k] = reset_byte(d, t, gerc);
+    e0[k] = *(p0 ? w.dhin + (long)gerc * D + n0 + lt : d.logit + (long)tp * B * SK + (long)gerc * SK + cs);
+    e1[k].load(d, d.d_stoch, d.d_stoch2, tp, gerc, cs, SK, w.ch);
+    e2[k].load(d, d.d_logit, nullptr, tp, gerc, cs, SK, w.ch);
+  }
+  if (wx2) {  // (last: the branch may drain the queue, which then holds only loads needed anyway)
+#pragma unroll
+    for (int g = 0; g < GM; ++g) ld_row(part2[g], w.dxs + (long)(g < KX ? g : KX - 1) * B * X + (long)grc * X + 2 * UH, t32);
+  }
+  const float rr = rv ? rr_ : 0.f;
   bool rs[NE];
 #pragma unroll
   for (int k = 0; k < NE; ++k) {
     const int i = tid + NTHR * k, er = (i / KD) & 15, lt = i % KD, ger = rb + er;
     const bool ev = i < MR * KD && er < nr;
-    rs[k] = ev && reset_at(d, t, ger);
-    e0[k] = e1[k] = e2[k] = gn[k] = 0.f;
-    if (p0) {
-      if (ev) e0[k] = w.dhin[(long)ger * D + n0 + lt];
-    } else {
-      const long o = (long)tp * B * SK + (long)ger * SK + n0 + lt;
-      if (ev) {
-        e0[k] = d.logit[o];
-        e1[k] = in_grad(d, d.d_stoch, d.d_stoch2, tp, ger, n0 + lt, SK);
-        e2[k] = in_grad(d, d.d_logit, nullptr, tp, ger, n0 + lt, SK);
-      }
+    rs[k] = ev && rf[k] != 0;
+    gn[k] = 0.f;
+    if (!p0)
       gn[k] = sd_gumbel(seed, (uint32_t)d.stream_id, (uint32_t)tp,
                         (uint64_t)((long)ger * S + n0 / KD + d.group_offset) * KD + lt);
-    }
   }
   // the sampler's forward half of step t - 1 (carry_s workgroups): needs only the logit and the noise, so it runs
   // here, beside the prologue loads, instead of after the contraction
@@ -1077,29 +1175,16 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
     for (int k = 0; k < NE; ++k)
       if (tid + NTHR * k < MR * KD) sf[k] = sampler_fwd<KD>(e0[k], gn[k], d.unimix, (tid + NTHR * k) % KD);
   }
-  // d_xcat part = sum of the slabs (k_dx01's order); the x2 writer stores its part and then rebuilds x0's
+  // d_xcat part = sum of the slabs (k_dx01's order); the x2 writer stores its part first
   f32x4 dx[NU];
-#pragma unroll
-  for (int i = 0; i < NU; ++i) {
-    dx[i] = part[0][i];
-#pragma unroll
-    for (int g = 1; g < GM; ++g) dx[i] += part[g][i];
-  }
   if (wx2) {
+    sum_slabs(dx, part2, KX);
     if (rv) {
       st_row(d.d_xcat + (tB + gr) * X + 2 * UH, dx, UH, t32);
       if (d.d_x2_bm) st_row(d.d_x2_bm + ((long)gr * d.T + t) * UH, dx, UH, t32);
     }
-#pragma unroll
-    for (int g = 0; g < GM; ++g)
-      ld_row(part[g], w.dxs + (long)g * B * X + (long)gr * X, UH, rv && g < kx_of(d.G), t32);
-#pragma unroll
-    for (int i = 0; i < NU; ++i) {
-      dx[i] = part[0][i];
-#pragma unroll
-      for (int g = 1; g < GM; ++g) dx[i] += part[g][i];
-    }
   }
+  sum_slabs(dx, part, KX);
   float dot = 0.f;
   f32x4 gg[NU], xh[NU];
 #pragma unroll
@@ -1138,8 +1223,8 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
         if (ev) w.ch[(long)ger * D + n0 + lt] = rs[k] ? 0.f : e0[k] + C[er * KD + lt];
       } else {
         const float cs = rs[k] ? 0.f : C[er * KD + lt];
-        const float dlv = sampler_bwd_tail<KD>(sf[k], ev ? e1[k] + cs : 0.f, d.unimix);
-        if (ev) d.dl[(long)tp * B * SK + (long)ger * SK + n0 + lt] = e2[k] + dlv;
+        const float dlv = sampler_bwd_tail<KD>(sf[k], ev ? e1[k].value(d, d.d_stoch, d.d_stoch2) + cs : 0.f, d.unimix);
+        if (ev) d.dl[(long)tp * B * SK + (long)ger * SK + n0 + lt] = e2[k].value(d, d.d_logit, nullptr) + dlv;
       }
     }
   }
@@ -1221,7 +1306,7 @@ int fwd_phase(const sd_rssm_scan& d, const Work& w, bool lrows, int which, int t
   if (cp_d < 0 || cp_s < 0 || cp_h < 0) return SD_ESHAPE;
   const size_t core1 = core_lds_floats<1>() * 4;
   const size_t lds_hid = core1 + (size_t)MR * (Ig + 4) * 4;
-  const size_t lds_gate = core_lds_floats<3>() * 4 + (size_t)MR * (Dg + 4) * 4;
+  const size_t lds_gate = core_lds_floats<SD_SCAN_GCW == 16 ? 3 : 2>() * 4 + (size_t)MR * (Dg + 4) * 4;
   const long BD = (long)B * D, BS = (long)B * SK;
   const long wod_ld = d.ld_wod > 0 ? d.ld_wod : D;
   sd_rssm_scan dd = d;
@@ -1229,24 +1314,26 @@ int fwd_phase(const sd_rssm_scan& d, const Work& w, bool lrows, int which, int t
   const int rt = dd.row_tile = row_tile_of(d), nt = row_tiles(d);
   dd.trace_slot = t * 8 + which;
   if (which == 0) {
-    SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, nullptr, d.trace, dd.trace_slot, 1};
+    SlabProb p{d.s_in + t * BS, SK, d.W1, SK, w.x1s, d.reset, d.trace, dd.trace_slot, 1, 0};
     SD_CPW_SWITCH(cp_s, k_slab<CP><<<dim3(UH / 16, ks_s * nt, 1), NTHR, core1, st>>>(p, p, B, UH, span_s, ks_s, rt));
   } else if (which == 1) {
     // x0 finished by the previous step's k_logit_rows (lrows, t > 0)
+    constexpr int HC = SD_SCAN_HCW;
     if (lrows && t > 0) {
-      SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG, true>>(lds_hid))) return SD_EARG;
-                                     k_hid<CP, NG, true><<<dim3(D / 16, 1, nt), NTHR, lds_hid, st>>>(dd, w, t)));
+      SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG, true, HC>>(lds_hid))) return SD_EARG;
+                                     k_hid<CP, NG, true, HC><<<dim3(D / HC, 1, nt), NTHR, lds_hid, st>>>(dd, w, t)));
     } else {
-      SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG, false>>(lds_hid))) return SD_EARG;
-                                     k_hid<CP, NG, false><<<dim3(D / 16, 1, nt), NTHR, lds_hid, st>>>(dd, w, t)));
+      SD_NG_SWITCH(Dg, SD_CPW_SWITCH(cp_h, if (!(raise_lds<k_hid<CP, NG, false, HC>>(lds_hid))) return SD_EARG;
+                                     k_hid<CP, NG, false, HC><<<dim3(D / HC, 1, nt), NTHR, lds_hid, st>>>(dd, w, t)));
     }
   } else if (which == 2) {
-    SD_NG_SWITCH(Dg, if (!(raise_lds<k_gate<NG, NG>>(lds_gate))) return SD_EARG;
-                 k_gate<NG, NG><<<dim3(D / 16, 1, nt), NTHR, lds_gate, st>>>(dd, w, t));
+    constexpr int GC = SD_SCAN_GCW, HC = SD_SCAN_HCW;
+    SD_NG_SWITCH(Dg, if (!(raise_lds<k_gate<NG, NG, GC, HC>>(lds_gate))) return SD_EARG;
+                 k_gate<NG, NG, GC, HC><<<dim3(D / GC, 1, nt), NTHR, lds_gate, st>>>(dd, w, t));
   } else if (which == 3) {
-    SlabProb po{d.deter + t * BD, D, d.WoD, wod_ld, w.ops, nullptr, d.trace, dd.trace_slot, 1};
+    SlabProb po{d.deter + t * BD, D, d.WoD, wod_ld, w.ops, d.reset, d.trace, dd.trace_slot, 1, 0};
     SlabProb px{d.deter + t * BD, D, d.W0, D, w.x0s, d.reset_bm ? d.reset + (t + 1) : d.reset + (t + 1) * B, d.trace,
-                dd.trace_slot, d.reset_bm ? d.T : 1};
+                dd.trace_slot, d.reset_bm ? d.T : 1, 1};
     const int np = t + 1 < d.T ? 2 : 1;
     SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d * nt, np), NTHR, core1, st>>>(po, px, B, UH, span_d,
                                                                                         d.ks_d, rt));
@@ -1296,7 +1383,7 @@ extern "C" int sd_rssm_scan_fwd(const sd_rssm_scan* dp, sd_stream stream_) {
   k_init<<<lrows ? 256 : 64, 256, 0, st>>>(d, lrows ? w.w1t : nullptr);
   SD_LAUNCH_CHECK();
   {  // x0p(0) = h_in[0] . W0^T
-    SlabProb p{d.h_in, D, d.W0, D, w.x0s, nullptr, nullptr, 0, 1};
+    SlabProb p{d.h_in, D, d.W0, D, w.x0s, d.reset, nullptr, 0, 1, 0};
     SD_CPW_SWITCH(cp_d, k_slab<CP><<<dim3(UH / 16, d.ks_d * row_tiles(d), 1), NTHR, core_lds_floats<1>() * 4, st>>>(
                             p, p, B, UH, D / d.ks_d, d.ks_d, row_tile_of(d)));
     SD_LAUNCH_CHECK();
@@ -1344,28 +1431,29 @@ extern "C" int sd_rssm_scan_bwd(const sd_rssm_scan* dp, sd_stream stream_) {
   // observed not to be ordered before the first k_dgru (garbage carry in replays)
   k_zero<<<sd_cdiv(B * D, 256), 256, 0, st>>>(w.ch, (long)B * D);
   SD_LAUNCH_CHECK();
+  constexpr int DLC = SD_SCAN_DLCW, DGC = SD_SCAN_DGCW, DHC = SD_SCAN_DHCW;
   const int NX = (3 * UH / 16) * kx_of(d.G);
   SD_KD_SWITCH(d.Kd, k_sbwd_last<KD><<<(int)(((long)B * SK + 255) / 256), 256, 0, st>>>(d));
   SD_LAUNCH_CHECK();
   for (int t = d.T - 1; t >= 0; --t) {
     d.trace_slot = (d.T + t) * 8;
     if (SK == 512) {
-      if (!(raise_lds<k_dlogit<4, 4>>(lds_dl))) return SD_EARG;
-      k_dlogit<4, 4><<<dim3(UH / 16, 1, nt), NTHR, lds_dl, st>>>(d, w, t);
+      if (!(raise_lds<k_dlogit<4, 4, DLC>>(lds_dl))) return SD_EARG;
+      k_dlogit<4, 4, DLC><<<dim3(UH / DLC, 1, nt), NTHR, lds_dl, st>>>(d, w, t);
     } else {
-      if (!(raise_lds<k_dlogit<8, 8>>(lds_dl))) return SD_EARG;
-      k_dlogit<8, 8><<<dim3(UH / 16, 1, nt), NTHR, lds_dl, st>>>(d, w, t);
+      if (!(raise_lds<k_dlogit<8, 8, DLC>>(lds_dl))) return SD_EARG;
+      k_dlogit<8, 8, DLC><<<dim3(UH / DLC, 1, nt), NTHR, lds_dl, st>>>(d, w, t);
     }
     SD_LAUNCH_CHECK();
     d.trace_slot = (d.T + t) * 8 + 1;
-    k_dgru<<<dim3(D / 16, 1, nt), NTHR, lds_dgru, st>>>(d, w, t);
+    k_dgru<DGC><<<dim3(D / DGC, 1, nt), NTHR, lds_dgru, st>>>(d, w, t);
     SD_LAUNCH_CHECK();
     d.trace_slot = (d.T + t) * 8 + 2;
-    SD_CPW_SWITCH(cp_g3, k_dhh<CP><<<dim3(D / 16, 1, nt), NTHR, core1, st>>>(d, w, t));
+    SD_CPW_SWITCH(cp_g3, k_dhh<CP, DHC><<<dim3(D / DHC, 1, nt), NTHR, core1, st>>>(d, w, t));
     SD_LAUNCH_CHECK();
     d.trace_slot = (d.T + t) * 8 + 3;
-    SD_CPW_SWITCH(kspan / 128, if (!(raise_lds<k_dhp<CP, CP>>(lds_dhp))) return SD_EARG;
-                  k_dhp<CP, CP><<<dim3(NX + D / 16, 1, nt), NTHR, lds_dhp, st>>>(d, w, t));
+    SD_CPW_SWITCH(kspan / 128, if (!(raise_lds<k_dhp<CP, CP, DHC>>(lds_dhp))) return SD_EARG;
+                  k_dhp<CP, CP, DHC><<<dim3(NX + D / 16, 1, nt), NTHR, lds_dhp, st>>>(d, w, t));
     SD_LAUNCH_CHECK();
     d.trace_slot = (d.T + t) * 8 + 4;
     if (t > 0) {  // k_carry builds d_x0p / d_x1p itself (the k_dx01 work in its prologue)

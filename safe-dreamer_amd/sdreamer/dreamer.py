@@ -237,7 +237,9 @@ class Dreamer(nn.Module):
         self.marks = K.Marks(self.device) if os.environ.get("SDREAMER_MARKS", "0") != "0" else None
         self._side = torch.cuda.Stream(device=self.device)
         self._prio_streams = None  # (main, side, fill, side fill) of STREAM_PRIO, created at the first replay
-        self._one = None  # device 1.0: the seed gradient of the world-model total (no fill launch per update)
+        # device 1.0: the seed gradient of the world-model total (no fill launch per update); made here, outside any
+        # capture, so its value never depends on which update first asks for it
+        self._one = torch.ones((), dtype=torch.float32, device=self.device)
         self._comm = None  # data parallel: the gradient all-reduce stream (created on first use)
         self._buckets = self._grad_buckets()
         self._graph = None

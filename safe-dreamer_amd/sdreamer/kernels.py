@@ -925,8 +925,8 @@ def metric_vector(values):
         nat.call("sd_multi_stats", ctypes.addressof(st), p(ws), p(dst), len(values), stream())
         if lo:  # a second table's slots add to the first's
             out.add_(dst)
-    if empty:
-        out.index_fill_(0, torch.tensor(sorted(set(empty)), device=out.device), float("nan"))
+    for i in sorted(set(empty)):  # no host-to-device index copy: capture-safe (the S2 phase graph builds metrics)
+        out[i:i + 1].fill_(float("nan"))
     return out
 
 

@@ -472,6 +472,8 @@ class ImagACLossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_total, _gp, _gv, _gadv):
+        if _gp is not None or _gv is not None:  # (set_materialize_grads(False): unused outputs arrive as None)
+            raise RuntimeError("ImagACLossFn: backpropagate the weighted total, not the policy / value loss alone")
         l2, bins, r, sl, w, adv = ctx.saved_tensors
         N, H = r.shape
         H1 = w.shape[1]

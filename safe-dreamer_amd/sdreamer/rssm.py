@@ -38,6 +38,7 @@ SCAN_ROW_TILE = int(os.environ.get("SDREAMER_SCAN_ROWTILE", "0"))
 # per direction (forward / backward launches), overriding SCAN_ROW_TILE when set
 SCAN_ROW_TILE_FWD = int(os.environ.get("SDREAMER_SCAN_ROWTILE_FWD", "-1"))
 SCAN_ROW_TILE_BWD = int(os.environ.get("SDREAMER_SCAN_ROWTILE_BWD", "-1"))
+SCAN_KSD = int(os.environ.get("SDREAMER_SCAN_KSD", "8"))
 SCAN_TRACE = None  # uint64 device tensor: per-launch / per-workgroup phase timestamps (tools/scan_trace.py)
 
 
@@ -54,7 +55,9 @@ def _scan_desc(rssm, P, B, T, seed, row_offset, rt, x2, eproj, work, stream_id=S
     d = nat.ScanDesc()
     D, U, SK, Kd, G = rssm._deter, rssm._hidden, rssm.flat_stoch, rssm._discrete, rssm._blocks
     d.B, d.T, d.D, d.U, d.SK, d.Kd, d.G = B, T, D, U, SK, Kd, G
-    d.ks_d, d.ks_s = 4, 2  # K splits of the D-wide / SK-wide step GEMMs (slabs summed by the consumer)
+    # K splits of the D-wide / SK-wide step GEMMs (slabs summed by the consumer): 8 D-wide slabs = 2 x the k_slab
+    # workgroups of 4, each staging half the weight and deter bytes
+    d.ks_d, d.ks_s = (SCAN_KSD if D % (16 * SCAN_KSD) == 0 else 4), 2
     side = SCAN_ROW_TILE_BWD if bwd else SCAN_ROW_TILE_FWD
     d.row_tile = side if side >= 0 else SCAN_ROW_TILE
     if SCAN_TRACE is not None:  # measurement aid (tools/scan_trace.py, a -DSD_SCAN_TRACE build of the library)
@@ -534,10 +537,9 @@ class ObserveScan(torch.autograd.Function):
             if gs2.stride(-1) == 1 and gd2.stride(-1) == 1 and gs2.stride(-2) == gd2.stride(-2) and \
                     gs2.stride(-3) == T * gs2.stride(-2) and gd2.stride(-3) == T * gd2.stride(-2):
                 d.d_stoch2, d.d_deter2, d.ld_g2 = gs2.data_ptr(), gd2.data_ptr(), gs2.stride(-2)
-            else:
-                ds_out = (0 if ds_out is None else ds_out) + gs2.reshape(B, T, SK)
-                dd_out = (0 if dd_out is None else dd_out) + gd2.reshape(B, T, D)
-                d.d_stoch, d.d_deter = ds_out.data_ptr(), dd_out.data_ptr()
+            else:  # never reached on the benched path (DxSink's halves are strided views of one (B, T, F) buffer)
+                raise RuntimeError("ObserveScan: extra posterior gradients must be (B, T, .) views with unit column "
+                                   "stride and a common row stride")
         nat.call("sd_rssm_scan_bwd", ctypes.addressof(d), K.stream())
         gb = ops.grad_buf
         f = lambda x: x.reshape(M, -1)  # noqa: E731

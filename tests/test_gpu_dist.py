@@ -9,7 +9,9 @@ all-reduce on the communication stream, Dreamer._allreduce_bucket). Stated toler
 world-model losses <= 1e-4 relative, other scalar losses <= 1e-3 (sums of differently ordered partial sums), the
 parameters after 4 updates: L2 distance <= 2% of the L2 norm of the 4-update change, and <= 0.1% of the elements off
 by more than 5% of the largest step (LaProp normalises per element, so summation-order noise on near-zero gradients
-moves single elements by up to a step).
+moves single elements by up to a step). The exchange steps themselves are held tighter: the all-reduced gradient
+arena of update 0 (eager: the step leaves the gradients in place) matches the 1-rank gradients element-wise at the
+golden gradient tolerance of test_cal_grad_matches_reference (2e-3 relative + 1e-4 of the tensor's largest |g|).
 """
 import os
 import socket
@@ -51,16 +53,21 @@ def _worker(name, rank, world, port, q):
         data = {k: v[rows].contiguous() for k, v in data.items()}
         init = tuple(t[rows].contiguous() for t in init)
         losses = []
+        g0 = None
         for u in range(UPDATES):
             _, mets = ag.update_batch(data, init, int(z["u0_seed"]) + u)
             losses.append({k: float(v) for k, v in mets.items() if k.startswith("loss/")})
+            if u == 0:  # eager update: all-reduced (mean) gradients, left in the arena by the step
+                g0 = ag._optimizer.arena.grad.detach().cpu().numpy().copy()
         torch.cuda.synchronize()
         p1 = ag._optimizer.arena.data.detach()
-        q.put((rank, losses, (p1 - p0).cpu().numpy(), p1.cpu().numpy(), ag._graph is not None))
+        a = ag._optimizer.arena
+        spans = [(o, o + p.numel()) for o, p in zip(a.offsets, a.params)]
+        q.put((rank, losses, (p1 - p0).cpu().numpy(), p1.cpu().numpy(), ag._graph is not None, g0, spans))
         if world > 1:
             dist.destroy_process_group()
     except BaseException as e:  # report instead of hanging the parent
-        q.put((rank, repr(e), None, None, None))
+        q.put((rank, repr(e), None, None, None, None, None))
         raise
 
 
@@ -103,3 +110,14 @@ def test_two_rank_update_equals_one_rank(name):
         frac = float((np.abs(d) > 0.05 * np.abs(one[2]).max()).mean())
         assert rel_l2 <= 0.02 and frac <= 1e-3, (rank, rel_l2, frac)
     assert np.array_equal(two[0][3], two[1][3]), "ranks diverged"
+    # update 0's gradient arena after the exchange, element-wise per tensor, on both ranks
+    bad = []
+    for rank in (0, 1):
+        g2 = two[rank][5]
+        for lo, hi in one[6]:
+            ref, got = one[5][lo:hi].astype(np.float64), g2[lo:hi].astype(np.float64)
+            err = np.abs(got - ref) - (2e-3 * np.abs(ref) + 1e-4 * np.abs(ref).max() + 1e-12)
+            if err.size and err.max() > 0:
+                i = int(np.argmax(err))
+                bad.append((rank, lo, hi, float(got[i]), float(ref[i])))
+    assert not bad, bad[:8]

@@ -234,7 +234,9 @@ def test_update_matches_reference(name):
     report["bound_ratio"] = {k: {"tensor": t, "ratio": r} for k, (t, r) in bounds.items()}
     report["bound_ratio_f64"] = {k: {"tensor": t, "ratio": r} for k, (t, r) in bounds64.items()}
     print(name, report)
-    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "golden")
+    if not os.environ.get("SDREAMER_GOLDEN_REPORT"):  # opt-in file report (tools/r05_*.sh set it)
+        return
+    out = os.environ["SDREAMER_GOLDEN_REPORT"]
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, f"{name}{'_f32' if os.environ.get('SDREAMER_FAST_GEMM') == '0' else ''}.json"),
               "w") as f:

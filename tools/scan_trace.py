@@ -63,7 +63,12 @@ def main():
         x = x[used]
         first, last_in, end = x[:, 0].min(), x[:, 0].max(), x[:, 3].max()
         r = rows.setdefault((ph, name), {"gap": [], "skew": [], "stage": [], "mma": [], "epi": [], "span": [],
-                                         "wgs": int(used.sum())})
+                                         "wstage": [], "wmma": [], "wepi": [], "wid": [], "wgs": int(used.sum())})
+        wi = int(np.argmax(x[:, 3]))  # the workgroup that exits last: its own phases
+        r["wstage"].append((x[wi, 1] - x[wi, 0]) * 10e-3)
+        r["wmma"].append((x[wi, 2] - x[wi, 1]) * 10e-3)
+        r["wepi"].append((x[wi, 3] - x[wi, 2]) * 10e-3)
+        r["wid"].append(int(np.flatnonzero(used)[wi]))
         if prev_end is not None:
             r["gap"].append((first - prev_end) * 10e-3)
         r["skew"].append((last_in - first) * 10e-3)
@@ -74,13 +79,16 @@ def main():
         prev_end = end
     print(f"scan phase breakdown: {config} B{B} T{T} row_tile {R.SCAN_ROW_TILE or 16} (us, median over steps)")
     print(f"{'phase':4s} {'kernel':16s} {'WGs':>5s} {'gap':>6s} {'skew':>6s} {'stage':>6s} {'mma':>6s} {'epi':>6s} "
-          f"{'span':>6s}")
+          f"{'span':>6s} | last-exiting WG: {'stage':>6s} {'mma':>6s} {'epi':>6s} {'id (mode)':>9s}")
     tot = {"fwd": 0.0, "bwd": 0.0}
     for (ph, name), r in rows.items():
-        med = {k: (float(np.median(v)) if v else float("nan")) for k, v in r.items() if k != "wgs"}
+        med = {k: (float(np.median(v)) if v else float("nan")) for k, v in r.items() if k not in ("wgs", "wid")}
+        ids, cnt = np.unique(np.array(r["wid"]), return_counts=True)
+        wid_mode = int(ids[np.argmax(cnt)])
         tot[ph] += med["span"] + (med["gap"] if med["gap"] == med["gap"] else 0.0)
         print(f"{ph:4s} {name:16s} {r['wgs']:5d} {med['gap']:6.2f} {med['skew']:6.2f} {med['stage']:6.2f} "
-              f"{med['mma']:6.2f} {med['epi']:6.2f} {med['span']:6.2f}")
+              f"{med['mma']:6.2f} {med['epi']:6.2f} {med['span']:6.2f} |                  {med['wstage']:6.2f} "
+              f"{med['wmma']:6.2f} {med['wepi']:6.2f} {wid_mode:9d}")
     print(f"per step: forward {tot['fwd']:.2f} us, backward {tot['bwd']:.2f} us (span + gap medians)")
 
 
