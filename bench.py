@@ -31,9 +31,11 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "imagined latent steps/sec at B16\u00b7L64\u00b7H15, 1/2/4/8 MI355X; WM-loss \u0394 vs ref"  # BASELINE.json
 PEAK_FP32_MFMA = 157.3  # TFLOP/s, MI355X_MICROARCH.md (dense f32 matrix = f32 vector peak)
 PEAK_HBM = 8000.0  # GB/s spec
+SCAN_SKELETON_US = 15.8  # 4 graph-captured launches per observe step, <= 32 KB weights + 32 KB operands each (r04 prototype)
 # split-bf16 ("bf16x3") kernels: three v_mfma_f32_16x16x32_bf16 per f32-equivalent product, so their f32-equivalent
 # peak is the dense bf16 MFMA peak (2.5 PFLOP/s, MI355X_MICROARCH.md) / 3
 PEAK_BF16X3 = 2500.0 / 3
+PEAK_BF16X6 = 2500.0 / 6  # the imagination's k_hid / k_gate / k_lin6: six bf16 MFMAs per f32-equivalent product
 
 
 class _Sp:
@@ -327,12 +329,12 @@ def probe_specs(agent, cfg, K):
     B, L, H = int(cfg.batch_size), int(cfg.batch_length), int(cfg.model.imag_horizon)
     N, D, U, SK, G, A = B * L, r._deter, r._hidden, r.flat_stoch, r._blocks, agent.act_dim
     Dg, Ig, F = D // G, D // G + 3 * U, SK + D
-    ksd, kss = 4, 8  # split-K slabs of x0p (k_slab) and x1p (k_logit_rows' categorical groups, SD_LR_NG) k_hid sums
+    ksd, kss = 8, 8  # split-K slabs of x0p (k_slab, rssm.SCAN_KSD) and x1p (k_logit_rows' categorical groups, SD_LR_NG)
     out = []
 
-    def add(key, name, grid, bound, work, algo, label, how, launches, peak=None):
+    def add(key, name, grid, bound, work, algo, label, how, launches, peak=None, alt_peak=None):
         out.append(dict(key=key, name=name, grid=list(grid), bound=bound, work=work, algo=algo, label=label, how=how,
-                        launches=launches, peak=peak))
+                        launches=launches, peak=peak, alt_peak=alt_peak))
 
     # encoder stage 2 forward (conv + pool + RMSNorm + SiLU, direct conv from an LDS patch)
     cp = dominant_probe(K)
@@ -371,19 +373,20 @@ def probe_specs(agent, cfg, K):
              4.0 * (N * D + 3 * N * U + D * Ig + N * D + N * D // 64), IMAG_LABELS[1], 1),
             ("imag_k_gate", "k_gate", (D // 32, N // 64, 1), 2.0 * N * 3 * D * Dg,
              4.0 * (N * D + 3 * D * Dg + 2 * N * D), IMAG_LABELS[2], 2)]
-    for key, name, grid, work, algo, label, which in imag:
-        add(key, name, grid, "mfma", work, algo, label, ("imag", which), H)
+    for key, name, grid, work, algo, label, which in imag:  # f32 peak, and (alt) the bf16x6 ceiling they run on
+        add(key, name, grid, "mfma", work, algo, label, ("imag", which), H,
+            alt_peak=None if (which == 0 and not lin6) else PEAK_BF16X6)
     # observe-scan forward phases (M = B rows: weight-streaming, bytes-bound)
-    scan = [("scan_k_hid", "k_hid<8, 2, true>", (D // 16, 1, 1), 4.0 * (D * Ig + 2 * B * D + (ksd + kss + 1) * B * U),
+    scan = [("scan_k_hid", "k_hid<8, 2, true, 16>", (D // 16, 1, 1), 4.0 * (D * Ig + 2 * B * D + (2 + kss + 1) * B * U),
              "scan k_hid (RSSM.observe step: _dyn_hid BlockLinear, M = B rows, 16-column tiles; x0 / x1 RMSNorm + SiLU "
              "prologue)", 1),
-            ("scan_k_gate", "k_gate<2, 2>", (D // 16, 1, 1), 4.0 * (3 * D * Dg + 8 * B * D),
-             "scan k_gate (_dyn_gru BlockLinear + GRU epilogue, M = B rows)", 2),
+            ("scan_k_gate", "k_gate<2, 2, 8, 16>", (D // 8, 1, 1), 4.0 * (3 * D * Dg + 8 * B * D),
+             "scan k_gate (_dyn_gru BlockLinear + GRU epilogue, M = B rows, 8 deter columns x 3 gates per workgroup)", 2),
             ("scan_k_logit", "k_logit_rows<%d, %d>" % (r._discrete, SK // (kss * r._discrete)), (kss, B, 1),
              4.0 * (2 * SK * U + (ksd + 1) * B * U + 5 * B * SK + 6 * B * U),
              "scan k_logit_rows (RSSM.observe step: obs_net RMSNorm + logits + unimix one-hot sampler by (categorical "
              "group, row), and the next step's _dyn_in1 as a gather of the sampled W1^T rows, staged in LDS)", 4),
-            ("scan_k_slab_obs", "k_slab<4>", (U // 16, ksd, 2), 4.0 * (2 * U * D + B * D + 2 * ksd * B * U),
+            ("scan_k_slab_obs", "k_slab<2>", (U // 16, ksd, 2), 4.0 * (2 * U * D + B * D + 2 * ksd * B * U),
              "scan k_slab (obs_net_0 deter half + next _dyn_in0, split-K slabs)", 3)]
     for key, name, grid, algo, label, which in scan:
         add(key, name, grid, "hbm", algo, algo, label, ("scan", which), L)
@@ -441,6 +444,8 @@ def roofline_entries(specs, agent, cfg, table):
         e = {"key": sp["key"], "kernel": sp["label"], "symbol": sp["name"], "grid": sp["grid"], "bound": sp["bound"],
              "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak, "avg_us": avg_us,
              "work_per_launch": sp["work"], "algorithmic_bytes": sp["algo"], "traffic": None}
+        if sp.get("alt_peak"):  # the ceiling of the arithmetic the kernel executes (bf16x6: 6 bf16 MFMAs per product)
+            e.update(alt_peak=sp["alt_peak"], frac_alt=achieved / sp["alt_peak"])
         row = next(((i, rw) for i, rw in enumerate(rows)
                     if _kernel_is(rw["kernel"], sp["name"]) and rw["grid"] == sp["grid"]), None)
         if row:
@@ -455,6 +460,8 @@ def roofline_entries(specs, agent, cfg, table):
                                                              "WRITE_SIZE, per dispatch)")
             if e["traffic"]:
                 e["traffic_over_algorithmic"] = e["traffic"] / sp["algo"]
+            if sp.get("alt_peak"):
+                e["frac_alt_trace"] = e["frac_trace"] * peak / sp["alt_peak"]
         else:
             e["launches_per_update"] = sp["launches"]
         e["ms_per_update"] = e["avg_us"] * e["launches_per_update"] / 1e3
@@ -535,21 +542,23 @@ def phase_rooflines(agent, cfg, cfg_name, ms_update, table=None, reps=10):
                         "achieved": f_img / (ms_img * 1e-3) / 1e12, "peak": 157.3, "unit": "TFLOP/s",
                         "frac": f_img / (ms_img * 1e-3) / 1e12 / 157.3, "work": f_img,
                         "what": f"_imagine_tm: N={N} start rows, H={H} img_steps + {H + 1} actor samples, alone"},
-        # the weights stream from L2/MALL, so the HBM fraction is no bound; the real bound is the dependent launch
-        # chain: 4 fused launches per step, each >= one kernel boundary (1.45 us between trivial kernels,
-        # MI355X_MICROARCH.md price list row 'boundary') plus its dependent prologue load (~1 us, an L2 round trip)
-        "observe_scan": {"bound": "launch latency", "ms": ms_obs, "launches": 4 * L,
-                         "latency_floor_ms": 4 * L * (1.45 + 1.0) * 1e-3,
-                         "frac": 4 * L * (1.45 + 1.0) * 1e-3 / ms_obs,
-                         "weight_stream_GBps": b_obs / (ms_obs * 1e-3) / 1e9, "work": b_obs,
-                         "what": f"RSSM.observe forward, B={B} L={L}: 4 dependent launches per step; weight bytes "
-                                 "(Deter + obs_net once per step) over the phase time as weight_stream_GBps"},
+        # the observe scan against the HBM roofline (the north star's 'achieved HBM GB/s on the recurrent scan'):
+        # algorithmic bytes = the Deter + obs_net weights streamed once per step; what actually bounds it is the
+        # dependent launch chain (4 launches per step), so the same time is also given against the measured floor of
+        # 4 graph-captured launches per step that each stage <= 32 KB of weights and <= 32 KB of activations
+        # (15.8 us per step, tools/hip/persist_scan_proto.hip, profiles/r04_persist_proto.txt)
+        "observe_scan": {"bound": "hbm", "ms": ms_obs, "launches": 4 * L, "work": b_obs,
+                         "achieved": b_obs / (ms_obs * 1e-3) / 1e9, "peak": PEAK_HBM, "unit": "GB/s",
+                         "frac": b_obs / (ms_obs * 1e-3) / 1e9 / PEAK_HBM,
+                         "skeleton_floor_ms": L * SCAN_SKELETON_US * 1e-3,
+                         "frac_of_skeleton_floor": L * SCAN_SKELETON_US * 1e-3 / ms_obs,
+                         "what": f"RSSM.observe forward, B={B} L={L}: 4 dependent launches per step; algorithmic bytes "
+                                 "= Deter + obs_net weights once per step"},
     }
     if table:  # counter bytes of the scan forward's kernels (k_slab / k_hid / k_gate / k_logit of the fused scan) from the
         # committed PMC passes, per update, over the live phase time: the 'achieved HBM GB/s on the recurrent scan'
         scan_rows = [rw for rw in table["rows"]
-                     if rw["kernel"].split("<")[0] in ("k_slab", "k_logit", "k_logit_rows", "k_init") or
-                     rw["kernel"].startswith("k_hid<8, 2") or rw["kernel"] == "k_gate<2, 2>"]
+                     if rw["kernel"].split("<")[0] in ("k_slab", "k_logit", "k_logit_rows", "k_init", "k_hid", "k_gate")]
         cb = sum(rw.get("hbm_bytes", 0.0) * rw["launches_per_update"] for rw in scan_rows)
         tm = sum(rw["ms_per_update"] for rw in scan_rows)
         hit = [(rw.get("l2_hit"), rw["ms_per_update"]) for rw in scan_rows if rw.get("l2_hit") is not None]
@@ -578,6 +587,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="dmc/cnn", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0,
+                    help="per-GPU batch_size override (e.g. one rank's shard of an 8-GPU global batch, timed on one GPU)")
     ap.add_argument("--global-batch", action="store_true",
                     help="divide the config's batch_size over the ranks (strong scaling of the batch) instead of "
                          "keeping it per GPU (weak scaling, the default)")
@@ -606,6 +617,9 @@ def main():
     A, discrete, workload = WORKLOADS[args.config]
     ovr = [f"device=cuda:{local}", "model.compile=False"]
     B0 = int(load_config(args.config, ovr).batch_size)
+    if args.batch:
+        ovr.append(f"batch_size={args.batch}")
+        B0 = args.batch
     if args.global_batch:
         if B0 % world:
             raise SystemExit(f"--global-batch: batch_size {B0} does not split over {world} ranks")

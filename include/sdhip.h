@@ -393,6 +393,10 @@ int sd_clock_probe(long long* stamps, float* sink, int nwg, int iters, sd_stream
  * (SDREAMER_FILL_CUS, dreamer.py). sd_stream_destroy releases it. */
 int sd_stream_create_cumask(int first_cu, int ncu, sd_stream* out);
 int sd_stream_destroy(sd_stream stream);
+/* Scheduling aid: dynamic LDS (bytes, 0..65536) reserved by every split-bf16 / f32 GEMM launch issued after this
+ * call (the kernels do not use it), so fewer of their workgroups fit on a CU beside the latency-bound chain of the
+ * other stream; graph-captured per phase (SDREAMER_FILL_LDS, dreamer.py). Returns the previous value. */
+int sd_set_lds_pad(int bytes);
 /* Dreamer.preprocess + ConvEncoder's "-0.5": out = in/255 - shift (dreamer.py:710-713, networks.py:224) */
 int sd_u8_to_f32(const uint8_t* in, float* out, long n, float shift, sd_stream stream);
 /* NHWC channel pad + shift: out[p][c] = in[p][c] - shift (c < C), 0 (C <= c < Cp). The ConvEncoder input

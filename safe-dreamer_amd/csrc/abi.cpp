@@ -22,3 +22,27 @@ extern "C" int sd_stream_create_cumask(int first_cu, int ncu, sd_stream* out) {
 }
 
 extern "C" int sd_stream_destroy(sd_stream stream) { return (int)hipStreamDestroy((hipStream_t)stream); }
+
+static int g_lds_pad = 0;
+extern "C" int sd_set_lds_pad(int bytes) {
+  if (bytes < 0 || bytes > 65536) return SD_EARG;
+  const int old = g_lds_pad;
+  g_lds_pad = bytes;
+  return old;
+}
+int sd_lds_pad_bytes() { return g_lds_pad; }
+// the pad for one kernel: raises the kernel's dynamic-LDS limit once per (kernel, size); 0 when unset
+size_t sd_lds_pad_for(const void* kern) {
+  static const void* done_k[256];
+  static int done_b[256], n = 0;
+  const int p = g_lds_pad;
+  if (p <= 0) return 0;
+  for (int i = 0; i < n; ++i)
+    if (done_k[i] == kern && done_b[i] >= p) return (size_t)p;
+  if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, p) != hipSuccess) return 0;
+  if (n < 256) {
+    done_k[n] = kern;
+    done_b[n++] = p;
+  }
+  return (size_t)p;
+}

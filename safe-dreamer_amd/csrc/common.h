@@ -96,6 +96,14 @@ SD_DEV float siluf_(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)
 
 static inline int sd_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// sd_set_lds_pad (abi.cpp): the dynamic LDS a GEMM launch reserves beyond its own (0 = none)
+size_t sd_lds_pad_for(const void* kern);
+#define SD_PAD_LAUNCH(KERN, GRID, BLOCK, ST, ...)                                             \
+  do {                                                                                       \
+    auto* k_ = KERN;                                                                         \
+    hipLaunchKernelGGL(k_, GRID, BLOCK, sd_lds_pad_for(reinterpret_cast<const void*>(k_)), ST, __VA_ARGS__); \
+  } while (0)
+
 // Phase timestamps (measurement build, -DSD_SCAN_TRACE; scan.hip and img.hip kernels): thread 0 of every workgroup keeps entry / operands staged /
 // contraction reduced / exit (s_memrealtime, 100 MHz) and stores them at exit into trace[slot][workgroup][4].
 #ifdef SD_SCAN_TRACE

@@ -25,10 +25,10 @@ using namespace sdg;
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC>
 void launch_tile(const GemmArgs& g, bool va, bool vb, hipStream_t st) {
   dim3 grid(sd_cdiv(g.N, BN), sd_cdiv(g.M, BM), g.batch * g.ksplit);
-  if (va && vb) gemm_kernel<BM, BN, WM, WN, AK, BKC, true, true><<<grid, 256, 0, st>>>(g);
-  else if (va) gemm_kernel<BM, BN, WM, WN, AK, BKC, true, false><<<grid, 256, 0, st>>>(g);
-  else if (vb) gemm_kernel<BM, BN, WM, WN, AK, BKC, false, true><<<grid, 256, 0, st>>>(g);
-  else gemm_kernel<BM, BN, WM, WN, AK, BKC, false, false><<<grid, 256, 0, st>>>(g);
+  if (va && vb) SD_PAD_LAUNCH((gemm_kernel<BM, BN, WM, WN, AK, BKC, true, true>), grid, 256, st, g);
+  else if (va) SD_PAD_LAUNCH((gemm_kernel<BM, BN, WM, WN, AK, BKC, true, false>), grid, 256, st, g);
+  else if (vb) SD_PAD_LAUNCH((gemm_kernel<BM, BN, WM, WN, AK, BKC, false, true>), grid, 256, st, g);
+  else SD_PAD_LAUNCH((gemm_kernel<BM, BN, WM, WN, AK, BKC, false, false>), grid, 256, st, g);
 }
 
 template <bool AK, bool BKC>

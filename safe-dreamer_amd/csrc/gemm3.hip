@@ -110,17 +110,17 @@ void launch3_tile(const GemmArgs& g, bool va, bool vb, hipStream_t st) {
   dim3 grid(sd_cdiv(g.N, BN), sd_cdiv(g.M, BM), g.batch * g.ksplit);
   if constexpr (!AK) {
     if (g.rowsum) {
-      if (va && vb) gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, true, true><<<grid, 256, 0, st>>>(g);
-      else if (va) gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, false, true><<<grid, 256, 0, st>>>(g);
-      else if (vb) gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, true, true><<<grid, 256, 0, st>>>(g);
-      else gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, false, true><<<grid, 256, 0, st>>>(g);
+      if (va && vb) SD_PAD_LAUNCH((gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, true, true>), grid, 256, st, g);
+      else if (va) SD_PAD_LAUNCH((gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, false, true>), grid, 256, st, g);
+      else if (vb) SD_PAD_LAUNCH((gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, true, true>), grid, 256, st, g);
+      else SD_PAD_LAUNCH((gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, false, true>), grid, 256, st, g);
       return;
     }
   }
-  if (va && vb) gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, true><<<grid, 256, 0, st>>>(g);
-  else if (va) gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, false><<<grid, 256, 0, st>>>(g);
-  else if (vb) gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, true><<<grid, 256, 0, st>>>(g);
-  else gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, false><<<grid, 256, 0, st>>>(g);
+  if (va && vb) SD_PAD_LAUNCH((gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, true>), grid, 256, st, g);
+  else if (va) SD_PAD_LAUNCH((gemm3_kernel<BM, BN, WM, WN, AK, BKC, true, false>), grid, 256, st, g);
+  else if (vb) SD_PAD_LAUNCH((gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, true>), grid, 256, st, g);
+  else SD_PAD_LAUNCH((gemm3_kernel<BM, BN, WM, WN, AK, BKC, false, false>), grid, 256, st, g);
 }
 
 template <bool AK, bool BKC>
@@ -341,10 +341,10 @@ extern "C" int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd
 #define SD_MLP_LAUNCH(BN_)                                                                             \
   do {                                                                                                 \
     const dim3 grid(sd_cdiv(g.N, BN_), sd_cdiv(g.M, 128), g.batch);                                    \
-    if (rms && pout) gemm3_mlp_kernel<true, true, BN_><<<grid, 256, 0, st>>>(g, e);                    \
-    else if (rms) gemm3_mlp_kernel<true, false, BN_><<<grid, 256, 0, st>>>(g, e);                      \
-    else if (pout) gemm3_mlp_kernel<false, true, BN_><<<grid, 256, 0, st>>>(g, e);                     \
-    else gemm3_mlp_kernel<false, false, BN_><<<grid, 256, 0, st>>>(g, e);                              \
+    if (rms && pout) SD_PAD_LAUNCH((gemm3_mlp_kernel<true, true, BN_>), grid, 256, st, g, e);                    \
+    else if (rms) SD_PAD_LAUNCH((gemm3_mlp_kernel<true, false, BN_>), grid, 256, st, g, e);                      \
+    else if (pout) SD_PAD_LAUNCH((gemm3_mlp_kernel<false, true, BN_>), grid, 256, st, g, e);                     \
+    else SD_PAD_LAUNCH((gemm3_mlp_kernel<false, false, BN_>), grid, 256, st, g, e);                              \
   } while (0)
   if (wide) SD_MLP_LAUNCH(256);
   else SD_MLP_LAUNCH(128);

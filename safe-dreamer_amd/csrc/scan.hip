@@ -1,5 +1,6 @@
 // Fused RSSM posterior scan: RSSM.observe (rssm.py:140-156) -> obs_step (rssm.py:158-178) -> Deter.forward
-// (rssm.py:36-75), forward and BPTT backward, for B <= 16 rows per step.
+// (rssm.py:36-75), forward and BPTT backward; B <= 4096 rows per step as ceil(B / row_tile) row tiles of <= 16 rows
+// side by side in each launch's grid (grid z).
 //
 // Why launches and not one persistent kernel: on MI355X a dependent kernel boundary costs ~1.5 us, an XCD-
 // hierarchical grid barrier ~4-5 us (MI355X_MICROARCH.md price list), so the win is in FEWER, FATTER launches:
@@ -639,17 +640,20 @@ __global__ __launch_bounds__(NTHR) void k_logit_rows(sd_rssm_scan d, Work w, int
   const float blv = d.bl[n0 + (tid % NC)];
   const unsigned char rflag = reset_byte(d, t + 1, b);
   const int uc = tid % UH;
-  float part[KSM];
+  float part[KSM], ev_ = 0.f, nw_ = 0.f;
+  if (tid < UH) {  // (waves 0-3: a wave-uniform branch; the slab index is clamped, not predicated)
 #pragma unroll
-  for (int s = 0; s < KSM; ++s) part[s] = w.ops[(long)(s < d.ks_d ? s : d.ks_d - 1) * B * UH + (long)b * UH + uc];
-  const float ev_ = d.eproj[in_row(d, t, b) * UH + uc], nw_ = d.no[uc];
+    for (int s = 0; s < KSM; ++s) part[s] = w.ops[(long)(s < d.ks_d ? s : d.ks_d - 1) * B * UH + (long)b * UH + uc];
+    ev_ = d.eproj[in_row(d, t, b) * UH + uc];
+    nw_ = d.no[uc];
+  }
   // one workgroup per row also forms the NEXT step's x0 = silu(rms(x0p)), x0p = sum of the _dyn_in0 slabs k_slab
   // wrote before this launch + b0 (rssm.py:52-56), so k_hid stages the finished row instead of every column tile
   // summing the slabs and normalising again (same slab order and bias add as k_hid's own path). Its loads come last:
   // the branch around them may drain the queue, which by then holds nothing that is not needed anyway.
   const bool x0w = more && g == (gridDim.x > 1 ? 1 : 0);
   float part0[KSM], b0_ = 0.f, n0w = 0.f;
-  if (x0w) {
+  if (x0w && tid < UH) {
 #pragma unroll
     for (int s = 0; s < KSM; ++s) part0[s] = w.x0s[(long)(s < d.ks_d ? s : d.ks_d - 1) * B * UH + (long)b * UH + uc];
     b0_ = d.b0[uc];
@@ -1234,13 +1238,14 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
 // ------------------------------------------------------------------------------------------- host side
 int cpw_for(int k) {  // chunks per wave for a k span (16-deep chunks over 8 waves), rounded to an instantiation
   const int c = (k / 16 + NW - 1) / NW;
-  return c <= 2 ? 2 : c <= 4 ? 4 : c <= 8 ? 8 : c <= 12 ? 12 : c <= 16 ? 16 : -1;
+  return c <= 2 ? 2 : c <= 4 ? 4 : c <= 6 ? 6 : c <= 8 ? 8 : c <= 12 ? 12 : c <= 16 ? 16 : -1;
 }
 
 #define SD_CPW_SWITCH(cpw, ...)                            \
   switch (cpw) {                                           \
     case 2: { constexpr int CP = 2; __VA_ARGS__; } break;  \
     case 4: { constexpr int CP = 4; __VA_ARGS__; } break;  \
+    case 6: { constexpr int CP = 6; __VA_ARGS__; } break;  \
     case 8: { constexpr int CP = 8; __VA_ARGS__; } break;  \
     case 12: { constexpr int CP = 12; __VA_ARGS__; } break; \
     case 16: { constexpr int CP = 16; __VA_ARGS__; } break; \

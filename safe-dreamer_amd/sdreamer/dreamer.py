@@ -69,6 +69,9 @@ FILL_CUS = os.environ.get("SDREAMER_FILL_CUS", "")
 # trajectories' large (H*N)-row GEMMs) are queued and run at the start of S3, beside the encoder backward, instead of
 # beside the scan backward (M2a, the latency-bound chain S2 slows)
 AC_DEFER = os.environ.get("SDREAMER_AC_DEFER", "0") == "1"
+# KB of dynamic LDS every GEMM launch of the filler phases (M1, S2, S3, S4) reserves without using it (sd_set_lds_pad):
+# fewer filler workgroups fit on a CU, leaving LDS for the latency-bound chain's workgroups beside them (0 = off)
+FILL_LDS = int(os.environ.get("SDREAMER_FILL_LDS", "0"))
 
 
 def _symexp_bins(n, device):  # symexp_twohot bins, distributions.py:242-251
@@ -578,31 +581,37 @@ class Dreamer(nn.Module):
             mode = "global" if self.world == 1 else "thread_local"
             torch.cuda.synchronize()
 
-            def cap(fn, stream):
-                return parallel.capture_phase(fn, stream, mode)
+            def cap(fn, stream, fill=False):
+                if not (fill and FILL_LDS):
+                    return parallel.capture_phase(fn, stream, mode)
+                old = nat.fns["sd_set_lds_pad"](FILL_LDS * 1024)  # returns the previous pad
+                try:
+                    return parallel.capture_phase(fn, stream, mode)
+                finally:
+                    nat.fns["sd_set_lds_pad"](max(old, 0))
 
             # zero_grad folded into the optimizer step (M3 zeroes what it reads); the gradients are zeroed eagerly
             # before a replay whenever something else wrote them (_grads_clean)
             self._step_zeroes = True
             gP, st = cap(lambda: self._core_forward(self._g_in, self._g_init, self._seed_dev, ro), main_cap)
             gS1, _ = cap(lambda: self._ph_side_returns(st), side_cap)
-            gM1, _ = cap(lambda: self._ph_wm(st, defer=DEFER_WM), main_cap)
+            gM1, _ = cap(lambda: self._ph_wm(st, defer=DEFER_WM), main_cap, fill=True)
             gR, _ = cap(lambda: self._ph_repval(st), main_cap)
             gM2a, _ = cap(lambda: self._ph_scan_bwd(st, defer=True), main_cap)
             if AC_DEFER:  # S2 captured before S3: its queued weight gradients are flushed at the start of S3
                 st["rr"]["ac_wgrads"] = []
-                gS2, (post, keys, mvec) = cap(lambda: self._side_ac_metrics(st), side_cap)
+                gS2, (post, keys, mvec) = cap(lambda: self._side_ac_metrics(st), side_cap, fill=True)
             gS3, _ = cap(lambda: self._flush(st["rr"].get("ac_wgrads", []) + st["scan_wgrads"], "side:scan_wgrads"),
-                         side_cap)
+                         side_cap, fill=True)
             gM2b, _ = cap(lambda: self._ph_encoder_bwd_hi(st, defer=True), main_cap)
             if S4_MAIN:
                 st["enc_wgrads_main"] = st["enc_wgrads"][:S4_MAIN]
                 del st["enc_wgrads"][:S4_MAIN]
-            gS4, _ = cap(lambda: self._flush(st["enc_wgrads"], "side:enc_wgrads"), side_cap)
+            gS4, _ = cap(lambda: self._flush(st["enc_wgrads"], "side:enc_wgrads"), side_cap, fill=True)
             gM2c, _ = cap(lambda: self._ph_encoder_bwd_lo(st), main_cap)
             gM2d = cap(lambda: self._main_tail(st), main_cap)[0] if (DEFER_WM or S4_MAIN) else None
             if not AC_DEFER:
-                gS2, (post, keys, mvec) = cap(lambda: self._side_ac_metrics(st), side_cap)
+                gS2, (post, keys, mvec) = cap(lambda: self._side_ac_metrics(st), side_cap, fill=True)
             self._optimizer.zero_grads_after = True
             gM3, _ = cap(lambda: self._core_step(st), main_cap)
             self._optimizer.zero_grads_after = False  # eager steps (step()) keep the PyTorch semantics

@@ -1,6 +1,6 @@
 """Two-stream timeline of one graph-replayed update at the bench shape from device timestamps (SDREAMER_MARKS=1,
 kernels.Marks): prints each phase boundary in microseconds since the update's first mark. Usage:
-python tools/timeline.py [updates]"""
+python tools/timeline.py [updates] [config (bench.WORKLOADS)] [per-GPU batch]"""
 import os
 import sys
 
@@ -15,12 +15,18 @@ import bench  # noqa: E402
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+    name = sys.argv[2] if len(sys.argv) > 2 else "dmc/cnn"
     from sdreamer.config import load_config
     from sdreamer.dreamer import Dreamer
-    cfg = load_config("dmc/cnn", ["device=cuda:0", "model.compile=False"])
+    ovr = ["device=cuda:0", "model.compile=False"] + ([f"batch_size={sys.argv[3]}"] if len(sys.argv) > 3 else [])
+    cfg = load_config(name, ovr)
+    A, discrete, _ = bench.WORKLOADS[name]
+    act = bench._Sp((A,))
+    if discrete:
+        act.discrete = True
     torch.manual_seed(0)
-    agent = Dreamer(cfg.model, bench._Spaces({"image": bench._Sp((64, 64, 3))}), bench._Sp((6,)))
-    buf = bench.synth_buffer(cfg, torch.device("cuda", 0), 0)
+    agent = Dreamer(cfg.model, bench._Spaces({"image": bench._Sp((64, 64, 3))}), act)
+    buf = bench.synth_buffer(cfg, torch.device("cuda", 0), 0, A=A, discrete=discrete)
     for _ in range(n):
         agent.update(buf)
     torch.cuda.synchronize()
