@@ -1147,6 +1147,19 @@ struct DirectW3 {
   int J, PW, PH, CP, PS, blocks;
 };
 
+// SD_WD3_PRE (default 1): the input patch is staged PRE-SPLIT, each element as one 32-bit word (bf16 hi in the low
+// half, bf16 lo in the high half: the same split2 values), so the inner loop forms a lane's 8 B-values of each plane
+// with 4 v_perm_b32 instead of re-splitting 8 floats per use (every patch element feeds kh * kw taps x the column
+// blocks): bit-identical products, the split VALU moved from the k loop to the stage.
+#ifndef SD_WD3_PRE
+#define SD_WD3_PRE 1
+#endif
+SD_DEV uint32_t pack_split(float v) {  // (bf16 hi | bf16 lo << 16), hi + lo = v up to 2^-17 |v| (split2's values)
+  const f32x4 x = {v, 0.f, 0.f, 0.f};
+  sdb::bf16x4 hi, lo;
+  sdb::split2(x, hi, lo);
+  return (uint32_t)__builtin_bit_cast(uint16_t, hi[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, lo[0]) << 16);
+}
 template <int TM, int NBW>
 __global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1222,13 +1235,29 @@ __global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
       const int i = tid + 512 * v;
       if (i < nP) {
         const int pix = i / cq, c = 4 * (i - pix * cq);
-        *reinterpret_cast<f32x4*>(xp + pix * d.CP + c) = rp[v];
+        if (SD_WD3_PRE) {
+          sdb::bf16x4 hi, lo;
+          sdb::split2(rp[v], hi, lo);
+          const uint64_t h = __builtin_bit_cast(uint64_t, hi), l = __builtin_bit_cast(uint64_t, lo);
+          typedef uint32_t u32x4_ __attribute__((ext_vector_type(4)));
+          u32x4_ w;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) w[k] = (uint32_t)((h >> (16 * k)) & 0xffffu) | ((uint32_t)((l >> (16 * k)) & 0xffffu) << 16);
+          *reinterpret_cast<u32x4_*>(xp + pix * d.CP + c) = w;
+        } else {
+          *reinterpret_cast<f32x4*>(xp + pix * d.CP + c) = rp[v];
+        }
       }
     }
   };
   for (int pix = tid; pix < d.PH * d.PW; pix += 512) {
-    xp[pix * d.CP + d.Ci] = 1.f;
-    xp[pix * d.CP + d.Ci + 1] = 0.f;
+    if (SD_WD3_PRE) {
+      reinterpret_cast<uint32_t*>(xp)[pix * d.CP + d.Ci] = pack_split(1.f);
+      reinterpret_cast<uint32_t*>(xp)[pix * d.CP + d.Ci + 1] = 0u;
+    } else {
+      xp[pix * d.CP + d.Ci] = 1.f;
+      xp[pix * d.CP + d.Ci + 1] = 0.f;
+    }
   }
   int rb = blockIdx.y;
   if (rb < d.blocks) fetch(rb);
@@ -1253,13 +1282,30 @@ __global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
       }
 #pragma unroll
       for (int b = 0; b < NBW; ++b) {
-        const f32x4 v0 = {xp[pb[0] + off[b]], xp[pb[1] + off[b]], xp[pb[2] + off[b]], xp[pb[3] + off[b]]};
-        const f32x4 v1 = {xp[pb[4] + off[b]], xp[pb[5] + off[b]], xp[pb[6] + off[b]], xp[pb[7] + off[b]]};
-        sdb::bf16x4 h0, h1, e0, e1;
-        sdb::split2(v0, h0, e0);
-        sdb::split2(v1, h1, e1);
-        const sdb::bf16x8 bh = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-        const sdb::bf16x8 bl = __builtin_shufflevector(e0, e1, 0, 1, 2, 3, 4, 5, 6, 7);
+        sdb::bf16x8 bh, bl;
+        if (SD_WD3_PRE) {  // 8 packed words -> the two planes, 2 elements per v_perm_b32
+          const uint32_t* xu = reinterpret_cast<const uint32_t*>(xp);
+          uint32_t wv[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) wv[i] = xu[pb[i] + off[b]];
+          typedef uint32_t u32x4_ __attribute__((ext_vector_type(4)));
+          u32x4_ ph, pl;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            ph[i] = __builtin_amdgcn_perm(wv[2 * i + 1], wv[2 * i], 0x05040100u);  // lo halves: the hi plane
+            pl[i] = __builtin_amdgcn_perm(wv[2 * i + 1], wv[2 * i], 0x07060302u);  // hi halves: the lo plane
+          }
+          bh = __builtin_bit_cast(sdb::bf16x8, ph);
+          bl = __builtin_bit_cast(sdb::bf16x8, pl);
+        } else {
+          const f32x4 v0 = {xp[pb[0] + off[b]], xp[pb[1] + off[b]], xp[pb[2] + off[b]], xp[pb[3] + off[b]]};
+          const f32x4 v1 = {xp[pb[4] + off[b]], xp[pb[5] + off[b]], xp[pb[6] + off[b]], xp[pb[7] + off[b]]};
+          sdb::bf16x4 h0, h1, e0, e1;
+          sdb::split2(v0, h0, e0);
+          sdb::split2(v1, h1, e1);
+          bh = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+          bl = __builtin_shufflevector(e0, e1, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           acc[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, acc[i][b], 0, 0, 0);
