@@ -26,7 +26,8 @@ def main():
         act.discrete = True
     torch.manual_seed(0)
     agent = Dreamer(cfg.model, bench._Spaces({"image": bench._Sp((64, 64, 3))}), act)
-    buf = bench.synth_buffer(cfg, torch.device("cuda", 0), 0, A=A, discrete=discrete)
+    L = int(cfg.batch_length)
+    buf = bench.synth_buffer(cfg, torch.device("cuda", 0), 0, T=max(160, 2 * (L + 1)), A=A, discrete=discrete)
     for _ in range(n):
         agent.update(buf)
     torch.cuda.synchronize()
