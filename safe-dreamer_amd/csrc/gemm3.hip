@@ -296,6 +296,175 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void gemm3_mlp_kernel(GemmA
   }
 }
 
+// ---- The wide form for long layers without an input norm (SD_MLP_W256; the imagined heads' first layers: M = H1 * N
+// = 16,384 rows, K = feat 2,560, four 256-wide heads on one input). One 256 x 256 tile per workgroup = one entry's
+// whole width over 256 rows: 512 threads as 2 (rows) x 4 (columns) waves of 128 x 64, on v_mfma_f32_32x32x16_bf16
+// (twice the FLOP per fragment byte of the 16x16x32 tile, so the LDS reads stay under half the MFMA time). Against
+// gemm3_mlp_kernel's 128 x 128 tiles every A row panel is read by 4 workgroups instead of 8 and every B panel by 64
+// instead of 128; the four entries of a row panel run back to back on one XCD (its L2 serves the panel). One
+// workgroup per CU (147 KB of LDS): the next k tile's global loads are issued before this tile's MFMAs and split into
+// the other LDS stage after them, one barrier per k tile. Same split products as gemm3_core.h (lo*hi, hi*lo, hi*hi per
+// 16-deep step); the 32x32 MFMA sums its 16 k in its own order, so the results differ from the 128 x 128 kernel's at
+// the split's ~1e-5 level, not bit for bit.
+#ifndef SD_MLP_W256
+#define SD_MLP_W256 1
+#endif
+#ifndef SD_W256_PASSES
+#define SD_W256_PASSES 1
+#endif
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+namespace w256 {
+constexpr int BM = 256, BN = 256, NT = 512, WM = 128, WN = 64, TM = WM / 32, TN = WN / 32;
+constexpr int NV = BM * BK / 4 / NT;  // float4 per thread per operand per k tile (= TM: one per MFMA group)
+constexpr int SA = BM * LROW, STAGE = (BM + BN) * LROW;
+}  // namespace w256
+
+template <bool POUT>
+__global__ __launch_bounds__(512, 1) void gemm3_w256_kernel(GemmArgs g, MlpExt e) {
+  using namespace w256;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 2, wc = wave & 3;
+  const int l32 = lane & 31, h = lane >> 5;
+  // tile order: the batch entries of one row panel consecutive, runs of T / 8 consecutive tiles per XCD
+  const int T = (int)gridDim.x, per = T / 8, rem = T % 8, xcd = (int)blockIdx.x % 8, slot = (int)blockIdx.x / 8;
+  const int L = xcd * per + (xcd < rem ? xcd : rem) + slot;
+  const int b = L % g.batch, bm0 = (L / g.batch) * BM;
+  const float* A = g.A + (long)b * g.sA;
+  const float* wpb = pick_b(e.wp, b);
+  const float* Bp = wpb ? wpb : g.B + (long)b * g.sB;
+  const int wr_b = pick_b(e.wrows, b), nb = wr_b > 0 ? wr_b : g.N;
+  // loader slots: float4 v of thread tid = row (tid + NT v) / 8, k quad tid % 8 of the 256 x 32 tile, as byte offsets
+  // into range-checked buffer descriptors: rows past M and weight rows past nb get an offset past the range and read
+  // 0 (no branch around any load; past-M rows are never stored)
+  const sd_rsrc rsa = sd_make_rsrc(A, ((long)(g.M - 1) * g.lda + g.K) * 4);
+  const sd_rsrc rsb = sd_make_rsrc(Bp, ((long)(nb - 1) * g.ldb + g.K) * 4);
+  uint32_t oa[NV], ob[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int r = (tid + NT * v) >> 3, kq = tid & 7;
+    oa[v] = bm0 + r < g.M ? (uint32_t)(((long)(bm0 + r) * g.lda + 4 * kq) * 4) : SD_OOB;
+    ob[v] = r < nb ? (uint32_t)(((long)r * g.ldb + 4 * kq) * 4) : SD_OOB;
+  }
+  const int nk = g.K / BK;
+  struct Set {
+    f32x4 a[NV], b[NV];
+  };
+  auto load = [&](Set& x, int kt) {  // tile kt (clamped to the last: the loop's loads are unconditional)
+    const uint32_t kb = (uint32_t)((kt < nk ? kt : nk - 1) * BK * 4);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      x.a[v] = sd_bload4(rsa, oa[v] == SD_OOB ? SD_OOB : oa[v] + kb);
+      x.b[v] = sd_bload4(rsb, ob[v] == SD_OOB ? SD_OOB : ob[v] + kb);
+    }
+  };
+  const int sr = (tid >> 3) * LROW + 4 * (tid & 7);  // this thread's LDS element in row-slot v = 0
+  auto store1 = [&](const Set& x, __bf16* st, int v, int opb) {  // float4 v of operand A (opb 0) / B, split
+    split_store(st + (opb ? SA : 0) + sr + v * (NT / 8) * LROW, opb ? x.b[v] : x.a[v]);
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // tile kt's MFMAs in 8 groups of 6 (one row tile i of one 16-deep step s each), each followed by the split + store
+  // of one float4 slot of tile kt + 1 (A's slots in step 0, B's in step 1; held in register set y since the previous
+  // iteration) into the other stage, so
+  // the split's VALU work and LDS writes run between this tile's MFMAs instead of after them
+  auto step = [&](int kt, Set& x, Set& y) {  // x: free now (tile kt is staged) -> tile kt + 2; y: tile kt + 1
+    load(x, kt + 2);
+    __builtin_amdgcn_sched_barrier(0);  // issued first: hipcc otherwise sinks them behind the MFMAs
+    const __bf16* cur = smem + (kt & 1) * STAGE;
+    __bf16* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const __bf16* p = cur + SA + (wc * WN + 32 * j + l32) * LROW + 16 * s + 8 * h;
+        bh[j] = *reinterpret_cast<const bf16x8*>(p);
+        bl[j] = *reinterpret_cast<const bf16x8*>(p + BK);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const __bf16* p = cur + (wr * WM + 32 * i + l32) * LROW + 16 * s + 8 * h;
+        ah[i] = *reinterpret_cast<const bf16x8*>(p);
+        al[i] = *reinterpret_cast<const bf16x8*>(p + BK);
+      }
+#if SD_W256_PASSES  // the three products as three passes over the 8 accumulators (no dependent MFMA back to back)
+#pragma unroll
+      for (int u = 0; u < 3 * TM * TN; ++u) {
+        const int pass = u / (TM * TN), i = (u / TN) % TM, j = u % TN;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pass == 1 ? ah[i] : pass ? ah[i] : al[i],
+                                                           pass == 0 ? bh[j] : pass == 1 ? bl[j] : bh[j],
+                                                           acc[i][j], 0, 0, 0);
+        if (u % 6 == 5) store1(y, nxt, u / 6, s);
+      }
+#else
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+        store1(y, nxt, i, s);
+      }
+#endif
+    }
+    __syncthreads();
+  };
+  Set x0, x1;
+  load(x0, 0);
+  load(x1, 1);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    store1(x0, smem, v, 0);
+    store1(x0, smem, v, 1);
+  }
+  __syncthreads();
+  int kt = 0;
+  for (; kt + 2 <= nk; kt += 2) {
+    step(kt, x0, x1);
+    step(kt + 1, x1, x0);
+  }
+  if (kt < nk) step(kt, x0, x1);
+  // epilogue: register r of tile (i, j) = row 32 i + (r & 3) + 8 (r >> 2) + 4 h, column 32 j + l32 of the wave tile
+  float* C = g.C + (long)b * g.sC;
+  const float* bpb = pick_b(e.bp, b);
+  const float* bias = bpb ? bpb : g.bias ? g.bias + (long)b * g.sBias : nullptr;
+  float bv[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = wc * WN + 32 * j + l32;
+    bv[j] = (bias && n < nb) ? bias[n] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = bm0 + wr * WM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = wc * WN + 32 * j + l32;
+        const float v = g.alpha * acc[i][j][r] + bv[j];
+        if (m < g.M && n < g.N) C[(long)m * g.ldc + n] = v;
+        ss += n < g.N ? v * v : 0.f;
+      }
+      if (POUT) {  // the wave's 64 columns = one partial of the row's sum of squares
+        ss += __shfl_xor(ss, 1, 64);
+        ss += __shfl_xor(ss, 2, 64);
+        ss += __shfl_xor(ss, 4, 64);
+        ss += __shfl_xor(ss, 8, 64);
+        ss += __shfl_xor(ss, 16, 64);
+        if (l32 == 0 && m < g.M) e.pout[(long)b * e.sPout + (long)wc * g.M + m] = ss;
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd_stream stream_) {
@@ -336,6 +505,15 @@ extern "C" int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd
     e.wrows[b] = x->w_rows[b];
   }
   hipStream_t st = (hipStream_t)stream_;
+  // long layers without an input norm, one 256-wide entry per tile: the 256 x 256 kernel once it fills the chip
+  if (SD_MLP_W256 && !rms && g.N == 256 && (long)sd_cdiv(g.M, 256) * g.batch >= 192) {
+    const dim3 grid(sd_cdiv(g.M, 256) * g.batch);
+    // (no LDS pad: its 147 KB already hold the CU)
+    if (pout) hipLaunchKernelGGL((gemm3_w256_kernel<true>), grid, dim3(512), 0, st, g, e);
+    else hipLaunchKernelGGL((gemm3_w256_kernel<false>), grid, dim3(512), 0, st, g, e);
+    SD_LAUNCH_CHECK();
+    return SD_OK;
+  }
   // 256-column tiles where the layer is exactly that wide (every imagined head's hidden layers), else 128
   const bool wide = SD_MLP_WIDE && g.N % 256 == 0;
 #define SD_MLP_LAUNCH(BN_)                                                                             \

@@ -118,12 +118,13 @@ def test_gemm_bf16x3_batched_split():
 
 
 @pytest.mark.parametrize("M,N,K,n,rms", [(1000, 256, 2560, 4, False), (4096, 256, 256, 2, True),
-                                          (2048, 255, 256, 2, True), (300, 128, 96, 1, True)])
+                                          (2048, 255, 256, 2, True), (300, 128, 96, 1, True),
+                                          (12345, 256, 512, 4, False)])
 def test_gemm_bf16x3_mlp(M, N, K, n, rms):
     """sd_gemm_bf16x3_mlp: out[b] = silu(rms(x[b]) * nw[b]) @ w[b]^T + bias[b] (RMSNorm from the producer's row
     partials, nn.RMSNorm eps 1e-4) and this layer's row partial sums of squares per 64 columns, against torch fp32
     (split-bf16 tolerance 4e-5 * sum |a||b| per output, as test_gemm_bf16x3_*); x broadcast over the batch when not
-    normalised (the imagined heads' first layers)."""
+    normalised (the imagined heads' first layers; M = 12345 takes the 256 x 256 wide kernel, ragged last row tile)."""
     from sdreamer import kernels as kern
     g = torch.Generator().manual_seed(M + N + K)
     x = torch.randn(n if rms else 1, M, K, generator=g) * 2
@@ -189,15 +190,16 @@ def test_wgrad_fused_bias(R, O, I):
     assert torch.allclose(db.double().cpu(), dref, rtol=1e-5, atol=1e-4 * float(dy.abs().sum(0).max()) * 1e-2)
 
 
-@pytest.mark.parametrize("rms", [False, True])
-def test_gemm_bf16x3_mlp_entries(rms):
+@pytest.mark.parametrize("rms,wide", [(False, False), (True, False), (False, True)])
+def test_gemm_bf16x3_mlp_entries(rms, wide):
     """sd_gemm_bf16x3_mlp's per-entry operands (sd_mlp_ext.w_ptr / bias_ptr / norm_w_ptr / w_rows): separate weight
     tensors of different row counts in one launch, bit-identical to the stacked, zero-padded batch (what
-    networks._heads_rest_fused did before), columns past an entry's rows exactly 0."""
+    networks._heads_rest_fused did before), columns past an entry's rows exactly 0 (wide: N = 256 over 12,800 rows,
+    the 256 x 256 kernel)."""
     from sdreamer import kernels as kern
     g = torch.Generator().manual_seed(7)
-    M, K, N = 1500, 256, 255
-    rows = [255, 1, 255, 64]
+    M, K, N = (12800, 256, 256) if wide else (1500, 256, 255)
+    rows = [256, 1, 256, 64] if wide else [255, 1, 255, 64]
     n = len(rows)
     x = (torch.randn(n if rms else 1, M, K, generator=g) * 2).cuda()
     ws = [(torch.randn(r, K, generator=g) / 16).cuda() for r in rows]

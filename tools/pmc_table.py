@@ -98,6 +98,11 @@ def main(tdir, *pdirs):
         print(f"| {100 * sum(ts) / tot:.1f}% | `{k[0]}` | {k[1]}x{k[2]}x{k[3]} | {len(ts)} | {avg / 1e3:.1f} | "
               f"{fmt(clk)} | {fmt(util)} | {fmt(wpc, '{:.1f}')} | {pct('SQ_WAIT_ANY')} | {pct('SQ_WAIT_INST_ANY')} | "
               f"{pct('SQ_ACTIVE_INST_ANY')} | {fmt(hbm, '{:.1f}')} | {fmt(hit, '{:.0f}')} |")
+    import os
+    for k, ts in rows[:int(os.environ.get("PMC_RAW", "0"))]:  # every counter of the top kernels, per dispatch
+        print(f"\n### `{k[0]}` {k[1]}x{k[2]}x{k[3]} ({sum(ts) / len(ts) / 1e3:.1f} us)")
+        for cn, v in sorted(cs.get(k, {}).items()):
+            print(f"- {cn}: {v:.4g}")
 
 
 if __name__ == "__main__":
