@@ -887,7 +887,11 @@ __global__ __launch_bounds__(256, KH_WAVES) void k_hid(sd_imagine d, const float
   if (!APRE) wg_rstd<BM, 8>(px1, npx1, M, m0, U, d.eps, rs1, red);
   SD_TR(1)
   const float* Wseg = d.Wh + (long)n0 * Ig;  // rows n0.. of Wh viewed as (D, Ig)
-  const int ct = n0 / BN, nkt = Ig / BK6;
+#ifndef KH_BWTEST  // timing probe only (wrong results): 1 = every workgroup reads column tile 0's weights, 2 = row tile
+#define KH_BWTEST 0  // 0's activations, 3 = both — what k_hid costs without its L2 -> CU operand traffic
+#endif
+  const int ct = (KH_BWTEST & 1) ? 0 : n0 / BN, nkt = Ig / BK6;
+  const int mt = (KH_BWTEST & 2) ? 0 : m0;
   // the four K segments of [h_g | x0 | x1 | x2]: B from the pre-split image (KH_PRE) or split while staged
   auto bseg = [&](int k0) {
     if constexpr (KH_PRE && F6_HID)
@@ -897,18 +901,18 @@ __global__ __launch_bounds__(256, KH_WAVES) void k_hid(sd_imagine d, const float
   };
   f32x4 acc[1][WN / 16];
   if constexpr (APRE) {  // h, x1 and x2 from their producers' pre-split images (64-row tiles of m0 / 64)
-    hid_seg<BM, BN, WN>(BPre6<BM>(himg, m0 / BM, d.D / BK6, g * Dg / BK6), bseg(0), Dg, acc, false);
+    hid_seg<BM, BN, WN>(BPre6<BM>(himg, mt / BM, d.D / BK6, g * Dg / BK6), bseg(0), Dg, acc, false);
   } else {
     const APlain<BM> a0(h + (long)g * Dg, ldh, m0, M, Dg);
     hid_seg<BM, BN, WN>(a0, bseg(0), Dg, acc, false);
   }
   {
-    const ARms<BM> a0(x0p, U, d.n0, rs0, m0, M, U);
+    const ARms<BM> a0(x0p, U, d.n0, rs0, mt, M, U);
     hid_seg<BM, BN, WN>(a0, bseg(Dg), U, acc, true);
   }
   if constexpr (APRE) {
-    hid_seg<BM, BN, WN>(BPre6<BM>(x1img, m0 / BM, U / BK6, 0), bseg(Dg + U), U, acc, true);
-    hid_seg<BM, BN, WN>(BPre6<BM>(x2img, m0 / BM, U / BK6, 0), bseg(Dg + 2 * U), U, acc, true);
+    hid_seg<BM, BN, WN>(BPre6<BM>(x1img, mt / BM, U / BK6, 0), bseg(Dg + U), U, acc, true);
+    hid_seg<BM, BN, WN>(BPre6<BM>(x2img, mt / BM, U / BK6, 0), bseg(Dg + 2 * U), U, acc, true);
   } else {
     {
       const ARms<BM> a0(x1p, U, d.n1, rs1, m0, M, U);
@@ -921,6 +925,121 @@ __global__ __launch_bounds__(256, KH_WAVES) void k_hid(sd_imagine d, const float
   }
   SD_TR(2)
   ep_bias_part<BM, BN, WN, KH_PW>(acc, d.bh, hp, d.D, ph, M, m0, n0);
+  SD_TR_END(tr.p, tr.slot)
+}
+
+// k_hid on register A operands (KH_AREG): the same 64 x 64 tile, bf16x6 products and k order as k_hid<true>
+// (bit-identical), restructured around what bounds it. k_hid<true> runs its four K segments as four single-stage loops
+// that stage A and B through LDS (two barriers per k tile, LDS writes and reads serialised with the MFMAs: mma phase
+// ~28 us of a 36 us launch, MFMA busy ~0.3, and unchanged when every workgroup reads one tile's operands —
+// profiles/r05n: not the L2 -> CU traffic). Here wave w's A operand is its own 16 rows, so each lane loads its
+// fragment (row l16, k 8q..8q+7 of each plane) straight from the producers' pre-split images into registers — deter
+// (k_gate), x0 (k_action_rows), x1 (k_onehot_lin), x2 (k_action_rows) — and only B (the weight tile the four waves
+// share) goes through a double-buffered LDS stage; the whole K (NKT = Dg/32 + 24 tiles) is one fully unrolled loop
+// with A two tiles ahead in three register sets, B's next tile stored between this tile's MFMAs, one barrier per tile.
+// Step trace (profiles/r05s): k_hid 35.4 -> 27.0 us per step, the imagination step 149.7 -> 142.8 us; update A/B
+// 11.09 -> 11.01 ms. (Measured against it, r05p / r05r: 32-row waves — 2 x 2 waves on 64 x 64, or 4 x 2 on 128 x 64
+// tiles, B fragments reused by two row tiles — run slower, 36.4 / 33.6 vs 28.8 us: their fragment-shaped A loads
+// double per lane.)
+#ifndef KH_STAGES  // B's LDS stages: 3 = each tile's fragments read a step ahead, between the previous tile's MFMAs
+#define KH_STAGES 2  // (3: 27.2 vs 27.0 us per launch, r05s — the reads were not what the MFMAs waited on)
+#endif
+template <int NKT>
+__global__ __launch_bounds__(256, 2) void k_hid_areg(sd_imagine d, float* hp, float* ph, const __bf16* wh6,
+                                                     const __bf16* himg, const __bf16* x0img, const __bf16* x1img,
+                                                     const __bf16* x2img, Tr tr) {
+  SD_TR_BEGIN
+  constexpr int BM = 64, BN = 64, TN = 4, NH = NKT - 24;  // NH: deter tiles (Dg / 32); 8 tiles each of x0 / x1 / x2
+  constexpr int STG = BN * LROW6, BP = BN * PRE_ROW / 8 / 256;  // LDS stage (bf16); 16-B B pieces per thread
+  static_assert(BN * PRE_ROW / 8 == 256 * BP, "whole B pieces per thread");
+  __bf16* smem = sd_smem6<KH_STAGES * STG>();
+  const int Dg = d.D / d.G, M = d.N;
+  const int n0 = xcd_col(blockIdx.x, gridDim.x, Dg / BN) * BN, m0 = blockIdx.y * BM, g = n0 / Dg;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, q = lane >> 4;
+  SD_TR(1)
+  // this lane's A row in the 64-row image tiles (tile m0 / 64), plane offsets 0 / 32 / 64 at k 8q
+  const long rt = m0 / 64, lrow = (long)(16 * wave + l16) * PRE_ROW + 8 * q;
+  const __bf16* ah = himg + (rt * (d.D / BK6) + (long)g * Dg / BK6) * 64 * PRE_ROW + lrow;
+  const __bf16* a0 = x0img + rt * 8 * 64 * PRE_ROW + lrow;
+  const __bf16* a1 = x1img + rt * 8 * 64 * PRE_ROW + lrow;
+  const __bf16* a2 = x2img + rt * 8 * 64 * PRE_ROW + lrow;
+  const __bf16* bt = wh6 + (long)(n0 / BN) * NKT * BN * PRE_ROW + tid * 8;  // this thread's first B piece of tile 0
+  auto aptr = [&](int kt) {  // (kt is a compile-time constant in the unrolled loop)
+    return kt < NH ? ah + (long)kt * 64 * PRE_ROW
+                   : (kt < NH + 8 ? a0 : kt < NH + 16 ? a1 : a2) + (long)((kt - NH) % 8) * 64 * PRE_ROW;
+  };
+  u32x4 A[3][3], B[2][BP];  // A: tiles kt, kt+1, kt+2 (3 planes each); B: pieces of the tiles two / three ahead
+  auto load_a = [&](u32x4 (&a)[3], int kt) {
+    const __bf16* p = aptr(kt);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) a[s] = *reinterpret_cast<const u32x4*>(p + s * BK6);
+  };
+  auto load_b = [&](u32x4 (&b)[BP], int kt) {
+#pragma unroll
+    for (int u = 0; u < BP; ++u) b[u] = *reinterpret_cast<const u32x4*>(bt + ((long)kt * BN * PRE_ROW + u * 256 * 8));
+  };
+  auto store_b = [&](const u32x4 (&b)[BP], __bf16* st, int u) {
+    const int i = tid + 256 * u;
+    *reinterpret_cast<u32x4*>(st + (i / (PRE_ROW / 8)) * LROW6 + (i % (PRE_ROW / 8)) * 8) = b[u];
+  };
+  // B fragments of a stage: tile j's are read during step j - 1 (KH_STAGES 3: the stage was written a step earlier)
+  // or at the start of step j (2 stages)
+  bf16x8 fb[2][TN][3];
+  auto read_b = [&](bf16x8 (&f)[TN][3], const __bf16* st, int j) {
+    const __bf16* pb = st + (16 * j + l16) * LROW6 + 8 * q;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) f[j][s] = *reinterpret_cast<const bf16x8*>(pb + s * BK6);
+  };
+  f32x4 acc[1][TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int NS = KH_STAGES;
+  load_a(A[0], 0);
+  load_b(B[0], 0);
+  load_a(A[1], 1);
+  load_b(B[1], 1);
+#pragma unroll
+  for (int u = 0; u < BP; ++u) store_b(B[0], smem, u);
+  if constexpr (NS == 3) {
+#pragma unroll
+    for (int u = 0; u < BP; ++u) store_b(B[1], smem + STG, u);
+    load_b(B[0], 2);
+  }
+  __syncthreads();
+  if constexpr (NS == 3) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) read_b(fb[0], smem, j);
+  }
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    // B pieces in flight: 2 stages: tile kt+2 into set kt % 2 (tile kt+1, set (kt+1) % 2, is stored this step);
+    // 3 stages: tile kt+3 into set (kt+1) % 2 (tile kt+2, set kt % 2, is stored this step)
+    if (kt + NS < NKT) load_b(B[(kt + NS) % 2], kt + NS);
+    if (kt + 2 < NKT) load_a(A[(kt + 2) % 3], kt + 2);
+    __builtin_amdgcn_sched_barrier(0);  // the loads first
+    const int ts = kt + NS - 1;  // the tile this step stages
+    __bf16* stg = smem + (ts % NS) * STG;
+    bf16x8(&f)[TN][3] = fb[kt % 2];
+    if constexpr (NS == 2) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) read_b(f, smem + (kt % 2) * STG, j);
+    }
+    // gemm6_core.h's six products per accumulator in its order (a2b0, a1b1, a0b2, a1b0, a0b1, a0b0), as six passes over
+    // the four accumulators; between the passes the staged tile's pieces and (3 stages) tile kt+1's fragments
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int as = u == 0 ? 2 : (u == 1 || u == 3) ? 1 : 0, bs = u == 0 || u == 3 || u == 5 ? 0 : u == 2 ? 2 : 1;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, A[kt % 3][as]), f[j][bs],
+                                                            acc[0][j], 0, 0, 0);
+      if (ts < NKT && u < BP) store_b(B[ts % 2], stg, u);
+      if (NS == 3 && kt + 1 < NKT && u >= 1 && u <= TN) read_b(fb[(kt + 1) % 2], smem + ((kt + 1) % NS) * STG, u - 1);
+    }
+    __syncthreads();
+  }
+  SD_TR(2)
+  ep_bias_part<BM, BN, 64, KH_PW>(acc, d.bh, hp, d.D, ph, M, m0, n0);
   SD_TR_END(tr.p, tr.slot)
 }
 
@@ -1238,10 +1357,19 @@ __global__ __launch_bounds__(256) void k_action(sd_imagine d, const float* X, co
 #ifndef KA_ROWS
 #define KA_ROWS 1
 #endif
+// X0: also the next k_hid's x0 operand as a pre-split image, x0img = split(silu(rms(x0p) * n0)) (k_hid_areg; the
+// row's rstd summed from k_lin6's partials in wg_rstd<64, 8>'s association, so the planes are those k_hid's own ARms
+// loader would stage)
+struct X0Img {
+  const float* x0p;
+  const float* px0;
+  int npx0;
+  __bf16* img;
+};
 template <int MO>  // >= the output logits (2A or A): 16 or 32
 __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* X, const float* nw,
                                                      const float* part_in, int np, float* act, float* x2, int t,
-                                                     int want_x2, __bf16* x2img, Tr tr) {
+                                                     int want_x2, __bf16* x2img, X0Img x0i, Tr tr) {
   SD_TR_BEGIN
   constexpr int U = 256, MA = 16;  // <= 16 actions
   __shared__ float w2s[U * MA];    // _dyn_in2's weight (U, A), staged coalesced while the logits chain runs
@@ -1271,6 +1399,11 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
     w2r[k] = d.W2[i < U * A ? i : U * A - 1];
   }
   const f32x4 b2 = ld4(d.b2 + 4 * lane), n2 = ld4(d.n2 + 4 * lane);
+  const bool x0w = x0i.img != nullptr && want_x2 != 0;  // (uniform over the launch)
+  const float* x0src = x0w ? x0i.x0p : X;  // (a valid row either way: the loads stay unconditional)
+  const f32x4 x0v = ld4(x0src + mc * U + 4 * lane), n0v = ld4((x0w ? d.n0 : nw) + 4 * lane);
+  const int np0 = x0w ? x0i.npx0 : np;
+  const float p0_ = (x0w ? x0i.px0 : part_in)[(long)(lane < np0 ? lane : np0 - 1) * M + mc];
   const int la = lane < A ? lane : A - 1;
   float nz = *(d.noise_act ? d.noise_act + ((long)t * M + mc) * A + la : d.b2);
   if (!d.noise_act) {  // drawn here (the same counter-based values as the drawn-ahead noise)
@@ -1327,6 +1460,22 @@ __global__ __launch_bounds__(256) void k_action_rows(sd_imagine d, const float* 
     }
   }
   if (live && lane < A) act[m * A + lane] = a;
+  if (x0w) {  // wg_rstd<64, 8>: partial group g = p % 4 sums p = g, g + 4, ... in order, then the groups in order
+    const float pp = lane < np0 ? p0_ : 0.f;
+    float tt = 0.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float sg = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sg += __shfl(pp, g + 4 * k, 64);
+      tt += sg;
+    }
+    const float r0 = rsqrtf(tt / (float)U + d.eps);
+    f32x4 y0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y0[j] = siluf_(x0v[j] * r0 * n0v[j]);
+    if (live) pre_store4(x0i.img, m, 4 * lane, U, y0);
+  }
   if (!x2w) {  // (uniform over the launch)
     SD_TR_END(tr.p, tr.slot)
     return;
@@ -1667,6 +1816,7 @@ struct IWork {
   __bf16 *wh6, *wg6;  // pre-split _dyn_hid / _dyn_gru weights (BPre6 images, 3 bf16 per element)
   float *waT, *w1T;   // actor layer 0's stoch columns and _dyn_in1, transposed (SK, U) for k_onehot_lin
   __bf16 *h6, *x16, *x26;  // pre-split activation images (KH_APRE): deter, silu(rms(x1p)), x2; rows padded to 64
+  __bf16* x06;             // and silu(rms(x0p)) for k_hid_areg (KH_AREG)
   __bf16 *wi6, *w06, *wad6;  // pre-split img_net_0 / _dyn_in0 / actor layer 0 (deter columns) weights (KL_PRE)
   long total;
 };
@@ -1693,6 +1843,7 @@ IWork iwork(const sd_imagine& d, float* base) {
   w.h6 = reinterpret_cast<__bf16*>(take(rows * d.D * 3 / 2));
   w.x16 = reinterpret_cast<__bf16*>(take(rows * d.U * 3 / 2));
   w.x26 = reinterpret_cast<__bf16*>(take(rows * d.U * 3 / 2));
+  w.x06 = reinterpret_cast<__bf16*>(take(rows * d.U * 3 / 2));
   w.wi6 = reinterpret_cast<__bf16*>(take((long)d.U * d.D * 3 / 2));
   w.w06 = reinterpret_cast<__bf16*>(take((long)d.U * d.D * 3 / 2));
   w.wad6 = reinterpret_cast<__bf16*>(take((long)d.U * d.D * 3 / 2));
@@ -1737,6 +1888,24 @@ static bool img_apre(const sd_imagine& d) {
   return KH_APRE && KH_1S && F6_HID && KH_PRE && KH_BM == 64 && KL_ONEHOT && d.SK / d.Kd <= 64 && KA_ROWS &&
          !SD_FUSED_ACTOR && d.U / KL2_PW == 16 && !getenv("SDHIP_KH_NOAPRE");
 }
+// k_hid on register A operands (k_hid_areg) at the block widths it is built for (Dg = 256 / 512); SDHIP_KH_NOAREG set:
+// k_hid<true>, for A/B and the bit-identity test
+#ifndef KH_AREG
+#define KH_AREG 1
+#endif
+static int img_areg_nkt(const sd_imagine& d) {
+  const int nkt = (d.D / d.G + 3 * d.U) / BK6;
+  return (KH_AREG && img_apre(d) && (nkt == 32 || nkt == 40) && !getenv("SDHIP_KH_NOAREG")) ? nkt : 0;
+}
+static void launch_hid_areg(const sd_imagine& d, const IWork& w, int nkt, const float* feat_t, int F, Tr tr,
+                            hipStream_t st) {
+  (void)feat_t; (void)F;
+  const dim3 grid(d.D / 64, sd_cdiv(d.N, 64));
+  if (nkt == 32)
+    k_hid_areg<32><<<grid, 256, 0, st>>>(d, w.hp, w.ph, w.wh6, w.h6, w.x06, w.x16, w.x26, tr);
+  else
+    k_hid_areg<40><<<grid, 256, 0, st>>>(d, w.hp, w.ph, w.wh6, w.h6, w.x06, w.x16, w.x26, tr);
+}
 // the deter contractions on pre-split operands (k_lin6): A the deter image (img_apre), B the weights split once per
 // imagination; SDHIP_KL_NOPRE set: the fp32 k_lin, for A/B and tests
 static bool img_lpre(const sd_imagine& d) {
@@ -1766,6 +1935,8 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
                                                                          N, Tr{});
     else
       k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, Tr{});
+  } else if (which == 1 && img_areg_nkt(d)) {  // (the images the run built)
+    launch_hid_areg(d, w, img_areg_nkt(d), feats(t) + SK, F, Tr{}, st);
   } else if (which == 1) {
     k_hid<false><<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1,
                                                                  U / KL3_PW, npU, w.x2, w.hp, w.ph, w.wh6, nullptr,
@@ -1796,6 +1967,8 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   const float* Wa0d = d.Wa[0] + SK;  // (U, F) columns SK.. of the actor's first weight
   const int t_end = d.t_end > 0 ? d.t_end : d.H1;
   const bool apre = img_apre(d);  // pre-split k_hid operands
+  const int areg = img_areg_nkt(d);  // k_hid_areg (and the x0 image k_action_rows writes for it)
+  const X0Img x0i{w.x0p, w.px0, U / KL3_PW, areg ? w.x06 : nullptr};
   if (d.t_begin == 0 && apre) {  // the start state's deter image
     k_presplit_rows<<<(int)sd_cdiv((long)N * D / 4, 256), 256, 0, st>>>(feats(0) + SK, F, N, D, w.h6);
     SD_LAUNCH_CHECK();
@@ -1874,10 +2047,10 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
         float* acts = d.actions + (long)t * N * d.A;
         if ((d.act_discrete ? d.A : 2 * d.A) <= 16)
           k_action_rows<16><<<sd_cdiv(N, 4), 256, 0, st>>>(d, xa, d.na[d.actor_layers - 1], w.pa[cur], npa, acts,
-                                                           w.x2, t, last ? 0 : 1, apre ? w.x26 : nullptr, tr(4));
+                                                           w.x2, t, last ? 0 : 1, apre ? w.x26 : nullptr, x0i, tr(4));
         else
           k_action_rows<32><<<sd_cdiv(N, 4), 256, 0, st>>>(d, xa, d.na[d.actor_layers - 1], w.pa[cur], npa, acts,
-                                                           w.x2, t, last ? 0 : 1, apre ? w.x26 : nullptr, tr(4));
+                                                           w.x2, t, last ? 0 : 1, apre ? w.x26 : nullptr, x0i, tr(4));
       }
       else
         k_action<<<dim3(1, sd_cdiv(N, KA_BM)), 256, 0, st>>>(d, d.actor_layers == 1 ? a0 : w.a[cur],
@@ -1886,7 +2059,9 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     }
     SD_LAUNCH_CHECK();
     if (last) break;
-    if (apre)
+    if (areg)
+      launch_hid_areg(d, w, areg, feats(t) + SK, F, tr(5), st);
+    else if (apre)
       k_hid<true><<<dim3(D / 64, sd_cdiv(N, KH_BM)), 256, 0, st>>>(d, feats(t) + SK, F, w.x0p, w.x1p, w.px0, w.px1,
                                                                   U / KL3_PW, npU, w.x2, w.hp, w.ph, w.wh6, w.h6,
                                                                   w.x16, w.x26, tr(5));

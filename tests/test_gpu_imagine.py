@@ -65,9 +65,9 @@ def test_fused_imagination_deterministic():
 
 @pytest.mark.parametrize("name,N", [("walker_r2", 192), ("atari_r2", 100), ("maze_r2", 128)])
 def test_presplit_images_bit_identical(name, N):
-    """k_hid reading deter / x1 / x2 from their producers' pre-split bf16x3 images (KH_APRE) gives exactly the
-    imagination of the in-loader split (SDHIP_KH_NOAPRE): the same fp32 values are split, x1's rstd is summed in
-    wg_rstd's order."""
+    """k_hid reading deter / x1 / x2 from their producers' pre-split bf16x3 images (KH_APRE; on k_hid_areg also x0,
+    from k_action_rows) gives exactly the imagination of the in-loader split (SDHIP_KH_NOAPRE): the same fp32 values
+    are split, x0's and x1's rstd are summed in wg_rstd's order."""
     import os
     ag, z, spec, obs = build_agent(name)
     start = _start(ag, N, 11)
@@ -102,3 +102,19 @@ def test_lin6_matches_fp32_lin(name, N):
     assert rows_same.float().mean() >= 0.98
     da, db = a[0][:, rows_same, SK:], b[0][:, rows_same, SK:]
     assert (da - db).abs().max() <= 1e-5 * (1 + db.abs().max())
+
+
+@pytest.mark.parametrize("name,N", [("walker_r2", 192), ("atari_r2", 100), ("maze_r2", 128)])
+def test_hid_areg_bit_identical(name, N):
+    """k_hid_areg (register A operands from the pre-split images, one fully unrolled K loop; Dg 256 and 512) gives
+    exactly k_hid<true>'s imagination (SDHIP_KH_NOAREG): same planes, same six products per k tile in the same order."""
+    import os
+    ag, z, spec, obs = build_agent(name)
+    start = _start(ag, N, 17)
+    a = _run(ag, start, 6, True)
+    os.environ["SDHIP_KH_NOAREG"] = "1"
+    try:
+        b = _run(ag, start, 6, True)
+    finally:
+        del os.environ["SDHIP_KH_NOAREG"]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])

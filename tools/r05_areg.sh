@@ -1,0 +1,13 @@
+#!/bin/bash
+# k_hid_areg: imagination tests (bit identity against k_hid<true>), the dreamer golden tests, the step trace with and
+# without it, and a same-box update A/B (SDHIP_KH_NOAREG=1 = k_hid<true>). Usage: bash tools/r05_areg.sh <tag>
+set -o pipefail
+O=gpurun_out/$1; mkdir -p $O
+L=safe-dreamer_amd/sdreamer
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_imagine.py \
+  > $O/tests_imagine.txt 2>&1 || exit 1
+SDHIP_LIB=$L/_lib_trace/libsdhip.so timeout -k 10 200 python -u tools/imag_trace.py > $O/imag_trace.txt 2>&1 || exit 1
+SDHIP_KH_NOAREG=1 SDHIP_LIB=$L/_lib_trace/libsdhip.so timeout -k 10 200 python -u tools/imag_trace.py > $O/imag_trace_noareg.txt 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_dreamer.py \
+  > $O/tests_dreamer.txt 2>&1 || exit 1
+bash tools/ab_env.sh 3 "" "SDHIP_KH_NOAREG=1" > $O/ab.txt 2>&1 || exit 1
