@@ -540,9 +540,15 @@ typedef struct sd_imagine {
                              for one-hot; stream stream_act, step t), drawn ahead by sd_imagine_noise */
   uint64_t* trace;        /* measurement aid, -DSD_SCAN_TRACE builds only (NULL otherwise): per launch slot
                              (t * 16 + launch of the step) and workgroup, entry / staged / contracted / exit timestamps */
+  int prepped;            /* 1: sd_imagine_prep already wrote the weight images into `work` (the t_begin == 0 chunk
+                             skips them) */
 } sd_imagine;
 int sd_imagine_work_floats(const sd_imagine* d);
 int sd_imagine_run(const sd_imagine* d, sd_stream stream);
+/* The weight-only part of the t_begin == 0 chunk — the pre-split bf16 images of _dyn_hid, _dyn_gru, img_net_0,
+ * _dyn_in0 and actor layer 0's deter columns, the transposed one-hot weights — into `work`, ahead of the run (e.g. on
+ * another stream beside the work that produces the start state); the run then sets `prepped`. */
+int sd_imagine_prep(const sd_imagine* d, sd_stream stream);
 /* noise (H1 - 1, N, SK) = the Gumbel noise of every imagined prior sample (Philox stream d->stream_img, step t, element
  * (row + row_offset) * SK + k; the effective seed read on the device as sd_imagine_run reads it), and when noise_act
  * is non-null (H1, N, A) the action samples' noise (stream d->stream_act, element (row + row_offset) * A + j): one

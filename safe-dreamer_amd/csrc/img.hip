@@ -1866,7 +1866,11 @@ int icheck(const sd_imagine* d) {
 }  // namespace
 
 extern "C" int sd_imagine_noise(const sd_imagine* dp, float* noise, float* noise_act, sd_stream stream_) {
-  const int rc = icheck(dp);
+  if (!dp) return SD_EARG;
+  sd_imagine dc = *dp;  // (feats / actions need not exist yet: the noise reads neither)
+  if (!dc.feats) dc.feats = noise;
+  if (!dc.actions) dc.actions = noise;
+  const int rc = icheck(&dc);
   if (rc) return rc;
   if (!noise || ((uintptr_t)noise & 15)) return SD_EARG;
   long n = (long)(dp->H1 - 1) * dp->N * dp->SK / 4;
@@ -1950,6 +1954,45 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
   return SD_OK;
 }
 
+// the weight-only setup of an imagination: pre-split images and transposed one-hot weights (sd_imagine_prep)
+static int imagine_prep(const sd_imagine& d, const IWork& w, hipStream_t st) {
+  const int U = d.U, SK = d.SK, D = d.D, F = SK + D;
+  const float* Wa0d = d.Wa[0] + SK;
+  if (KH_PRE && F6_HID) {  // _dyn_hid's weight split into its bf16 planes once per imagination
+    const long Ig = D / d.G + 3L * U;
+    k_presplit6<64><<<(int)sd_cdiv((long)D * Ig / 4, 256), 256, 0, st>>>(d.Wh, D, (int)Ig, w.wh6);
+    SD_LAUNCH_CHECK();
+  }
+  if (KL_ONEHOT) {  // the one-hot contractions' weights, transposed
+    k_transpose_w<<<sd_cdiv((long)SK * U, 256), 256, 0, st>>>(d.Wa[0], F, U, SK, w.waT);
+    k_transpose_w<<<sd_cdiv((long)SK * U, 256), 256, 0, st>>>(d.W1, SK, U, SK, w.w1T);
+    SD_LAUNCH_CHECK();
+  }
+  if (KG_PRE && KG_1S && F6_GATE) {  // and _dyn_gru's
+    k_presplit6_gate<<<(int)sd_cdiv((long)3 * D * (D / d.G) / 4, 256), 256, 0, st>>>(d.Wg, D, D / d.G, w.wg6);
+    SD_LAUNCH_CHECK();
+  }
+  const bool lpre = img_lpre(d);  // the deter contractions' weights (img_net_0, _dyn_in0, actor layer 0's deter part)
+  if (lpre) {
+    const int gsz = (int)sd_cdiv((long)U * D / 4, 256);
+    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.Wi[0], U, D, w.wi6, D);
+    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.W0, U, D, w.w06, D);
+    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(Wa0d, U, D, w.wad6, F);
+    SD_LAUNCH_CHECK();
+  }
+  return SD_OK;
+}
+
+extern "C" int sd_imagine_prep(const sd_imagine* dp, sd_stream stream_) {
+  if (!dp) return SD_EARG;
+  sd_imagine d = *dp;  // (feats / actions need not exist yet: the weight images read neither)
+  if (!d.feats) d.feats = d.work;
+  if (!d.actions) d.actions = d.work;
+  const int rc = icheck(&d);
+  if (rc) return rc;
+  return imagine_prep(d, iwork(d, d.work), (hipStream_t)stream_);
+}
+
 extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
   int rc = icheck(dp);
   if (rc) return rc;
@@ -1973,29 +2016,11 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     k_presplit_rows<<<(int)sd_cdiv((long)N * D / 4, 256), 256, 0, st>>>(feats(0) + SK, F, N, D, w.h6);
     SD_LAUNCH_CHECK();
   }
-  if (d.t_begin == 0 && KH_PRE && F6_HID) {  // _dyn_hid's weight split into its bf16 planes once per imagination
-    const long Ig = D / d.G + 3L * U;
-    k_presplit6<64><<<(int)sd_cdiv((long)D * Ig / 4, 256), 256, 0, st>>>(d.Wh, D, (int)Ig, w.wh6);
-    SD_LAUNCH_CHECK();
+  if (d.t_begin == 0 && !d.prepped) {
+    const int e = imagine_prep(d, w, st);
+    if (e) return e;
   }
-  if (d.t_begin == 0 && KL_ONEHOT) {  // the one-hot contractions' weights, transposed
-    k_transpose_w<<<sd_cdiv((long)SK * U, 256), 256, 0, st>>>(d.Wa[0], F, U, SK, w.waT);
-    k_transpose_w<<<sd_cdiv((long)SK * U, 256), 256, 0, st>>>(d.W1, SK, U, SK, w.w1T);
-    SD_LAUNCH_CHECK();
-  }
-  if (d.t_begin == 0 && KG_PRE && KG_1S && F6_GATE) {  // and _dyn_gru's
-    k_presplit6_gate<<<(int)sd_cdiv((long)3 * D * (D / d.G) / 4, 256), 256, 0, st>>>(d.Wg, D, D / d.G, w.wg6);
-    SD_LAUNCH_CHECK();
-  }
-  // the deter contractions (img_net_0, _dyn_in0, actor layer 0's deter part) on pre-split operands (k_lin6)
   const bool lpre = img_lpre(d);
-  if (d.t_begin == 0 && lpre) {
-    const int gsz = (int)sd_cdiv((long)U * D / 4, 256);
-    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.Wi[0], U, D, w.wi6, D);
-    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.W0, U, D, w.w06, D);
-    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(Wa0d, U, D, w.wad6, F);
-    SD_LAUNCH_CHECK();
-  }
   if (d.t_begin == 0) {  // x0p(0) = h0 . W0^T + b0 and the deter part of actor layer 0 at t = 0
     LinProb p{feats(0) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
     LinProb pd{feats(0) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};

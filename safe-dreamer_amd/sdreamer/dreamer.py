@@ -72,6 +72,11 @@ AC_DEFER = os.environ.get("SDREAMER_AC_DEFER", "0") == "1"
 # KB of dynamic LDS every GEMM launch of the filler phases (M1, S2, S3, S4) reserves without using it (sd_set_lds_pad):
 # fewer filler workgroups fit on a CU, leaving LDS for the latency-bound chain's workgroups beside them (0 = off)
 FILL_LDS = int(os.environ.get("SDREAMER_FILL_LDS", "0"))
+# S0: the imagination's noise and weight images (1), and also the scan backward's transposed and the encoder's flipped
+# weights (2), as a side-stream phase beside the encoder forward instead of at the head of S1 (imagination) and inside
+# M1. Measured neutral (profiles/r05v, r05w: the encoder forward slows by what S1 / M1 save; 3-round A/B 10.90 / 10.91 /
+# 10.96 ms for 0 / 1 / 2): off by default
+SIDE_PREP = int(os.environ.get("SDREAMER_SIDE_PREP", "0"))
 
 
 def _symexp_bins(n, device):  # symexp_twohot bins, distributions.py:242-251
@@ -594,6 +599,7 @@ class Dreamer(nn.Module):
             # before a replay whenever something else wrote them (_grads_clean)
             self._step_zeroes = True
             gP, st = cap(lambda: self._core_forward(self._g_in, self._g_init, self._seed_dev, ro), main_cap)
+            gS0, _ = cap(lambda: self._ph_side_prep(st), side_cap) if SIDE_PREP else (None, None)
             gS1, _ = cap(lambda: self._ph_side_returns(st), side_cap)
             gM1, _ = cap(lambda: self._ph_wm(st, defer=DEFER_WM), main_cap, fill=True)
             gR, _ = cap(lambda: self._ph_repval(st), main_cap)
@@ -617,10 +623,10 @@ class Dreamer(nn.Module):
             self._optimizer.zero_grads_after = False  # eager steps (step()) keep the PyTorch semantics
             self._grads_clean = False
             torch.cuda.synchronize()
-            for g in (gP, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gM3):
+            for g in (gS0, gP, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gM3):
                 if g is not None and g.n_collectives:
                     raise RuntimeError("unexpected exchange step in a single-graph phase")
-            self._graph = (gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gS2, gM3)
+            self._graph = (gS0, gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gS2, gM3)
             self._gst, self._g_post, self._g_keys, self._g_mvec = st, post, keys, mvec
         if data is not None:
             for k, v in data.items():
@@ -635,7 +641,7 @@ class Dreamer(nn.Module):
             self._ema_updates += 1
             self._proto_gate.copy_(torch.tensor([0.0 if self._protos_frozen() else 1.0]).pin_memory()
                                    .reshape(self._proto_gate.shape), non_blocking=True)
-        gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gS2, gM3 = self._graph
+        gS0, gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gS2, gM3 = self._graph
         caller = torch.cuda.current_stream()
         if STREAM_PRIO and self.use_side_stream:
             # the critical chain (P, S1, R, M2a..M2d, M3) on high-priority streams, the phases that fill its idle CUs
@@ -655,6 +661,11 @@ class Dreamer(nn.Module):
             main = caller
             side = self._side if self.use_side_stream else main
             fill, side_fill = main, side
+        if gS0 is not None:  # S0 (weights and seed only) beside P: after the seed copy and the last optimizer step
+            if side is not main:
+                side.wait_stream(main)
+            with torch.cuda.stream(side):
+                gS0.replay()
         with torch.cuda.stream(main):
             if not self._grads_clean:
                 self._optimizer.zero_grad()
@@ -829,6 +840,19 @@ class Dreamer(nn.Module):
                     post_deter=post_deter, post_logit=post_logit, leaves=leaves, feat_l=feat_l, feat_r=feat_r,
                     ifeats=ifeats, fsink=fsink)
 
+    def _ph_side_prep(self, st):
+        """side, beside the encoder forward (S0): what depends on the weights and the seed only — the imagination's
+        noise and weight images (_imagine_prepare), the scan backward's transposed weights and the encoder's flipped
+        conv weights (read by the backward phases)."""
+        data = st["data"]
+        B, T = data["action"].shape[:2]
+        if self._fused_imag_ok():
+            st["imag_prep"] = self._imagine_prepare(B * T, self.imag_horizon + 1, st["seed"], st["ro"] * T,
+                                                    data["action"].device)
+        if SIDE_PREP >= 2:
+            st["scan_tr"] = self.rssm._bwd_tr = self.rssm.scan_bwd_weights()
+            st["enc_flip"] = K.set_flip_cache(self.encoder.dgrad_weights())
+
     def _ph_side_returns(self, st):
         """side: imagination (dreamer.py:578-597), imagined heads, lambda-returns + ReturnEMA (598-636)."""
         data = st["data"]
@@ -840,7 +864,8 @@ class Dreamer(nn.Module):
         # actor layer 0's fp32 output of every imagined step, kept for the policy loss's actor forward (REUSE_H0)
         ah0 = torch.empty(H1, N, self.actor.mlp.out_dim, device=start[1].device) \
             if REUSE_H0 and self._fused_imag_ok() and not self.actor.mlp._symlog_inputs else None
-        ifeat, iact = self._imagine_tm(start, H1, st["seed"], st["ro"] * T, actor_h0=ah0, feats=st.get("ifeats"))
+        ifeat, iact = self._imagine_tm(start, H1, st["seed"], st["ro"] * T, actor_h0=ah0, feats=st.get("ifeats"),
+                                       prep=st.get("imag_prep"))
         self._mark("side:imagine")
         rr = self._heads_returns(ifeat)
         rr["act_h0"] = ah0
@@ -854,8 +879,9 @@ class Dreamer(nn.Module):
         st["wm_wgrads"] = []
         # the scan backward's transposed weights and the encoder's flipped conv weights, while main has slack (it
         # waits for the imagined returns next): off the chain from the head losses to the encoder gradient
-        st["scan_tr"] = self.rssm._bwd_tr = self.rssm.scan_bwd_weights()
-        st["enc_flip"] = K.set_flip_cache(self.encoder.dgrad_weights())
+        if "scan_tr" not in st:  # (made by _ph_side_prep when that phase ran)
+            st["scan_tr"] = self.rssm._bwd_tr = self.rssm.scan_bwd_weights()
+            st["enc_flip"] = K.set_flip_cache(self.encoder.dgrad_weights())
         st["flags"] = self._episode_flags(st["data"])
         with ops.defer_wgrads(st["wm_wgrads"] if defer else None):
             st["wm_total"], st["wm_losses"], st["wm_metrics"] = self._wm_heads(st["data"], st["embed"], st["leaves"],
@@ -1233,12 +1259,12 @@ class Dreamer(nn.Module):
             (A <= 16 if self.act_discrete else 2 * A <= 32) and 1 <= a.mlp.n <= 4 and 1 <= r._img_layers <= 4 and \
             a.last.weight.shape[0] <= 32
 
-    def _imagine_fused(self, feats, actions, H1, seed, row_offset, chunks=None, keep=None, actor_h0=None):
-        """sd_imagine_run (csrc/img.hip): feats[0] holds the start state. chunks: step boundaries [t0, t1, ..., H1];
-        the steps run as one launch sequence per chunk with an event recorded after each (returned), so consumers on
-        other streams can start on a chunk's feats while the next chunk is imagined."""
+    def _imagine_prepare(self, N, H1, seed, row_offset, device):
+        """The imagination's descriptor, workspace and everything in it that depends on the weights and the seed only:
+        the drawn-ahead noise (sd_imagine_noise) and the pre-split / transposed weight images (sd_imagine_prep). The
+        graphed update runs it as its own side-stream phase beside the encoder forward (S0), off the chain from the
+        posterior to the imagined returns; _imagine_fused(prep=...) then runs the steps."""
         r, a = self.rssm, self.actor
-        N = feats.shape[1]
         P = r._p()
         d = nat.ImagineDesc()
         d.N, d.H1, d.D, d.U, d.SK, d.Kd, d.G, d.A = N, H1, r._deter, r._hidden, r.flat_stoch, r._discrete, r._blocks, \
@@ -1262,27 +1288,42 @@ class Dreamer(nn.Module):
         for i, (lin, norm) in enumerate(mods):
             d.Wi[i], d.bi[i], d.ni[i] = lin.weight.data_ptr(), lin.bias.data_ptr(), norm.weight.data_ptr()
         d.Wl, d.bl = last.weight.data_ptr(), last.bias.data_ptr()
-        d.feats, d.actions = feats.data_ptr(), actions.data_ptr()
-        if IMAG_TRACE is not None:  # measurement aid (tools/imag_trace.py, a -DSD_SCAN_TRACE build of the library)
-            d.trace = IMAG_TRACE.data_ptr()
-        if actor_h0 is not None:
-            assert actor_h0.is_contiguous() and tuple(actor_h0.shape) == (H1, N, r._hidden), actor_h0.shape
-            d.actor_h0 = actor_h0.data_ptr()
         nwork = nat.fns["sd_imagine_work_floats"](ctypes.addressof(d))
         if nwork < 0:
             raise nat.NativeError(f"sd_imagine_work_floats failed with status {nwork}")
-        work = torch.empty(nwork, dtype=torch.float32, device=feats.device)
+        work = torch.empty(nwork, dtype=torch.float32, device=device)
         d.work = work.data_ptr()
         noise = None
         if IMAG_NOISE and H1 > 1:  # the prior samples' and actions' noise drawn in one full-chip launch up front
-            noise = torch.empty((H1 - 1) * N * r.flat_stoch + H1 * N * self.act_dim, dtype=torch.float32,
-                                device=feats.device)
+            noise = torch.empty((H1 - 1) * N * r.flat_stoch + H1 * N * self.act_dim, dtype=torch.float32, device=device)
             nact = noise[(H1 - 1) * N * r.flat_stoch:]
             d.noise_img, d.noise_act = noise.data_ptr(), nact.data_ptr()
             nat.call("sd_imagine_noise", ctypes.addressof(d), noise.data_ptr(), nact.data_ptr(), K.stream())
+        nat.call("sd_imagine_prep", ctypes.addressof(d), K.stream())
+        d.prepped = 1
+        return dict(desc=d, work=work, wo=wo, P=P, noise=noise, N=N, H1=H1)
+
+    def _imagine_fused(self, feats, actions, H1, seed, row_offset, chunks=None, keep=None, actor_h0=None, prep=None):
+        """sd_imagine_run (csrc/img.hip): feats[0] holds the start state. chunks: step boundaries [t0, t1, ..., H1];
+        the steps run as one launch sequence per chunk with an event recorded after each (returned), so consumers on
+        other streams can start on a chunk's feats while the next chunk is imagined. prep: _imagine_prepare's result
+        for this shape and seed (made here when None)."""
+        N = feats.shape[1]
+        if prep is None:
+            prep = self._imagine_prepare(N, H1, seed, row_offset, feats.device)
+        assert prep["N"] == N and prep["H1"] == H1, (prep["N"], prep["H1"], N, H1)
+        d = prep["desc"]
+        d.feats, d.actions = feats.data_ptr(), actions.data_ptr()
+        if IMAG_TRACE is not None:  # measurement aid (tools/imag_trace.py, a -DSD_SCAN_TRACE build of the library)
+            d.trace = IMAG_TRACE.data_ptr()
+        d.actor_h0 = None
+        if actor_h0 is not None:
+            assert actor_h0.is_contiguous() and tuple(actor_h0.shape) == (H1, N, self.rssm._hidden), actor_h0.shape
+            d.actor_h0 = actor_h0.data_ptr()
         bounds = list(chunks) if chunks else [0, H1]
         if keep is not None:  # measurement aid (bench.py): the descriptor and every buffer it points to
-            keep.update(desc=d, work=work, wo=wo, feats=feats, actions=actions, P=P, noise=noise)
+            keep.update(desc=d, work=prep["work"], wo=prep["wo"], feats=feats, actions=actions, P=prep["P"],
+                        noise=prep["noise"])
         events = []
         for t0, t1 in zip(bounds[:-1], bounds[1:]):
             d.t_begin, d.t_end = int(t0), int(t1)
@@ -1293,7 +1334,7 @@ class Dreamer(nn.Module):
                 events.append(ev)
         return events
 
-    def _imagine_tm(self, start, H1, seed, row_offset=0, chunks=None, actor_h0=None, feats=None):
+    def _imagine_tm(self, start, H1, seed, row_offset=0, chunks=None, actor_h0=None, feats=None, prep=None):
         """Dreamer._imagine (dreamer.py:673-692), time-major: feats (H1, N, F), actions (H1, N, A).
         The reference's last img_step (whose output is discarded) is skipped. With `chunks` (step boundaries) returns
         (feats, actions, events) with one event per chunk (see _imagine_fused). feats (fused path): a buffer whose
@@ -1311,7 +1352,7 @@ class Dreamer(nn.Module):
             if not preset:
                 feats[0, :, :SK] = s
                 feats[0, :, SK:] = h
-            events = self._imagine_fused(feats, actions, H1, seed, row_offset, chunks, actor_h0=actor_h0)
+            events = self._imagine_fused(feats, actions, H1, seed, row_offset, chunks, actor_h0=actor_h0, prep=prep)
             return (feats, actions, events) if chunks else (feats, actions)
         s, h = s.contiguous(), h.contiguous()
         for t in range(H1):

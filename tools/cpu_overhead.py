@@ -24,7 +24,7 @@ def main():
     torch.cuda.synchronize()
     gs = agent._graph if isinstance(agent._graph, tuple) else (agent._graph,)
     n = 10
-    for i, g in enumerate(gs):
+    for i, g in enumerate(x for x in gs if x is not None):
         t0 = time.perf_counter()
         for _ in range(n):
             g.replay()

@@ -52,7 +52,7 @@ def contention(agent, reps):
     """Which property of a filler phase slows a latency-bound phase beside it: the critical S1 / M2a graphs replayed
     alone, beside their real filler (M1 / S2), beside a filler of empty dispatches (launch count only) and beside a few
     long memory-bound launches (occupancy and bandwidth only)."""
-    G = dict(zip(("P", "S1", "M1", "R", "M2a", "S3", "M2b", "S4", "M2c", "M2d", "S2", "M3"), agent._graph))
+    G = dict(zip(("S0", "P", "S1", "M1", "R", "M2a", "S3", "M2b", "S4", "M2c", "M2d", "S2", "M3"), agent._graph))
     empty = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
@@ -109,7 +109,7 @@ def main():
     if only == ["contention"]:
         contention(agent, reps)
         return
-    names = ("P", "S1", "M1", "R", "M2a", "S3", "M2b", "S4", "M2c", "M2d", "S2", "M3")
+    names = ("S0", "P", "S1", "M1", "R", "M2a", "S3", "M2b", "S4", "M2c", "M2d", "S2", "M3")
     for nm, g in zip(names, agent._graph):
         if g is not None and (only is None or nm in only):
             if only is not None:  # kernel-trace window around this phase's timed replays (tools/phase_trace.sh)
