@@ -374,7 +374,12 @@ __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
   const int grc = rv ? gr : rb + nr - 1;  // rows past the tile read the tile's last row (results discarded)
   const long tBU = (long)t * B * UH;
   f32x4 h[NG], x0[NU], x1[NU], x2v[NU], b0v[NU], b1v[NU], n0v[NU], n1v[NU];
-  f32x4 x0p[X0F ? 1 : KSM][NU], x1p[KS1][NU];
+#ifndef SD_SCAN_PROBE_SLABS  // timing probe only (wrong results): k_hid reads / sums one x1p slab instead of ks_s
+#define SD_SCAN_PROBE_SLABS 0
+#endif
+  constexpr int KX1 = SD_SCAN_PROBE_SLABS ? 1 : KS1;
+  const int ks1 = SD_SCAN_PROBE_SLABS ? 1 : d.ks_s;
+  f32x4 x0p[X0F ? 1 : KSM][NU], x1p[KX1][NU];
   ld_row(h, d.h_in + (long)t * B * D + (long)grc * D + (long)g * Dg, t32);
   if constexpr (X0F) {
     ld_row(x0, d.xcat + 3 * tBU + (long)grc * 3 * UH, t32);
@@ -383,7 +388,7 @@ __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
     ld_row(b0v, d.b0, t32);
     ld_row(n0v, d.n0, t32);
   }
-  ld_slabs<NU, KS1>(x1p, w.x1s + (long)grc * UH, (long)B * UH, d.ks_s, t32);
+  ld_slabs<NU, KX1>(x1p, w.x1s + (long)grc * UH, (long)B * UH, ks1, t32);
   ld_row(b1v, d.b1, t32);
   ld_row(n1v, d.n1, t32);
   ld_row(x2v, d.x2 + in_row(d, t, grc) * UH, t32);
@@ -401,7 +406,7 @@ __global__ __launch_bounds__(NTHR) void k_hid(sd_rssm_scan d, Work w, int t) {
     for (int i = 0; i < NU; ++i) x0[i] += b0v[i];
     r0 = rms_silu_rows(x0, n0v, UH, d.eps, rv, y0);
   }
-  sum_slabs(x1, x1p, d.ks_s);
+  sum_slabs(x1, x1p, ks1);
 #pragma unroll
   for (int i = 0; i < NU; ++i) x1[i] += b1v[i];
   const float r1 = rms_silu_rows(x1, n1v, UH, d.eps, rv, y1);
