@@ -357,10 +357,14 @@ def probe_specs(agent, cfg, K):
     M = N * (H + 1)
     hp = K.LaunchProbe("sd_gemm_bf16x3_mlp", lambda a: a[0]._obj.batch == 4 and a[0]._obj.strideA == 0,
                        lambda a: 2.0 * a[0]._obj.M * a[0]._obj.N * a[0]._obj.K * a[0]._obj.batch,
-                       label="gemm3_mlp_kernel (imagined reward / continue / value / slow-value first layers: "
-                             "(M, F) x 4 (F, U) split-bf16, per-entry weights, row partials for the next layer's "
-                             "RMSNorm; 3 bf16 MFMAs per f32-equivalent product)")
-    add("heads_l0", "gemm3_mlp_kernel<false, true, 128>", (U // 128, M // 128, 4), "mfma",
+                       label="gemm3_w256_kernel (imagined reward / continue / value / slow-value first layers: "
+                             "(M, F) x 4 (F, U) split-bf16, 256 x 256 tiles on v_mfma_f32_32x32x16_bf16, per-entry "
+                             "weights, row partials for the next layer's RMSNorm; 3 bf16 MFMAs per f32-equivalent "
+                             "product)")
+    # (the 256 x 256-tile kernel where one 256-wide entry per tile fills the chip: gemm3.hip SD_MLP_W256)
+    w256 = U == 256 and -(-M // 256) * 4 >= 192
+    add("heads_l0", "gemm3_w256_kernel<true>" if w256 else "gemm3_mlp_kernel<false, true, 128>",
+        (-(-M // 256) * 4, 1, 1) if w256 else (U // 128, M // 128, 4), "mfma",
         2.0 * M * F * U * 4, 4.0 * (M * F + 4 * F * U + 4 * M * U + 4 * (U // 64) * M), hp.label, ("launch", hp), 1,
         peak=PEAK_BF16X3)
     # imagination step kernels
@@ -369,7 +373,8 @@ def probe_specs(agent, cfg, K):
     imag = [("imag_k_lin", "k_lin6<32, 32>" if lin6 else "k_lin<32, 32>", (U // 32, N // 32, 3),
              3 * 2.0 * N * D * U, 4.0 * (N * D + 3 * U * D + 3 * N * U + 2 * (U // 16) * N),
              IMAG_LABELS[3 if lin6 else 0], 0),
-            ("imag_k_hid", "k_hid", (D // 64, N // 64, 1), 2.0 * N * D * Ig,
+            ("imag_k_hid", "k_hid_areg" if (Ig // 32 in (32, 40) and not os.environ.get("SDHIP_KH_NOAREG"))
+             else "k_hid", (D // 64, N // 64, 1), 2.0 * N * D * Ig,
              4.0 * (N * D + 3 * N * U + D * Ig + N * D + N * D // 64), IMAG_LABELS[1], 1),
             ("imag_k_gate", "k_gate", (D // 32, N // 64, 1), 2.0 * N * 3 * D * Dg,
              4.0 * (N * D + 3 * D * Dg + 2 * N * D), IMAG_LABELS[2], 2)]
@@ -396,8 +401,8 @@ def probe_specs(agent, cfg, K):
 IMAG_LABELS = {
     0: "k_lin<32, 32> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
        "GEMMs in one launch, RMSNorm row partials in the epilogue; v_mfma_f32_16x16x4_f32)",
-    1: "k_hid (imagination step: _dyn_hid BlockLinear, K = Dg + 3U per block, RMSNorm + SiLU of x0 / x1 in the A "
-       "loader; bf16x6)",
+    1: "k_hid_areg (imagination step: _dyn_hid BlockLinear, K = Dg + 3U per block; A fragments loaded per lane from the "
+       "pre-split deter / x0 / x1 / x2 images, the weight tile through LDS; bf16x6)",
     2: "k_gate (imagination step: _dyn_gru BlockLinear + GRU epilogue, RMSNorm + SiLU of hp in the A loader; bf16x6)",
     3: "k_lin6<32, 32> x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
        "GEMMs in one launch on pre-split bf16x6 operands — the deter image k_gate writes, weight images split once per "
