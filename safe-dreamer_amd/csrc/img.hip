@@ -455,8 +455,12 @@ __global__ __launch_bounds__(256) void k_lin6(const __bf16* aimg, int K, const _
   const int n0 = tx * BN, m0 = ty * BM;
   f32x4 acc[1][WN / 16];
   SD_TR(1)
-  mainloop<true, FP_LIN, BM, BN, 16, WN, pf_of(KL_PF)>(BPre6<BM, 64>(aimg, m0 / 64, K / BK6, 0, m0 % 64),
-                                                      BPre6<BN>(wimg, tx, K / BK6, 0), 0, K, acc);
+#ifndef KL_BWTEST  // timing probe only (wrong results): 1 = every workgroup reads column tile 0's weights, 2 = row
+#define KL_BWTEST 0  // tile 0's deter rows, 3 = both (profiles/r05kl: 33.3 / 34.4 / 33.3 us — not operand traffic)
+#endif
+  const int ma = (KL_BWTEST & 2) ? 0 : m0, ta = (KL_BWTEST & 1) ? 0 : tx;
+  mainloop<true, FP_LIN, BM, BN, 16, WN, pf_of(KL_PF)>(BPre6<BM, 64>(aimg, ma / 64, K / BK6, 0, ma % 64),
+                                                      BPre6<BN>(wimg, ta, K / BK6, 0), 0, K, acc);
   SD_TR(2)
   ep_bias_part<BM, BN, WN, KL3_PW>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
   SD_TR_END(tr.p, tr.slot)
