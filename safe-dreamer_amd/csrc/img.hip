@@ -1047,6 +1047,110 @@ __global__ __launch_bounds__(256, 2) void k_hid_areg(sd_imagine d, float* hp, fl
   SD_TR_END(tr.p, tr.slot)
 }
 
+// k_lin6 on register A operands (KL_AREG): the step's three (N, D) x (D, U) deter contractions as 64 x 64 tiles of
+// 512 threads, the K range split between two halves of the workgroup (waves 0-3: k tiles 0 .. NKH - 1, waves 4-7:
+// NKH .. 2 NKH - 1), each half k_hid_areg's structure — wave w's 16 rows loaded per lane from the deter image into
+// register fragments two tiles ahead, the half's 64-column weight tile through its own double-buffered LDS stage, 24
+// MFMAs per A fragment set (k_lin6's 32 x 32 tiles have 6, too few to pay for fragment-shaped loads, profiles/r05za) —
+// and the two halves' accumulators added through LDS (half 0 + half 1) before k_lin6's epilogue. Per CU the same
+// work and waves as k_hid_areg (192 workgroups of 8 waves). The K order differs from k_lin6's one pass (the sums of
+// the two halves are added at the end), so the outputs agree with it to fp32 rounding, not bit for bit
+// (test_lin6_areg_matches_lin6). The weight images are in 64-column tiles (k_presplit6<64>) when this kernel runs.
+#ifndef KL_AREG
+#define KL_AREG 1
+#endif
+template <int NKH>
+__global__ __launch_bounds__(512, 2) void k_lin6_areg(const __bf16* aimg, int K, const __bf16* w0, const __bf16* w1,
+                                                      const __bf16* w2, LinProb p0, LinProb p1, LinProb p2, int M,
+                                                      Tr tr) {
+  SD_TR_BEGIN
+  constexpr int BM = 64, BN = 64, TN = 4, NS = 2;
+  constexpr int STG = BN * LROW6, BP = BN * PRE_ROW / 8 / 256;
+  static_assert(BN * PRE_ROW / 8 == 256 * BP && BM * (BN + 4) * 4 <= 2 * NS * STG * 2, "B pieces; reduce buffer");
+  __bf16* smem = sd_smem6<2 * NS * STG>();
+  int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
+  if (KL_XCD) xcd_tile(tx, ty, tz);
+  const LinProb p = tz == 0 ? p0 : (tz == 1 ? p1 : p2);
+  const __bf16* wimg = tz == 0 ? w0 : (tz == 1 ? w1 : w2);
+  const int n0 = tx * BN, m0 = ty * BM, nkt = K / BK6;
+  const int tid = threadIdx.x, half = tid >> 8, htid = tid & 255, lane = tid & 63, wave = (tid >> 6) & 3;
+  const int l16 = lane & 15, q = lane >> 4;
+  SD_TR(1)
+  const int kt0 = half * NKH;
+  const __bf16* ah = aimg + ((long)(m0 / 64) * nkt + kt0) * 64 * PRE_ROW + (long)(16 * wave + l16) * PRE_ROW + 8 * q;
+  const __bf16* bt = wimg + ((long)(n0 / BN) * nkt + kt0) * BN * PRE_ROW + htid * 8;
+  __bf16* hs = smem + half * NS * STG;
+  u32x4 A[3][3], B[2][BP];
+  auto load_a = [&](u32x4 (&a)[3], int kt) {
+    const __bf16* pa = ah + (long)kt * 64 * PRE_ROW;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) a[s] = *reinterpret_cast<const u32x4*>(pa + s * BK6);
+  };
+  auto load_b = [&](u32x4 (&b)[BP], int kt) {
+#pragma unroll
+    for (int u = 0; u < BP; ++u) b[u] = *reinterpret_cast<const u32x4*>(bt + ((long)kt * BN * PRE_ROW + u * 256 * 8));
+  };
+  auto store_b = [&](const u32x4 (&b)[BP], __bf16* st, int u) {
+    const int i = htid + 256 * u;
+    *reinterpret_cast<u32x4*>(st + (i / (PRE_ROW / 8)) * LROW6 + (i % (PRE_ROW / 8)) * 8) = b[u];
+  };
+  bf16x8 f[TN][3];
+  f32x4 acc[1][TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load_a(A[0], 0);
+  load_b(B[0], 0);
+  load_a(A[1], 1);
+  load_b(B[1], 1);
+#pragma unroll
+  for (int u = 0; u < BP; ++u) store_b(B[0], hs, u);
+  __syncthreads();
+#pragma unroll
+  for (int kt = 0; kt < NKH; ++kt) {
+    if (kt + NS < NKH) load_b(B[(kt + NS) % 2], kt + NS);
+    if (kt + 2 < NKH) load_a(A[(kt + 2) % 3], kt + 2);
+    __builtin_amdgcn_sched_barrier(0);  // the loads first
+    const int ts = kt + 1;  // the tile this step stages
+    __bf16* stg = hs + (ts % NS) * STG;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const __bf16* pb = hs + (kt % NS) * STG + (16 * j + l16) * LROW6 + 8 * q;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) f[j][s] = *reinterpret_cast<const bf16x8*>(pb + s * BK6);
+    }
+    // gemm6_core.h's six products per accumulator in its order, as six passes over the four accumulators
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int as = u == 0 ? 2 : (u == 1 || u == 3) ? 1 : 0, bs = u == 0 || u == 3 || u == 5 ? 0 : u == 2 ? 2 : 1;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, A[kt % 3][as]), f[j][bs],
+                                                            acc[0][j], 0, 0, 0);
+      if (ts < NKH && u < BP) store_b(B[ts % 2], stg, u);
+    }
+    __syncthreads();
+  }
+  SD_TR(2)
+  // half 1's accumulators through LDS (the stages are free after the loop's last barrier), added by half 0
+  constexpr int LDR = BN + 4;
+  float* red = reinterpret_cast<float*>(smem);
+  if (half == 1) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16] = acc[0][j][r];
+  }
+  __syncthreads();
+  if (half == 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[0][j][r] += red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16];
+    ep_bias_part<BM, BN, 64, KL3_PW>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
+  }
+  SD_TR_END(tr.p, tr.slot)
+}
+
 // gates = BlockLinear(dyn_gru)(silu(rms(hp))) + bg; deter' = GRU (rssm.py:65-75) -> feats[t+1][:, SK:].
 // Tile: 64 rows x (r | c | u) for 32 deter columns of block g (BN = 96). grid (D/32, M/64)
 // k_gate's B operand: the pre-split image of tile c0 / 32, or the r / c / u gate rows of Wg split while staged
@@ -1919,6 +2023,20 @@ static void launch_hid_areg(const sd_imagine& d, const IWork& w, int nkt, const 
 static bool img_lpre(const sd_imagine& d) {
   return KL_PRE && img_apre(d) && d.U % KL3_BN == 0 && d.D % BK6 == 0 && !getenv("SDHIP_KL_NOPRE");
 }
+// k_lin6_areg where it is built (D = 2048: two halves of 32 k tiles, U = 256); SDHIP_KL_NOAREG set: k_lin6 (A/B, and
+// the agreement test). Decides the weight images' column-tile width too (64 here, KL3_BN for k_lin6).
+static bool img_lareg(const sd_imagine& d) {
+  return KL_AREG && img_lpre(d) && d.D == 64 * BK6 && d.U == 256 && !getenv("SDHIP_KL_NOAREG");
+}
+// one k_lin6 / k_lin6_areg launch over nprob (2 or 3) problems sharing A = the deter image
+static void launch_lin6(const sd_imagine& d, const IWork& w, const __bf16* wa, const __bf16* wb, const __bf16* wc,
+                        const LinProb& pa, const LinProb& pb, const LinProb& pc, int nprob, Tr tr, hipStream_t st) {
+  if (img_lareg(d))
+    k_lin6_areg<32><<<dim3(d.U / 64, sd_cdiv(d.N, 64), nprob), 512, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc, d.N, tr);
+  else
+    k_lin6<KL6_BM, KL3_BN><<<dim3(d.U / KL3_BN, sd_cdiv(d.N, KL6_BM), nprob), 256, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb,
+                                                                                          pc, d.N, tr);
+}
 
 // One launch of step t's k_lin / k_lin6 (img_net_0 + _dyn_in0 + actor layer 0's deter part: which = 0), k_hid (1) or
 // k_gate (2), exactly as sd_imagine_run issues it (same descriptor and workspace; the launch recomputes the values that
@@ -1939,8 +2057,7 @@ extern "C" int sd_imagine_step_kernel(const sd_imagine* dp, int which, int t, sd
     LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
     LinProb pd{feats(t + 1) + SK, F, D, d.Wa[0] + SK, F, nullptr, w.ad, U, nullptr, nullptr};
     if (img_lpre(d))  // the images the run built (the deter image holds its last step: the timing is the same)
-      k_lin6<KL6_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL6_BM), 3), 256, 0, st>>>(w.h6, D, w.wi6, w.w06, w.wad6, pi, px, pd,
-                                                                         N, Tr{});
+      launch_lin6(d, w, w.wi6, w.w06, w.wad6, pi, px, pd, 3, Tr{}, st);
     else
       k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, Tr{});
   } else if (which == 1 && img_areg_nkt(d)) {  // (the images the run built)
@@ -1979,9 +2096,15 @@ static int imagine_prep(const sd_imagine& d, const IWork& w, hipStream_t st) {
   const bool lpre = img_lpre(d);  // the deter contractions' weights (img_net_0, _dyn_in0, actor layer 0's deter part)
   if (lpre) {
     const int gsz = (int)sd_cdiv((long)U * D / 4, 256);
-    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.Wi[0], U, D, w.wi6, D);
-    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.W0, U, D, w.w06, D);
-    k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(Wa0d, U, D, w.wad6, F);
+    if (img_lareg(d)) {  // 64-column tiles for k_lin6_areg
+      k_presplit6<64><<<gsz, 256, 0, st>>>(d.Wi[0], U, D, w.wi6, D);
+      k_presplit6<64><<<gsz, 256, 0, st>>>(d.W0, U, D, w.w06, D);
+      k_presplit6<64><<<gsz, 256, 0, st>>>(Wa0d, U, D, w.wad6, F);
+    } else {
+      k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.Wi[0], U, D, w.wi6, D);
+      k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.W0, U, D, w.w06, D);
+      k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(Wa0d, U, D, w.wad6, F);
+    }
     SD_LAUNCH_CHECK();
   }
   return SD_OK;
@@ -2030,8 +2153,7 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
     LinProb pd{feats(0) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
     // the 3-problem launch's tile, so x0p's row partials have one width for every step
     if (lpre)
-      k_lin6<KL6_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL6_BM), 2), 256, 0, st>>>(w.h6, D, w.w06, w.wad6, w.wad6, p, pd, pd,
-                                                                         N, Tr{});
+      launch_lin6(d, w, w.w06, w.wad6, w.wad6, p, pd, pd, 2, Tr{}, st);
     else
       k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 2), 256, 0, st>>>(p, pd, pd, N, Tr{});
     SD_LAUNCH_CHECK();
@@ -2107,8 +2229,7 @@ extern "C" int sd_imagine_run(const sd_imagine* dp, sd_stream stream_) {
       LinProb px{feats(t + 1) + SK, F, D, d.W0, D, d.b0, w.x0p, U, w.px0, nullptr};
       LinProb pd{feats(t + 1) + SK, F, D, Wa0d, F, nullptr, w.ad, U, nullptr, nullptr};
       if (lpre)
-        k_lin6<KL6_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL6_BM), 3), 256, 0, st>>>(w.h6, D, w.wi6, w.w06, w.wad6, pi, px,
-                                                                           pd, N, tr(7));
+        launch_lin6(d, w, w.wi6, w.w06, w.wad6, pi, px, pd, 3, tr(7), st);
       else
         k_lin<KL3_BM, KL3_BN><<<dim3(U / KL3_BN, sd_cdiv(N, KL3_BM), 3), 256, 0, st>>>(pi, px, pd, N, tr(7));
       SD_LAUNCH_CHECK();

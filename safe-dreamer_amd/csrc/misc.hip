@@ -394,38 +394,84 @@ __global__ __launch_bounds__(256) void loss_terms_bwd_kernel(sd_loss_terms L, co
   for (long j = (long)blockIdx.x * 256 + threadIdx.x; j < t.n; j += (long)gridDim.x * 256) t.g[j] = g;
 }
 
-// Weight layout copies, one launch for a list: mode 0 = transpose dst[b][c][r] = src[b * sb + r * sr + c]
-// (32 x 32 tiles through LDS, both sides coalesced); mode 1 = column pad dst[b * rows + r][c] = c < cols ?
-// src[b * sb + r * sr + c] : 0 for c < dcols.
+// Weight layout copies, one launch for a list: mode 0 = transpose dst[b][c][r] = src[b * sb + r * sr + c]; mode 1 =
+// column pad dst[b * rows + r][c] = c < cols ? src[b * sb + r * sr + c] : 0 for c < dcols. One workgroup per 64 x 64
+// tile, the tiles of all entries numbered in one flat range (no workgroup idles on a small entry while another walks
+// a large one); a transpose moves the tile through LDS with 16-byte loads and stores on both HBM sides where the
+// entry's strides allow it (4-byte accesses otherwise and at ragged edges).
+namespace lcopy {
+constexpr int TS = 64, LD = TS + 4;
+__device__ inline int tiles_of(const sd_layout_copy& e) {
+  return e.batch * ((e.rows + TS - 1) / TS) * (((e.mode ? e.dcols : e.cols) + TS - 1) / TS);
+}
+}  // namespace lcopy
+
 __global__ __launch_bounds__(256) void layout_copy_kernel(sd_layout_copies L) {
-  __shared__ float tile[32][33];
-  const sd_layout_copy e = L.e[blockIdx.y];
-  const int tr = (e.rows + 31) / 32, tc = (e.mode ? (e.dcols + 31) / 32 : (e.cols + 31) / 32);
-  const long ntiles = (long)e.batch * tr * tc;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows of 32 lanes
-  for (long tile_i = blockIdx.x; tile_i < ntiles; tile_i += gridDim.x) {
-    const int b = (int)(tile_i / ((long)tr * tc)), rem = (int)(tile_i % ((long)tr * tc));
-    const int r0 = (rem / tc) * 32, c0 = (rem % tc) * 32;
-    const float* src = e.src + (long)b * e.sb;
-    if (e.mode == 1) {
-      for (int i = ty; i < 32; i += 8) {
-        const int r = r0 + i, c = c0 + tx;
-        if (r < e.rows && c < e.dcols)
-          e.dst[((long)b * e.rows + r) * (e.dld ? e.dld : e.dcols) + c] = c < e.cols ? src[(long)r * e.sr + c] : 0.f;
+  using namespace lcopy;
+  __shared__ float tile[TS * LD];
+  int id = blockIdx.x, ei = 0;
+  for (; ei < L.n; ++ei) {
+    const int n = tiles_of(L.e[ei]);
+    if (id < n) break;
+    id -= n;
+  }
+  if (ei >= L.n) return;
+  const sd_layout_copy& e = L.e[ei];
+  const int tc = ((e.mode ? e.dcols : e.cols) + TS - 1) / TS, tr = (e.rows + TS - 1) / TS;
+  const int b = id / (tr * tc), rem = id % (tr * tc), r0 = (rem / tc) * TS, c0 = (rem % tc) * TS;
+  const float* src = e.src + (long)b * e.sb;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;  // 16 rows of 16 four-column groups
+  if (e.mode == 1) {
+    const long ld = e.dld ? e.dld : e.dcols;
+    const int c = c0 + (int)(threadIdx.x & 63);  // a wave per row, lanes on consecutive columns
+    for (int i = threadIdx.x >> 6; i < TS; i += 4) {
+      const int r = r0 + i;
+      if (r >= e.rows) break;
+      if (c < e.dcols) e.dst[((long)b * e.rows + r) * ld + c] = c < e.cols ? src[(long)r * e.sr + c] : 0.f;
+    }
+    return;
+  }
+  const bool vin = ((e.sr | e.sb) & 3) == 0 && ((uintptr_t)e.src & 15) == 0;
+  const bool vout = (e.rows & 3) == 0 && ((uintptr_t)e.dst & 15) == 0;
+  const int c = c0 + 4 * tx;
+#pragma unroll
+  for (int i = 0; i < TS / 16; ++i) {
+    const int rl = ty + 16 * i, r = r0 + rl;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < e.rows) {
+      const float* p = src + (long)r * e.sr + c;
+      if (vin && c + 3 < e.cols) {
+        v = *reinterpret_cast<const float4*>(p);
+      } else {
+        if (c < e.cols) v.x = p[0];
+        if (c + 1 < e.cols) v.y = p[1];
+        if (c + 2 < e.cols) v.z = p[2];
+        if (c + 3 < e.cols) v.w = p[3];
       }
-      continue;
     }
-    for (int i = ty; i < 32; i += 8) {
-      const int r = r0 + i, c = c0 + tx;
-      tile[i][tx] = (r < e.rows && c < e.cols) ? src[(long)r * e.sr + c] : 0.f;
+    *reinterpret_cast<float4*>(&tile[rl * LD + 4 * tx]) = v;
+  }
+  __syncthreads();
+  float* dst = e.dst + (long)b * e.rows * e.cols;
+  const int r = r0 + 4 * tx;  // dst columns r .. r + 3
+#pragma unroll
+  for (int i = 0; i < TS / 16; ++i) {
+    const int cl = ty + 16 * i, cc = c0 + cl;  // dst row
+    if (cc >= e.cols) break;
+    float4 v;
+    v.x = tile[(4 * tx + 0) * LD + cl];
+    v.y = tile[(4 * tx + 1) * LD + cl];
+    v.z = tile[(4 * tx + 2) * LD + cl];
+    v.w = tile[(4 * tx + 3) * LD + cl];
+    float* p = dst + (long)cc * e.rows + r;
+    if (vout && r + 3 < e.rows) {
+      *reinterpret_cast<float4*>(p) = v;
+    } else {
+      if (r < e.rows) p[0] = v.x;
+      if (r + 1 < e.rows) p[1] = v.y;
+      if (r + 2 < e.rows) p[2] = v.z;
+      if (r + 3 < e.rows) p[3] = v.w;
     }
-    __syncthreads();
-    float* dst = e.dst + (long)b * e.rows * e.cols;
-    for (int i = ty; i < 32; i += 8) {
-      const int c = c0 + i, r = r0 + tx;  // dst row c, column r
-      if (c < e.cols && r < e.rows) dst[(long)c * e.rows + r] = tile[tx][i];
-    }
-    __syncthreads();
   }
 }
 
@@ -516,16 +562,16 @@ extern "C" int sd_loss_terms_bwd(const sd_loss_terms* L, const float* g_total, c
 
 extern "C" int sd_layout_copies_run(const sd_layout_copies* L, sd_stream s) {
   if (!L || L->n < 1 || L->n > SD_MAX_LAYOUT_COPIES) return SD_EARG;
-  long most = 0;
+  long total = 0;
   for (int i = 0; i < L->n; ++i) {
     const sd_layout_copy& e = L->e[i];
     if (!e.src || !e.dst || e.batch < 1 || e.rows < 1 || e.cols < 1 || e.mode < 0 || e.mode > 1) return SD_EARG;
     if (e.mode == 1 && e.dcols < e.cols) return SD_EARG;
-    const long t = (long)e.batch * ((e.rows + 31) / 32) * (((e.mode ? e.dcols : e.cols) + 31) / 32);
-    most = t > most ? t : most;
+    total += (long)e.batch * ((e.rows + lcopy::TS - 1) / lcopy::TS) *
+             (((e.mode ? e.dcols : e.cols) + lcopy::TS - 1) / lcopy::TS);
   }
-  const int gx = (int)(most < 1024 ? most : 1024);
-  layout_copy_kernel<<<dim3(gx, L->n), 256, 0, (hipStream_t)s>>>(*L);
+  if (total > 0x7fffffffL) return SD_ESHAPE;
+  layout_copy_kernel<<<dim3((unsigned)total), 256, 0, (hipStream_t)s>>>(*L);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }

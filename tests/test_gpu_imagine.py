@@ -105,6 +105,34 @@ def test_lin6_matches_fp32_lin(name, N):
 
 
 @pytest.mark.parametrize("name,N", [("walker_r2", 192), ("atari_r2", 100), ("maze_r2", 128)])
+def test_lin6_areg_matches_lin6(name, N):
+    """k_lin6_areg (the deter contractions as 64 x 64 tiles whose K range is split between two halves of the
+    workgroup, D = 2048; maze's D = 4096 keeps k_lin6) against k_lin6 (SDHIP_KL_NOAREG): the same bf16x6 products,
+    summed as two halves then added — fp32 rounding apart, so the same imagined indices except near-ties and deter /
+    actions within 1e-5 relative."""
+    import os
+    ag, z, spec, obs = build_agent(name)
+    start = _start(ag, N, 19)
+    a = _run(ag, start, 6, True)
+    os.environ["SDHIP_KL_NOAREG"] = "1"
+    try:
+        b = _run(ag, start, 6, True)
+    finally:
+        del os.environ["SDHIP_KL_NOAREG"]
+    if ag.rssm._deter != 2048:
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+        return
+    SK = ag.rssm.flat_stoch
+    ia = a[0][..., :SK].reshape(*a[0].shape[:2], -1, ag.rssm._discrete).argmax(-1)
+    ib = b[0][..., :SK].reshape(*b[0].shape[:2], -1, ag.rssm._discrete).argmax(-1)
+    rows_same = (ia == ib).reshape(ia.shape[0], ia.shape[1], -1).all(-1).all(0)
+    assert rows_same.float().mean() >= 0.98
+    da, db = a[0][:, rows_same, SK:], b[0][:, rows_same, SK:]
+    assert (da - db).abs().max() <= 1e-5 * (1 + db.abs().max())
+    assert not torch.equal(a[0], b[0]), "k_lin6_areg did not run"
+
+
+@pytest.mark.parametrize("name,N", [("walker_r2", 192), ("atari_r2", 100), ("maze_r2", 128)])
 def test_hid_areg_bit_identical(name, N):
     """k_hid_areg (register A operands from the pre-split images, one fully unrolled K loop; Dg 256 and 512) gives
     exactly k_hid<true>'s imagination (SDHIP_KH_NOAREG): same planes, same six products per k tile in the same order."""

@@ -736,3 +736,29 @@ def test_first_stage_pooled_wgrad_reordered_sums(ci, co, hw, nb):
     else:
         for a, r, what in zip(grads[0], grads[1], ("w", "b", "nw")):
             close(a, r, 2e-5, what)
+
+
+def test_layout_copies_exact():
+    """sd_layout_copies_run (the scan backward's W^T images, the conv pad, get_feat's strided concat): transposes of
+    batched, ragged (not multiple of 64 / 4), strided and misaligned sources and column pads into a strided slot,
+    all in one launch, must equal torch's copies bit for bit."""
+    from sdreamer import kernels as K
+    g = _g(11)
+    ents, want = [], []
+    for nb, rows, cols, sr_pad, off in [(1, 2048, 256, 0, 0), (8, 256, 512, 0, 0), (3, 70, 45, 3, 1),
+                                        (1, 5, 130, 0, 0), (2, 129, 64, 4, 0), (1, 1, 1, 0, 0), (1, 64, 7, 1, 2)]:
+        base = torch.randn(nb * rows * (cols + sr_pad) + off, generator=g).to(DEV)
+        src = base[off:].view(nb, rows, cols + sr_pad)[:, :, :cols]
+        dst = torch.full((nb, cols, rows), float("nan"), device=DEV)
+        ents.append((src, dst, nb, rows, cols, src.stride(0), src.stride(1), cols, 0))
+        want.append((dst, src.transpose(1, 2)))
+    x = torch.randn(33, 5, generator=g).to(DEV)
+    slot = torch.full((33, 12), float("nan"), device=DEV)
+    ents.append((x, slot, 1, 33, 5, 0, 5, 9, 1, 12))
+    ref = torch.cat([x, torch.zeros(33, 4, device=DEV)], 1)
+    K.layout_copies(ents)
+    torch.cuda.synchronize()
+    for i, (d, r) in enumerate(want):
+        assert torch.equal(d, r.contiguous()), f"entry {i}"
+    assert torch.equal(slot[:, :9], ref)
+    assert torch.isnan(slot[:, 9:]).all()
