@@ -369,11 +369,12 @@ def probe_specs(agent, cfg, K):
         peak=PEAK_BF16X3)
     # imagination step kernels
     # k_lin6 (pre-split deter image + weight images, 32-row tiles) unless SDHIP_KL_NOPRE selects the fp32 k_lin
-    # (k_lin6_areg — 64 x 64 tiles, K split over two halves of a 512-thread workgroup — at D = 2048, U = 256)
+    # (k_lin6_areg — 64 x 48 tiles over the three problems' columns, K split over two halves of a 512-thread
+    # workgroup — at D = 2048, U = 256)
     lin6 = not os.environ.get("SDHIP_KL_NOPRE")
     lareg = lin6 and D == 2048 and U == 256 and not os.environ.get("SDHIP_KL_NOAREG")
     imag = [("imag_k_lin", "k_lin6_areg" if lareg else "k_lin6<32, 32>" if lin6 else "k_lin<32, 32>",
-             (U // 64, N // 64, 3) if lareg else (U // 32, N // 32, 3),
+             (3 * U // 48, N // 64, 1) if lareg else (U // 32, N // 32, 3),
              3 * 2.0 * N * D * U, 4.0 * (N * D + 3 * U * D + 3 * N * U + 2 * (U // 16) * N),
              IMAG_LABELS[4 if lareg else 3 if lin6 else 0], 0),
             ("imag_k_hid", "k_hid_areg" if (Ig // 32 in (32, 40) and not os.environ.get("SDHIP_KH_NOAREG"))
@@ -411,7 +412,8 @@ IMAG_LABELS = {
        "GEMMs in one launch on pre-split bf16x6 operands — the deter image k_gate writes, weight images split once per "
        "imagination — RMSNorm row partials in the epilogue; 6 v_mfma_f32_16x16x32_bf16 per f32-equivalent product)",
     4: "k_lin6_areg x3 (imagination step: img_net_0 + _dyn_in0 + actor layer 0's deter part, three (N, D) x (D, U) "
-       "GEMMs in one launch, 64 x 64 tiles of 512 threads with the K range split over two halves; deter fragments "
+       "GEMMs in one launch, 64 x 48 tiles over their concatenated columns (256 workgroups of 512 threads, the K range "
+       "split over two halves); deter fragments "
        "loaded per lane from the pre-split image, weight tiles through LDS; bf16x6)",
 }
 

@@ -1047,38 +1047,51 @@ __global__ __launch_bounds__(256, 2) void k_hid_areg(sd_imagine d, float* hp, fl
   SD_TR_END(tr.p, tr.slot)
 }
 
-// k_lin6 on register A operands (KL_AREG): the step's three (N, D) x (D, U) deter contractions as 64 x 64 tiles of
-// 512 threads, the K range split between two halves of the workgroup (waves 0-3: k tiles 0 .. NKH - 1, waves 4-7:
-// NKH .. 2 NKH - 1), each half k_hid_areg's structure — wave w's 16 rows loaded per lane from the deter image into
-// register fragments two tiles ahead, the half's 64-column weight tile through its own double-buffered LDS stage, 24
-// MFMAs per A fragment set (k_lin6's 32 x 32 tiles have 6, too few to pay for fragment-shaped loads, profiles/r05za) —
-// and the two halves' accumulators added through LDS (half 0 + half 1) before k_lin6's epilogue. Per CU the same
-// work and waves as k_hid_areg (192 workgroups of 8 waves). The K order differs from k_lin6's one pass (the sums of
-// the two halves are added at the end), so the outputs agree with it to fp32 rounding, not bit for bit
-// (test_lin6_areg_matches_lin6). The weight images are in 64-column tiles (k_presplit6<64>) when this kernel runs.
+// k_lin6 on register A operands (KL_AREG): the step's three (N, D) x (D, U) deter contractions as one (N, D) x
+// (D, nprob * U) product over the problems' concatenated columns, in 64-row x (16 NSUB)-column tiles of 512 threads
+// whose K range is split between the two halves of the workgroup (waves 0-3: k tiles 0 .. NKH - 1, waves 4-7:
+// NKH .. 2 NKH - 1). Each half has k_hid_areg's structure: wave w's 16 rows loaded per lane from the deter image into
+// register fragments two tiles ahead, the half's weight tile through its own double-buffered LDS stage, 6 NSUB MFMAs
+// per A fragment set (k_lin6's 32 x 32 tiles have 6, too few to pay for fragment-shaped loads, profiles/r05za); then
+// half 1's accumulators are added to half 0's through LDS before k_lin6's epilogue. NSUB = 3 (48 columns: 16 x 16 =
+// 256 workgroups for three problems, one per CU) or 4 (the two-problem launch). The weight images are in 16-column
+// tiles (k_presplit6<16>), so a tile's three or four 16-column pieces may come from different problems; the 16-column
+// row-partial groups never straddle two. The halves' sums are added at the end, so the outputs agree with k_lin6's
+// one pass to fp32 rounding, not bit for bit (test_lin6_areg_matches_lin6); NSUB 3 and 4 give the same values.
 #ifndef KL_AREG
 #define KL_AREG 1
 #endif
-template <int NKH>
+#ifndef KL_NSUB  // 16-column pieces per tile of the three-problem launch
+#define KL_NSUB 3
+#endif
+template <int NKH, int NSUB>
 __global__ __launch_bounds__(512, 2) void k_lin6_areg(const __bf16* aimg, int K, const __bf16* w0, const __bf16* w1,
-                                                      const __bf16* w2, LinProb p0, LinProb p1, LinProb p2, int M,
-                                                      Tr tr) {
+                                                      const __bf16* w2, LinProb p0, LinProb p1, LinProb p2, int U,
+                                                      int M, Tr tr) {
   SD_TR_BEGIN
-  constexpr int BM = 64, BN = 64, TN = 4, NS = 2;
-  constexpr int STG = BN * LROW6, BP = BN * PRE_ROW / 8 / 256;
-  static_assert(BN * PRE_ROW / 8 == 256 * BP && BM * (BN + 4) * 4 <= 2 * NS * STG * 2, "B pieces; reduce buffer");
+  constexpr int BM = 64, BN = 16 * NSUB, NS = 2, PPS = 16 * PRE_ROW / 8;  // PPS: 16-B pieces per 16-column piece
+  constexpr int STG = BN * LROW6, BP = (NSUB * PPS + 255) / 256;
+  static_assert(BM * (BN + 4) * 4 <= 2 * NS * STG * 2, "reduce buffer within the stages");
   __bf16* smem = sd_smem6<2 * NS * STG>();
-  int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
+  int tx = blockIdx.x, ty = blockIdx.y, tz = 0;
   if (KL_XCD) xcd_tile(tx, ty, tz);
-  const LinProb p = tz == 0 ? p0 : (tz == 1 ? p1 : p2);
-  const __bf16* wimg = tz == 0 ? w0 : (tz == 1 ? w1 : w2);
-  const int n0 = tx * BN, m0 = ty * BM, nkt = K / BK6;
+  const int c0 = tx * BN, m0 = ty * BM, nkt = K / BK6;
   const int tid = threadIdx.x, half = tid >> 8, htid = tid & 255, lane = tid & 63, wave = (tid >> 6) & 3;
   const int l16 = lane & 15, q = lane >> 4;
   SD_TR(1)
   const int kt0 = half * NKH;
   const __bf16* ah = aimg + ((long)(m0 / 64) * nkt + kt0) * 64 * PRE_ROW + (long)(16 * wave + l16) * PRE_ROW + 8 * q;
-  const __bf16* bt = wimg + ((long)(n0 / BN) * nkt + kt0) * BN * PRE_ROW + htid * 8;
+  // this thread's B pieces: piece i = htid + 256 u of the tile, 16-column piece i / PPS (column c0 + 16 (i / PPS))
+  const __bf16* bt[BP];
+  int boff[BP];
+#pragma unroll
+  for (int u = 0; u < BP; ++u) {
+    const int i = htid + 256 * u, sp = i < NSUB * PPS ? i / PPS : 0, c = c0 + 16 * sp, pz = c / U;
+    const __bf16* img = pz == 0 ? w0 : (pz == 1 ? w1 : w2);
+    bt[u] = img + (((long)((c % U) / 16) * nkt + kt0) * 16) * PRE_ROW + (i % PPS) * 8;
+    boff[u] = (16 * sp + (i % PPS) / (PRE_ROW / 8)) * LROW6 + (i % (PRE_ROW / 8)) * 8;
+  }
+  auto live = [&](int u) { return 256 * (u + 1) <= NSUB * PPS || htid + 256 * u < NSUB * PPS; };
   __bf16* hs = smem + half * NS * STG;
   u32x4 A[3][3], B[2][BP];
   auto load_a = [&](u32x4 (&a)[3], int kt) {
@@ -1088,16 +1101,16 @@ __global__ __launch_bounds__(512, 2) void k_lin6_areg(const __bf16* aimg, int K,
   };
   auto load_b = [&](u32x4 (&b)[BP], int kt) {
 #pragma unroll
-    for (int u = 0; u < BP; ++u) b[u] = *reinterpret_cast<const u32x4*>(bt + ((long)kt * BN * PRE_ROW + u * 256 * 8));
+    for (int u = 0; u < BP; ++u)
+      if (live(u)) b[u] = *reinterpret_cast<const u32x4*>(bt[u] + (long)kt * 16 * PRE_ROW);
   };
   auto store_b = [&](const u32x4 (&b)[BP], __bf16* st, int u) {
-    const int i = htid + 256 * u;
-    *reinterpret_cast<u32x4*>(st + (i / (PRE_ROW / 8)) * LROW6 + (i % (PRE_ROW / 8)) * 8) = b[u];
+    if (live(u)) *reinterpret_cast<u32x4*>(st + boff[u]) = b[u];
   };
-  bf16x8 f[TN][3];
-  f32x4 acc[1][TN];
+  bf16x8 f[NSUB][3];
+  f32x4 acc[NSUB];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < NSUB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   load_a(A[0], 0);
   load_b(B[0], 0);
   load_a(A[1], 1);
@@ -1113,19 +1126,19 @@ __global__ __launch_bounds__(512, 2) void k_lin6_areg(const __bf16* aimg, int K,
     const int ts = kt + 1;  // the tile this step stages
     __bf16* stg = hs + (ts % NS) * STG;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
+    for (int j = 0; j < NSUB; ++j) {
       const __bf16* pb = hs + (kt % NS) * STG + (16 * j + l16) * LROW6 + 8 * q;
 #pragma unroll
       for (int s = 0; s < 3; ++s) f[j][s] = *reinterpret_cast<const bf16x8*>(pb + s * BK6);
     }
-    // gemm6_core.h's six products per accumulator in its order, as six passes over the four accumulators
+    // gemm6_core.h's six products per accumulator in its order, as six passes over the accumulators
 #pragma unroll
     for (int u = 0; u < 6; ++u) {
       const int as = u == 0 ? 2 : (u == 1 || u == 3) ? 1 : 0, bs = u == 0 || u == 3 || u == 5 ? 0 : u == 2 ? 2 : 1;
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, A[kt % 3][as]), f[j][bs],
-                                                            acc[0][j], 0, 0, 0);
+      for (int j = 0; j < NSUB; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, A[kt % 3][as]), f[j][bs], acc[j],
+                                                         0, 0, 0);
       if (ts < NKH && u < BP) store_b(B[ts % 2], stg, u);
     }
     __syncthreads();
@@ -1136,17 +1149,36 @@ __global__ __launch_bounds__(512, 2) void k_lin6_areg(const __bf16* aimg, int K,
   float* red = reinterpret_cast<float*>(smem);
   if (half == 1) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < NSUB; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16] = acc[0][j][r];
+      for (int r = 0; r < 4; ++r) red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16] = acc[j][r];
   }
   __syncthreads();
   if (half == 0) {
+    // ep_bias_part's arithmetic per 16-column piece of its problem: out = acc + bias (+ add), part = the piece's
+    // sum of squares (one 16-column group)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < NSUB; ++j) {
+      const int c = c0 + 16 * j, pz = c / U, n = c % U + l16;
+      const LinProb& p = pz == 0 ? p0 : (pz == 1 ? p1 : p2);
+      const float bv = p.bias ? p.bias[n] : 0.f;
+      float ss[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[0][j][r] += red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16];
-    ep_bias_part<BM, BN, 64, KL3_PW>(acc, p.bias, p.out, p.ldo, p.part, M, m0, n0, p.add);
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 16 * wave + 4 * q + r;
+        float v = (acc[j][r] + red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16]) + bv;
+        if (p.add && m < M) v += p.add[(long)m * p.ldo + n];
+        if (m < M) p.out[(long)m * p.ldo + n] = v;
+        ss[r] = 0.f;
+        ss[r] += v * v;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sv = group_sum<16>(ss[r]);
+        const int m = m0 + 16 * wave + 4 * q + r;
+        if (l16 == 0 && p.part && m < M) p.part[(long)((c % U) / 16) * M + m] = sv;
+      }
+    }
   }
   SD_TR_END(tr.p, tr.slot)
 }
@@ -2024,7 +2056,7 @@ static bool img_lpre(const sd_imagine& d) {
   return KL_PRE && img_apre(d) && d.U % KL3_BN == 0 && d.D % BK6 == 0 && !getenv("SDHIP_KL_NOPRE");
 }
 // k_lin6_areg where it is built (D = 2048: two halves of 32 k tiles, U = 256); SDHIP_KL_NOAREG set: k_lin6 (A/B, and
-// the agreement test). Decides the weight images' column-tile width too (64 here, KL3_BN for k_lin6).
+// the agreement test). Decides the weight images' column-tile width too (16 here, KL3_BN for k_lin6).
 static bool img_lareg(const sd_imagine& d) {
   return KL_AREG && img_lpre(d) && d.D == 64 * BK6 && d.U == 256 && !getenv("SDHIP_KL_NOAREG");
 }
@@ -2032,7 +2064,12 @@ static bool img_lareg(const sd_imagine& d) {
 static void launch_lin6(const sd_imagine& d, const IWork& w, const __bf16* wa, const __bf16* wb, const __bf16* wc,
                         const LinProb& pa, const LinProb& pb, const LinProb& pc, int nprob, Tr tr, hipStream_t st) {
   if (img_lareg(d))
-    k_lin6_areg<32><<<dim3(d.U / 64, sd_cdiv(d.N, 64), nprob), 512, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc, d.N, tr);
+    if (nprob == 3 && KL_NSUB == 3 && !getenv("SDHIP_KL_NSUB4"))  // (SDHIP_KL_NSUB4: 64-column tiles, the A/B and test)
+      k_lin6_areg<32, 3><<<dim3(3 * d.U / 48, sd_cdiv(d.N, 64)), 512, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc, d.U,
+                                                                              d.N, tr);
+    else
+      k_lin6_areg<32, 4><<<dim3(nprob * d.U / 64, sd_cdiv(d.N, 64)), 512, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc,
+                                                                                  d.U, d.N, tr);
   else
     k_lin6<KL6_BM, KL3_BN><<<dim3(d.U / KL3_BN, sd_cdiv(d.N, KL6_BM), nprob), 256, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb,
                                                                                           pc, d.N, tr);
@@ -2096,10 +2133,10 @@ static int imagine_prep(const sd_imagine& d, const IWork& w, hipStream_t st) {
   const bool lpre = img_lpre(d);  // the deter contractions' weights (img_net_0, _dyn_in0, actor layer 0's deter part)
   if (lpre) {
     const int gsz = (int)sd_cdiv((long)U * D / 4, 256);
-    if (img_lareg(d)) {  // 64-column tiles for k_lin6_areg
-      k_presplit6<64><<<gsz, 256, 0, st>>>(d.Wi[0], U, D, w.wi6, D);
-      k_presplit6<64><<<gsz, 256, 0, st>>>(d.W0, U, D, w.w06, D);
-      k_presplit6<64><<<gsz, 256, 0, st>>>(Wa0d, U, D, w.wad6, F);
+    if (img_lareg(d)) {  // 16-column tiles for k_lin6_areg
+      k_presplit6<16><<<gsz, 256, 0, st>>>(d.Wi[0], U, D, w.wi6, D);
+      k_presplit6<16><<<gsz, 256, 0, st>>>(d.W0, U, D, w.w06, D);
+      k_presplit6<16><<<gsz, 256, 0, st>>>(Wa0d, U, D, w.wad6, F);
     } else {
       k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.Wi[0], U, D, w.wi6, D);
       k_presplit6<KL3_BN><<<gsz, 256, 0, st>>>(d.W0, U, D, w.w06, D);

@@ -132,6 +132,22 @@ def test_lin6_areg_matches_lin6(name, N):
     assert not torch.equal(a[0], b[0]), "k_lin6_areg did not run"
 
 
+@pytest.mark.parametrize("name,N", [("walker_r2", 192), ("atari_r2", 100)])
+def test_lin6_areg_tiles_bit_identical(name, N):
+    """k_lin6_areg's 48-column tiles over the three problems' concatenated columns (pieces of two problems in one
+    tile) against its 64-column tiles (SDHIP_KL_NSUB4): the same k order per element, so the same bits."""
+    import os
+    ag, z, spec, obs = build_agent(name)
+    start = _start(ag, N, 23)
+    a = _run(ag, start, 6, True)
+    os.environ["SDHIP_KL_NSUB4"] = "1"
+    try:
+        b = _run(ag, start, 6, True)
+    finally:
+        del os.environ["SDHIP_KL_NSUB4"]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
 @pytest.mark.parametrize("name,N", [("walker_r2", 192), ("atari_r2", 100), ("maze_r2", 128)])
 def test_hid_areg_bit_identical(name, N):
     """k_hid_areg (register A operands from the pre-split images, one fully unrolled K loop; Dg 256 and 512) gives
