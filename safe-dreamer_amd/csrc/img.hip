@@ -1053,7 +1053,8 @@ __global__ __launch_bounds__(256, 2) void k_hid_areg(sd_imagine d, float* hp, fl
 // NKH .. 2 NKH - 1). Each half has k_hid_areg's structure: wave w's 16 rows loaded per lane from the deter image into
 // register fragments two tiles ahead, the half's weight tile through its own double-buffered LDS stage, 6 NSUB MFMAs
 // per A fragment set (k_lin6's 32 x 32 tiles have 6, too few to pay for fragment-shaped loads, profiles/r05za); then
-// half 1's accumulators are added to half 0's through LDS before k_lin6's epilogue. NSUB = 3 (48 columns: 16 x 16 =
+// the halves exchange half of their accumulators through LDS and each runs k_lin6's epilogue on two of every lane's
+// four rows. NSUB = 3 (48 columns: 16 x 16 =
 // 256 workgroups for three problems, one per CU) or 4 (the two-problem launch). The weight images are in 16-column
 // tiles (k_presplit6<16>), so a tile's three or four 16-column pieces may come from different problems; the 16-column
 // row-partial groups never straddle two. The halves' sums are added at the end, so the outputs agree with k_lin6's
@@ -1144,40 +1145,39 @@ __global__ __launch_bounds__(512, 2) void k_lin6_areg(const __bf16* aimg, int K,
     __syncthreads();
   }
   SD_TR(2)
-  // half 1's accumulators through LDS (the stages are free after the loop's last barrier), added by half 0
+  // the two halves' sums meet through LDS (the stages are free after the loop's last barrier): half h finishes rows
+  // r = 2h, 2h + 1 of each lane's four (acc[j][r] of both halves added, a + b = b + a), so both run the epilogue
   constexpr int LDR = BN + 4;
   float* red = reinterpret_cast<float*>(smem);
-  if (half == 1) {
+  const int rk = 2 * half;  // the rows this half keeps; it hands over the other two
 #pragma unroll
-    for (int j = 0; j < NSUB; ++j)
+  for (int j = 0; j < NSUB; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16] = acc[j][r];
-  }
+    for (int r = 0; r < 4; ++r)
+      if ((r >> 1) != half) red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16] = acc[j][r];
   __syncthreads();
-  if (half == 0) {
-    // ep_bias_part's arithmetic per 16-column piece of its problem: out = acc + bias (+ add), part = the piece's
-    // sum of squares (one 16-column group)
+  // ep_bias_part's arithmetic per 16-column piece of its problem: out = acc + bias (+ add), part = the piece's sum
+  // of squares (one 16-column group)
 #pragma unroll
-    for (int j = 0; j < NSUB; ++j) {
-      const int c = c0 + 16 * j, pz = c / U, n = c % U + l16;
-      const LinProb& p = pz == 0 ? p0 : (pz == 1 ? p1 : p2);
-      const float bv = p.bias ? p.bias[n] : 0.f;
-      float ss[4];
+  for (int j = 0; j < NSUB; ++j) {
+    const int c = c0 + 16 * j, pz = c / U, n = c % U + l16;
+    const LinProb& p = pz == 0 ? p0 : (pz == 1 ? p1 : p2);
+    const float bv = p.bias ? p.bias[n] : 0.f;
+    float ss[2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + 16 * wave + 4 * q + r;
-        float v = (acc[j][r] + red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16]) + bv;
-        if (p.add && m < M) v += p.add[(long)m * p.ldo + n];
-        if (m < M) p.out[(long)m * p.ldo + n] = v;
-        ss[r] = 0.f;
-        ss[r] += v * v;
-      }
+    for (int i = 0; i < 2; ++i) {
+      const int r = rk + i, m = m0 + 16 * wave + 4 * q + r;
+      float v = (acc[j][r] + red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16]) + bv;
+      if (p.add && m < M) v += p.add[(long)m * p.ldo + n];
+      if (m < M) p.out[(long)m * p.ldo + n] = v;
+      ss[i] = 0.f;
+      ss[i] += v * v;
+    }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float sv = group_sum<16>(ss[r]);
-        const int m = m0 + 16 * wave + 4 * q + r;
-        if (l16 == 0 && p.part && m < M) p.part[(long)((c % U) / 16) * M + m] = sv;
-      }
+    for (int i = 0; i < 2; ++i) {
+      const float sv = group_sum<16>(ss[i]);
+      const int m = m0 + 16 * wave + 4 * q + rk + i;
+      if (l16 == 0 && p.part && m < M) p.part[(long)((c % U) / 16) * M + m] = sv;
     }
   }
   SD_TR_END(tr.p, tr.slot)

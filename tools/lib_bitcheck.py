@@ -1,5 +1,5 @@
 """Bit-identity check between two builds of libsdhip.so (A/B aid): computes the split-bf16 conv bwd-weight /
-bwd-data and one scan forward + backward on fixed inputs with the library SDHIP_LIB points at and saves them to
+bwd-data and the fused imagination of the bench agent (random init, seed 0) on fixed inputs with the library SDHIP_LIB points at and saves them to
 argv[1]; `python tools/lib_bitcheck.py cmp a.npz b.npz` reports whether every array is bit-identical."""
 import os
 import sys
@@ -21,6 +21,19 @@ def run(out):
         w = (torch.randn(co, 5, 5, ci, generator=g) / (ci * 25) ** 0.5).cuda()
         res[f"dw_{ci}_{co}"] = K.conv2d_wgrad(x, dy, 5, 5, fast=True).cpu().numpy()
         res[f"dx_{ci}_{co}"] = K.conv2d_dgrad(dy, w, fast=True).cpu().numpy()
+    import bench
+    from sdreamer.config import load_config
+    from sdreamer.dreamer import Dreamer
+    cfg = load_config("dmc/cnn", ["device=cuda:0", "model.compile=False"])
+    torch.manual_seed(0)
+    ag = Dreamer(cfg.model, bench._Spaces({"image": bench._Sp((64, 64, 3))}), bench._Sp((6,)))
+    g = torch.Generator().manual_seed(3)
+    N, S, Kd, D = 1024, ag.rssm._stoch, ag.rssm._discrete, ag.rssm._deter
+    stoch = torch.nn.functional.one_hot(torch.randint(0, Kd, (N, S), generator=g), Kd).float().cuda()
+    deter = (0.5 * torch.randn(N, D, generator=g)).cuda()
+    f, a = ag._imagine_tm((stoch, deter), 16, seed=77, row_offset=0)
+    torch.cuda.synchronize()
+    res["imag_feat"], res["imag_act"] = f.cpu().numpy(), a.cpu().numpy()
     np.savez(out, **res)
 
 
