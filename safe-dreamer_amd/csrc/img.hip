@@ -1196,6 +1196,9 @@ SD_DEV auto gate_b(const __bf16* wg6, int ct, int nkt, const float* Wblk, int Dg
 #ifndef KG_PRE  // k_gate reads _dyn_gru's weight from the once-per-imagination pre-split image (BPre6)
 #define KG_PRE 1
 #endif
+#ifndef KG_HOLDPF  // k_gate loads its GRU epilogue operands before the main loop
+#define KG_HOLDPF 1
+#endif
 #ifndef KG_WAVES  // minimum waves per SIMD for k_gate's register allocation (occupancy; its LDS admits 4 per CU)
 #define KG_WAVES 4
 #endif
@@ -1213,6 +1216,25 @@ __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const floa
   constexpr bool PRE = KG_PRE && KG_1S && F6_GATE;
   using OpB = std::conditional_t<PRE, BPre6<BN>, BRows<BN>>;
   const OpB b0 = gate_b<PRE, BN>(wg6, c0 / 32, Dg / BK6, d.Wg + (long)g * 3 * Dg * Dg, Dg, j0);
+  // the GRU epilogue's operands (old deter, gate biases) loaded before the main loop (KG_HOLDPF), rows clamped: they
+  // arrive with the first k tile instead of as a dependent round trip after the last
+  const Lane L = lane_ids<BN, BN>();
+  const float* bg = d.bg + (long)g * 3 * Dg;
+  float hold_[2][4], bias_[2][3];
+  if (KG_HOLDPF) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = 16 * j + L.l16, jj = j0 + c, col = c0 + c;
+      bias_[j][0] = bg[jj];
+      bias_[j][1] = bg[Dg + jj];
+      bias_[j][2] = bg[2 * Dg + jj];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long m = m0 + L.wr * 16 + 4 * L.q + r;
+        hold_[j][r] = hold[(m < d.N ? m : d.N - 1) * ldf + col];
+      }
+    }
+  }
   f32x4 acc[1][6];
   if constexpr (KG_1S && F6_GATE) {
     ARms<BM> la[KG_PF];
@@ -1227,13 +1249,12 @@ __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const floa
     mainloop<F6_GATE, FP_GATE, BM, BN, 16, BN, pf_of(KG_PF)>(a0, b0, 0, Dg, acc);
   }
   SD_TR(2)
-  const Lane L = lane_ids<BN, BN>();
-  const float* bg = d.bg + (long)g * 3 * Dg;
   float hv_[2][4] = {};
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int c = 16 * j + L.l16, jj = j0 + c, col = c0 + c;
-    const float br = bg[jj], bc = bg[Dg + jj], bu = bg[2 * Dg + jj];
+    const float br = KG_HOLDPF ? bias_[j][0] : bg[jj], bc = KG_HOLDPF ? bias_[j][1] : bg[Dg + jj],
+                bu = KG_HOLDPF ? bias_[j][2] : bg[2 * Dg + jj];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const long m = m0 + L.wr * 16 + 4 * L.q + r;
@@ -1242,7 +1263,7 @@ __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const floa
       const float rs = sigmoidf_(ra);
       const float cc = tanhf(rs * ca);
       const float u = sigmoidf_(ua - 1.f);
-      const float hv = u * cc + (1.f - u) * hold[m * ldf + col];
+      const float hv = u * cc + (1.f - u) * (KG_HOLDPF ? hold_[j][r] : hold[m * ldf + col]);
       hnew[m * ldf + col] = hv;
       hv_[j][r] = hv;
     }
