@@ -328,7 +328,7 @@ SD_DEV Lane lane_ids() {
 // MLP layers, 64 for dyn_hid). WN % PW == 0.
 template <int BM, int BN, int WN, int PW = 32>
 SD_DEV void ep_bias_part(const f32x4 (&acc)[1][WN / 16], const float* bias, float* out, long ldo, float* part, int M,
-                         int m0, int n0, const float* add = nullptr) {
+                         int m0, int n0, const float* add = nullptr, const float* bvals = nullptr) {
   constexpr int TN = WN / 16, TP = PW / 16;
   static_assert(WN % PW == 0, "whole row-partial groups per wave");
   const Lane L = lane_ids<BN, WN>();
@@ -336,7 +336,7 @@ SD_DEV void ep_bias_part(const f32x4 (&acc)[1][WN / 16], const float* bias, floa
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + L.wc * WN + 16 * j + L.l16;
-    const float bv = bias ? bias[n] : 0.f;
+    const float bv = bvals ? bvals[j] : bias ? bias[n] : 0.f;  // (bvals: the bias values, loaded by the caller)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + L.wr * 16 + 4 * L.q + r;
@@ -997,6 +997,9 @@ __global__ __launch_bounds__(256, 2) void k_hid_areg(sd_imagine d, float* hp, fl
   f32x4 acc[1][TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bpre[TN];  // the epilogue's bias values, loaded ahead of the main loop
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bpre[j] = d.bh[n0 + 16 * j + l16];
   constexpr int NS = KH_STAGES;
   load_a(A[0], 0);
   load_b(B[0], 0);
@@ -1043,7 +1046,7 @@ __global__ __launch_bounds__(256, 2) void k_hid_areg(sd_imagine d, float* hp, fl
     __syncthreads();
   }
   SD_TR(2)
-  ep_bias_part<BM, BN, 64, KH_PW>(acc, d.bh, hp, d.D, ph, M, m0, n0);
+  ep_bias_part<BM, BN, 64, KH_PW>(acc, d.bh, hp, d.D, ph, M, m0, n0, nullptr, bpre);
   SD_TR_END(tr.p, tr.slot)
 }
 
@@ -1112,6 +1115,16 @@ __global__ __launch_bounds__(512, 2) void k_lin6_areg(const __bf16* aimg, int K,
   f32x4 acc[NSUB];
 #pragma unroll
   for (int j = 0; j < NSUB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the epilogue's bias values, loaded ahead of the main loop (a problem without a bias reads a valid dummy address,
+  // unconditionally, and takes 0)
+  float bpre[NSUB];
+#pragma unroll
+  for (int j = 0; j < NSUB; ++j) {
+    const int c = c0 + 16 * j, pz = c / U;
+    const float* bp = pz == 0 ? p0.bias : (pz == 1 ? p1.bias : p2.bias);
+    const float bl = (bp ? bp : reinterpret_cast<const float*>(aimg))[c % U + l16];
+    bpre[j] = bp ? bl : 0.f;
+  }
   load_a(A[0], 0);
   load_b(B[0], 0);
   load_a(A[1], 1);
@@ -1162,7 +1175,7 @@ __global__ __launch_bounds__(512, 2) void k_lin6_areg(const __bf16* aimg, int K,
   for (int j = 0; j < NSUB; ++j) {
     const int c = c0 + 16 * j, pz = c / U, n = c % U + l16;
     const LinProb& p = pz == 0 ? p0 : (pz == 1 ? p1 : p2);
-    const float bv = p.bias ? p.bias[n] : 0.f;
+    const float bv = bpre[j];
     float ss[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
