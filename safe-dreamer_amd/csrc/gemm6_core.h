@@ -53,6 +53,19 @@ SD_DEV void split3_store(__bf16* dst, f32x4 v) {
   *reinterpret_cast<bf16x4*>(dst + 2 * BK6) = __builtin_convertvector(l, bf16x4);
 }
 
+// split3_store with non-temporal stores (written for another XCD's next launch: streamed out of this XCD's L2)
+SD_DEV void split3_store_nt(__bf16* dst, f32x4 v) {
+  float h0, h1, h2, h3, m0, m1, m2, m3;
+  const u32x2 h{bf16_pair(v[0], v[1], h0, h1), bf16_pair(v[2], v[3], h2, h3)};
+  const float r0 = v[0] - h0, r1 = v[1] - h1, r2 = v[2] - h2, r3 = v[3] - h3;
+  const u32x2 m{bf16_pair(r0, r1, m0, m1), bf16_pair(r2, r3, m2, m3)};
+  const f32x4 l{r0 - m0, r1 - m1, r2 - m2, r3 - m3};
+  __builtin_nontemporal_store(h, reinterpret_cast<u32x2*>(dst));
+  __builtin_nontemporal_store(m, reinterpret_cast<u32x2*>(dst + BK6));
+  __builtin_nontemporal_store(__builtin_bit_cast(u32x2, __builtin_convertvector(l, bf16x4)),
+                              reinterpret_cast<u32x2*>(dst + 2 * BK6));
+}
+
 template <int N>
 SD_DEV __bf16* sd_smem6() {
   __shared__ __attribute__((aligned(16))) __bf16 s[N];

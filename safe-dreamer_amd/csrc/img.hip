@@ -248,6 +248,17 @@ SD_DEV long pre_off(long row, int col, int K) {
 }
 // 4 consecutive columns (col % 4 == 0) of one row
 SD_DEV void pre_store4(__bf16* img, long row, int col, int K, f32x4 v) { split3_store(img + pre_off(row, col, K), v); }
+SD_DEV void pre_store4_nt(__bf16* img, long row, int col, int K, f32x4 v) {
+  split3_store_nt(img + pre_off(row, col, K), v);
+}
+// IMG_NT (bitmask): step-kernel outputs written with non-temporal stores — 1 = k_gate's fp32 deter (feats; next read
+// a step later), 2 = k_gate's deter image, 4 = k_hid's hp. All three (profiles/r05nt): the next launch's gap shrinks
+// (k_lin 2.8 -> 1.5 us: less dirty L2 to write back at k_gate's end) but its reads of the image slow by more (mma
+// 20.6 -> 23.8 us), step 130.6 -> 135.0 us; the fp32 deter alone (1): update 10.84 vs 10.85 ms, neutral
+// (profiles/r05nt1). Off.
+#ifndef IMG_NT
+#define IMG_NT 0
+#endif
 // the image of a strided (rows, K) fp32 matrix (feats(0)'s deter at the first step)
 __global__ __launch_bounds__(256) void k_presplit_rows(const float* X, long ldx, int rows, int K, __bf16* out) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -328,7 +339,7 @@ SD_DEV Lane lane_ids() {
 // MLP layers, 64 for dyn_hid). WN % PW == 0.
 template <int BM, int BN, int WN, int PW = 32>
 SD_DEV void ep_bias_part(const f32x4 (&acc)[1][WN / 16], const float* bias, float* out, long ldo, float* part, int M,
-                         int m0, int n0, const float* add = nullptr, const float* bvals = nullptr) {
+                         int m0, int n0, const float* add = nullptr, const float* bvals = nullptr, bool nt = false) {
   constexpr int TN = WN / 16, TP = PW / 16;
   static_assert(WN % PW == 0, "whole row-partial groups per wave");
   const Lane L = lane_ids<BN, WN>();
@@ -342,7 +353,12 @@ SD_DEV void ep_bias_part(const f32x4 (&acc)[1][WN / 16], const float* bias, floa
       const int m = m0 + L.wr * 16 + 4 * L.q + r;
       float v = acc[0][j][r] + bv;
       if (add && m < M) v += add[(long)m * ldo + n];
-      if (m < M) out[(long)m * ldo + n] = v;
+      if (m < M) {
+        if (nt)
+          __builtin_nontemporal_store(v, out + (long)m * ldo + n);
+        else
+          out[(long)m * ldo + n] = v;
+      }
       ss[j / TP][r] += v * v;
     }
   }
@@ -1046,7 +1062,7 @@ __global__ __launch_bounds__(256, 2) void k_hid_areg(sd_imagine d, float* hp, fl
     __syncthreads();
   }
   SD_TR(2)
-  ep_bias_part<BM, BN, 64, KH_PW>(acc, d.bh, hp, d.D, ph, M, m0, n0, nullptr, bpre);
+  ep_bias_part<BM, BN, 64, KH_PW>(acc, d.bh, hp, d.D, ph, M, m0, n0, nullptr, bpre, (IMG_NT & 4) != 0);
   SD_TR_END(tr.p, tr.slot)
 }
 
@@ -1277,7 +1293,10 @@ __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const floa
       const float cc = tanhf(rs * ca);
       const float u = sigmoidf_(ua - 1.f);
       const float hv = u * cc + (1.f - u) * (KG_HOLDPF ? hold_[j][r] : hold[m * ldf + col]);
-      hnew[m * ldf + col] = hv;
+      if (IMG_NT & 1)
+        __builtin_nontemporal_store(hv, hnew + m * ldf + col);
+      else
+        hnew[m * ldf + col] = hv;
       hv_[j][r] = hv;
     }
   }
@@ -1292,8 +1311,13 @@ __global__ __launch_bounds__(256, KG_WAVES) void k_gate(sd_imagine d, const floa
     __syncthreads();
     const int row = threadIdx.x >> 2, c8 = (threadIdx.x & 3) * 8;
     if (m0 + row < d.N) {
-      pre_store4(himg, m0 + row, c0 + c8, d.D, *reinterpret_cast<const f32x4*>(T + row * 36 + c8));
-      pre_store4(himg, m0 + row, c0 + c8 + 4, d.D, *reinterpret_cast<const f32x4*>(T + row * 36 + c8 + 4));
+      if (IMG_NT & 2) {
+        pre_store4_nt(himg, m0 + row, c0 + c8, d.D, *reinterpret_cast<const f32x4*>(T + row * 36 + c8));
+        pre_store4_nt(himg, m0 + row, c0 + c8 + 4, d.D, *reinterpret_cast<const f32x4*>(T + row * 36 + c8 + 4));
+      } else {
+        pre_store4(himg, m0 + row, c0 + c8, d.D, *reinterpret_cast<const f32x4*>(T + row * 36 + c8));
+        pre_store4(himg, m0 + row, c0 + c8 + 4, d.D, *reinterpret_cast<const f32x4*>(T + row * 36 + c8 + 4));
+      }
     }
   }
   SD_TR_END(tr.p, tr.slot)
