@@ -203,7 +203,8 @@ struct KC3Rms {
 // BN = 128: 2 x 2 waves of 64 x 64 (2 workgroups per CU). BN = 256 (the heads' 256-column layers): 2 x 2 waves of
 // 64 x 128, one workgroup per CU — each B fragment read from LDS feeds 4 row tiles and each A fragment 8 column tiles,
 // 1.33x the MFMAs per LDS byte of the 64 x 64 wave tile (whose main loop the LDS traffic bounds: MFMA busy ~0.35)
-#ifndef SD_MLP_WIDE  // measured slower on the imagined heads' first layer (335 vs 274 us alone, r04e): off
+#ifndef SD_MLP_WIDE  // measured slower on the imagined heads' first layer (335 vs 274 us alone, r04e), neutral on the
+                     // normed hidden layers once that layer moved to gemm3_w256 (update 10.84 vs 10.84 ms, r05mw): off
 #define SD_MLP_WIDE 0
 #endif
 template <bool RMS, bool POUT, int BN>
