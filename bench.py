@@ -370,9 +370,9 @@ def probe_specs(agent, cfg, K):
     # imagination step kernels
     # k_lin6 (pre-split deter image + weight images, 32-row tiles) unless SDHIP_KL_NOPRE selects the fp32 k_lin
     # (k_lin6_areg — 64 x 48 tiles over the three problems' columns, K split over two halves of a 512-thread
-    # workgroup — at D = 2048, U = 256)
+    # workgroup — at D = 2048 / 4096, U = 256)
     lin6 = not os.environ.get("SDHIP_KL_NOPRE")
-    lareg = lin6 and D == 2048 and U == 256 and not os.environ.get("SDHIP_KL_NOAREG")
+    lareg = lin6 and D in (2048, 4096) and U == 256 and not os.environ.get("SDHIP_KL_NOAREG")
     imag = [("imag_k_lin", "k_lin6_areg" if lareg else "k_lin6<32, 32>" if lin6 else "k_lin<32, 32>",
              (3 * U // 48, N // 64, 1) if lareg else (U // 32, N // 32, 3),
              3 * 2.0 * N * D * U, 4.0 * (N * D + 3 * U * D + 3 * N * U + 2 * (U // 16) * N),

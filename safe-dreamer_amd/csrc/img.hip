@@ -2113,24 +2113,33 @@ static void launch_hid_areg(const sd_imagine& d, const IWork& w, int nkt, const 
 static bool img_lpre(const sd_imagine& d) {
   return KL_PRE && img_apre(d) && d.U % KL3_BN == 0 && d.D % BK6 == 0 && !getenv("SDHIP_KL_NOPRE");
 }
-// k_lin6_areg where it is built (D = 2048: two halves of 32 k tiles, U = 256); SDHIP_KL_NOAREG set: k_lin6 (A/B, and
-// the agreement test). Decides the weight images' column-tile width too (16 here, KL3_BN for k_lin6).
+// k_lin6_areg where it is built (D = 2048 / 4096: two halves of 32 / 64 k tiles, U = 256); SDHIP_KL_NOAREG set:
+// k_lin6 (A/B, and the agreement test). Decides the weight images' column-tile width too (16 here, KL3_BN for k_lin6).
 static bool img_lareg(const sd_imagine& d) {
-  return KL_AREG && img_lpre(d) && d.D == 64 * BK6 && d.U == 256 && !getenv("SDHIP_KL_NOAREG");
+  return KL_AREG && img_lpre(d) && (d.D == 64 * BK6 || d.D == 128 * BK6) && d.U == 256 && !getenv("SDHIP_KL_NOAREG");
 }
 // one k_lin6 / k_lin6_areg launch over nprob (2 or 3) problems sharing A = the deter image
 static void launch_lin6(const sd_imagine& d, const IWork& w, const __bf16* wa, const __bf16* wb, const __bf16* wc,
                         const LinProb& pa, const LinProb& pb, const LinProb& pc, int nprob, Tr tr, hipStream_t st) {
-  if (img_lareg(d))
-    if (nprob == 3 && KL_NSUB == 3 && !getenv("SDHIP_KL_NSUB4"))  // (SDHIP_KL_NSUB4: 64-column tiles, the A/B and test)
-      k_lin6_areg<32, 3><<<dim3(3 * d.U / 48, sd_cdiv(d.N, 64)), 512, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc, d.U,
-                                                                              d.N, tr);
+  if (img_lareg(d)) {
+    const bool n3 = nprob == 3 && KL_NSUB == 3 && !getenv("SDHIP_KL_NSUB4");  // (SDHIP_KL_NSUB4: 64-column tiles)
+    const dim3 grid(n3 ? 3 * d.U / 48 : nprob * d.U / 64, sd_cdiv(d.N, 64));
+#define SD_LIN6A(NKH_)                                                                                          \
+  do {                                                                                                          \
+    if (n3)                                                                                                     \
+      k_lin6_areg<NKH_, 3><<<grid, 512, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc, d.U, d.N, tr);             \
+    else                                                                                                        \
+      k_lin6_areg<NKH_, 4><<<grid, 512, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc, d.U, d.N, tr);             \
+  } while (0)
+    if (d.D == 64 * BK6)
+      SD_LIN6A(32);
     else
-      k_lin6_areg<32, 4><<<dim3(nprob * d.U / 64, sd_cdiv(d.N, 64)), 512, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc,
-                                                                                  d.U, d.N, tr);
-  else
+      SD_LIN6A(64);
+#undef SD_LIN6A
+  } else {
     k_lin6<KL6_BM, KL3_BN><<<dim3(d.U / KL3_BN, sd_cdiv(d.N, KL6_BM), nprob), 256, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb,
                                                                                           pc, d.N, tr);
+  }
 }
 
 // One launch of step t's k_lin / k_lin6 (img_net_0 + _dyn_in0 + actor layer 0's deter part: which = 0), k_hid (1) or
