@@ -216,7 +216,8 @@ SD_DEV void st_row(float* rowp, const f32x4 (&v)[NI], int N, int t32) {
 
 constexpr int KSM = 8;         // max split-K slabs (ks_d, ks_s)
 #ifndef SD_LR_NG
-#define SD_LR_NG 8  // 4: 12.03 / 12.01 ms, 8: 11.98 / 11.95 ms per update (same box, profiles/r03ng_env.txt)
+#define SD_LR_NG 8  // 4: 12.03 / 12.01 ms, 8: 11.98 / 11.95 ms per update (same box, profiles/r03ng_env.txt); again
+                    // on round-5 code, 4: 11.01 vs 8: 10.88 ms (k_logit_rows 6.2 -> 8.2 us, k_hid 6.9 -> 6.7, r05ng)
 #endif
 constexpr int LR_NG = SD_LR_NG;                 // x1p slabs written by k_logit_rows (categorical groups per row)
 constexpr int KS1 = LR_NG > KSM ? LR_NG : KSM;  // max x1p slabs k_hid sums
