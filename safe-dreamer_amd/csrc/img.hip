@@ -1081,22 +1081,25 @@ __global__ __launch_bounds__(256, 2) void k_hid_areg(sd_imagine d, float* hp, fl
 #ifndef KL_AREG
 #define KL_AREG 1
 #endif
+#ifndef KL_KQ  // K parts per workgroup (256 threads each): 2, or 4 (1,024 threads, 4 waves per SIMD: k_lin span 25.6 ->
+#define KL_KQ 2  // 24.7 us but the main loop unchanged at 20.8 us, update 10.82 -> 10.87 ms, profiles/r05kq)
+#endif
 #ifndef KL_NSUB  // 16-column pieces per tile of the three-problem launch
 #define KL_NSUB 3
 #endif
-template <int NKH, int NSUB>
-__global__ __launch_bounds__(512, 2) void k_lin6_areg(const __bf16* aimg, int K, const __bf16* w0, const __bf16* w1,
+template <int NKH, int NSUB, int KQ>
+__global__ __launch_bounds__(256 * KQ, KQ == 4 ? 4 : 2) void k_lin6_areg(const __bf16* aimg, int K, const __bf16* w0, const __bf16* w1,
                                                       const __bf16* w2, LinProb p0, LinProb p1, LinProb p2, int U,
                                                       int M, Tr tr) {
   SD_TR_BEGIN
   constexpr int BM = 64, BN = 16 * NSUB, NS = 2, PPS = 16 * PRE_ROW / 8;  // PPS: 16-B pieces per 16-column piece
   constexpr int STG = BN * LROW6, BP = (NSUB * PPS + 255) / 256;
-  static_assert(BM * (BN + 4) * 4 <= 2 * NS * STG * 2, "reduce buffer within the stages");
-  __bf16* smem = sd_smem6<2 * NS * STG>();
+  static_assert(KQ * BM * (BN + 4) * 4 <= KQ * NS * STG * 2, "reduce buffer within the stages");
+  __bf16* smem = sd_smem6<KQ * NS * STG>();
   int tx = blockIdx.x, ty = blockIdx.y, tz = 0;
   if (KL_XCD) xcd_tile(tx, ty, tz);
   const int c0 = tx * BN, m0 = ty * BM, nkt = K / BK6;
-  const int tid = threadIdx.x, half = tid >> 8, htid = tid & 255, lane = tid & 63, wave = (tid >> 6) & 3;
+  const int tid = threadIdx.x, half = tid >> 8, htid = tid & 255, lane = tid & 63, wave = (tid >> 6) & 3;  // half: K part
   const int l16 = lane & 15, q = lane >> 4;
   SD_TR(1)
   const int kt0 = half * NKH;
@@ -1174,16 +1177,17 @@ __global__ __launch_bounds__(512, 2) void k_lin6_areg(const __bf16* aimg, int K,
     __syncthreads();
   }
   SD_TR(2)
-  // the two halves' sums meet through LDS (the stages are free after the loop's last barrier): half h finishes rows
-  // r = 2h, 2h + 1 of each lane's four (acc[j][r] of both halves added, a + b = b + a), so both run the epilogue
-  constexpr int LDR = BN + 4;
+  // the K parts' sums meet through LDS (the stages are free after the loop's last barrier): part p finishes rows
+  // r = p RPP .. of each lane's four, adding the KQ parts in index order (KQ = 2: a + b = b + a either way), so every
+  // part runs the epilogue
+  constexpr int LDR = BN + 4, RPP = 4 / KQ;
   float* red = reinterpret_cast<float*>(smem);
-  const int rk = 2 * half;  // the rows this half keeps; it hands over the other two
+  const int rk = RPP * half;  // the rows this part keeps; it hands over the others
 #pragma unroll
   for (int j = 0; j < NSUB; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if ((r >> 1) != half) red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16] = acc[j][r];
+      if (r / RPP != half) red[((half * BM) + 16 * wave + 4 * q + r) * LDR + 16 * j + l16] = acc[j][r];
   __syncthreads();
   // ep_bias_part's arithmetic per 16-column piece of its problem: out = acc + bias (+ add), part = the piece's sum
   // of squares (one 16-column group)
@@ -1192,18 +1196,21 @@ __global__ __launch_bounds__(512, 2) void k_lin6_areg(const __bf16* aimg, int K,
     const int c = c0 + 16 * j, pz = c / U, n = c % U + l16;
     const LinProb& p = pz == 0 ? p0 : (pz == 1 ? p1 : p2);
     const float bv = bpre[j];
-    float ss[2];
+    float ss[RPP];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = rk + i, m = m0 + 16 * wave + 4 * q + r;
-      float v = (acc[j][r] + red[(16 * wave + 4 * q + r) * LDR + 16 * j + l16]) + bv;
+    for (int i = 0; i < RPP; ++i) {
+      const int r = rk + i, m = m0 + 16 * wave + 4 * q + r, o = (16 * wave + 4 * q + r) * LDR + 16 * j + l16;
+      float sum = half == 0 ? acc[j][r] : red[o];
+#pragma unroll
+      for (int pp = 1; pp < KQ; ++pp) sum += pp == half ? acc[j][r] : red[pp * BM * LDR + o];
+      float v = sum + bv;
       if (p.add && m < M) v += p.add[(long)m * p.ldo + n];
       if (m < M) p.out[(long)m * p.ldo + n] = v;
       ss[i] = 0.f;
       ss[i] += v * v;
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < RPP; ++i) {
       const float sv = group_sum<16>(ss[i]);
       const int m = m0 + 16 * wave + 4 * q + rk + i;
       if (l16 == 0 && p.part && m < M) p.part[(long)((c % U) / 16) * M + m] = sv;
@@ -2127,14 +2134,14 @@ static void launch_lin6(const sd_imagine& d, const IWork& w, const __bf16* wa, c
 #define SD_LIN6A(NKH_)                                                                                          \
   do {                                                                                                          \
     if (n3)                                                                                                     \
-      k_lin6_areg<NKH_, 3><<<grid, 512, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc, d.U, d.N, tr);             \
+      k_lin6_areg<NKH_, 3, KL_KQ><<<grid, 256 * KL_KQ, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc, d.U, d.N, tr); \
     else                                                                                                        \
-      k_lin6_areg<NKH_, 4><<<grid, 512, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc, d.U, d.N, tr);             \
+      k_lin6_areg<NKH_, 4, KL_KQ><<<grid, 256 * KL_KQ, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb, pc, d.U, d.N, tr); \
   } while (0)
     if (d.D == 64 * BK6)
-      SD_LIN6A(32);
+      SD_LIN6A(64 / KL_KQ);
     else
-      SD_LIN6A(64);
+      SD_LIN6A(128 / KL_KQ);
 #undef SD_LIN6A
   } else {
     k_lin6<KL6_BM, KL3_BN><<<dim3(d.U / KL3_BN, sd_cdiv(d.N, KL6_BM), nprob), 256, 0, st>>>(w.h6, d.D, wa, wb, wc, pa, pb,
