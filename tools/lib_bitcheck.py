@@ -1,5 +1,6 @@
 """Bit-identity check between two builds of libsdhip.so (A/B aid): computes the split-bf16 conv bwd-weight /
-bwd-data and the fused imagination of the bench agent (random init, seed 0) on fixed inputs with the library SDHIP_LIB points at and saves them to
+bwd-data, the fused imagination of the bench agent (random init, seed 0) and the parameters after two eager updates
+of that agent on the bench's synthetic buffer, on fixed inputs, with the library SDHIP_LIB points at, and saves them to
 argv[1]; `python tools/lib_bitcheck.py cmp a.npz b.npz` reports whether every array is bit-identical."""
 import os
 import sys
@@ -34,6 +35,13 @@ def run(out):
     f, a = ag._imagine_tm((stoch, deter), 16, seed=77, row_offset=0)
     torch.cuda.synchronize()
     res["imag_feat"], res["imag_act"] = f.cpu().numpy(), a.cpu().numpy()
+    # two eager updates (scan, encoder, heads, imagination, optimizer) on the bench's synthetic buffer
+    L = int(cfg.batch_length)
+    buf = bench.synth_buffer(cfg, torch.device("cuda", 0), 0, T=max(160, 2 * (L + 1)), A=6, discrete=False)
+    for _ in range(2):
+        ag.update(buf)
+    torch.cuda.synchronize()
+    res["update_params"] = ag._optimizer.arena.data.detach().cpu().numpy()
     np.savez(out, **res)
 
 
