@@ -553,6 +553,9 @@ extern "C" int sd_gemm_bf16x3_wgrad(const sd_gemm_desc* d, float* workspace, lon
 }
 
 namespace {
+#ifndef SD_G3_T128  // 128 x 128 tiles once the launch has this many of them (else 64 x 64). 192 (was 256): the S2
+#define SD_G3_T128 192  // input-gradient GEMMs of the imagined actor / value (240 tiles of 128) on 128 x 128 tiles, one
+#endif              // round of workgroups: update 10.86 -> 10.79 ms over 6 same-box rounds, bit-identical (r05t128*)
 int gemm3_run(const sd_gemm_desc* d, float* workspace, long workspace_floats, float* rowsum, int rs_acc,
               sd_stream stream_) {
   hipStream_t stream = (hipStream_t)stream_;
@@ -578,7 +581,7 @@ int gemm3_run(const sd_gemm_desc* d, float* workspace, long workspace_floats, fl
   const bool ak = d->a_kcontig != 0, bk = d->b_kcontig != 0;
   if (tile != 0 && tile != 1 && tile != 2) {
     const long tiles128 = (long)sd_cdiv(d->M, 128) * sd_cdiv(d->N, 128) * d->batch * ks;
-    tile = tiles128 >= 256 ? 0 : 1;
+    tile = tiles128 >= SD_G3_T128 ? 0 : 1;
     // weight-gradient shape (M <= 256 output rows, long split K, both operands rows-contiguous: dW = dy^T x): one
     // 256-row tile covers every M, so each k chunk of x is read once instead of once per 128-row tile
     if (SD_G3_M256 && !ak && !bk && d->M > 128 && d->M <= 256 && ks > 1 && g.kchunk >= 512 && tile == 0) tile = 2;
