@@ -79,7 +79,8 @@ FAST_GEMM = os.environ.get("SDREAMER_FAST_GEMM", "1") != "0"
 
 # workgroups a long-K split-bf16 GEMM aims for: 512 (2 per CU). Alone the 256 x 2560 x 15360 weight gradient runs
 # faster with more (1024: 157 vs 192 us), but in the update, beside the latency-bound scan backward, 512 measured
-# best (11.70 vs 11.80 ms at 1024, 11.76 at 2048 per update; gpurun_out r04v)
+# best (11.70 vs 11.80 ms at 1024, 11.76 at 2048 per update; gpurun_out r04v); again in round 5 against fewer
+# (10.70 vs 10.74 at 384, 10.86 at 256; profiles/r05wg)
 _G3_WG_TARGET = int(os.environ.get("SDREAMER_G3_WGS", "512"))
 # longest K chunk (rows) a split-bf16 workgroup takes when that needs more splits than the workgroup target — at most
 # twice as many (SDREAMER_G3_CHUNK, off). The atari-like config's 256 x 3072 x 30720 weight gradients go from 10
