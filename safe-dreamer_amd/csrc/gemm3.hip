@@ -14,6 +14,7 @@ using namespace sdb;
 #define SD_G3_FP 0
 #endif
 
+// (re-measured on the round-5 tree: 1 / 2 = 10.84 / 10.81 vs 10.80 ms, profiles/r05d2: off)
 #ifndef SD_G3_D2  // two-deep register prefetch main loop (gemm3_core.h gemm3_mainloop_d2): 1 = 128-row tiles, 2 = all
 #define SD_G3_D2 0
 #endif
