@@ -382,9 +382,10 @@ def probe_specs(agent, cfg, K):
              4.0 * (N * D + 3 * N * U + D * Ig + N * D + N * D // 64), IMAG_LABELS[1], 1),
             ("imag_k_gate", "k_gate", (D // 32, N // 64, 1), 2.0 * N * 3 * D * Dg,
              4.0 * (N * D + 3 * D * Dg + 2 * N * D), IMAG_LABELS[2], 2)]
-    for key, name, grid, work, algo, label, which in imag:  # f32 peak, and (alt) the bf16x6 ceiling they run on
+    for key, name, grid, work, algo, label, which in imag:  # the bf16x6 ceiling they run on (alt: the f32 peak)
+        x6 = not (which == 0 and not lin6)
         add(key, name, grid, "mfma", work, algo, label, ("imag", which), H,
-            alt_peak=None if (which == 0 and not lin6) else PEAK_BF16X6)
+            peak=PEAK_BF16X6 if x6 else None, alt_peak=PEAK_FP32_MFMA if x6 else None)
     # observe-scan forward phases (M = B rows: weight-streaming, bytes-bound)
     scan = [("scan_k_hid", "k_hid<8, 2, true, 16>", (D // 16, 1, 1), 4.0 * (D * Ig + 2 * B * D + (2 + kss + 1) * B * U),
              "scan k_hid (RSSM.observe step: _dyn_hid BlockLinear, M = B rows, 16-column tiles; x0 / x1 RMSNorm + SiLU "
@@ -416,6 +417,79 @@ IMAG_LABELS = {
        "split over two halves); deter fragments "
        "loaded per lane from the pre-split image, weight tiles through LDS; bf16x6)",
 }
+
+
+class FlopCensus:
+    """Counts the algorithmic FLOP of one eager update by the arithmetic that executes them, from the C-ABI calls
+    (registered in _native.PROBES): split-bf16 ("bf16x3") GEMMs / MLP layers / weight gradients / conv bwd-data and
+    bwd-weight, the imagination's three bf16x6 step contractions (k_hid, k_gate, k_lin6 per step), and everything
+    else exact f32. Gives phases.update its precision-weighted ceiling: the time the update's FLOP would take at the
+    peak of the arithmetic each part runs on."""
+
+    X3 = ("sd_gemm_bf16x3_wgrad", "sd_gemm_bf16x3_wgrad2", "sd_gemm_bf16x3_mlp", "sd_conv2d_dgrad_bf16x3",
+          "sd_conv2d_dgrad_direct", "sd_conv2d_wgrad_bf16x3")
+
+    def __init__(self, agent):
+        r = agent.rssm
+        self.D, self.U, self.G = r._deter, r._hidden, r._blocks
+        self.flop = {"f32": 0.0, "bf16x3": 0.0, "bf16x6": 0.0}
+
+    def match(self, name, args):
+        if name.startswith(("sd_gemm", "sd_conv2d", "sd_imagine_run")):
+            self._name = name
+            return True
+        return False
+
+    def begin(self):
+        pass
+
+    def end(self, args):  # after the launch (call_shaped skips it when the entry point declined the shape)
+        self.record(self._name, args)
+
+    def record(self, name, args):
+        if name in ("sd_gemm_f32", "sd_gemm_bf16x3") or name in self.X3[:3]:
+            d = args[0]._obj if hasattr(args[0], "_obj") else None
+            if d is None:
+                return
+            f = 2.0 * d.M * d.N * d.K * d.batch
+            x3 = name != "sd_gemm_f32" and (name != "sd_gemm_bf16x3" or min(d.M, d.N, d.K) >= 64)
+            self.flop["bf16x3" if x3 else "f32"] += f
+        elif name in ("sd_conv2d_fwd_pool", "sd_conv2d_fwd_pool6"):  # (in, w, b, nw, pooled, amax, y, rstd, Nb, ...)
+            Nb, Hs, Ws, Ci, Co, kh, kw = args[8:15]
+            self.flop["bf16x6" if name.endswith("6") else "f32"] += 2.0 * Nb * Hs * Ws * Co * kh * kw * Ci
+        elif name == "sd_conv2d_fwd":  # (in, w, b, out, Nb, Hs, Ws, Ci, Co, kh, kw, pad, ups)
+            Nb, Hs, Ws, Ci, Co, kh, kw, _, ups = args[4:13]
+            self.flop["f32"] += 2.0 * Nb * (Hs << ups) * (Ws << ups) * Co * kh * kw * Ci
+        elif name in ("sd_conv2d_dgrad_bf16x3", "sd_conv2d_dgrad_direct"):  # (dout, w, din, Nb, Hs, Ws, Ci, Co, kh, kw)
+            Nb, Hs, Ws, Ci, Co, kh, kw = args[3:10]
+            self.flop["bf16x3"] += 2.0 * Nb * Hs * Ws * Ci * Co * kh * kw
+        elif name == "sd_conv2d_wgrad_bf16x3":  # (in, dout, dw_db, ws, wsf, Nb, Hs, Ws, Ci, Co, kh, kw, ...)
+            Nb, Hs, Ws, Ci, Co, kh, kw = args[5:12]
+            self.flop["bf16x3"] += 2.0 * Nb * Hs * Ws * Ci * Co * kh * kw
+        elif name == "sd_conv2d_wgrad":  # (in, dout, dw_db, ws, wsf, ksplit, Nb, Hs, Ws, Ci, Co, kh, kw, pad, ups)
+            Nb, Hs, Ws, Ci, Co, kh, kw, _, ups = args[6:15]
+            self.flop["f32"] += 2.0 * Nb * (Hs << ups) * (Ws << ups) * Ci * Co * kh * kw
+        elif name == "sd_conv2d_wgrad_pool":  # (in, dpool, amax, dw_db, ws, wsf, Nb, H, W, Ci, Co, kh, kw, ...)
+            Nb, H_, W_, Ci, Co, kh, kw = args[6:13]
+            self.flop["f32"] += 2.0 * Nb * H_ * W_ * Ci * Co * kh * kw
+        elif name == "sd_imagine_run":  # per img_step: _dyn_hid, _dyn_gru and the three (N, D) x (D, U) contractions
+            import ctypes
+            from sdreamer import _native as nat
+            d = ctypes.cast(args[0], ctypes.POINTER(nat.ImagineDesc)).contents if isinstance(args[0], int) else \
+                args[0]._obj
+            D, U, G = self.D, self.U, self.G
+            Dg = D // G
+            per_step = D * (Dg + 3 * U) + 3 * D * Dg + 3 * D * U
+            self.flop["bf16x6"] += 2.0 * d.N * (d.H1 - 1) * per_step
+
+    def ceiling(self, total):
+        """(ms at the precision-weighted peak, FLOP per class): the f32 class is the reference's counted total minus
+        the split-bf16 classes (the scan, encoder forward, WM-loss contractions, samplers and the imagination's small
+        kernels run exact f32)."""
+        x3, x6 = self.flop["bf16x3"], self.flop["bf16x6"]
+        f32 = max(total - x3 - x6, 0.0)
+        ms = (f32 / (PEAK_FP32_MFMA * 1e12) + x3 / (PEAK_BF16X3 * 1e12) + x6 / (PEAK_BF16X6 * 1e12)) * 1e3
+        return ms, {"f32": f32, "bf16x3": x3, "bf16x6": x6, "census_f32": self.flop["f32"]}
 
 
 def _kernel_is(row_name, name):
@@ -457,8 +531,11 @@ def roofline_entries(specs, agent, cfg, table):
         e = {"key": sp["key"], "kernel": sp["label"], "symbol": sp["name"], "grid": sp["grid"], "bound": sp["bound"],
              "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak, "avg_us": avg_us,
              "work_per_launch": sp["work"], "algorithmic_bytes": sp["algo"], "traffic": None}
-        if sp.get("alt_peak"):  # the ceiling of the arithmetic the kernel executes (bf16x6: 6 bf16 MFMAs per product)
-            e.update(alt_peak=sp["alt_peak"], frac_alt=achieved / sp["alt_peak"])
+        if sp.get("alt_peak"):  # `peak` is the ceiling of the arithmetic the kernel executes (bf16x6: 6 bf16 MFMAs
+            # per f32-equivalent product); alt = the same FLOP against the f32 MFMA peak
+            e.update(alt_peak=sp["alt_peak"], frac_alt=achieved / sp["alt_peak"], alt_is="f32 MFMA peak")
+        e["arith"] = ("bf16x6" if peak == PEAK_BF16X6 else "bf16x3" if peak == PEAK_BF16X3 else
+                      "f32" if sp["bound"] == "mfma" else "bytes")
         row = next(((i, rw) for i, rw in enumerate(rows)
                     if _kernel_is(rw["kernel"], sp["name"]) and rw["grid"] == sp["grid"]), None)
         if row:
@@ -507,7 +584,7 @@ def dominant_probe(K):
                                "N tile = 48)")
 
 
-def phase_rooflines(agent, cfg, cfg_name, ms_update, table=None, reps=10):
+def phase_rooflines(agent, cfg, cfg_name, ms_update, table=None, reps=10, census=None):
     """SURVEY §8(d) 'report separately': (i) the imagination rollout alone (secondary metric N*H / t_rollout; FLOP =
     2 * weights per img_step (Deter + img_net) per imagined latent + 2 * actor weights per actor sample, H img_steps
     and H+1 actor samples per start row), (ii) the observe scan forward (RSSM.observe: bytes = the Deter + obs_net
@@ -560,11 +637,14 @@ def phase_rooflines(agent, cfg, cfg_name, ms_update, table=None, reps=10):
         # dependent launch chain (4 launches per step), so the same time is also given against the measured floor of
         # 4 graph-captured launches per step that each stage <= 32 KB of weights and <= 32 KB of activations
         # (15.8 us per step, tools/hip/persist_scan_proto.hip, profiles/r04_persist_proto.txt)
-        "observe_scan": {"bound": "hbm", "ms": ms_obs, "launches": 4 * L, "work": b_obs,
-                         "achieved": b_obs / (ms_obs * 1e-3) / 1e9, "peak": PEAK_HBM, "unit": "GB/s",
-                         "frac": b_obs / (ms_obs * 1e-3) / 1e9 / PEAK_HBM,
+        "observe_scan": {"bound": "launch latency", "ms": ms_obs, "launches": 4 * L, "work": b_obs,
+                         "us_per_step": ms_obs * 1e3 / L,
                          "skeleton_floor_ms": L * SCAN_SKELETON_US * 1e-3,
                          "frac_of_skeleton_floor": L * SCAN_SKELETON_US * 1e-3 / ms_obs,
+                         # NOT a bound: the weights stream from L2 / MALL and the dependent chain of 4 launches per
+                         # step is what sets the time; the algorithmic weight bytes over the phase time, against HBM
+                         "algorithmic_GBps": b_obs / (ms_obs * 1e-3) / 1e9,
+                         "algorithmic_frac_of_hbm": b_obs / (ms_obs * 1e-3) / 1e9 / PEAK_HBM, "hbm_peak": PEAK_HBM,
                          "what": f"RSSM.observe forward, B={B} L={L}: 4 dependent launches per step; algorithmic bytes "
                                  "= Deter + obs_net weights once per step"},
     }
@@ -591,6 +671,15 @@ def phase_rooflines(agent, cfg, cfg_name, ms_update, table=None, reps=10):
         out["update"] = {"bound": "mfma", "achieved": f_upd / (ms_update * 1e-3) / 1e12, "peak": 157.3,
                          "unit": "TFLOP/s", "frac": f_upd / (ms_update * 1e-3) / 1e12 / 157.3, "work": f_upd,
                          "what": f"whole Dreamer.update, {f_upd / 1e9:.1f} GFLOP fwd+bwd (SURVEY §8(d)) / ms_per_step"}
+        if census is not None and sum(census.flop.values()) > 0:
+            ms_c, cls = census.ceiling(f_upd)
+            out["update"]["precision_weighted"] = {
+                "ceiling_ms": ms_c, "frac": ms_c / ms_update, "flop": cls,
+                "peaks_TFLOPs": {"f32": PEAK_FP32_MFMA, "bf16x3": PEAK_BF16X3, "bf16x6": PEAK_BF16X6},
+                "what": "the update's FLOP at the peak of the arithmetic each part runs on (bench.FlopCensus over one "
+                        "eager update: split-bf16 GEMMs / conv backward at 2.5 PF / 3, the imagination's bf16x6 step "
+                        "contractions at 2.5 PF / 6, the rest of the reference's 927.7 GFLOP at the f32 MFMA peak) "
+                        "over ms_per_step"}
     return out
 
 
@@ -650,8 +739,15 @@ def main():
     # update or graph capture) and re-time that exact launch with HIP events on its stream after the timed steps;
     # the imagination / scan kernels are re-issued through their step entry points
     specs = None if args.no_roofline else probe_specs(agent, cfg, K)
-    for _ in range(args.warmup):
+    census = None
+    if not args.no_roofline and args.warmup > 0:  # FLOP by arithmetic of the first (eager) warm-up update
+        from sdreamer import _native as nat
+        census = FlopCensus(agent)
+        nat.PROBES.append(census)
+    for i in range(args.warmup):
         agent.update(buf)
+        if census is not None and i == 0:
+            nat.PROBES.remove(census)
     trace_mark(1)  # kernel-trace window of the timed steps (tools/kernel_table.py); outside the timed region
     torch.cuda.synchronize()
     if world > 1:
@@ -706,7 +802,16 @@ def main():
         # s_memrealtime): DVFS state of this box while the probes ran
         out["clock_ghz_mfma_load"] = [clk0, clk1]
     if not args.no_roofline:
-        out["phases"] = phase_rooflines(agent, cfg, args.config, ms, table)
+        out["phases"] = phase_rooflines(agent, cfg, args.config, ms, table, census=census)
+        sc = out["phases"]["observe_scan"]
+        # the recurrent scan beside the dominant kernel: what bounds the observe phase (the dependent launch chain),
+        # its time per step against the measured 4-launch floor, and its weight bytes against HBM
+        out["roofline_scan"] = {
+            "bound": "launch latency", "us_per_step": sc["us_per_step"],
+            "floor_us_per_step": SCAN_SKELETON_US, "frac_of_floor": sc["frac_of_skeleton_floor"],
+            "algorithmic_GBps": sc["algorithmic_GBps"], "algorithmic_frac_of_hbm": sc["algorithmic_frac_of_hbm"],
+            "counter_GBps": sc.get("counter_GBps"), "counter_frac_of_hbm": sc.get("counter_frac_of_hbm"),
+            "what": "RSSM.observe forward alone (phases.observe_scan)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if args.config == "dmc/cnn":  # checker legs beside the CPU baseline
             out["parity"] = wm_loss_parity_full()

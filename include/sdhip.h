@@ -59,6 +59,12 @@ int sd_gemm_bf16x3(const sd_gemm_desc* d, float* workspace, long workspace_float
  * after the ksplit * M * N partial slabs. SD_ESHAPE for shapes the split-bf16 kernel does not take (M, N or K < 64). */
 int sd_gemm_bf16x3_wgrad(const sd_gemm_desc* d, float* workspace, long workspace_floats, float* rowsum, int accumulate,
                          sd_stream stream);
+/* The same for two layers' weight gradients over one input (dW = [dy_a | dy_b]^T x, C rows [0, rs_split) the first
+ * layer's, the rest the second's, ldc apart — e.g. the imagined actor's and value head's first layers, whose weights
+ * the arena places back to back, dreamer.py:607,613): the bias gradients of rows >= rs_split go to
+ * rowsum2[m - rs_split]. 0 < rs_split < M. */
+int sd_gemm_bf16x3_wgrad2(const sd_gemm_desc* d, float* workspace, long workspace_floats, float* rowsum,
+                          float* rowsum2, int rs_split, int accumulate, sd_stream stream);
 /* One MLP layer (networks.py:313-336 Linear -> RMSNorm -> SiLU chains) on the split-bf16 core, batched like the GEMM:
  * C[b] = act(rms(A[b]) * norm_w[b]) . B[b] + bias[b] with k-contiguous A (M, K) and B = W^T (W (N, K) row-major),
  * K a multiple of 32, beta 0, no split-K. norm_w null: A used as is. Otherwise rstd(row m) = 1 / sqrt(sum_q
@@ -103,6 +109,11 @@ int sd_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const floa
 int sd_rmsnorm_bwd_ld(const float* x, const float* w, const float* rstd, const float* dy, long ldy, float* dx,
                       float* dw, float* dw_partial, int M, int N, int act, int accumulate_dx, int accumulate_dw,
                       sd_stream stream);
+/* the same with dx rows of stride ldx as well (writes into a column block of a wider gradient: two MLP heads' first
+ * layers on the same input, whose weight gradients are then one sd_gemm_bf16x3_wgrad2 over the joint dy) */
+int sd_rmsnorm_bwd_ldx(const float* x, const float* w, const float* rstd, const float* dy, long ldy, float* dx,
+                       long ldx, float* dw, float* dw_partial, int M, int N, int act, int accumulate_dx,
+                       int accumulate_dw, sd_stream stream);
 /* out[n] (+)= sum_r in[r*ld + n] (fixed-order column sums; bias gradients) */
 int sd_colsum(const float* in, float* out, int R, int N, long ld, int accumulate, sd_stream stream);
 /* two-pass variant for long columns: workspace >= sd_colsum_chunks(R) * N floats */
@@ -397,6 +408,9 @@ int sd_stream_destroy(sd_stream stream);
  * call (the kernels do not use it), so fewer of their workgroups fit on a CU beside the latency-bound chain of the
  * other stream; graph-captured per phase (SDREAMER_FILL_LDS, dreamer.py). Returns the previous value. */
 int sd_set_lds_pad(int bytes);
+/* number of launches that ran without the requested pad because the runtime refused the kernel's dynamic-LDS limit
+ * (each refused kernel is also named once on stderr) */
+int sd_lds_pad_failures(void);
 /* Dreamer.preprocess + ConvEncoder's "-0.5": out = in/255 - shift (dreamer.py:710-713, networks.py:224) */
 int sd_u8_to_f32(const uint8_t* in, float* out, long n, float shift, sd_stream stream);
 /* NHWC channel pad + shift: out[p][c] = in[p][c] - shift (c < C), 0 (C <= c < Cp). The ConvEncoder input

@@ -90,8 +90,10 @@ __global__ __launch_bounds__(256, (BM >= 256 ? 1 : 2)) void gemm3_kernel(GemmArg
         if (m >= g.M) continue;
         if (g.ksplit > 1)
           g.rs_ws[(long)split * g.M + m] = rows[r];
-        else
-          g.rowsum[m] = (g.rs_acc ? g.rowsum[m] : 0.f) + g.alpha * rows[r];
+        else {
+          float* o = rowsum_at(g, m);
+          *o = (g.rs_acc ? *o : 0.f) + g.alpha * rows[r];
+        }
       }
     }
   } else if (SD_G3_FP) {
@@ -508,7 +510,8 @@ extern "C" int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd
   }
   hipStream_t st = (hipStream_t)stream_;
   // long layers without an input norm, one 256-wide entry per tile: the 256 x 256 kernel once it fills the chip
-  if (SD_MLP_W256 && !rms && g.N == 256 && (long)sd_cdiv(g.M, 256) * g.batch >= 192) {
+  // (SDHIP_MLP_NOW256 set: the 128-tile kernel instead, for the agreement test of the two paths)
+  if (SD_MLP_W256 && !rms && g.N == 256 && (long)sd_cdiv(g.M, 256) * g.batch >= 192 && !getenv("SDHIP_MLP_NOW256")) {
     const dim3 grid(sd_cdiv(g.M, 256) * g.batch);
     // (no LDS pad: its 147 KB already hold the CU)
     if (pout) hipLaunchKernelGGL((gemm3_w256_kernel<true>), grid, dim3(512), 0, st, g, e);
@@ -535,7 +538,7 @@ extern "C" int sd_gemm_bf16x3_mlp(const sd_gemm_desc* d, const sd_mlp_ext* x, sd
 
 namespace {
 int gemm3_run(const sd_gemm_desc* d, float* workspace, long workspace_floats, float* rowsum, int rs_acc,
-              sd_stream stream_);
+              sd_stream stream_, int rs_split = 1 << 30, float* rowsum2 = nullptr);
 }
 
 extern "C" int sd_gemm_bf16x3(const sd_gemm_desc* d, float* workspace, long workspace_floats, sd_stream stream_) {
@@ -553,16 +556,27 @@ extern "C" int sd_gemm_bf16x3_wgrad(const sd_gemm_desc* d, float* workspace, lon
   return gemm3_run(d, workspace, workspace_floats, rowsum, accumulate, stream_);
 }
 
+extern "C" int sd_gemm_bf16x3_wgrad2(const sd_gemm_desc* d, float* workspace, long workspace_floats, float* rowsum,
+                                     float* rowsum2, int rs_split, int accumulate, sd_stream stream_) {
+  if (!d || !d->A || !d->B || !d->C || !rowsum || !rowsum2) return SD_EARG;
+  if (d->M <= 0 || d->N <= 0) return SD_OK;
+  if (d->M < 64 || d->N < 64 || d->K < 64 || d->batch != 1 || d->a_kcontig) return SD_ESHAPE;
+  if (rs_split <= 0 || rs_split >= d->M) return SD_ESHAPE;
+  return gemm3_run(d, workspace, workspace_floats, rowsum, accumulate, stream_, rs_split, rowsum2);
+}
+
 namespace {
 #ifndef SD_G3_T128  // 128 x 128 tiles once the launch has this many of them (else 64 x 64). 192 (was 256): the S2
 #define SD_G3_T128 192  // input-gradient GEMMs of the imagined actor / value (240 tiles of 128) on 128 x 128 tiles, one
 #endif              // round of workgroups: update 10.86 -> 10.79 ms over 6 same-box rounds, bit-identical (r05t128*)
 int gemm3_run(const sd_gemm_desc* d, float* workspace, long workspace_floats, float* rowsum, int rs_acc,
-              sd_stream stream_) {
+              sd_stream stream_, int rs_split, float* rowsum2) {
   hipStream_t stream = (hipStream_t)stream_;
   GemmArgs g{};
   g.rowsum = rowsum;
   g.rs_acc = rs_acc;
+  g.rs_split = rs_split;
+  g.rowsum2 = rowsum2;
   g.rs_ws = nullptr;
   g.A = d->A; g.B = d->B; g.C = d->C; g.bias = d->bias; g.ws = workspace;
   g.lda = d->lda; g.ldb = d->ldb; g.ldc = d->ldc;

@@ -25,7 +25,15 @@ struct GemmArgs {
   float* rowsum;
   float* rs_ws;
   int rs_acc;
+  // rows m >= rs_split sum into rowsum2[m - rs_split] (two heads' bias gradients from one weight-gradient GEMM over
+  // their concatenated dy, sd_gemm_bf16x3_wgrad2); rs_split >= M: rowsum only
+  int rs_split;
+  float* rowsum2;
 };
+
+SD_DEV float* rowsum_at(const GemmArgs& g, int m) {
+  return (!g.rowsum2 || m < g.rs_split) ? g.rowsum + m : g.rowsum2 + (m - g.rs_split);
+}
 
 // Load a ROWS x BK tile of an operand into registers (rows = m for A / n for B).
 // KC: k contiguous (row-major in k, `ld` between rows) ; else rows contiguous (`ld` between k's).
@@ -674,7 +682,8 @@ __global__ void gemm_reduce_kernel(GemmArgs g) {
     for (long m = blockIdx.x * (long)blockDim.x + threadIdx.x; m < g.M; m += (long)gridDim.x * blockDim.x) {
       float v = 0.f;
       for (int s = 0; s < g.ksplit; ++s) v += g.rs_ws[(long)s * g.M + m];
-      g.rowsum[m] = (g.rs_acc ? g.rowsum[m] : 0.f) + g.alpha * v;
+      float* o = rowsum_at(g, (int)m);
+      *o = (g.rs_acc ? *o : 0.f) + g.alpha * v;
     }
   }
 }

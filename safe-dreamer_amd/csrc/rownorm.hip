@@ -58,7 +58,7 @@ template <int TEAM, int VPT>
 __global__ __launch_bounds__(256) void rms_bwd(const float* __restrict__ x, const float* __restrict__ w,
                                                const float* __restrict__ rstd, const float* __restrict__ dy,
                                                float* __restrict__ dx, float* __restrict__ dw_part, int M, int N,
-                                               int act, int accumulate_dx, long ldy) {
+                                               int act, int accumulate_dx, long ldy, long ldx) {
   constexpr int TPB = 256 / TEAM;
   __shared__ float red[4];
   __shared__ float wpart[TEAM == 256 ? 1 : TPB * TEAM * VPT];
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void rms_bwd(const float* __restrict__ x, cons
       }
     }
     dot = team_sum<TEAM>(dot, red) / (float)N;
-    float* dxr = dx + row * N;
+    float* dxr = dx + row * ldx;
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
       const int c = t + j * TEAM;
@@ -121,6 +121,100 @@ __global__ __launch_bounds__(256) void rms_bwd(const float* __restrict__ x, cons
       for (int tm = 0; tm < TPB; ++tm) s += wpart[(tm * VPT + j) * TEAM + tt];
       dw_part[(long)blockIdx.x * N + c] = s;
     }
+  }
+}
+
+// Vector forms for rows of N = 256 * NV (the MLPs' 256..1024-wide layers): a wave per row, each lane NV float4 of
+// contiguous columns (lane t: columns 256 j + 4 t .. + 3), so every load / store is one dwordx4 instead of four
+// strided dwords (rms_fwd / rms_bwd above: 1.5 TB/s on the imagined actor / value layers, round-5 kernel table)
+template <int NV>
+__global__ __launch_bounds__(256) void rms_fwd_v(const float* __restrict__ x, const float* __restrict__ w,
+                                                 float* __restrict__ y, float* __restrict__ rstd, int M, float eps,
+                                                 int act, long ldy) {
+  constexpr int N = 256 * NV;
+  const int team = threadIdx.x >> 6, t = threadIdx.x & 63;
+  f32x4 wv[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) wv[j] = *reinterpret_cast<const f32x4*>(w + j * 256 + 4 * t);
+  for (long row = (long)blockIdx.x * 4 + team; row < M; row += (long)gridDim.x * 4) {
+    f32x4 v[NV];
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      v[j] = *reinterpret_cast<const f32x4*>(x + row * N + j * 256 + 4 * t);
+      ss += (v[j][0] * v[j][0] + v[j][1] * v[j][1]) + (v[j][2] * v[j][2] + v[j][3] * v[j][3]);
+    }
+    ss = group_sum<64>(ss);
+    const float r = rsqrtf(ss / (float)N + eps);
+    if (t == 0 && rstd) rstd[row] = r;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float z = v[j][e] * r * wv[j][e];
+        o[e] = act ? siluf_(z) : z;
+      }
+      *reinterpret_cast<f32x4*>(y + row * ldy + j * 256 + 4 * t) = o;
+    }
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void rms_bwd_v(const float* __restrict__ x, const float* __restrict__ w,
+                                                 const float* __restrict__ rstd, const float* __restrict__ dy,
+                                                 float* __restrict__ dx, float* __restrict__ dw_part, int M, int act,
+                                                 int accumulate_dx, long ldy, long ldx) {
+  constexpr int N = 256 * NV;
+  __shared__ f32x4 wpart[4][64 * NV];
+  const int team = threadIdx.x >> 6, t = threadIdx.x & 63;
+  f32x4 wv[NV], dwacc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    wv[j] = *reinterpret_cast<const f32x4*>(w + j * 256 + 4 * t);
+    dwacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (long row = (long)blockIdx.x * 4 + team; row < M; row += (long)gridDim.x * 4) {
+    const float r = rstd[row];
+    f32x4 xh[NV], g[NV];
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + row * N + j * 256 + 4 * t);
+      const f32x4 dv = *reinterpret_cast<const f32x4*>(dy + row * ldy + j * 256 + 4 * t);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xn = xv[e] * r, wn = wv[j][e];
+        float dz = dv[e];
+        if (act) {
+          const float z = xn * wn;
+          const float sg = sigmoidf_(z);
+          dz *= sg * (1.f + z * (1.f - sg));
+        }
+        xh[j][e] = xn;
+        g[j][e] = dz * wn;
+        dwacc[j][e] += dz * xn;
+        dot += g[j][e] * xn;
+      }
+    }
+    dot = group_sum<64>(dot) / (float)N;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      float* q = dx + row * ldx + j * 256 + 4 * t;
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = r * (g[j][e] - xh[j][e] * dot);
+      if (accumulate_dx) o += *reinterpret_cast<const f32x4*>(q);
+      *reinterpret_cast<f32x4*>(q) = o;
+    }
+  }
+  if (!dw_part) return;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) wpart[team][j * 64 + t] = dwacc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * NV; i += 256) {  // float4 i = columns 256 (i / 64) + 4 (i % 64) ..
+    const f32x4 a = (wpart[0][i] + wpart[1][i]) + (wpart[2][i] + wpart[3][i]);
+    *reinterpret_cast<f32x4*>(dw_part + (long)blockIdx.x * N + (i / 64) * 256 + 4 * (i % 64)) = a;
   }
 }
 
@@ -184,6 +278,39 @@ __global__ void colsum_kernel(const float* __restrict__ in, float* __restrict__ 
   }
 }
 
+// short columns (R <= COLSUM_RCH, e.g. the RMSNorm weight-gradient partials of sd_rmsnorm_bwd): 32 columns x 32 row
+// phases per 1024-thread block, so a 512 x 256 partial block is summed by 8 x 1024 threads at 16 loads each instead
+// of 4 x 256 threads at 128 (colsum_kernel: 7 us per launch, round-5 kernel table); fixed order, deterministic
+__global__ __launch_bounds__(1024) void colsum_short(const float* __restrict__ in, float* __restrict__ out, int R,
+                                                     int N, long ld, int accumulate) {
+  const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
+  const int n = blockIdx.x * 32 + cl;
+  __shared__ float red[32][33];
+  __shared__ float red4[4][32];
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    int r = ph;
+    for (; r + 96 < R; r += 128) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] += in[(long)(r + 32 * j) * ld + n];
+    }
+    for (; r < R; r += 32) a[0] += in[(long)r * ld + n];
+  }
+  red[ph][cl] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (ph < 4) {  // 4 x 8 partial rows, then one lane per column adds the 4
+    float s = 0.f;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) s += red[ph * 8 + p][cl];
+    red4[ph][cl] = s;
+  }
+  __syncthreads();
+  if (ph == 0 && n < N) {
+    const float v = (red4[0][cl] + red4[1][cl]) + (red4[2][cl] + red4[3][cl]);
+    out[n] = accumulate ? out[n] + v : v;
+  }
+}
+
 int pick_vpt(int n) {
   if (n <= 1) return 1;
   if (n <= 2) return 2;
@@ -216,6 +343,12 @@ int grid_bwd(int M) {
     default: KERNEL<TEAMV, 16><<<grid, 256, 0, stream>>>(__VA_ARGS__); break;            \
   }
 
+// the vector forms: N = 256, 512 or 1024, every row start 16-B aligned
+bool vec_ok(int N, const void* a, const void* b, const void* c, long ld) {
+  const bool al = (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) & 15) == 0;
+  return al && (N == 256 || N == 512 || N == 1024) && ld % 4 == 0;
+}
+
 int team_for(int N) {
   if (N <= 64) return 16;
   if (N <= 1024) return 64;
@@ -235,6 +368,16 @@ extern "C" int sd_rmsnorm_fwd_ld(const float* x, const float* w, float* y, long 
   if (M <= 0) return SD_OK;
   if (N <= 0 || N > 4096) return SD_ESHAPE;
   const int team = team_for(N);
+  if (vec_ok(N, x, w, y, ldy)) {
+    const int grid = grid_for<64>(M);
+    switch (N / 256) {
+      case 1: rms_fwd_v<1><<<grid, 256, 0, stream>>>(x, w, y, rstd, M, eps, act, ldy); break;
+      case 2: rms_fwd_v<2><<<grid, 256, 0, stream>>>(x, w, y, rstd, M, eps, act, ldy); break;
+      default: rms_fwd_v<4><<<grid, 256, 0, stream>>>(x, w, y, rstd, M, eps, act, ldy); break;
+    }
+    SD_LAUNCH_CHECK();
+    return SD_OK;
+  }
   if (team == 16) { int grid = grid_for<16>(M); SD_RMS_DISPATCH(rms_fwd, 16, x, w, y, rstd, M, N, eps, act, ldy) }
   else if (team == 64) { int grid = grid_for<64>(M); SD_RMS_DISPATCH(rms_fwd, 64, x, w, y, rstd, M, N, eps, act, ldy) }
   else { int grid = grid_for<256>(M); SD_RMS_DISPATCH(rms_fwd, 256, x, w, y, rstd, M, N, eps, act, ldy) }
@@ -256,15 +399,29 @@ extern "C" int sd_rmsnorm_bwd(const float* x, const float* w, const float* rstd,
 extern "C" int sd_rmsnorm_bwd_ld(const float* x, const float* w, const float* rstd, const float* dy, long ldy,
                                  float* dx, float* dw, float* dw_partial, int M, int N, int act, int accumulate_dx,
                                  int accumulate_dw, sd_stream stream_) {
+  return sd_rmsnorm_bwd_ldx(x, w, rstd, dy, ldy, dx, N, dw, dw_partial, M, N, act, accumulate_dx, accumulate_dw,
+                            stream_);
+}
+
+extern "C" int sd_rmsnorm_bwd_ldx(const float* x, const float* w, const float* rstd, const float* dy, long ldy,
+                                  float* dx, long ldx, float* dw, float* dw_partial, int M, int N, int act,
+                                  int accumulate_dx, int accumulate_dw, sd_stream stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   if (M <= 0) return SD_OK;
-  if (N <= 0 || N > 4096) return SD_ESHAPE;
+  if (N <= 0 || N > 4096 || ldx < N || ldy < N) return SD_ESHAPE;
   const int team = team_for(N);
   float* part = dw ? dw_partial : nullptr;
   int grid;
-  if (team == 16) { grid = grid_bwd<16>(M); SD_RMS_DISPATCH(rms_bwd, 16, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx, ldy) }
-  else if (team == 64) { grid = grid_bwd<64>(M); SD_RMS_DISPATCH(rms_bwd, 64, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx, ldy) }
-  else { grid = grid_bwd<256>(M); SD_RMS_DISPATCH(rms_bwd, 256, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx, ldy) }
+  if (vec_ok(N, x, w, dx, ldx) && vec_ok(N, dy, w, dx, ldy)) {
+    grid = grid_bwd<64>(M);
+    switch (N / 256) {
+      case 1: rms_bwd_v<1><<<grid, 256, 0, stream>>>(x, w, rstd, dy, dx, part, M, act, accumulate_dx, ldy, ldx); break;
+      case 2: rms_bwd_v<2><<<grid, 256, 0, stream>>>(x, w, rstd, dy, dx, part, M, act, accumulate_dx, ldy, ldx); break;
+      default: rms_bwd_v<4><<<grid, 256, 0, stream>>>(x, w, rstd, dy, dx, part, M, act, accumulate_dx, ldy, ldx); break;
+    }
+  } else if (team == 16) { grid = grid_bwd<16>(M); SD_RMS_DISPATCH(rms_bwd, 16, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx, ldy, ldx) }
+  else if (team == 64) { grid = grid_bwd<64>(M); SD_RMS_DISPATCH(rms_bwd, 64, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx, ldy, ldx) }
+  else { grid = grid_bwd<256>(M); SD_RMS_DISPATCH(rms_bwd, 256, x, w, rstd, dy, dx, part, M, N, act, accumulate_dx, ldy, ldx) }
   SD_LAUNCH_CHECK();
   if (dw) return sd_colsum_ws(dw_partial, dw, grid, N, N, accumulate_dw, nullptr, stream_);
   return SD_OK;
@@ -278,6 +435,11 @@ extern "C" int sd_colsum_ws(const float* in, float* out, int R, int N, long ld, 
   hipStream_t stream = (hipStream_t)stream_;
   if (N <= 0) return SD_OK;
   const int chunks = (R + COLSUM_RCH - 1) / COLSUM_RCH;
+  if (chunks <= 1 && N <= 4096) {
+    colsum_short<<<(N + 31) / 32, 1024, 0, stream>>>(in, out, R, N, ld, accumulate);
+    SD_LAUNCH_CHECK();
+    return SD_OK;
+  }
   if (chunks <= 1 || !workspace) {
     colsum_kernel<<<(N + 63) / 64, 256, 0, stream>>>(in, out, R, N, ld, accumulate);
     SD_LAUNCH_CHECK();

@@ -31,7 +31,8 @@ from . import _native as nat
 from . import kernels as K
 from . import ops
 from . import parallel
-from .networks import Linear, MLPHead, MultiDecoder, MultiEncoder, Projector, ReturnEMA, heads_nograd
+from .networks import (Linear, MLPHead, MultiDecoder, MultiEncoder, Projector, ReturnEMA, heads_nograd,
+                       pair_forward_from_first)
 from .optim import LaProp, WarmupSchedule
 from .rssm import RSSM, STREAM_ACT, STREAM_IMG, STREAM_OBS_AUG, STREAM_POLICY, STREAM_POLICY_ACT
 
@@ -69,6 +70,9 @@ FILL_CUS = os.environ.get("SDREAMER_FILL_CUS", "")
 # trajectories' large (H*N)-row GEMMs) are queued and run at the start of S3, beside the encoder backward, instead of
 # beside the scan backward (M2a, the latency-bound chain S2 slows)
 AC_DEFER = os.environ.get("SDREAMER_AC_DEFER", "0") == "1"
+# the imagined actor's and value head's first-layer weight gradients as ONE split-bf16 GEMM over their joint dy: the
+# 157 MB imagined-feature operand read once instead of twice (ops.PairFirstFn). 0 = one per head
+PAIR_FIRST = os.environ.get("SDREAMER_PAIR_FIRST", "1") != "0"
 # KB of dynamic LDS every GEMM launch of the filler phases (M1, S2, S3, S4) reserves without using it (sd_set_lds_pad):
 # fewer filler workgroups fit on a CU, leaving LDS for the latency-bound chain's workgroups beside them (0 = off)
 FILL_LDS = int(os.environ.get("SDREAMER_FILL_LDS", "0"))
@@ -215,7 +219,7 @@ class Dreamer(nn.Module):
         self._optimizer = LaProp(self._named_params.values(), lr=float(config.lr),
                                  betas=(float(config.beta1), float(config.beta2)), eps=float(config.eps),
                                  agc=float(config.agc), pmin=float(config.pmin), warmup=int(config.warmup or 0),
-                                 ref_layouts=self._ref_layouts)
+                                 ref_layouts=self._ref_layouts, order=self._arena_order())
         self._scheduler = WarmupSchedule(self._optimizer)
         # slow critic arena mirrors the value head's slice of the parameter arena (one Polyak kernel)
         a = self._optimizer.arena
@@ -475,6 +479,28 @@ class Dreamer(nn.Module):
         self._updates += 1
         return post, mets
 
+    def _arena_order(self):
+        """Physical order of the parameter arena: the named order, except that the actor's first linear weight closes
+        the actor's block, so that it sits right before the value head's first linear weight (the value block's first
+        tensor, kept contiguous for the slow critic's Polyak mirror): the two imagined heads' first-layer weight
+        gradients are then one (2U, F) matrix that a single GEMM over their joint dy writes (ops.PairFirstFn)."""
+        names = list(self._named_params)
+        prms = list(self._named_params.values())
+        idx = {id(p): i for i, p in enumerate(prms)}
+        order = list(range(len(names)))
+        self._pair_first = False
+        if not (PAIR_FIRST and self.actor.mlp.n >= 1 and self.value.mlp.n >= 1):
+            return order
+        ia = idx.get(id(self.actor.mlp._mods[0][0].weight))
+        iv = idx.get(id(self.value.mlp._mods[0][0].weight))
+        act = [i for i, n in enumerate(names) if n.startswith("actor.")]
+        if ia is not None and iv is not None and act and iv == act[-1] + 1 and \
+                act == list(range(act[0], act[-1] + 1)) and prms[ia].shape == prms[iv].shape:
+            order = [i for i in order if i != ia]
+            order.insert(order.index(act[-1]) + 1, ia)
+            self._pair_first = True
+        return order
+
     def _grad_buckets(self):
         """Data parallel: the gradient arena split into all-reduce buckets by the phase after which each parameter's
         gradient is final (_update_graphed), as merged contiguous arena ranges:
@@ -489,12 +515,15 @@ class Dreamer(nn.Module):
         for name, prm in self._named_params.items():
             i = pos[id(prm)]
             b = group.get(name.split(".")[0], "heads")
-            lo, hi = a.offsets[i], (a.offsets[i + 1] if i + 1 < len(a.offsets) else a.total)
-            rng = out[b]
-            if rng and rng[-1][1] == lo:
-                rng[-1] = (rng[-1][0], hi)
-            else:
-                rng.append((lo, hi))
+            out[b].append((a.offsets[i], a.offsets[i] + a.padded[i]))
+        for b, rs in out.items():  # merged contiguous ranges (the arena's physical order need not be the named one)
+            merged = []
+            for lo, hi in sorted(rs):
+                if merged and merged[-1][1] == lo:
+                    merged[-1] = (merged[-1][0], hi)
+                else:
+                    merged.append((lo, hi))
+            out[b] = merged
         return out
 
     def _allreduce_bucket(self, name, *events):
@@ -1142,11 +1171,13 @@ class Dreamer(nn.Module):
         every posterior step (the loss reads its first T - 1 in place: no copy of feat[:, :-1], no slice backward)."""
         B, T = data["action"].shape[:2]
         N = B * T
+        vd = self.value(feat_r)
         with torch.no_grad():
             fd = feat_r.detach().reshape(N, -1)
-            value = K.twohot_mode(self.value.logits_nograd(fd), self.vbins).view(B, T)
+            # _frozen_value aliases value (dreamer.py:642 vs 648): its mode is read off the logits the loss's forward
+            # computes anyway (same f32 kernels, so the same values), not from a second forward of the head
+            value = K.twohot_mode(vd.detach().reshape(N, -1), self.vbins).view(B, T)
             slow_value = K.twohot_mode(self._slow_value.logits_nograd(fd), self.vbins).view(B, T)
-        vd = self.value(feat_r)
         last, term, _ = flags if flags is not None else self._episode_flags(data)
         reward = data["reward"].float().reshape(B, T)
         return dict(value=value, slow_value=slow_value, vd=vd, last=last, term=term,
@@ -1206,8 +1237,16 @@ class Dreamer(nn.Module):
         H = H1 - 1
         ret, weight, i_slow = rr["ret"], rr["weight"], rr["i_slow"]
         xh = ifeat[:H].reshape(H * N, -1)
-        a_h0 = rr.get("act_h0")
-        if a_h0 is not None:  # layer 0 from the imagination (fp32), layers 1.. and the output on split-bf16
+        a_h0, v_h0 = rr.get("act_h0"), rr.get("val_h0")
+        pair = None
+        if self._pair_first and a_h0 is not None and v_h0 is not None:
+            # both first layers given (the actor's from the imagination, the value head's from the imagined heads):
+            # their weight gradients are one GEMM over the joint dy (ops.PairFirstFn)
+            pair = pair_forward_from_first(self.actor, self.value, xh, a_h0[:H].reshape(H * N, -1), v_h0[:H * N],
+                                           fast=True)
+        if pair is not None:
+            pl, vl = pair
+        elif a_h0 is not None:  # layer 0 from the imagination (fp32), layers 1.. and the output on split-bf16
             pl = self.actor.forward_from_first(xh, a_h0[:H].reshape(H * N, -1), fast=True)
         else:
             pl = self.actor(xh, fast=True)
@@ -1218,11 +1257,11 @@ class Dreamer(nn.Module):
             d = self.config.actor.dist
             logpi, ent = ops.BNormalLogProbEntFn.apply(pl, iact[:H].reshape(H * N, -1), float(d.min_std),
                                                         float(d.max_std))
-        v_h0 = rr.get("val_h0")
-        if v_h0 is not None:  # layer 0 from the imagined heads' batched launch (its first H * N rows)
-            vl = self.value.forward_from_first(xh, v_h0[:H * N], fast=True)
-        else:
-            vl = self.value(xh, fast=True)
+        if pair is None:
+            if v_h0 is not None:  # layer 0 from the imagined heads' batched launch (its first H * N rows)
+                vl = self.value.forward_from_first(xh, v_h0[:H * N], fast=True)
+            else:
+                vl = self.value(xh, fast=True)
         # policy (dreamer.py:653-660) and value (661-671) losses and the advantage (628-636): one launch each way
         total, losses["policy"], losses["value"], adv = ops.ImagACLossFn.apply(
             vl, logpi, ent, self.vbins, ret, i_slow[:H], weight, rr["i_val"], rr["ret_scale"], self.act_entropy,

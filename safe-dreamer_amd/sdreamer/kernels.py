@@ -178,6 +178,34 @@ def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1, fast=F
     return out
 
 
+def wgrad2(dy, x, dw, db_a, db_b, split):
+    """Two linear layers' weight gradients over one input x in one split-bf16 GEMM: dw (Oa + Ob, I) += dy^T x with
+    dy (R, Oa + Ob) their joint output gradient and dw a view over both weight gradients back to back; the bias
+    gradients of rows < split go to db_a, the rest to db_b (sd_gemm_bf16x3_wgrad2). Returns False (nothing launched)
+    for shapes outside the split-bf16 kernel (M, N or K < 64): the caller then runs per-layer wgrad()."""
+    a = dy.t()
+    M, Kk = a.shape
+    Nn = x.shape[1]
+    _chk(a, x, dw, db_a, db_b)
+    if not (dw.is_contiguous() and db_a.is_contiguous() and db_b.is_contiguous() and tuple(dw.shape) == (M, Nn)
+            and x.shape[0] == Kk and 0 < split < M and db_a.numel() == split and db_b.numel() == M - split):
+        raise ValueError(f"wgrad2 shapes dy {tuple(dy.shape)} x {tuple(x.shape)} dw {tuple(dw.shape)} split {split}")
+    ak, lda = _layout(a, 0, 1)
+    bk, ldb = _layout(x, 1, 0)
+    ksplit = _fast_split(M, Nn, Kk, 1)
+    d = nat.GemmDesc()
+    d.A, d.B, d.C, d.bias = p(a), p(x), p(dw), None
+    d.lda, d.ldb, d.ldc = lda, ldb, Nn
+    d.strideA = d.strideB = d.strideC = d.strideBias = 0
+    d.M, d.N, d.K, d.batch = M, Nn, Kk, 1
+    d.a_kcontig, d.b_kcontig = int(ak), int(bk)
+    d.ksplit, d.tile = int(ksplit), -1
+    d.alpha, d.beta = 1.0, 1.0
+    ws = torch.empty(ksplit * M * Nn + ksplit * M, dtype=torch.float32, device=dw.device) if ksplit > 1 else None
+    return nat.call_shaped("sd_gemm_bf16x3_wgrad2", ctypes.byref(d), p(ws), ws.numel() if ws is not None else 0,
+                           p(db_a), p(db_b), int(split), 1, stream())
+
+
 def wgrad(dy, x, dw, db=None):
     """nn.Linear backward's parameter gradients on the split-bf16 path: dw += dy^T x, db += column sums of dy (in the
     same launch when the shape allows, else a separate column-sum launch). dy (R, O), x (R, I), dw (O, I)."""
@@ -307,11 +335,17 @@ def rmsnorm_bwd(x, w, rstd, dy, act=1, dx=None, dw=None, accumulate_dx=False, ac
     else:
         dy, ldy = _c(dy), N
     dx = torch.empty_like(x) if dx is None else dx
+    if dx.is_contiguous():
+        ldx = N
+    elif dx.dim() == 2 and dx.shape == (M, N) and dx.stride(1) == 1:
+        ldx = dx.stride(0)  # a column block of a wider gradient buffer (ops.PairFirstFn)
+    else:
+        raise ValueError(f"rmsnorm_bwd dx needs unit column stride, got {tuple(dx.stride())}")
     part = None
     if dw is not None:
         nb = nat.fns["sd_rmsnorm_bwd_blocks"](M, N)
         part = torch.empty(nb * N, dtype=torch.float32, device=x.device)
-    nat.call("sd_rmsnorm_bwd_ld", p(x), p(w), p(rstd), p(dy), ldy, p(dx), p(dw), p(part), M, N, int(act),
+    nat.call("sd_rmsnorm_bwd_ldx", p(x), p(w), p(rstd), p(dy), ldy, p(dx), ldx, p(dw), p(part), M, N, int(act),
              int(accumulate_dx), int(accumulate_dw), stream())
     return dx
 

@@ -191,6 +191,12 @@ class MLPHead(nn.Module):
             return self.forward(x, fast)
         return ops.linear(self.mlp.forward_from_first(x, h0, fast), self.last.weight, self.last.bias, fast)
 
+    def logits_rest(self, h, fast=False):
+        """logits given the first layer's normalised, activated output h (ops.PairFirstFn)"""
+        for lin, norm in self.mlp._mods[1:]:
+            h = ops.rms_silu(ops.linear(h, lin.weight, lin.bias, fast), norm.weight)
+        return ops.linear(h, self.last.weight, self.last.bias, fast)
+
     @torch.no_grad()
     def logits_nograd(self, x, fast=False):
         h = self.mlp.forward_nograd(x.reshape(-1, x.shape[-1]), fast)
@@ -204,6 +210,18 @@ class MLPHead(nn.Module):
         for lin, norm in rest:
             h = K.rmsnorm_fwd(K.linear(h, lin.weight, lin.bias, fast=fast), norm.weight, act=1)[0]
         return K.linear(h, self.last.weight, self.last.bias, fast=fast)
+
+
+def pair_forward_from_first(ha, hb, x, h0a, h0b, fast=False):
+    """Logits of two MLPHeads on the same detached rows x whose first linear outputs h0a / h0b are given; their first
+    layers' backward is one joint weight-gradient GEMM (ops.PairFirstFn). None when the heads do not qualify."""
+    if ha.mlp._symlog_inputs or hb.mlp._symlog_inputs or ha.mlp.n < 1 or hb.mlp.n < 1:
+        return None
+    (la, na), (lb, nb) = ha.mlp._mods[0], hb.mlp._mods[0]
+    if la.bias is None or lb.bias is None or la.weight.shape[1] != lb.weight.shape[1]:
+        return None
+    ya, yb = ops.PairFirstFn.apply(h0a, h0b, x, la.weight, la.bias, na.weight, lb.weight, lb.bias, nb.weight)
+    return ha.logits_rest(ya, fast), hb.logits_rest(yb, fast)
 
 
 FUSED_HEADS = os.environ.get("SDREAMER_FUSED_HEADS", "1") != "0"

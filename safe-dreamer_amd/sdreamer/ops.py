@@ -147,6 +147,50 @@ class LinearPreFn(torch.autograd.Function):
         return None, None, None, None
 
 
+class PairFirstFn(torch.autograd.Function):
+    """The first layer (Linear -> RMSNorm -> SiLU) of two MLPs on the same detached input x whose linear outputs
+    h0a, h0b were computed elsewhere: the imagined actor's (the imagination's fp32 layer 0) and the value head's (the
+    imagined heads' batched first layer), dreamer.py:607,613. Forward = the two norms (as RmsSiluFn). Backward: both
+    norms' input gradients into the two column blocks of one (R, Ua + Ub) buffer, then ONE split-bf16 weight-gradient
+    GEMM over it (sd_gemm_bf16x3_wgrad2) — x (H*N x feat, 157 MB at the bench config) is read once instead of once per
+    head, and its K chunks are twice as long. The two weight gradients must lie back to back (Dreamer._arena_order);
+    otherwise two GEMMs over the buffer's column blocks."""
+
+    @staticmethod
+    def forward(ctx, h0a, h0b, x, wa, ba, na, wb, bb, nb):
+        h0a, h0b = h0a.contiguous(), h0b.contiguous()
+        ya, ra = k.rmsnorm_fwd(h0a, na, act=1)
+        yb, rb = k.rmsnorm_fwd(h0b, nb, act=1)
+        ctx.save_for_backward(h0a, h0b, ra, rb, _flat(x).contiguous(), wa, ba, na, wb, bb, nb)
+        return ya, yb
+
+    @staticmethod
+    def backward(ctx, dya, dyb):
+        h0a, h0b, ra, rb, x2, wa, ba, na, wb, bb, nb = ctx.saved_tensors
+        R, Ua = h0a.shape
+        Ub = h0b.shape[1]
+        buf = torch.empty(R, Ua + Ub, dtype=torch.float32, device=h0a.device)
+        for h0, nw, r, dy, cols in ((h0a, na, ra, dya, slice(0, Ua)), (h0b, nb, rb, dyb, slice(Ua, Ua + Ub))):
+            if dy is None:
+                buf[:, cols].zero_()
+            else:
+                k.rmsnorm_bwd(h0, nw, r, dy, act=1, dx=buf[:, cols], dw=grad_buf(nw) if nw.requires_grad else None)
+
+        def wgrad():
+            ga, gb = grad_buf(wa), grad_buf(wb)
+            if not (gb.data_ptr() == ga.data_ptr() + ga.numel() * ga.element_size() and ga.is_contiguous() and
+                    gb.is_contiguous() and k.wgrad2(buf, x2, ga.as_strided((Ua + Ub, ga.shape[1]), (ga.shape[1], 1)),
+                                                    grad_buf(ba), grad_buf(bb), Ua) is not False):
+                k.wgrad(buf[:, :Ua], x2, ga, grad_buf(ba))
+                k.wgrad(buf[:, Ua:], x2, gb, grad_buf(bb))
+
+        if _DEFER is not None:
+            _DEFER.append((wgrad, (buf, x2)))
+        else:
+            wgrad()
+        return (None,) * 9
+
+
 class RmsSiluFn(torch.autograd.Function):
     """nn.RMSNorm(eps=1e-4) followed by SiLU (act=1) or nothing (act=0)."""
 

@@ -20,14 +20,22 @@ CHUNK = 16384  # elements per optimiser block (one 256-thread workgroup streams 
 
 
 class FlatArena:
-    def __init__(self, params, device):
+    """order: optional physical placement (a permutation of the parameter indices); tensor i stays index i for the
+    optimizer state, the chunk tables and the checkpoint, only its offset follows the order. Used to put two layers
+    whose weight gradients one GEMM writes back to back (the imagined actor's and value head's first layers)."""
+
+    def __init__(self, params, device, order=None):
         self.params = list(params)
         self.sizes = [p.numel() for p in self.params]
-        self.offsets = []
+        order = list(range(len(self.params))) if order is None else list(order)
+        if sorted(order) != list(range(len(self.params))):
+            raise ValueError("FlatArena order must be a permutation of the parameter indices")
+        self.offsets = [0] * len(self.params)
+        self.padded = [(n + 63) // 64 * 64 for n in self.sizes]  # 256-B aligned starts: float4-friendly views
         off = 0
-        for n in self.sizes:
-            self.offsets.append(off)
-            off += (n + 63) // 64 * 64  # 256-B aligned starts: float4-friendly views
+        for i in order:
+            self.offsets[i] = off
+            off += self.padded[i]
         self.total = off
         self.data = torch.zeros(self.total, dtype=torch.float32, device=device)
         self.grad = torch.zeros(self.total, dtype=torch.float32, device=device)
@@ -67,7 +75,7 @@ class LaProp(torch.optim.Optimizer):
     fused with clip_grad_agc_ and the LambdaLR warm-up of Dreamer (dreamer.py:209-225)."""
 
     def __init__(self, params, lr=4e-4, betas=(0.9, 0.999), eps=1e-15, agc=0.3, pmin=1e-3, warmup=0, arena=None,
-                 ref_layouts=None):
+                 ref_layouts=None, order=None):
         params = list(params)
         # per parameter: None, or (to_ref, from_ref) views between the internal and the reference layout, so that
         # state_dict() holds moments shaped like the reference's parameters (checkpoint interop)
@@ -80,7 +88,7 @@ class LaProp(torch.optim.Optimizer):
         # needs no zero_grad launch at its start
         self.zero_grads_after = False
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False, centered=False))
-        self.arena = arena if arena is not None else FlatArena(params, params[0].device)
+        self.arena = arena if arena is not None else FlatArena(params, params[0].device, order)
         dev = self.arena.data.device
         self.exp_avg = torch.zeros_like(self.arena.data)
         self.exp_avg_sq = torch.zeros_like(self.arena.data)

@@ -537,9 +537,12 @@ class ObserveScan(torch.autograd.Function):
             if gs2.stride(-1) == 1 and gd2.stride(-1) == 1 and gs2.stride(-2) == gd2.stride(-2) and \
                     gs2.stride(-3) == T * gs2.stride(-2) and gd2.stride(-3) == T * gd2.stride(-2):
                 d.d_stoch2, d.d_deter2, d.ld_g2 = gs2.data_ptr(), gd2.data_ptr(), gs2.stride(-2)
-            else:  # never reached on the benched path (DxSink's halves are strided views of one (B, T, F) buffer)
-                raise RuntimeError("ObserveScan: extra posterior gradients must be (B, T, .) views with unit column "
-                                   "stride and a common row stride")
+            else:  # (not the benched path: DxSink's halves are strided views of one (B, T, F) buffer) both halves
+                # copied into one (B, T, SK + D) buffer, whose two column blocks share a row stride; kept on ctx until
+                # the backward's launches have run
+                g2 = torch.cat([gs2.reshape(B, T, -1), gd2.reshape(B, T, -1)], -1)
+                ctx.g2_hold = g2
+                d.d_stoch2, d.d_deter2, d.ld_g2 = g2.data_ptr(), g2[..., SK:].data_ptr(), g2.stride(1)
         nat.call("sd_rssm_scan_bwd", ctypes.addressof(d), K.stream())
         gb = ops.grad_buf
         f = lambda x: x.reshape(M, -1)  # noqa: E731

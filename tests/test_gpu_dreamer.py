@@ -344,3 +344,74 @@ def test_weight_init_matches_reference(name):
         if amax > max(2 * sigma * (1 + 4 / np.sqrt(n)), amax_r) * 1.001 or amax < 0.5 * amax_r:
             bad.append((k, "max", amax, amax_r))
     assert not bad, bad
+
+
+def test_pair_first_matches_per_head():
+    """ops.PairFirstFn (the imagined actor's and value head's first-layer weight gradients as one GEMM over their
+    joint dy, their weights back to back in the arena) against the per-head path on the same agent, at the bench's
+    full C2 size (H * N = 15,360 rows: the joint GEMM runs; at the golden sizes it falls back to per-head GEMMs): every
+    gradient outside those two layers' weights / biases bit-identical, those within the split-bf16 bound."""
+    from fullsize_io import FULL, OVERRIDES, PARAM_SEED, SEED, full_inputs
+    from oracle.init import params_for
+    from oracle.ref_cpu import Spec
+    from sdreamer.dreamer import Dreamer
+    name = "C2_walker_r2"
+    cfg_name, ovr, obs, A, discrete, B, L, H = FULL[name]
+    gcfg = load_config(cfg_name, ["device=cuda:0"] + ovr + OVERRIDES)
+    spec = Spec(gcfg.model, obs, A, discrete)
+    ag = Dreamer(copy.deepcopy(gcfg.model), _Spaces({k: _Sp(v) for k, v in obs.items()}), _Sp((A,)))
+    sd = {k: torch.from_numpy(v) for k, v in params_for(spec.shapes, PARAM_SEED).items()}
+    ag.load_state_dict(sd, strict=False)
+    assert ag._pair_first
+    ag.use_graphs = False
+    data_np, init_np = full_inputs(name, spec.K, spec.S, spec.D)
+    data = ag.preprocess({k: torch.from_numpy(v).cuda() for k, v in data_np.items()})
+    init = tuple(torch.from_numpy(v).cuda() for v in init_np)
+    ag._update_slow_target()
+    grads = []
+    for pair in (True, False):
+        ag._pair_first = pair
+        ag._optimizer.zero_grad()
+        ag._cal_grad(data, init, SEED, 0)
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.detach().clone() for n, p in ag._named_params.items()})
+    first = {id(ag.actor.mlp._mods[0][0].weight), id(ag.actor.mlp._mods[0][0].bias),
+             id(ag.value.mlp._mods[0][0].weight), id(ag.value.mlp._mods[0][0].bias)}
+    checked = 0
+    for n, p in ag._named_params.items():
+        a, b = grads[0][n], grads[1][n]
+        if id(p) in first:
+            scale = float(b.abs().max())
+            assert float((a - b).abs().max()) <= 2e-3 * scale + 1e-12, (n, float((a - b).abs().max()), scale)
+            checked += 1
+        else:
+            assert torch.equal(a, b), n
+    assert checked == 4
+
+
+def test_side_prep_graph_matches_eager(monkeypatch):
+    """The S0 side phase (SDREAMER_SIDE_PREP=2: the imagination's noise / weight images and the backward's weight
+    layouts beside the encoder forward) and the filler LDS pad (SDREAMER_FILL_LDS) only move work between streams /
+    change occupancy: graph replays equal the eager updates exactly (cf. test_graph_replay_matches_eager)."""
+    import sdreamer.dreamer as D
+    monkeypatch.setattr(D, "SIDE_PREP", 2)
+    monkeypatch.setattr(D, "FILL_LDS", 32)
+    runs = []
+    for graphs in (False, True):
+        ag, z, spec, obs = build_agent("walker_r2")
+        ag.use_graphs = graphs
+        out = []
+        for u in range(4):
+            (ps, pd), mets = ag.update_batch(batch(z, u % 2, obs, DEV), initial(z, u % 2, spec, DEV), 700 + u)
+            out.append((float(mets["loss/dyn"]), float(mets["loss/value"]), float(mets["opt/loss"]),
+                        pd.detach().clone()))
+        sd = ag.state_dict()
+        out.append(torch.cat([sd[k].reshape(-1) for k in spec.shapes]).clone())
+        runs.append(out)
+    e, g = runs
+    for u in range(4):
+        assert e[u][:3] == g[u][:3], (u, e[u][:3], g[u][:3])
+        assert torch.equal(e[u][3], g[u][3])
+    assert torch.equal(e[4], g[4])
+    from sdreamer import _native as nat
+    assert nat.fns["sd_lds_pad_failures"]() == 0  # every padded filler launch got its pad

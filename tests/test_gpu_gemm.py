@@ -1,4 +1,6 @@
 """GEMM kernel (sd_gemm_f32) vs torch fp32 reference, all operand layouts, batching, split-K, bias/beta."""
+import os
+
 import pytest
 import torch
 
@@ -220,3 +222,52 @@ def test_gemm_bf16x3_mlp_entries(rms, wide):
     assert torch.equal(got, ref)
     for j, r in enumerate(rows):
         assert not got[j, :, r:].any()
+
+
+def test_heads_w256_matches_128_tiles():
+    """The imagined heads at the bench's row count (H1 * N = 16 * 1024): their first layer takes the 256 x 256-tile
+    kernel (gemm3_w256_kernel, 32x32x16 MFMAs: its own k order) — against the same launch on the 128-tile kernel
+    (SDHIP_MLP_NOW256) and against the per-head fp32 forwards, every head's logits at the split-bf16 bound."""
+    from sdreamer.networks import heads_nograd
+    from test_gpu_dreamer import build_agent
+    ag, _, _, _ = build_agent("walker_r2")
+    heads = (ag.reward, ag.cont, ag.value, ag._slow_value)
+    F = heads[0].mlp._mods[0][0].weight.shape[1]
+    x = torch.randn(16384, F, generator=torch.Generator().manual_seed(5)).to("cuda")
+    f0 = []
+    got = heads_nograd(heads, x, True, firsts_out=f0)
+    os.environ["SDHIP_MLP_NOW256"] = "1"
+    try:
+        f1 = []
+        alt = heads_nograd(heads, x, True, firsts_out=f1)
+    finally:
+        del os.environ["SDHIP_MLP_NOW256"]
+    s0 = float(f1[0].abs().max())
+    assert float((f0[0] - f1[0]).abs().max()) <= 1e-4 * s0  # the first layers: same products, other k order
+    assert not torch.equal(f0[0], f1[0])  # (the two kernels did run: their sums differ in rounding)
+    for h, g, a in zip(heads, got, alt):
+        ref = h.logits_nograd(x, False)
+        scale = float(ref.abs().max()) + 1e-6
+        assert float((g - ref).abs().max()) <= 2e-4 * scale, (float((g - ref).abs().max()), scale)
+        assert float((g - a).abs().max()) <= 2e-4 * scale
+
+
+@pytest.mark.parametrize("R,O,I", [(15360, 256, 2560), (4096, 128, 512)])
+def test_wgrad2_matches_two_wgrads(R, O, I):
+    """kernels.wgrad2 (two layers' weight gradients over one input: one GEMM over the joint dy, rows >= split's bias
+    gradients into the second buffer) against torch fp32 at the split-bf16 bound, and the bias sums to 1e-5."""
+    from sdreamer import kernels as kern
+    g = torch.Generator().manual_seed(R + 2 * O)
+    dy = torch.randn(R, 2 * O, generator=g)
+    x = torch.randn(R, I, generator=g)
+    dw0 = torch.randn(2 * O, I, generator=g)
+    da0, db0 = torch.randn(O, generator=g), torch.randn(O, generator=g)
+    dw, da, db = dw0.clone().to("cuda"), da0.clone().to("cuda"), db0.clone().to("cuda")
+    kern.wgrad2(dy.to("cuda"), x.to("cuda"), dw, da, db, O)
+    ref = dw0.double() + dy.double().t() @ x.double()
+    bound = (dy.abs().double().t() @ x.abs().double()) * 4e-5 + 1e-5
+    assert ((dw.double().cpu() - ref).abs() <= bound).all()
+    s = dy.double().sum(0)
+    tol = 1e-4 * float(dy.abs().sum(0).max()) * 1e-2
+    assert torch.allclose(da.double().cpu(), da0.double() + s[:O], rtol=1e-5, atol=tol)
+    assert torch.allclose(db.double().cpu(), db0.double() + s[O:], rtol=1e-5, atol=tol)

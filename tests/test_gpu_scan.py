@@ -108,3 +108,33 @@ def test_scan_row_tiles_bit_identical(cfg_name, B, T):
             assert torch.equal(x, y)
         for n in a[4]:
             assert torch.equal(a[4][n], b[4][n]), n
+
+
+def test_extra_grads_fallback_matches_views():
+    """The backward's second posterior-gradient summands (RSSM._bwd_extra, Dreamer._ph_scan_bwd's feat gradient): as
+    the two column halves of one (B, T, SK + D) buffer (the benched DxSink path, read in place) and as two separate
+    tensors (a non-conforming pair, copied into one buffer by the fallback) — the same sums in the same kernels, so
+    bit-identical gradients."""
+    B, T = 16, 6
+    m, embed, action, reset, init, ups = _model("dmc/cnn", B, T)
+    SK, D = m.flat_stoch, m._deter
+    g = torch.Generator().manual_seed(7)
+    gfeat = (torch.randn(B, T, SK + D, generator=g) * 0.05).to(DEV)
+    outs = []
+    for extra in ((gfeat[..., :SK], gfeat[..., SK:]),
+                  (gfeat[..., :SK].contiguous(), gfeat[..., SK:].contiguous())):
+        assert m.takes_extra_grads(B)
+        for p in m.parameters():
+            p.grad = torch.zeros_like(p)
+        e = embed.clone().requires_grad_(True)
+        st, de, lo = m.observe(e, action, init, reset, seed=1234, row_offset=0)
+        m._bwd_extra = extra
+        loss = (st * ups[0]).sum() + (de * ups[1]).sum() + (lo * ups[2]).sum()
+        loss.backward()
+        torch.cuda.synchronize()
+        assert m._bwd_extra is None
+        outs.append((e.grad.clone(), {n: p.grad.clone() for n, p in m.named_parameters()}))
+    (e0, g0), (e1, g1) = outs
+    assert torch.equal(e0, e1)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n

@@ -95,7 +95,21 @@ __device__ void stage_weights(float* wl, const float* wg, int p) {
 
 // one phase: A panel <- 16 x K of the previous phase's outputs (other WGs'), contraction with the LDS weights,
 // cross-wave reduction, SiLU, plain stores of this WG's outputs
-template <int P>
+typedef __attribute__((address_space(1))) unsigned gu32;  // global (never flat) for every handed-off word
+
+__device__ __forceinline__ float4 ld_sc1(const float4* p) {  // four 4-B global_load_dword sc1 (bypass this CU's L1)
+  gu32* q = (gu32*)(p);
+  float4 v;
+  v.x = __uint_as_float(__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  v.y = __uint_as_float(__hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  v.z = __uint_as_float(__hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  v.w = __uint_as_float(__hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  return v;
+}
+
+// SC1: the A panel was handed over inside this launch (pair variant): every load of it sc1; the outputs are stored
+// sc1 (write-through) for a consumer in the same launch
+template <int P, bool SC1 = false, bool SC1_OUT = false>
 __device__ void phase_body(float* wl, float* al, const float* in, float* out, uint64_t* st) {
   constexpr int K = PK[P], NTL = PN[P];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -104,7 +118,7 @@ __device__ void phase_body(float* wl, float* al, const float* in, float* out, ui
     constexpr int N4 = M * K / 4, PER = N4 / NT;
     float4 v[PER];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) v[i] = src[threadIdx.x + i * NT];
+    for (int i = 0; i < PER; ++i) v[i] = SC1 ? ld_sc1(src + threadIdx.x + i * NT) : src[threadIdx.x + i * NT];
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int e = (threadIdx.x + i * NT) * 4, r = e / K, c = e % K;
@@ -140,7 +154,11 @@ __device__ void phase_body(float* wl, float* al, const float* in, float* out, ui
 #pragma unroll
     for (int w = 0; w < NWAVE; ++w) s += al[((w * NTL + t) * 64 + (e >> 2)) * 4 + (e & 3)];
     s = s / (1.f + __expf(-s)) * 0.5f;
-    out[(long)blockIdx.x * OUT_PER_WG + t * 256 + e] = s;
+    if (SC1_OUT)
+      __hip_atomic_store((gu32*)(out + (long)blockIdx.x * OUT_PER_WG + t * 256 + e), __float_as_uint(s),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      out[(long)blockIdx.x * OUT_PER_WG + t * 256 + e] = s;
   }
 }
 
@@ -178,6 +196,54 @@ __global__ __launch_bounds__(NT, 1) void launch_phase(const float* wg, float* co
   stage_weights(wl, wg, P);
   if (threadIdx.x == 0) st[3] = now();  // weights issued (the A panel load below waits for them too)
   phase_body<P>(wl, al, bufs[(P + 3) % 4], bufs[P], st);
+}
+
+// ---- round 6: the block-local pair _dyn_hid -> _dyn_gru (phases 0 and 1) as ONE launch per step,
+// phases 2 and 3 as launches: 3 launches per step. Every WG stages both phases' weights up front (phase 1's weight
+// staging overlaps phase 0), runs phase 0, publishes its outputs write-through (sc1 stores, every storing wave drained,
+// barrier, one lane's sc1 flag = step + 1), then polls its producers' flags with sc1 loads: the 16 WGs whose outputs
+// form its phase-1 A panel, or with NORM all 256 (the RMSNorm between _dyn_hid and _dyn_gru needs every column
+// tile's partial sums of squares of the rows: an all-to-all edge), and loads the panel with sc1 loads (the handoff
+// table's first row: hipMalloc'd, one WG per CU, 4-B sc1 stores and loads). Spins are bounded (error word).
+template <bool NORM>
+__global__ __launch_bounds__(NT, 1) void pair_launch(const float* wg, float* const* bufs, uint64_t* tr, int step,
+                                                      unsigned* flags, unsigned* err) {
+  __shared__ __attribute__((aligned(16))) float wl[W_FLOATS];
+  __shared__ __attribute__((aligned(16))) float al[A_FLOATS];
+  __shared__ int ok;
+  const unsigned epoch = step + 1;
+  uint64_t* st0 = tr + (((long)step * NPH + 0) * NWG + blockIdx.x) * 4;
+  uint64_t* st1 = tr + (((long)step * NPH + 1) * NWG + blockIdx.x) * 4;
+  if (threadIdx.x == 0) st0[0] = now();
+  stage_weights(wl, wg, 0);
+  stage_weights(wl, wg, 1);
+  if (threadIdx.x == 0) st0[3] = now();
+  phase_body<0, false, true>(wl, al, bufs[3], bufs[0], st0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    st1[0] = now();
+    __hip_atomic_store((gu32*)&flags[blockIdx.x * 32], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) ok = 1;
+  __syncthreads();
+  constexpr int NPOLL = NORM ? NWG : 16;
+  if (threadIdx.x < NPOLL) {
+    const int src = NORM ? threadIdx.x : (blockIdx.x % 16) * 16 + threadIdx.x;
+    long spins = 0;
+    while (__hip_atomic_load((gu32*)&flags[src * 32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+      if (++spins > SPIN_LIMIT || __hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  if (!ok) return;
+  if (threadIdx.x == 0) st1[3] = now();  // released: every producer's flag seen
+  phase_body<1, true, false>(wl, al, bufs[0], bufs[1], st1);
 }
 
 static double med(std::vector<double> v) {
@@ -305,5 +371,50 @@ int main() {
   }
   hipMemcpy(h.data(), tr, trn * 8, hipMemcpyDeviceToHost);
   report("launches (weights re-staged every launch)", h, false);
+  // the pair variants: phases 0 + 1 in one launch, phases 2, 3 as launches (3 launches per step)
+  unsigned *flags, *err;
+  hipMalloc(&flags, NWG * 32 * 4);
+  hipMalloc(&err, 128);
+  for (int norm = 0; norm < 2; ++norm) {
+    hipGraph_t pg;
+    hipGraphExec_t pe;
+    hipStreamBeginCapture(stream, hipStreamCaptureModeGlobal);
+    for (int st = 0; st < STEPS; ++st) {
+      if (norm)
+        pair_launch<true><<<NWG, NT, 0, stream>>>(wg, bufs, tr, st, flags, err);
+      else
+        pair_launch<false><<<NWG, NT, 0, stream>>>(wg, bufs, tr, st, flags, err);
+      launch_phase<2><<<NWG, NT, 0, stream>>>(wg, bufs, tr, st);
+      launch_phase<3><<<NWG, NT, 0, stream>>>(wg, bufs, tr, st);
+    }
+    hipStreamEndCapture(stream, &pg);
+    if (hipGraphInstantiate(&pe, pg, nullptr, nullptr, 0) != hipSuccess) {
+      printf("pair graph instantiate failed\n");
+      return 1;
+    }
+    for (int rep = 0; rep < 3; ++rep) {
+      hipMemset(tr, 0, trn * 8);
+      hipMemset(flags, 0, NWG * 32 * 4);
+      hipMemset(err, 0, 128);
+      hipDeviceSynchronize();
+      hipEventRecord(e0, stream);
+      hipGraphLaunch(pe, stream);
+      hipEventRecord(e1, stream);
+      hipEventSynchronize(e1);
+      unsigned herr = 0;
+      hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost);
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, e0, e1);
+      if (herr) {
+        printf("pair%s: a hand-off wait timed out: no timing\n", norm ? "+norm" : "");
+        return 1;
+      }
+      printf("pair%s (graph) rep %d: %d steps x 3 launches %.2f us = %.2f us per step\n", norm ? "+norm" : "", rep,
+             STEPS, ms * 1e3, ms * 1e3 / STEPS);
+    }
+    hipMemcpy(h.data(), tr, trn * 8, hipMemcpyDeviceToHost);
+    report(norm ? "pair + all-256 norm wait (phase 1: entry = published, 'weights' = the hand-off wait)"
+                : "pair, 16-producer panel wait (phase 1: entry = published, 'weights' = the hand-off wait)", h, false);
+  }
   return 0;
 }

@@ -1,0 +1,8 @@
+#!/bin/bash
+# round-6 baseline on a fresh box: bench line, two-stream timeline, phases alone, contention probe, phase kernel lists
+set -o pipefail
+O=gpurun_out/$1; mkdir -p $O
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err &&
+timeout -k 10 200 python3 tools/timeline.py > $O/timeline.txt 2>&1 &&
+timeout -k 10 300 python3 tools/phase_bench.py > $O/phases_alone.txt 2>&1 &&
+timeout -k 10 300 python3 tools/phase_bench.py 10 contention > $O/contention.txt 2>&1
