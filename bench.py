@@ -336,12 +336,14 @@ def probe_specs(agent, cfg, K):
         out.append(dict(key=key, name=name, grid=list(grid), bound=bound, work=work, algo=algo, label=label, how=how,
                         launches=launches, peak=peak, alt_peak=alt_peak))
 
-    # encoder stage 2 forward (conv + pool + RMSNorm + SiLU, direct conv from an LDS patch)
+    # encoder stage 2 forward (conv + pool + RMSNorm + SiLU, direct conv from an LDS patch; on bf16x6 by default)
     cp = dominant_probe(K)
     if K.ops_fused_pool():
         pix = N * 32 * 32
-        add("conv_stage2", "conv_fwd_direct_pool<48, 32, 5, 5, 1>", (N * 32 * 32 // 128, 1, 1), "mfma",
-            2.0 * pix * 48 * 25 * 32, 4.0 * pix * 32 + N * 16 * 16 * (48 * 9 + 4), cp.label, ("launch", cp), 1)
+        c6 = bool(K.CONV6)
+        add("conv_stage2", "conv_fwd6_direct_pool<48, 32, 5, 5>" if c6 else "conv_fwd_direct_pool<48, 32, 5, 5, 1>",
+            (N * 32 * 32 // 128, 1, 1), "mfma", 2.0 * pix * 48 * 25 * 32, 4.0 * pix * 32 + N * 16 * 16 * (48 * 9 + 4),
+            cp.label, ("launch", cp), 1, peak=PEAK_BF16X6 if c6 else None, alt_peak=PEAK_FP32_MFMA if c6 else None)
     # encoder stage 2 bwd-data (split-bf16 direct conv from a pre-split dOut patch in LDS): sd_conv2d_dgrad_direct(dout,
     # wsplit, din, Nb, Hs, Ws, Ci = dout channels, Co = din channels, kh, kw, pad, stream)
     dg = K.LaunchProbe("sd_conv2d_dgrad_direct", lambda a: a[6] == 48 and a[7] == 32,
@@ -578,6 +580,12 @@ def dominant_probe(K):
     def flops(a):  # sd_conv2d_fwd_pool(in, w, b, nw, pooled, amax, y, rstd, Nb, Hs, Ws, Ci, Co, kh, kw, ...)
         Nb, Hs, Ws, Ci, Co, kh, kw = a[8], a[9], a[10], a[11], a[12], a[13], a[14]
         return 2.0 * Nb * Hs * Ws * Co * kh * kw * Ci
+    if K.CONV6:  # sd_conv2d_fwd_pool6: the same arguments with the split weight image in place of w
+        return K.LaunchProbe("sd_conv2d_fwd_pool6", lambda a: a[11] == 32 and a[12] == 48, flops,
+                             label="conv_fwd6_direct_pool<48, 32, 5, 5> (encoder stage 2: 32->48 ch, 32x32, 5x5 conv + "
+                                   "2x2 max-pool + RMSNorm + SiLU epilogue; direct conv from the input patch staged "
+                                   "once as three bf16 planes, the pre-split weight per lane from L2; bf16x6 = 6 "
+                                   "v_mfma_f32_16x16x32_bf16 per f32-equivalent product, fp32-accurate)")
     return K.LaunchProbe("sd_conv2d_fwd_pool", lambda a: a[11] == 32 and a[12] == 48, flops,
                          label="conv_fwd_direct_pool<48> (encoder stage 2: 32->48 ch, 32x32, 5x5 conv + 2x2 max-pool + "
                                "RMSNorm + SiLU epilogue; direct conv from an LDS input patch, v_mfma_f32_16x16x4_f32, "

@@ -261,6 +261,14 @@ int sd_conv2d_wgrad_bf16x3_slabs(int Nb, int Hs, int Ws, int Ci, int Co, int kh,
 int sd_conv2d_wgrad_bf16x3(const float* in, const float* dout, float* dw_db, float* workspace, long ws_floats,
                            int Nb, int Hs, int Ws, int Ci, int Co, int kh, int kw, int pad, const sd_wgrad_acc* acc,
                            sd_stream stream);
+/* sd_conv2d_wgrad_pool (the pooled first stage's bwd-weight from sd_pool_rms_bwd_compact's gradient + argmax) on the
+ * split-bf16 direct kernel (conv_wgrad3_direct, the 32-pixel steps dealt to the 8 waves, the pooled gradient routed
+ * through the argmax while staged). Same arguments; _slabs: workspace slabs (each Co x (kh*kw*Ci+1) floats), 0 when
+ * the shape is outside it (J + 1 <= 112, W a power of two dividing 256 into an even row count; then SD_ESHAPE). */
+int sd_conv2d_wgrad_pool_bf16x3_slabs(int Nb, int H, int W, int Ci, int Co, int kh, int kw);
+int sd_conv2d_wgrad_pool_bf16x3(const float* in, const float* dpool, const uint8_t* amax, float* dw_db,
+                                float* workspace, long ws_floats, int Nb, int H, int W, int Ci, int Co, int kh, int kw,
+                                int pad, const sd_wgrad_acc* acc, sd_stream stream);
 /* The same bwd-data as a direct convolution (csrc/conv.hip conv_dgrad3_direct: each workgroup stages its dOut patch
  * once, split to bf16 planes; same products and order per k as sd_conv2d_dgrad_bf16x3, k summed in the same order).
  * wsplit = sd_conv_split_weight(wflip, rows = Co, K = kh*kw*Ci). Instantiated for the 5x5 pad-2 stages of the

@@ -106,9 +106,18 @@ size_t sd_lds_pad_for(const void* kern);
 
 // Phase timestamps (measurement build, -DSD_SCAN_TRACE; scan.hip and img.hip kernels): thread 0 of every workgroup keeps entry / operands staged /
 // contraction reduced / exit (s_memrealtime, 100 MHz) and stores them at exit into trace[slot][workgroup][4].
+// SD_CHAIN_PRIO (1..3): the latency-bound chains' kernels (the observe scan's and the imagination's step launches, the
+// ones that open with SD_TR_BEGIN) raise their waves' issue priority (s_setprio) at entry, so on a SIMD shared with a
+// filler phase's waves (the other stream's GEMMs, priority 0) their instructions issue first (MI355X_MICROARCH.md:
+// VALU issue is arbitrated by priority, then age). 0 = off.
+#ifndef SD_CHAIN_PRIO
+#define SD_CHAIN_PRIO 0
+#endif
+#define SD_CHAIN_PRIO_SET                                     \
+  if constexpr (SD_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(SD_CHAIN_PRIO);
 #ifdef SD_SCAN_TRACE
 constexpr int TR_WG = 2048;  // workgroup slots per launch
-#define SD_TR_BEGIN uint64_t tr_[4] = {__builtin_amdgcn_s_memrealtime(), 0ull, 0ull, 0ull};
+#define SD_TR_BEGIN SD_CHAIN_PRIO_SET uint64_t tr_[4] = {__builtin_amdgcn_s_memrealtime(), 0ull, 0ull, 0ull};
 #define SD_TR(k) tr_[k] = __builtin_amdgcn_s_memrealtime();
 #define SD_TR_END(buf, slot)                                                                               \
   if (threadIdx.x == 0 && (buf)) {                                                                         \
@@ -120,7 +129,7 @@ constexpr int TR_WG = 2048;  // workgroup slots per launch
     }                                                                                                      \
   }
 #else
-#define SD_TR_BEGIN
+#define SD_TR_BEGIN SD_CHAIN_PRIO_SET
 #define SD_TR(k)
 #define SD_TR_END(buf, slot)
 #endif

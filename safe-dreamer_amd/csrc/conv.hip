@@ -1141,7 +1141,8 @@ __global__ __launch_bounds__(256) void slab_reduce(const float* __restrict__ ws,
 // TM 16-row blocks of co (rows >= Co read zero rows).
 struct DirectW3 {
   const float* x;
-  const float* dy;
+  const float* dy;      // (Nb, H, W, Co) conv-output gradient, or (PL) the pooled-resolution gradient
+  const uint8_t* amax;  // PL: the 2x2 max-pool argmax per pooled element
   float* ws;
   int Nb, H, W, Ci, Co, kh, kw, pad, R, lw;
   int J, PW, PH, CP, PS, blocks;
@@ -1160,7 +1161,12 @@ SD_DEV uint32_t pack_split(float v) {  // (bf16 hi | bf16 lo << 16), hi + lo = v
   sdb::split2(x, hi, lo);
   return (uint32_t)__builtin_bit_cast(uint16_t, hi[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, lo[0]) << 16);
 }
-template <int TM, int NBW>
+// WS (wave split, as conv_wgrad_direct): for few column blocks (the 4-channel first stage: J + 1 = 101 -> 7 blocks)
+// every wave covers all of them over every 8th 32-pixel step, and the 8 waves' tiles are summed through LDS at the end.
+// PL: dy is the max-pool backward's pooled-resolution gradient + argmax (sd_pool_rms_bwd_compact), routed to its
+// window position while fetched (conv_wgrad_direct's PL): the first stage's bwd-weight without the full-resolution
+// conv gradient, on split-bf16.
+template <int TM, int NBW, bool WS = false, bool PL = false>
 __global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1176,7 +1182,7 @@ __global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
   int off[NBW];
 #pragma unroll
   for (int b = 0; b < NBW; ++b) {
-    const int j = 16 * ((blockIdx.x * NW_D + wave) * NBW + b) + l16;
+    const int j = 16 * (WS ? b : (blockIdx.x * NW_D + wave) * NBW + b) + l16;
     if (j < d.J) {
       const int t = j / d.Ci, ci = j - t * d.Ci, ky = t / d.kw, kx = t - ky * d.kw;
       off[b] = (ky * d.PW + kx) * d.CP + ci;
@@ -1195,13 +1201,25 @@ __global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
   const int dq4 = tid % c4, drest = tid / c4;
   const int dc = drest % 4, dih = (drest / 4) % 2, dsb = drest / 8;
   f32x4 rd[4], rp[WD_VP];
+  uint32_t aw[PL ? 4 : 1];  // PL: the 4 channels' argmax bytes of each pixel's pooled element
+  int qd[PL ? 4 : 1];       // PL: the pixel's position in its 2x2 window
   auto fetch = [&](int rb) {
     const int n = rb / rows_per_img, y0 = (rb - n * rows_per_img) * d.R;
-    const float* dsrc = d.dy + ((long)n * d.H + y0) * d.W * d.Co;
+    [[maybe_unused]] const float* dsrc = d.dy + ((long)n * d.H + y0) * d.W * d.Co;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int px = 32 * dsb + dc + 4 * (4 * dih + t);
-      rd[t] = tid < nD ? *reinterpret_cast<const f32x4*>(dsrc + (long)px * d.Co + 4 * dq4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (PL) {  // the pooled element of pixel px (row y0 + px / W), loaded whole; masked in stage()
+        const int yy = y0 + (px >> d.lw), xx = px & (d.W - 1);
+        const long pp = (((long)n * (d.H >> 1) + (yy >> 1)) * (d.W >> 1) + (xx >> 1)) * d.Co + 4 * dq4;
+        const bool ok = tid < nD;
+        rd[t] = ok ? *reinterpret_cast<const f32x4*>(d.dy + pp) : f32x4{0.f, 0.f, 0.f, 0.f};
+        aw[t] = ok ? *reinterpret_cast<const uint32_t*>(d.amax + pp) : 0xffffffffu;
+        qd[t] = (yy & 1) * 2 + (xx & 1);
+      } else {
+        rd[t] = tid < nD ? *reinterpret_cast<const f32x4*>(dsrc + (long)px * d.Co + 4 * dq4)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
 #pragma unroll
     for (int v = 0; v < WD_VP; ++v) {
@@ -1220,6 +1238,13 @@ __global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
   auto stage = [&]() {
     if (tid < nD) {
       const int pos = 32 * dsb + 8 * dc + 4 * dih;
+      if constexpr (PL) {  // route the pooled gradient to its argmax position of the 2x2 window, zeros elsewhere
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (((aw[t] >> (8 * k)) & 0xffu) != (uint32_t)qd[t]) rd[t][k] = 0.f;
+      }
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const f32x4 t = {rd[0][jj], rd[1][jj], rd[2][jj], rd[3][jj]};
@@ -1266,7 +1291,7 @@ __global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
     stage();
     __syncthreads();
     if (rb + (int)gridDim.y < d.blocks) fetch(rb + gridDim.y);  // next block's loads overlap this block's MFMAs
-    for (int s = 0; s < P / 32; ++s) {
+    for (int s = WS ? wave : 0; s < P / 32; s += WS ? NW_D : 1) {
       sdb::bf16x8 ah[TM], al[TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -1316,6 +1341,26 @@ __global__ __launch_bounds__(512) void conv_wgrad3_direct(DirectW3 d) {
     }
   }
   float* out = d.ws + (long)blockIdx.y * d.Co * (d.J + 1);
+  if constexpr (WS) {  // sum the 8 waves' tiles through LDS (the staging area is free now), one 16x16 tile at a time
+#pragma unroll
+    for (int b = 0; b < NBW; ++b)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lds[(wave * 4 + r) * 64 + lane] = acc[i][b][r];
+        __syncthreads();
+        if (tid < 256) {
+          const int r = tid >> 6, ln = tid & 63;
+          float v = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW_D; ++w) v += lds[(w * 4 + r) * 64 + ln];
+          const int j = 16 * b + (ln & 15), co = 16 * i + 4 * (ln >> 4) + r;
+          if (j <= d.J && co < d.Co) out[(long)co * (d.J + 1) + j] = v;
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int b = 0; b < NBW; ++b) {
     const int j = 16 * ((blockIdx.x * NW_D + wave) * NBW + b) + l16;
@@ -1903,8 +1948,17 @@ namespace {
 
 
 namespace {
+// SDHIP_WGRAD3_CI4 (study knob): the split-bf16 direct bwd-weight also for 4-channel inputs (the encoder's first
+// stage, which otherwise stays on the f32 direct kernel) — to measure that stage's gradient parity on split-bf16
+bool wgrad3_ci4() {
+  static int a = -1;
+  if (a < 0) a = getenv("SDHIP_WGRAD3_CI4") ? 1 : 0;
+  return a == 1;
+}
 bool direct3_plan(int Nb, int H, int W, int Ci, int Co, int kh, int kw, int ups, DirectPlan& pl) {
-  if (ups != 0 || Co % 4 || Co > 64 || Ci % 4 || Ci < 16 || W < 8 || ilog2_exact(W) < 0 || W > 128) return false;
+  if (ups != 0 || Co % 4 || Co > 64 || Ci % 4 || Ci < (wgrad3_ci4() ? 4 : 16) || W < 8 || ilog2_exact(W) < 0 ||
+      W > 128)
+    return false;
   pl.R = 128 / W < H ? 128 / W : H;
   const int P = pl.R * W;
   if (H % pl.R || P % 32) return false;
@@ -1932,10 +1986,35 @@ bool direct3_plan(int Nb, int H, int W, int Ci, int Co, int kh, int kw, int ups,
   return true;
 }
 
+// the first stage's plan for conv_wgrad3_direct<TM, 7, WS, PL>: dy at pooled resolution (R even), every wave over
+// all <= 7 column blocks (J + 1 <= 112), 32-pixel steps dealt to the 8 waves: R rows of W pixels with 8 steps per
+// block (P = 256), one 4-channel x 4-pixel dy item per thread ((Co / 4) (P / 4) <= 512)
+bool pool3_plan(int Nb, int H, int W, int Ci, int Co, int kh, int kw, DirectPlan& pl) {
+  if (Co % 4 || Co > 64 || Ci % 4 || W < 8 || ilog2_exact(W) < 0 || W > 256 || H % 2) return false;
+  const int J = kh * kw * Ci, JB = (J + 1 + 15) / 16;
+  if (JB > 7) return false;
+  pl.R = 256 / W;
+  if (pl.R < 2 || pl.R % 2 || H % pl.R) return false;
+  const int P = pl.R * W, TM = (Co + 15) / 16, CP = patch_stride(Ci);
+  const int PH = pl.R + kh - 1, PW = W + kw - 1;
+  if ((Co / 4) * (P / 4) > 512 || PH * PW * (Ci / 4) > WD_VP * 512) return false;
+  pl.lds = (size_t)PH * PW * CP * 4 + (size_t)TM * 16 * (P + 8) * 2 * 2;
+  if (pl.lds > 160 * 1024) return false;
+  pl.ws = true;
+  pl.nbw = 7;
+  pl.gx = 1;
+  const int blocks = Nb * (H / pl.R);
+  pl.gy = blocks < 256 ? blocks : 256;
+  pl.slabs = pl.gy;
+  return true;
+}
+
 int wgrad3_direct(const float* in, const float* dout, float* dw_db, float* ws, long ws_floats, int Nb, int H, int W,
-                  int Ci, int Co, int kh, int kw, int pad, const DirectPlan& pl, hipStream_t s, sd_wgrad_acc acc) {
+                  int Ci, int Co, int kh, int kw, int pad, const DirectPlan& pl, hipStream_t s, sd_wgrad_acc acc,
+                  const uint8_t* amax = nullptr) {
   DirectW3 d;
-  d.x = in; d.dy = dout; d.Nb = Nb; d.H = H; d.W = W; d.Ci = Ci; d.Co = Co; d.kh = kh; d.kw = kw; d.pad = pad;
+  d.x = in; d.dy = dout; d.amax = amax; d.Nb = Nb; d.H = H; d.W = W; d.Ci = Ci; d.Co = Co; d.kh = kh; d.kw = kw;
+  d.pad = pad;
   d.lw = ilog2_exact(W); d.J = kh * kw * Ci; d.R = pl.R;
   d.PW = W + kw - 1; d.PH = d.R + kh - 1;
   d.CP = patch_stride(Ci);
@@ -1946,23 +2025,26 @@ int wgrad3_direct(const float* in, const float* dout, float* dw_db, float* ws, l
   const dim3 grid(pl.gx, pl.gy);
   const int TM = (Co + 15) / 16;
   bool launched = false;
-#define SD_WD3(TM_, NB_)                                                                                   \
-  if (TM == TM_ && pl.nbw == NB_) {                                                                       \
+#define SD_WD3X(TM_, NB_, WS_, PL_)                                                                        \
+  if (TM == TM_ && pl.nbw == NB_ && pl.ws == WS_ && (amax != nullptr) == PL_) {                            \
     static bool raised = false;                                                                            \
     if (!raised && pl.lds > 65536) {                                                                       \
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad3_direct<TM_, NB_>),                 \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_wgrad3_direct<TM_, NB_, WS_, PL_>),       \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)       \
         return SD_EARG;                                                                                    \
       raised = true;                                                                                       \
     }                                                                                                      \
-    conv_wgrad3_direct<TM_, NB_><<<grid, 512, pl.lds, s>>>(d);                                            \
+    conv_wgrad3_direct<TM_, NB_, WS_, PL_><<<grid, 512, pl.lds, s>>>(d);                                  \
     launched = true;                                                                                       \
   }
+#define SD_WD3(TM_, NB_) SD_WD3X(TM_, NB_, false, false)
   SD_WD3(1, 2) SD_WD3(1, 4) SD_WD3(1, 5) SD_WD3(1, 7)
   SD_WD3(2, 2) SD_WD3(2, 4) SD_WD3(2, 5) SD_WD3(2, 7)
   SD_WD3(3, 2) SD_WD3(3, 4) SD_WD3(3, 5) SD_WD3(3, 7)
   SD_WD3(4, 2) SD_WD3(4, 4) SD_WD3(4, 5) SD_WD3(4, 7)
+  SD_WD3X(1, 7, true, true) SD_WD3X(2, 7, true, true) SD_WD3X(3, 7, true, true) SD_WD3X(4, 7, true, true)
 #undef SD_WD3
+#undef SD_WD3X
   if (!launched) return SD_ESHAPE;
   SD_LAUNCH_CHECK();
   const long n = (long)Co * (d.J + 1);
@@ -2091,6 +2173,24 @@ extern "C" int sd_conv2d_wgrad_bf16x3_slabs(int Nb, int Hs, int Ws, int Ci, int 
   DirectPlan pl;
   if (!direct3_plan(Nb, Hs, Ws, Ci, Co, kh, kw, ups, pl)) return SD_ESHAPE;
   return pl.slabs;
+}
+
+extern "C" int sd_conv2d_wgrad_pool_bf16x3_slabs(int Nb, int H, int W, int Ci, int Co, int kh, int kw) {
+  DirectPlan pl;
+  if (!pool3_plan(Nb, H, W, Ci, Co, kh, kw, pl)) return 0;
+  return pl.slabs;
+}
+extern "C" int sd_conv2d_wgrad_pool_bf16x3(const float* in, const float* dpool, const uint8_t* amax, float* dw_db,
+                                           float* workspace, long ws_floats, int Nb, int H, int W, int Ci, int Co,
+                                           int kh, int kw, int pad, const sd_wgrad_acc* acc_p, sd_stream stream_) {
+  if (Nb <= 0) return SD_OK;
+  const sd_wgrad_acc acc = acc_p ? *acc_p : sd_wgrad_acc{nullptr, nullptr, 0};
+  if (acc.dw && (!acc.db || acc.ci_w < 1 || acc.ci_w > Ci)) return SD_EARG;
+  DirectPlan pl;
+  if (!pool3_plan(Nb, H, W, Ci, Co, kh, kw, pl)) return SD_ESHAPE;
+  if (!al16(dpool) || !al16(in) || !amax || reinterpret_cast<uintptr_t>(amax) % 4) return SD_EARG;
+  return wgrad3_direct(in, dpool, dw_db, workspace, ws_floats, Nb, H, W, Ci, Co, kh, kw, pad, pl,
+                       (hipStream_t)stream_, acc, amax);
 }
 
 extern "C" int sd_conv2d_wgrad_bf16x3(const float* in, const float* dout, float* dw_db, float* workspace,

@@ -73,6 +73,11 @@ AC_DEFER = os.environ.get("SDREAMER_AC_DEFER", "0") == "1"
 # the imagined actor's and value head's first-layer weight gradients as ONE split-bf16 GEMM over their joint dy: the
 # 157 MB imagined-feature operand read once instead of twice (ops.PairFirstFn). 0 = one per head
 PAIR_FIRST = os.environ.get("SDREAMER_PAIR_FIRST", "1") != "0"
+# SDREAMER_SLOW_IN_S2=1: the imagined slow-critic head in the actor-critic phase S2 instead of with the other imagined
+# heads in S1 (which end the path to the lambda-returns and the replay-value loss). Measured slower (10.87 -> 10.91 ms
+# per update, profiles/r06f: the heads' batched first layer loses its fourth entry's reuse of the imagined features
+# and S2 beside the scan backward grows), so off
+SLOW_IN_S2 = os.environ.get("SDREAMER_SLOW_IN_S2", "0") == "1"
 # KB of dynamic LDS every GEMM launch of the filler phases (M1, S2, S3, S4) reserves without using it (sd_set_lds_pad):
 # fewer filler workgroups fit on a CU, leaving LDS for the latency-bound chain's workgroups beside them (0 = off)
 FILL_LDS = int(os.environ.get("SDREAMER_FILL_LDS", "0"))
@@ -817,7 +822,8 @@ class Dreamer(nn.Module):
             for t in (st["ifeat"], st["iact"]):
                 t.record_stream(main)
             for v in st["rr"].values():
-                v.record_stream(main)
+                if isinstance(v, torch.Tensor):
+                    v.record_stream(main)
         self._ph_repval(st)
         ev_rep = torch.cuda.Event()
         ev_rep.record()
@@ -1000,6 +1006,7 @@ class Dreamer(nn.Module):
         """side: the replay-value loss's deferred value-head weight gradients, ReturnEMA + advantage, policy / value
         losses on the imagined trajectories and their backward."""
         ops.flush_wgrads(st["rv_wgrads"])
+        self._slow_values(st["ifeat"], st["rr"])
         self._returns_norm(st["rr"])
         st["ac_losses"], st["ac_metrics"] = self._ac_losses(st["ifeat"], st["iact"], st["rr"])
         with torch.no_grad():  # replay-value statistics (dreamer.py:649-651), off the main stream's critical path
@@ -1206,12 +1213,15 @@ class Dreamer(nn.Module):
         # frozen heads on the imagined trajectories: split-bf16 contractions (no sampled index depends on them), the
         # four first layers as one batched launch
         firsts = []
-        l_rew, l_cont, l_val, l_slow = heads_nograd((self.reward, self.cont, self.value, self._slow_value), flat, True,
-                                                    firsts_out=firsts)
+        # the slow critic feeds only the value loss's target and a metric (dreamer.py:606,616,666): with SLOW_IN_S2 it
+        # runs in the actor-critic phase (_slow_values), off the path from the imagination to the lambda-returns
+        heads = (self.reward, self.cont, self.value) + (() if SLOW_IN_S2 else (self._slow_value,))
+        outs = heads_nograd(heads, flat, True, firsts_out=firsts)
+        l_rew, l_cont, l_val = outs[:3]
         i_rew = K.twohot_mode(l_rew, self.rbins).view(H1, N)
         i_contl = l_cont.reshape(H1, N)  # a column of the fused output layer's padded logits
         i_val = K.twohot_mode(l_val, self.vbins).view(H1, N)
-        i_slow = K.twohot_mode(l_slow, self.vbins).view(H1, N)
+        i_slow = None if SLOW_IN_S2 else K.twohot_mode(outs[3], self.vbins).view(H1, N)
         disc = 1 - 1 / self.horizon
         i_cont = torch.empty(N, H1, device=dev)
         weight = torch.empty(N, H1, device=dev)
@@ -1222,6 +1232,15 @@ class Dreamer(nn.Module):
         # (_frozen_value aliases value; the weights change only at the optimizer step)
         val_h0 = firsts[0][2] if (firsts and REUSE_H0) else None
         return dict(ret=ret, weight=weight, i_cont=i_cont, i_rew=i_rew, i_val=i_val, i_slow=i_slow, val_h0=val_h0)
+
+    @torch.no_grad()
+    def _slow_values(self, ifeat, rr):
+        """The slow critic's mode on the imagined trajectories (dreamer.py:593 _frozen_slow_value(imag_feat).mode()),
+        when _heads_returns left it out (SLOW_IN_S2)."""
+        if rr.get("i_slow") is None:
+            H1, N = ifeat.shape[:2]
+            (l_slow,) = heads_nograd((self._slow_value,), ifeat.reshape(H1 * N, -1), True)
+            rr["i_slow"] = K.twohot_mode(l_slow, self.vbins).view(H1, N)
 
     @torch.no_grad()
     def _returns_norm(self, rr):

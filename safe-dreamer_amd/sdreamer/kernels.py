@@ -65,8 +65,15 @@ def _skinny_split(M, N, K, batch):
     return max(1, min(ks, 64))
 
 
+# SDREAMER_F32_SPLIT2=1 (A/B knob): exact-f32 GEMMs of one round of 64 x 64 tiles (256..511) with K >= 1024 split K in
+# two (the world-model phase's 1024 x 1024 x 1024 Barlow contractions: 256 workgroups over 32 k tiles each)
+_F32_SPLIT2 = os.environ.get("SDREAMER_F32_SPLIT2", "0") == "1"
+
+
 def _auto_split(M, N, K, batch):
     tiles = -(-M // 64) * -(-N // 64) * batch
+    if _F32_SPLIT2 and 256 <= tiles < 512 and K >= 1024:
+        return 2
     if tiles >= 256 or K < 512:
         return 1
     ks = min(K // 256, max(1, 512 // tiles))
@@ -115,6 +122,21 @@ def _fast_split(M, N, K, batch):
     return max(1, min(K // 128, -(-256 // t64), 16))
 
 
+_WGRAD_T128 = int(os.environ.get("SDREAMER_WGRAD_T128", "0"))
+
+
+def _wgrad_t128_split(M, N, K):
+    """split count for ~_WGRAD_T128 workgroups of 128 x 128 tiles, an even divisor of K's 32-deep tiles if one is near"""
+    tiles = -(-M // 128) * -(-N // 128)
+    want = max(1, min(32, round(_WGRAD_T128 / tiles), K // 512))
+    kt = K // 32 if K % 32 == 0 else 0
+    if kt:
+        for d in sorted(range(1, 33), key=lambda d: (abs(d - want), -d)):
+            if kt % d == 0 and abs(d - want) <= max(1, want // 4):
+                return d
+    return want
+
+
 def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1, fast=False, rowsum=None):
     """out[M,N] = alpha * a[M,K] @ b[K,N] (+ bias[N]) (+ beta*out). Strided views allowed (one unit stride each);
     3-D operands are a strided batch over dim 0. fast=True: split-bf16 MFMA path (sd_gemm_bf16x3, ~1e-5 relative)
@@ -153,6 +175,10 @@ def gemm(a, b, out, bias=None, alpha=1.0, beta=0.0, ksplit=None, tile=-1, fast=F
     fast = fast and FAST_GEMM and M >= 64 and Nn >= 64 and K >= 64
     if rowsum is not None and not (fast and Bt == 1 and not ak and rowsum.is_contiguous()):
         return False
+    if ksplit is None and fast and _WGRAD_T128 and not ak and not bk and M <= 512 and K >= 4096 and tile < 0:
+        # weight-gradient shape (dW = dy^T x: long K, both operands rows-contiguous) on 128 x 128 tiles with about
+        # _WGRAD_T128 workgroups (SDREAMER_WGRAD_T128, A/B knob): fewer, longer split-K workgroups
+        ksplit, tile = _wgrad_t128_split(M, Nn, K), 0
     if ksplit is None:
         if fast:
             ksplit = _fast_split(M, Nn, K, Bt)
@@ -643,14 +669,32 @@ def conv2d_wgrad_pool_slabs(x, Co, kh, kw):
     return nat.fns["sd_conv2d_wgrad_pool_slabs"](Nb, H, W, Ci, Co, kh, kw)
 
 
+# SDREAMER_WGRAD1_X3: the first encoder stage's bwd-weight (the pooled-gradient form) on the split-bf16 direct kernel
+# (sd_conv2d_wgrad_pool_bf16x3) instead of the f32 one — the last f32 gradient contraction of the encoder, on the
+# critical path (phase M2c). Default on (round 6: golden update + gradient tests green, LaProp moments as close to
+# float64 as the f32 kernel's, profiles/r06f; update 10.91 -> 10.85 ms); 0 = the f32 kernel
+WGRAD1_X3 = os.environ.get("SDREAMER_WGRAD1_X3", "1") == "1"
+
+
 def conv2d_wgrad_pool(x, dpool, amax, kh, kw, pad=None, acc=None):
     """[dW | db] (Co, kh*kw*Ci + 1) of a pooled stage from the max-pool backward's pooled-resolution gradient and the
     forward's argmax (the f32 direct kernel expands them while staging; the same products as conv2d_wgrad on the
-    expanded gradient, summed in 512-pixel row blocks instead of 128: reordered f32 sums, ~2e-5 relative)."""
+    expanded gradient, summed in 512-pixel row blocks instead of 128: reordered f32 sums, ~2e-5 relative). With
+    WGRAD1_X3 the split-bf16 direct kernel where its plan takes the shape (~1e-5 of sum |a b| per element)."""
     Nb, H, W, Ci = x.shape
     Co = dpool.shape[-1]
     pad = (kh - 1) // 2 if pad is None else pad
     J = kh * kw * Ci
+    if WGRAD1_X3 and FAST_GEMM:
+        ks = nat.fns["sd_conv2d_wgrad_pool_bf16x3_slabs"](Nb, H, W, Ci, Co, kh, kw)
+        if ks > 0:
+            out = torch.empty(Co, J + 1, dtype=torch.float32, device=x.device)
+            ws = torch.empty(ks * Co * (J + 1), dtype=torch.float32, device=x.device)
+            keep, ap = _wgrad_acc(acc)
+            nat.call("sd_conv2d_wgrad_pool_bf16x3", p(_c(x)), p(_c(dpool)), p(_c(amax)), p(out), p(ws), ws.numel(),
+                     Nb, H, W, Ci, Co, kh, kw, pad, ap, stream())
+            del keep
+            return None if acc is not None else out
     ks = conv2d_wgrad_pool_slabs(x, Co, kh, kw)
     if ks <= 0:
         raise nat.NativeError("sd_conv2d_wgrad_pool: shape outside the direct kernel")
@@ -665,10 +709,14 @@ def conv2d_wgrad_pool(x, dpool, amax, kh, kw, pad=None, acc=None):
 
 _FLIP = {}  # weight data_ptr -> flipped weight, built ahead of the backward (set_flip_cache)
 _SPLIT = {}  # weight data_ptr -> split-bf16 image of the flipped weight (sd_conv_split_weight), same lifetime
-# SDREAMER_CONV6=1: the encoder stages' forward on the fp32-accurate three-way split-bf16 direct kernel instead of the
-# exact f32 kernels (sd_conv2d_fwd_pool6; opt-in: 0.54 vs 0.68 ms on stage 2 but the golden optimizer check of the
-# first conv layer, already at 1.85 % of its 2 % bound on f32, goes over it)
-CONV6 = os.environ.get("SDREAMER_CONV6", "0") == "1"
+# SDREAMER_CONV6: the encoder stages' forward on the fp32-accurate three-way split-bf16 direct kernel
+# (sd_conv2d_fwd_pool6) instead of the exact f32 kernels. Default "s2": the second stage (32 -> 48 channels at 32 x 32,
+# 0.54 vs 0.68 ms; stage 3 on bf16x6 is slower: "1" takes every instantiated stage, "0" none). Round 6 measured its
+# parity against exact arithmetic (tools/precision_study.py over the golden cases' LaProp moments, profiles/r06f): it
+# sits as close to the float64 answer as the f32 kernels do (walker/r2aug first conv layer 0.013 vs 0.018 of the
+# golden bound; the reference's own f32 sits 0.502 from it), every golden update test passes; update 10.91 -> 10.79 ms.
+CONV6 = os.environ.get("SDREAMER_CONV6", "s2")
+CONV6 = CONV6 if CONV6 in ("1", "s2") else ""
 # SDREAMER_DIRECT_DGRAD=0: the encoder's bwd-data on the implicit-GEMM split-bf16 kernel (A/B knob)
 DIRECT_DGRAD = os.environ.get("SDREAMER_DIRECT_DGRAD", "1") != "0"
 
@@ -753,7 +801,7 @@ def conv2d_fwd_pool(x, w, b, nw, nchw_flat=False):
     amax = torch.empty(Nb, H // 2, W // 2, Co, dtype=torch.uint8, device=x.device)
     y = torch.empty_like(pooled)
     rstd = torch.empty(Nb, H // 2, W // 2, dtype=torch.float32, device=x.device)
-    if CONV6:  # fp32-accurate three-way split-bf16 direct kernel where instantiated
+    if CONV6 and (CONV6 == "1" or (Ci, Co) == (32, 48)):  # fp32-accurate three-way split-bf16 direct kernel
         K = kh * kw * Ci
         ws = torch.empty(3 * Co * (-(-K // 32) * 32), dtype=torch.int16, device=x.device)
         nat.call("sd_conv_split3_weight", p(_c(w)), p(ws), Co, K, stream())

@@ -301,7 +301,7 @@ def test_conv_pool_fused_matches_two_launches(ci, co, hw, nb, nchw, monkeypatch)
     k tiles' interleave: pooled within 1e-6, argmax equal except on near-ties. (The f32 kernels: the bf16x6 direct
     kernel has its own test below.)"""
     from sdreamer import kernels as K
-    monkeypatch.setattr(K, "CONV6", False)
+    monkeypatch.setattr(K, "CONV6", "")
     x = (torch.rand(nb, hw, hw, ci, generator=_g(ci)) - 0.5).to(DEV)
     w = (torch.randn(co, 5, 5, ci, generator=_g(co)) / (ci * 25) ** 0.5).to(DEV)
     b = (0.1 * torch.randn(co, generator=_g(1))).to(DEV)
@@ -671,9 +671,9 @@ def test_conv_pool_bf16x6_matches_f32(ci, co, hw, nb, nchw, monkeypatch):
     b = (0.1 * torch.randn(co, generator=_g(1))).to(DEV)
     nw = (1 + 0.1 * torch.randn(co, generator=_g(2))).to(DEV)
     x[0, 1, 1, 0] = float("nan")
-    monkeypatch.setattr(K, "CONV6", True)
+    monkeypatch.setattr(K, "CONV6", "1")
     six = K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)
-    monkeypatch.setattr(K, "CONV6", False)
+    monkeypatch.setattr(K, "CONV6", "")
     ref = K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)
     conv_abs = K.conv2d_fwd(x.abs().nan_to_num(), w.abs(), None)  # (nb, hw, hw, co) bound operand
     bound = 2e-6 * F.max_pool2d(conv_abs.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1) + 1e-7
@@ -736,6 +736,40 @@ def test_first_stage_pooled_wgrad_reordered_sums(ci, co, hw, nb):
     else:
         for a, r, what in zip(grads[0], grads[1], ("w", "b", "nw")):
             close(a, r, 2e-5, what)
+
+
+@pytest.mark.parametrize("nb", [3, 16])
+def test_first_stage_pooled_wgrad_bf16x3(nb, monkeypatch):
+    """sd_conv2d_wgrad_pool_bf16x3 (the first stage's bwd-weight on the split-bf16 direct kernel, pooled gradient routed
+    through the argmax while staged, 32-pixel steps dealt to the 8 waves) against the f32 pooled kernel on the same
+    (pooled gradient, argmax): the weight / bias gradients within the split-bf16 bound 4e-5 * sum |dy| |x| per element
+    (the bound the dense split-bf16 bwd-weight meets), the norm gradient (not a contraction) exact."""
+    from sdreamer import kernels as K
+    from sdreamer import ops
+    ci, co, hw = 4, 32, 64
+    x = torch.rand(nb, hw, hw, ci, generator=_g(15)).to(DEV) - 0.5
+    x[..., 3] = 0.0  # the padded fourth channel, as the encoder feeds it
+    if K.nat.fns["sd_conv2d_wgrad_pool_bf16x3_slabs"](nb, hw, hw, ci, co, 5, 5) <= 0:
+        pytest.skip("shape outside the split-bf16 pooled kernel")
+    grads = []
+    for x3 in (True, False):
+        monkeypatch.setattr(K, "WGRAD1_X3", x3)
+        w = (torch.randn(co, 5, 5, ci, generator=_g(16)) / (ci * 25) ** 0.5).to(DEV).requires_grad_()
+        b = (0.1 * torch.randn(co, generator=_g(17))).to(DEV).requires_grad_()
+        nw = (1 + 0.1 * torch.randn(co, generator=_g(18))).to(DEV).requires_grad_()
+        y = ops.ConvPoolNormFn.apply(x, w, b, nw, False)
+        gy = torch.randn(y.shape, generator=_g(19)).to(DEV)
+        y.backward(gy)
+        grads.append((w.grad.clone(), b.grad.clone(), nw.grad.clone()))
+        if not x3:  # the bound: the same contraction on |dy| and |x|, from the dense f32 path's expanded gradient
+            _, pooled, amax, rstd = K.conv2d_fwd_pool(x.contiguous(), w.detach(), b.detach(), nw.detach())
+            dconv = K.pool_rms_bwd(pooled, amax, nw.detach(), rstd, gy, hw, hw, torch.zeros_like(nw))
+            absw = K.conv2d_wgrad(x.abs(), dconv.abs(), 5, 5, fast=False)
+    assert torch.equal(grads[0][2], grads[1][2]), "nw"
+    bound = 4e-5 * absw + 1e-6
+    got = torch.cat([grads[0][0].reshape(co, -1), grads[0][1][:, None]], 1)
+    ref = torch.cat([grads[1][0].reshape(co, -1), grads[1][1][:, None]], 1)
+    assert ((got - ref).abs() - bound).max().item() <= 0, float(((got - ref).abs() / bound).max())
 
 
 def test_layout_copies_exact():

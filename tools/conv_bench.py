@@ -39,11 +39,11 @@ def main():
         K.set_flip_cache([w])  # the update's state: flipped + split weights cached ahead of the backward
 
         def fpool6():
-            K.CONV6 = True
+            K.CONV6 = "1"
             try:
                 return K.conv2d_fwd_pool(x, w, b, nw)
             finally:
-                K.CONV6 = False
+                K.CONV6 = ""
 
         del ws
         for name, fn in (("fwd", lambda: K.conv2d_fwd(x, w, b)), ("fpool", lambda: K.conv2d_fwd_pool(x, w, b, nw)),

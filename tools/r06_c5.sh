@@ -4,7 +4,7 @@
 # the scan's launch traces at D = 4096 for both, and the skeleton (tools/hip/persist_scan_proto, D = 2048 geometry)
 set -o pipefail
 O=gpurun_out/$1; mkdir -p $O
-timeout -k 10 120 tools/hip/persist_scan_proto > $O/proto.txt 2>&1 &&
+timeout -k 10 60 tools/hip/scan_floor_proto > $O/scan_floor.txt 2>&1 &&
 timeout -k 10 200 python3 tools/scan_trace.py dmc/memory_maze 16 256 > $O/c5_b16_scan_trace.txt 2>&1 &&
 timeout -k 10 200 python3 tools/scan_trace.py dmc/memory_maze 2 256 > $O/c5_b2_scan_trace.txt 2>&1 &&
 timeout -k 10 900 bash tools/profile_round.sh ${1}_c5b16 --config dmc/memory_maze > $O/prof_b16.log 2>&1 &&
