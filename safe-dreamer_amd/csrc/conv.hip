@@ -620,6 +620,122 @@ __global__ __launch_bounds__(256, 2) void conv_fwd6_direct_pool(GemmArgs g, Geom
                         nchw_flat);
 }
 
+// conv_fwd6_direct_pool with the weight through LDS (round 6): 256-pixel tiles on 512-thread workgroups, the input
+// patch staged once as three bf16 planes (as there), and the pre-split weight staged per 32-deep k chunk into a
+// double-buffered LDS ring shared by the 8 waves (conv_dgrad3_direct's ring, three planes) instead of every lane loading
+// its own fragments from L2 (0.9 MB of weight per 128-pixel tile: the L2 -> CU path bound the kernel, MFMA busy 0.37).
+// Same products in the same k order: bit-identical to conv_fwd6_direct_pool.
+template <int BN, int CI, int LW, int KS>
+__global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geom G, int lhw,
+                                                                  const __bf16* __restrict__ wsp, const float* nw,
+                                                                  float* pooled, uint8_t* amax, float* y, float* rstd,
+                                                                  float eps, int nchw_flat) {
+  constexpr int NTH = 512, TP = 256;
+  constexpr int W = 1 << LW, R = TP / W, PH = R + KS - 1, PW = W + KS - 1, CP = CI + 8, PAD = KS / 2;
+  constexpr int PLANE = PH * PW * CP, K = KS * KS * CI, NKC = (K + 31) / 32, KP = NKC * 32, TN = BN / 16;
+  constexpr int CI4 = CI / 4, NEL = PH * PW * CI4, NE = (NEL + NTH - 1) / NTH;
+  constexpr int BROW = 40, SB = 3 * BN * BROW, NPC = 3 * BN * 4, NPT = (NPC + NTH - 1) / NTH;  // ring: [plane][n][40]
+  static_assert(CI % 8 == 0 && TP % W == 0 && BN % 16 == 0, "geometry");
+  static_assert(TP * (BN + 1) * 4 <= 3 * PLANE * 2, "epilogue tile fits the patch area");
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  extern __shared__ __attribute__((aligned(16))) __bf16 patch6r[];  // [plane][PH][PW][CP], then the ring [2][SB]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, q = lane >> 4;
+  const int bm0 = blockIdx.x * TP, n = bm0 >> lhw, y0 = (bm0 & ((1 << lhw) - 1)) >> LW;
+  __bf16* bst = patch6r + 3 * PLANE;
+  bf16x8 br[NPT];
+  auto bload = [&](int kc) {  // piece i: plane i / (4 BN), row (i / 4) % BN, 16-B piece i % 4 of the chunk
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int i = tid + NTH * u;
+      if (i < NPC) br[u] = *reinterpret_cast<const bf16x8*>(wsp + (long)(i >> 2) * KP + 32 * kc + 8 * (i & 3));
+    }
+  };
+  auto bstore = [&](int st) {
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int i = tid + NTH * u;
+      if (i < NPC) *reinterpret_cast<bf16x8*>(bst + st * SB + (i >> 2) * BROW + 8 * (i & 3)) = br[u];
+    }
+  };
+  bload(0);
+  {
+    f32x4 v[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int i = tid + NTH * e, c4 = i % CI4, pix = i / CI4, pc = pix % PW, pr = pix / PW;
+      const int yy = y0 + pr - PAD, xx = pc - PAD;
+      v[e] = (i < NEL && (unsigned)yy < (unsigned)G.Hs && (unsigned)xx < (unsigned)W)
+                 ? *reinterpret_cast<const f32x4*>(G.in + (((long)n * G.Hs + yy) * W + xx) * CI + 4 * c4)
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int i = tid + NTH * e;
+      if (i < NEL) {
+        const int c4 = i % CI4, pix = i / CI4;
+        float h0, h1, h2, h3, m0, m1, m2, m3;
+        const u32x2 h{bf16_pair(v[e][0], v[e][1], h0, h1), bf16_pair(v[e][2], v[e][3], h2, h3)};
+        const float r0 = v[e][0] - h0, r1 = v[e][1] - h1, r2 = v[e][2] - h2, r3 = v[e][3] - h3;
+        const u32x2 m{bf16_pair(r0, r1, m0, m1), bf16_pair(r2, r3, m2, m3)};
+        const f32x4 l{r0 - m0, r1 - m1, r2 - m2, r3 - m3};
+        __bf16* dst = patch6r + pix * CP + 4 * c4;
+        *reinterpret_cast<u32x2*>(dst) = h;
+        *reinterpret_cast<u32x2*>(dst + PLANE) = m;
+        *reinterpret_cast<bf16x4*>(dst + 2 * PLANE) = __builtin_convertvector(l, bf16x4);
+      }
+    }
+  }
+  bstore(0);
+  if (NKC > 1) bload(1);
+  int pbase[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int p = 32 * wave + 16 * mt + l16;
+    pbase[mt] = ((p >> LW) * PW + (p & (W - 1))) * CP;
+  }
+  f32x4 acc[2][TN];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  for (int kc = 0; kc < NKC; ++kc) {
+    const __bf16* bs = bst + (kc & 1) * SB + l16 * BROW + 8 * q;
+    bf16x8 b[TN][3];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) b[j][pl] = *reinterpret_cast<const bf16x8*>(bs + (pl * BN + 16 * j) * BROW);
+    int k0 = 32 * kc + 8 * q;
+    k0 = k0 < K ? k0 : K - 8;  // past K: any in-patch address (the weight is zero there)
+    const int tap = k0 / CI, c0 = k0 - tap * CI, ky = tap / KS, kx = tap - ky * KS;
+    const int off = (ky * PW + kx) * CP + c0;
+    bf16x8 a[2][3];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[mt][pl] = *reinterpret_cast<const bf16x8*>(patch6r + pl * PLANE + pbase[mt] + off);
+    if (kc + 1 < NKC) bstore((kc + 1) & 1);  // chunk kc + 1 (loaded one iteration ago) into the other stage
+    if (kc + 2 < NKC) bload(kc + 2);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x4 c = acc[mt][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][2], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][1], b[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][0], b[j][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][1], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][0], b[j][1], c, 0, 0, 0);
+        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][0], b[j][0], c, 0, 0, 0);
+      }
+    __syncthreads();
+  }
+  pool_epilogue<BN, 32>(acc, reinterpret_cast<float*>(patch6r), g, G, LW, lhw, bm0, nw, pooled, amax, y, rstd, eps,
+                        nchw_flat);
+}
+
 // [plane][n][KP] three-way split-bf16 image (gemm6_core.h split) of a (rows, K) fp32 matrix, zero past K
 __global__ __launch_bounds__(256) void split3_weight(const float* __restrict__ w, __bf16* __restrict__ out, int rows,
                                                      int K, int KP) {
@@ -2090,10 +2206,31 @@ extern "C" int sd_conv_split3_weight(const float* w, void* wsplit, int rows, int
 }
 
 namespace {
+// SDHIP_CONV6_RING=0: the per-lane-weight kernel (conv_fwd6_direct_pool) instead of the LDS-ring one (A/B knob)
+bool conv6_ring() {  // read per call (host only): tests toggle it in-process
+  const char* e = getenv("SDHIP_CONV6_RING");
+  return e ? atoi(e) != 0 : true;
+}
 template <int BN, int CI, int LW>
 int fwd6_launch(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, const float* nw, float* pooled,
                 uint8_t* amax, float* y, float* rstd, float eps, int nchw_flat, hipStream_t s) {
   constexpr int W = 1 << LW, R = 128 / W, KS = 5;
+  constexpr int R2 = 256 / W;
+  constexpr size_t lds2 = (size_t)3 * (R2 + KS - 1) * (W + KS - 1) * (CI + 8) * 2 + (size_t)2 * 3 * BN * 40 * 2;
+  // (the 48 -> 64 stage at 16 x 16 needs 165 KB there: it keeps the per-lane kernel)
+  if (conv6_ring() && lds2 <= 160 * 1024 && g.M % 256 == 0 && G.Hs % R2 == 0) {
+    static bool raised2 = false;
+    if (!raised2) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_fwd6r_direct_pool<BN, CI, LW, KS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2) != hipSuccess)
+        return SD_EARG;
+      raised2 = true;
+    }
+    conv_fwd6r_direct_pool<BN, CI, LW, KS><<<g.M / 256, 512, lds2, s>>>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps,
+                                                                       nchw_flat);
+    SD_LAUNCH_CHECK();
+    return SD_OK;
+  }
   const size_t lds = (size_t)3 * (R + KS - 1) * (W + KS - 1) * (CI + 8) * 2;
   static bool raised = false;
   if (!raised && lds > 65536) {

@@ -687,6 +687,25 @@ def test_conv_pool_bf16x6_matches_f32(ci, co, hw, nb, nchw, monkeypatch):
     close(y6.nan_to_num(), yr.nan_to_num(), 1e-5, "y")
 
 
+@pytest.mark.parametrize("nb,nchw", [(4, False), (3, True)])
+def test_conv_pool_bf16x6_ring_bit_identical(nb, nchw, monkeypatch):
+    """The stage-2 bf16x6 forward with the weight through the LDS ring (conv_fwd6r_direct_pool, 256-pixel tiles)
+    against the per-lane-weight kernel (SDHIP_CONV6_RING=0, 128-pixel tiles): the same products in the same k order,
+    so every output is bit-identical."""
+    from sdreamer import kernels as K
+    ci, co, hw = 32, 48, 32
+    x = (torch.rand(nb, hw, hw, ci, generator=_g(21)) - 0.5).to(DEV)
+    w = (torch.randn(co, 5, 5, ci, generator=_g(22)) / (ci * 25) ** 0.5).to(DEV)
+    b = (0.1 * torch.randn(co, generator=_g(23))).to(DEV)
+    nw = (1 + 0.1 * torch.randn(co, generator=_g(24))).to(DEV)
+    monkeypatch.setattr(K, "CONV6", "s2")
+    ring = K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)
+    monkeypatch.setenv("SDHIP_CONV6_RING", "0")
+    lane = K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)
+    for a, r, what in zip(ring, lane, ("y", "pooled", "amax", "rstd")):
+        assert torch.equal(a, r), what
+
+
 @pytest.mark.parametrize("cd,ci,hw,nb", [(48, 32, 32, 8), (64, 48, 16, 16), (48, 32, 32, 1)])
 def test_conv_dgrad_direct_matches_implicit_gemm(cd, ci, hw, nb):
     """The direct bwd-data kernel (sd_conv2d_dgrad_direct: dOut patch staged once per workgroup) against the
