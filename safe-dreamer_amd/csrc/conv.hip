@@ -625,16 +625,24 @@ __global__ __launch_bounds__(256, 2) void conv_fwd6_direct_pool(GemmArgs g, Geom
 // double-buffered LDS ring shared by the 8 waves (conv_dgrad3_direct's ring, three planes) instead of every lane loading
 // its own fragments from L2 (0.9 MB of weight per 128-pixel tile: the L2 -> CU path bound the kernel, MFMA busy 0.37).
 // Same products in the same k order: bit-identical to conv_fwd6_direct_pool.
-template <int BN, int CI, int LW, int KS>
+// CG: the patch planes channel-group-major ([plane][CI / 8][PH * PW][8] bf16) instead of pixel-major with a pad: the 16
+// lanes of a fragment read 16 consecutive pixels' 16-B pieces (conflict-free with no pad), so the 48 -> 64 stage's
+// whole-image 256-pixel tile (20 x 20 x 48 patch) fits beside the ring (146 KB; pixel-major with its pad is 165 KB).
+// PIPE: the fragments of chunk kc + 1 are read from LDS into a second register set under chunk kc's MFMAs (the ring
+// stage chunk kc + 2 goes to is the one every wave finished reading before the previous barrier), so the LDS read
+// latency is no longer exposed once per chunk; one barrier per chunk either way, same products in the same order.
+template <int BN, int CI, int LW, int KS, bool CG, bool PIPE>
 __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geom G, int lhw,
                                                                   const __bf16* __restrict__ wsp, const float* nw,
                                                                   float* pooled, uint8_t* amax, float* y, float* rstd,
                                                                   float eps, int nchw_flat) {
   constexpr int NTH = 512, TP = 256;
-  constexpr int W = 1 << LW, R = TP / W, PH = R + KS - 1, PW = W + KS - 1, CP = CI + 8, PAD = KS / 2;
-  constexpr int PLANE = PH * PW * CP, K = KS * KS * CI, NKC = (K + 31) / 32, KP = NKC * 32, TN = BN / 16;
+  constexpr int W = 1 << LW, R = TP / W, PH = R + KS - 1, PW = W + KS - 1, CP = CG ? CI : CI + 8, PAD = KS / 2;
+  constexpr int NPIX = PH * PW, PLANE = NPIX * CP, K = KS * KS * CI, NKC = (K + 31) / 32, KP = NKC * 32, TN = BN / 16;
   constexpr int CI4 = CI / 4, NEL = PH * PW * CI4, NE = (NEL + NTH - 1) / NTH;
   constexpr int BROW = 40, SB = 3 * BN * BROW, NPC = 3 * BN * 4, NPT = (NPC + NTH - 1) / NTH;  // ring: [plane][n][40]
+  // element offset of (pixel, channel c, c % 4 == 0) in a plane
+  auto poff = [](int pix, int c) { return CG ? ((c >> 3) * NPIX + pix) * 8 + (c & 7) : pix * CP + c; };
   static_assert(CI % 8 == 0 && TP % W == 0 && BN % 16 == 0, "geometry");
   static_assert(TP * (BN + 1) * 4 <= 3 * PLANE * 2, "epilogue tile fits the patch area");
   typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -678,7 +686,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
         const float r0 = v[e][0] - h0, r1 = v[e][1] - h1, r2 = v[e][2] - h2, r3 = v[e][3] - h3;
         const u32x2 m{bf16_pair(r0, r1, m0, m1), bf16_pair(r2, r3, m2, m3)};
         const f32x4 l{r0 - m0, r1 - m1, r2 - m2, r3 - m3};
-        __bf16* dst = patch6r + pix * CP + 4 * c4;
+        __bf16* dst = patch6r + poff(pix, 4 * c4);
         *reinterpret_cast<u32x2*>(dst) = h;
         *reinterpret_cast<u32x2*>(dst + PLANE) = m;
         *reinterpret_cast<bf16x4*>(dst + 2 * PLANE) = __builtin_convertvector(l, bf16x4);
@@ -691,7 +699,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     const int p = 32 * wave + 16 * mt + l16;
-    pbase[mt] = ((p >> LW) * PW + (p & (W - 1))) * CP;
+    pbase[mt] = (p >> LW) * PW + (p & (W - 1));  // pixel index at tap (0, 0)
   }
   f32x4 acc[2][TN];
 #pragma unroll
@@ -699,6 +707,54 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
+  if constexpr (PIPE) {
+    bf16x8 a[2][2][3], b[2][TN][3];
+    auto frag = [&](int kc, int s) {  // chunk kc's fragments (ring stage kc & 1, the patch) into register set s
+      const __bf16* bs = bst + (kc & 1) * SB + l16 * BROW + 8 * q;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          b[s][j][pl] = *reinterpret_cast<const bf16x8*>(bs + (pl * BN + 16 * j) * BROW);
+      int k0 = 32 * kc + 8 * q;
+      k0 = k0 < K ? k0 : K - 8;  // past K: any in-patch address (the weight is zero there)
+      const int tap = k0 / CI, c0 = k0 - tap * CI, ky = tap / KS, kx = tap - ky * KS;
+      const int toff = ky * PW + kx;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          a[s][mt][pl] = *reinterpret_cast<const bf16x8*>(patch6r + pl * PLANE + poff(pbase[mt] + toff, c0));
+    };
+    frag(0, 0);
+    if (NKC > 1) bstore(1);  // chunk 1 (in br) into stage 1
+    if (NKC > 2) bload(2);
+    __syncthreads();  // chunk 1 visible; every wave's chunk-0 reads are done
+    auto step = [&](int kc, int s) {  // register set s holds chunk kc; stage (kc + 1) & 1 holds chunk kc + 1
+      if (kc + 1 < NKC) frag(kc + 1, s ^ 1);
+      if (kc + 2 < NKC) bstore(kc & 1);  // chunk kc + 2 (in br) over chunk kc, read before the last barrier
+      if (kc + 3 < NKC) bload(kc + 3);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          f32x4 c = acc[mt][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s][mt][2], b[s][j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s][mt][1], b[s][j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s][mt][0], b[s][j][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s][mt][1], b[s][j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s][mt][0], b[s][j][1], c, 0, 0, 0);
+          acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s][mt][0], b[s][j][0], c, 0, 0, 0);
+        }
+      __syncthreads();
+    };
+    int kc = 0;
+    for (; kc + 2 <= NKC; kc += 2) {
+      step(kc, 0);
+      step(kc + 1, 1);
+    }
+    if (kc < NKC) step(kc, 0);
+  } else
   for (int kc = 0; kc < NKC; ++kc) {
     const __bf16* bs = bst + (kc & 1) * SB + l16 * BROW + 8 * q;
     bf16x8 b[TN][3];
@@ -709,13 +765,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
     int k0 = 32 * kc + 8 * q;
     k0 = k0 < K ? k0 : K - 8;  // past K: any in-patch address (the weight is zero there)
     const int tap = k0 / CI, c0 = k0 - tap * CI, ky = tap / KS, kx = tap - ky * KS;
-    const int off = (ky * PW + kx) * CP + c0;
+    const int toff = ky * PW + kx;
     bf16x8 a[2][3];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        a[mt][pl] = *reinterpret_cast<const bf16x8*>(patch6r + pl * PLANE + pbase[mt] + off);
+        a[mt][pl] = *reinterpret_cast<const bf16x8*>(patch6r + pl * PLANE + poff(pbase[mt] + toff, c0));
     if (kc + 1 < NKC) bstore((kc + 1) & 1);  // chunk kc + 1 (loaded one iteration ago) into the other stage
     if (kc + 2 < NKC) bload(kc + 2);
 #pragma unroll
@@ -2211,26 +2267,40 @@ bool conv6_ring() {  // read per call (host only): tests toggle it in-process
   const char* e = getenv("SDHIP_CONV6_RING");
   return e ? atoi(e) != 0 : true;
 }
+// SDHIP_CONV6_PIPE=0: the ring kernel without the fragment register pipeline (A/B knob)
+bool conv6_pipe() {
+  const char* e = getenv("SDHIP_CONV6_PIPE");
+  return e ? atoi(e) != 0 : true;
+}
+template <int BN, int CI, int LW, int KS, bool CG, bool PIPE>
+int fwd6r_launch(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, const float* nw, float* pooled,
+                 uint8_t* amax, float* y, float* rstd, float eps, int nchw_flat, size_t lds, hipStream_t s) {
+  static bool raised = false;
+  if (!raised) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return SD_EARG;
+    raised = true;
+  }
+  conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE><<<g.M / 256, 512, lds, s>>>(g, G, lhw, wsp, nw, pooled, amax, y,
+                                                                              rstd, eps, nchw_flat);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
 template <int BN, int CI, int LW>
 int fwd6_launch(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, const float* nw, float* pooled,
                 uint8_t* amax, float* y, float* rstd, float eps, int nchw_flat, hipStream_t s) {
   constexpr int W = 1 << LW, R = 128 / W, KS = 5;
   constexpr int R2 = 256 / W;
-  constexpr size_t lds2 = (size_t)3 * (R2 + KS - 1) * (W + KS - 1) * (CI + 8) * 2 + (size_t)2 * 3 * BN * 40 * 2;
-  // (the 48 -> 64 stage at 16 x 16 needs 165 KB there: it keeps the per-lane kernel)
-  if (conv6_ring() && lds2 <= 160 * 1024 && g.M % 256 == 0 && G.Hs % R2 == 0) {
-    static bool raised2 = false;
-    if (!raised2) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_fwd6r_direct_pool<BN, CI, LW, KS>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2) != hipSuccess)
-        return SD_EARG;
-      raised2 = true;
-    }
-    conv_fwd6r_direct_pool<BN, CI, LW, KS><<<g.M / 256, 512, lds2, s>>>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps,
-                                                                       nchw_flat);
-    SD_LAUNCH_CHECK();
-    return SD_OK;
-  }
+  // pixel-major patch with its pad where it fits (stage 2), channel-group-major otherwise (stage 3: 165 vs 146 KB)
+  constexpr bool CG = (size_t)3 * (R2 + KS - 1) * (W + KS - 1) * (CI + 8) * 2 + (size_t)2 * 3 * BN * 40 * 2 > 160 * 1024;
+  constexpr size_t lds2 =
+      (size_t)3 * (R2 + KS - 1) * (W + KS - 1) * (CG ? CI : CI + 8) * 2 + (size_t)2 * 3 * BN * 40 * 2;
+  if (conv6_ring() && lds2 <= 160 * 1024 && g.M % 256 == 0 && G.Hs % R2 == 0)
+    return conv6_pipe() ? fwd6r_launch<BN, CI, LW, KS, CG, true>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps,
+                                                                 nchw_flat, lds2, s)
+                        : fwd6r_launch<BN, CI, LW, KS, CG, false>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps,
+                                                                  nchw_flat, lds2, s);
   const size_t lds = (size_t)3 * (R + KS - 1) * (W + KS - 1) * (CI + 8) * 2;
   static bool raised = false;
   if (!raised && lds > 65536) {

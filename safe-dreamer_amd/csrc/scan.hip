@@ -1115,7 +1115,9 @@ __global__ __launch_bounds__(NTHR) void k_dx01(sd_rssm_scan d, Work w, int t) {
 // The A operand d_x0p (carry_h workgroups) / d_x1p (carry_s workgroups) is built by the prologue, as k_dx01 builds it:
 // sum of the G d_xcat slabs of k_dhp + the _dyn_in0 / _dyn_in1 RMSNorm-SiLU backward, 16 rows into an LDS panel. The
 // first workgroup of each half also writes its d_xcat part and d_x0p / d_x1p (read by the deferred weight gradients);
-// the second carry_h workgroup writes the x2 part of d_xcat. So k_dx01 runs only at t = 0 (no k_carry there).
+// one extra workgroup (the last) writes the x2 part of d_xcat and does nothing else, so the others hold no registers
+// for it (188 -> 128 VGPRs: two workgroups per CU, so deter 4096's 288 workgroups run as one round instead of two).
+// So k_dx01 runs only at t = 0 (no k_carry there).
 template <int KD>
 __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   extern __shared__ float smem[];
@@ -1124,6 +1126,23 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   SD_ROW_TILE
   constexpr int NT = KD / 16, NE = (MR * KD + NTHR - 1) / NTHR, GM = 8, X = 3 * UH, ldp = UH + 4;
   const int B = d.B, D = d.D, SK = d.SK, S = SK / KD;
+  if ((int)blockIdx.x == D / KD + SK / KD) {  // the x2 part of d_xcat: sum of k_dhp's slabs (k_dx01's order)
+    const int row = tid >> 5, t32 = tid & 31, gr = rb + row, KX = kx_of(d.G);
+    const int grc = row < nr ? gr : rb + nr - 1;
+    const long tB = (long)t * B;
+    f32x4 part2[GM][NU], dx[NU];
+#pragma unroll
+    for (int g = 0; g < GM; ++g) ld_row(part2[g], w.dxs + (long)(g < KX ? g : KX - 1) * B * X + (long)grc * X + 2 * UH, t32);
+    sum_slabs(dx, part2, KX);
+    if (row < nr) {
+      st_row(d.d_xcat + (tB + gr) * X + 2 * UH, dx, UH, t32);
+      if (d.d_x2_bm) st_row(d.d_x2_bm + ((long)gr * d.T + t) * UH, dx, UH, t32);
+    }
+    SD_TR(1)
+    SD_TR(2)
+    SD_TR_END(d.trace, d.trace_slot)
+    return;
+  }
   const bool p0 = (int)blockIdx.x < D / KD;
   const int wid = p0 ? xcd_tile(blockIdx.x, D / KD) : xcd_tile(blockIdx.x - D / KD, SK / KD), n0 = wid * KD;
   Core<NT, 2> core;
@@ -1138,8 +1157,7 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
   const int grc = rv ? gr : rb + nr - 1, KX = kx_of(d.G);
   const long tB = (long)t * B;
   const int hoff = p0 ? 0 : UH;
-  const bool wx2 = p0 && wid == 1;  // the x2 part's writer
-  f32x4 part[GM][NU], part2[GM][NU], xv[NU], nv[NU];
+  f32x4 part[GM][NU], xv[NU], nv[NU];
 #pragma unroll
   for (int g = 0; g < GM; ++g) ld_row(part[g], w.dxs + (long)(g < KX ? g : KX - 1) * B * X + (long)grc * X + hoff, t32);
   const float rr_ = (p0 ? d.r0 : d.r1)[tB + grc];
@@ -1161,10 +1179,6 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
     e1[k].load(d, d.d_stoch, d.d_stoch2, tp, gerc, cs, SK, w.ch);
     e2[k].load(d, d.d_logit, nullptr, tp, gerc, cs, SK, w.ch);
   }
-  if (wx2) {  // (last: the branch may drain the queue, which then holds only loads needed anyway)
-#pragma unroll
-    for (int g = 0; g < GM; ++g) ld_row(part2[g], w.dxs + (long)(g < KX ? g : KX - 1) * B * X + (long)grc * X + 2 * UH, t32);
-  }
   const float rr = rv ? rr_ : 0.f;
   bool rs[NE];
 #pragma unroll
@@ -1185,15 +1199,8 @@ __global__ __launch_bounds__(NTHR) void k_carry(sd_rssm_scan d, Work w, int t) {
     for (int k = 0; k < NE; ++k)
       if (tid + NTHR * k < MR * KD) sf[k] = sampler_fwd<KD>(e0[k], gn[k], d.unimix, (tid + NTHR * k) % KD);
   }
-  // d_xcat part = sum of the slabs (k_dx01's order); the x2 writer stores its part first
+  // d_xcat part = sum of the slabs (k_dx01's order)
   f32x4 dx[NU];
-  if (wx2) {
-    sum_slabs(dx, part2, KX);
-    if (rv) {
-      st_row(d.d_xcat + (tB + gr) * X + 2 * UH, dx, UH, t32);
-      if (d.d_x2_bm) st_row(d.d_x2_bm + ((long)gr * d.T + t) * UH, dx, UH, t32);
-    }
-  }
   sum_slabs(dx, part, KX);
   float dot = 0.f;
   f32x4 gg[NU], xh[NU];
@@ -1468,7 +1475,7 @@ extern "C" int sd_rssm_scan_bwd(const sd_rssm_scan* dp, sd_stream stream_) {
     SD_LAUNCH_CHECK();
     d.trace_slot = (d.T + t) * 8 + 4;
     if (t > 0) {  // k_carry builds d_x0p / d_x1p itself (the k_dx01 work in its prologue)
-      SD_KD_SWITCH(d.Kd, k_carry<KD><<<dim3(D / KD + SK / KD, 1, nt), NTHR,
+      SD_KD_SWITCH(d.Kd, k_carry<KD><<<dim3(D / KD + SK / KD + 1, 1, nt), NTHR,
                                        core_lds_floats<KD / 16>() * 4 + (size_t)MR * (UH + 4) * 4, st>>>(d, w, t));
     } else {
       k_dx01<<<B, NTHR, 0, st>>>(d, w, t);

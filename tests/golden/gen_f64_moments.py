@@ -8,6 +8,8 @@ reference's f32 run (the golden) and the product approximate: tests/test_gpu_dre
 distance from them, and tools/grad_attrib.py shows the reference's. Posterior indices must equal the golden's
 (no near-tie flips at these sizes), else the case is skipped.
   python tests/golden/gen_f64_moments.py [case ...]   -> tests/golden/f64/<case>.npz
+  python tests/golden/gen_f64_moments.py --grads [case ...]   adds g_<tensor>__n / __s: the float64 gradients of one
+      _cal_grad at the initial weights, sampled like the golden's g_* (tests/test_gpu_dreamer.py's gradient test)
 """
 import os
 import sys
@@ -47,8 +49,42 @@ def moments(name, dt):
         ref_cpu.DT = torch.float32
 
 
+def grads(name, dt):
+    """{g_<tensor>__n, g_<tensor>__s}: one cal_grad at the initial weights (as the golden's g_*, gen_golden.py)"""
+    ref_cpu.DT = dt
+    try:
+        z, cfg, spec, params, obs = load_case(name)
+        ag = ref_cpu.OracleAgent(spec, params)
+        cast = lambda t: t.to(dt) if torch.is_tensor(t) and t.is_floating_point() else t  # noqa: E731
+        ag.update_slow_target()
+        if spec.rep_loss == "dreamerpro":
+            ag.ema_update()
+        data = {k: cast(v) for k, v in batch(z, 0, obs).items()}
+        init = type(initial(z, 0, spec))(cast(t) for t in initial(z, 0, spec))
+        ag.cal_grad(data, init, int(z["u0_seed"]))
+        out = {}
+        for k in spec.shapes:
+            g = ag.P[k].grad
+            flat = (torch.zeros_like(ag.P[k]) if g is None else g).reshape(-1).double().numpy()
+            out[f"g_{k}__n"] = np.asarray(np.linalg.norm(flat))
+            out[f"g_{k}__s"] = flat[sample_idx(k, flat.size)]
+        return out
+    finally:
+        ref_cpu.DT = torch.float32
+
+
 def main():
     torch.set_num_threads(8)
+    if sys.argv[1:2] == ["--grads"]:
+        for name in sys.argv[2:] or list(CASES):
+            fx = os.path.join(HERE, "f64", f"{name}.npz")
+            if not os.path.exists(fx):
+                continue
+            arrs = dict(np.load(fx))
+            arrs.update(grads(name, torch.float64))
+            np.savez_compressed(fx, **arrs)
+            print(f"{name}: {len(arrs)} arrays")
+        return
     for name in sys.argv[1:] or list(CASES):
         res = moments(name, torch.float64)
         if any(f for _, f in res):

@@ -687,18 +687,18 @@ def test_conv_pool_bf16x6_matches_f32(ci, co, hw, nb, nchw, monkeypatch):
     close(y6.nan_to_num(), yr.nan_to_num(), 1e-5, "y")
 
 
-@pytest.mark.parametrize("nb,nchw", [(4, False), (3, True)])
-def test_conv_pool_bf16x6_ring_bit_identical(nb, nchw, monkeypatch):
-    """The stage-2 bf16x6 forward with the weight through the LDS ring (conv_fwd6r_direct_pool, 256-pixel tiles)
-    against the per-lane-weight kernel (SDHIP_CONV6_RING=0, 128-pixel tiles): the same products in the same k order,
-    so every output is bit-identical."""
+@pytest.mark.parametrize("ci,co,hw,nb,nchw", [(32, 48, 32, 4, False), (32, 48, 32, 3, True), (48, 64, 16, 5, True),
+                                               (48, 64, 16, 2, False)])
+def test_conv_pool_bf16x6_ring_bit_identical(ci, co, hw, nb, nchw, monkeypatch):
+    """The bf16x6 stage forward with the weight through the LDS ring (conv_fwd6r_direct_pool, 256-pixel tiles; the
+    48 -> 64 stage on the channel-group-major patch) against the per-lane-weight kernel (SDHIP_CONV6_RING=0, 128-pixel
+    tiles): the same products in the same k order, so every output is bit-identical."""
     from sdreamer import kernels as K
-    ci, co, hw = 32, 48, 32
     x = (torch.rand(nb, hw, hw, ci, generator=_g(21)) - 0.5).to(DEV)
     w = (torch.randn(co, 5, 5, ci, generator=_g(22)) / (ci * 25) ** 0.5).to(DEV)
     b = (0.1 * torch.randn(co, generator=_g(23))).to(DEV)
     nw = (1 + 0.1 * torch.randn(co, generator=_g(24))).to(DEV)
-    monkeypatch.setattr(K, "CONV6", "s2")
+    monkeypatch.setattr(K, "CONV6", "1")
     ring = K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)
     monkeypatch.setenv("SDHIP_CONV6_RING", "0")
     lane = K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)
