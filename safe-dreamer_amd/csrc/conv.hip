@@ -631,7 +631,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd6_direct_pool(GemmArgs g, Geom
 // PIPE: the fragments of chunk kc + 1 are read from LDS into a second register set under chunk kc's MFMAs (the ring
 // stage chunk kc + 2 goes to is the one every wave finished reading before the previous barrier), so the LDS read
 // latency is no longer exposed once per chunk; one barrier per chunk either way, same products in the same order.
-template <int BN, int CI, int LW, int KS, bool CG, bool PIPE>
+// TPW: a workgroup runs TPW consecutive tiles (XCD-contiguous ranges, so the halo rows adjacent tiles share are L2
+// hits), the next tile's patch loaded into registers under this tile's MFMAs and the ring's first chunk under its
+// epilogue: with one workgroup per CU the prologue's HBM round trip was otherwise exposed once per tile.
+template <int BN, int CI, int LW, int KS, bool CG, bool PIPE, int TPW>
 __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geom G, int lhw,
                                                                   const __bf16* __restrict__ wsp, const float* nw,
                                                                   float* pooled, uint8_t* amax, float* y, float* rstd,
@@ -648,7 +651,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
   typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
   extern __shared__ __attribute__((aligned(16))) __bf16 patch6r[];  // [plane][PH][PW][CP], then the ring [2][SB]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, q = lane >> 4;
-  const int bm0 = blockIdx.x * TP, n = bm0 >> lhw, y0 = (bm0 & ((1 << lhw) - 1)) >> LW;
+  const int nwg = gridDim.x, ntiles = g.M / TP;
+  const int wg = (nwg & 7) ? blockIdx.x : (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
   __bf16* bst = patch6r + 3 * PLANE;
   bf16x8 br[NPT];
   auto bload = [&](int kc) {  // piece i: plane i / (4 BN), row (i / 4) % BN, 16-B piece i % 4 of the chunk
@@ -665,17 +669,19 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
       if (i < NPC) *reinterpret_cast<bf16x8*>(bst + st * SB + (i >> 2) * BROW + 8 * (i & 3)) = br[u];
     }
   };
-  bload(0);
-  {
-    f32x4 v[NE];
+  f32x4 v[NE];
+  auto load_patch = [&](int tile) {
+    const int bm0 = tile * TP, n = bm0 >> lhw, y0 = (bm0 & ((1 << lhw) - 1)) >> LW;
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
       const int i = tid + NTH * e, c4 = i % CI4, pix = i / CI4, pc = pix % PW, pr = pix / PW;
       const int yy = y0 + pr - PAD, xx = pc - PAD;
-      v[e] = (i < NEL && (unsigned)yy < (unsigned)G.Hs && (unsigned)xx < (unsigned)W)
+      v[e] = (i < NEL && tile < ntiles && (unsigned)yy < (unsigned)G.Hs && (unsigned)xx < (unsigned)W)
                  ? *reinterpret_cast<const f32x4*>(G.in + (((long)n * G.Hs + yy) * W + xx) * CI + 4 * c4)
                  : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+  };
+  auto store_patch = [&]() {
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
       const int i = tid + NTH * e;
@@ -692,21 +698,29 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
         *reinterpret_cast<bf16x4*>(dst + 2 * PLANE) = __builtin_convertvector(l, bf16x4);
       }
     }
-  }
-  bstore(0);
-  if (NKC > 1) bload(1);
+  };
   int pbase[2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     const int p = 32 * wave + 16 * mt + l16;
     pbase[mt] = (p >> LW) * PW + (p & (W - 1));  // pixel index at tap (0, 0)
   }
+  bload(0);
+  load_patch(wg * TPW);
+  for (int it = 0; it < TPW; ++it) {
+  const int tile = wg * TPW + it;
+  if (tile >= ntiles) break;  // uniform over the workgroup
+  if (it > 0) __syncthreads();  // the previous tile's epilogue is done with the patch area
+  store_patch();
+  bstore(0);
+  if (NKC > 1) bload(1);
   f32x4 acc[2][TN];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
+  if (it + 1 < TPW) load_patch(tile + 1);
   if constexpr (PIPE) {
     bf16x8 a[2][2][3], b[2][TN][3];
     auto frag = [&](int kc, int s) {  // chunk kc's fragments (ring stage kc & 1, the patch) into register set s
@@ -788,8 +802,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
       }
     __syncthreads();
   }
-  pool_epilogue<BN, 32>(acc, reinterpret_cast<float*>(patch6r), g, G, LW, lhw, bm0, nw, pooled, amax, y, rstd, eps,
-                        nchw_flat);
+  if (it + 1 < TPW) bload(0);  // the next tile's first weight chunk (the same weights) under the epilogue
+  pool_epilogue<BN, 32>(acc, reinterpret_cast<float*>(patch6r), g, G, LW, lhw, tile * TP, nw, pooled, amax, y, rstd,
+                        eps, nchw_flat);
+  }
 }
 
 // [plane][n][KP] three-way split-bf16 image (gemm6_core.h split) of a (rows, K) fp32 matrix, zero past K
@@ -2267,25 +2283,42 @@ bool conv6_ring() {  // read per call (host only): tests toggle it in-process
   const char* e = getenv("SDHIP_CONV6_RING");
   return e ? atoi(e) != 0 : true;
 }
-// SDHIP_CONV6_PIPE=0: the ring kernel without the fragment register pipeline (A/B knob)
+// SDHIP_CONV6_PIPE=1: the ring kernel with the fragment register pipeline, one tile per workgroup (A/B knob; 1 %
+// faster alone than without it, profiles/r06s3b, and slower than the prefetching multi-tile workgroups)
 bool conv6_pipe() {
   const char* e = getenv("SDHIP_CONV6_PIPE");
-  return e ? atoi(e) != 0 : true;
+  return e ? atoi(e) != 0 : false;
 }
-template <int BN, int CI, int LW, int KS, bool CG, bool PIPE>
-int fwd6r_launch(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, const float* nw, float* pooled,
-                 uint8_t* amax, float* y, float* rstd, float eps, int nchw_flat, size_t lds, hipStream_t s) {
+template <int BN, int CI, int LW, int KS, bool CG, bool PIPE, int TPW>
+int fwd6r_launch_t(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, const float* nw, float* pooled,
+                   uint8_t* amax, float* y, float* rstd, float eps, int nchw_flat, size_t lds, hipStream_t s) {
   static bool raised = false;
   if (!raised) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE, TPW>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return SD_EARG;
     raised = true;
   }
-  conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE><<<g.M / 256, 512, lds, s>>>(g, G, lhw, wsp, nw, pooled, amax, y,
-                                                                              rstd, eps, nchw_flat);
+  const int nwg = (sd_cdiv(g.M / 256, TPW) + 7) / 8 * 8;  // a multiple of 8: XCD-contiguous tile ranges
+  conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE, TPW><<<nwg, 512, lds, s>>>(g, G, lhw, wsp, nw, pooled, amax, y,
+                                                                             rstd, eps, nchw_flat);
   SD_LAUNCH_CHECK();
   return SD_OK;
+}
+// SDHIP_CONV6_TPW: tiles per workgroup (1, 2, 4, 8, 16); default: enough for one workgroup per CU, at most 16.
+// (The fragment pipeline, SDHIP_CONV6_PIPE=1, runs one tile per workgroup: with the prefetched patch it spills.)
+template <int BN, int CI, int LW, int KS, bool CG>
+int fwd6r_launch(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, const float* nw, float* pooled,
+                 uint8_t* amax, float* y, float* rstd, float eps, int nchw_flat, size_t lds, hipStream_t s) {
+  if (conv6_pipe())
+    return fwd6r_launch_t<BN, CI, LW, KS, CG, true, 1>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps, nchw_flat, lds,
+                                                       s);
+  const char* e = getenv("SDHIP_CONV6_TPW");
+  const int want = e ? atoi(e) : sd_cdiv(g.M / 256, 256);
+#define SD_F6R(T) \
+  fwd6r_launch_t<BN, CI, LW, KS, CG, false, T>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps, nchw_flat, lds, s)
+  return want <= 1 ? SD_F6R(1) : want <= 2 ? SD_F6R(2) : want <= 4 ? SD_F6R(4) : want <= 8 ? SD_F6R(8) : SD_F6R(16);
+#undef SD_F6R
 }
 template <int BN, int CI, int LW>
 int fwd6_launch(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, const float* nw, float* pooled,
@@ -2297,10 +2330,7 @@ int fwd6_launch(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, co
   constexpr size_t lds2 =
       (size_t)3 * (R2 + KS - 1) * (W + KS - 1) * (CG ? CI : CI + 8) * 2 + (size_t)2 * 3 * BN * 40 * 2;
   if (conv6_ring() && lds2 <= 160 * 1024 && g.M % 256 == 0 && G.Hs % R2 == 0)
-    return conv6_pipe() ? fwd6r_launch<BN, CI, LW, KS, CG, true>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps,
-                                                                 nchw_flat, lds2, s)
-                        : fwd6r_launch<BN, CI, LW, KS, CG, false>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps,
-                                                                  nchw_flat, lds2, s);
+    return fwd6r_launch<BN, CI, LW, KS, CG>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps, nchw_flat, lds2, s);
   const size_t lds = (size_t)3 * (R + KS - 1) * (W + KS - 1) * (CI + 8) * 2;
   static bool raised = false;
   if (!raised && lds > 65536) {

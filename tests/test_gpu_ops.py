@@ -692,18 +692,27 @@ def test_conv_pool_bf16x6_matches_f32(ci, co, hw, nb, nchw, monkeypatch):
 def test_conv_pool_bf16x6_ring_bit_identical(ci, co, hw, nb, nchw, monkeypatch):
     """The bf16x6 stage forward with the weight through the LDS ring (conv_fwd6r_direct_pool, 256-pixel tiles; the
     48 -> 64 stage on the channel-group-major patch) against the per-lane-weight kernel (SDHIP_CONV6_RING=0, 128-pixel
-    tiles): the same products in the same k order, so every output is bit-identical."""
+    tiles), one tile or several per workgroup, with or without the fragment pipeline: the same products in the same k
+    order, so every output is bit-identical."""
     from sdreamer import kernels as K
     x = (torch.rand(nb, hw, hw, ci, generator=_g(21)) - 0.5).to(DEV)
     w = (torch.randn(co, 5, 5, ci, generator=_g(22)) / (ci * 25) ** 0.5).to(DEV)
     b = (0.1 * torch.randn(co, generator=_g(23))).to(DEV)
     nw = (1 + 0.1 * torch.randn(co, generator=_g(24))).to(DEV)
     monkeypatch.setattr(K, "CONV6", "1")
-    ring = K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)
+    rings = [K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)]
+    for tpw in ("3", "16"):  # multi-tile workgroups (the bench's default), ragged tile ranges, idle workgroups
+        monkeypatch.setenv("SDHIP_CONV6_TPW", tpw)
+        rings.append(K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw))
+    monkeypatch.delenv("SDHIP_CONV6_TPW")
+    monkeypatch.setenv("SDHIP_CONV6_PIPE", "1")
+    rings.append(K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw))
+    monkeypatch.delenv("SDHIP_CONV6_PIPE")
     monkeypatch.setenv("SDHIP_CONV6_RING", "0")
     lane = K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw)
-    for a, r, what in zip(ring, lane, ("y", "pooled", "amax", "rstd")):
-        assert torch.equal(a, r), what
+    for ring in rings:
+        for a, r, what in zip(ring, lane, ("y", "pooled", "amax", "rstd")):
+            assert torch.equal(a, r), what
 
 
 @pytest.mark.parametrize("cd,ci,hw,nb", [(48, 32, 32, 8), (64, 48, 16, 16), (48, 32, 32, 1)])

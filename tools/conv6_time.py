@@ -1,7 +1,7 @@
 """Encoder stage forward, per kernel variant, at the bench's B*L = 1024 images (GPU box, measurement aid):
-exact f32 (sd_conv2d_fwd_pool), bf16x6 per-lane weight (SDHIP_CONV6_RING=0) and bf16x6 LDS ring (without / with
-the fragment pipeline, SDHIP_CONV6_PIPE), for the 32 -> 48
-stage at 32 x 32 and the 48 -> 64 stage at 16 x 16. Prints median us of back-to-back launches.
+exact f32 (sd_conv2d_fwd_pool), bf16x6 per-lane weight (SDHIP_CONV6_RING=0) and bf16x6 LDS ring, for the 32 -> 48
+stage at 32 x 32 and the 48 -> 64 stage at 16 x 16; the ring kernel one tile per workgroup (with / without the
+fragment pipeline) and with its default multi-tile workgroups (SDHIP_CONV6_TPW). Prints median us of back-to-back launches.
   python tools/conv6_time.py"""
 import os
 import sys
@@ -36,11 +36,17 @@ def main():
         b = torch.zeros(co).cuda()
         nw = torch.ones(co).cuda()
         res = {}
-        for name, c6, ring, pipe in [("f32", "", "1", "1"), ("bf16x6 lane", "1", "0", "1"),
-                                     ("bf16x6 ring nopipe", "1", "1", "0"), ("bf16x6 ring", "1", "1", "1")]:
+        for name, c6, ring, pipe, tpw in [("f32", "", "1", "0", ""), ("bf16x6 lane", "1", "0", "0", ""),
+                                          ("bf16x6 ring pipe 1 tile", "1", "1", "1", ""),
+                                          ("bf16x6 ring 1 tile", "1", "1", "0", "1"),
+                                          ("bf16x6 ring", "1", "1", "0", "")]:
             K.CONV6 = c6
             os.environ["SDHIP_CONV6_RING"] = ring
             os.environ["SDHIP_CONV6_PIPE"] = pipe
+            if tpw:
+                os.environ["SDHIP_CONV6_TPW"] = tpw
+            else:
+                os.environ.pop("SDHIP_CONV6_TPW", None)
             res[name] = timeit(lambda: K.conv2d_fwd_pool(x, w, b, nw))
         flop = 2 * 1024 * hw * hw * co * 25 * ci
         print(f"stage {ci}->{co} at {hw}x{hw}: " + "  ".join(f"{k} {v:.1f} us" for k, v in res.items()) +

@@ -1,0 +1,13 @@
+#!/bin/bash
+# The 4-channel first stage on bf16x6 (conv_fwd6_c4_pool): kernel tests, per-stage timing, the golden update /
+# gradient tests, then a same-box A/B against the f32 first stage (SDHIP_CONV6_C4=0). Usage: bash tools/r06_s1.sh <tag>
+set -o pipefail
+O=gpurun_out/$1; mkdir -p $O
+T="--timeout 300 --timeout-method thread"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -k "bf16x6" -q $T > $O/tests_ops.txt 2>&1 &&
+timeout -k 10 200 python3 tools/conv6_time.py > $O/conv6_time.txt 2>&1 &&
+SDREAMER_GOLDEN_REPORT=$O/rep timeout -k 10 600 python -u -m pytest tests/test_gpu_dreamer.py \
+  -k "test_update_matches_reference or test_cal_grad_matches_reference" -q -s $T > $O/tests_golden.txt 2>&1
+rc=$?; [ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python3 tools/dump_opt.py $O/c6c4 > $O/dump_c6c4.txt 2>&1 &&
+timeout -k 10 900 bash tools/ab_env.sh 2 "" "SDHIP_CONV6_C4=0" > $O/ab.txt 2>&1
