@@ -341,8 +341,11 @@ def probe_specs(agent, cfg, K):
     if K.ops_fused_pool():
         pix = N * 32 * 32
         c6 = bool(K.CONV6)
-        add("conv_stage2", "conv_fwd6r_direct_pool<48, 32, 5, 5, false, true>" if c6 else
-            "conv_fwd_direct_pool<48, 32, 5, 5, 1>", (N * 32 * 32 // (256 if c6 else 128), 1, 1), "mfma", 2.0 * pix * 48 * 25 * 32, 4.0 * pix * 32 + N * 16 * 16 * (48 * 9 + 4),
+        tiles = N * 32 * 32 // 256  # the ring kernel's 256-pixel tiles, dealt to one workgroup per CU (<= 16 each)
+        tpw = next(t for t in (1, 2, 4, 8, 16) if t >= min(-(-tiles // 256), 16))
+        add("conv_stage2", f"conv_fwd6r_direct_pool<48, 32, 5, 5, false, false, {tpw}>" if c6 else
+            "conv_fwd_direct_pool<48, 32, 5, 5, 1>", ((-(-tiles // tpw) + 7) // 8 * 8 if c6 else N * 32 * 32 // 128,
+                                                       1, 1), "mfma", 2.0 * pix * 48 * 25 * 32, 4.0 * pix * 32 + N * 16 * 16 * (48 * 9 + 4),
             cp.label, ("launch", cp), 1, peak=PEAK_BF16X6 if c6 else None, alt_peak=PEAK_FP32_MFMA if c6 else None)
     # encoder stage 2 bwd-data (split-bf16 direct conv from a pre-split dOut patch in LDS): sd_conv2d_dgrad_direct(dout,
     # wsplit, din, Nb, Hs, Ws, Ci = dout channels, Co = din channels, kh, kw, pad, stream)
