@@ -223,7 +223,7 @@ def wm_loss_parity_full(name="C2_walker_r2"):
 # The committed kernel table of this build (tools/profile_round.sh -> tools/kernel_table.py: the rocprofv3 kernel trace
 # of a bench run, windowed to its timed steps, joined with the separate --pmc passes). Named explicitly, never "the
 # newest file": its rows rank the update's launch shapes by time per update and carry their counter traffic.
-KERNEL_TABLE = "profiles/r05zy_kernel_table.json"
+KERNEL_TABLE = "profiles/r06final/r06final_kernel_table.json"
 
 
 def clock_probe(nwg=256, iters=20000, reps=3):
