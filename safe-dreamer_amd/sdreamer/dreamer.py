@@ -86,6 +86,10 @@ FILL_LDS = int(os.environ.get("SDREAMER_FILL_LDS", "0"))
 # M1. Measured neutral (profiles/r05v, r05w: the encoder forward slows by what S1 / M1 save; 3-round A/B 10.90 / 10.91 /
 # 10.96 ms for 0 / 1 / 2): off by default
 SIDE_PREP = int(os.environ.get("SDREAMER_SIDE_PREP", "0"))
+# SDREAMER_SIDE_PREP_AT=scan: S0 forks off after the encoder forward, beside the posterior scan (a latency-bound chain
+# of ~128-workgroup launches that leaves most CUs idle) instead of beside the compute-bound encoder: phase P gets a
+# split point there (parallel.collective) whose host step records an event and queues S0 on the side stream
+SIDE_PREP_AT = os.environ.get("SDREAMER_SIDE_PREP_AT", "enc")
 
 
 def _symexp_bins(n, device):  # symexp_twohot bins, distributions.py:242-251
@@ -658,7 +662,10 @@ class Dreamer(nn.Module):
             self._grads_clean = False
             torch.cuda.synchronize()
             for g in (gS0, gP, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gM3):
-                if g is not None and g.n_collectives:
+                if g is gP and SIDE_PREP and SIDE_PREP_AT == "scan":
+                    if g.n_collectives != 1:
+                        raise RuntimeError("P should hold exactly the S0 fork point")
+                elif g is not None and g.n_collectives:
                     raise RuntimeError("unexpected exchange step in a single-graph phase")
             self._graph = (gS0, gP, gS1, gM1, gR, gM2a, gS3, gM2b, gS4, gM2c, gM2d, gS2, gM3)
             self._gst, self._g_post, self._g_keys, self._g_mvec = st, post, keys, mvec
@@ -695,7 +702,8 @@ class Dreamer(nn.Module):
             main = caller
             side = self._side if self.use_side_stream else main
             fill, side_fill = main, side
-        if gS0 is not None:  # S0 (weights and seed only) beside P: after the seed copy and the last optimizer step
+        if gS0 is not None and SIDE_PREP_AT != "scan":  # S0 (weights and seed only) beside P: after the seed copy and
+            # the last optimizer step (SIDE_PREP_AT=scan: forked from P itself, _fork_side_prep)
             if side is not main:
                 side.wait_stream(main)
             with torch.cuda.stream(side):
@@ -845,6 +853,8 @@ class Dreamer(nn.Module):
         split = []  # the first encoder stage is backpropagated separately (_ph_encoder_bwd_lo)
         embed = self.encoder(data, split=split)
         mk("encoder_fwd")
+        if SIDE_PREP and SIDE_PREP_AT == "scan" and parallel._active is not None:  # (graph capture of P only)
+            parallel.collective(self._fork_side_prep)
         # the scan sees a leaf copy of embed: its backward stops there, so scan and encoder backward are separate
         # phases (_ph_scan_bwd / _ph_encoder_bwd)
         embed_l = embed.detach().requires_grad_(embed.requires_grad)
@@ -874,6 +884,18 @@ class Dreamer(nn.Module):
                     enc_split=split[0] if split else None, post_stoch=post_stoch,
                     post_deter=post_deter, post_logit=post_logit, leaves=leaves, feat_l=feat_l, feat_r=feat_r,
                     ifeats=ifeats, fsink=fsink)
+
+    def _fork_side_prep(self):
+        """P's split point after the encoder forward (SIDE_PREP_AT=scan), run on the host between P's two graphs at
+        every replay: S0 on the side stream, after what main has queued so far (weights of the last step, the seed)."""
+        g = self._graph
+        if g is None or g[0] is None or not self.use_side_stream:
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self._side.wait_event(ev)
+        with torch.cuda.stream(self._side):
+            g[0].replay()
 
     def _ph_side_prep(self, st):
         """side, beside the encoder forward (S0): what depends on the weights and the seed only — the imagination's

@@ -424,12 +424,15 @@ def test_pair_first_matches_per_head():
     assert checked == 4
 
 
-def test_side_prep_graph_matches_eager(monkeypatch):
+@pytest.mark.parametrize("at", ["enc", "scan"])
+def test_side_prep_graph_matches_eager(at, monkeypatch):
     """The S0 side phase (SDREAMER_SIDE_PREP=2: the imagination's noise / weight images and the backward's weight
-    layouts beside the encoder forward) and the filler LDS pad (SDREAMER_FILL_LDS) only move work between streams /
-    change occupancy: graph replays equal the eager updates exactly (cf. test_graph_replay_matches_eager)."""
+    layouts beside the encoder forward, or forked from P after it, beside the scan: SDREAMER_SIDE_PREP_AT=scan) and the
+    filler LDS pad (SDREAMER_FILL_LDS) only move work between streams / change occupancy: graph replays equal the
+    eager updates exactly (cf. test_graph_replay_matches_eager)."""
     import sdreamer.dreamer as D
     monkeypatch.setattr(D, "SIDE_PREP", 2)
+    monkeypatch.setattr(D, "SIDE_PREP_AT", at)
     monkeypatch.setattr(D, "FILL_LDS", 32)
     runs = []
     for graphs in (False, True):
