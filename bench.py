@@ -357,11 +357,9 @@ def probe_specs(agent, cfg, K):
     if K.ops_fused_pool():
         pix = N * 32 * 32
         c6 = bool(K.CONV6)
-        tiles = N * 32 * 32 // 256  # the ring kernel's 256-pixel tiles, dealt to one workgroup per CU (<= 16 each)
-        tpw = next(t for t in (1, 2, 4, 8, 16) if t >= min(-(-tiles // 256), 16))
-        add("conv_stage2", f"conv_fwd6r_direct_pool<48, 32, 5, 5, false, false, {tpw}>" if c6 else
-            "conv_fwd_direct_pool<48, 32, 5, 5, 1>", ((-(-tiles // tpw) + 7) // 8 * 8 if c6 else N * 32 * 32 // 128,
-                                                       1, 1), "mfma", 2.0 * pix * 48 * 25 * 32, 4.0 * pix * 32 + N * 16 * 16 * (48 * 9 + 4),
+        tiles = N * 32 * 32 // 512  # the ring kernel's 512-pixel tiles (64 pixels per wave), one per workgroup
+        add("conv_stage2", "conv_fwd6r_direct_pool<48, 32, 5, 5, true, false, 1, 4, 32>" if c6 else
+            "conv_fwd_direct_pool<48, 32, 5, 5, 1>", ((tiles + 7) // 8 * 8 if c6 else N * 32 * 32 // 128, 1, 1), "mfma", 2.0 * pix * 48 * 25 * 32, 4.0 * pix * 32 + N * 16 * 16 * (48 * 9 + 4),
             cp.label, ("launch", cp), 1, peak=PEAK_BF16X6 if c6 else None, alt_peak=PEAK_FP32_MFMA if c6 else None)
     # encoder stage 2 bwd-data (split-bf16 direct conv from a pre-split dOut patch in LDS): sd_conv2d_dgrad_direct(dout,
     # wsplit, din, Nb, Hs, Ws, Ci = dout channels, Co = din channels, kh, kw, pad, stream)
@@ -605,7 +603,7 @@ def dominant_probe(K):
     if K.CONV6:  # sd_conv2d_fwd_pool6: the same arguments with the split weight image in place of w
         return K.LaunchProbe("sd_conv2d_fwd_pool6", lambda a: a[11] == 32 and a[12] == 48, flops,
                              label="conv_fwd6r_direct_pool<48, 32, 5, 5> (encoder stage 2: 32->48 ch, 32x32, 5x5 "
-                                   "conv + 2x2 max-pool + RMSNorm + SiLU epilogue; direct conv over 256-pixel tiles "
+                                   "conv + 2x2 max-pool + RMSNorm + SiLU epilogue; direct conv over 512-pixel tiles "
                                    "from the input patch staged once as three bf16 planes, the pre-split weight "
                                    "through an LDS ring shared by 8 waves; bf16x6 = 6 v_mfma_f32_16x16x32_bf16 per "
                                    "f32-equivalent product, fp32-accurate)")

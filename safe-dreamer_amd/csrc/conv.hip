@@ -340,7 +340,10 @@ SD_DEV void pool_epilogue(const f32x4 (&acc)[WM / 16][BN / 16], float* C, const 
     }
   __syncthreads();
   constexpr int NK = BN / 8;
-  const int tid = threadIdx.x, pp = tid >> 3, t8 = tid & 7;  // 32 pooled pixels x 8 threads
+  // WM / 32 passes of (threads / 8) pooled pixels x 8 threads (a wave's WM pixels hold WM / 4 pooled ones)
+#pragma unroll
+  for (int ps = 0; ps < WM / 32; ++ps) {
+  const int tid = threadIdx.x, pp = (tid >> 3) + ps * (int)(blockDim.x >> 3), t8 = tid & 7;
   const int W = G.Wg, Wo = W >> 1, lwo = lw - 1;
   const int yo = pp >> lwo, xo = pp & (Wo - 1);
   const int l0 = (2 * yo) * W + 2 * xo;                     // local pixel of the window's top-left
@@ -378,6 +381,7 @@ SD_DEV void pool_epilogue(const f32x4 (&acc)[WM / 16][BN / 16], float* C, const 
     const float z = v[k] * r * nw[c];
     const long o = nchw_flat ? (long)n * BN * Ho * Wo + (long)c * Ho * Wo + prem : gpp * BN + c;
     if (valid) y[o] = siluf_(z);
+  }
   }
 }
 
@@ -634,16 +638,20 @@ __global__ __launch_bounds__(256, 2) void conv_fwd6_direct_pool(GemmArgs g, Geom
 // TPW: a workgroup runs TPW consecutive tiles (XCD-contiguous ranges, so the halo rows adjacent tiles share are L2
 // hits), the next tile's patch loaded into registers under this tile's MFMAs and the ring's first chunk under its
 // epilogue: with one workgroup per CU the prologue's HBM round trip was otherwise exposed once per tile.
-template <int BN, int CI, int LW, int KS, bool CG, bool PIPE, int TPW>
+// MT: 16-pixel m tiles per wave (2: 256-pixel tiles; 4: 512-pixel tiles, each wave 64 pixels x BN channels — 21
+// fragment reads per 72 MFMAs instead of 15 per 36: less LDS traffic per product). BROW: the ring's row stride in bf16
+// (40 = 32 + a pad; 32 = packed, the 64-B rows of a fragment read are still 1 KB contiguous).
+template <int BN, int CI, int LW, int KS, bool CG, bool PIPE, int TPW, int MT = 2, int BROW = 40>
 __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geom G, int lhw,
                                                                   const __bf16* __restrict__ wsp, const float* nw,
                                                                   float* pooled, uint8_t* amax, float* y, float* rstd,
                                                                   float eps, int nchw_flat) {
-  constexpr int NTH = 512, TP = 256;
+  constexpr int NTH = 512, TP = 128 * MT;
+  static_assert(!PIPE || MT == 2, "the fragment pipeline is built for two m tiles");
   constexpr int W = 1 << LW, R = TP / W, PH = R + KS - 1, PW = W + KS - 1, CP = CG ? CI : CI + 8, PAD = KS / 2;
   constexpr int NPIX = PH * PW, PLANE = NPIX * CP, K = KS * KS * CI, NKC = (K + 31) / 32, KP = NKC * 32, TN = BN / 16;
   constexpr int CI4 = CI / 4, NEL = PH * PW * CI4, NE = (NEL + NTH - 1) / NTH;
-  constexpr int BROW = 40, SB = 3 * BN * BROW, NPC = 3 * BN * 4, NPT = (NPC + NTH - 1) / NTH;  // ring: [plane][n][40]
+  constexpr int SB = 3 * BN * BROW, NPC = 3 * BN * 4, NPT = (NPC + NTH - 1) / NTH;  // ring: [plane][n][BROW]
   // element offset of (pixel, channel c, c % 4 == 0) in a plane
   auto poff = [](int pix, int c) { return CG ? ((c >> 3) * NPIX + pix) * 8 + (c & 7) : pix * CP + c; };
   static_assert(CI % 8 == 0 && TP % W == 0 && BN % 16 == 0, "geometry");
@@ -699,10 +707,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
       }
     }
   };
-  int pbase[2];
+  int pbase[MT];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int p = 32 * wave + 16 * mt + l16;
+  for (int mt = 0; mt < MT; ++mt) {
+    const int p = 16 * MT * wave + 16 * mt + l16;
     pbase[mt] = (p >> LW) * PW + (p & (W - 1));  // pixel index at tap (0, 0)
   }
   bload(0);
@@ -714,9 +722,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
   store_patch();
   bstore(0);
   if (NKC > 1) bload(1);
-  f32x4 acc[2][TN];
+  f32x4 acc[MT][TN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
@@ -780,16 +788,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
     k0 = k0 < K ? k0 : K - 8;  // past K: any in-patch address (the weight is zero there)
     const int tap = k0 / CI, c0 = k0 - tap * CI, ky = tap / KS, kx = tap - ky * KS;
     const int toff = ky * PW + kx;
-    bf16x8 a[2][3];
+    bf16x8 a[MT][3];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
         a[mt][pl] = *reinterpret_cast<const bf16x8*>(patch6r + pl * PLANE + poff(pbase[mt] + toff, c0));
     if (kc + 1 < NKC) bstore((kc + 1) & 1);  // chunk kc + 1 (loaded one iteration ago) into the other stage
     if (kc + 2 < NKC) bload(kc + 2);
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         f32x4 c = acc[mt][j];
@@ -803,8 +811,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geo
     __syncthreads();
   }
   if (it + 1 < TPW) bload(0);  // the next tile's first weight chunk (the same weights) under the epilogue
-  pool_epilogue<BN, 32>(acc, reinterpret_cast<float*>(patch6r), g, G, LW, lhw, tile * TP, nw, pooled, amax, y, rstd,
-                        eps, nchw_flat);
+  pool_epilogue<BN, 16 * MT>(acc, reinterpret_cast<float*>(patch6r), g, G, LW, lhw, tile * TP, nw, pooled, amax, y,
+                             rstd, eps, nchw_flat);
   }
 }
 
@@ -1156,14 +1164,20 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad3(GemmArgs g, Geom G, int lw
 // per plane), one k chunk ahead. M = R*W output pixels per workgroup (128), 4 waves x 2 16-pixel tiles, NT 16-channel
 // tiles of dIn; per 32-deep k chunk a lane's 8 k values are 8 consecutive channels of one tap (CIN % 8 == 0), one
 // ds_read_b128 per plane. Products: lo_a*hi_b + hi_a*lo_b + hi_a*hi_b (gemm3_mainloop's order), f32 accumulation.
-template <int CIN, int NT, int LW, int KS>
-__global__ __launch_bounds__(256, 2) void conv_dgrad3_direct(const float* __restrict__ dout,
-                                                              const __bf16* __restrict__ wsp, float* __restrict__ din,
-                                                              int Nb, int H, int pad) {
-  constexpr int W = 1 << LW, R = 128 / W, PH = R + KS - 1, PW = W + KS - 1, CP = CIN + 8;
+// MT / CG / NTHR (round 6): MT 16-pixel m tiles per wave over NTHR threads (the tile is 16 MT NTHR / 64 pixels), the
+// patch channel-group-major when CG ([plane][CIN / 8][pixel][8]: no pad, conflict-free), as conv_fwd6r_direct_pool's
+// 64-pixel waves: 12 fragment reads per 24 MFMAs instead of 8 per 12. Same products in the same k order.
+template <int CIN, int NT, int LW, int KS, int MT = 2, bool CG = false, int NTHR = 256>
+__global__ __launch_bounds__(NTHR, 2) void conv_dgrad3_direct(const float* __restrict__ dout,
+                                                               const __bf16* __restrict__ wsp, float* __restrict__ din,
+                                                               int Nb, int H, int pad) {
+  constexpr int TP = 16 * MT * (NTHR / 64);
+  constexpr int W = 1 << LW, R = TP / W, PH = R + KS - 1, PW = W + KS - 1, CP = CG ? CIN : CIN + 8, NPIX = PH * PW;
   constexpr int PLANE = PH * PW * CP, K = KS * KS * CIN, NKC = (K + 31) / 32, KP = NKC * 32, NOUT = 16 * NT;
-  constexpr int CIN4 = CIN / 4, NEL = PH * PW * CIN4, NE = (NEL + 255) / 256;
-  static_assert(CIN % 8 == 0 && R >= 1 && 128 % W == 0, "geometry");
+  constexpr int CIN4 = CIN / 4, NEL = PH * PW * CIN4, NE = (NEL + NTHR - 1) / NTHR;
+  static_assert(CIN % 8 == 0 && R >= 1 && TP % W == 0, "geometry");
+  // element offset of (pixel, channel c, c % 4 == 0) in a plane
+  auto poff = [](int pix, int c) { return CG ? ((c >> 3) * NPIX + pix) * 8 + (c & 7) : pix * CP + c; };
   extern __shared__ __attribute__((aligned(16))) __bf16 patch[];  // [plane][PH][PW][CP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, q = lane >> 4;
   const int rows_per_img = H / R, n = blockIdx.x / rows_per_img, y0 = (blockIdx.x % rows_per_img) * R;
@@ -1172,7 +1186,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad3_direct(const float* __rest
     f32x4 v[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
-      const int i = tid + 256 * e, c4 = i % CIN4, pix = i / CIN4, pc = pix % PW, pr = pix / PW;
+      const int i = tid + NTHR * e, c4 = i % CIN4, pix = i / CIN4, pc = pix % PW, pr = pix / PW;
       const int y = y0 + pr - pad, x = pc - pad;
       v[e] = (i < NEL && y >= 0 && y < H && x >= 0 && x < W)
                  ? *reinterpret_cast<const f32x4*>(dout + (((long)n * H + y) * W + x) * CIN + 4 * c4)
@@ -1180,46 +1194,46 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad3_direct(const float* __rest
     }
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
-      const int i = tid + 256 * e;
+      const int i = tid + NTHR * e;
       if (i < NEL) {
         const int c4 = i % CIN4, pix = i / CIN4;
         sdb::bf16x4 hi, lo;
         sdb::split2(v[e], hi, lo);
-        *reinterpret_cast<sdb::bf16x4*>(patch + pix * CP + 4 * c4) = hi;
-        *reinterpret_cast<sdb::bf16x4*>(patch + PLANE + pix * CP + 4 * c4) = lo;
+        *reinterpret_cast<sdb::bf16x4*>(patch + poff(pix, 4 * c4)) = hi;
+        *reinterpret_cast<sdb::bf16x4*>(patch + PLANE + poff(pix, 4 * c4)) = lo;
       }
     }
   }
-  // this lane's two pixel tiles: pixel p = 32 wave + 16 mt + l16 -> patch-local (row, x)
-  int pbase[2];
+  // this lane's MT pixel tiles: pixel p = 16 MT wave + 16 mt + l16 -> patch-local pixel index (row, x)
+  int pbase[MT];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int p = 32 * wave + 16 * mt + l16;
-    pbase[mt] = ((p >> LW) * PW + (p & (W - 1))) * CP;
+  for (int mt = 0; mt < MT; ++mt) {
+    const int p = 16 * MT * wave + 16 * mt + l16;
+    pbase[mt] = (p >> LW) * PW + (p & (W - 1));
   }
   // B: one k chunk of the pre-split weight ([plane][NOUT][32] bf16, 16-B pieces) per LDS stage, double-buffered and
   // shared by the 4 waves (each wave reading its fragments from global memory itself made the L1 path the bound)
   typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-  constexpr int BROW = 40, SB = 2 * NOUT * BROW, NPC = 8 * NOUT, NPT = (NPC + 255) / 256;
+  constexpr int BROW = 40, SB = 2 * NOUT * BROW, NPC = 8 * NOUT, NPT = (NPC + NTHR - 1) / NTHR;
   __bf16* bst = patch + 2 * PLANE;
   bf16x8 br[NPT];
   auto bload = [&](int kc) {
 #pragma unroll
     for (int u = 0; u < NPT; ++u) {
-      const int i = tid + 256 * u;
+      const int i = tid + NTHR * u;
       if (i < NPC) br[u] = *reinterpret_cast<const bf16x8*>(wsp + (long)(i >> 2) * KP + 32 * kc + 8 * (i & 3));
     }
   };
   auto bstore = [&](int stage) {
 #pragma unroll
     for (int u = 0; u < NPT; ++u) {
-      const int i = tid + 256 * u;
+      const int i = tid + NTHR * u;
       if (i < NPC) *reinterpret_cast<bf16x8*>(bst + stage * SB + (i >> 2) * BROW + 8 * (i & 3)) = br[u];
     }
   };
-  f32x4 acc[2][NT];
+  f32x4 acc[MT][NT];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bload(0);
@@ -1237,17 +1251,17 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad3_direct(const float* __rest
     int k0 = 32 * kc + 8 * q;
     k0 = k0 < K ? k0 : K - 8;  // past K: any in-patch address (B is zero there)
     const int tap = k0 / CIN, c0 = k0 - tap * CIN, ky = tap / KS, kx = tap - ky * KS;
-    const int off = (ky * PW + kx) * CP + c0;
-    bf16x8 ah[2], al[2];
+    const int toff = ky * PW + kx;
+    bf16x8 ah[MT], al[MT];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      ah[mt] = *reinterpret_cast<const bf16x8*>(patch + pbase[mt] + off);
-      al[mt] = *reinterpret_cast<const bf16x8*>(patch + PLANE + pbase[mt] + off);
+    for (int mt = 0; mt < MT; ++mt) {
+      ah[mt] = *reinterpret_cast<const bf16x8*>(patch + poff(pbase[mt] + toff, c0));
+      al[mt] = *reinterpret_cast<const bf16x8*>(patch + PLANE + poff(pbase[mt] + toff, c0));
     }
     if (kc + 1 < NKC) bstore((kc + 1) & 1);  // chunk kc+1 (loaded one iteration ago) into the other stage
     if (kc + 2 < NKC) bload(kc + 2);
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mt], bh[j], acc[mt][j], 0, 0, 0);
@@ -1256,12 +1270,12 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad3_direct(const float* __rest
       }
     __syncthreads();
   }
-  // acc[mt][j][r]: pixel 32 wave + 16 mt + 4 q + r, channel 16 j + l16
+  // acc[mt][j][r]: pixel 16 MT wave + 16 mt + 4 q + r, channel 16 j + l16
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int p = 32 * wave + 16 * mt + 4 * q + r, y = y0 + (p >> LW), x = p & (W - 1);
+      const int p = 16 * MT * wave + 16 * mt + 4 * q + r, y = y0 + (p >> LW), x = p & (W - 1);
       float* o = din + (((long)n * H + y) * W + x) * NOUT + l16;
 #pragma unroll
       for (int j = 0; j < NT; ++j) o[16 * j] = acc[mt][j][r];
@@ -2289,19 +2303,20 @@ bool conv6_pipe() {
   const char* e = getenv("SDHIP_CONV6_PIPE");
   return e ? atoi(e) != 0 : false;
 }
-template <int BN, int CI, int LW, int KS, bool CG, bool PIPE, int TPW>
+template <int BN, int CI, int LW, int KS, bool CG, bool PIPE, int TPW, int MT = 2, int BROW = 40>
 int fwd6r_launch_t(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, const float* nw, float* pooled,
                    uint8_t* amax, float* y, float* rstd, float eps, int nchw_flat, size_t lds, hipStream_t s) {
   static bool raised = false;
   if (!raised) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE, TPW>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    if (hipFuncSetAttribute(
+            reinterpret_cast<const void*>(conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE, TPW, MT, BROW>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return SD_EARG;
     raised = true;
   }
-  const int nwg = (sd_cdiv(g.M / 256, TPW) + 7) / 8 * 8;  // a multiple of 8: XCD-contiguous tile ranges
-  conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE, TPW><<<nwg, 512, lds, s>>>(g, G, lhw, wsp, nw, pooled, amax, y,
-                                                                             rstd, eps, nchw_flat);
+  const int nwg = (sd_cdiv(g.M / (128 * MT), TPW) + 7) / 8 * 8;  // a multiple of 8: XCD-contiguous tile ranges
+  conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE, TPW, MT, BROW><<<nwg, 512, lds, s>>>(g, G, lhw, wsp, nw, pooled,
+                                                                                       amax, y, rstd, eps, nchw_flat);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
@@ -2313,6 +2328,23 @@ int fwd6r_launch(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, c
   if (conv6_pipe())
     return fwd6r_launch_t<BN, CI, LW, KS, CG, true, 1>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps, nchw_flat, lds,
                                                        s);
+  // the 32 -> 48 stage: 512-pixel tiles, 64 pixels per wave, channel-group-major patch, packed ring (356 vs 392 us
+  // alone, profiles/r06mt4), one tile per workgroup by default (its prefetch registers spill: 386 us); SDHIP_CONV6_MT=2:
+  // the 256-pixel tiles
+  if constexpr (CI == 32 && BN == 48) {
+    const char* m = getenv("SDHIP_CONV6_MT");
+    constexpr int R4 = 512 / (1 << LW);
+    constexpr size_t lds4 = (size_t)3 * (R4 + KS - 1) * ((1 << LW) + KS - 1) * CI * 2 + (size_t)2 * 3 * BN * 32 * 2;
+    if ((!m || atoi(m) == 4) && lds4 <= 160 * 1024 && g.M % 512 == 0 && G.Hs % R4 == 0) {
+      const char* e = getenv("SDHIP_CONV6_TPW");
+      const int want = e ? atoi(e) : 1;
+#define SD_F6R4(T) \
+  fwd6r_launch_t<BN, CI, LW, KS, true, false, T, 4, 32>(g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps, nchw_flat, \
+                                                        lds4, s)
+      return want <= 1 ? SD_F6R4(1) : want <= 4 ? SD_F6R4(4) : SD_F6R4(8);
+#undef SD_F6R4
+    }
+  }
   const char* e = getenv("SDHIP_CONV6_TPW");
   const int want = e ? atoi(e) : sd_cdiv(g.M / 256, 256);
 #define SD_F6R(T) \
@@ -2392,6 +2424,26 @@ int dgrad_direct_launch(const float* dout, const __bf16* wsp, float* din, int Nb
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
+// 512-pixel tiles over 8 waves of 64 pixels, channel-group-major patch (one workgroup per CU); SDHIP_DGRAD_MT=2: the
+// 128-pixel tiles of 32-pixel waves (two per CU)
+template <int CIN, int NT, int LW>
+int dgrad_direct_launch4(const float* dout, const __bf16* wsp, float* din, int Nb, int H, int pad, hipStream_t s) {
+  constexpr int W = 1 << LW, R = 512 / W, KS = 5;
+  constexpr size_t lds = (size_t)2 * (R + KS - 1) * (W + KS - 1) * CIN * 2 + (size_t)2 * 2 * (16 * NT) * 40 * 2;
+  static_assert(lds <= 160 * 1024, "LDS");
+  const char* e = getenv("SDHIP_DGRAD_MT");
+  if ((e && atoi(e) == 2) || H % R) return dgrad_direct_launch<CIN, NT, LW>(dout, wsp, din, Nb, H, pad, s);
+  static bool raised = false;
+  if (!raised) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_dgrad3_direct<CIN, NT, LW, KS, 4, true, 512>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return SD_EARG;
+    raised = true;
+  }
+  conv_dgrad3_direct<CIN, NT, LW, KS, 4, true, 512><<<Nb * (H / R), 512, lds, s>>>(dout, wsp, din, Nb, H, pad);
+  SD_LAUNCH_CHECK();
+  return SD_OK;
+}
 }  // namespace
 
 extern "C" int sd_conv2d_dgrad_direct(const float* dout, const void* wsplit, float* din, int Nb, int Hs, int Ws,
@@ -2401,7 +2453,7 @@ extern "C" int sd_conv2d_dgrad_direct(const float* dout, const void* wsplit, flo
   if (kh != 5 || kw != 5 || pad != 2 || Hs != Ws || !al16(dout) || !al16(wsplit) || !al16(din)) return SD_ESHAPE;
   const __bf16* wsp = static_cast<const __bf16*>(wsplit);
   // a workgroup takes 128 / Ws whole rows of one image
-  if (Ci == 48 && Co == 32 && Ws == 32) return dgrad_direct_launch<48, 2, 5>(dout, wsp, din, Nb, Hs, pad, s);
+  if (Ci == 48 && Co == 32 && Ws == 32) return dgrad_direct_launch4<48, 2, 5>(dout, wsp, din, Nb, Hs, pad, s);
   if (Ci == 64 && Co == 48 && Ws == 16) return dgrad_direct_launch<64, 3, 4>(dout, wsp, din, Nb, Hs, pad, s);
   return SD_ESHAPE;
 }

@@ -690,10 +690,11 @@ def test_conv_pool_bf16x6_matches_f32(ci, co, hw, nb, nchw, monkeypatch):
 @pytest.mark.parametrize("ci,co,hw,nb,nchw", [(32, 48, 32, 4, False), (32, 48, 32, 3, True), (48, 64, 16, 5, True),
                                                (48, 64, 16, 2, False)])
 def test_conv_pool_bf16x6_ring_bit_identical(ci, co, hw, nb, nchw, monkeypatch):
-    """The bf16x6 stage forward with the weight through the LDS ring (conv_fwd6r_direct_pool, 256-pixel tiles; the
-    48 -> 64 stage on the channel-group-major patch) against the per-lane-weight kernel (SDHIP_CONV6_RING=0, 128-pixel
-    tiles), one tile or several per workgroup, with or without the fragment pipeline: the same products in the same k
-    order, so every output is bit-identical."""
+    """The bf16x6 stage forward with the weight through the LDS ring (conv_fwd6r_direct_pool: the 32 -> 48 stage on
+    512-pixel tiles with 64 pixels per wave, or 256 / 32 (SDHIP_CONV6_MT=2); the 48 -> 64 stage on 256-pixel tiles and
+    the channel-group-major patch) against the per-lane-weight kernel (SDHIP_CONV6_RING=0, 128-pixel tiles), one tile or
+    several per workgroup, with or without the fragment pipeline: the same products in the same k order, so every
+    output is bit-identical."""
     from sdreamer import kernels as K
     x = (torch.rand(nb, hw, hw, ci, generator=_g(21)) - 0.5).to(DEV)
     w = (torch.randn(co, 5, 5, ci, generator=_g(22)) / (ci * 25) ** 0.5).to(DEV)
@@ -704,6 +705,11 @@ def test_conv_pool_bf16x6_ring_bit_identical(ci, co, hw, nb, nchw, monkeypatch):
     for tpw in ("3", "16"):  # multi-tile workgroups (the bench's default), ragged tile ranges, idle workgroups
         monkeypatch.setenv("SDHIP_CONV6_TPW", tpw)
         rings.append(K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw))
+    monkeypatch.setenv("SDHIP_CONV6_MT", "2")  # (32 -> 48: 256-pixel tiles, 32 pixels per wave; default 4: 512, 64)
+    for tpw in ("1", "3"):
+        monkeypatch.setenv("SDHIP_CONV6_TPW", tpw)
+        rings.append(K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw))
+    monkeypatch.delenv("SDHIP_CONV6_MT")
     monkeypatch.delenv("SDHIP_CONV6_TPW")
     monkeypatch.setenv("SDHIP_CONV6_PIPE", "1")
     rings.append(K.conv2d_fwd_pool(x, w, b, nw, nchw_flat=nchw))
@@ -716,10 +722,11 @@ def test_conv_pool_bf16x6_ring_bit_identical(ci, co, hw, nb, nchw, monkeypatch):
 
 
 @pytest.mark.parametrize("cd,ci,hw,nb", [(48, 32, 32, 8), (64, 48, 16, 16), (48, 32, 32, 1)])
-def test_conv_dgrad_direct_matches_implicit_gemm(cd, ci, hw, nb):
-    """The direct bwd-data kernel (sd_conv2d_dgrad_direct: dOut patch staged once per workgroup) against the
-    implicit-GEMM one (sd_conv2d_dgrad_bf16x3): the same (hi, lo) splits, the same three products per k and the same k
-    order, so bit for bit the same dIn; and both within the split-bf16 bound of the f32 kernel."""
+def test_conv_dgrad_direct_matches_implicit_gemm(cd, ci, hw, nb, monkeypatch):
+    """The direct bwd-data kernel (sd_conv2d_dgrad_direct: dOut patch staged once per workgroup; the 48 -> 32 stage on
+    512-pixel tiles of 64-pixel waves, or 128 / 32 with SDHIP_DGRAD_MT=2) against the implicit-GEMM one
+    (sd_conv2d_dgrad_bf16x3): the same (hi, lo) splits, the same three products per k and the same k order, so bit for
+    bit the same dIn; and both within the split-bf16 bound of the f32 kernel."""
     from sdreamer import kernels as K
     w = (torch.randn(cd, 5, 5, ci, generator=_g(cd + ci)) / (ci * 25) ** 0.5).to(DEV)
     dy = torch.randn(nb, hw, hw, cd, generator=_g(hw)).to(DEV)
@@ -730,6 +737,12 @@ def test_conv_dgrad_direct_matches_implicit_gemm(cd, ci, hw, nb):
                              K.stream()), "direct kernel not instantiated for this shape"
     dx_gemm = K.conv2d_dgrad(dy, w, fast=True, direct=False)
     assert torch.equal(dx, dx_gemm)
+    monkeypatch.setenv("SDHIP_DGRAD_MT", "2")
+    dx2 = torch.empty_like(dx)
+    assert K.nat.call_shaped("sd_conv2d_dgrad_direct", K.p(dy), K.p(ws), K.p(dx2), nb, hw, hw, cd, ci, 5, 5, 2,
+                             K.stream())
+    monkeypatch.delenv("SDHIP_DGRAD_MT")
+    assert torch.equal(dx2, dx_gemm)
     dx_ref = K.conv2d_dgrad(dy, w, fast=False)
     bound = 4e-5 * K.conv2d_dgrad(dy.abs(), w.abs(), fast=False) + 1e-6
     assert ((dx - dx_ref).abs() - bound).max().item() <= 0

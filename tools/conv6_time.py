@@ -38,11 +38,17 @@ def main():
         res = {}
         for name, c6, ring, pipe, tpw in [("f32", "", "1", "0", ""), ("bf16x6 lane", "1", "0", "0", ""),
                                           ("bf16x6 ring pipe 1 tile", "1", "1", "1", ""),
-                                          ("bf16x6 ring 1 tile", "1", "1", "0", "1"),
+                                          ("bf16x6 ring MT2 1 tile", "1", "1", "0", "mt2:1"),
+                                          ("bf16x6 ring MT2", "1", "1", "0", "mt2:"),
+                                          ("bf16x6 ring MT4 prefetch x4", "1", "1", "0", "mt4:4"),
                                           ("bf16x6 ring", "1", "1", "0", "")]:
             K.CONV6 = c6
             os.environ["SDHIP_CONV6_RING"] = ring
             os.environ["SDHIP_CONV6_PIPE"] = pipe
+            os.environ.pop("SDHIP_CONV6_MT", None)
+            if tpw.startswith("mt"):  # the 32 -> 48 stage's m tiles per wave (the 48 -> 64 stage has 2 either way)
+                os.environ["SDHIP_CONV6_MT"] = tpw[2]
+                tpw = tpw[4:]
             if tpw:
                 os.environ["SDHIP_CONV6_TPW"] = tpw
             else:
