@@ -641,12 +641,14 @@ __global__ __launch_bounds__(256, 2) void conv_fwd6_direct_pool(GemmArgs g, Geom
 // MT: 16-pixel m tiles per wave (2: 256-pixel tiles; 4: 512-pixel tiles, each wave 64 pixels x BN channels — 21
 // fragment reads per 72 MFMAs instead of 15 per 36: less LDS traffic per product). BROW: the ring's row stride in bf16
 // (40 = 32 + a pad; 32 = packed, the 64-B rows of a fragment read are still 1 KB contiguous).
-template <int BN, int CI, int LW, int KS, bool CG, bool PIPE, int TPW, int MT = 2, int BROW = 40>
-__global__ __launch_bounds__(512, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geom G, int lhw,
+// NTH: threads (the 48 -> 64 stage's whole image as four 64-pixel waves on 256 threads measured slower than eight
+// 32-pixel waves, 213.7 vs 180.5 us, profiles/r06m3: one wave per SIMD).
+template <int BN, int CI, int LW, int KS, bool CG, bool PIPE, int TPW, int MT = 2, int BROW = 40, int NTH = 512>
+__global__ __launch_bounds__(NTH, 1) void conv_fwd6r_direct_pool(GemmArgs g, Geom G, int lhw,
                                                                   const __bf16* __restrict__ wsp, const float* nw,
                                                                   float* pooled, uint8_t* amax, float* y, float* rstd,
                                                                   float eps, int nchw_flat) {
-  constexpr int NTH = 512, TP = 128 * MT;
+  constexpr int TP = 16 * MT * (NTH / 64);
   static_assert(!PIPE || MT == 2, "the fragment pipeline is built for two m tiles");
   constexpr int W = 1 << LW, R = TP / W, PH = R + KS - 1, PW = W + KS - 1, CP = CG ? CI : CI + 8, PAD = KS / 2;
   constexpr int NPIX = PH * PW, PLANE = NPIX * CP, K = KS * KS * CI, NKC = (K + 31) / 32, KP = NKC * 32, TN = BN / 16;
@@ -2303,20 +2305,20 @@ bool conv6_pipe() {
   const char* e = getenv("SDHIP_CONV6_PIPE");
   return e ? atoi(e) != 0 : false;
 }
-template <int BN, int CI, int LW, int KS, bool CG, bool PIPE, int TPW, int MT = 2, int BROW = 40>
+template <int BN, int CI, int LW, int KS, bool CG, bool PIPE, int TPW, int MT = 2, int BROW = 40, int NTH = 512>
 int fwd6r_launch_t(const GemmArgs& g, const Geom& G, int lhw, const __bf16* wsp, const float* nw, float* pooled,
                    uint8_t* amax, float* y, float* rstd, float eps, int nchw_flat, size_t lds, hipStream_t s) {
   static bool raised = false;
   if (!raised) {
     if (hipFuncSetAttribute(
-            reinterpret_cast<const void*>(conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE, TPW, MT, BROW>),
+            reinterpret_cast<const void*>(conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE, TPW, MT, BROW, NTH>),
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return SD_EARG;
     raised = true;
   }
-  const int nwg = (sd_cdiv(g.M / (128 * MT), TPW) + 7) / 8 * 8;  // a multiple of 8: XCD-contiguous tile ranges
-  conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE, TPW, MT, BROW><<<nwg, 512, lds, s>>>(g, G, lhw, wsp, nw, pooled,
-                                                                                       amax, y, rstd, eps, nchw_flat);
+  const int nwg = (sd_cdiv(g.M / (16 * MT * (NTH / 64)), TPW) + 7) / 8 * 8;  // a multiple of 8: XCD-contiguous
+  conv_fwd6r_direct_pool<BN, CI, LW, KS, CG, PIPE, TPW, MT, BROW, NTH><<<nwg, NTH, lds, s>>>(
+      g, G, lhw, wsp, nw, pooled, amax, y, rstd, eps, nchw_flat);
   SD_LAUNCH_CHECK();
   return SD_OK;
 }
@@ -2454,7 +2456,25 @@ extern "C" int sd_conv2d_dgrad_direct(const float* dout, const void* wsplit, flo
   const __bf16* wsp = static_cast<const __bf16*>(wsplit);
   // a workgroup takes 128 / Ws whole rows of one image
   if (Ci == 48 && Co == 32 && Ws == 32) return dgrad_direct_launch4<48, 2, 5>(dout, wsp, din, Nb, Hs, pad, s);
-  if (Ci == 64 && Co == 48 && Ws == 16) return dgrad_direct_launch<64, 3, 4>(dout, wsp, din, Nb, Hs, pad, s);
+  if (Ci == 64 && Co == 48 && Ws == 16) {
+    // whole-image 256-pixel tiles of four 64-pixel waves, channel-group-major patch (183 -> 131 us alone,
+    // profiles/r06dg3); SDHIP_DGRAD3_MT=2: the 128-pixel tiles of 32-pixel waves
+    const char* e = getenv("SDHIP_DGRAD3_MT");
+    if (!(e && atoi(e) == 2) && Hs == 16) {
+      constexpr size_t lds = (size_t)2 * 20 * 20 * 64 * 2 + (size_t)2 * 2 * 48 * 40 * 2;
+      static bool raised = false;
+      if (!raised) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(conv_dgrad3_direct<64, 3, 4, 5, 4, true, 256>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+          return SD_EARG;
+        raised = true;
+      }
+      conv_dgrad3_direct<64, 3, 4, 5, 4, true, 256><<<Nb, 256, lds, s>>>(dout, wsp, din, Nb, Hs, pad);
+      SD_LAUNCH_CHECK();
+      return SD_OK;
+    }
+    return dgrad_direct_launch<64, 3, 4>(dout, wsp, din, Nb, Hs, pad, s);
+  }
   return SD_ESHAPE;
 }
 

@@ -724,7 +724,8 @@ def test_conv_pool_bf16x6_ring_bit_identical(ci, co, hw, nb, nchw, monkeypatch):
 @pytest.mark.parametrize("cd,ci,hw,nb", [(48, 32, 32, 8), (64, 48, 16, 16), (48, 32, 32, 1)])
 def test_conv_dgrad_direct_matches_implicit_gemm(cd, ci, hw, nb, monkeypatch):
     """The direct bwd-data kernel (sd_conv2d_dgrad_direct: dOut patch staged once per workgroup; the 48 -> 32 stage on
-    512-pixel tiles of 64-pixel waves, or 128 / 32 with SDHIP_DGRAD_MT=2) against the implicit-GEMM one
+    512-pixel tiles of 64-pixel waves and the 64 -> 48 one on whole-image tiles of 64-pixel waves, or both on 128-pixel
+    tiles of 32-pixel waves with SDHIP_DGRAD_MT=2 / SDHIP_DGRAD3_MT=2) against the implicit-GEMM one
     (sd_conv2d_dgrad_bf16x3): the same (hi, lo) splits, the same three products per k and the same k order, so bit for
     bit the same dIn; and both within the split-bf16 bound of the f32 kernel."""
     from sdreamer import kernels as K
@@ -737,12 +738,13 @@ def test_conv_dgrad_direct_matches_implicit_gemm(cd, ci, hw, nb, monkeypatch):
                              K.stream()), "direct kernel not instantiated for this shape"
     dx_gemm = K.conv2d_dgrad(dy, w, fast=True, direct=False)
     assert torch.equal(dx, dx_gemm)
-    monkeypatch.setenv("SDHIP_DGRAD_MT", "2")
-    dx2 = torch.empty_like(dx)
-    assert K.nat.call_shaped("sd_conv2d_dgrad_direct", K.p(dy), K.p(ws), K.p(dx2), nb, hw, hw, cd, ci, 5, 5, 2,
-                             K.stream())
-    monkeypatch.delenv("SDHIP_DGRAD_MT")
-    assert torch.equal(dx2, dx_gemm)
+    for knob, val in (("SDHIP_DGRAD_MT", "2"), ("SDHIP_DGRAD3_MT", "2")):  # (each applies to one stage)
+        monkeypatch.setenv(knob, val)
+        dx2 = torch.empty_like(dx)
+        assert K.nat.call_shaped("sd_conv2d_dgrad_direct", K.p(dy), K.p(ws), K.p(dx2), nb, hw, hw, cd, ci, 5, 5, 2,
+                                 K.stream())
+        monkeypatch.delenv(knob)
+        assert torch.equal(dx2, dx_gemm), knob
     dx_ref = K.conv2d_dgrad(dy, w, fast=False)
     bound = 4e-5 * K.conv2d_dgrad(dy.abs(), w.abs(), fast=False) + 1e-6
     assert ((dx - dx_ref).abs() - bound).max().item() <= 0

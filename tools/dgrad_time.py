@@ -24,6 +24,17 @@ def main():
         us = timeit(lambda: K.nat.call("sd_conv2d_dgrad_direct", K.p(dy), K.p(ws), K.p(dx), 1024, 32, 32, 48, 32, 5, 5,
                                        2, K.stream()))
         print(f"dgrad MT{mt}: {us:.1f} us ({fl / us / 1e6:.1f} TF f32-equivalent)")
+    os.environ.pop("SDHIP_DGRAD_MT", None)
+    w = (torch.randn(64, 5, 5, 48, generator=g) / (48 * 25) ** 0.5).cuda()  # stage 3: 64 -> 48 at 16 x 16
+    dy = torch.randn(1024, 16, 16, 64, generator=g).cuda()
+    ws = K.conv_split_weight(K.conv_flip_weight(w))
+    dx = torch.empty(1024, 16, 16, 48, device="cuda")
+    fl = 2 * 1024 * 16 * 16 * 64 * 25 * 48
+    for mt in ("2", "4"):  # (SDHIP_DGRAD3_MT: 4 = whole-image tiles of 64-pixel waves, the default)
+        os.environ["SDHIP_DGRAD3_MT"] = mt
+        us = timeit(lambda: K.nat.call("sd_conv2d_dgrad_direct", K.p(dy), K.p(ws), K.p(dx), 1024, 16, 16, 64, 48, 5, 5,
+                                       2, K.stream()))
+        print(f"stage-3 dgrad MT{mt}: {us:.1f} us ({fl / us / 1e6:.1f} TF f32-equivalent)")
 
 
 if __name__ == "__main__":
