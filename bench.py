@@ -358,19 +358,21 @@ def probe_specs(agent, cfg, K):
         pix = N * 32 * 32
         c6 = bool(K.CONV6)
         tiles = N * 32 * 32 // 512  # the ring kernel's 512-pixel tiles (64 pixels per wave), one per workgroup
-        add("conv_stage2", "conv_fwd6r_direct_pool<48, 32, 5, 5, true, false, 1, 4, 32>" if c6 else
+        add("conv_stage2", "conv_fwd6r_direct_pool<48, 32, 5, 5, true, false, 1, 4, 32, 512>" if c6 else
             "conv_fwd_direct_pool<48, 32, 5, 5, 1>", ((tiles + 7) // 8 * 8 if c6 else N * 32 * 32 // 128, 1, 1), "mfma", 2.0 * pix * 48 * 25 * 32, 4.0 * pix * 32 + N * 16 * 16 * (48 * 9 + 4),
             cp.label, ("launch", cp), 1, peak=PEAK_BF16X6 if c6 else None, alt_peak=PEAK_FP32_MFMA if c6 else None)
     # encoder stage 2 bwd-data (split-bf16 direct conv from a pre-split dOut patch in LDS): sd_conv2d_dgrad_direct(dout,
     # wsplit, din, Nb, Hs, Ws, Ci = dout channels, Co = din channels, kh, kw, pad, stream)
     dg = K.LaunchProbe("sd_conv2d_dgrad_direct", lambda a: a[6] == 48 and a[7] == 32,
                        lambda a: 2.0 * a[3] * a[4] * a[5] * a[6] * a[7] * a[8] * a[9],
-                       label="conv_dgrad3_direct<48, 2, 5, 5> (encoder stage 2 bwd-data: dOut 48 ch -> dIn 32 ch at "
-                             "32x32, 5x5 flipped weight; direct conv, the dOut patch of 4 rows split once into (hi, lo) "
-                             "bf16 planes in LDS, pre-split weight from L2, 3 v_mfma_f32_16x16x32_bf16 per "
-                             "f32-equivalent product)")
+                       label="conv_dgrad3_direct<48, 2, 5, 5, 4, true, 512> (encoder stage 2 bwd-data: dOut 48 ch -> "
+                             "dIn 32 ch at 32x32, 5x5 flipped weight; direct conv over 512-pixel tiles of 64-pixel "
+                             "waves, the dOut patch of 16 rows split once into (hi, lo) bf16 planes in LDS, the "
+                             "pre-split weight through an LDS ring, 3 v_mfma_f32_16x16x32_bf16 per f32-equivalent "
+                             "product)")
     pix = N * 32 * 32
-    add("conv_stage2_dgrad", "conv_dgrad3_direct<48, 2, 5, 5>", (pix // 128, 1, 1), "mfma", 2.0 * pix * 48 * 25 * 32,
+    add("conv_stage2_dgrad", "conv_dgrad3_direct<48, 2, 5, 5, 4, true, 512>", (pix // 512, 1, 1), "mfma",
+        2.0 * pix * 48 * 25 * 32,
         4.0 * (pix * 48 + pix * 32) + 2.0 * 2 * 32 * 1216, dg.label, ("launch", dg), 1, peak=PEAK_BF16X3)
     # imagined heads' first layers: one split-bf16 MLP-layer launch, A = the imagined feats broadcast over 4 weights
     M = N * (H + 1)
