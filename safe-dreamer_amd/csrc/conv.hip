@@ -841,16 +841,21 @@ __global__ __launch_bounds__(256) void split3_weight(const float* __restrict__ w
 // float4 per pixel: the b32 fragment reads of 64 lanes hit 64 distinct banks). A workgroup runs TPW vertically
 // adjacent tiles (XCD-aware: an XCD's workgroups cover a contiguous tile range), prefetching the next tile's patch
 // into registers under the current tile's MFMAs; the epilogue is conv_fwd16_pool's, in its own LDS area.
-template <int BN, int LW, int KS, int TPW>
-__global__ __launch_bounds__(256) void conv_fwd_direct_pool_c4(GemmArgs g, Geom G, int lhw, const float* nw,
-                                                               float* pooled, uint8_t* amax, float* y, float* rstd,
-                                                               float eps, int nchw_flat) {
+// tpw (runtime) tiles per workgroup: the launcher sizes the grid to one round of resident workgroups (OCC per CU),
+// so no partial last round of long workgroups idles part of the chip.
+template <int BN, int LW, int KS, int OCC>
+__global__ __launch_bounds__(256, OCC) void conv_fwd_direct_pool_c4(GemmArgs g, Geom G, int lhw, int TPW,
+                                                                    const float* nw, float* pooled, uint8_t* amax,
+                                                                    float* y, float* rstd, float eps, int nchw_flat) {
   constexpr int BM = 128, WM = 32, TM = WM / 16, TN = BN / 16, W = 1 << LW, R = BM / W;
   constexpr int PH = R + KS - 1, PW = W + KS - 1, PAD = KS / 2, NT = KS * KS;
   constexpr int NQ = PH * PW, NQT = (NQ + 255) / 256;
-  float* smem = sd_smem<NQ * 4 + BM * (BN + 1)>();
+  // the patch area is padded to NQT * 256 pixels, so every thread's staging store is unconditional (a store under a
+  // branch left the compiler a path on which the loop-invariant weight loads looked outstanding: it then waited for
+  // the next tile's prefetch, vmcnt(0), before the first MFMA of every tile)
+  float* smem = sd_smem<NQT * 256 * 4 + BM * (BN + 1)>();
   float* patch = smem;
-  float* C = smem + NQ * 4;
+  float* C = smem + NQT * 256 * 4;
   const int nwg = gridDim.x, ntiles = g.M / BM;
   const int wg = (nwg & 7) ? blockIdx.x : (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
@@ -886,10 +891,7 @@ __global__ __launch_bounds__(256) void conv_fwd_direct_pool_c4(GemmArgs g, Geom 
     const int tile = wg * TPW + it;
     if (tile >= ntiles) break;  // uniform over the workgroup
 #pragma unroll
-    for (int u = 0; u < NQT; ++u) {
-      const int i = threadIdx.x + 256 * u;
-      if ((u + 1) * 256 <= NQ || i < NQ) *reinterpret_cast<f32x4*>(patch + 4 * i) = v[u];
-    }
+    for (int u = 0; u < NQT; ++u) *reinterpret_cast<f32x4*>(patch + 4 * (threadIdx.x + 256 * u)) = v[u];
     __syncthreads();  // patch staged (and the previous tile's epilogue is past its C reads)
     if (it + 1 < TPW) load_patch(tile + 1);
     f32x4 acc[TM][TN];
@@ -1963,16 +1965,16 @@ extern "C" int sd_conv2d_fwd_pool(const float* in, const float* w, const float* 
   }
   if (conv_direct_fwd() && es && Co == 32 && Ci == 4 && Ws == 64 && kh == 5 && kw == 5 && pad == 2 &&
       Hs % 2 == 0 && al16(in)) {
+    // SDHIP_C4_TPW = n > 0: n tiles per workgroup (the round-5 default was 16: 2048 workgroups, 2.67 rounds of
+    // the 768 then resident); default 0 = one round of resident workgroups (SDHIP_C4_OCC per CU, default 4).
     const char* e = getenv("SDHIP_C4_TPW");
-    const int tpw = e ? atoi(e) : 16;
-#define SD_C4(TPW)                                                                                                \
-  conv_fwd_direct_pool_c4<32, 6, 5, TPW><<<sd_cdiv(g.M / 128, TPW), 256, 0, s>>>(g, G, lhw, nw, pooled, amax, y, \
-                                                                               rstd, eps, nchw_flat)
-    if (tpw == 16) SD_C4(16);
-    else if (tpw == 8) SD_C4(8);
-    else if (tpw == 2) SD_C4(2);
-    else SD_C4(4);
-#undef SD_C4
+    const char* eo = getenv("SDHIP_C4_OCC");
+    const int occ = eo ? atoi(eo) : 4, tiles = g.M / 128;
+    int tpw = e ? atoi(e) : 0;
+    if (tpw <= 0) tpw = sd_cdiv(tiles, 256 * (occ > 0 ? occ : 4));
+    const int nwg = sd_cdiv(tiles, tpw);
+    conv_fwd_direct_pool_c4<32, 6, 5, 4><<<nwg, 256, 0, s>>>(g, G, lhw, tpw, nw, pooled, amax, y, rstd, eps,
+                                                             nchw_flat);
     SD_LAUNCH_CHECK();
     return SD_OK;
   }
