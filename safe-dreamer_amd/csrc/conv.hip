@@ -323,10 +323,18 @@ __global__ __launch_bounds__(256) void conv_fwd16(GemmArgs g, Geom G, int lw, in
 // Stage epilogue shared by the fused forward kernels: the 128-pixel conv tile (+ bias) is staged in LDS at C, 2x2
 // max-pooled (argmax kept for the backward), RMS-normalised over the BN channels (8 threads per pooled pixel) and
 // SiLU'd; only the pooled outputs are written (pooled pre-norm values, argmax, rstd; y NHWC or NCHW-flat).
+// pre (optional): the caller's registers holding this lane's bias values (BN / 16: column 16 j + l16) and norm
+// weights (BN / 8: channel t8 + 8 k), loaded once per workgroup — in a kernel with loads in flight at the epilogue
+// (a prefetched next patch) the per-tile loads here would each wait for them too (vmcnt counts in issue order).
+template <int BN>
+struct EpiPre {
+  float bias[BN / 16];
+  float nw[BN / 8];
+};
 template <int BN, int WM>
 SD_DEV void pool_epilogue(const f32x4 (&acc)[WM / 16][BN / 16], float* C, const GemmArgs& g, const Geom& G, int lw,
                           int lhw, int bm0, const float* nw, float* pooled, uint8_t* amax, float* y, float* rstd,
-                          float eps, int nchw_flat) {
+                          float eps, int nchw_flat, const EpiPre<BN>* pre = nullptr) {
   constexpr int LDC = BN + 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l16 = lane & 15, q = lane >> 4;
 #pragma unroll
@@ -334,7 +342,7 @@ SD_DEV void pool_epilogue(const f32x4 (&acc)[WM / 16][BN / 16], float* C, const 
 #pragma unroll
     for (int j = 0; j < BN / 16; ++j) {
       const int col = 16 * j + l16;
-      const float bv = g.bias ? g.bias[col] : 0.f;
+      const float bv = pre ? pre->bias[j] : g.bias ? g.bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) C[(wave * WM + 16 * i + 4 * q + r) * LDC + col] = acc[i][j][r] + bv;
     }
@@ -378,7 +386,7 @@ SD_DEV void pool_epilogue(const f32x4 (&acc)[WM / 16][BN / 16], float* C, const 
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     const int c = t8 + 8 * k;
-    const float z = v[k] * r * nw[c];
+    const float z = v[k] * r * (pre ? pre->nw[k] : nw[c]);
     const long o = nchw_flat ? (long)n * BN * Ho * Wo + (long)c * Ho * Wo + prem : gpp * BN + c;
     if (valid) y[o] = siluf_(z);
   }
@@ -867,6 +875,11 @@ __global__ __launch_bounds__(256, OCC) void conv_fwd_direct_pool_c4(GemmArgs g, 
 #pragma unroll
       for (int j = 0; j < TN; ++j) bw[t][j] = sd_bload1(rb, (uint32_t)(((16 * j + l16) * g.ldb + 4 * t + q) * 4));
   }
+  EpiPre<BN> pre;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) pre.bias[j] = g.bias ? g.bias[16 * j + l16] : 0.f;
+#pragma unroll
+  for (int k = 0; k < BN / 8; ++k) pre.nw[k] = nw[(threadIdx.x & 7) + 8 * k];
   const sd_rsrc rs = sd_make_rsrc(G.in, (long)G.Nb * G.Hs * G.Ws * 16);
   f32x4 v[NQT];
   auto load_patch = [&](int tile) {
@@ -912,7 +925,7 @@ __global__ __launch_bounds__(256, OCC) void conv_fwd_direct_pool_c4(GemmArgs g, 
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], bw[t][j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();  // every wave is done reading the patch before the next tile's is stored
-    pool_epilogue<BN, WM>(acc, C, g, G, LW, lhw, tile * BM, nw, pooled, amax, y, rstd, eps, nchw_flat);
+    pool_epilogue<BN, WM>(acc, C, g, G, LW, lhw, tile * BM, nw, pooled, amax, y, rstd, eps, nchw_flat, &pre);
   }
 }
 

@@ -321,6 +321,31 @@ def test_conv_pool_fused_matches_two_launches(ci, co, hw, nb, nchw, monkeypatch)
             close(a.nan_to_num(), r.nan_to_num(), 1e-6, what)
 
 
+@pytest.mark.parametrize("nb", [3, 40])
+def test_conv_pool_c4_grid_bit_identical(nb, monkeypatch):
+    """Stage-1 direct kernel (conv_fwd_direct_pool_c4): every tile runs the same products in the same order whatever
+    the grid, so the default one-round grid (SDHIP_C4_OCC resident workgroups per CU, 32 tiles each at the bench's
+    1024 images), the round-5 grid (SDHIP_C4_TPW=16), a ragged 3 tiles per workgroup and a 3-per-CU round all give
+    bit-identical outputs; nb = 3 leaves most workgroups of the default grid without a tile."""
+    from sdreamer import kernels as K
+    monkeypatch.setattr(K, "CONV6", "")
+    x = (torch.rand(nb, 64, 64, 4, generator=_g(nb)) - 0.5).to(DEV)
+    w = (torch.randn(32, 5, 5, 4, generator=_g(7)) / 10).to(DEV)
+    b = (0.1 * torch.randn(32, generator=_g(1))).to(DEV)
+    nw = (1 + 0.1 * torch.randn(32, generator=_g(2))).to(DEV)
+    monkeypatch.delenv("SDHIP_C4_TPW", raising=False)
+    monkeypatch.delenv("SDHIP_C4_OCC", raising=False)
+    ref = [t.clone() for t in K.conv2d_fwd_pool(x, w, b, nw)]
+    for env in ({"SDHIP_C4_TPW": "16"}, {"SDHIP_C4_TPW": "3"}, {"SDHIP_C4_TPW": "1"}, {"SDHIP_C4_OCC": "3"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        out = K.conv2d_fwd_pool(x, w, b, nw)
+        for a, r, what in zip(out, ref, ("y", "pooled", "amax", "rstd")):
+            assert torch.equal(a, r), (env, what)
+        for k in env:
+            monkeypatch.delenv(k)
+
+
 def test_upconv():
     from sdreamer import ops
     nb, hw, ci, co = 3, 8, 64, 48
