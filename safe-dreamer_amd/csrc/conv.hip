@@ -406,6 +406,11 @@ __global__ __launch_bounds__(256) void conv_fwd16_pool(GemmArgs g, Geom G, int l
   build_taps(tab, G, g.K);
   constexpr int BM = 128, WM = 32;
   const int bm0 = blockIdx.x * BM;
+  EpiPre<BN> pre;  // epilogue operands issued ahead of the main loop (no loads behind the epilogue's own stores)
+#pragma unroll
+  for (int j = 0; j < BN / 16; ++j) pre.bias[j] = g.bias ? g.bias[16 * j + (threadIdx.x & 15)] : 0.f;
+#pragma unroll
+  for (int k = 0; k < BN / 8; ++k) pre.nw[k] = nw[(threadIdx.x & 7) + 8 * k];
   f32x4 acc[WM / 16][BN / 16];
   if constexpr (ES) {
     Im2colRowsB<BM> la(G, tab, g.M, bm0, lw, lhw);
@@ -419,7 +424,7 @@ __global__ __launch_bounds__(256) void conv_fwd16_pool(GemmArgs g, Geom G, int l
   __syncthreads();  // every wave is done reading the staging area
   float* C = sd_smem<gemm16_smem_floats<BM, BN>()>();
   static_assert(BM * (BN + 1) <= gemm16_smem_floats<BM, BN>(), "tile fits the staging area");
-  pool_epilogue<BN, WM>(acc, C, g, G, lw, lhw, bm0, nw, pooled, amax, y, rstd, eps, nchw_flat);
+  pool_epilogue<BN, WM>(acc, C, g, G, lw, lhw, bm0, nw, pooled, amax, y, rstd, eps, nchw_flat, &pre);
 }
 
 // Direct ConvEncoder stage forward (stride 1, same padding, no upsample): the 128-pixel tile is R = 128 / W whole
